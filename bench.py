@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: CML GCN training throughput (windows/s) on N MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...      (driver launches N > 1 like this)
+
+One process per GPU, data parallel over RCCL (backend "nccl"). Per-GPU batch is the
+reference's ``batch_size`` 128 windows (weak scaling: global batch = 128 * N).
+Model = the reference CML GCN architecture (GeneralConv 2->16 + mean pooling +
+7-layer LSTM TimeLayer 16/16/32/32/64/64/128 + dense head, 188,193 trainables),
+random init; data = synthetic CML neighbourhood (23 links, 28 days at 1 min, the
+shape of ``cml_raw_example.nc``) windowed with T = 181. Every timed step is a full
+training step: on-device window gather, forward, weighted BCE, backward, gradient
+all-reduce (N > 1), Adam update.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REF_GCN_WINDOWS_PER_S = 350.0   # reference GCN predict() on V100 (training not published)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128, help="windows per GPU per step")
+    ap.add_argument("--model", choices=["gcn", "baseline"], default="gcn")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--no-graph", action="store_true", help="disable HIP-graph capture of the step")
+    ap.add_argument("--sensors", type=int, default=23)
+    ap.add_argument("--days", type=int, default=28)
+    args = ap.parse_args(argv)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gnnqc import config as C
+    from gnnqc.data.preprocessing import create_windows_dataset, load_dataset
+    from gnnqc.data.store import DeviceLoader, DeviceStore
+    from gnnqc.data.synthetic import make_cml_raw
+    from gnnqc.models import BaselineClassifier, GCNClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.parallel import dist as D
+    from gnnqc.train.engine import Trainer
+    from gnnqc.train.loss import calculate_weights
+
+    dev = D.init_distributed()
+    world, rank = D.world_size(), D.rank()
+    torch.manual_seed(1234)
+    pc = C.normalize_preproc(C.default("preprocessing_cml"))
+    pc.batch_size = args.batch
+    mc = C.default("model_cml")
+    mc.runtime.compute_dtype = args.dtype
+    raw = make_cml_raw(n_sensors=args.sensors, n_minutes=args.days * 1440, seed=7)
+    ws = create_windows_dataset(pc, raw=raw)
+    store = DeviceStore(ws, "rolling_median", pc.graph, device=dev)
+    tr, _, _ = load_dataset(pc, ws)
+    loader = DeviceLoader(store, tr, args.batch, shuffle=True, seed=44, rank=rank, world_size=world,
+                          drop_last=True)
+    baseline = args.model == "baseline"
+    model = (BaselineClassifier if baseline else GCNClassifier)(mc, pc).to(dev)
+    n_params = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    opt = make_optimizer("adam", model.parameters(), mc.learning_rate)
+    D.broadcast_module(model)
+    trainer = Trainer(model, store, opt, calculate_weights(mc), baseline,
+                      use_graph=not args.no_graph, batch_size=args.batch)
+    rows = loader.batch_ids()                 # [n_batches, B] device tensor, no host sync while stepping
+    nb = rows.shape[0]
+
+    def run(k, start):
+        for i in range(k):
+            trainer.train_step(rows[(start + i) % nb])
+
+    run(args.warmup, 0)
+    D.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, args.warmup)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    D.barrier()
+    dt = time.perf_counter() - t0
+    dt = D.max_over_ranks(dt)
+    loss = float(trainer.last_loss.item())
+    windows = args.steps * args.batch * world
+    value = windows / dt
+    if rank == 0:
+        out = {
+            "metric": "ROC-AUC (5-fold CV) + train windows/sec, CML GCN at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "train windows/s (whole job)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / REF_GCN_WINDOWS_PER_S, 2),
+            "vs_baseline_basis": "reference GCN predict() 350 windows/s on V100 (BASELINE.md nb:321); "
+                                 "reference training windows/s is not published",
+            "dtype": args.dtype,
+            "data": "synthetic (CML example shape: %d links x %d days @1min, T=181), random-init weights"
+                    % (args.sensors, args.days),
+            "config": {
+                "model": "CML GCN (GeneralConv16+mean pool+LSTM TimeLayer f16 n_stacks2+dense64)" if not baseline
+                else "CML baseline LSTM",
+                "global_batch": args.batch * world,
+                "seq_len": ws.seq_len,
+                "parallelism": f"dp{world}",
+                "trainable_params": n_params,
+                "hip_graph": trainer.use_graph,
+                "final_loss": round(loss, 5),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    D.destroy()
+
+
+if __name__ == "__main__":
+    main()

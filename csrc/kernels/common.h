@@ -1,0 +1,40 @@
+// Shared device helpers for the gnnqc gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+namespace gq {
+
+__device__ __forceinline__ float sigmoidf_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float tanhf_fast(float x) {
+  // tanh(x) = 2*sigmoid(2x) - 1 ; saturates correctly for |x| -> inf
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define GQ_CHECK(cond, msg) TORCH_CHECK(cond, "gnnqc: ", msg)
+#define GQ_LAUNCH_CHECK() do { hipError_t e__ = hipGetLastError(); TORCH_CHECK(e__ == hipSuccess, "gnnqc kernel launch failed: ", hipGetErrorString(e__)); } while (0)
+
+inline void check_f32_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "gnnqc: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "gnnqc: ", name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), "gnnqc: ", name, " must be contiguous");
+}
+
+}  // namespace gq

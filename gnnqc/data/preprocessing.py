@@ -1,0 +1,289 @@
+"""Reference-named preprocessing entry points (``libs/preprocessing_functions.py``).
+
+Pipeline, MI355X-first:
+
+    raw SensorData --prepare_groups--> [SensorGroup] --create_windows_dataset--> WindowSet
+        --load_dataset / load_dataset_CV--> window-id splits
+        --create_batched_dataset--> DeviceLoader (HBM-resident, GPU gather, static shapes)
+
+``create_sensors_ncfiles`` / ``create_tfrecords_dataset`` keep the reference's on-disk
+artefacts available: per-neighbourhood NetCDF files, a compact ``.npz`` window
+index per (tb, ta), and (optionally) genuine TFRecord ``SequenceExample`` files via
+:mod:`gnnqc.data.tfrecord`.
+"""
+from __future__ import annotations
+
+import glob
+import os
+from typing import List, Optional
+
+import numpy as np
+
+from ..config import Config, freq_minutes, normalize_preproc
+from .graph import compute_depth_matrix, compute_distance_matrix, get_neighbors, sensor_positions
+from .interp import interpolate_gaps
+from .raw_io import SensorData, read_netcdf, write_netcdf
+from .splits import chronological_split, day_numbers, kfold_split, monthly_random_split
+from .stats import calculate_statistics
+from .targets import CML_FLAG_VARS, create_target
+from .windows import SensorGroup, WindowSet, build_window_index
+
+CML_FEATURES = ["TL_1", "TL_2"]
+SOIL_FEATURES = ["moisture", "temp", "battv"]
+
+# which statistics each normalisation needs (the reference computes all of them)
+_NEEDS = {
+    "rolling_median": ("median",), "rolling_median_fractional": ("median",),
+    "rolling_mean": ("mean", "std"), "standarization": (), "scale": (), "median": (),
+    "scale_range": (), "none": (),
+}
+
+
+def _interp(values, time, max_gap):
+    return interpolate_gaps(values, time, max_gap).astype(np.float32)
+
+
+def prepare_cml_groups(ds: SensorData, cfg) -> List[SensorGroup]:
+    """CML part of ``create_sensors_ncfiles`` (``:79-120``) in memory."""
+    cfg = normalize_preproc(cfg)
+    time = ds.time
+    feats = []
+    for name in CML_FEATURES:
+        v = np.array(ds[name].data, dtype=np.float32)
+        v[v >= 200] = np.nan          # "High (over 200 dB) values replaced with NaN"
+        if cfg.interpolate:
+            v = _interp(v, time, np.timedelta64(5, "m"))
+        feats.append(v)
+    X = np.stack(feats, axis=1)       # [S, C, T]
+    target = create_target(ds, CML_FLAG_VARS, 3, "cml")
+    dist = compute_distance_matrix(ds, "cml", unit=cfg.get("distance_unit", "km"))
+    lat, lon = sensor_positions(ds, "cml")
+    flagged = np.nonzero(np.asarray(ds["flagged"].data, bool))[0]
+    max_dist = cfg.graph.max_sample_distance
+    groups = []
+    ids = ds.sensor_ids
+    for s in flagged:
+        nb = get_neighbors(dist, s, max_dist, "cml")
+        coords = {k: np.asarray(ds[k].data)[nb] for k in ("site_a_latitude", "site_a_longitude",
+                                                          "site_b_latitude", "site_b_longitude", "length")
+                  if k in ds}
+        groups.append(SensorGroup(
+            group_id=str(ids[s]), ds_type="cml", sensor_ids=ids[nb],
+            anomalous_pos=int(np.nonzero(nb == s)[0][0]), feature_names=list(CML_FEATURES),
+            features=np.ascontiguousarray(X[nb]), time=time, target=target[s].astype(bool),
+            distances=dist[np.ix_(nb, nb)], lat=lat[nb], lon=lon[nb], coords=coords))
+    return groups
+
+
+def prepare_soilnet_groups(ds: SensorData, cfg) -> List[SensorGroup]:
+    """SoilNet part of ``create_tfrecords_dataset`` (``:414-447``): one network-wide graph."""
+    cfg = normalize_preproc(cfg)
+    lat_all = np.asarray(ds["latitude"].data, np.float64)
+    lon_all = np.asarray(ds["longitude"].data, np.float64)
+    keep = ~(np.isnan(lat_all) | np.isnan(lon_all))
+    ds = ds.isel(sensor_id=np.nonzero(keep)[0])
+    time = ds.time
+    feats = []
+    for name in SOIL_FEATURES:
+        v = np.array(ds[name].data, dtype=np.float32)
+        if cfg.interpolate:
+            v = _interp(v, time, np.timedelta64(60, "m"))
+        feats.append(v)
+    X = np.stack(feats, axis=1)
+    target = create_target(ds, ds_type="soilnet", flags_type=cfg.get("flags_type", "manual"))
+    dist = compute_distance_matrix(ds, "soilnet", unit=cfg.get("distance_unit", "m"))
+    depths = compute_depth_matrix(ds)
+    lat, lon = sensor_positions(ds, "soilnet")
+    coords = {k: np.asarray(ds[k].data) for k in ("box_id", "level_id", "depth") if k in ds}
+    return [SensorGroup(group_id="soilnet", ds_type="soilnet", sensor_ids=ds.sensor_ids, anomalous_pos=-1,
+                        feature_names=list(SOIL_FEATURES), features=X, time=time, target=target,
+                        distances=dist, depths=depths, lat=lat, lon=lon, coords=coords)]
+
+
+def prepare_groups(ds: SensorData, cfg) -> List[SensorGroup]:
+    return prepare_cml_groups(ds, cfg) if cfg["ds_type"] == "cml" else prepare_soilnet_groups(ds, cfg)
+
+
+def add_statistics(groups: List[SensorGroup], cfg, normalization: Optional[str] = None):
+    """``calculate_statistics`` (``:123-173``) for what the normalisation needs."""
+    cfg = normalize_preproc(cfg)
+    norm = normalization or cfg.get("normalization") or ("rolling_median" if cfg.ds_type == "cml" else "scale_range")
+    needs = _NEEDS.get(norm, ("mean", "std", "median"))
+    for g in groups:
+        feats = {n: g.features[:, i, :] for i, n in enumerate(g.feature_names)}
+        g.stats = calculate_statistics(feats, int(cfg.window_length), which_rolling=needs)
+    return groups
+
+
+# ----------------------------------------------------------------- NetCDF files
+def group_to_sensordata(g: SensorGroup) -> SensorData:
+    ds = SensorData(attrs={"anomalous_sensor_id": g.group_id, "ds_type": g.ds_type})
+    ds.set_coord("sensor_id", "sensor_id", g.sensor_ids)
+    ds.set_coord("time", "time", g.time)
+    for k, v in g.coords.items():
+        ds.set_coord(k, "sensor_id", v)
+    if g.lat is not None:
+        ds.set_coord("lat", "sensor_id", g.lat)
+        ds.set_coord("lon", "sensor_id", g.lon)
+    for i, n in enumerate(g.feature_names):
+        ds[n] = (("sensor_id", "time"), g.features[:, i, :])
+    if g.ds_type == "cml":
+        ds["target"] = ("time", g.target.astype(bool))
+        flagged = np.zeros(g.n_nodes, bool)
+        flagged[g.anomalous_pos] = True
+        ds["flagged"] = ("sensor_id", flagged)
+    else:
+        ds["target"] = (("sensor_id", "time"), g.target.astype(np.float32))
+        ds["depths"] = (("sensor_id", "sensor_id1"), g.depths)
+    ds["distances"] = (("sensor_id", "sensor_id1"), g.distances)
+    return ds
+
+
+def sensordata_to_group(ds: SensorData) -> SensorGroup:
+    ds_type = ds.attrs.get("ds_type", "cml")
+    names = CML_FEATURES if ds_type == "cml" else SOIL_FEATURES
+    X = np.stack([np.asarray(ds[n].data, np.float32) for n in names], axis=1)
+    coords = {k: v.data for k, v in ds.coords.items() if k not in ("sensor_id", "time", "lat", "lon")}
+    if ds_type == "cml":
+        flagged = np.asarray(ds["flagged"].data, bool)
+        anom = int(np.nonzero(flagged)[0][0])
+        target = np.asarray(ds["target"].data, bool)
+        depths = None
+    else:
+        anom = -1
+        target = np.asarray(ds["target"].data, np.float32)
+        depths = np.asarray(ds["depths"].data)
+    return SensorGroup(group_id=str(ds.attrs.get("anomalous_sensor_id", "group")), ds_type=ds_type,
+                       sensor_ids=ds.sensor_ids, anomalous_pos=anom, feature_names=list(names), features=X,
+                       time=ds.time, target=target, distances=np.asarray(ds["distances"].data), depths=depths,
+                       lat=ds["lat"].data if "lat" in ds else None, lon=ds["lon"].data if "lon" in ds else None,
+                       coords=coords)
+
+
+def create_sensors_ncfiles(ds: SensorData, preproc_config) -> List[str]:
+    """Write one NetCDF per neighbourhood into ``ncfiles_dir`` (``:79-120``)."""
+    cfg = normalize_preproc(preproc_config)
+    out_dir = cfg.ncfiles_dir
+    os.makedirs(out_dir, exist_ok=True)
+    paths = []
+    for g in prepare_groups(ds, cfg):
+        p = os.path.join(out_dir, f"{g.group_id}.nc")
+        write_netcdf(group_to_sensordata(g), p)
+        paths.append(p)
+    return paths
+
+
+def load_sensor_groups(preproc_config) -> List[SensorGroup]:
+    cfg = normalize_preproc(preproc_config)
+    files = sorted(glob.glob(os.path.join(cfg.ncfiles_dir, "*.nc")))
+    return [sensordata_to_group(read_netcdf(f)) for f in files]
+
+
+# ----------------------------------------------------------------- windows
+def create_windows_dataset(preproc_config, groups: Optional[List[SensorGroup]] = None,
+                           raw: Optional[SensorData] = None, normalization: Optional[str] = None) -> WindowSet:
+    """Compute statistics and the window index of every group (the work of
+    ``create_tfrecords_dataset`` ``:343-482`` without serialising records)."""
+    cfg = normalize_preproc(preproc_config)
+    if groups is None:
+        if raw is not None:
+            groups = prepare_groups(raw, cfg)
+        elif cfg.ds_type == "cml":
+            groups = load_sensor_groups(cfg)
+        else:
+            groups = prepare_groups(read_netcdf(cfg.raw_dataset_path), cfg)
+    add_statistics(groups, cfg, normalization)
+    f = freq_minutes(cfg.ds_type)
+    min_date = cfg.get("min_date")
+    max_date = cfg.get("max_date")
+    indices = [build_window_index(g, i, cfg.timestep_before, cfg.timestep_after, f, min_date, max_date)
+               for i, g in enumerate(groups)]
+    return WindowSet(groups=groups, indices=indices, ds_type=cfg.ds_type,
+                     timestep_before=int(cfg.timestep_before), timestep_after=int(cfg.timestep_after), freq=f)
+
+
+def create_tfrecords_dataset(preproc_config, windows: Optional[WindowSet] = None, write_records: bool = False,
+                             max_records: Optional[int] = None) -> str:
+    """Persist the window index (and optionally real TFRecord files).
+
+    Output dir: ``<tfrecords_dataset_dir>/<tb>_<ta>`` like ``:355-360``. The index is
+    ``windows.npz``; with ``write_records`` every window is also written as a
+    ``SequenceExample`` into ``<sensor>_<day>.tfrec`` / ``<day>.tfrec`` files.
+    """
+    cfg = normalize_preproc(preproc_config)
+    if windows is None:
+        windows = create_windows_dataset(cfg)
+    out = os.path.join(cfg.tfrecords_dataset_dir, f"{cfg.timestep_before}_{cfg.timestep_after}")
+    os.makedirs(out, exist_ok=True)
+    arrays = {}
+    for i, ix in enumerate(windows.indices):
+        arrays[f"g{i}_center"] = ix.center
+        arrays[f"g{i}_valid"] = ix.node_valid
+        arrays[f"g{i}_labels"] = ix.labels
+        if ix.label_valid is not None:
+            arrays[f"g{i}_label_valid"] = ix.label_valid
+    arrays["group_ids"] = np.array([g.group_id for g in windows.groups])
+    np.savez_compressed(os.path.join(out, "windows.npz"), **arrays)
+    if write_records:
+        from .tfrecord import write_window_records
+        write_window_records(windows, out, normalization=cfg.get("normalization"), max_records=max_records)
+    return out
+
+
+# ----------------------------------------------------------------- splits
+def load_dataset(preproc_config, windows: WindowSet):
+    """(train_ids, val_ids, test_ids) window-id arrays (``:485-563``)."""
+    cfg = normalize_preproc(preproc_config)
+    days = windows.window_days()
+    if windows.ds_type == "cml":
+        tr, va, te = chronological_split(days, cfg.train_fraction, cfg.val_fraction,
+                                         cfg.timestep_before, cfg.timestep_after)
+    else:
+        tr, va, te = monthly_random_split(days, cfg.train_fraction, cfg.val_fraction,
+                                          cfg.timestep_before, cfg.timestep_after, seed=cfg.random_state)
+    ids = np.arange(windows.n_windows)
+    return ids[tr], ids[va], ids[te]
+
+
+def load_dataset_CV(preproc_config, windows: WindowSet, test_split: int = 0, gap_days: Optional[int] = None):
+    """(train_ids, test_ids, cfg) for fold ``test_split`` (``xai/...:804-836``).
+
+    File numbers are day numbers (one record file per group and day).
+    """
+    cfg = normalize_preproc(preproc_config)
+    cfg.split = test_split
+    k = int(cfg.dataset.get("split_numb", cfg.get("split_numb", 5)))
+    fn = day_numbers(windows.window_days())
+    gap = int(cfg.get("cv_gap_days", 0) if gap_days is None else gap_days)
+    tr, te = kfold_split(fn, k, test_split, gap=gap)
+    ids = np.arange(windows.n_windows)
+    return ids[tr], ids[te], cfg
+
+
+def create_batched_dataset(window_ids, preproc_config, store, shuffle: bool = True, baseline: bool = False,
+                           rank: int = 0, world_size: int = 1, batch_size: Optional[int] = None):
+    """DeviceLoader over ``window_ids`` + config + wrapping functions (``:936-965``).
+
+    Like the reference, ``preproc_config.normalization`` is set from the loader's
+    normalisation (``:941,964``).
+    """
+    from .store import DeviceLoader
+    cfg = preproc_config
+    loader = DeviceLoader(store, window_ids, batch_size or cfg["batch_size"], shuffle=shuffle,
+                          seed=cfg.get("random_state", 44), rank=rank, world_size=world_size)
+    cfg["normalization"] = store.normalization
+
+    def wrap_model(batch):
+        return batch.model_inputs(store.ds_type, baseline), batch.y
+
+    def wrap_plot(batch):
+        return (batch.model_inputs(store.ds_type, baseline), batch.wid), batch.y
+
+    return loader, cfg, [wrap_model, wrap_plot]
+
+
+__all__ = [
+    "prepare_cml_groups", "prepare_soilnet_groups", "prepare_groups", "add_statistics",
+    "create_sensors_ncfiles", "load_sensor_groups", "create_windows_dataset", "create_tfrecords_dataset",
+    "load_dataset", "load_dataset_CV", "create_batched_dataset", "group_to_sensordata", "sensordata_to_group",
+]

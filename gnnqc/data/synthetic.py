@@ -1,0 +1,322 @@
+"""Synthetic raw datasets with the reference schemas.
+
+The reference's raw archives (``example_data/*.nc``) are not available, so these
+generators produce data of the same shape and schema, with physics chosen so that
+the spatial context matters (the mechanism the paper's GCN exploits):
+
+* **CML** - microwave links around a centre point. Total loss ``TL_1/TL_2`` =
+  per-link baseline + diurnal drift + noise + **rain attenuation** from moving,
+  spatially coherent rain cells (seen by every link the cell passes: NOT an
+  anomaly) + sensor-specific **anomalies** on the flagged links (jumps, dew bumps,
+  fluctuations, unknown drops/spikes) that only that link shows. Four simulated
+  experts flag each anomaly with boundary jitter; the label is >=3 experts
+  (``create_target``). Gaps and >200 dB spikes emulate data problems.
+* **SoilNet** - boxes with sensors at 6 depths; moisture responds to site-wide
+  rain with depth-dependent lag and damping, temperature follows a damped diurnal
+  cycle, battery voltage decays with recharges. Sensor-specific faults (drops,
+  spikes, drift, noise) are flagged ``moisture_flag_Manual``; normal data
+  ``moisture_flag_OK``; some periods are unlabelled.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .raw_io import SensorData
+
+_KM_PER_DEG_LAT = 111.2
+
+
+def _offset_latlon(lat0, lon0, dx_km, dy_km):
+    lat = lat0 + dy_km / _KM_PER_DEG_LAT
+    lon = lon0 + dx_km / (_KM_PER_DEG_LAT * np.cos(np.radians(lat0)))
+    return lat, lon
+
+
+def _smooth_bump(n, rise, rng):
+    """A smooth 0->1->0 envelope of length n."""
+    t = np.linspace(0, np.pi, n)
+    return np.sin(t) ** (1.0 + rise * rng.random())
+
+
+def _rain_field(n_sensors, n_time, mx, my, rng, rain_fraction=0.06, minutes_per_step=1.0):
+    """Rain rate [sensor, time] (mm/h) from moving Gaussian rain cells."""
+    rate = np.zeros((n_sensors, n_time), dtype=np.float32)
+    total_h = n_time * minutes_per_step / 60.0
+    n_cells = max(1, int(total_h * rain_fraction / 1.5))
+    for _ in range(n_cells):
+        dur = int(rng.uniform(30, 300) / minutes_per_step)
+        t0 = int(rng.integers(0, max(1, n_time - dur)))
+        # cell path across the domain
+        ang = rng.uniform(0, 2 * np.pi)
+        speed = rng.uniform(15, 60) / 60.0 * minutes_per_step  # km per step
+        start = np.array([rng.uniform(-25, 25), rng.uniform(-25, 25)])
+        radius = rng.uniform(3, 14)
+        peak = rng.gamma(2.0, 8.0)
+        tt = np.arange(dur)
+        cx = start[0] + np.cos(ang) * speed * (tt - dur / 2)
+        cy = start[1] + np.sin(ang) * speed * (tt - dur / 2)
+        env = _smooth_bump(dur, 1.0, rng)
+        # small-scale variability within the cell
+        env = env * np.clip(1 + 0.3 * np.convolve(rng.standard_normal(dur), np.ones(9) / 9, "same"), 0.2, 2)
+        d2 = (mx[:, None] - cx[None, :]) ** 2 + (my[:, None] - cy[None, :]) ** 2
+        rate[:, t0:t0 + dur] += (peak * env[None, :] * np.exp(-d2 / (2 * radius ** 2))).astype(np.float32)
+    return rate
+
+
+def make_cml_raw(n_sensors: int = 23, n_flagged: int = 1, n_minutes: int = 40320,
+                 start: str = "2019-07-02T00:00", seed: int = 0, center=(51.5, 7.45),
+                 extent_km: float = 12.0, anomaly_rate: float = 1.0, rain_fraction: float = 0.06,
+                 gap_rate: float = 2e-4, difficulty: float = 1.0) -> SensorData:
+    """CML raw dataset (schema of ``cml_raw_example.nc``).
+
+    ``anomaly_rate`` scales the number of anomaly events per flagged link
+    (1.0 ~ 10-15% anomalous minutes); ``difficulty`` scales how rain-like the
+    anomalies look (amplitudes/shape overlap with rain attenuation).
+    """
+    rng = np.random.default_rng(seed)
+    S, T = n_sensors, n_minutes
+    time = np.arange(np.datetime64(start, "m"), np.datetime64(start, "m") + np.timedelta64(T, "m"))
+    # --- geometry: link mid-points in a disc, random orientation and length
+    r = extent_km * np.sqrt(rng.random(S))
+    th = rng.uniform(0, 2 * np.pi, S)
+    mx, my = r * np.cos(th), r * np.sin(th)
+    length = rng.uniform(0.5, 12.0, S)
+    orient = rng.uniform(0, np.pi, S)
+    ax_, ay_ = mx - np.cos(orient) * length / 2, my - np.sin(orient) * length / 2
+    bx_, by_ = mx + np.cos(orient) * length / 2, my + np.sin(orient) * length / 2
+    lat_a, lon_a = _offset_latlon(center[0], center[1], ax_, ay_)
+    lat_b, lon_b = _offset_latlon(center[0], center[1], bx_, by_)
+    freq1 = rng.choice([15.0, 18.0, 23.0, 26.0, 32.0, 38.0], S)
+    freq2 = freq1 + rng.choice([-1.0, 1.0], S) * rng.uniform(0.5, 1.5, S)
+    pol1 = rng.choice(np.array(["H", "V"]), S)
+    pol2 = np.where(rng.random(S) < 0.8, pol1, np.where(pol1 == "H", "V", "H"))
+    # --- baseline signal
+    minute_of_day = (np.arange(T) % 1440).astype(np.float32)
+    diurnal = np.sin(2 * np.pi * (minute_of_day - 300) / 1440.0)
+    base1 = rng.uniform(40, 70, S)[:, None]
+    base2 = base1 + rng.normal(0, 2.0, S)[:, None]
+    drift_amp = rng.uniform(0.1, 0.5, S)[:, None]
+    slow = np.cumsum(rng.normal(0, 0.01, (S, T)), axis=1).astype(np.float32)
+    slow -= np.linspace(0, 1, T)[None, :] * slow[:, -1:]
+    tl1 = base1 + drift_amp * diurnal[None, :] + slow + rng.normal(0, 0.12, (S, T))
+    tl2 = base2 + drift_amp * 0.9 * diurnal[None, :] + slow + rng.normal(0, 0.12, (S, T))
+    # --- rain attenuation (spatially coherent, not an anomaly)
+    rain = _rain_field(S, T, mx, my, rng, rain_fraction=rain_fraction)
+    kcoef1 = (0.0009 * freq1 ** 1.8)[:, None]
+    kcoef2 = (0.0009 * freq2 ** 1.8)[:, None]
+    wet = 1.2 * (1 - np.exp(-rain / 1.5))
+    tl1 = tl1 + kcoef1 * rain ** 1.05 * length[:, None] + wet
+    tl2 = tl2 + kcoef2 * rain ** 1.05 * length[:, None] + wet
+    # --- anomalies on flagged links + expert flags
+    flagged = np.zeros(S, bool)
+    # flagged links are drawn among the most central links so they have neighbours
+    order = np.argsort(mx ** 2 + my ** 2)
+    flagged[order[:n_flagged]] = True
+    n_exp = 4
+    flag_names = ["Jump", "Dew", "Fluctuation", "Unknown anomaly"]
+    flags = {k: np.zeros((n_exp, S, T), dtype=bool) for k in flag_names}
+    days = T / 1440.0
+    for s in np.nonzero(flagged)[0]:
+        n_events = rng.poisson(anomaly_rate * days * 1.6)
+        for _ in range(n_events):
+            kind = rng.choice(4, p=[0.3, 0.25, 0.3, 0.15])
+            if kind == 0:    # jump: level shift for a while
+                dur = int(rng.uniform(20, 240))
+                t0 = int(rng.integers(0, T - dur))
+                amp = rng.choice([-1, 1]) * rng.uniform(1.0, 6.0) / difficulty
+                prof = np.ones(dur) * amp
+                ramp = min(3, dur // 4)
+                if ramp > 0:
+                    prof[:ramp] *= np.linspace(0.3, 1, ramp)
+            elif kind == 1:  # dew: morning bump
+                dur = int(rng.uniform(60, 240))
+                day0 = int(rng.integers(0, max(1, int(days) - 1)))
+                t0 = min(T - dur - 1, day0 * 1440 + int(rng.uniform(180, 420)))
+                amp = rng.uniform(1.0, 4.0) / difficulty
+                prof = amp * _smooth_bump(dur, 0.5, rng)
+            elif kind == 2:  # fluctuation: high-frequency noise burst
+                dur = int(rng.uniform(30, 240))
+                t0 = int(rng.integers(0, T - dur))
+                sig = rng.uniform(0.6, 2.5) / difficulty
+                prof = rng.normal(0, sig, dur) + np.abs(rng.normal(0, sig / 2, dur))
+            else:            # unknown: deep drops/spikes or drift
+                dur = int(rng.uniform(10, 120))
+                t0 = int(rng.integers(0, T - dur))
+                amp = rng.uniform(3, 12) / difficulty
+                prof = amp * (rng.random(dur) < 0.3) * rng.uniform(0.3, 1.0, dur)
+            tl1[s, t0:t0 + dur] += prof
+            tl2[s, t0:t0 + dur] += prof * rng.uniform(0.7, 1.1)
+            name = flag_names[kind]
+            for e in range(n_exp):
+                if rng.random() < 0.92:
+                    j0 = int(np.clip(t0 + rng.integers(-6, 7), 0, T - 1))
+                    j1 = int(np.clip(t0 + dur + rng.integers(-6, 7), j0 + 1, T))
+                    flags[name][e, s, j0:j1] = True
+    # --- quantisation, gaps, out-of-range spikes
+    tl1 = np.round(tl1 * 10) / 10
+    tl2 = np.round(tl2 * 10) / 10
+    for arr in (tl1, tl2):
+        g = rng.random((S, T)) < gap_rate
+        for s, t in zip(*np.nonzero(g)):
+            arr[s, t:t + int(rng.integers(1, 8))] = np.nan
+        spikes = rng.random((S, T)) < gap_rate / 4
+        arr[spikes] = 255.0
+    # occasional long outages on unflagged links
+    for s in range(S):
+        if not flagged[s] and rng.random() < 0.3:
+            t0 = int(rng.integers(0, T - 600))
+            d = int(rng.uniform(60, 600))
+            tl1[s, t0:t0 + d] = np.nan
+            tl2[s, t0:t0 + d] = np.nan
+    ids = np.array([f"SY{1000 + i:04d}_2_SY{5000 + 7 * i:04d}_{1 + i % 4}" for i in range(S)])
+    ds = SensorData(attrs={"title": "synthetic CML raw dataset (gnnqc)", "seed": seed})
+    ds.set_coord("sensor_id", "sensor_id", ids)
+    ds.set_coord("time", "time", time)
+    ds.set_coord("expert", "expert", np.arange(n_exp, dtype=np.int32))
+    ds.set_coord("length", "sensor_id", length.astype(np.float64))
+    ds.set_coord("site_a_latitude", "sensor_id", lat_a)
+    ds.set_coord("site_a_longitude", "sensor_id", lon_a)
+    ds.set_coord("site_b_latitude", "sensor_id", lat_b)
+    ds.set_coord("site_b_longitude", "sensor_id", lon_b)
+    ds.set_coord("frequency_1", "sensor_id", freq1)
+    ds.set_coord("frequency_2", "sensor_id", freq2)
+    ds.set_coord("polarization_1", "sensor_id", pol1)
+    ds.set_coord("polarization_2", "sensor_id", pol2)
+    ds["TL_1"] = (("sensor_id", "time"), tl1.astype(np.float32))
+    ds["TL_2"] = (("sensor_id", "time"), tl2.astype(np.float32))
+    for k in flag_names:
+        ds[k] = (("expert", "sensor_id", "time"), flags[k])
+    ds["flagged"] = ("sensor_id", flagged)
+    return ds
+
+
+def make_soilnet_raw(n_boxes: int = 40, n_time: int = 8545, start: str = "2014-08-01T00:00",
+                     seed: int = 0, center=(51.35, 12.43), extent_m: float = 60.0,
+                     fault_rate: float = 1.0, max_sensors: int | None = 210) -> SensorData:
+    """SoilNet raw dataset (schema of ``soilnet_raw_example.nc``), 15-min resolution."""
+    rng = np.random.default_rng(seed)
+    depths_all = np.array([0.05, 0.1, 0.2, 0.3, 0.4, 0.6])
+    box_xy = rng.uniform(-extent_m, extent_m, (n_boxes, 2)) / 1000.0  # km
+    # many boxes share one of a few clusters so same-depth neighbours exist within 20 m
+    n_clusters = max(1, n_boxes // 4)
+    cl = rng.uniform(-extent_m, extent_m, (n_clusters, 2)) / 1000.0
+    which = rng.integers(0, n_clusters, n_boxes)
+    box_xy = cl[which] + rng.normal(0, 0.008, (n_boxes, 2))
+    sensors = []
+    for b in range(n_boxes):
+        nlev = 6 if rng.random() < 0.75 else int(rng.integers(3, 6))
+        for lvl in range(nlev):
+            sensors.append((b, lvl, depths_all[lvl]))
+    if max_sensors is not None:
+        sensors = sensors[:max_sensors]
+    S, T = len(sensors), n_time
+    box_id = np.array([s[0] for s in sensors], dtype=np.int32)
+    level_id = np.array([s[1] for s in sensors], dtype=np.int32)
+    depth = np.array([s[2] for s in sensors], dtype=np.float64)
+    lat, lon = _offset_latlon(center[0], center[1], box_xy[box_id, 0], box_xy[box_id, 1])
+    step_h = 0.25
+    tt = np.arange(T)
+    hour = (tt * step_h) % 24
+    # --- site rain (event based), spatially varying intensity per box
+    rain = np.zeros(T)
+    n_ev = int(T * step_h / 24 * 0.35)
+    for _ in range(n_ev):
+        t0 = int(rng.integers(0, T - 40))
+        d = int(rng.integers(2, 24))
+        rain[t0:t0 + d] += rng.gamma(1.5, 1.2)
+    box_gain = rng.uniform(0.7, 1.3, n_boxes)[box_id]
+    # infiltration: first order response, lag & damping grow with depth
+    moist = np.zeros((S, T))
+    base = rng.uniform(12, 35, S)
+    tau_dry = 150 + 400 * depth  # steps
+    for i in range(S):
+        lag = int(depth[i] * 40)
+        resp = np.convolve(rain, np.exp(-np.arange(200) / (4 + 30 * depth[i])), "full")[:T]
+        resp = np.roll(resp, lag)
+        resp[:lag] = 0
+        from scipy.signal import lfilter
+        a = np.exp(-1.0 / tau_dry[i])
+        gain = box_gain[i] * (1.6 - depth[i]) * 0.9
+        wet = lfilter([1.0], [1.0, -a], gain * resp * 0.12)
+        moist[i] = base[i] + np.minimum(wet, 25) + rng.normal(0, 0.15, T)
+    # --- temperature
+    season = 15 - 8 * (tt / T)
+    temp = np.zeros((S, T))
+    for i in range(S):
+        amp = 8 * np.exp(-depth[i] / 0.12)
+        ph = depth[i] * 10
+        temp[i] = season + amp * np.sin(2 * np.pi * (hour - 9 - ph) / 24) + rng.normal(0, 0.1, T)
+    # --- battery (per box)
+    batt_box = np.zeros((n_boxes, T))
+    for b in range(n_boxes):
+        v = rng.uniform(3300, 3550)
+        for t in range(T):
+            v -= rng.uniform(0.0, 0.08)
+            if v < 2950 and rng.random() < 0.02:
+                v = rng.uniform(3400, 3550)
+            batt_box[b, t] = v
+    battv = batt_box[box_id] + rng.normal(0, 2, (S, T))
+    # --- faults (sensor specific) -> manual flags
+    manual = np.zeros((S, T), bool)
+    n_days = T * step_h / 24
+    for i in range(S):
+        n_f = rng.poisson(fault_rate * n_days / 12)
+        for _ in range(n_f):
+            kind = rng.integers(0, 4)
+            d = int(rng.integers(8, 300))
+            t0 = int(rng.integers(0, T - d))
+            if kind == 0:    # drop to implausibly low value
+                moist[i, t0:t0 + d] = moist[i, t0:t0 + d] * rng.uniform(0.2, 0.6)
+            elif kind == 1:  # spikes
+                idx = t0 + np.nonzero(rng.random(d) < 0.3)[0]
+                moist[i, idx] += rng.uniform(5, 25, idx.size)
+            elif kind == 2:  # drift
+                moist[i, t0:t0 + d] += np.linspace(0, rng.uniform(-10, 10), d)
+            else:            # noise
+                moist[i, t0:t0 + d] += rng.normal(0, rng.uniform(1, 4), d)
+            manual[i, t0:t0 + d] = True
+    # --- flags
+    flags = {}
+    no_label = np.zeros((S, T), bool)
+    for i in range(S):
+        if rng.random() < 0.2:
+            d = int(rng.integers(50, 800))
+            t0 = int(rng.integers(0, T - d))
+            no_label[i, t0:t0 + d] = True
+    no_label &= ~manual
+    auto_batt = battv < 2900
+    auto_range = (moist <= 0) | (moist >= 100)
+    dm = np.abs(np.diff(moist, axis=1, prepend=moist[:, :1]))
+    auto_spike = dm > 8
+    ok = ~(manual | no_label | auto_batt | auto_range)
+    for var in ("moisture", "temp"):
+        flags[f"{var}_flag_no_label"] = no_label.copy()
+        flags[f"{var}_flag_Auto:BattV"] = auto_batt.copy()
+        flags[f"{var}_flag_Auto:Range"] = auto_range.copy() if var == "moisture" else np.zeros_like(ok)
+        flags[f"{var}_flag_Auto:Spike"] = auto_spike.copy() if var == "moisture" else np.zeros_like(ok)
+        flags[f"{var}_flag_Manual"] = manual.copy() if var == "moisture" else np.zeros_like(ok)
+        flags[f"{var}_flag_OK"] = ok.copy() if var == "moisture" else ~no_label
+    # --- gaps
+    for arr in (moist, temp, battv):
+        g = rng.random((S, T)) < 3e-4
+        for i, t in zip(*np.nonzero(g)):
+            arr[i, t:t + int(rng.integers(1, 10))] = np.nan
+    time = np.arange(np.datetime64(start, "m"), np.datetime64(start, "m") + np.timedelta64(15 * T, "m"),
+                     np.timedelta64(15, "m"))
+    ds = SensorData(attrs={"title": "synthetic SoilNet raw dataset (gnnqc)", "seed": seed})
+    ds.set_coord("sensor_id", "sensor_id", np.arange(S, dtype=np.int64))
+    ds.set_coord("time", "time", time)
+    ds.set_coord("box_id", "sensor_id", box_id)
+    ds.set_coord("level_id", "sensor_id", level_id)
+    ds.set_coord("latitude", "sensor_id", lat)
+    ds.set_coord("longitude", "sensor_id", lon)
+    ds.set_coord("depth", "sensor_id", depth)
+    ds["moisture"] = (("sensor_id", "time"), moist.astype(np.float32))
+    ds["temp"] = (("sensor_id", "time"), temp.astype(np.float32))
+    ds["battv"] = (("sensor_id", "time"), battv.astype(np.float32))
+    for k, v in flags.items():
+        ds[k] = (("sensor_id", "time"), v)
+    return ds
+
+
+__all__ = ["make_cml_raw", "make_soilnet_raw"]

@@ -1,0 +1,96 @@
+"""TimeLayer: stacked temporal encoder (``libs/create_model.py:43-136``).
+
+LSTM branch: ``LSTM(f) -> LSTM(f) -> MaxPool(p)``, then ``n_stacks`` x
+[``LSTM(f*2^(i+1)) x 2 -> MaxPool(p)``], then ``LSTM(f*2^(n+1))`` returning the last
+state. CNN branch: the same pattern with ``Conv1D(same) + LeakyReLU(alpha)`` and a
+final ``GlobalAveragePooling1D``. (The reference's TimeLayer hard-codes pool size 3
+for the CNN stack pools, ``:99``; the baseline uses ``pool_size``, ``:320``.)
+
+Attribute names mirror the reference (``time1, time2, time_layers, pooling_layers,
+time4``) so checkpoint variable paths line up.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .layers import LSTM, Conv1D, GlobalAveragePooling1D, LeakyReLU, MaxPooling1D
+
+
+class TimeLayer(nn.Module):
+    def __init__(self, in_features: int, filter_1_size: int = 8, n_stacks: int = 2, layer_type: str = "lstm",
+                 activation: str = "tanh", kernel_size: Optional[int] = 5, regularizer: Optional[float] = None,
+                 pool_size: int = 3, alpha: float = 0.3, cnn_stack_pool: Optional[int] = 3,
+                 compute_bf16: bool = True):
+        super().__init__()
+        self.layer_type = layer_type
+        self.filter_1_size, self.n_stacks, self.pool_size, self.alpha = filter_1_size, n_stacks, pool_size, alpha
+        f = filter_1_size
+        self.time_layers = nn.ModuleList()
+        self.pooling_layers = nn.ModuleList()
+        if layer_type == "lstm":
+            mk = lambda i, o, seq=True: LSTM(i, o, activation, seq, regularizer, compute_bf16)  # noqa: E731
+            self.time1 = mk(in_features, f)
+            self.time2 = mk(f, f)
+            self.max_pooling = MaxPooling1D(pool_size)
+            prev = f
+            for i in range(n_stacks):
+                u = f * 2 ** (i + 1)
+                self.time_layers.append(mk(prev, u))
+                self.time_layers.append(mk(u, u))
+                self.pooling_layers.append(MaxPooling1D(pool_size))
+                prev = u
+            self.time4 = mk(prev, f * 2 ** (n_stacks + 1), False)
+        else:
+            if kernel_size is None:
+                raise ValueError("CNN TimeLayer needs kernel_size")
+            self.time1 = Conv1D(in_features, f, kernel_size, regularizer=regularizer)
+            self.time2 = Conv1D(f, f, kernel_size, regularizer=regularizer)
+            self.leakyrelu1 = LeakyReLU(alpha)
+            self.leakyrelu2 = LeakyReLU(alpha)
+            self.max_pooling = MaxPooling1D(pool_size)
+            self.leakyrelu_layers = nn.ModuleList()
+            prev = f
+            for i in range(n_stacks):
+                u = f * 2 ** (i + 1)
+                self.time_layers.append(Conv1D(prev, u, kernel_size, regularizer=regularizer))
+                self.leakyrelu_layers.append(LeakyReLU(alpha))
+                self.time_layers.append(Conv1D(u, u, kernel_size, regularizer=regularizer))
+                self.leakyrelu_layers.append(LeakyReLU(alpha))
+                self.pooling_layers.append(MaxPooling1D(cnn_stack_pool or pool_size))
+                prev = u
+            self.time4 = Conv1D(prev, f * 2 ** (n_stacks + 1), kernel_size, regularizer=regularizer)
+            self.leakyrelu3 = LeakyReLU(alpha)
+            self.global_pooling = GlobalAveragePooling1D()
+
+    @property
+    def out_features(self) -> int:
+        return self.filter_1_size * 2 ** (self.n_stacks + 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        cnn = self.layer_type != "lstm"
+        x1 = self.time1(x)
+        if cnn:
+            x1 = self.leakyrelu1(x1)
+        x1 = self.time2(x1)
+        if cnn:
+            x1 = self.leakyrelu2(x1)
+        x1 = self.max_pooling(x1)
+        for i in range(len(self.pooling_layers)):
+            x1 = self.time_layers[2 * i](x1)
+            if cnn:
+                x1 = self.leakyrelu_layers[2 * i](x1)
+            x1 = self.time_layers[2 * i + 1](x1)
+            if cnn:
+                x1 = self.leakyrelu_layers[2 * i + 1](x1)
+            x1 = self.pooling_layers[i](x1)
+        x1 = self.time4(x1)
+        if cnn:
+            x1 = self.leakyrelu3(x1)
+            x1 = self.global_pooling(x1)
+        return x1
+
+
+__all__ = ["TimeLayer"]

@@ -1,0 +1,178 @@
+"""Flat-buffer optimisers.
+
+All trainable parameters of a model are re-homed into ONE contiguous fp32
+buffer (each ``Parameter.data`` becomes a view), and their ``.grad`` tensors into
+a second one. Consequences on MI355X:
+
+* the data-parallel gradient all-reduce is a single RCCL collective on one
+  753 KB buffer (no per-tensor launches, no bucketing metadata);
+* the Adam update is one HIP kernel over the whole buffer;
+* lr / step live on the device, so the optimiser launch can be captured in a HIP
+  graph and replayed while the LR schedule changes.
+
+Optimisers by name like ``libs/fit_model.py:71-74``: adam (Keras eps 1e-7,
+"epsilon-hat" update), sgd, rmsprop (Keras defaults rho .9, eps 1e-7).
+"""
+from __future__ import annotations
+
+from typing import Iterable, List
+
+import torch
+
+
+def flatten_parameters(params: Iterable[torch.nn.Parameter], align: int = 4):
+    """Move params (and grads) into contiguous buffers; returns (flat_p, flat_g, slices)."""
+    params = [p for p in params if p.requires_grad]
+    if not params:
+        raise ValueError("no trainable parameters")
+    dev, dt = params[0].device, params[0].dtype
+    sizes = []
+    off = 0
+    for p in params:
+        n = p.numel()
+        sizes.append((off, n))
+        off += (n + align - 1) // align * align
+    flat_p = torch.zeros(off, device=dev, dtype=dt)
+    flat_g = torch.zeros(off, device=dev, dtype=dt)
+    for p, (o, n) in zip(params, sizes):
+        flat_p[o:o + n].copy_(p.data.reshape(-1))
+        p.data = flat_p[o:o + n].view_as(p.data)
+        p.grad = flat_g[o:o + n].view_as(p.data)
+    return flat_p, flat_g, params
+
+
+class FlatOptimizer:
+    """Base: owns the flat buffers of a module's trainables."""
+
+    def __init__(self, params, lr: float):
+        self.flat_p, self.flat_g, self.params = flatten_parameters(params)
+        dev = self.flat_p.device
+        self.lr_t = torch.tensor([float(lr)], device=dev, dtype=torch.float32)
+        self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.iterations = 0
+
+    @property
+    def lr(self) -> float:
+        return float(self.lr_t.item())
+
+    @lr.setter
+    def lr(self, value: float):
+        self.lr_t.fill_(float(value))
+
+    def zero_grad(self):
+        # grads are views into flat_g: never set them to None
+        self.flat_g.zero_()
+
+    def relink_grads(self):
+        """Re-attach grads as views (autograd may have replaced .grad)."""
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            if p.grad is None or p.grad.data_ptr() != self.flat_g[off:off + n].data_ptr():
+                g = self.flat_g[off:off + n].view_as(p.data)
+                if p.grad is not None:
+                    g.copy_(p.grad)
+                p.grad = g
+            off += (n + 3) // 4 * 4
+
+    def state_dict(self):
+        return {"lr": self.lr, "iterations": self.iterations}
+
+    def load_state_dict(self, sd):
+        self.lr = sd["lr"]
+        self.iterations = int(sd["iterations"])
+        self.step_t.fill_(float(self.iterations))
+
+
+class FlatAdam(FlatOptimizer):
+    def __init__(self, params, lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-7,
+                 weight_decay: float = 0.0):
+        super().__init__(params, lr)
+        self.beta1, self.beta2, self.eps, self.wd = beta1, beta2, eps, weight_decay
+        self.m = torch.zeros_like(self.flat_p)
+        self.v = torch.zeros_like(self.flat_p)
+
+    def step(self, grad_scale: float = 1.0):
+        from . import use_hip
+        self.step_t.add_(1.0)
+        self.iterations += 1
+        if use_hip(self.flat_p):
+            from ..utils.native import hip_ops
+            hip_ops().adam_step(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
+                                self.beta2, self.eps, float(grad_scale), self.wd)
+            return
+        with torch.no_grad():
+            g = self.flat_g * grad_scale
+            if self.wd:
+                g = g + self.wd * self.flat_p
+            self.m.mul_(self.beta1).add_(g * (1 - self.beta1))
+            self.v.mul_(self.beta2).add_(g * g * (1 - self.beta2))
+            t = self.step_t
+            alpha = self.lr_t * torch.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
+            self.flat_p.sub_(alpha * self.m / (torch.sqrt(self.v) + self.eps))
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd.update(m=self.m.detach().cpu(), v=self.v.detach().cpu())
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        self.m.copy_(sd["m"].to(self.m.device))
+        self.v.copy_(sd["v"].to(self.v.device))
+
+    def slots(self) -> List[torch.Tensor]:
+        return [self.m, self.v]
+
+
+class FlatSGD(FlatOptimizer):
+    def __init__(self, params, lr: float = 0.01, momentum: float = 0.0):
+        super().__init__(params, lr)
+        self.momentum = momentum
+        self.buf = torch.zeros_like(self.flat_p) if momentum else None
+
+    def step(self, grad_scale: float = 1.0):
+        self.step_t.add_(1.0)
+        self.iterations += 1
+        with torch.no_grad():
+            g = self.flat_g * grad_scale
+            if self.buf is not None:
+                self.buf.mul_(self.momentum).sub_(self.lr_t * g)
+                self.flat_p.add_(self.buf)
+            else:
+                self.flat_p.sub_(self.lr_t * g)
+
+    def slots(self):
+        return [self.buf] if self.buf is not None else []
+
+
+class FlatRMSprop(FlatOptimizer):
+    def __init__(self, params, lr: float = 1e-3, rho: float = 0.9, eps: float = 1e-7):
+        super().__init__(params, lr)
+        self.rho, self.eps = rho, eps
+        self.ms = torch.zeros_like(self.flat_p)
+
+    def step(self, grad_scale: float = 1.0):
+        self.step_t.add_(1.0)
+        self.iterations += 1
+        with torch.no_grad():
+            g = self.flat_g * grad_scale
+            self.ms.mul_(self.rho).add_(g * g * (1 - self.rho))
+            self.flat_p.sub_(self.lr_t * g / (torch.sqrt(self.ms) + self.eps))
+
+    def slots(self):
+        return [self.ms]
+
+
+def make_optimizer(name: str, params, lr: float):
+    name = (name or "adam").lower()
+    if name == "adam":
+        return FlatAdam(params, lr)
+    if name == "sgd":
+        return FlatSGD(params, lr)
+    if name == "rmsprop":
+        return FlatRMSprop(params, lr)
+    raise ValueError(f"unknown optimizer {name}")
+
+
+__all__ = ["flatten_parameters", "FlatAdam", "FlatSGD", "FlatRMSprop", "make_optimizer"]

@@ -1,0 +1,206 @@
+"""Training / evaluation engine: device-resident, HIP-graph captured steps.
+
+One training step = gather batch from HBM by window id -> forward -> weighted BCE
+-> backward into the flat gradient buffer -> (DP) one RCCL all-reduce -> one Adam
+kernel. On GPU the gather+forward+backward(+optimizer when world == 1) is
+captured once into a HIP graph (``torch.cuda.CUDAGraph``) and replayed with new
+window ids, so a step costs a handful of host calls regardless of the ~100 kernels
+inside. Metric accumulators (loss sums, confusion counts, score histograms) live
+on the device and are only read at epoch end - no host sync per step.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..eval import metrics as M
+from ..ops.metrics import score_histogram
+from ..parallel import dist as D
+from .loss import weighted_bce_with_logits
+
+HIST_BINS = 1001
+
+
+class MetricAccumulator:
+    """Device-side running sums for the Keras compile metrics of ``libs/fit_model.py:79-86``."""
+
+    def __init__(self, device):
+        self.device = device
+        self.sums = torch.zeros(6, device=device, dtype=torch.float64)   # loss*n, n, tp, tn, fp, fn
+        self.hist = torch.zeros(2, HIST_BINS, device=device, dtype=torch.float32)
+
+    def reset(self):
+        self.sums.zero_()
+        self.hist.zero_()
+
+    @torch.no_grad()
+    def update(self, loss, logits, y, mask):
+        p = torch.sigmoid(logits.float())
+        m = mask.float()
+        n = m.sum()
+        pred = (p > 0.5).float()
+        yy = (y > 0.5).float()
+        vals = torch.stack([loss.detach().double() * n.double(), n.double(), (pred * yy * m).sum().double(),
+                            ((1 - pred) * (1 - yy) * m).sum().double(), (pred * (1 - yy) * m).sum().double(),
+                            ((1 - pred) * yy * m).sum().double()])
+        self.sums.add_(vals)
+        self.hist.add_(score_histogram(p, yy, m, HIST_BINS))
+
+    def result(self, prefix: str = "") -> Dict[str, float]:
+        sums = self.sums.clone()
+        hist = self.hist.clone()
+        D.all_reduce_(sums)
+        D.all_reduce_(hist)
+        s = sums.cpu().numpy()
+        out = {"loss": float(s[0] / max(s[1], 1.0))}
+        out.update(M.keras_metrics_from_counts(s[2], s[3], s[4], s[5]))
+        out["auc"] = M.auc_from_hist(hist.cpu().numpy())
+        return {prefix + k: v for k, v in out.items()}
+
+
+class Trainer:
+    def __init__(self, model, store, optimizer, class_weights: Optional[Dict[int, float]], baseline: bool = False,
+                 use_graph: bool = True, batch_size: int = 128):
+        self.model = model
+        self.store = store
+        self.opt = optimizer
+        self.ds_type = store.ds_type
+        self.baseline = baseline
+        cw = class_weights or {0: 1.0, 1: 1.0}
+        self.w0, self.w1 = float(cw[0]), float(cw[1])
+        self.device = store.device
+        self.world = D.world_size()
+        self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        self.batch_size = int(batch_size)
+        self.train_metrics = MetricAccumulator(self.device)
+        self.graph = None
+        self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
+        self.last_loss = torch.zeros((), device=self.device)
+
+    # ---------------------------------------------------------------- body
+    def _loss(self, wids):
+        b = self.store.gather(wids)
+        z = self.model.logits(b.model_inputs(self.ds_type, self.baseline))
+        loss = weighted_bce_with_logits(z, b.y, b.y_mask, self.w0, self.w1)
+        reg = self.model.regularization_loss() if hasattr(self.model, "regularization_loss") else None
+        total = loss + reg if reg is not None else loss
+        return total, loss, z, b
+
+    def _body(self, wids, with_opt: bool):
+        self.opt.zero_grad()
+        total, loss, z, b = self._loss(wids)
+        total.backward()
+        self.train_metrics.update(loss, z, b.y, b.y_mask)
+        self.last_loss.copy_(loss.detach())
+        if with_opt:
+            self.opt.step(grad_scale=1.0)
+
+    def _capture(self):
+        # warm up on a side stream (allocator + lazy init), then capture
+        snap = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+        with_opt = self.world == 1
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._body(self.static_wids, with_opt=False)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._body(self.static_wids, with_opt=with_opt)
+        # undo warm-up side effects (BN running stats, metric sums)
+        with torch.no_grad():
+            for k, v in self.model.state_dict().items():
+                v.copy_(snap[k])
+        self.train_metrics.reset()
+        self.opt.zero_grad()
+
+    def train_step(self, wids: torch.Tensor):
+        self.model.train()
+        if self.use_graph:
+            if self.graph is None:
+                self._capture()
+            self.static_wids.copy_(wids, non_blocking=True)
+            self.graph.replay()
+            if self.world == 1:
+                self.opt.iterations += 1
+                return self.last_loss
+        else:
+            self._body(wids.to(self.device), with_opt=self.world == 1)
+            if self.world == 1:
+                return self.last_loss
+        # data parallel: one all-reduce of the flat gradient buffer, then Adam
+        D.all_reduce_(self.opt.flat_g)
+        self.opt.step(grad_scale=1.0 / self.world)
+        return self.last_loss
+
+    # ---------------------------------------------------------------- epoch helpers
+    def train_epoch(self, loader, epoch: int) -> Dict[str, float]:
+        loader.set_epoch(epoch)
+        self.train_metrics.reset()
+        for row in loader.batch_ids():
+            self.train_step(row)
+        return self.train_metrics.result()
+
+    @torch.no_grad()
+    def evaluate(self, loader, prefix: str = "val_") -> Dict[str, float]:
+        acc = MetricAccumulator(self.device)
+        self.model.eval()
+        for row in loader.batch_ids():
+            b = self.store.gather(row)
+            z = self.model.logits(b.model_inputs(self.ds_type, self.baseline))
+            loss = weighted_bce_with_logits(z, b.y, b.y_mask, self.w0, self.w1)
+            acc.update(loss, z, b.y, b.y_mask)
+        self.model.train()
+        return acc.result(prefix)
+
+
+@torch.no_grad()
+def predict(model, store, loader, baseline: bool = False, gather_all: bool = True):
+    """Probabilities, labels and label mask for every window in ``loader`` (host numpy).
+
+    CML: one value per window; SoilNet: one per (window, node) with mask.
+    Returns dict with ``p``, ``y``, ``mask``, ``wid`` (window id per row) and, for
+    SoilNet, ``node`` (node position).
+    """
+    was_training = model.training
+    model.eval()
+    ps, ys, ms, ws = [], [], [], []
+    for row in loader.batch_ids():
+        b = store.gather(row)
+        p = model(b.model_inputs(store.ds_type, baseline))
+        ps.append(p.float())
+        ys.append(b.y.float())
+        ms.append(b.y_mask.float())
+        ws.append(b.wid)
+    if was_training:
+        model.train()
+    p = torch.cat(ps)
+    y = torch.cat(ys)
+    m = torch.cat(ms)
+    w = torch.cat(ws)
+    if gather_all:
+        p, y, m, w = (D.all_gather_var(t) for t in (p, y, m, w))
+    out = {"p": p.cpu().numpy(), "y": y.cpu().numpy(), "mask": m.cpu().numpy(), "wid": w.cpu().numpy()}
+    if store.ds_type == "soilnet":
+        N = out["p"].shape[1]
+        out["node"] = np.broadcast_to(np.arange(N), out["p"].shape).copy()
+    return out
+
+
+def flatten_predictions(pred: dict):
+    """Drop padding / unlabelled rows -> (p, y, wid[, node]) 1-D arrays."""
+    keep = pred["mask"].reshape(-1) > 0
+    res = {"p": pred["p"].reshape(-1)[keep], "y": pred["y"].reshape(-1)[keep]}
+    wid = pred["wid"]
+    if pred["p"].ndim == 2:
+        wid = np.repeat(wid, pred["p"].shape[1])
+        res["node"] = pred["node"].reshape(-1)[keep]
+    res["wid"] = wid.reshape(-1)[keep]
+    return res
+
+
+__all__ = ["Trainer", "MetricAccumulator", "predict", "flatten_predictions"]

@@ -1,0 +1,164 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (run on the MI355X box)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lstm_params(Din, H, gen, dev):
+    W = (torch.randn(Din, 4 * H, generator=gen) * 0.3).to(dev)
+    U = (torch.randn(H, 4 * H, generator=gen) * 0.3).to(dev)
+    b = (torch.randn(4 * H, generator=gen) * 0.1).to(dev)
+    return W, U, b
+
+
+@pytest.mark.parametrize("H", [16, 32, 64, 128])
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("ret_seq", [True, False])
+def test_lstm_fwd_bwd_matches_eager(cuda_device, H, bf16, ret_seq):
+    from gnnqc.ops.lstm import _HipLSTM, lstm_eager
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(H + 7 * bf16)
+    M, T, Din = 40, 13, 18
+    x = torch.randn(M, T, Din, generator=gen).to(dev)
+    W, U, b = _lstm_params(Din, H, gen, dev)
+    params = [t.clone().requires_grad_(True) for t in (x, W, U, b)]
+    ref_params = [t.clone().double().requires_grad_(True) for t in (x, W, U, b)]
+    out = _HipLSTM.apply(*params, bf16, ret_seq)
+    ref = lstm_eager(*ref_params, return_sequences=ret_seq)
+    tol = 3e-2 if bf16 else 2e-5
+    assert torch.allclose(out.double(), ref, atol=tol, rtol=tol), (out.double() - ref).abs().max()
+    g = torch.randn(out.shape, generator=gen).to(dev)
+    out.backward(g)
+    ref.backward(g.double())
+    for p, r, name in zip(params, ref_params, "xWUb"):
+        err = (p.grad.double() - r.grad).abs().max().item()
+        scale = r.grad.abs().max().item() + 1e-6
+        assert err / scale < (5e-2 if bf16 else 1e-4), f"grad {name}: rel err {err / scale}"
+
+
+def test_lstm_long_sequence_fp32_exact(cuda_device):
+    from gnnqc.ops.lstm import _HipLSTM, lstm_eager
+    gen = torch.Generator().manual_seed(3)
+    dev = cuda_device
+    x = torch.randn(128, 181, 18, generator=gen).to(dev)
+    W, U, b = _lstm_params(18, 16, gen, dev)
+    out = _HipLSTM.apply(x, W, U, b, False, True)
+    ref = lstm_eager(x.double(), W.double(), U.double(), b.double())
+    assert (out.double() - ref).abs().max().item() < 1e-4
+
+
+def _gcn_inputs(gen, dev, B=6, T=9, N=7, Cin=2, F=16):
+    x = torch.randn(B, T, N, Cin, generator=gen)
+    mask = (torch.rand(B, N, generator=gen) > 0.25).float()
+    mask[:, 0] = 1
+    adj = (torch.rand(B, N, N, generator=gen) > 0.5).float()
+    adj = ((adj + adj.transpose(1, 2)) > 0).float()
+    adj = adj + torch.eye(N)
+    adj = (adj > 0).float() * mask[:, :, None] * mask[:, None, :]
+    x = x * mask[:, None, :, None]
+    anom = torch.randn(B, T, Cin, generator=gen)
+    anom_pos = torch.zeros(B, dtype=torch.long)
+    W = torch.randn(Cin, F, generator=gen) * 0.5
+    bb = torch.randn(F, generator=gen) * 0.1
+    gamma = 1 + 0.1 * torch.randn(F, generator=gen)
+    beta = 0.1 * torch.randn(F, generator=gen)
+    alpha = 0.2 * torch.rand(F, generator=gen)
+    return [t.to(dev) for t in (x, adj, mask, anom, anom_pos, W, bb, gamma, beta, alpha)]
+
+
+@pytest.mark.parametrize("training", [True, False])
+@pytest.mark.parametrize("pooling", ["mean", "sum", "selection"])
+def test_gcn_pool_matches_eager(cuda_device, training, pooling):
+    from gnnqc.ops import gcn as G
+    gen = torch.Generator().manual_seed(5)
+    x, adj, mask, anom, ap, W, bb, gamma, beta, alpha = _gcn_inputs(gen, cuda_device)
+    F = W.shape[1]
+    rm_h, rv_h = torch.zeros(F, device=x.device), torch.ones(F, device=x.device)
+    rm_e, rv_e = rm_h.clone(), rv_h.clone()
+    if not training:
+        rm_h.normal_(0, 0.1); rv_h.uniform_(0.5, 2.0)
+        rm_e.copy_(rm_h); rv_e.copy_(rv_h)
+    hp = [t.clone().requires_grad_(True) for t in (x, anom, W, bb, gamma, beta, alpha)]
+    ep = [t.clone().double().requires_grad_(True) for t in (x, anom, W, bb, gamma, beta, alpha)]
+    w = G.node_pool_weights(adj, mask, ap, "mean", pooling)
+    out = G._HipGCNPool.apply(hp[0], w, mask, hp[1], hp[2], hp[3], hp[4], hp[5], hp[6], rm_h, rv_h, training,
+                              0.99, 1e-3)
+    h = G.general_conv_eager(ep[0], adj.double(), mask.double(), ep[2], ep[3], ep[4], ep[5], rm_e.double(),
+                             rv_e.double(), ep[6], training, "mean")
+    ref = torch.cat([ep[1], G.pool_nodes(h, mask.double(), ap, pooling)], -1)
+    assert torch.allclose(out.double(), ref, atol=1e-4, rtol=1e-4), (out.double() - ref).abs().max()
+    g = torch.randn(out.shape, generator=gen).to(x.device)
+    out.backward(g)
+    ref.backward(g.double())
+    for p, r, name in zip(hp, ep, ["x", "anom", "W", "b", "gamma", "beta", "alpha"]):
+        err = (p.grad.double() - r.grad).abs().max().item()
+        assert err < 2e-3 * (1 + r.grad.abs().max().item()), f"{name}: {err}"
+
+
+def test_adam_kernel_matches_eager(cuda_device):
+    from gnnqc.ops.optim import FlatAdam
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(37, 5)), torch.nn.Parameter(torch.randn(11))]
+    ps_gpu = [torch.nn.Parameter(p.detach().clone().to(cuda_device)) for p in ps]
+    a_cpu, a_gpu = FlatAdam(ps, 1e-2), FlatAdam(ps_gpu, 1e-2)
+    for _ in range(5):
+        g = torch.randn_like(a_cpu.flat_g)
+        a_cpu.flat_g.copy_(g)
+        a_gpu.flat_g.copy_(g.to(cuda_device))
+        a_cpu.step(0.5)
+        a_gpu.step(0.5)
+    assert torch.allclose(a_cpu.flat_p, a_gpu.flat_p.cpu(), atol=1e-6)
+
+
+def test_score_histogram_matches_eager(cuda_device):
+    import gnnqc.ops.metrics as Mx
+    torch.manual_seed(1)
+    s = torch.rand(10000)
+    y = (torch.rand(10000) > 0.8).float()
+    m = (torch.rand(10000) > 0.1).float()
+    ref = Mx.score_histogram(s, y, m, 1001)
+    out = Mx.score_histogram(s.to(cuda_device), y.to(cuda_device), m.to(cuda_device), 1001)
+    assert torch.equal(ref, out.cpu())
+
+
+def test_window_gather_matches_torch(cuda_device, cml_windows):
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.utils.native import hip_ops
+    pc, ws = cml_windows
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    st_cpu = DeviceStore(ws, "rolling_median", pc.graph, device="cpu")
+    wids = torch.tensor([0, 5, -1, 17, st.n_windows - 1])
+    ref = st_cpu.gather(wids)
+    out = hip_ops().window_gather(st.series, st.shift, st.scale, st.win_group, st.win_center,
+                                  st.win_valid_u8, wids.to(cuda_device), st.tb, st.seq_len, True)
+    assert torch.allclose(out.cpu(), ref.x, atol=1e-5)
+    b = st.gather(wids.to(cuda_device))
+    assert torch.allclose(b.anom.cpu(), ref.anom, atol=1e-5)
+    assert torch.equal(b.adj.cpu(), ref.adj)
+
+
+def test_graph_captured_train_step_learns(cuda_device, cml_windows):
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceLoader, DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    pc, ws = cml_windows
+    mc = C.default("model_cml")
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    torch.manual_seed(0)
+    model = GCNClassifier(mc, pc).to(cuda_device)
+    opt = make_optimizer("adam", model.parameters(), 1e-3)
+    tr = Trainer(model, st, opt, {0: 1.0, 1: 5.0}, use_graph=True, batch_size=64)
+    loader = DeviceLoader(st, list(range(st.n_windows)), 64, shuffle=True)
+    losses = []
+    for epoch in range(3):
+        loader.set_epoch(epoch)
+        for row in loader.batch_ids():
+            losses.append(float(tr.train_step(row).item()))
+    assert tr.graph is not None
+    assert all(map(lambda v: v == v, losses))
+    first = sum(losses[:5]) / 5
+    last = sum(losses[-5:]) / 5
+    assert last < first, (first, last)
