@@ -20,6 +20,16 @@ __device__ __forceinline__ float tanhf_fast(float x) {
   return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
 }
 
+// Workgroup barrier that orders LDS traffic only. __syncthreads() also drains
+// vmcnt (outstanding global loads AND stores on CDNA4), which in a persistent
+// recurrence turns every step into a full HBM round trip; prefetched loads and
+// fire-and-forget stores must be allowed to stay in flight across the step.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -47,17 +47,19 @@ __global__ void gcn_stats_kernel(const float* __restrict__ x, const float* __res
     }
     acc[nstat - 1] += m;
   }
-  // block reduction through LDS (fp64)
-  __shared__ double red[256];
+  // wave reduction by shuffles, then one LDS slot per wave, one atomic per block
+  __shared__ double red[4][nstat];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   _Pragma("unroll") for (int i = 0; i < nstat; ++i) {
-    red[threadIdx.x] = acc[i];
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) atomicAdd(&out[i], red[0]);
-    __syncthreads();
+    double v = acc[i];
+    _Pragma("unroll") for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wv][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < nstat) {
+    double v = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[k][threadIdx.x];
+    atomicAdd(&out[threadIdx.x], v);
   }
 }
 
@@ -137,17 +139,21 @@ __global__ void gcn_pool_bwd_kernel(const float* __restrict__ x, const float* __
       _Pragma("unroll") for (int k = 0; k < Cin; ++k) acc[3 + k] += xr[n * Cin + k] * dy;
     }
   }
-  // reduce over the rows of the block (threads with equal f)
-  __shared__ float red[256];
+  // reduce over the rows of the block (threads with equal f): shuffles inside the
+  // wave (lanes f, f+F, ...), then the 4 wave partials through LDS
+  __shared__ float red[4][nacc][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   _Pragma("unroll") for (int j = 0; j < nacc; ++j) {
-    red[threadIdx.x] = acc[j];
-    __syncthreads();
-    for (int s = rows_per_blk / 2; s > 0; s >>= 1) {
-      if (rsub < s) red[threadIdx.x] += red[threadIdx.x + s * F];
-      __syncthreads();
-    }
-    if (rsub == 0) partial[(long)blockIdx.x * nacc * F + j * F + f] = red[threadIdx.x];
-    __syncthreads();
+    float v = acc[j];
+    for (int o = 32; o >= F; o >>= 1) v += __shfl_xor(v, o, 64);
+    red[wv][j][lane] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nacc * F; e += blockDim.x) {
+    const int j = e / F, ff = e % F;
+    float v = 0.f;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[k][j][ff];
+    partial[(long)blockIdx.x * nacc * F + j * F + ff] = v;
   }
 }
 

@@ -221,7 +221,7 @@ def make_soilnet_raw(n_boxes: int = 40, n_time: int = 8545, start: str = "2014-0
     rain = np.zeros(T)
     n_ev = int(T * step_h / 24 * 0.35)
     for _ in range(n_ev):
-        t0 = int(rng.integers(0, T - 40))
+        t0 = int(rng.integers(0, max(1, T - 40)))
         d = int(rng.integers(2, 24))
         rain[t0:t0 + d] += rng.gamma(1.5, 1.2)
     box_gain = rng.uniform(0.7, 1.3, n_boxes)[box_id]
@@ -263,7 +263,7 @@ def make_soilnet_raw(n_boxes: int = 40, n_time: int = 8545, start: str = "2014-0
         n_f = rng.poisson(fault_rate * n_days / 12)
         for _ in range(n_f):
             kind = rng.integers(0, 4)
-            d = int(rng.integers(8, 300))
+            d = int(rng.integers(8, max(9, min(300, T // 2))))
             t0 = int(rng.integers(0, T - d))
             if kind == 0:    # drop to implausibly low value
                 moist[i, t0:t0 + d] = moist[i, t0:t0 + d] * rng.uniform(0.2, 0.6)
@@ -280,7 +280,7 @@ def make_soilnet_raw(n_boxes: int = 40, n_time: int = 8545, start: str = "2014-0
     no_label = np.zeros((S, T), bool)
     for i in range(S):
         if rng.random() < 0.2:
-            d = int(rng.integers(50, 800))
+            d = int(rng.integers(min(50, T // 4), max(min(50, T // 4) + 1, min(800, T // 2))))
             t0 = int(rng.integers(0, T - d))
             no_label[i, t0:t0 + d] = True
     no_label &= ~manual

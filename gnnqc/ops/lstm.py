@@ -11,6 +11,8 @@ plain GEMMs over all (sequence, step) rows.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 _ACT = {
@@ -43,19 +45,46 @@ def lstm_eager(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     return torch.stack(outs, 1) if return_sequences else h
 
 
+class _DirectGrad:
+    """When enabled (by the training engine), LSTM weight gradients are atomically
+    accumulated by the ``lstm_grads`` kernel straight into ``param.grad`` (the
+    optimiser's flat gradient buffer views) instead of being returned to autograd
+    - no separate AccumulateGrad add per parameter. Off by default so that
+    ``torch.autograd.grad`` (e.g. integrated gradients) never touches ``.grad``."""
+
+    enabled = False
+
+
+@contextlib.contextmanager
+def direct_grad_accumulation(flag: bool = True):
+    prev = _DirectGrad.enabled
+    _DirectGrad.enabled = flag
+    try:
+        yield
+    finally:
+        _DirectGrad.enabled = prev
+
+
+def _grad_sink(p: torch.Tensor):
+    g = p.grad if _DirectGrad.enabled and isinstance(p, torch.nn.Parameter) else None
+    if g is not None and g.is_contiguous() and g.dtype == torch.float32 and g.device == p.device:
+        return g, True
+    return torch.zeros_like(p), False
+
+
 class _HipLSTM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, U, b, bf16: bool, return_sequences: bool):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        M, T, Din = x.shape
-        H = U.shape[0]
-        x = x.contiguous()
-        xp = torch.addmm(b, x.reshape(M * T, Din), W).view(M, T, 4 * H)
+        # rows may be padded (e.g. a channel-padded producer): only unit inner stride needed
+        if not (x.stride(2) == 1 and x.stride(0) == x.shape[1] * x.stride(1)):
+            x = x.contiguous()
         need = any(ctx.needs_input_grad[:4])
-        h, c, g = ops.lstm_fwd(xp, U.contiguous(), need, bf16)
+        h, c, g = ops.lstm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need, bf16)
         ctx.bf16 = bf16
         ctx.return_sequences = return_sequences
+        ctx.params = (W, U, b)       # leaf Parameters (for direct gradient accumulation)
         if need:
             ctx.save_for_backward(x, W, U, h, c, g)
         return h if return_sequences else h[:, -1]
@@ -73,21 +102,17 @@ class _HipLSTM(torch.autograd.Function):
             dh = dout.new_zeros(M, T, H)
             dh[:, -1] = dout
         dz = ops.lstm_bwd(dh, g, c, U.contiguous(), ctx.bf16)
-        dz2 = dz.view(M * T, 4 * H)
-        dx = dW = dU = db = None
-        if ctx.needs_input_grad[0]:
-            dx = (dz2 @ W.t()).view(M, T, Din)
-        if ctx.needs_input_grad[1]:
-            dW = x.reshape(M * T, Din).t() @ dz2
-        if ctx.needs_input_grad[2]:
-            # dU = sum_t h_{t-1}^T dz_t  (h_{-1} = 0)
-            if T > 1:
-                dU = torch.einsum("mth,mtg->hg", h[:, :-1], dz[:, 1:])
-            else:
-                dU = U.new_zeros(U.shape)
-        if ctx.needs_input_grad[3]:
-            db = dz2.sum(0)
-        return dx, dW, dU, db, None, None
+        Wp, Up, bp = ctx.params
+        gW, dW_in = _grad_sink(Wp)
+        gU, dU_in = _grad_sink(Up)
+        gb, db_in = _grad_sink(bp)
+        need_dx = bool(ctx.needs_input_grad[0])
+        dx = ops.lstm_grads(dz, x, h, W.contiguous(), gW, gU, gb, need_dx)
+        return (dx if need_dx else None,
+                None if dW_in or not ctx.needs_input_grad[1] else gW,
+                None if dU_in or not ctx.needs_input_grad[2] else gU,
+                None if db_in or not ctx.needs_input_grad[3] else gb,
+                None, None)
 
 
 def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
@@ -95,7 +120,7 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     """Dispatch: HIP persistent kernel on GPU (tanh, H multiple of 16), eager otherwise."""
     from . import use_hip
     H = U.shape[0]
-    if use_hip(x) and activation == "tanh" and H % 16 == 0 and 16 <= H <= (256 if bf16 else 128):
+    if use_hip(x) and activation == "tanh" and H % 16 == 0 and H in (16, 32, 64, 128) and x.shape[-1] <= 128:
         return _HipLSTM.apply(x, W, U, b, bool(bf16), bool(return_sequences))
     return lstm_eager(x, W, U, b, return_sequences, activation)
 

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from ..eval import metrics as M
+from ..ops.lstm import direct_grad_accumulation
 from ..ops.metrics import score_histogram
 from ..parallel import dist as D
 from .loss import weighted_bce_with_logits
@@ -92,7 +93,8 @@ class Trainer:
     def _body(self, wids, with_opt: bool):
         self.opt.zero_grad()
         total, loss, z, b = self._loss(wids)
-        total.backward()
+        with direct_grad_accumulation(True):
+            total.backward()
         self.train_metrics.update(loss, z, b.y, b.y_mask)
         self.last_loss.copy_(loss.detach())
         if with_opt:

@@ -37,6 +37,34 @@ def test_lstm_fwd_bwd_matches_eager(cuda_device, H, bf16, ret_seq):
         assert err / scale < (5e-2 if bf16 else 1e-4), f"grad {name}: rel err {err / scale}"
 
 
+@pytest.mark.parametrize("Din,H", [(18, 16), (16, 16), (32, 64), (64, 128), (19, 16)])
+def test_lstm_direct_grad_accumulation_and_padded_rows(cuda_device, Din, H):
+    """Strided (row-padded) input + gradients accumulated straight into .grad views."""
+    from gnnqc.ops.lstm import _HipLSTM, direct_grad_accumulation, lstm_eager
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(Din * H)
+    M, T = 37, 11
+    buf = torch.randn(M, T, Din + 6, generator=gen).to(dev)
+    x = buf[..., :Din]                                   # row stride Din + 6
+    W, U, b = _lstm_params(Din, H, gen, dev)
+    pW, pU, pb = (torch.nn.Parameter(t.clone()) for t in (W, U, b))
+    for p in (pW, pU, pb):
+        p.grad = torch.full_like(p, 0.5)                 # pre-existing buffer: must accumulate
+    xg = x.clone().requires_grad_(True)
+    with direct_grad_accumulation(True):
+        out = _HipLSTM.apply(xg, pW, pU, pb, True, True)
+        g = torch.randn(out.shape, generator=gen).to(dev)
+        out.backward(g)
+    ref_p = [t.clone().double().requires_grad_(True) for t in (x, W, U, b)]
+    ref = lstm_eager(*ref_p)
+    ref.backward(g.double())
+    assert (out.double() - ref).abs().max().item() < 3e-2
+    for p, r, name in zip((xg, pW, pU, pb), ref_p, "xWUb"):
+        got = p.grad.double() - (0.0 if name == "x" else 0.5)
+        err = (got - r.grad).abs().max().item() / (r.grad.abs().max().item() + 1e-6)
+        assert err < 5e-2, f"{name}: {err}"
+
+
 def test_lstm_long_sequence_fp32_exact(cuda_device):
     from gnnqc.ops.lstm import _HipLSTM, lstm_eager
     gen = torch.Generator().manual_seed(3)
