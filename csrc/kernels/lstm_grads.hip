@@ -26,7 +26,7 @@ template <int H, int DT>            // DT = ceil((Din + 1) / 16) din tiles (incl
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ dU,
-    float* __restrict__ db, int M, int T, int Din, int ldx, int dx_atomic) {
+    float* __restrict__ db, int M, int T, int Din, int ldx, long dx_cb_stride) {
   constexpr int G4 = 4 * H;
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
@@ -138,13 +138,12 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
           const long r = r0 + 16 * rt + col;
           if (r < rows) {
             const long sq = r / T, t = r % T;
-            float* o = dx + ((size_t)sq * T + t) * Din;
+            float* o = dx + cb * dx_cb_stride + ((size_t)sq * T + t) * Din;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int din = dtile * 16 + 4 * quad + q;
               if (din < Din) {
-                if (dx_atomic) atomicAdd(o + din, acc[q]);
-                else o[din] = acc[q];
+                o[din] = acc[q];
               }
             }
           }
@@ -153,30 +152,38 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
     }
     __syncthreads();
   }
-  // ---- flush partial weight gradients (C layout: row = gate-unit 4quad+q, col = din / k)
+  // ---- flush partial weight gradients. The C tiles hold [gate-unit][din|k] with
+  // the gate-unit on 4 rows per lane; transpose them through LDS so that every
+  // atomic wave-instruction adds 64 consecutive gate-units (256 contiguous bytes:
+  // the full-rate shape; one lane per row would run ~17x slower).
+  __shared__ float fl[DP + H][GR_CB + 1];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int gu = gu0 + 16 * w + 4 * quad + q;
+    const int c = 16 * w + 4 * quad + q;
 #pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      const int din = 16 * d + col;
-      if (din < Din) atomicAdd(dW + (size_t)din * G4 + gu, accW[d][q]);
-      else if (din == Din && db != nullptr) atomicAdd(db + gu, accW[d][q]);
-    }
+    for (int d = 0; d < DT; ++d) fl[16 * d + col][c] = accW[d][q];
 #pragma unroll
-    for (int k = 0; k < HT; ++k) atomicAdd(dU + (size_t)(16 * k + col) * G4 + gu, accU[k][q]);
+    for (int k = 0; k < HT; ++k) fl[DP + 16 * k + col][c] = accU[k][q];
+  }
+  __syncthreads();
+  for (int e = tid; e < (DP + H) * GR_CB; e += 256) {
+    const int row = e / GR_CB, c = e % GR_CB;
+    const float v = fl[row][c];
+    if (row < Din) atomicAdd(dW + (size_t)row * G4 + gu0 + c, v);
+    else if (row == Din) atomicAdd(db + gu0 + c, v);
+    else if (row >= DP) atomicAdd(dU + (size_t)(row - DP) * G4 + gu0 + c, v);
   }
 }
 
 template <int H>
 void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const float* x, const float* h,
                     const float* W, float* dx, float* dW, float* dU, float* db, int M, int T, int Din, int ldx,
-                    int dx_atomic) {
+                    long dx_cb_stride) {
   switch (DT) {
 #define GQ_DT(D)                                                                                              \
   case D:                                                                                                     \
     hipLaunchKernelGGL((lstm_grads_kernel<H, D>), grid, dim3(256), 0, st, dz, x, h, W, dx, dW, dU, db, M, T, \
-                       Din, ldx, dx_atomic);                                                                  \
+                       Din, ldx, dx_cb_stride);                                                                  \
     break;
     GQ_DT(1) GQ_DT(2) GQ_DT(3) GQ_DT(4) GQ_DT(5) GQ_DT(6) GQ_DT(7) GQ_DT(8) GQ_DT(9)
 #undef GQ_DT
@@ -206,27 +213,29 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
                   dU.size(1) == 4 * H && db.numel() == 4 * H, "gradient buffer shapes");
   c10::DeviceGuard guard(x.device());
   const int ncb = (4 * H) / GR_CB;
-  const int dx_atomic = ncb > 1 ? 1 : 0;
-  at::Tensor dx = need_dx ? (dx_atomic ? at::zeros({M, T, Din}, x.options()) : at::empty({M, T, Din}, x.options()))
-                          : at::empty({0}, x.options());
+  // dx = dz W^T contracts over all 4H gate-units: with several column blocks each
+  // block writes its partial product to its own slab (plain stores), summed below
+  at::Tensor dx = need_dx ? at::empty({ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
+  const long dx_cb_stride = (long)M * T * Din;
   const long rows = (long)M * T;
-  if (rows == 0) return dx;
+  if (rows == 0) return need_dx ? dx.sum(0) : dx;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
   // enough workgroups to fill the chip, few enough that the final atomics stay cheap
-  const int splits = (int)std::max<long>(1, std::min<long>(ntiles, std::max(64, 384 / ncb)));
+  const int splits = (int)std::max<long>(1, std::min<long>(ntiles, std::max(32, 256 / ncb)));
   dim3 grid(ncb, splits);
   const int DT = (Din + 1 + 15) / 16;
   auto st = stream();
   float* dxp = need_dx ? dx.data_ptr<float>() : nullptr;
   switch (H) {
-    case 16: launch_grads_h<16>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_atomic); break;
-    case 32: launch_grads_h<32>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_atomic); break;
-    case 64: launch_grads_h<64>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_atomic); break;
-    case 128: launch_grads_h<128>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_atomic); break;
+    case 16: launch_grads_h<16>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
+    case 32: launch_grads_h<32>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
+    case 64: launch_grads_h<64>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
+    case 128: launch_grads_h<128>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
     default: TORCH_CHECK(false, "gnnqc lstm_grads: unsupported hidden size ", H);
   }
   GQ_LAUNCH_CHECK();
-  return dx;
+  if (!need_dx) return dx;
+  return ncb == 1 ? dx[0] : dx.sum(0);
 }
 
 }  // namespace gq

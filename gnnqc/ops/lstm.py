@@ -102,6 +102,16 @@ class _HipLSTM(torch.autograd.Function):
             dh = dout.new_zeros(M, T, H)
             dh[:, -1] = dout
         dz = ops.lstm_bwd(dh, g, c, U.contiguous(), ctx.bf16)
+        if not ctx.bf16:
+            # fp32 numerics-reference mode: exact fp32 GEMMs for the weight gradients
+            dz2 = dz.reshape(M * T, 4 * H)
+            dx = (dz2 @ W.t()).view(M, T, Din) if ctx.needs_input_grad[0] else None
+            dW = torch.einsum("mtd,mtg->dg", x, dz) if ctx.needs_input_grad[1] else None
+            dU = None
+            if ctx.needs_input_grad[2]:
+                dU = torch.einsum("mth,mtg->hg", h[:, :-1], dz[:, 1:]) if T > 1 else torch.zeros_like(U)
+            db = dz2.sum(0) if ctx.needs_input_grad[3] else None
+            return dx, dW, dU, db, None, None
         Wp, Up, bp = ctx.params
         gW, dW_in = _grad_sink(Wp)
         gU, dU_in = _grad_sink(Up)
