@@ -56,11 +56,8 @@ def save_model(model, path: str, optimizer=None, epoch: Optional[int] = None, pr
     with open(os.path.join(path, META_FILE), "w") as f:
         json.dump(meta, f, indent=1, default=str)
     if keras_layout:
-        try:
-            from .keras_layout import write_keras_variables
-            write_keras_variables(model, path, optimizer)
-        except ImportError:
-            pass
+        from .keras_layout import write_keras_variables
+        write_keras_variables(model, path, optimizer)
 
 
 def load_model(path: str, device="cpu", with_optimizer: bool = False):
@@ -86,4 +83,6 @@ def load_model(path: str, device="cpu", with_optimizer: bool = False):
     return model
 
 
-__all__ = ["save_model", "load_model"]
+from .keras_layout import build_from_keras, load_keras_optimizer, load_keras_weights  # noqa: E402
+
+__all__ = ["save_model", "load_model", "load_keras_weights", "load_keras_optimizer", "build_from_keras"]

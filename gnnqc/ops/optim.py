@@ -75,6 +75,15 @@ class FlatOptimizer:
                 p.grad = g
             off += (n + 3) // 4 * 4
 
+    def views(self, flat: torch.Tensor) -> List[torch.Tensor]:
+        """Per-parameter views of a flat buffer laid out like ``flat_p`` (slots, grads)."""
+        out, off = [], 0
+        for p in self.params:
+            n = p.numel()
+            out.append(flat[off:off + n].view_as(p.data))
+            off += (n + 3) // 4 * 4
+        return out
+
     def state_dict(self):
         return {"lr": self.lr, "iterations": self.iterations}
 
