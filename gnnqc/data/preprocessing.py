@@ -226,7 +226,8 @@ def create_tfrecords_dataset(preproc_config, windows: Optional[WindowSet] = None
     np.savez_compressed(os.path.join(out, "windows.npz"), **arrays)
     if write_records:
         from .tfrecord import write_window_records
-        write_window_records(windows, out, normalization=cfg.get("normalization"), max_records=max_records)
+        write_window_records(windows, out, normalization=cfg.get("normalization"), max_records=max_records,
+                             graph_cfg=cfg.graph)
     return out
 
 

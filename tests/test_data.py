@@ -8,6 +8,7 @@ from gnnqc import config as C
 from gnnqc.data import geo
 from gnnqc.data.interp import interpolate_gaps
 from gnnqc.data.raw_io import SensorData, read_netcdf, write_netcdf
+from gnnqc.data.preprocessing import create_windows_dataset
 from gnnqc.data.splits import chronological_split, kfold_split, monthly_random_split
 from gnnqc.data.stats import rolling_stats
 from gnnqc.data.synthetic import make_cml_raw, make_soilnet_raw
@@ -191,3 +192,48 @@ def test_soilnet_windows_and_store():
     tb = 300 // 15
     n0 = int(torch.nonzero(b.node_mask[0])[0])
     assert abs(float(b.x[0, tb, n0, 0]) - g.features[n0, 0, c] / 60.0) < 1e-5
+
+
+@pytest.mark.parametrize("ds", ["cml", "soilnet"])
+def test_tfrecord_roundtrip_matches_device_store(ds, tmp_path):
+    """Windows written as SequenceExample TFRecords (reference ``create_example`` layout)
+    and read back give the same normalised node tensors / adjacency / labels as the
+    device-resident gather path."""
+    import torch
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.data.synthetic import make_soilnet_raw
+    from gnnqc.data.tfrecord import TFRecordWindows, read_tfrecord, write_window_records
+    pc = C.normalize_preproc(C.default(f"preprocessing_{ds}"))
+    raw = (make_cml_raw(n_sensors=10, n_minutes=2 * 1440, seed=3) if ds == "cml"
+           else make_soilnet_raw(n_boxes=6, n_time=20 * 96, seed=3))
+    ws = create_windows_dataset(pc, raw=raw)
+    files = write_window_records(ws, str(tmp_path), max_records=64, graph_cfg=pc.graph)
+    assert sum(1 for f in files for _ in read_tfrecord(f)) == 64
+    tw = TFRecordWindows(str(tmp_path), ds)
+    order = np.argsort(ws.window_keys(), kind="stable")[:16]
+    b = DeviceStore(ws, tw.normalization, pc.graph).gather(torch.as_tensor(order))
+    rb = next(tw.batches(16))
+    for i in range(16):
+        v = b.node_mask[i] > 0
+        n = int(v.sum())
+        torch.testing.assert_close(b.x[i][:, v], rb.x[i][:, :n], atol=1e-4, rtol=1e-5)
+        assert torch.equal(b.adj[i][v][:, v], rb.adj[i][:n, :n])
+        if ds == "soilnet":
+            assert torch.equal(b.y[i][v], rb.y[i][:n])
+    if ds == "cml":
+        assert torch.equal(b.y, rb.y)
+        torch.testing.assert_close(b.anom, rb.anom, atol=1e-4, rtol=1e-5)
+
+
+def test_tfrecord_crc_detects_corruption(tmp_path):
+    from gnnqc.data.tfrecord import TFRecordWriter, read_tfrecord
+    p = str(tmp_path / "x.tfrec")
+    with TFRecordWriter(p) as w:
+        w.write(b"hello")
+        w.write(b"world" * 10)
+    assert list(read_tfrecord(p)) == [b"hello", b"world" * 10]
+    raw = bytearray(open(p, "rb").read())
+    raw[14] ^= 1
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(ValueError):
+        list(read_tfrecord(p))
