@@ -134,7 +134,7 @@ def cmd_cv(args):
     out = {}
     for baseline in kinds:
         s = run_cv(pc, mc, ws, folds=args.folds, baseline=baseline, store=store, seed=args.seed,
-                   gap_days=args.gap_days, log_path=args.log)
+                   gap_days=args.gap_days, log_path=args.log, max_folds=args.max_folds)
         out[s["model"]] = s
         if D.is_main():
             print(json.dumps({"model": s["model"], "mean_auc": round(s["mean_auc"], 4), "std_auc": round(s["std_auc"], 4),
@@ -179,6 +179,7 @@ def main(argv=None):
     p.add_argument("--baseline", action="store_true")
     p.add_argument("--both", action="store_true")
     p.add_argument("--gap-days", type=int, default=None)
+    p.add_argument("--max-folds", type=int, default=None, help="only run the first K folds")
     p.add_argument("--out", default=None)
     p.add_argument("--log", default=None)
     p.set_defaults(fn=cmd_cv)

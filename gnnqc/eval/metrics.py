@@ -79,7 +79,7 @@ def auc(x, y) -> float:
     y = np.asarray(y, dtype=np.float64)
     d = np.diff(x)
     direction = -1.0 if np.all(d <= 0) and np.any(d < 0) else 1.0
-    return float(direction * np.trapz(y, x))
+    return float(direction * np.trapezoid(y, x))
 
 
 def roc_auc_score(y_true, scores) -> float:

@@ -138,11 +138,15 @@ class _HipGCNPool(torch.autograd.Function):
         (x, w, mask, W, b, gamma, alpha, mu, invstd, scale, shift, S1, S2, cnt) = ctx.saved_tensors
         dout = dout.contiguous()
         Cin = x.shape[-1]
-        acc = ops.gcn_pool_bwd(x, w, dout, W.contiguous(), b.contiguous(), scale, shift, alpha.contiguous(), ctx.ca)
-        A, Z, P, Q = acc[0], acc[1], acc[2], acc[3:3 + Cin]
-        dbeta = A
-        dgamma = invstd * (Z - mu * A)
-        dalpha = P
+        need_w = any(ctx.needs_input_grad[4:9])
+        dW = db = dgamma = dbeta = dalpha = None
+        if ctx.training or need_w:
+            acc = ops.gcn_pool_bwd(x, w, dout, W.contiguous(), b.contiguous(), scale, shift, alpha.contiguous(),
+                                   ctx.ca)
+            A, Z, P, Q = acc[0], acc[1], acc[2], acc[3:3 + Cin]
+            dbeta = A
+            dgamma = invstd * (Z - mu * A)
+            dalpha = P
         if ctx.training:
             n = cnt[0]
             sxx = invstd * (S2 @ W + torch.outer(S1, b - mu))       # sum_rows x_k * xhat_f
@@ -151,8 +155,11 @@ class _HipGCNPool(torch.autograd.Function):
             c0 = scale * (-A / n + mu * invstd * dgamma / n)
             c2 = -scale * invstd * dgamma / n
         else:
-            dW = scale * Q
-            db = scale * A
+            # inference-mode BN is a fixed affine map (e.g. integrated gradients: frozen weights,
+            # input gradients only -> no weight-gradient reduction at all)
+            if need_w:
+                dW = scale * Q
+                db = scale * A
             c0 = torch.zeros_like(scale)
             c2 = torch.zeros_like(scale)
         dx = None

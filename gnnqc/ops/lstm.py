@@ -112,6 +112,10 @@ class _HipLSTM(torch.autograd.Function):
                 dU = torch.einsum("mth,mtg->hg", h[:, :-1], dz[:, 1:]) if T > 1 else torch.zeros_like(U)
             db = dz2.sum(0) if ctx.needs_input_grad[3] else None
             return dx, dW, dU, db, None, None
+        if not any(ctx.needs_input_grad[1:4]):
+            # frozen weights (integrated gradients): only dx = dz W^T, one library GEMM
+            dx = (dz.reshape(M * T, 4 * H) @ W.t()).view(M, T, Din) if ctx.needs_input_grad[0] else None
+            return dx, None, None, None, None, None
         Wp, Up, bp = ctx.params
         gW, dW_in = _grad_sink(Wp)
         gU, dU_in = _grad_sink(Up)

@@ -28,7 +28,7 @@ from .fit import train_model
 
 def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, baseline: bool = False,
            device="cpu", seed: int = 0, store: Optional[DeviceStore] = None, gap_days: Optional[int] = None,
-           verbose: int = 1, log_path: Optional[str] = None) -> Dict:
+           verbose: int = 1, log_path: Optional[str] = None, max_folds: Optional[int] = None) -> Dict:
     pc = preproc_config
     mc = model_config
     k = int(folds or pc.get("split_numb", 5))
@@ -38,7 +38,7 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
     store = store or DeviceStore(windows, norm, pc.graph, device=device)
     rank, world = D.rank(), D.world_size()
     results: List[Dict] = []
-    for fold in range(k):
+    for fold in range(min(k, int(max_folds)) if max_folds else k):
         t0 = time.time()
         tr, te, pcf = load_dataset_CV(pc, windows, fold, gap_days=gap_days)
         torch.manual_seed(seed + fold)
@@ -57,10 +57,12 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
         res = {"fold": fold, "auc": auc, "mcc": M.matthews_corrcoef(y, yp), "precision": M.precision_score(y, yp),
                "recall": M.recall_score(y, yp), "accuracy": M.accuracy_score(y, yp), "threshold": thr,
                "n_train": int(len(tr)), "n_test": int(len(te)), "test_pos_rate": float(y.mean()) if y.size else 0.0,
-               "final_train_loss": float(hist.history["loss"][-1]), "seconds": time.time() - t0}
+               "final_train_loss": float(hist.history["loss"][-1]), "seconds": time.time() - t0,
+               "loss_curve": [round(float(v), 5) for v in hist.history["loss"]]}
         results.append(res)
         if verbose and D.is_main():
-            print(json.dumps({k2: (round(v, 4) if isinstance(v, float) else v) for k2, v in res.items()}), flush=True)
+            print(json.dumps({k2: (round(v, 4) if isinstance(v, float) else v) for k2, v in res.items()
+                              if k2 != "loss_curve"}), flush=True)
         if log_path and D.is_main():
             with open(log_path, "a") as f:
                 f.write(json.dumps(res) + "\n")

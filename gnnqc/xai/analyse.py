@@ -1,0 +1,434 @@
+"""Analysis of saved integrated-gradients results (SURVEY L7;
+reference ``xai/libs/integrated_gradients_analyser.py``, class ``IntegrateGradientsAnalyser``).
+
+Works on the directory tree written by :class:`gnnqc.xai.ig.IntegratedGradientsExplainer`::
+
+    <output_dir>/integrated_gradients/<project>/<ds>/<dataset>/<sensor>/<sensor>_<YYYYmmdd_HHMMSS>_<t>_<p>/
+        gradients_features_unwrapped_<stem>.npy   [n_nodes, T, C]
+        gradients_anom_ts_unwrapped_<stem>.npy    [T, C]
+        features_unwrapped_<stem>.npy, anom_ts_unwrapped_<stem>.npy, predictions_unwrapped_<stem>.npy, ...
+
+Methods mirror the reference: :meth:`get_overview` (``:343-529``: sample table, time-range
+scatter and confusion bar plots, selection by confusion class with ``keep_surrounding``
+context samples), :meth:`spatial_aggregate_gradients` (``:531-695``),
+:meth:`plot_spatial_aggregated_gradients` (``:811-964``), :meth:`concatenate_images`
+(``:697-731``), :meth:`create_videos` (GIF via PIL; ``:185-308,733-809``),
+:meth:`plot_agg_samples_over_time` (``:1169-1710``), :meth:`scale_gradients_with_input`
+(``:992-1074``), :meth:`rename_based_on_threshold` (``:1076-1120``). Work is split by
+sensor over SLURM array tasks or ``torch.distributed`` ranks.
+
+Differences on purpose: sample directory names are parsed from the right
+(``rsplit``), so sensor ids need not have exactly four ``_``-separated parts
+(``get_sensor_id``/``get_datetime``, ``:310-327``); the ``dont_scale.txt`` exclusion
+list is optional.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import numpy as np
+import pandas as pd
+
+import matplotlib
+
+matplotlib.use("Agg")
+import matplotlib.colors as mcolors  # noqa: E402
+import matplotlib.pyplot as plt  # noqa: E402
+
+from .. import config as C  # noqa: E402
+from ..viz.ig import parse_sample_dir  # noqa: E402
+from .ig import CONFUSION  # noqa: E402
+
+COLOR_MAP = {(0, 0): "white", (0, 1): "orange", (1, 0): "red", (1, 1): "green"}
+COLOR_NAMES = {(0, 0): "True Negative", (0, 1): "False Positive", (1, 0): "False Negative", (1, 1): "True Positive"}
+STEM_GF, STEM_GA = "gradients_features_unwrapped", "gradients_anom_ts_unwrapped"
+STEM_F, STEM_A = "features_unwrapped", "anom_ts_unwrapped"
+STEM_P, STEM_Y = "predictions_unwrapped", "anomaly_flag_true_unwrapped"
+
+
+class IntegrateGradientsAnalyser:
+    def __init__(self, preproc_config, model_config=None, xai_config=None):
+        load = lambda c: C.load(c) if isinstance(c, str) else c  # noqa: E731
+        self.preproc_config = C.normalize_preproc(load(preproc_config))
+        self.model_config = load(model_config) if model_config is not None else None
+        self.xai_config = load(xai_config) if xai_config is not None else C.default("xai_ig")
+        ig = self.xai_config.integrated_gradients
+        self.ig = ig
+        self.an = ig.analyser
+        self.ds_type = self.preproc_config.ds_type
+        self.dp_results_parent = os.path.join(self.xai_config.output_dir, "integrated_gradients",
+                                              self.xai_config.project, self.ds_type, ig.dataset)
+        self.stem = f"{self.xai_config.project}_{self.ds_type}_{ig.dataset}"
+        self.conf_matrix_string = "_".join(sorted(str(x) for x in self.an.which_samples))
+        from ..parallel import dist as D
+        if "SLURM_ARRAY_TASK_ID" in os.environ:
+            self.workerid = int(os.environ["SLURM_ARRAY_TASK_ID"])
+            self.n_worker = int(os.environ["SLURM_ARRAY_TASK_COUNT"])
+        elif D.world_size() > 1:
+            self.workerid, self.n_worker = D.rank(), D.world_size()
+        else:
+            self.workerid = self.n_worker = None
+        self.output_dir_analysis = os.path.join(
+            os.path.dirname(self.dp_results_parent),
+            f"{ig.dataset}_analysis_{self.an.concat_images_scale}_{self.an.video.video_fps}")
+        self.df = self.df_unfiltered = None
+        self.selected_sensors: List[str] = []
+
+    # ----------------------------------------------------------------- helpers
+    def get_filename(self, stem: str, dn_sample: str) -> str:
+        return f"{stem}_{self.stem}_{dn_sample}"
+
+    def _load(self, row, stem: str) -> Optional[np.ndarray]:
+        p = os.path.join(row["path"], self.get_filename(stem, row["sample_name"]) + ".npy")
+        return np.load(p) if os.path.exists(p) else None
+
+    @staticmethod
+    def _split_work(items, workerid, n_worker):
+        return [it for i, it in enumerate(items) if i % n_worker == workerid]
+
+    # ----------------------------------------------------------------- overview
+    def get_overview(self, plots: bool = True) -> pd.DataFrame:
+        os.makedirs(self.output_dir_analysis, exist_ok=True)
+        rows = []
+        if os.path.isdir(self.dp_results_parent):
+            for sensor in sorted(os.listdir(self.dp_results_parent)):
+                dsens = os.path.join(self.dp_results_parent, sensor)
+                if sensor in ("log",) or sensor.startswith(".") or not os.path.isdir(dsens):
+                    continue
+                for dn in sorted(os.listdir(dsens)):
+                    if not os.path.isdir(os.path.join(dsens, dn)):
+                        continue
+                    try:
+                        info = parse_sample_dir(dn)
+                    except ValueError:
+                        continue
+                    rows.append({"sensor_id": sensor, "sample_name": dn,
+                                 "date_time": pd.to_datetime(info["date"], format="%Y%m%d_%H%M%S"),
+                                 "true": info["true"], "pred": info["pred"], "path": os.path.join(dsens, dn)})
+        df = pd.DataFrame(rows, columns=["sensor_id", "sample_name", "date_time", "true", "pred", "path"])
+        self.df_unfiltered = df.copy()
+        which_sensors = self.an.which_sensors
+        self.selected_sensors = list(df["sensor_id"].unique()) if which_sensors in ("all", None) else \
+            [str(s) for s in which_sensors]
+        df = df[df["sensor_id"].isin(self.selected_sensors)]
+        if self.workerid is not None:
+            self.selected_sensors = self._split_work(self.selected_sensors, self.workerid, self.n_worker)
+        df = df.sort_values("date_time").reset_index(drop=True)
+        if len(df):
+            df["color"] = [COLOR_MAP[(t, p)] for t, p in zip(df["true"], df["pred"])]
+            df["confusion_matrix"] = [COLOR_NAMES[(t, p)] for t, p in zip(df["true"], df["pred"])]
+            df["confusion_matrix_abbr"] = [CONFUSION[(t, p)] for t, p in zip(df["true"], df["pred"])]
+            if plots:
+                self._overview_plots(df)
+            # selection + surrounding context samples
+            sel = df["confusion_matrix_abbr"].isin(list(self.an.which_samples)).to_numpy()
+            surr = int(self.an.get("keep_surrounding", 0) or 0)
+            keep = sel.copy()
+            for i in np.nonzero(sel)[0]:
+                keep[max(0, i - surr): i + surr + 1] = True
+            df = df[keep].reset_index(drop=True)
+        else:
+            print("NoSamplesError: no IG sample directories found under", self.dp_results_parent)
+        self.df = df
+        return df
+
+    def _overview_plots(self, df):
+        fig, ax = plt.subplots(figsize=(12, 8))
+        for sid in df["sensor_id"].unique():
+            sub = df[df["sensor_id"] == sid]
+            ax.scatter(sub["date_time"], [sid] * len(sub), c=sub["color"], s=12, marker="|")
+        ax.set_xlabel("Date and Time")
+        ax.set_ylabel("sensor ID")
+        ax.set_title("Analysed Samples per sensor ID")
+        ax.legend(handles=[plt.Line2D([0], [0], color=COLOR_MAP[k], label=COLOR_NAMES[k]) for k in COLOR_MAP])
+        fig.savefig(os.path.join(self.output_dir_analysis, "sensor_samples_time_range.png"), bbox_inches="tight")
+        plt.close(fig)
+        counts = df.groupby("sensor_id")["confusion_matrix"].value_counts().unstack().fillna(0)
+        colors = [COLOR_MAP[k] for k in COLOR_MAP if COLOR_NAMES[k] in counts.columns]
+        counts = counts[[COLOR_NAMES[k] for k in COLOR_MAP if COLOR_NAMES[k] in counts.columns]]
+        ax = counts.plot(kind="barh", stacked=True, color=colors, alpha=0.6, edgecolor="k")
+        ax.get_legend().set_title(None)
+        ax.figure.savefig(os.path.join(self.output_dir_analysis, "sensor_samples_confusion_matrix.png"),
+                          bbox_inches="tight")
+        plt.close(ax.figure)
+
+    # ----------------------------------------------------------------- aggregation
+    def spatial_aggregate_gradients(self) -> dict:
+        """Per sensor: mean over selected samples of (node-mean feature gradients, anomalous-series
+        gradients), optionally normalised per sample by the max |gradient|."""
+        if self.df is None:
+            self.get_overview(plots=False)
+        which = list(self.an.spatial_aggregation.which_samples)
+        normalize = bool(self.an.spatial_aggregation.normalize)
+        out = {}
+        for sid in self.selected_sensors:
+            sub = self.df[(self.df["sensor_id"] == sid) & self.df["confusion_matrix_abbr"].isin(which)]
+            sf = sa = None
+            n = 0
+            for _, row in sub.iterrows():
+                gf, ga = self._load(row, STEM_GF), self._load(row, STEM_GA)
+                if gf is None and ga is None:
+                    continue
+                if normalize:
+                    parts = [np.abs(a).reshape(-1) for a in (gf, ga) if a is not None]
+                    m = float(np.max(np.concatenate(parts))) if parts else 0.0
+                    if m > 0:
+                        gf = gf / m if gf is not None else None
+                        ga = ga / m if ga is not None else None
+                f = gf.sum(0) / gf.shape[0] if gf is not None else None      # neighbour count varies: node mean
+                sf = f if sf is None else sf + f
+                sa = ga if sa is None else (sa + ga if ga is not None else sa)
+                n += 1
+            if n == 0:
+                print("No samples found for", sid)
+                continue
+            d = os.path.join(self.output_dir_analysis, str(sid))
+            os.makedirs(d, exist_ok=True)
+            res = {}
+            if sf is not None:
+                res["features"] = sf / n
+                np.save(os.path.join(d, f"spatial_aggregated_gradients_features_{self.conf_matrix_string}.npy"),
+                        res["features"])
+            if sa is not None:
+                res["anom_ts"] = sa / n
+                np.save(os.path.join(d, f"spatial_aggregated_gradients_anom_ts_{self.conf_matrix_string}.npy"),
+                        res["anom_ts"])
+            res["n_samples"] = n
+            out[sid] = res
+        self.spatial = out
+        return out
+
+    def plot_spatial_aggregated_gradients(self) -> List[str]:
+        if not hasattr(self, "spatial"):
+            self.spatial_aggregate_gradients()
+        scale = float(self.an.spatial_aggregation.scale_feature_gradients)
+        paths = []
+        for sid, res in self.spatial.items():
+            panels = [(k, v * (scale if k == "features" else 1.0)) for k, v in res.items() if k != "n_samples"]
+            fig, axes = plt.subplots(len(panels), 1, figsize=(12, 1.8 * len(panels)), squeeze=False, sharex=True)
+            vmax = max(float(np.abs(v).max()) for _, v in panels) or 1.0
+            norm = mcolors.Normalize(-vmax, vmax)
+            for ax, (k, v) in zip(axes[:, 0], panels):
+                m = ax.pcolormesh(v.T, cmap="RdBu_r", norm=norm)
+                ax.set_ylabel(k + (f" x{scale:g}" if k == "features" else ""))
+            fig.colorbar(m, ax=list(axes[:, 0]))
+            axes[0, 0].set_title(f"{sid}: mean attribution over {res['n_samples']} samples ({self.conf_matrix_string})")
+            p = os.path.join(self.output_dir_analysis, str(sid), f"spatial_aggregated_{self.conf_matrix_string}.png")
+            fig.savefig(p, bbox_inches="tight")
+            plt.close(fig)
+            paths.append(p)
+        return paths
+
+    def plot_agg_samples_over_time(self, sensor: str, time_from=None, time_to=None, agg_type: Optional[str] = None,
+                                   norm_by_prediction: Optional[bool] = None, cbar_limits=None) -> Optional[str]:
+        """Consecutive samples of one sensor: centre value of the flagged series, score,
+        outcome, and the per-sample aggregated attribution (over time) of every channel
+        and neighbour - a spatio-temporal attribution map (``:1169-1710``)."""
+        cfg = self.an.aggregate_sample_along_time
+        agg_type = agg_type or cfg.agg_type
+        norm_by_prediction = cfg.norm_by_prediction if norm_by_prediction is None else norm_by_prediction
+        cbar_limits = cbar_limits if cbar_limits is not None else cfg.cbar_limits
+        if self.df_unfiltered is None:
+            self.get_overview(plots=False)
+        sub = self.df_unfiltered[self.df_unfiltered["sensor_id"] == str(sensor)].sort_values("date_time")
+        if time_from is not None:
+            sub = sub[sub["date_time"] >= pd.to_datetime(time_from)]
+        if time_to is not None:
+            sub = sub[sub["date_time"] <= pd.to_datetime(time_to)]
+        if not len(sub):
+            return None
+        agg = {"mean": np.nanmean, "sum": np.nansum, "max": np.nanmax, "min": np.nanmin}[agg_type]
+        tb = int(round(self.preproc_config.timestep_before / max(1, int(self.preproc_config.get("freq", 1) or 1))))
+        times, centre, scores, flags, ga_rows, gf_rows = [], [], [], [], [], []
+        n_nb = None
+        scale = cfg.scale_feature_gradients
+        for _, row in sub.iterrows():
+            a, ga, gf = self._load(row, STEM_A), self._load(row, STEM_GA), self._load(row, STEM_GF)
+            p = self._load(row, STEM_P)
+            score = float(np.asarray(p).reshape(-1)[0]) if p is not None else np.nan
+            if norm_by_prediction and score > 0:
+                ga = ga / score if ga is not None else None
+                gf = gf / score if gf is not None else None
+            if gf is not None:
+                gf = gf / gf.shape[0] * 2 if scale == "auto" else gf * float(scale)
+                if n_nb is None:
+                    n_nb = gf.shape[0]
+                if gf.shape[0] != n_nb:      # neighbour set changed: mark missing (reference does the same)
+                    gf = np.full((n_nb,) + gf.shape[1:], np.nan)
+            times.append(row["date_time"])
+            centre.append(a[min(tb, a.shape[0] - 1)] if a is not None else np.nan)
+            scores.append(score)
+            flags.append(row["true"])
+            ga_rows.append(agg(ga, axis=0) if ga is not None else None)
+            gf_rows.append(agg(gf, axis=1) if gf is not None else None)
+        thr = float(self.ig.threshold)
+        pred_cls = (np.asarray(scores) > thr).astype(int)
+        rows_maps = []
+        if any(g is not None for g in ga_rows):
+            rows_maps.append(("flagged", np.stack([g for g in ga_rows if g is not None]).T))
+        if any(g is not None for g in gf_rows):
+            G = np.stack([g for g in gf_rows if g is not None])               # [S, n_nb, C]
+            if cfg.get("group_tl_channels", True):
+                G = G.mean(-1, keepdims=True)
+            for j in range(G.shape[1]):
+                rows_maps.append((f"node {j}", G[:, j].T))
+        nrows = 2 + len(rows_maps)
+        fig, axes = plt.subplots(nrows, 1, figsize=tuple(cfg.figsize), sharex=True,
+                                 height_ratios=[2, 0.5] + [1] * len(rows_maps))
+        x = np.arange(len(times))
+        cen = np.asarray([c if np.ndim(c) else [c] for c in centre], dtype=np.float64)
+        axes[0].plot(x, cen)
+        axes[0].plot(x, scores, color="k", linewidth=0.8, label="score")
+        if isinstance(cfg.ylims, (list, tuple)):
+            axes[0].set_ylim(*cfg.ylims)
+        axes[0].legend(loc="upper right")
+        cols = [COLOR_MAP[(int(t), int(p))] for t, p in zip(flags, pred_cls)]
+        axes[1].bar(x, 1, width=1.0, color=cols, edgecolor="none")
+        axes[1].set_yticks([])
+        vmin, vmax = (cbar_limits if isinstance(cbar_limits, (list, tuple)) else
+                      (-np.nanmax(np.abs(np.concatenate([m.reshape(-1) for _, m in rows_maps]))),
+                       np.nanmax(np.abs(np.concatenate([m.reshape(-1) for _, m in rows_maps])))))
+        mesh = None
+        for ax, (name, m) in zip(axes[2:], rows_maps):
+            mesh = ax.pcolormesh(np.arange(len(x) + 1) - 0.5, np.arange(m.shape[0] + 1), m, cmap="RdBu_r",
+                                 vmin=vmin, vmax=vmax, shading="flat")
+            ax.set_ylabel(name, rotation=0, ha="right", fontsize=7)
+            ax.set_yticks([])
+        if mesh is not None:
+            fig.colorbar(mesh, ax=list(axes[2:]), shrink=0.8)
+        tick = max(1, len(x) // 8)
+        axes[-1].set_xticks(x[::tick])
+        axes[-1].set_xticklabels([pd.Timestamp(t).strftime("%m-%d %H:%M") for t in times][::tick], rotation=30)
+        fig.suptitle(f"{sensor}: {agg_type} attribution per sample")
+        d = os.path.join(self.output_dir_analysis, str(sensor))
+        os.makedirs(d, exist_ok=True)
+        p = os.path.join(d, f"agg_samples_over_time_{agg_type}.png")
+        fig.savefig(p, bbox_inches="tight")
+        plt.close(fig)
+        return p
+
+    # ----------------------------------------------------------------- images / videos
+    def concatenate_images(self) -> List[str]:
+        """Stack each sample's heatmap over its classified-series plot (if both exist)."""
+        from PIL import Image
+        out = []
+        scale = float(self.an.concat_images_scale)
+        for _, row in (self.df if self.df is not None else self.get_overview(plots=False)).iterrows():
+            imgs = sorted(p for p in os.listdir(row["path"]) if p.endswith(".png") and not p.startswith("concat_"))
+            if len(imgs) < 2:
+                continue
+            dst = os.path.join(row["path"], f"concat_{row['sample_name']}.png")
+            if os.path.exists(dst) and not self.an.overwrite_concat_images:
+                continue
+            ims = [Image.open(os.path.join(row["path"], p)).convert("RGB") for p in imgs]
+            w = max(i.width for i in ims)
+            canvas = Image.new("RGB", (w, sum(i.height for i in ims)), "white")
+            y = 0
+            for im in ims:
+                canvas.paste(im, (0, y))
+                y += im.height
+            if scale != 1.0:
+                canvas = canvas.resize((int(canvas.width * scale), int(canvas.height * scale)))
+            canvas.save(dst)
+            out.append(dst)
+        return out
+
+    def create_videos(self, sensor=None, time_from=None, time_to=None) -> List[str]:
+        """Animated GIF per sensor of the IG heatmaps in time order (PIL; the reference
+        also writes mp4 through imageio/ffmpeg, which this image does not ship)."""
+        from PIL import Image, ImageDraw
+        if self.df is None:
+            self.get_overview(plots=False)
+        fps = float(self.an.video.video_fps)
+        sensors = [sensor] if sensor is not None else self.selected_sensors
+        out = []
+        for sid in sensors:
+            sub = self.df[self.df["sensor_id"] == str(sid)]
+            if time_from is not None:
+                sub = sub[sub["date_time"] >= pd.to_datetime(time_from)]
+            if time_to is not None:
+                sub = sub[sub["date_time"] <= pd.to_datetime(time_to)]
+            frames = []
+            prefix = "concat_" if self.an.video.videos_from_concat_images else "ig_heatmap_"
+            for k, (_, row) in enumerate(sub.iterrows()):
+                cand = [p for p in os.listdir(row["path"]) if p.startswith(prefix) and p.endswith(".png")]
+                if not cand:
+                    continue
+                im = Image.open(os.path.join(row["path"], cand[0])).convert("RGB")
+                # progress bar coloured by the sample's outcome
+                dr = ImageDraw.Draw(im)
+                frac = (k + 1) / max(1, len(sub))
+                dr.rectangle([0, im.height - 8, int(im.width * frac), im.height], fill=COLOR_MAP[(row["true"],
+                                                                                                  row["pred"])])
+                frames.append(im)
+            if not frames:
+                continue
+            d = os.path.join(self.output_dir_analysis, str(sid))
+            os.makedirs(d, exist_ok=True)
+            p = os.path.join(d, f"ig_{sid}_{self.conf_matrix_string}.gif")
+            frames[0].save(p, save_all=True, append_images=frames[1:], duration=int(1000 / fps), loop=0)
+            out.append(p)
+        return out
+
+    # ----------------------------------------------------------------- maintenance
+    def scale_gradients_with_input(self, dont_scale: Optional[List[str]] = None) -> int:
+        """Multiply saved gradients by the saved inputs in place (zero baseline; for results
+        produced with ``scale_gradients: false``)."""
+        if self.df is None:
+            self.get_overview(plots=False)
+        skip = set(dont_scale or [])
+        n = 0
+        for _, row in self.df[self.df["sensor_id"].isin(self.selected_sensors)].iterrows():
+            if row["sample_name"] in skip:
+                continue
+            for gs, fs in ((STEM_GF, STEM_F), (STEM_GA, STEM_A)):
+                g, f = self._load(row, gs), self._load(row, fs)
+                if g is None or f is None:
+                    continue
+                np.save(os.path.join(row["path"], self.get_filename(gs, row["sample_name"]) + ".npy"), g * f)
+            n += 1
+        return n
+
+    def rename_based_on_threshold(self, threshold: Optional[float] = None) -> int:
+        """Re-derive the predicted class of each sample from its saved score and rename
+        its directory / files (``..._<true>_<pred>``)."""
+        thr = float(self.ig.threshold if threshold is None else threshold)
+        if self.df is None:
+            self.get_overview(plots=False)
+        n = 0
+        for _, row in self.df_unfiltered[self.df_unfiltered["sensor_id"].isin(self.selected_sensors)].iterrows():
+            p = self._load(row, STEM_P)
+            if p is None:
+                continue
+            cls = int(float(np.asarray(p).reshape(-1)[0]) > thr)
+            if cls == row["pred"]:
+                continue
+            old = row["sample_name"]
+            new = old[:-1] + str(cls)
+            for f in os.listdir(row["path"]):
+                if old in f:
+                    os.rename(os.path.join(row["path"], f), os.path.join(row["path"], f.replace(old, new)))
+            os.rename(row["path"], os.path.join(os.path.dirname(row["path"]), new))
+            n += 1
+        self.get_overview(plots=False)
+        return n
+
+
+def run_analyser(args):
+    import json
+    from ..cli.common import load_configs
+    pc, mc = load_configs(args)
+    xc = C.load(args.xai_config) if args.xai_config else C.default("xai_ig")
+    xc["output_dir"] = args.xai_dir
+    an = IntegrateGradientsAnalyser(pc, mc, xc)
+    df = an.get_overview()
+    agg = an.spatial_aggregate_gradients()
+    plots = an.plot_spatial_aggregated_gradients()
+    for s in an.selected_sensors[:4]:
+        an.plot_agg_samples_over_time(s)
+    print(json.dumps({"samples": int(len(df)), "sensors": len(an.selected_sensors), "aggregated": len(agg),
+                      "plots": len(plots), "output_dir": an.output_dir_analysis}))
+
+
+__all__ = ["IntegrateGradientsAnalyser", "run_analyser", "COLOR_MAP", "COLOR_NAMES"]

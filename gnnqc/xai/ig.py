@@ -1,0 +1,417 @@
+"""Integrated Gradients.
+
+Reference: ``xai/libs/integrated_gradients.py`` - ``IntegratedGradientsExplainer``
+(``:91-2044``): zero baseline (``:898-917``), ``m_steps + 1`` linearly interpolated
+inputs (``:919-942``), one forward + ``GradientTape`` backward per interpolation
+step on the whole batch (``:955-1004``), trapezoidal Riemann average (``:1006-1015``),
+optional input scaling and negative-value policy (``:1180-1208``), threshold
+classification and TP/TN/FP/FN sample selection (``:495-546``, ``:1226-1262``),
+per-sample ``.npy`` outputs in ``<out>/integrated_gradients/<project>/<ds>/<dataset>/
+<sensor>/<sensor>_<YYYYmmdd_HHMMSS>_<true>_<pred>/`` (``:221-384``, ``:1248-1400``) and
+SLURM array sharding (``:190-199``, ``:432-448``).
+
+MI355X design: the reference runs 101 sequential forward/backward passes over a
+batch of 128 windows - each pass uses a sliver of the GPU. Here the alpha axis is
+folded into the batch: ``k`` interpolation steps x ``B`` windows go through ONE
+forward + ONE input-gradient backward (frozen weights: the LSTM backward skips the
+weight-gradient kernel, the fused GCN backward skips its reduction), so the
+persistent LSTM kernels get ``k*B`` sequences to spread over 256 CUs. The
+trapezoid weights are applied while accumulating on the device; nothing goes to the
+host until a batch is finished. Batches are sharded across ranks (one process per
+GPU, ``torch.distributed``) or SLURM array tasks exactly like the reference's
+``_split_work``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import config as C
+
+CONFUSION = {(0, 0): "TN", (0, 1): "FP", (1, 0): "FN", (1, 1): "TP"}
+
+
+def trapezoid_weights(m_steps: int, device=None) -> torch.Tensor:
+    """Weights w_i with sum_i w_i g_i == mean_i (g_i + g_{i+1}) / 2 over m_steps intervals."""
+    w = torch.full((m_steps + 1,), 1.0 / m_steps, device=device, dtype=torch.float32)
+    w[0] = w[-1] = 0.5 / m_steps
+    return w
+
+
+def _frozen(model):
+    """Context: weights do not require grad (input gradients only), restored afterwards."""
+    class _Ctx:
+        def __enter__(self):
+            self.flags = [(p, p.requires_grad) for p in model.parameters()]
+            for p, _ in self.flags:
+                p.requires_grad_(False)
+
+        def __exit__(self, *a):
+            for p, f in self.flags:
+                p.requires_grad_(f)
+    return _Ctx()
+
+
+class IntegratedGradients:
+    """Alpha-batched IG engine for the GCN / baseline classifiers.
+
+    ``attribute(batch)`` returns device tensors:
+
+    * ``grad_x``    [B, T, N, C] node-feature attributions (GCN models),
+    * ``grad_anom`` [B, T, C] flagged-sensor series attributions (CML),
+    * ``pred``      [B] model output at alpha = 1 (the actual prediction),
+    * ``path_pred`` [m+1, B] outputs along the path (gradient-saturation plots).
+
+    SoilNet models emit one score per node; ``target`` [B] picks the node whose score
+    is explained (default: the highest-scoring valid node).
+    """
+
+    def __init__(self, model, ds_type: str, m_steps: int = 100, baseline: str = "zero",
+                 max_rows: int = 16384, scale_gradients: bool = True, negative_values: str = "keep"):
+        if baseline != "zero":
+            raise NotImplementedError("only the zero baseline is implemented (as in the reference, :901-917)")
+        if negative_values not in ("keep", "clip", "abs"):
+            raise ValueError(f"negative_values must be keep/clip/abs, got {negative_values!r}")
+        self.model = model
+        self.ds_type = ds_type
+        self.m_steps = int(m_steps)
+        self.max_rows = int(max_rows)
+        self.scale_gradients = scale_gradients
+        self.negative_values = negative_values
+        self.is_baseline = type(model).__name__ == "BaselineClassifier"
+
+    # -- inputs that are interpolated ------------------------------------------------
+    def _split(self, batch):
+        """(interpolated tensors, static tensors, rebuild fn)."""
+        if self.ds_type == "cml":
+            if self.is_baseline:
+                return [batch.anom], [], lambda v, s: (v[0],)
+            return ([batch.x, batch.anom], [batch.adj, batch.node_mask, batch.anom_pos],
+                    lambda v, s: (v[0], v[1], s[0], s[1], s[2]))
+        if self.is_baseline:
+            return [batch.x], [batch.node_mask], lambda v, s: (v[0], s[0])
+        return [batch.x], [batch.adj, batch.node_mask], lambda v, s: (v[0], s[0], s[1])
+
+    def _select(self, out: torch.Tensor, B: int, k: int, target: Optional[torch.Tensor]):
+        out = out.reshape(k * B, -1)
+        if out.shape[1] == 1:
+            return out[:, 0]
+        t = target.repeat(k)
+        return out.gather(1, t[:, None])[:, 0]
+
+    def attribute(self, batch, target: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        model = self.model
+        was_training = model.training
+        model.eval()
+        vals, static, build = self._split(batch)
+        B = vals[0].shape[0]
+        with torch.no_grad():
+            pred_full = model(build(vals, static)).reshape(B, -1).float()
+        if pred_full.shape[1] > 1:
+            if target is None:
+                masked = pred_full.masked_fill(batch.node_mask <= 0, -1.0)
+                target = masked.argmax(1)
+            pred = pred_full.gather(1, target[:, None])[:, 0]
+        else:
+            pred = pred_full[:, 0]
+        alphas = torch.linspace(0.0, 1.0, self.m_steps + 1, device=vals[0].device)
+        wts = trapezoid_weights(self.m_steps, vals[0].device)
+        acc = [torch.zeros_like(v, dtype=torch.float32) for v in vals]
+        path_pred = torch.empty(self.m_steps + 1, B, device=vals[0].device)
+        k = max(1, min(self.m_steps + 1, self.max_rows // max(B, 1)))
+        with _frozen(model), torch.enable_grad():
+            for s in range(0, self.m_steps + 1, k):
+                a = alphas[s:s + k]
+                kk = a.numel()
+                # zero baseline: x_alpha = alpha * x, folded into the batch dimension
+                xs = []
+                for v in vals:
+                    shp = (kk,) + (1,) * v.dim()
+                    xi = (a.view(shp) * v.unsqueeze(0).float()).reshape((kk * B,) + tuple(v.shape[1:]))
+                    xs.append(xi.requires_grad_(True))
+                st = [t.repeat((kk,) + (1,) * (t.dim() - 1)) for t in static]
+                out = model(build(xs, st))
+                y = self._select(out, B, kk, target)
+                grads = torch.autograd.grad(y.sum(), xs)
+                path_pred[s:s + kk] = y.detach().view(kk, B)
+                w = wts[s:s + kk]
+                for j, g in enumerate(grads):
+                    g = g.view((kk, B) + tuple(g.shape[1:]))
+                    acc[j] += torch.tensordot(w, g, dims=1)
+        model.train(was_training)
+        if self.scale_gradients:
+            acc = [g * v.float() for g, v in zip(acc, vals)]       # (x - baseline) * avg grad
+        if self.negative_values == "abs":
+            acc = [g.abs() for g in acc]
+        elif self.negative_values == "clip":
+            acc = [g.clamp(min=0) for g in acc]
+        res = {"pred": pred, "path_pred": path_pred, "target": target}
+        if self.ds_type == "cml":
+            if self.is_baseline:
+                res["grad_anom"] = acc[0]
+            else:
+                res["grad_x"], res["grad_anom"] = acc
+        else:
+            res["grad_x"] = acc[0]
+        return res
+
+
+def completeness_gap(ig_res: Dict[str, torch.Tensor]) -> torch.Tensor:
+    """IG axiom check: sum of (input-scaled) attributions ~= f(x) - f(baseline)."""
+    tot = 0
+    for k in ("grad_x", "grad_anom"):
+        if k in ig_res:
+            g = ig_res[k]
+            tot = tot + g.reshape(g.shape[0], -1).sum(1)
+    return tot - (ig_res["path_pred"][-1] - ig_res["path_pred"][0])
+
+
+# ====================================================================================
+class IntegratedGradientsExplainer:
+    """Config-driven explainer with the reference's output layout.
+
+    ``IntegratedGradientsExplainer(preproc_config, model_config, xai_config)`` - paths
+    or Config objects. ``prepare_data()`` builds the window store; ``get_gradients()``
+    runs IG over the selected batches and writes per-sample files.
+    """
+
+    def __init__(self, preproc_config, model_config, xai_config, model=None, windows=None, device=None,
+                 raw=None):
+        load = lambda c: C.load(c) if isinstance(c, str) else c  # noqa: E731
+        self.preproc_config = C.normalize_preproc(load(preproc_config))
+        self.model_config = load(model_config)
+        self.xai_config = load(xai_config) if xai_config is not None else C.default("xai_ig")
+        self.ig_cfg = self.xai_config.integrated_gradients
+        self.ds_type = self.preproc_config.ds_type
+        from ..parallel import dist as D
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        # SLURM array job sharding (``:190-199``) or one rank per GPU
+        if "SLURM_ARRAY_TASK_ID" in os.environ:
+            self.workerid = int(os.environ["SLURM_ARRAY_TASK_ID"])
+            self.n_worker = int(os.environ["SLURM_ARRAY_TASK_COUNT"])
+        elif D.world_size() > 1:
+            self.workerid, self.n_worker = D.rank(), D.world_size()
+        else:
+            self.workerid = self.n_worker = None
+        self.output_dir = self._save_path()
+        os.makedirs(self.output_dir, exist_ok=True)
+        torch.manual_seed(int(self.ig_cfg.get("random_seed", 42)))
+        np.random.seed(int(self.ig_cfg.get("random_seed", 42)))
+        self.model = model if model is not None else self._load_model()
+        self.model.to(self.device).eval()
+        self.is_baseline = type(self.model).__name__ == "BaselineClassifier"
+        self.windows = windows
+        self.raw = raw
+        self.store = None
+        self.sample_ids = None
+        self.results: List[dict] = []
+
+    # -- paths (``:221-384``) ----------------------------------------------------------
+    def _save_path(self, sensor: str = "", date: str = "", true="", pred="") -> str:
+        base = os.path.join(self.xai_config.output_dir, "integrated_gradients", self.xai_config.project,
+                            self.ds_type, self.ig_cfg.dataset)
+        if sensor == "" and date == "":
+            return base
+        return os.path.join(base, sensor, f"{sensor}_{date}_{true}_{pred}")
+
+    def _file_name(self, sensor: str = "", date: str = "", true="", pred="") -> str:
+        stem = f"{self.xai_config.project}_{self.ds_type}_{self.ig_cfg.dataset}"
+        if sensor == "" and date == "":
+            return stem
+        return f"{stem}_{sensor}_{date}_{true}_{pred}"
+
+    def log_file(self, batch_id: int, index: int, sensor: str, date: str):
+        d = os.path.join(self.output_dir, "log")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "log.txt" if self.workerid is None else f"log_{self.workerid}.txt"), "a") as f:
+            f.write(f"{self.xai_config.project},{self.ds_type},{self.ig_cfg.dataset},{batch_id},{index},{sensor},"
+                    f"{date}\n")
+
+    @staticmethod
+    def _split_work(items: Sequence, workerid: int, n_worker: int) -> list:
+        return [it for i, it in enumerate(items) if i % n_worker == workerid]
+
+    def copy_config_files(self, paths: Sequence[str]):
+        for p in paths:
+            if isinstance(p, str) and os.path.exists(p):
+                shutil.copy(p, self.output_dir)
+
+    # -- model / data ----------------------------------------------------------------
+    def _load_model(self):
+        path = self.model_config.get("model_path")
+        if path and os.path.exists(os.path.join(path, "gnnqc_state.pt")):
+            from ..ckpt import load_model
+            return load_model(path, device=self.device)
+        if path and os.path.exists(os.path.join(path, "variables", "variables.index")):
+            from ..ckpt.keras_layout import build_from_keras
+            return build_from_keras(path, ds_type=self.ds_type, device=self.device)[0]
+        raise FileNotFoundError(f"no model at {path!r}")
+
+    def prepare_data(self):
+        """Window store + the id list of the configured dataset split (``:590-703``)."""
+        from ..data.preprocessing import create_windows_dataset, load_dataset
+        from ..data.store import DeviceStore
+        if self.windows is None:
+            self.windows = create_windows_dataset(self.preproc_config, raw=self.raw)
+        norm = getattr(self.model, "model_normalization", getattr(self.model, "normalization", None))
+        self.store = DeviceStore(self.windows, norm, self.preproc_config.graph, device=self.device)
+        tr, va, te = load_dataset(self.preproc_config, self.windows)
+        which = self.ig_cfg.dataset
+        ids = {"train": tr, "val": va, "test": te}.get(which)
+        if ids is None or which == "all":
+            ids = np.arange(self.windows.n_windows)
+        self.sample_ids = np.asarray(ids, np.int64)
+        if self.ig_cfg.get("evaluate_model", False):
+            self.evaluate()
+        return self.sample_ids
+
+    def evaluate(self) -> dict:
+        from ..eval.metrics import roc_auc_score
+        preds, ys = [], []
+        for b in self._batches(range(self.n_batches)):
+            with torch.no_grad():
+                p = self.model(b[1].model_inputs(self.ds_type, self.is_baseline)).reshape(b[1].y.shape)
+            keep = b[1].y_mask > 0
+            preds.append(p[keep].float().cpu().numpy())
+            ys.append(b[1].y[keep].cpu().numpy())
+        y, p = np.concatenate(ys), np.concatenate(preds)
+        res = {"auc": float(roc_auc_score(y, p)) if 0 < y.sum() < len(y) else float("nan"), "n": int(len(y))}
+        print(res)
+        return res
+
+    @property
+    def batch_size(self) -> int:
+        return int(self.preproc_config.batch_size)
+
+    @property
+    def n_batches(self) -> int:
+        return -(-len(self.sample_ids) // self.batch_size)
+
+    def _batches(self, batch_ids):
+        for bid in batch_ids:
+            ids = self.sample_ids[bid * self.batch_size:(bid + 1) * self.batch_size]
+            if len(ids) == 0:
+                raise ValueError(f"Batch {bid} not found. The dataset has fewer batches.")
+            yield bid, self.store.gather(torch.as_tensor(ids, device=self.device)), ids
+
+    # -- IG over batches ---------------------------------------------------------------
+    def get_gradients(self, max_batches: Optional[int] = None):
+        if self.store is None:
+            self.prepare_data()
+        sel = self.ig_cfg.batch_ids
+        bids = list(range(self.n_batches)) if sel in ("all", None) else [int(b) for b in sel]
+        if self.workerid is not None:
+            bids = self._split_work(bids, self.workerid, self.n_worker)
+        if max_batches is not None:
+            bids = bids[:max_batches]
+        engine = IntegratedGradients(self.model, self.ds_type, m_steps=int(self.ig_cfg.m_steps),
+                                     baseline=self.ig_cfg.get("baseline", "zero"),
+                                     scale_gradients=bool(self.ig_cfg.get("scale_gradients", True)),
+                                     negative_values=self.ig_cfg.get("negative_values", "keep"),
+                                     max_rows=int(self.ig_cfg.get("max_rows", 16384)))
+        for bid, batch, ids in self._batches(bids):
+            res = None
+            if not self.ig_cfg.get("load_gradients_from_sample_file", False):
+                res = engine.attribute(batch)
+            else:
+                with torch.no_grad():
+                    res = {"pred": self.model(batch.model_inputs(self.ds_type, self.is_baseline)).reshape(
+                        len(batch.wid), -1)[:, 0].float()}
+            self._unwrap_and_save(bid, batch, ids, res)
+        return self.results
+
+    def _sample_info(self, wid: int):
+        ws = self.windows
+        g_of, l_of = ws.flat() if not hasattr(self, "_flat") else self._flat
+        self._flat = (g_of, l_of)
+        g = ws.groups[int(g_of[wid])]
+        ix = ws.indices[int(g_of[wid])]
+        c = int(ix.center[int(l_of[wid])])
+        date = np.datetime64(g.time[c], "s").astype(object).strftime("%Y%m%d_%H%M%S")
+        return str(g.group_id), date
+
+    def _unwrap_and_save(self, bid: int, batch, ids, res):
+        thr = float(self.ig_cfg.threshold)
+        pred = res["pred"].detach().float().cpu().numpy()
+        pred_cls = (pred > thr).astype(int)
+        if self.ds_type == "cml":
+            true = batch.y.detach().cpu().numpy().astype(int)
+        else:
+            t = res.get("target")
+            yv = batch.y.detach().cpu().numpy()
+            true = (yv[np.arange(len(ids)), t.cpu().numpy()] if t is not None else yv.max(1)).astype(int)
+        which = list(self.ig_cfg.which_samples)
+        keep = [i for i in range(len(ids)) if CONFUSION[(int(true[i]), int(pred_cls[i]))] in which]
+        x = batch.x.detach().float().cpu().numpy()
+        mask = batch.node_mask.detach().cpu().numpy() > 0
+        anom = batch.anom.detach().float().cpu().numpy() if batch.anom is not None else None
+        gx = res["grad_x"].detach().cpu().numpy() if "grad_x" in res else None
+        ga = res["grad_anom"].detach().cpu().numpy() if "grad_anom" in res else None
+        for i in keep:
+            sensor, date = self._sample_info(int(ids[i]))
+            tr, pr = int(true[i]), int(pred_cls[i])
+            out = self._save_path(sensor, date, tr, pr)
+            os.makedirs(out, exist_ok=True)
+            fn = self._file_name(sensor, date, tr, pr)
+            nodes = np.nonzero(mask[i])[0]
+            feats = x[i][:, nodes].transpose(1, 0, 2)                      # [n, T, C] like ``_unwrap_features``
+            files = {"features_unwrapped": feats, "predictions_unwrapped": np.array([pred[i]], np.float32),
+                     "anomaly_flag_true_unwrapped": np.array(tr)}
+            if anom is not None:
+                files["anom_ts_unwrapped"] = anom[i]
+            if gx is not None:
+                files["gradients_features_unwrapped"] = gx[i][:, nodes].transpose(1, 0, 2)
+            if ga is not None:
+                files["gradients_anom_ts_unwrapped"] = ga[i]
+            if "path_pred" in res:
+                files["path_predictions_unwrapped"] = res["path_pred"][:, i].detach().cpu().numpy()
+            if self.ig_cfg.get("load_gradients_from_sample_file", False):
+                for k in ("gradients_features_unwrapped", "gradients_anom_ts_unwrapped"):
+                    p = os.path.join(out, f"{k}_{fn}.npy")
+                    if os.path.exists(p):
+                        files[k] = np.load(p)
+            for k, v in files.items():
+                np.save(os.path.join(out, f"{k}_{fn}.npy"), v)
+            self.log_file(bid, i, sensor, date)
+            rec = {"batch": bid, "index": i, "sensor": sensor, "date": date, "true": tr, "pred": pr,
+                   "score": float(pred[i]), "dir": out, "file_stem": fn,
+                   "timestep_before_steps": int(round(self.windows.timestep_before / self.windows.freq))}
+            self.results.append(rec)
+            if self.ig_cfg.get("plot_heatmap", False):
+                from ..viz.ig import plot_ig_heatmap
+                plot_ig_heatmap(files, rec, self.xai_config, out_path=os.path.join(out, f"ig_heatmap_{fn}.png"),
+                                batch_id=bid)
+            if self.ig_cfg.get("plot_gradient_saturation", False) and "path_pred" in res:
+                from ..viz.ig import plot_gradient_saturation
+                plot_gradient_saturation(files["path_predictions_unwrapped"],
+                                         os.path.join(out, f"gradient_saturation_{fn}.png"))
+
+    def plot_ig_heatmap_from_directory(self, directory: Optional[str] = None):
+        from ..viz.ig import plot_ig_heatmap_from_directory
+        return plot_ig_heatmap_from_directory(directory or self.output_dir, self.xai_config)
+
+
+def run_explainer(args):
+    """CLI: ``python -m gnnqc.cli explain --model-dir ... [--xai-config ...]``."""
+    import json
+    from ..cli.common import load_configs, make_raw, resolve_device
+    pc, mc = load_configs(args)
+    dev = resolve_device(args.device)
+    xc = C.load(args.xai_config) if args.xai_config else C.default("xai_ig")
+    if args.out_dir:
+        xc["output_dir"] = args.out_dir
+    mc["model_path"] = args.model_dir
+    raw = make_raw(args, pc)
+    ex = IntegratedGradientsExplainer(pc, mc, xc, device=dev, raw=raw)
+    ex.prepare_data()
+    res = ex.get_gradients(max_batches=args.max_batches)
+    print(json.dumps({"samples": len(res), "output_dir": ex.output_dir}))
+
+
+__all__ = ["IntegratedGradients", "IntegratedGradientsExplainer", "trapezoid_weights", "completeness_gap",
+           "run_explainer", "CONFUSION"]

@@ -1,0 +1,162 @@
+"""Integrated gradients engine, explainer output layout, analyser, plots."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gnnqc import config as C
+from gnnqc.data.preprocessing import create_windows_dataset
+from gnnqc.data.store import DeviceStore
+from gnnqc.data.synthetic import make_cml_raw, make_soilnet_raw
+from gnnqc.models import create_model
+from gnnqc.xai.ig import IntegratedGradients, IntegratedGradientsExplainer, completeness_gap, trapezoid_weights
+
+
+@pytest.fixture(scope="module")
+def cml_small():
+    pc = C.normalize_preproc(C.default("preprocessing_cml"))
+    ws = create_windows_dataset(pc, raw=make_cml_raw(n_sensors=8, n_minutes=2 * 1440, seed=5))
+    return pc, ws, DeviceStore(ws, "rolling_median", pc.graph)
+
+
+def _sharp(model, gain=40.0):
+    """Random-init outputs sit at ~0.5; scale the output layer so IG has something to explain."""
+    with torch.no_grad():
+        model.dense_out.kernel.mul_(gain)
+    return model.eval()
+
+
+def _sequential_ig(model, batch, m):
+    """Reference semantics (``integrated_gradients.py:955-1015``): one pass per alpha."""
+    xs, gx, ga = batch.x, [], []
+    for a in torch.linspace(0, 1, m + 1):
+        x = (a * batch.x).requires_grad_(True)
+        an = (a * batch.anom).requires_grad_(True)
+        y = model((x, an, batch.adj, batch.node_mask, batch.anom_pos)).reshape(-1)
+        g1, g2 = torch.autograd.grad(y.sum(), [x, an])
+        gx.append(g1)
+        ga.append(g2)
+    gx, ga = torch.stack(gx), torch.stack(ga)
+    ix = ((gx[:-1] + gx[1:]) / 2).mean(0) * xs
+    ia = ((ga[:-1] + ga[1:]) / 2).mean(0) * batch.anom
+    return ix, ia
+
+
+def test_trapezoid_weights():
+    w = trapezoid_weights(4)
+    g = torch.arange(5.0)
+    assert torch.isclose((w * g).sum(), ((g[:-1] + g[1:]) / 2).mean())
+
+
+def test_alpha_batched_matches_sequential(cml_small):
+    pc, ws, store = cml_small
+    torch.manual_seed(1)
+    model = _sharp(create_model(C.default("model_cml"), pc))
+    for p in model.parameters():
+        p.requires_grad_(False)
+    b = store.gather(torch.arange(0, 40, 8))
+    ix, ia = _sequential_ig(model, b, 6)
+    for max_rows in (5, 12, 10_000):            # alpha chunking must not change the result
+        r = IntegratedGradients(model, "cml", m_steps=6, max_rows=max_rows).attribute(b)
+        torch.testing.assert_close(r["grad_x"], ix, atol=1e-6, rtol=1e-4)
+        torch.testing.assert_close(r["grad_anom"], ia, atol=1e-6, rtol=1e-4)
+    # weights left trainable state untouched by the engine
+    assert all(not p.requires_grad for p in model.parameters())
+
+
+def test_completeness_improves_with_steps(cml_small):
+    pc, ws, store = cml_small
+    torch.manual_seed(2)
+    model = _sharp(create_model(C.default("model_cml"), pc, baseline=True), 60.0)
+    b = store.gather(torch.arange(0, 60, 6))
+    gaps = []
+    for m in (4, 64):
+        r = IntegratedGradients(model, "cml", m_steps=m).attribute(b)
+        delta = (r["path_pred"][-1] - r["path_pred"][0]).abs()
+        gaps.append(float(completeness_gap(r).abs().max() / delta.max().clamp(min=1e-6)))
+    assert gaps[1] < 0.05 and gaps[1] <= gaps[0] + 1e-6
+
+
+def test_soilnet_target_node():
+    pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
+    pc["timestep_before"], pc["timestep_after"] = 360, 60         # T = 29 survives three pool-3 stages
+    pc = C.normalize_preproc(pc)
+    ws = create_windows_dataset(pc, raw=make_soilnet_raw(n_boxes=4, n_time=6 * 96, seed=2))
+    store = DeviceStore(ws, "scale_range", pc.graph)
+    torch.manual_seed(0)
+    model = _sharp(create_model(C.default("model_soilnet"), pc))
+    b = store.gather(torch.arange(3))
+    r = IntegratedGradients(model, "soilnet", m_steps=4).attribute(b)
+    assert r["grad_x"].shape == b.x.shape and r["target"].shape == (3,)
+    assert bool((b.node_mask.gather(1, r["target"][:, None]) > 0).all())
+
+
+def test_explainer_writes_reference_layout_and_analyser(cml_small, tmp_path):
+    from gnnqc.ckpt import save_model
+    from gnnqc.xai.analyse import IntegrateGradientsAnalyser
+    pc, ws, _ = cml_small
+    torch.manual_seed(3)
+    mc = C.default("model_cml")
+    model = _sharp(create_model(mc, pc))
+    mdir = str(tmp_path / "model")
+    save_model(model, mdir, preproc_config=pc)
+    mc["model_path"] = mdir
+    xc = C.default("xai_ig")
+    xc["output_dir"] = str(tmp_path / "xplain")
+    ig = xc.integrated_gradients
+    ig["m_steps"], ig["dataset"], ig["threshold"], ig["plot_heatmap"] = 4, "all", 0.5, True
+    ig["plot_gradient_saturation"] = True
+    pc2 = C.Config(dict(pc))
+    pc2["batch_size"] = 16
+    ex = IntegratedGradientsExplainer(pc2, mc, xc, windows=ws, device="cpu")
+    ex.prepare_data()
+    ex.sample_ids = ex.sample_ids[:32]
+    res = ex.get_gradients()
+    assert len(res) == 32                       # all four confusion classes selected
+    r0 = res[0]
+    stem = r0["file_stem"]
+    for k in ("gradients_features_unwrapped", "gradients_anom_ts_unwrapped", "features_unwrapped",
+              "anom_ts_unwrapped", "predictions_unwrapped", "anomaly_flag_true_unwrapped"):
+        assert os.path.exists(os.path.join(r0["dir"], f"{k}_{stem}.npy")), k
+    gf = np.load(os.path.join(r0["dir"], f"gradients_features_unwrapped_{stem}.npy"))
+    f = np.load(os.path.join(r0["dir"], f"features_unwrapped_{stem}.npy"))
+    assert gf.shape == f.shape and gf.shape[1] == ws.seq_len     # [n_nodes, T, C]
+    assert os.path.exists(os.path.join(r0["dir"], f"ig_heatmap_{stem}.png"))
+    assert os.path.basename(r0["dir"]).startswith(r0["sensor"] + "_")
+    assert os.path.exists(os.path.join(ex.output_dir, "log", "log.txt"))
+
+    xc.integrated_gradients.analyser["which_samples"] = ["TP", "FP", "TN", "FN"]
+    xc.integrated_gradients.analyser.spatial_aggregation["which_samples"] = ["TP", "FP", "TN", "FN"]
+    an = IntegrateGradientsAnalyser(pc2, mc, xc)
+    df = an.get_overview()
+    assert len(df) == 32
+    agg = an.spatial_aggregate_gradients()
+    sid = r0["sensor"]
+    assert agg[sid]["features"].shape == (ws.seq_len, 2) and agg[sid]["anom_ts"].shape == (ws.seq_len, 2)
+    assert an.plot_spatial_aggregated_gradients()
+    assert an.plot_agg_samples_over_time(sid) is not None
+    gifs = an.create_videos()
+    assert gifs and os.path.getsize(gifs[0]) > 0
+    # re-threshold: everything above 0 becomes positive -> directories renamed to *_1
+    n = an.rename_based_on_threshold(threshold=0.0)
+    assert n >= 0 and (an.df_unfiltered["pred"] == 1).all()
+
+
+def test_roc_and_result_plots(cml_small, tmp_path):
+    from gnnqc.eval.metrics import roc_curve
+    from gnnqc.viz import extract_target_info, plot_results, plot_roc_curves
+    pc, ws, store = cml_small
+    rng = np.random.default_rng(0)
+    y = rng.integers(0, 2, 300)
+    p = np.clip(y * 0.4 + rng.random(300) * 0.6, 0, 1)
+    fpr, tpr, thr = roc_curve(y, p)
+    out = plot_roc_curves([fpr], [tpr], None, [thr], [0.5], str(tmp_path / "roc.png"), ["GCN"])
+    assert os.path.getsize(out) > 0
+    ids = np.arange(min(200, ws.n_windows))
+    sids, dates, flags = extract_target_info(ws, ids)
+    assert len(sids) == len(ids) == len(dates)
+    mc = C.Config({"plotting": {"outdir": str(tmp_path / "plots"), "alpha": 0.2, "plot_time_range": 24}})
+    paths = plot_results(sids, dates, (rng.random(len(ids)) > 0.5).astype(int), flags, rng.random(len(ids)), pc, mc,
+                         windows=ws)
+    assert paths and all(os.path.exists(q) for q in paths)
