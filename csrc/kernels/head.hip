@@ -1,0 +1,390 @@
+// Fused classifier head + weighted BCE + metric accumulation (forward) and its
+// backward, for gfx950.
+//
+// Reference: the Keras head Dense(64) -> LeakyReLU(.3) -> Dense(64) -> LeakyReLU(.3)
+// -> Dense(1, sigmoid) (libs/create_model.py:204-239, :356-376), compiled with
+// binary_crossentropy + class_weight (libs/fit_model.py:76-111) and the metric list
+// Recall/BinaryAccuracy/Precision/AUC/TP/FP/TN/FN (:79-86).
+//
+// On the eager path this is ~50 launches of 1-5 us each per training step (GEMMs
+// with 128 rows, bias adds, activations, BCE pieces, metric reductions, histogram).
+// Here: ONE forward kernel (activations, logits, loss, confusion counts, score
+// histogram) and ONE backward kernel (all weight gradients + d features).
+//
+// Layout: rows are tiled by 64; 256 threads = 4 waves; thread (j = tid & 63,
+// g = tid >> 6) owns output column j of rows g*16 .. g*16+15. Input tiles and
+// activations live in LDS; inner products read LDS with wave-uniform addresses
+// (broadcast, conflict free) and weights with lane-contiguous addresses. The
+// backward kernel is persistent over row tiles and keeps its weight-gradient
+// partials in registers, flushing them once per block with coalesced atomics
+// straight into the optimiser's flat gradient buffer (or a zeroed sink).
+#include "common.h"
+
+namespace gq {
+
+constexpr int HT = 64;     // rows per tile
+constexpr int HU = 64;     // dense units (model_config dense.units)
+
+__device__ __forceinline__ float leaky(float z, float a) { return z > 0.f ? z : a * z; }
+__device__ __forceinline__ float dleaky(float z, float a) { return z > 0.f ? 1.f : a; }
+
+// mask sum over all rows (every block recomputes it: no cross-block dependency)
+__device__ float block_mask_sum(const float* __restrict__ mask, int R, float* red) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < R; i += blockDim.x) s += mask[i];
+  s = wave_sum(s);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = s;
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return s;
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void head_fwd_kernel(
+    const float* __restrict__ feat, int ldf, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ W3,
+    const float* __restrict__ b3, const float* __restrict__ y, const float* __restrict__ mask, int R,
+    float alpha1, float alpha2, float w0, float w1, float* __restrict__ z1o, float* __restrict__ z2o,
+    float* __restrict__ logits, float* __restrict__ aux, double* __restrict__ sums, float* __restrict__ hist,
+    int bins) {
+  __shared__ float sf[HT][F + 4];
+  __shared__ float sa1[HT][HU + 4];
+  __shared__ float sa2[HT][HU + 4];
+  __shared__ float red[4];
+  __shared__ float mred[4][8];
+  const int tid = threadIdx.x, j = tid & 63, g = tid >> 6;
+  const float nm = block_mask_sum(mask, R, red);
+  const float inv = 1.f / fmaxf(nm, 1.f);
+  if (blockIdx.x == 0 && tid == 0) aux[1] = nm;
+  float m_loss = 0.f, m_n = 0.f, m_tp = 0.f, m_tn = 0.f, m_fp = 0.f, m_fn = 0.f;
+  const int ntiles = (R + HT - 1) / HT;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row0 = tile * HT;
+    // stage the feature tile (float4; rows past R are zero)
+    for (int e = tid; e < HT * (F / 4); e += 256) {
+      const int r = e / (F / 4), c4 = e % (F / 4);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row0 + r < R) v = *reinterpret_cast<const float4*>(feat + (long)(row0 + r) * ldf + 4 * c4);
+      *reinterpret_cast<float4*>(&sf[r][4 * c4]) = v;
+    }
+    __syncthreads();
+    float acc[16];
+    const float bj1 = b1[j];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = bj1;
+    #pragma unroll 4
+    for (int k = 0; k < F; ++k) {
+      const float w = W1[k * HU + j];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] += sf[g * 16 + i][k] * w;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = g * 16 + i;
+      if (row0 + r < R) z1o[(long)(row0 + r) * HU + j] = acc[i];
+      sa1[r][j] = leaky(acc[i], alpha1);
+    }
+    __syncthreads();
+    const float bj2 = b2[j];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = bj2;
+    #pragma unroll 4
+    for (int k = 0; k < HU; ++k) {
+      const float w = W2[k * HU + j];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] += sa1[g * 16 + i][k] * w;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = g * 16 + i;
+      if (row0 + r < R) z2o[(long)(row0 + r) * HU + j] = acc[i];
+      sa2[r][j] = leaky(acc[i], alpha2);
+    }
+    __syncthreads();
+    // output unit: wave g reduces its 16 rows; lane i < 16 keeps row g*16+i
+    const float w3 = W3[j];
+    float zr = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = wave_sum(sa2[g * 16 + i][j] * w3);
+      if (j == i) zr = v;
+    }
+    if (j < 16) {
+      const int row = row0 + g * 16 + j;
+      if (row < R) {
+        const float z = zr + b3[0];
+        logits[row] = z;
+        const float yy = y[row], m = mask[row];
+        const float l = fmaxf(z, 0.f) - z * yy + log1pf(__expf(-fabsf(z)));
+        const float wc = yy > 0.5f ? w1 : w0;
+        m_loss += m * wc * l;
+        m_n += m;
+        const float p = sigmoidf_fast(z);
+        const bool pos = yy > 0.5f, pp = p > 0.5f;
+        m_tp += (pp && pos) ? m : 0.f;
+        m_tn += (!pp && !pos) ? m : 0.f;
+        m_fp += (pp && !pos) ? m : 0.f;
+        m_fn += (!pp && pos) ? m : 0.f;
+        if (hist != nullptr && m != 0.f) {
+          int b = (int)rintf(fminf(fmaxf(p, 0.f), 1.f) * (float)(bins - 1));
+          b = b < 0 ? 0 : (b >= bins ? bins - 1 : b);
+          atomicAdd(&hist[(pos ? bins : 0) + b], m);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // block reduction of the loss / metric partials (lanes >= 16 hold zeros)
+  float v[6] = {m_loss, m_n, m_tp, m_tn, m_fp, m_fn};
+#pragma unroll
+  for (int q = 0; q < 6; ++q) v[q] = wave_sum(v[q]);
+  if (j == 0) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) mred[g][q] = v[q];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float t[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) t[q] = mred[0][q] + mred[1][q] + mred[2][q] + mred[3][q];
+    atomicAdd(&aux[0], t[0] * inv);
+    if (sums != nullptr) {
+      for (int q = 0; q < 6; ++q) atomicAdd(&sums[q], (double)t[q]);
+    }
+  }
+}
+
+// Backward. gout: device scalar dL/dloss; aux[1]: mask sum from the forward.
+template <int F>
+__global__ __launch_bounds__(256) void head_bwd_kernel(
+    const float* __restrict__ feat, int ldf, const float* __restrict__ W1, const float* __restrict__ W2,
+    const float* __restrict__ W3, const float* __restrict__ z1, const float* __restrict__ z2,
+    const float* __restrict__ logits, const float* __restrict__ y, const float* __restrict__ mask, int R,
+    float alpha1, float alpha2, float w0, float w1, const float* __restrict__ gout, const float* __restrict__ aux,
+    float* __restrict__ dfeat, int ldd, float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ dW2,
+    float* __restrict__ db2, float* __restrict__ dW3, float* __restrict__ db3) {
+  constexpr int KPT = F / 4;            // dW1 rows per thread
+  constexpr int RPT = HT * F / 256;     // dfeat rows per thread
+  __shared__ float sf[HT][F + 4];
+  __shared__ float sW1[F][HU + 1];
+  __shared__ float sW2[HU][HU + 1];
+  __shared__ float sa1[HT][HU + 4];      // a1 = leaky(z1)
+  __shared__ float sz1[HT][HU + 4];      // z1, then dz1
+  __shared__ float sz2[HT][HU + 4];      // z2, then dz2
+  __shared__ float sdz3[HT];
+  __shared__ float red[4][HU + 1];
+  const int tid = threadIdx.x, j = tid & 63, g = tid >> 6;
+  const float scale = gout[0] / fmaxf(aux[1], 1.f);
+  for (int e = tid; e < F * HU; e += 256) sW1[e / HU][e % HU] = W1[e];
+  for (int e = tid; e < HU * HU; e += 256) sW2[e / HU][e % HU] = W2[e];
+  const float w3j = W3[j];
+  float aW1[KPT], aW2[16], aW3 = 0.f, ab1 = 0.f, ab2 = 0.f, ab3 = 0.f;
+#pragma unroll
+  for (int q = 0; q < KPT; ++q) aW1[q] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) aW2[q] = 0.f;
+  const int ntiles = (R + HT - 1) / HT;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row0 = tile * HT;
+    for (int e = tid; e < HT * (F / 4); e += 256) {
+      const int r = e / (F / 4), c4 = e % (F / 4);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row0 + r < R) v = *reinterpret_cast<const float4*>(feat + (long)(row0 + r) * ldf + 4 * c4);
+      *reinterpret_cast<float4*>(&sf[r][4 * c4]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = g * 16 + i, row = row0 + r;
+      const float a = row < R ? z1[(long)row * HU + j] : 0.f;
+      const float b = row < R ? z2[(long)row * HU + j] : 0.f;
+      sz1[r][j] = a;
+      sa1[r][j] = leaky(a, alpha1);
+      sz2[r][j] = b;
+    }
+    if (tid < HT) {
+      const int row = row0 + tid;
+      float d = 0.f;
+      if (row < R) {
+        const float yy = y[row];
+        const float wc = yy > 0.5f ? w1 : w0;
+        d = scale * mask[row] * wc * (sigmoidf_fast(logits[row]) - yy);
+      }
+      sdz3[tid] = d;
+      ab3 += d;
+    }
+    __syncthreads();
+    // dW3 / db... and dz2 = dz3 * W3 * leaky'(z2) (in place)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = g * 16 + i;
+      const float z = sz2[r][j], d3 = sdz3[r];
+      aW3 += leaky(z, alpha2) * d3;
+      sz2[r][j] = d3 * w3j * dleaky(z, alpha2);
+    }
+    __syncthreads();
+    // dW2[i][j] = sum_r a1[r][i] dz2[r][j] ; db2 ; da1 -> dz1
+    #pragma unroll 4
+    for (int r = 0; r < HT; ++r) {
+      const float d = sz2[r][j];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) aW2[q] += sa1[r][g * 16 + q] * d;
+      if (g == 0) ab2 += d;
+    }
+    float da[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) da[q] = 0.f;
+    // thread owns unit i = j of rows g*16..: da1[r][i] = sum_k dz2[r][k] W2[i][k]
+    #pragma unroll 4
+    for (int k = 0; k < HU; ++k) {
+      const float w = sW2[j][k];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) da[q] += sz2[g * 16 + q][k] * w;
+    }
+    __syncthreads();     // all reads of sz1 (raw z1) by other threads are per-owner: safe, but sz2 reads end here
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = g * 16 + q;
+      sz1[r][j] = da[q] * dleaky(sz1[r][j], alpha1);
+    }
+    __syncthreads();
+    // dW1[k][j] = sum_r feat[r][k] dz1[r][j] ; db1
+    #pragma unroll 4
+    for (int r = 0; r < HT; ++r) {
+      const float d = sz1[r][j];
+#pragma unroll
+      for (int q = 0; q < KPT; ++q) aW1[q] += sf[r][g * KPT + q] * d;
+      if (g == 0) ab1 += d;
+    }
+    // dfeat[r][k] = sum_j dz1[r][j] W1[k][j]
+    if (dfeat != nullptr) {
+      const int k = tid % F, rg = tid / F;
+      float o[RPT];
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) o[q] = 0.f;
+      #pragma unroll 4
+      for (int jj = 0; jj < HU; ++jj) {
+        const float w = sW1[k][jj];
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) o[q] += sz1[rg * RPT + q][jj] * w;
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        const int row = row0 + rg * RPT + q;
+        if (row < R) dfeat[(long)row * ldd + k] = o[q];
+      }
+    }
+    __syncthreads();
+  }
+  // flush: coalesced atomics (lanes = consecutive j)
+#pragma unroll
+  for (int q = 0; q < KPT; ++q) atomicAdd(&dW1[(g * KPT + q) * HU + j], aW1[q]);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) atomicAdd(&dW2[(g * 16 + q) * HU + j], aW2[q]);
+  red[g][j] = aW3;
+  __syncthreads();
+  if (g == 0) {
+    atomicAdd(&dW3[j], red[0][j] + red[1][j] + red[2][j] + red[3][j]);
+    atomicAdd(&db1[j], ab1);
+    atomicAdd(&db2[j], ab2);
+    const float s3 = wave_sum(ab3);
+    if (j == 0) atomicAdd(&db3[0], s3);
+  }
+}
+
+static int head_grid(int R) {
+  const int nt = (R + HT - 1) / HT;
+  return std::max(1, std::min(nt, 256));
+}
+
+#define GQ_HEAD_F_DISPATCH(F_, ...)                                 \
+  switch (F_) {                                                      \
+    case 32: { constexpr int FF = 32; __VA_ARGS__; break; }          \
+    case 64: { constexpr int FF = 64; __VA_ARGS__; break; }          \
+    case 128: { constexpr int FF = 128; __VA_ARGS__; break; }        \
+    default: TORCH_CHECK(false, "gnnqc head: feature width must be 32, 64 or 128, got ", F_); \
+  }
+
+// returns [z1 (R,64), z2 (R,64), logits (R), aux (2): loss, mask-sum]
+std::vector<at::Tensor> head_fwd(const at::Tensor& feat, const at::Tensor& W1, const at::Tensor& b1,
+                                 const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& W3,
+                                 const at::Tensor& b3, const at::Tensor& y, const at::Tensor& mask, double alpha1,
+                                 double alpha2, double w0, double w1, at::Tensor sums, at::Tensor hist) {
+  TORCH_CHECK(feat.is_cuda() && feat.scalar_type() == at::kFloat && feat.dim() == 2 && feat.stride(1) == 1,
+              "gnnqc head: feat must be a float32 GPU matrix with unit inner stride");
+  const int R = (int)feat.size(0), F = (int)feat.size(1);
+  TORCH_CHECK(feat.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(feat.data_ptr()) % 16 == 0,
+              "gnnqc head: feat rows must be 16-byte aligned");
+  const at::Tensor* ops[] = {&W1, &b1, &W2, &b2, &W3, &b3, &y, &mask};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "head operand");
+  TORCH_CHECK(W1.size(0) == F && W1.size(1) == HU && W2.size(0) == HU && W2.size(1) == HU &&
+                  W3.numel() == HU && b1.numel() == HU && b2.numel() == HU && b3.numel() == 1,
+              "gnnqc head: expected Dense(F,64)-Dense(64,64)-Dense(64,1)");
+  TORCH_CHECK(y.numel() == R && mask.numel() == R, "gnnqc head: y/mask must have one entry per row");
+  double* sp = nullptr;
+  float* hp = nullptr;
+  int bins = 2;
+  if (sums.numel() > 0) {
+    TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.numel() == 6, "sums: 6 float64");
+    sp = sums.data_ptr<double>();
+  }
+  if (hist.numel() > 0) {
+    check_f32_cuda(hist, "hist");
+    TORCH_CHECK(hist.dim() == 2 && hist.size(0) == 2, "hist must be [2, bins]");
+    hp = hist.data_ptr<float>();
+    bins = (int)hist.size(1);
+  }
+  c10::DeviceGuard guard(feat.device());
+  auto opt = feat.options();
+  at::Tensor z1 = at::empty({R, HU}, opt), z2 = at::empty({R, HU}, opt), lo = at::empty({R}, opt);
+  at::Tensor aux = at::zeros({2}, opt);
+  const int grid = head_grid(R);
+  GQ_HEAD_F_DISPATCH(F, hipLaunchKernelGGL(head_fwd_kernel<FF>, dim3(grid), dim3(256), 0, stream(),
+                                           feat.data_ptr<float>(), (int)feat.stride(0), W1.data_ptr<float>(),
+                                           b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
+                                           W3.data_ptr<float>(), b3.data_ptr<float>(), y.data_ptr<float>(),
+                                           mask.data_ptr<float>(), R, (float)alpha1, (float)alpha2, (float)w0,
+                                           (float)w1, z1.data_ptr<float>(), z2.data_ptr<float>(),
+                                           lo.data_ptr<float>(), aux.data_ptr<float>(), sp, hp, bins));
+  GQ_LAUNCH_CHECK();
+  return {z1, z2, lo, aux};
+}
+
+// Accumulates into dW1..db3 (which may be the optimiser's gradient views); returns dfeat.
+at::Tensor head_bwd(const at::Tensor& feat, const at::Tensor& W1, const at::Tensor& W2, const at::Tensor& W3,
+                    const at::Tensor& z1, const at::Tensor& z2, const at::Tensor& logits, const at::Tensor& y,
+                    const at::Tensor& mask, double alpha1, double alpha2, double w0, double w1, const at::Tensor& gout,
+                    const at::Tensor& aux, at::Tensor dW1, at::Tensor db1, at::Tensor dW2, at::Tensor db2,
+                    at::Tensor dW3, at::Tensor db3, bool need_dfeat) {
+  const int R = (int)feat.size(0), F = (int)feat.size(1);
+  TORCH_CHECK(feat.stride(1) == 1 && feat.stride(0) % 4 == 0, "gnnqc head_bwd: feat layout");
+  const at::Tensor* ops[] = {&W1, &W2, &W3, &z1, &z2, &logits, &y, &mask, &gout, &aux, &dW1, &db1, &dW2, &db2,
+                             &dW3, &db3};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "head_bwd operand");
+  TORCH_CHECK(z1.size(0) == R && z2.size(0) == R && logits.numel() == R, "gnnqc head_bwd: saved tensor rows");
+  TORCH_CHECK(dW1.numel() == (long)F * HU && dW2.numel() == HU * HU && dW3.numel() == HU && db1.numel() == HU &&
+                  db2.numel() == HU && db3.numel() == 1, "gnnqc head_bwd: gradient shapes");
+  c10::DeviceGuard guard(feat.device());
+  at::Tensor dfeat = need_dfeat ? at::empty({R, F}, feat.options()) : at::empty({0}, feat.options());
+  const int grid = head_grid(R);
+  GQ_HEAD_F_DISPATCH(F, hipLaunchKernelGGL(head_bwd_kernel<FF>, dim3(grid), dim3(256), 0, stream(),
+                                           feat.data_ptr<float>(), (int)feat.stride(0), W1.data_ptr<float>(),
+                                           W2.data_ptr<float>(), W3.data_ptr<float>(), z1.data_ptr<float>(),
+                                           z2.data_ptr<float>(), logits.data_ptr<float>(), y.data_ptr<float>(),
+                                           mask.data_ptr<float>(), R, (float)alpha1, (float)alpha2, (float)w0,
+                                           (float)w1, gout.data_ptr<float>(), aux.data_ptr<float>(),
+                                           need_dfeat ? dfeat.data_ptr<float>() : nullptr, F,
+                                           dW1.data_ptr<float>(), db1.data_ptr<float>(), dW2.data_ptr<float>(),
+                                           db2.data_ptr<float>(), dW3.data_ptr<float>(), db3.data_ptr<float>()));
+  GQ_LAUNCH_CHECK();
+  return dfeat;
+}
+
+}  // namespace gq
+
+TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("head_fwd", &gq::head_fwd);
+  m.impl("head_bwd", &gq::head_bwd);
+}

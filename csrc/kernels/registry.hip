@@ -24,6 +24,15 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("nonfinite_count(Tensor x) -> Tensor");
   // metrics (metrics.hip)
   m.def("score_histogram(Tensor scores, Tensor labels, Tensor mask, int bins) -> Tensor");
+  // fused dense head + weighted BCE + metrics (head.hip)
+  m.def("head_fwd(Tensor feat, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y, "
+        "Tensor mask, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");
+  m.def("head_bwd(Tensor feat, Tensor W1, Tensor W2, Tensor W3, Tensor z1, Tensor z2, Tensor logits, Tensor y, "
+        "Tensor mask, float alpha1, float alpha2, float w0, float w1, Tensor gout, Tensor aux, Tensor(a!) dW1, "
+        "Tensor(b!) db1, Tensor(c!) dW2, Tensor(d!) db2, Tensor(e!) dW3, Tensor(f!) db3, bool need_dfeat) -> Tensor");
+  // MaxPooling1D with byte argmax (pool.hip)
+  m.def("maxpool1d_fwd(Tensor x, int p) -> Tensor[]");
+  m.def("maxpool1d_bwd(Tensor dy, Tensor idx, int T, int p) -> Tensor");
   // window gather (gather.hip)
   m.def("window_gather(Tensor series, Tensor shift, Tensor scale, Tensor win_group, Tensor win_center, "
         "Tensor win_valid, Tensor wids, int tb, int seq_len, bool time_norm) -> Tensor");

@@ -64,6 +64,16 @@ class BaselineClassifier(nn.Module):
         d = self.dropout2(self.leakyrelu5(self.dense2(d)))
         return self.dense_out(d).squeeze(-1)
 
+    def features(self, inputs) -> torch.Tensor:
+        return self.time_layer(self.temporal_input(inputs))
+
+    def head_spec(self):
+        if self.training and (self.dropout1.rate > 0 or self.dropout2.rate > 0):
+            return None
+        if any(d.activation not in (None, "linear") for d in (self.dense1, self.dense2, self.dense_out)):
+            return None
+        return self.dense1, self.dense2, self.dense_out, self.leakyrelu4.alpha, self.leakyrelu5.alpha
+
     def logits(self, inputs) -> torch.Tensor:
         z = self.head(self.time_layer(self.temporal_input(inputs)))
         if self.ds_type == "soilnet":

@@ -161,6 +161,19 @@ class GCNClassifier(nn.Module):
         d = self.leakyrelu5(self.dense2(d))
         return self.dense_out(d).squeeze(-1)
 
+    def features(self, inputs) -> torch.Tensor:
+        """TimeLayer output rows [R, F] (CML: R = B; SoilNet: R = B*N) - the head's input."""
+        return self.time_layer(self.temporal_input(inputs))
+
+    def head_spec(self):
+        """(dense, dense2, dense_out, alpha1, alpha2) when the head is the plain
+        Dense-LeakyReLU-Dense-LeakyReLU-Dense stack the fused HIP kernel implements."""
+        if self.training and (self.dropout1.rate > 0 or self.dropout2.rate > 0):
+            return None
+        if any(d.activation not in (None, "linear") for d in (self.dense, self.dense2, self.dense_out)):
+            return None
+        return self.dense, self.dense2, self.dense_out, self.leakyrelu4.alpha, self.leakyrelu5.alpha
+
     def logits(self, inputs) -> torch.Tensor:
         z = self.head(self.time_layer(self.temporal_input(inputs)))
         if self.ds_type == "soilnet":

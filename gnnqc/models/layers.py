@@ -157,10 +157,8 @@ class MaxPooling1D(nn.Module):
         self.pool_size = int(pool_size)
 
     def forward(self, x):                           # [M, T, C], valid padding, stride = pool
-        p = self.pool_size
-        T = x.shape[1] // p * p
-        M, _, C = x.shape
-        return x[:, :T].reshape(M, T // p, p, C).amax(2)
+        from ..ops.pool import max_pool1d
+        return max_pool1d(x, self.pool_size)
 
 
 class GlobalAveragePooling1D(nn.Module):

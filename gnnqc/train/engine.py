@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from ..eval import metrics as M
+from ..ops.head import fused_head_loss
 from ..ops.lstm import direct_grad_accumulation
 from ..ops.metrics import score_histogram
 from ..parallel import dist as D
@@ -39,16 +40,22 @@ class MetricAccumulator:
 
     @torch.no_grad()
     def update(self, loss, logits, y, mask):
-        p = torch.sigmoid(logits.float())
-        m = mask.float()
+        self.update_buffers(self.sums, self.hist, loss, logits, y, mask)
+
+    @staticmethod
+    @torch.no_grad()
+    def update_buffers(sums, hist, loss, logits, y, mask):
+        p = torch.sigmoid(logits.float()).reshape(-1)
+        m = mask.float().reshape(-1)
         n = m.sum()
         pred = (p > 0.5).float()
-        yy = (y > 0.5).float()
+        yy = (y.reshape(-1) > 0.5).float()
         vals = torch.stack([loss.detach().double() * n.double(), n.double(), (pred * yy * m).sum().double(),
                             ((1 - pred) * (1 - yy) * m).sum().double(), (pred * (1 - yy) * m).sum().double(),
                             ((1 - pred) * yy * m).sum().double()])
-        self.sums.add_(vals)
-        self.hist.add_(score_histogram(p, yy, m, HIST_BINS))
+        sums.add_(vals)
+        if hist is not None:
+            hist.add_(score_histogram(p, yy, m, hist.shape[1]))
 
     def result(self, prefix: str = "") -> Dict[str, float]:
         sums = self.sums.clone()
@@ -82,20 +89,31 @@ class Trainer:
         self.last_loss = torch.zeros((), device=self.device)
 
     # ---------------------------------------------------------------- body
-    def _loss(self, wids):
+    def _loss(self, wids, metrics: Optional["MetricAccumulator"] = None):
+        """(total, loss, logits, batch). With a fused-head model the loss, logits and
+        the metric update come out of one HIP kernel (``gnnqc.ops.head``)."""
         b = self.store.gather(wids)
-        z = self.model.logits(b.model_inputs(self.ds_type, self.baseline))
-        loss = weighted_bce_with_logits(z, b.y, b.y_mask, self.w0, self.w1)
+        inputs = b.model_inputs(self.ds_type, self.baseline)
+        spec = self.model.head_spec() if hasattr(self.model, "head_spec") else None
+        if spec is not None:
+            dense, dense2, dense_out, a1, a2 = spec
+            loss, z = fused_head_loss(self.model.features(inputs), dense, dense2, dense_out, a1, a2, b.y, b.y_mask,
+                                      self.w0, self.w1, metrics.sums if metrics else None,
+                                      metrics.hist if metrics else None)
+        else:
+            z = self.model.logits(inputs)
+            loss = weighted_bce_with_logits(z, b.y, b.y_mask, self.w0, self.w1)
+            if metrics is not None:
+                metrics.update(loss, z, b.y, b.y_mask)
         reg = self.model.regularization_loss() if hasattr(self.model, "regularization_loss") else None
         total = loss + reg if reg is not None else loss
         return total, loss, z, b
 
     def _body(self, wids, with_opt: bool):
         self.opt.zero_grad()
-        total, loss, z, b = self._loss(wids)
+        total, loss, z, b = self._loss(wids, self.train_metrics)
         with direct_grad_accumulation(True):
             total.backward()
-        self.train_metrics.update(loss, z, b.y, b.y_mask)
         self.last_loss.copy_(loss.detach())
         if with_opt:
             self.opt.step(grad_scale=1.0)
@@ -152,10 +170,7 @@ class Trainer:
         acc = MetricAccumulator(self.device)
         self.model.eval()
         for row in loader.batch_ids():
-            b = self.store.gather(row)
-            z = self.model.logits(b.model_inputs(self.ds_type, self.baseline))
-            loss = weighted_bce_with_logits(z, b.y, b.y_mask, self.w0, self.w1)
-            acc.update(loss, z, b.y, b.y_mask)
+            self._loss(row, acc)
         self.model.train()
         return acc.result(prefix)
 

@@ -190,3 +190,88 @@ def test_graph_captured_train_step_learns(cuda_device, cml_windows):
     first = sum(losses[:5]) / 5
     last = sum(losses[-5:]) / 5
     assert last < first, (first, last)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Fdim,R", [(128, 128), (64, 5), (32, 700), (128, 20000)])
+def test_fused_head_loss_matches_eager(cuda_device, Fdim, R):
+    """head_fwd/head_bwd vs the fp32 PyTorch head + weighted BCE + metric updates."""
+    from gnnqc.models.layers import Dense
+    from gnnqc.ops.head import fused_head_loss, head_eager
+    from gnnqc.train.engine import HIST_BINS, MetricAccumulator
+    from gnnqc.train.loss import weighted_bce_with_logits
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(Fdim + R)
+    layers = [Dense(Fdim, 64), Dense(64, 64), Dense(64, 1)]
+    for d in layers:
+        d.to(dev)
+        with torch.no_grad():
+            d.bias.normal_(0, 0.1)
+    feat = (torch.randn(R, Fdim, generator=gen) * 0.7).to(dev).requires_grad_(True)
+    y = (torch.rand(R, generator=gen) < 0.3).float().to(dev)
+    mask = (torch.rand(R, generator=gen) < 0.9).float().to(dev)
+    acc = MetricAccumulator(dev)
+    loss, z = fused_head_loss(feat, *layers, 0.3, 0.3, y, mask, 1.0, 5.0, acc.sums, acc.hist)
+    loss.backward()
+    g_fused = [feat.grad.clone()] + [p.grad.clone() for d in layers for p in (d.kernel, d.bias)]
+    feat.grad = None
+    for d in layers:
+        d.kernel.grad = d.bias.grad = None
+    ref = MetricAccumulator(dev)
+    zr = head_eager(feat, layers[0].kernel, layers[0].bias, layers[1].kernel, layers[1].bias, layers[2].kernel,
+                    layers[2].bias, 0.3, 0.3)
+    lr = weighted_bce_with_logits(zr, y, mask, 1.0, 5.0)
+    lr.backward()
+    ref.update(lr, zr, y, mask)
+    g_ref = [feat.grad] + [p.grad for d in layers for p in (d.kernel, d.bias)]
+    torch.testing.assert_close(z, zr.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(loss, lr.detach(), atol=1e-5, rtol=1e-4)
+    for a, b in zip(g_fused, g_ref):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=2e-3)
+    torch.testing.assert_close(acc.sums, ref.sums, atol=1e-3, rtol=1e-5)
+    # histogram bins may differ by one where sigmoid implementations round differently
+    assert float((acc.hist - ref.hist).abs().sum()) <= 0.002 * float(mask.sum()) + 2
+    assert acc.hist.shape == (2, HIST_BINS)
+
+
+@pytest.mark.gpu
+def test_fused_head_direct_grad_accumulation(cuda_device):
+    """In direct mode the head gradients land in the flat optimiser buffer (views)."""
+    from gnnqc.models.layers import Dense
+    from gnnqc.ops.head import fused_head_loss
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    from gnnqc.ops.optim import FlatAdam
+    dev = cuda_device
+    layers = torch.nn.ModuleList([Dense(128, 64), Dense(64, 64), Dense(64, 1)]).to(dev)
+    opt = FlatAdam(layers.parameters())
+    feat = torch.randn(256, 128, device=dev)
+    y = (torch.rand(256, device=dev) < 0.2).float()
+    mask = torch.ones(256, device=dev)
+    opt.zero_grad()
+    loss, _ = fused_head_loss(feat, *layers, 0.3, 0.3, y, mask, 1.0, 5.0)
+    with direct_grad_accumulation(True):
+        loss.backward()
+    direct = opt.flat_g.clone()
+    opt.zero_grad()
+    loss, _ = fused_head_loss(feat, *layers, 0.3, 0.3, y, mask, 1.0, 5.0)
+    loss.backward()
+    opt.relink_grads()
+    torch.testing.assert_close(direct, opt.flat_g, atol=1e-6, rtol=1e-5)
+    assert float(direct.abs().sum()) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,T,C,p", [(50, 181, 16, 3), (7, 60, 32, 3), (3, 22, 128, 2), (5, 10, 64, 4)])
+def test_maxpool1d_matches_eager(cuda_device, M, T, C, p):
+    from gnnqc.ops.pool import max_pool1d
+    gen = torch.Generator().manual_seed(M * T + C)
+    x = torch.randn(M, T, C, generator=gen).to(cuda_device).requires_grad_(True)
+    y = max_pool1d(x, p)
+    g = torch.randn(y.shape, generator=gen).to(cuda_device)
+    (y * g).sum().backward()
+    xr = x.detach().clone().requires_grad_(True)
+    To = T // p
+    yr = xr[:, :To * p].reshape(M, To, p, C).max(2).values
+    (yr * g).sum().backward()
+    torch.testing.assert_close(y, yr, rtol=0, atol=0)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=0, atol=0)
