@@ -28,6 +28,27 @@ constexpr int HU = 64;     // dense units (model_config dense.units)
 __device__ __forceinline__ float leaky(float z, float a) { return z > 0.f ? z : a * z; }
 __device__ __forceinline__ float dleaky(float z, float a) { return z > 0.f ? 1.f : a; }
 
+// Copy N floats (N % 1024 == 0) global -> LDS rows of pitch P: every thread issues all of
+// its float4 loads before the first LDS store, so the copy costs one memory latency.
+template <int N, int COLS, int P>
+__device__ __forceinline__ void stage_lds(float* __restrict__ dst, const float* __restrict__ src) {
+  constexpr int PER = N / 4 / 256;
+  static_assert(N % 1024 == 0 && COLS % 4 == 0, "stage_lds shape");
+  float4 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] = reinterpret_cast<const float4*>(src)[threadIdx.x + 256 * i];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = 4 * (threadIdx.x + 256 * i), r = e / COLS, c = e % COLS;
+    float* d = dst + r * P + c;
+    if constexpr (P % 4 == 0) {
+      *reinterpret_cast<float4*>(d) = v[i];
+    } else {
+      d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
+    }
+  }
+}
+
 // mask sum over all rows (every block recomputes it: no cross-block dependency)
 __device__ float block_mask_sum(const float* __restrict__ mask, int R, float* red) {
   float s = 0.f;
@@ -51,11 +72,16 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     float* __restrict__ logits, float* __restrict__ aux, double* __restrict__ sums, float* __restrict__ hist,
     int bins) {
   __shared__ float sf[HT][F + 4];
+  __shared__ float sW1[F][HU];
+  __shared__ float sW2[HU][HU];
   __shared__ float sa1[HT][HU + 4];
   __shared__ float sa2[HT][HU + 4];
   __shared__ float red[4];
   __shared__ float mred[4][8];
   const int tid = threadIdx.x, j = tid & 63, g = tid >> 6;
+  stage_lds<F * HU, HU, HU>(&sW1[0][0], W1);
+  stage_lds<HU * HU, HU, HU>(&sW2[0][0], W2);
+  const float bj1 = b1[j], bj2 = b2[j], w3 = W3[j], b3v = b3[0];
   const float nm = block_mask_sum(mask, R, red);
   const float inv = 1.f / fmaxf(nm, 1.f);
   if (blockIdx.x == 0 && tid == 0) aux[1] = nm;
@@ -105,7 +131,6 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     }
     __syncthreads();
     // output unit: wave g reduces its 16 rows; lane i < 16 keeps row g*16+i
-    const float w3 = W3[j];
     float zr = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -115,7 +140,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     if (j < 16) {
       const int row = row0 + g * 16 + j;
       if (row < R) {
-        const float z = zr + b3[0];
+        const float z = zr + b3v;
         logits[row] = z;
         const float yy = y[row], m = mask[row];
         const float l = fmaxf(z, 0.f) - z * yy + log1pf(__expf(-fabsf(z)));
@@ -178,8 +203,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   __shared__ float red[4][HU + 1];
   const int tid = threadIdx.x, j = tid & 63, g = tid >> 6;
   const float scale = gout[0] / fmaxf(aux[1], 1.f);
-  for (int e = tid; e < F * HU; e += 256) sW1[e / HU][e % HU] = W1[e];
-  for (int e = tid; e < HU * HU; e += 256) sW2[e / HU][e % HU] = W2[e];
+  stage_lds<F * HU, HU, HU + 1>(&sW1[0][0], W1);
+  stage_lds<HU * HU, HU, HU + 1>(&sW2[0][0], W2);
   const float w3j = W3[j];
   float aW1[KPT], aW2[16], aW3 = 0.f, ab1 = 0.f, ab2 = 0.f, ab3 = 0.f;
 #pragma unroll

@@ -18,6 +18,12 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor alpha, int c_off) -> Tensor");
   m.def("gcn_pool_bwd_input(Tensor x, Tensor w, Tensor mask, Tensor dout, Tensor W, Tensor b, Tensor scale, "
         "Tensor shift, Tensor alpha, Tensor dzcoef, int c_off) -> Tensor");
+  // GCN glue: pooling weights, BN statistics, closed-form backward (gcn_glue.hip)
+  m.def("gcn_pool_weights(Tensor adj, Tensor mask, Tensor anom_pos, bool agg_mean, int pool) -> Tensor");
+  m.def("gcn_bn_prep(Tensor S, Tensor W, Tensor b, Tensor gamma, Tensor beta, Tensor(a!) rmean, Tensor(b!) rvar, "
+        "bool training, float momentum, float eps) -> Tensor");
+  m.def("gcn_bwd_finalize(Tensor acc, Tensor S, Tensor W, Tensor b, Tensor st, bool training, Tensor(a!) dW, "
+        "Tensor(b!) db, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) dalpha) -> Tensor");
   // flat-buffer optimiser (adam.hip)
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
         "float beta2, float eps, float grad_scale, float weight_decay) -> ()");

@@ -95,80 +95,54 @@ def general_conv_eager(x, adj, mask, W, b, gamma, beta, running_mean, running_va
 
 
 class _HipGCNPool(torch.autograd.Function):
-    """Fused stats -> affine/BN/PReLU -> weighted node sum -> concat (HIP)."""
+    """Fused stats -> affine/BN/PReLU -> weighted node sum -> concat (HIP).
+
+    Launches per training step: gcn_stats, gcn_bn_prep, gcn_pool_fwd forward;
+    gcn_pool_bwd, gcn_bwd_finalize (+ gcn_pool_bwd_input when dx is needed)
+    backward. Weight gradients go straight into the optimiser's flat buffer when
+    direct accumulation is on (see ``gnnqc.ops.lstm.direct_grad_accumulation``)."""
 
     @staticmethod
     def forward(ctx, x, w, mask, anom, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
                 momentum: float, eps: float):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        Cin = x.shape[-1]
-        if training:
-            S = ops.gcn_stats(x, mask)
-            cnt = S[-1].clamp(min=1.0)
-            S1 = S[:Cin]
-            S2 = S[Cin:Cin + Cin * Cin].view(Cin, Cin)
-            ex = S1 / cnt
-            cov = S2 / cnt - torch.outer(ex, ex)
-            Wd = W.double()
-            mu = (ex @ Wd + b.double()).float()
-            var = torch.einsum("kf,kl,lf->f", Wd, cov, Wd).clamp(min=0).float()
-            with torch.no_grad():
-                running_mean.mul_(momentum).add_(mu * (1 - momentum))
-                running_var.mul_(momentum).add_(var * (1 - momentum))
-        else:
-            mu, var = running_mean, running_var
-            S1 = S2 = cnt = None
-        invstd = torch.rsqrt(var + eps)
-        scale = (gamma * invstd).contiguous()
-        shift = (beta - mu * scale).contiguous()
+        S = ops.gcn_stats(x, mask) if training else x.new_zeros(0, dtype=torch.float64)
+        st = ops.gcn_bn_prep(S, W.contiguous(), b.contiguous(), gamma.contiguous(), beta.contiguous(),
+                             running_mean, running_var, bool(training), float(momentum), float(eps))
         anom_t = anom.contiguous() if anom is not None else x.new_zeros(0)
-        out = ops.gcn_pool_fwd(x, w, anom_t, W.contiguous(), b.contiguous(), scale, shift, alpha.contiguous())
+        out = ops.gcn_pool_fwd(x, w, anom_t, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous())
         ctx.training = training
         ctx.ca = 0 if anom is None else anom.shape[-1]
         ctx.has_anom = anom is not None
-        stats = (S1.float(), S2.float(), cnt.float().reshape(1)) if training else (x.new_zeros(0),) * 3
-        ctx.save_for_backward(x, w, mask, W, b, gamma, alpha, mu, invstd, scale, shift, *stats)
+        ctx.params = (W, b, gamma, beta, alpha)
+        ctx.save_for_backward(x, w, mask, W, b, alpha, st, S)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
+        from .lstm import _grad_sink
         ops = hip_ops()
-        (x, w, mask, W, b, gamma, alpha, mu, invstd, scale, shift, S1, S2, cnt) = ctx.saved_tensors
+        x, w, mask, W, b, alpha, st, S = ctx.saved_tensors
         dout = dout.contiguous()
-        Cin = x.shape[-1]
-        need_w = any(ctx.needs_input_grad[4:9])
-        dW = db = dgamma = dbeta = dalpha = None
+        need = ctx.needs_input_grad
+        need_w = any(need[4:9])
+        empty = x.new_zeros(0)
+        acc = empty
         if ctx.training or need_w:
-            acc = ops.gcn_pool_bwd(x, w, dout, W.contiguous(), b.contiguous(), scale, shift, alpha.contiguous(),
+            acc = ops.gcn_pool_bwd(x, w, dout, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous(),
                                    ctx.ca)
-            A, Z, P, Q = acc[0], acc[1], acc[2], acc[3:3 + Cin]
-            dbeta = A
-            dgamma = invstd * (Z - mu * A)
-            dalpha = P
-        if ctx.training:
-            n = cnt[0]
-            sxx = invstd * (S2 @ W + torch.outer(S1, b - mu))       # sum_rows x_k * xhat_f
-            dW = scale * (Q - torch.outer(S1, A / n) - sxx * (dgamma / n))
-            db = torch.zeros_like(b)
-            c0 = scale * (-A / n + mu * invstd * dgamma / n)
-            c2 = -scale * invstd * dgamma / n
-        else:
-            # inference-mode BN is a fixed affine map (e.g. integrated gradients: frozen weights,
-            # input gradients only -> no weight-gradient reduction at all)
-            if need_w:
-                dW = scale * Q
-                db = scale * A
-            c0 = torch.zeros_like(scale)
-            c2 = torch.zeros_like(scale)
+        sinks = [(_grad_sink(p) if n else (empty, True)) for p, n in zip(ctx.params, need[4:9])]
+        coef = ops.gcn_bwd_finalize(acc, S, W.contiguous(), b.contiguous(), st, bool(ctx.training),
+                                    *[s[0] for s in sinks])
         dx = None
-        if ctx.needs_input_grad[0]:
-            coef = torch.stack([c0, scale, c2]).contiguous()
-            dx = ops.gcn_pool_bwd_input(x, w, mask, dout, W.contiguous(), b.contiguous(), scale, shift,
+        if need[0]:
+            dx = ops.gcn_pool_bwd_input(x, w, mask, dout, W.contiguous(), b.contiguous(), st[2], st[3],
                                         alpha.contiguous(), coef, ctx.ca)
-        danom = dout[..., : ctx.ca] if (ctx.has_anom and ctx.needs_input_grad[3]) else None
-        return dx, None, None, danom, dW, db, dgamma, dbeta, dalpha, None, None, None, None, None
+        danom = dout[..., : ctx.ca] if (ctx.has_anom and need[3]) else None
+        grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need[4:9])]
+        return (dx, None, None, danom, *grads, None, None, None, None, None)
 
 
 def gcn_pool(x, adj, mask, anom, anom_pos, W, b, gamma, beta, alpha, running_mean, running_var,
@@ -182,7 +156,10 @@ def gcn_pool(x, adj, mask, anom, anom_pos, W, b, gamma, beta, alpha, running_mea
     from . import use_hip
     linear = aggregate in ("mean", "sum") and pooling in ("mean", "sum", "selection")
     if use_hip(x) and linear and not (dropout and training) and x.shape[-1] <= 8 and 256 % W.shape[1] == 0:
-        w = node_pool_weights(adj, mask, anom_pos, aggregate, pooling)
+        from ..utils.native import hip_ops
+        ap = anom_pos.long().contiguous() if (pooling == "selection" and anom_pos is not None) else x.new_zeros(0)
+        w = hip_ops().gcn_pool_weights(adj.float().contiguous(), mask.float().contiguous(), ap,
+                                       aggregate == "mean", {"mean": 0, "sum": 1, "selection": 2}[pooling])
         return _HipGCNPool.apply(x.contiguous(), w, mask.contiguous().float(), anom, W, b, gamma, beta, alpha,
                                  running_mean, running_var, bool(training), float(momentum), float(eps))
     h = general_conv_eager(x, adj, mask, W, b, gamma, beta, running_mean, running_var, alpha, training,

@@ -275,3 +275,22 @@ def test_maxpool1d_matches_eager(cuda_device, M, T, C, p):
     (yr * g).sum().backward()
     torch.testing.assert_close(y, yr, rtol=0, atol=0)
     torch.testing.assert_close(x.grad, xr.grad, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("aggregate", ["mean", "sum"])
+@pytest.mark.parametrize("pooling", ["mean", "sum", "selection"])
+def test_gcn_pool_weights_matches_eager(cuda_device, aggregate, pooling):
+    from gnnqc.ops.gcn import node_pool_weights
+    from gnnqc.utils.native import hip_ops
+    gen = torch.Generator().manual_seed(7)
+    B, N = 9, 23
+    mask = (torch.rand(B, N, generator=gen) < 0.8).float()
+    adj = (torch.rand(B, N, N, generator=gen) < 0.3).float()
+    adj = ((adj + adj.transpose(1, 2) + torch.eye(N)) > 0).float() * mask[:, :, None] * mask[:, None, :]
+    ap = torch.randint(0, N, (B,), generator=gen)
+    adj, mask, ap = adj.to(cuda_device), mask.to(cuda_device), ap.to(cuda_device)
+    ref = node_pool_weights(adj, mask, ap, aggregate, pooling)
+    got = hip_ops().gcn_pool_weights(adj, mask, ap, aggregate == "mean",
+                                     {"mean": 0, "sum": 1, "selection": 2}[pooling])
+    torch.testing.assert_close(got, ref, atol=1e-6, rtol=1e-5)
