@@ -31,6 +31,7 @@
 // (bf16) crossing LDS once per step; dz (fp32) is written for the weight-gradient
 // GEMMs.
 #include "common.h"
+#include <cstdlib>
 
 namespace gq {
 
@@ -410,6 +411,16 @@ void launch_bwd(int H, const float* dh, const float* g, const float* c, const fl
   }
 }
 
+// gate-split kernels for H <= 64 (lstm_v2.hip); GNNQC_LSTM_V1=1 forces this file's kernels
+bool launch_fwd_v2(int H, bool train, int M, int T, int Din, int ldx, const float* x, const float* W, const float* U,
+                   const float* b, float* h, float* c, float* g, hipStream_t st);
+bool launch_bwd_v2(int H, int M, int T, const float* dh, const float* gates, const float* c, const float* U,
+                   float* dz, hipStream_t st);
+static bool use_v2() {
+  static const bool v = [] { const char* e = std::getenv("GNNQC_LSTM_V1"); return !(e && e[0] == '1'); }();
+  return v;
+}
+
 std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
                                  bool train, bool bf16) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be a float32 GPU tensor");
@@ -436,7 +447,8 @@ std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const
   float* hp = h.data_ptr<float>();
   float* cp = train ? c.data_ptr<float>() : nullptr;
   float* gp = train ? g.data_ptr<float>() : nullptr;
-  if (bf16) {
+  if (bf16 && use_v2() && launch_fwd_v2(H, train, M, T, Din, ldx, xp, Wp, Up, bp, hp, cp, gp, st)) {
+  } else if (bf16) {
     if (train) launch_fwd<true, true>(H, xp, Wp, Up, bp, hp, cp, gp, M, T, Din, ldx, st);
     else launch_fwd<true, false>(H, xp, Wp, Up, bp, hp, cp, gp, M, T, Din, ldx, st);
   } else {
@@ -461,7 +473,9 @@ at::Tensor lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Ten
   at::Tensor dz = at::empty({Mp, T, 4 * H}, dh.options());
   if (M == 0 || T == 0) return dz.narrow(0, 0, M);
   auto st = stream();
-  if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
+  if (bf16 && use_v2() && launch_bwd_v2(H, M, T, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(),
+                                        U.data_ptr<float>(), dz.data_ptr<float>(), st)) {
+  } else if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
   else launch_bwd<false>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
   GQ_LAUNCH_CHECK();
   return Mp == M ? dz : dz.narrow(0, 0, M);
