@@ -92,8 +92,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     // stage the feature tile (float4; rows past R are zero)
     for (int e = tid; e < HT * (F / 4); e += 256) {
       const int r = e / (F / 4), c4 = e % (F / 4);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row0 + r < R) v = *reinterpret_cast<const float4*>(feat + (long)(row0 + r) * ldf + 4 * c4);
+      // clamped row + 0/1 scale instead of a guarded load (a branch around a load makes
+      // hipcc drain vmcnt at the join)
+      const float m_ = row0 + r < R ? 1.f : 0.f;
+      float4 v = *reinterpret_cast<const float4*>(feat + (long)min(row0 + r, R - 1) * ldf + 4 * c4);
+      v.x *= m_; v.y *= m_; v.z *= m_; v.w *= m_;
       *reinterpret_cast<float4*>(&sf[r][4 * c4]) = v;
     }
     __syncthreads();
@@ -137,12 +140,14 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
       const float v = wave_sum(sa2[g * 16 + i][j] * w3);
       if (j == i) zr = v;
     }
-    if (j < 16) {
-      const int row = row0 + g * 16 + j;
-      if (row < R) {
+    {
+      const int row = row0 + g * 16 + (j & 15);
+      const int rc = min(row, R - 1);
+      const float yy_ = y[rc], m_ = mask[rc];        // loads outside any per-lane branch
+      if (j < 16 && row < R) {
         const float z = zr + b3v;
         logits[row] = z;
-        const float yy = y[row], m = mask[row];
+        const float yy = yy_, m = m_;
         const float l = fmaxf(z, 0.f) - z * yy + log1pf(__expf(-fabsf(z)));
         const float wc = yy > 0.5f ? w1 : w0;
         m_loss += m * wc * l;
@@ -216,29 +221,33 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const int row0 = tile * HT;
     for (int e = tid; e < HT * (F / 4); e += 256) {
       const int r = e / (F / 4), c4 = e % (F / 4);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row0 + r < R) v = *reinterpret_cast<const float4*>(feat + (long)(row0 + r) * ldf + 4 * c4);
+      // clamped row + 0/1 scale instead of a guarded load (a branch around a load makes
+      // hipcc drain vmcnt at the join)
+      const float m_ = row0 + r < R ? 1.f : 0.f;
+      float4 v = *reinterpret_cast<const float4*>(feat + (long)min(row0 + r, R - 1) * ldf + 4 * c4);
+      v.x *= m_; v.y *= m_; v.z *= m_; v.w *= m_;
       *reinterpret_cast<float4*>(&sf[r][4 * c4]) = v;
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int r = g * 16 + i, row = row0 + r;
-      const float a = row < R ? z1[(long)row * HU + j] : 0.f;
-      const float b = row < R ? z2[(long)row * HU + j] : 0.f;
+      const float rm = row < R ? 1.f : 0.f;
+      const float a = z1[(long)min(row, R - 1) * HU + j] * rm;
+      const float b = z2[(long)min(row, R - 1) * HU + j] * rm;
       sz1[r][j] = a;
       sa1[r][j] = leaky(a, alpha1);
       sz2[r][j] = b;
     }
-    if (tid < HT) {
-      const int row = row0 + tid;
-      float d = 0.f;
-      if (row < R) {
-        const float yy = y[row];
-        const float wc = yy > 0.5f ? w1 : w0;
-        d = scale * mask[row] * wc * (sigmoidf_fast(logits[row]) - yy);
+    {
+      const int row = row0 + (tid & (HT - 1));
+      const int rc = min(row, R - 1);
+      const float yy = y[rc];
+      const float wc = yy > 0.5f ? w1 : w0;
+      const float d = (row < R ? 1.f : 0.f) * scale * mask[rc] * wc * (sigmoidf_fast(logits[rc]) - yy);
+      if (tid < HT) {             // LDS / register only inside the branch
+        sdz3[tid] = d;
+        ab3 += d;
       }
-      sdz3[tid] = d;
-      ab3 += d;
     }
     __syncthreads();
     // dW3 / db... and dz2 = dz3 * W3 * leaky'(z2) (in place)

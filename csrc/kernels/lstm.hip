@@ -94,7 +94,7 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_fwd_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 32 * s + 8 * quad + j;
-          v[j] = (__bf16)(k < H ? U[min(k, H - 1) * G4 + g * H + ua] : 0.0f);
+          v[j] = (__bf16)(U[min(k, H - 1) * G4 + g * H + ua] * (k < H ? 1.0f : 0.0f));
         }
         ufr[g][s] = v;
       } else {
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = b_k<BF16>(s, quad, j);
-        const float v = k < Din ? W[min(k, Din - 1) * G4 + g * H + ua] : 0.0f;
+        const float v = W[min(k, Din - 1) * G4 + g * H + ua] * (k < Din ? 1.0f : 0.0f);
         if constexpr (BF16) wfr[g][s][j] = (__bf16)v;
         else wfr[g][s * 8 + j] = v;
       }

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
       for (int j = 0; j < 8; ++j) {
         const int din = dtile * 16 + col;
         const int gu = gu0 + 32 * ks + 8 * quad + j;
-        v[j] = (__bf16)((item < DXT && din < Din) ? W[(size_t)min(din, Din - 1) * G4 + gu] : 0.f);
+        v[j] = (__bf16)(W[(size_t)min(din, Din - 1) * G4 + gu] * ((item < DXT && din < Din) ? 1.f : 0.f));
       }
       wa[i][ks] = v;
     }

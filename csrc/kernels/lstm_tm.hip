@@ -1,0 +1,639 @@
+// Time-major persistent LSTM (forward + fused backward) for gfx950.
+//
+// Layout: every activation inside the TimeLayer is time-major, [T][Mp][C] with Mp a
+// multiple of 16, so the per-step tile of a 16-sequence block is ONE contiguous run of
+// 16*C floats. All global traffic in the recurrences is tile-granular and coalesced:
+//   * loader lanes stream x_t / dh_t / h_{t-1} tiles (float4/float2 granules) through a
+//     register ring and stage them into LDS one step ahead;
+//   * storer lanes write whole h_t / dx_t tiles from an fp32 LDS copy;
+//   * the training-only state (gates, c) is written and re-read in a lane-natural layout
+//     ([T][tile][wave][cell][lane]) - one 1 KiB / 256 B contiguous run per wave and step.
+// (Measured on the CML shapes, per-cell scattered accesses - 16 rows per instruction -
+// were what bound lstm_v3; see profiles/r1_lstm_microbench.md.)
+//
+// Compute mapping (as lstm_v3): the rows of the MFMA A operand are permuted so one
+// 16x16 output tile holds (unit, gate) pairs and every lane receives the i,f,g,o
+// pre-activations of its own cell(s): 5 activations per cell and lane, one LDS
+// barrier per step. H <= 64: one cell per lane, H/4 waves; H = 128: two cells per lane,
+// 16 waves.
+//
+// The backward fuses what lstm_bwd + lstm_grads did: per reverse step
+//   cell phase   dz of the lane's cells (dh = dh_out + U dz_{t+1}), dz -> LDS (bf16, both
+//                row- and column-major)
+//   MFMA phase   dh_rec = U dz^T (the serial chain), dx^T = W dz^T (tile -> HBM next step),
+//                and the weight gradients dW^T += dz^T [x_t | 1], dU^T += dz^T h_{t-1}
+//                with v_mfma_f32_16x16x16_bf16 (K = the 16 sequences of the tile), kept in
+//                VGPRs for the whole sequence and flushed once with atomics.
+// So dz never goes to HBM and no separate weight-gradient kernel runs.
+#include "common.h"
+
+namespace gq {
+
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+// A wave-uniform predicate the compiler can SEE is uniform (an SGPR): branches on it are
+// scalar, so no exec-mask join -> no conservative s_waitcnt vmcnt(0) around the loads
+// inside (measured: with threadIdx-derived predicates every step drained the load ring).
+__device__ __forceinline__ bool wave_uniform(bool p) { return __builtin_amdgcn_readfirstlane((int)p) != 0; }
+
+template <int H>
+struct TMC {
+  static constexpr int CPL = H > 64 ? H / 64 : 1;   // cells per lane
+  static constexpr int NW = H / (4 * CPL);          // waves per 16-sequence tile (<= 16)
+  static constexpr int NT = 64 * NW;
+  static constexpr int G4 = 4 * H;
+  static constexpr int KPH = ((H + 31) / 32) * 32;
+  static constexpr int KSH = KPH / 32;              // K = H steps (forward recurrent part)
+  static constexpr int KB = G4 / 32;                // K = 4H steps (backward)
+};
+
+// ---- tile streamer: granules of GR floats of one contiguous tile, wave-uniform loaders
+template <int GR>
+struct Granule {
+  float v[4];
+  __device__ __forceinline__ void load(const float* p) {
+    if constexpr (GR == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else if constexpr (GR == 2) {
+      const float2 a = *reinterpret_cast<const float2*>(p);
+      v[0] = a.x; v[1] = a.y;
+    } else {
+      v[0] = *p;
+    }
+  }
+  __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
+};
+
+// =====================================================================================
+// forward
+// x: [T][Mp][Din]  hout: [T][Mp][H]  gbuf: [T][tiles][NW][CPL][64][4]  cbuf: [..][64]
+template <int H, bool TRAIN, int KX, int GR, int D>
+__global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
+    const float* __restrict__ bias, float* __restrict__ hout, float* __restrict__ gbuf,
+    float* __restrict__ cbuf, int Mp, int T, int Din) {
+  using C = TMC<H>;
+  constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
+  constexpr int KPX = 32 * KX;
+  __shared__ __attribute__((aligned(16))) __bf16 hs[2][16][C::KPH + 8];
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
+  __shared__ __attribute__((aligned(16))) float hf[2][16][H];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in an SGPR
+  const int col = lane & 15, quad = lane >> 4;
+  const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
+
+  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += NT) (&hs[0][0][0])[i] = (__bf16)0.0f;
+  for (int i = tid; i < 2 * 16 * (KPX + 8); i += NT) (&xs[0][0][0])[i] = (__bf16)0.0f;
+
+  // A fragments: tile row `col` of cell group gi = gate (col & 3) of unit 4 gi + (col >> 2)
+  bf16x8_t ufr[CPL][C::KSH], wfr[CPL][KX];
+  f32x4_t bias4[CPL];
+  int unit[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) {
+    const int gi = w + NW * cc;
+    const int au = 4 * gi + (col >> 2), ag = col & 3;
+    unit[cc] = 4 * gi + quad;
+#pragma unroll
+    for (int s = 0; s < C::KSH; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+      }
+      ufr[cc][s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(W[min(k, Din - 1) * G4 + ag * H + au] * (k < Din ? 1.0f : 0.0f));
+      }
+      wfr[cc][s] = v;
+    }
+    const int u = unit[cc];
+    bias4[cc] = f32x4_t{bias[u], bias[H + u], bias[2 * H + u], bias[3 * H + u]};
+  }
+
+  // x loader: every wave streams granule (tid mod n) of the contiguous [16][Din] tile and
+  // stages it (identical duplicates across waves). No branch surrounds a memory op: with a
+  // predicate around loads hipcc drained vmcnt at the join every step (seen in the ISA).
+  const int n_gx = 16 * Din / GR;
+  const int gx = (tid % n_gx) * GR;
+  const int gx_seq = gx / Din, gx_k = gx % Din;
+  const float* xbase = x + (size_t)row0 * Din + gx;
+  const size_t xstep = (size_t)Mp * Din;
+  Granule<GR> xr[D];
+  // h storer: every wave stores granule (tid mod n) of the [16][H] tile; a step without an
+  // h to store writes the scratch time row T.
+  constexpr int n_gh = 16 * H / 4;
+  const int gh = (tid % n_gh) * 4;
+  float* hbase = hout + (size_t)row0 * H + gh;
+  const size_t hstep = (size_t)Mp * H;
+
+#pragma unroll
+  for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < GR; ++q) xs[0][gx_seq][gx_k + q] = (__bf16)xr[0].v[q];
+  xr[0].load(xbase + (size_t)min(D, T - 1) * xstep);
+  float c[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) c[cc] = 0.f;
+  __syncthreads();
+
+  // steps 0 .. T (step T only stores h_{T-1})
+  for (int t0 = 0; t0 <= T; t0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int t = t0 + j;
+      const int p = t & 1;
+      const int jn = (j + 1 == D) ? 0 : j + 1;
+      {                                             // h_{t-1}: one contiguous tile
+        const int ts = (t >= 1 && t <= T) ? t - 1 : T;
+        const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][0][0] + gh);
+        *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+      }
+      f32x4_t acc[CPL];
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) {
+        acc[cc] = bias4[cc];
+#pragma unroll
+        for (int s = 0; s < KX; ++s) {
+          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
+          acc[cc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, acc[cc], 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < C::KSH; ++s) {
+          const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
+          acc[cc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acc[cc], 0, 0, 0);
+        }
+      }
+      // stage x_{t+1}, refill the slot with x_{t+1+D}
+#pragma unroll
+      for (int q = 0; q < GR; ++q) xs[p ^ 1][gx_seq][gx_k + q] = (__bf16)xr[jn].v[q];
+      xr[jn].load(xbase + (size_t)min(t + 1 + D, T - 1) * xstep);
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) {
+        const float iv = sigmoidf_fast(acc[cc][0]);
+        const float fv = sigmoidf_fast(acc[cc][1]);
+        const float gv = tanhf_fast(acc[cc][2]);
+        const float ov = sigmoidf_fast(acc[cc][3]);
+        c[cc] = fv * c[cc] + iv * gv;
+        const float hv = ov * tanhf_fast(c[cc]);
+        const int u = unit[cc];
+        hs[p ^ 1][col][u] = (__bf16)hv;
+        hf[p][col][u] = hv;
+        if constexpr (TRAIN) {                       // steps past T-1 write the scratch row T
+          const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
+          *reinterpret_cast<float4*>(gbuf + o * 4) = make_float4(iv, fv, gv, ov);
+          cbuf[o] = c[cc];
+        }
+      }
+      lds_barrier();
+    }
+  }
+}
+
+// =====================================================================================
+// backward (fused recurrence + weight gradients + input gradient)
+// dhout: [T][Mp][H] (or [Mp][H] for the last step only)  x: [T][Mp][Din]  hout: [T][Mp][H]
+// dx: [T][Mp][Din]  dW: [Din][4H]  dU: [H][4H]  db: [4H]   (dW/dU/db accumulated with atomics)
+template <int H, int KX, int GR, int D, bool WGRAD, bool DX, bool LAST>
+__global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
+    const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
+    const float* __restrict__ x, const float* __restrict__ hout, const float* __restrict__ W,
+    const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ dU,
+    float* __restrict__ db, int Mp, int T, int Din) {
+  using C = TMC<H>;
+  constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
+  constexpr int NDB = KX * 2;                     // 16-wide din blocks incl. the bias row (<= 32 KX)
+  constexpr int NRB = G4 / 16;                    // 16-row blocks of the gate dimension
+  constexpr int NHB = H / 16;
+  constexpr int TW = (NRB * NDB + NW - 1) / NW;   // dW^T tiles per wave
+  constexpr int TU = (NRB * NHB + NW - 1) / NW;   // dU^T tiles per wave
+  constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
+  constexpr int TX = (NXB + NW - 1) / NW;         // dx tiles per wave
+  __shared__ __attribute__((aligned(16))) __bf16 zs[2][16][G4 + 8];     // dz row-major (B of U dz^T, W dz^T)
+  __shared__ __attribute__((aligned(16))) __bf16 zt[2][G4][16 + 4];     // dz^T (A of dW^T, dU^T)
+  __shared__ __attribute__((aligned(16))) __bf16 xt[2][32 * KX][16 + 4]; // [x_t | 1]^T (B of dW^T)
+  __shared__ __attribute__((aligned(16))) __bf16 ht[2][H][16 + 4];      // h_{t-1}^T (B of dU^T)
+  __shared__ __attribute__((aligned(16))) float dhs[2][16][H];          // dh_out tile
+  __shared__ __attribute__((aligned(16))) float dxs[2][16][32 * KX];    // dx tile
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in an SGPR
+  const int col = lane & 15, quad = lane >> 4;
+  const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
+
+  for (int i = tid; i < 2 * G4 * 20; i += NT) (&zt[0][0][0])[i] = (__bf16)0.0f;
+  for (int i = tid; i < 2 * 32 * KX * 20; i += NT) {
+    const int r = (i / 20) % (32 * KX);
+    (&xt[0][0][0])[i] = (__bf16)(r == Din ? 1.0f : 0.0f);      // ones row: db as a column of dW^T
+  }
+  for (int i = tid; i < 2 * H * 20; i += NT) (&ht[0][0][0])[i] = (__bf16)0.0f;
+  for (int i = tid; i < 2 * 16 * H; i += NT) (&dhs[0][0][0])[i] = 0.f;
+
+  // A fragments of U (dh_rec) and W (dx^T): tile row `col` of cell group gi is unit
+  // 4 gi + (col >> 2) when col % 4 == 0 and zero otherwise -> acc[0] is the lane's own cell
+  bf16x8_t ufr[CPL][KB];
+  int unit[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) {
+    const int gi = w + NW * cc;
+    unit[cc] = 4 * gi + quad;
+    const int au = 4 * gi + (col >> 2);
+#pragma unroll
+    for (int s = 0; s < KB; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float val = U[(size_t)au * G4 + 32 * s + 8 * quad + j];
+        v[j] = (__bf16)(val * ((col & 3) == 0 ? 1.0f : 0.0f));
+      }
+      ufr[cc][s] = v;
+    }
+  }
+  bf16x8_t wfr[DX ? TX : 1][DX ? KB : 1];
+  if constexpr (DX) {
+#pragma unroll
+    for (int q = 0; q < TX; ++q) {
+      const int xb = w + NW * q;
+      const int din = 16 * xb + col;
+#pragma unroll
+      for (int s = 0; s < KB; ++s) {
+        bf16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = (__bf16)(W[(size_t)min(din, Din - 1) * G4 + 32 * s + 8 * quad + j] * ((xb < NXB && din < Din) ? 1.0f : 0.0f));
+        wfr[q][s] = v;
+      }
+    }
+  }
+  f32x4_t accW[WGRAD ? TW : 1], accU[WGRAD ? TU : 1];
+#pragma unroll
+  for (int q = 0; q < (WGRAD ? TW : 1); ++q) accW[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < (WGRAD ? TU : 1); ++q) accU[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // ---- streams. internal state (per lane, ring over reverse steps): gates, c_t
+  float4 rg[CPL][D];
+  float rc[CPL][D];
+  auto idx = [&](int tt, int cc) { return ((((size_t)tt * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane; };
+#define GQ_TMB_LOAD_STATE(J, SS)                                                    \
+  {                                                                                 \
+    const int tt_ = max(T - 1 - (SS), 0);                                           \
+    _Pragma("unroll") for (int cc = 0; cc < CPL; ++cc) {                            \
+      const size_t o_ = idx(tt_, cc);                                               \
+      rg[cc][J] = *reinterpret_cast<const float4*>(gbuf + o_ * 4);                  \
+      rc[cc][J] = cbuf[o_];                                                         \
+    }                                                                               \
+  }
+  // Streams: every wave loads and stages granule (tid mod n) of each contiguous tile (no
+  // branch around memory ops, see the forward). dh: [16][H] float4 granules.
+  constexpr int n_gd = 16 * H / 4;
+  const int gd = (tid % n_gd) * 4;
+  const int gd_seq = gd / H, gd_k = gd % H;
+  const float* dbase = dhout + (size_t)row0 * H + gd;
+  const size_t dstep = LAST ? 0 : (size_t)Mp * H;
+  float4 rd[D];
+  // x and h_{t-1} tiles (weight gradients)
+  const int n_gx = 16 * Din / GR;
+  const int gx = (tid % n_gx) * GR;
+  const int gx_seq = gx / Din, gx_k = gx % Din;
+  const float* xbase = x + (size_t)row0 * Din + gx;
+  const size_t xstep = (size_t)Mp * Din;
+  Granule<GR> rx[D];
+  const float* hbase = hout + (size_t)row0 * H + gd;
+  const size_t hstep = (size_t)Mp * H;
+  float4 rh[D];
+  // dx storer (same granule map as x); skipped stores go to the scratch time row T
+  float* sbase = dx + (size_t)row0 * Din + gx;
+
+  // reverse step s <-> time t = T-1-s. Streams for step s are loaded D steps ahead.
+#define GQ_TMB_LOAD_D(J, SS)                                                                \
+  {                                                                                         \
+    const int tt_ = max(T - 1 - (SS), 0);                                                   \
+    float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)tt_ * dstep);              \
+    if (LAST) {                                                                             \
+      const float m_ = (SS) == 0 ? 1.f : 0.f;                                               \
+      v_.x *= m_; v_.y *= m_; v_.z *= m_; v_.w *= m_;                                       \
+    }                                                                                       \
+    rd[J] = v_;                                                                             \
+  }
+#define GQ_TMB_LOAD_XH(J, SS)                                                               \
+  if constexpr (WGRAD) {                                                                    \
+    const int tt_ = max(T - 1 - (SS), 0);                                                   \
+    rx[J].load(xbase + (size_t)tt_ * xstep);                                                \
+    rh[J] = *reinterpret_cast<const float4*>(hbase + (size_t)max(tt_ - 1, 0) * hstep);      \
+  }
+#define GQ_TMB_STAGE_XH(J, BUF, TT)                                                         \
+  if constexpr (WGRAD) {                                                                    \
+    _Pragma("unroll") for (int q = 0; q < GR; ++q) xt[BUF][gx_k + q][gx_seq] = (__bf16)rx[J].v[q]; \
+    const float hm_ = (TT) > 0 ? 1.f : 0.f;    /* h_{-1} = 0 */                             \
+    ht[BUF][gd_k + 0][gd_seq] = (__bf16)(rh[J].x * hm_);                                    \
+    ht[BUF][gd_k + 1][gd_seq] = (__bf16)(rh[J].y * hm_);                                    \
+    ht[BUF][gd_k + 2][gd_seq] = (__bf16)(rh[J].z * hm_);                                    \
+    ht[BUF][gd_k + 3][gd_seq] = (__bf16)(rh[J].w * hm_);                                    \
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    GQ_TMB_LOAD_STATE(j, j)
+    GQ_TMB_LOAD_D(j, j)
+    GQ_TMB_LOAD_XH(j, j)
+  }
+  __syncthreads();
+  // stage step 0 (t = T-1) tiles
+  *reinterpret_cast<float4*>(&dhs[0][0][0] + gd) = rd[0];
+  GQ_TMB_LOAD_D(0, D)
+  GQ_TMB_STAGE_XH(0, 0, T - 1)
+  GQ_TMB_LOAD_XH(0, D)
+  float dc[CPL], dhr[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
+  __syncthreads();
+
+  for (int s0 = 0; s0 < T; s0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int s = s0 + j;
+      const int t = T - 1 - s;
+      const int p = s & 1;
+      const int jn = (j + 1 == D) ? 0 : j + 1;
+      // ---------------- cell phase
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) {
+        const int u = unit[cc];
+        const float cp = rc[cc][jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
+        const float dh = dhs[p][col][u] + dhr[cc];
+        const float4 g4 = rg[cc][j];
+        const float tc = tanhf_fast(rc[cc][j]);
+        const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
+        dc[cc] = dct * g4.y;
+        const float zi = dct * g4.z * g4.x * (1.f - g4.x);
+        const float zf = dct * cp * g4.y * (1.f - g4.y);
+        const float zg = dct * g4.x * (1.f - g4.z * g4.z);
+        const float zo = dh * tc * g4.w * (1.f - g4.w);
+        zs[p][col][0 * H + u] = (__bf16)zi;
+        zs[p][col][1 * H + u] = (__bf16)zf;
+        zs[p][col][2 * H + u] = (__bf16)zg;
+        zs[p][col][3 * H + u] = (__bf16)zo;
+        if constexpr (WGRAD) {
+          zt[p][0 * H + u][col] = (__bf16)zi;
+          zt[p][1 * H + u][col] = (__bf16)zf;
+          zt[p][2 * H + u][col] = (__bf16)zg;
+          zt[p][3 * H + u][col] = (__bf16)zo;
+        }
+      }
+      GQ_TMB_LOAD_STATE(j, s + D)
+      *reinterpret_cast<float4*>(&dhs[p ^ 1][0][0] + gd) = rd[jn];   // dh tile of step s+1
+      GQ_TMB_LOAD_D(jn, s + 1 + D)
+      lds_barrier();
+      // ---------------- MFMA phase
+      // (a) serial chain: dh_{t-1} = U dz_t
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) {
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+          if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][k], bz, a1, 0, 0, 0);
+          else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][k], bz, a0, 0, 0, 0);
+        }
+        dhr[cc] = a0[0] + a1[0];
+      }
+      // (b) previous step's dx tile -> HBM (written by all waves before this barrier)
+      if constexpr (DX) {
+        const int ts = (s >= 1 && s <= T) ? t + 1 : T;
+#pragma unroll
+        for (int q = 0; q < GR; ++q) sbase[(size_t)ts * xstep + q] = dxs[p ^ 1][gx_seq][gx_k + q];
+      }
+      // (c) dx^T = W dz^T for this step (steps past t = 0 only pad the unrolled chunk)
+      if (DX && t >= 0) {
+#pragma unroll
+        for (int q = 0; q < TX; ++q) {
+          const int xb = w + NW * q;
+          if (xb < NXB) {                           // wave-uniform
+            f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (!DX) continue;
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q][k], bz, a, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dxs[p][col][16 * xb + 4 * quad + r] = a[r];
+          }
+        }
+      }
+      // (d) weight gradients: dW^T += dz^T [x|1], dU^T += dz^T h_{t-1}   (K = 16 sequences)
+      if (WGRAD && t >= 0) {
+#pragma unroll
+        for (int q = 0; q < TW; ++q) {
+          const int tq = w + NW * q;
+          if (tq < NRB * NDB) {
+            const int rb = tq / NDB, dbk = tq % NDB;
+            const bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(&zt[p][16 * rb + col][4 * quad]);
+            const bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(&xt[p][16 * dbk + col][4 * quad]);
+            accW[q] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, accW[q], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < TU; ++q) {
+          const int tq = w + NW * q;
+          if (tq < NRB * NHB) {
+            const int rb = tq / NHB, hb = tq % NHB;
+            const bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(&zt[p][16 * rb + col][4 * quad]);
+            const bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(&ht[p][16 * hb + col][4 * quad]);
+            accU[q] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, accU[q], 0, 0, 0);
+          }
+        }
+      }
+      // stage x_{t-1} / h_{t-2} tiles for the next reverse step (garbage past t = 0: unused)
+      GQ_TMB_STAGE_XH(jn, p ^ 1, t - 1)
+      GQ_TMB_LOAD_XH(jn, s + 1 + D)
+    }
+  }
+  __syncthreads();
+  if constexpr (DX) {   // dx tile of t = 0
+    const int pl = (T - 1) & 1;
+#pragma unroll
+    for (int q = 0; q < GR; ++q) sbase[q] = dxs[pl][gx_seq][gx_k + q];
+  }
+  if constexpr (WGRAD) {
+    // C layout: lane (col = n, quad) holds rows 4 quad + r of the tile
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      const int tq = w + NW * q;
+      if (tq < NRB * NDB) {
+        const int rb = tq / NDB, dbk = tq % NDB;
+        const int din = 16 * dbk + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gr = 16 * rb + 4 * quad + r;
+          if (din < Din) atomicAdd(&dW[(size_t)din * G4 + gr], accW[q][r]);
+          else if (din == Din) atomicAdd(&db[gr], accW[q][r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TU; ++q) {
+      const int tq = w + NW * q;
+      if (tq < NRB * NHB) {
+        const int rb = tq / NHB, hb = tq % NHB;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(&dU[(size_t)(16 * hb + col) * G4 + 16 * rb + 4 * quad + r], accU[q][r]);
+      }
+    }
+  }
+#undef GQ_TMB_LOAD_STATE
+#undef GQ_TMB_LOAD_D
+#undef GQ_TMB_LOAD_XH
+#undef GQ_TMB_STAGE_XH
+}
+
+// =====================================================================================
+// host side
+static int tm_granule(int Din, const void* x) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(x);
+  if (Din % 4 == 0 && a % 16 == 0) return 4;
+  if (Din % 2 == 0 && a % 8 == 0) return 2;
+  return 1;
+}
+
+// H in {16, 32}: one cell per lane, 4 / 8 waves, comfortably inside the VGPR budget of the
+// fused backward (U and W fragments + stream rings + weight-gradient accumulators). Larger
+// hidden sizes keep the seq-major kernels of lstm.hip / lstm_grads.hip. The per-step
+// x tile must fit the loader lanes and Din + 1 (bias row) must fit 128.
+static bool tm_supported(int H, int Din, int gr) {
+  if (H != 16 && H != 32) return false;
+  if (Din < 1 || Din > 127) return false;
+  return 16 * Din / gr <= 16 * H;
+}
+
+template <int H, bool TRAIN, int KX, int GR>
+static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, float* g,
+                       float* c, int Mp, int T, int Din, hipStream_t st) {
+  constexpr int D = 6;
+  hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W, U, b,
+                     h, g, c, Mp, T, Din);
+}
+
+template <int H, int KX, int GR, bool WG, bool DXF, bool LAST>
+static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* x, const float* h,
+                       const float* W, const float* U, float* dx, float* dW, float* dU, float* db, int Mp, int T,
+                       int Din, hipStream_t st) {
+  constexpr int D = 4;
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, WG, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh,
+                     g, c, x, h, W, U, dx, dW, dU, db, Mp, T, Din);
+}
+
+#define GQ_TM_H_DISPATCH(HV, ...)                                  \
+  switch (HV) {                                                    \
+    case 16: { constexpr int HH = 16; __VA_ARGS__; break; }        \
+    case 32: { constexpr int HH = 32; __VA_ARGS__; break; }        \
+    default: TORCH_CHECK(false, "lstm_tm: hidden size must be 16 or 32");  \
+  }
+#define GQ_TM_KX_DISPATCH(KXN, ...)                                \
+  {                                                                \
+    const int kx_ = (KXN);                                         \
+    if (kx_ == 1) { constexpr int KXX = 1; __VA_ARGS__; }          \
+    else if (kx_ == 2) { constexpr int KXX = 2; __VA_ARGS__; }     \
+    else { constexpr int KXX = 4; __VA_ARGS__; }                   \
+  }
+#define GQ_TM_GR_DISPATCH(GRV, ...)                                \
+  {                                                                \
+    if (GRV == 4) { constexpr int GRR = 4; __VA_ARGS__; }          \
+    else if (GRV == 2) { constexpr int GRR = 2; __VA_ARGS__; }     \
+    else { constexpr int GRR = 1; __VA_ARGS__; }                   \
+  }
+
+// x: [T, Mp, Din] time-major. Returns [h (T,Mp,H), gates (state), c (state)].
+std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
+                                    const at::Tensor& b, bool train) {
+  check_f32_cuda(x, "x");
+  check_f32_cuda(W, "W");
+  check_f32_cuda(U, "U");
+  check_f32_cuda(b, "b");
+  TORCH_CHECK(x.dim() == 3, "lstm_tm_fwd: x must be [T, Mp, Din]");
+  const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
+  TORCH_CHECK(Mp % 16 == 0 && Mp > 0 && T > 0, "lstm_tm_fwd: Mp must be a positive multiple of 16");
+  TORCH_CHECK(U.size(1) == 4 * H && W.size(0) == Din && W.size(1) == 4 * H && b.numel() == 4 * H,
+              "lstm_tm_fwd: weight shapes");
+  const int gr = tm_granule(Din, x.data_ptr());
+  TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
+  c10::DeviceGuard guard(x.device());
+  auto opt = x.options();
+  // one extra (scratch) time row: stores of steps that have nothing to store land there
+  at::Tensor h = at::empty({T + 1, Mp, H}, opt);
+  at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt) : at::empty({0}, opt);
+  at::Tensor c = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
+  const int ntiles = Mp / 16;
+  auto st = stream();
+  float* gp = train ? g.data_ptr<float>() : nullptr;
+  float* cp = train ? c.data_ptr<float>() : nullptr;
+  GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
+      if (train) tm_fwd_cfg<HH, true, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
+                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, st);
+      else tm_fwd_cfg<HH, false, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
+                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, st))));
+  GQ_LAUNCH_CHECK();
+  return {h.narrow(0, 0, T), g, c};
+}
+
+// dh: [T, Mp, H] (or [Mp, H] when only the last step has a gradient). Returns dx [T, Mp, Din]
+// (empty if !need_dx) and accumulates dW, dU, db when they are non-empty.
+at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
+                       const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, at::Tensor dW, at::Tensor dU,
+                       at::Tensor db, bool need_dx) {
+  const at::Tensor* ops[] = {&dh, &g, &c, &x, &h, &W, &U};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
+  const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
+  const bool last = dh.dim() == 2;
+  TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H) : (dh.size(0) == T && dh.size(1) == Mp && dh.size(2) == H),
+              "lstm_tm_bwd: dh shape");
+  TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H &&
+                  h.numel() == (long)T * Mp * H, "lstm_tm_bwd: saved state shapes");
+  const bool wg = dW.numel() > 0;
+  if (wg) {
+    const at::Tensor* gs[] = {&dW, &dU, &db};
+    for (const at::Tensor* t : gs) check_f32_cuda(*t, "lstm_tm_bwd grad");
+    TORCH_CHECK(dW.numel() == (long)Din * 4 * H && dU.numel() == (long)H * 4 * H && db.numel() == 4 * H,
+                "lstm_tm_bwd: gradient buffer shapes");
+  }
+  const int gr = tm_granule(Din, x.data_ptr());
+  TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm_bwd: unsupported shape");
+  c10::DeviceGuard guard(x.device());
+  at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, x.options()) : at::empty({0}, x.options());
+  TORCH_CHECK(!need_dx || tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
+  const int ntiles = Mp / 16;
+  auto st = stream();
+  float* dxp = need_dx ? dx.data_ptr<float>() : nullptr;
+  float* dWp = wg ? dW.data_ptr<float>() : nullptr;
+  float* dUp = wg ? dU.data_ptr<float>() : nullptr;
+  float* dbp = wg ? db.data_ptr<float>() : nullptr;
+#define GQ_TM_BWD_CALL(WGV, DXV, LASTV)                                                                    \
+  tm_bwd_cfg<HH, KXX, GRR, WGV, DXV, LASTV>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(), c.data_ptr<float>(), \
+                                             x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),     \
+                                             U.data_ptr<float>(), dxp, dWp, dUp, dbp, Mp, T, Din, st)
+  GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 1 + 31) / 32, GQ_TM_GR_DISPATCH(gr,
+      if (wg && need_dx) { if (last) GQ_TM_BWD_CALL(true, true, true); else GQ_TM_BWD_CALL(true, true, false); }
+      else if (wg) { if (last) GQ_TM_BWD_CALL(true, false, true); else GQ_TM_BWD_CALL(true, false, false); }
+      else { if (last) GQ_TM_BWD_CALL(false, true, true); else GQ_TM_BWD_CALL(false, true, false); })));
+#undef GQ_TM_BWD_CALL
+  GQ_LAUNCH_CHECK();
+  return need_dx ? dx.narrow(0, 0, T) : dx;
+}
+
+}  // namespace gq
+
+TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("lstm_tm_fwd", &gq::lstm_tm_fwd);
+  m.impl("lstm_tm_bwd", &gq::lstm_tm_bwd);
+}

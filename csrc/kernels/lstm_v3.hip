@@ -64,7 +64,7 @@ __global__ __launch_bounds__(16 * H) void lstm_fwd3_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 32 * s + 8 * quad + j;
-      v[j] = (__bf16)(k < H ? U[min(k, H - 1) * C::G4 + ar_gate * H + ar_unit] : 0.0f);
+      v[j] = (__bf16)(U[min(k, H - 1) * C::G4 + ar_gate * H + ar_unit] * (k < H ? 1.0f : 0.0f));
     }
     ufr[s] = v;
   }
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(16 * H) void lstm_fwd3_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 32 * s + 8 * quad + j;
-      v[j] = (__bf16)(k < Din ? W[min(k, Din - 1) * C::G4 + ar_gate * H + ar_unit] : 0.0f);
+      v[j] = (__bf16)(W[min(k, Din - 1) * C::G4 + ar_gate * H + ar_unit] * (k < Din ? 1.0f : 0.0f));
     }
     wfr[s] = v;
   }
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(16 * H) void lstm_bwd3_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float val = U[(size_t)(4 * w + (col >> 2)) * C::G4 + 32 * s + 8 * quad + j];
-      v[j] = (__bf16)((col & 3) == 0 ? val : 0.0f);
+      v[j] = (__bf16)(val * ((col & 3) == 0 ? 1.0f : 0.0f));
     }
     afr[s] = v;
   }

@@ -10,6 +10,10 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_bwd(Tensor dh, Tensor gates, Tensor cseq, Tensor U, bool bf16) -> Tensor");
   m.def("lstm_grads(Tensor dz, Tensor x, Tensor hseq, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
         "bool need_dx) -> Tensor");
+  // time-major LSTM with fused backward (lstm_tm.hip)
+  m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train) -> Tensor[]");
+  m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor(a!) dW, "
+        "Tensor(b!) dU, Tensor(c!) db, bool need_dx) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)
   m.def("gcn_stats(Tensor x, Tensor mask) -> Tensor");
   m.def("gcn_pool_fwd(Tensor x, Tensor w, Tensor anom, Tensor W, Tensor b, Tensor scale, Tensor shift, "

@@ -11,6 +11,7 @@ time4``) so checkpoint variable paths line up.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -69,7 +70,50 @@ class TimeLayer(nn.Module):
     def out_features(self) -> int:
         return self.filter_1_size * 2 ** (self.n_stacks + 1)
 
+    def _sequence(self):
+        """The layer/pool sequence of the LSTM branch, in execution order."""
+        seq = [self.time1, self.time2, self.max_pooling]
+        for i in range(len(self.pooling_layers)):
+            seq += [self.time_layers[2 * i], self.time_layers[2 * i + 1], self.pooling_layers[i]]
+        return seq + [self.time4]
+
+    def _forward_tm(self, x: torch.Tensor) -> torch.Tensor:
+        """GPU LSTM branch: the leading H <= 32 layers (and their pools) run time-major
+        ([T, Mp, C], fused-backward kernels); the rest continues sequence-major."""
+        import torch.nn.functional as F
+        from ..ops.lstm import lstm_layer_tm, tm_eligible
+        from ..ops.pool import max_pool1d_tm
+        M = x.shape[0]
+        Mp = (M + 15) // 16 * 16
+        h = x.float().transpose(0, 1)
+        if Mp != M:
+            h = F.pad(h, (0, 0, 0, Mp - M))
+        h = h.contiguous()
+        tm = True
+        for mod in self._sequence():
+            if isinstance(mod, MaxPooling1D):
+                h = max_pool1d_tm(h, mod.pool_size) if tm else mod(h)
+                continue
+            if tm and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16):
+                h = lstm_layer_tm(h, mod.kernel, mod.recurrent_kernel, mod.bias, mod.return_sequences)
+                if not mod.return_sequences:
+                    return h[:M]
+                continue
+            if tm:                                   # leave time-major: [T, Mp, C] -> [M, T, C]
+                h = h.transpose(0, 1)[:M].contiguous()
+                tm = False
+            h = mod(h)
+        return h
+
+    def _tm_ok(self, x: torch.Tensor) -> bool:
+        from ..ops.lstm import tm_eligible
+        return (self.layer_type == "lstm" and self.time1.activation == "tanh"
+                and tm_eligible(x, self.time1.units, x.shape[-1], self.time1.activation, self.time1.compute_bf16)
+                and os.environ.get("GNNQC_NO_TM", "0") != "1")
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._tm_ok(x):
+            return self._forward_tm(x)
         cnn = self.layer_type != "lstm"
         x1 = self.time1(x)
         if cnn:

@@ -129,6 +129,55 @@ class _HipLSTM(torch.autograd.Function):
                 None, None)
 
 
+class _HipLSTMTM(torch.autograd.Function):
+    """Time-major LSTM layer (``lstm_tm.hip``): x [T, Mp, Din] -> h [T, Mp, H] (or the last
+    step [Mp, H]). The backward is ONE fused kernel: recurrence, dx, and dW/dU/db
+    accumulated straight into the gradient buffers (direct mode) or returned."""
+
+    @staticmethod
+    def forward(ctx, x, W, U, b, return_sequences: bool):
+        from ..utils.native import hip_ops
+        x = x.contiguous()
+        need = any(ctx.needs_input_grad[:4])
+        h, g, c = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need)
+        ctx.params = (W, U, b)
+        ctx.return_sequences = return_sequences
+        if need:
+            ctx.save_for_backward(x, W, U, h, g, c)
+        return h if return_sequences else h[-1]
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..utils.native import hip_ops
+        x, W, U, h, g, c = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        wgrad = any(need[1:4])
+        need_dx = bool(need[0])
+        if not wgrad and not need_dx:
+            return None, None, None, None, None
+        if wgrad:
+            sinks = [_grad_sink(p) for p in ctx.params]
+        else:
+            e = x.new_zeros(0)
+            sinks = [(e, True)] * 3
+        dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
+                                   sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
+        grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
+        return (dx if need_dx else None, *grads, None)
+
+
+def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf16: bool = True) -> bool:
+    """Whether the time-major fused kernels handle this layer (GPU, bf16, tanh, H in {16, 32})."""
+    from . import use_hip
+    return (use_hip(x) and bf16 and activation == "tanh" and H in (16, 32) and 1 <= Din <= 127
+            and (16 * Din) // (4 if Din % 4 == 0 else (2 if Din % 2 == 0 else 1)) <= 16 * H)
+
+
+def lstm_layer_tm(x_tm: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
+                  return_sequences: bool = True) -> torch.Tensor:
+    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences))
+
+
 def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
                return_sequences: bool = True, activation: str = "tanh", bf16: bool = True) -> torch.Tensor:
     """Dispatch: HIP persistent kernel on GPU (tanh, H multiple of 16), eager otherwise."""
@@ -139,4 +188,4 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     return lstm_eager(x, W, U, b, return_sequences, activation)
 
 
-__all__ = ["lstm_layer", "lstm_eager"]
+__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "tm_eligible"]

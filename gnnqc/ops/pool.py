@@ -34,4 +34,11 @@ def max_pool1d(x: torch.Tensor, p: int) -> torch.Tensor:
     return x[:, :To * p].reshape(M, To, p, C).max(2).values
 
 
-__all__ = ["max_pool1d"]
+def max_pool1d_tm(x_tm: torch.Tensor, p: int) -> torch.Tensor:
+    """Time-major pooling: [T, Mp, C] -> [T // p, Mp, C] (pool along the leading time axis)."""
+    T, Mp, C = x_tm.shape
+    y = max_pool1d(x_tm.contiguous().view(1, T, Mp * C), p)
+    return y.view(T // p, Mp, C)
+
+
+__all__ = ["max_pool1d", "max_pool1d_tm"]

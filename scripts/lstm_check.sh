@@ -5,8 +5,9 @@ OUT=gpurun_out/lstm_check; mkdir -p $OUT
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -ne 0 ] && exit $rc
-GNNQC_LSTM_V3=1 timeout -k 10 300 python scripts/lstm_microbench.py --M 128 1024 > $OUT/micro_new.jsonl 2>&1 || exit 3
-timeout -k 10 300 python scripts/lstm_microbench.py --M 128 > $OUT/micro_v1.jsonl 2>&1 || exit 3
+timeout -k 10 300 python scripts/lstm_microbench.py --M 128 1024 > $OUT/micro_new.jsonl 2>&1 || exit 3
 timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $OUT/bench.log 2>&1 || exit 3
+GNNQC_NO_TM=1 timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $OUT/bench_notm.log 2>&1 || exit 3
+tail -1 $OUT/bench_notm.log | cut -c1-200
 tail -1 $OUT/bench.log | cut -c1-250
 cat $OUT/micro_new.jsonl | grep '"M": 128'

@@ -294,3 +294,71 @@ def test_gcn_pool_weights_matches_eager(cuda_device, aggregate, pooling):
     got = hip_ops().gcn_pool_weights(adj, mask, ap, aggregate == "mean",
                                      {"mean": 0, "sum": 1, "selection": 2}[pooling])
     torch.testing.assert_close(got, ref, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("H", [16, 32])
+@pytest.mark.parametrize("Din", [18, 16, 2, 32])
+@pytest.mark.parametrize("ret_seq", [True, False])
+@pytest.mark.parametrize("wgrad", [True, False])
+def test_lstm_time_major_fused_bwd_matches_eager(cuda_device, H, Din, ret_seq, wgrad):
+    """lstm_tm_fwd / lstm_tm_bwd (recurrence + dx + fused dW/dU/db) vs fp64 eager."""
+    from gnnqc.ops.lstm import lstm_eager, lstm_layer_tm, tm_eligible
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(H * 100 + Din + 3 * ret_seq)
+    M, T = 40, 13                     # 3 tiles (Mp = 48), T not a multiple of the ring depth
+    x = torch.randn(M, T, Din, generator=gen).to(dev)
+    if not tm_eligible(x, H, Din):
+        pytest.skip("shape not handled by the time-major kernels")
+    W, U, b = _lstm_params(Din, H, gen, dev)
+    xt = torch.zeros(T, 48, Din, device=dev)
+    xt[:, :M] = x.transpose(0, 1)
+    xt.requires_grad_(True)
+    Wp, Up, bp = (t.clone().requires_grad_(wgrad) for t in (W, U, b))
+    out = lstm_layer_tm(xt, Wp, Up, bp, ret_seq)
+    out_m = out[:, :M].transpose(0, 1) if ret_seq else out[:M]
+    ref_params = [t.clone().double().requires_grad_(True) for t in (x, W, U, b)]
+    ref = lstm_eager(*ref_params, return_sequences=ret_seq)
+    assert torch.allclose(out_m.double(), ref, atol=3e-2, rtol=3e-2), (out_m.double() - ref).abs().max()
+    g = torch.randn(ref.shape, generator=gen).to(dev)
+    out_m.backward(g)
+    ref.backward(g.double())
+    got = [xt.grad[:, :M].transpose(0, 1)] + ([Wp.grad, Up.grad, bp.grad] if wgrad else [])
+    for p, r, name in zip(got, ref_params, "xWUb"):
+        err = (p.double() - r.grad).abs().max().item()
+        scale = r.grad.abs().max().item() + 1e-6
+        assert err / scale < 5e-2, f"grad {name}: rel err {err / scale}"
+    assert float(xt.grad[:, M:].abs().max()) == 0.0          # padded rows get no gradient
+
+
+def test_timelayer_time_major_matches_sequence_major(cuda_device, monkeypatch):
+    """The CML TimeLayer (LSTM 16,16 | pool | 32,32 | pool | 64,64 | pool | 128): time-major
+    fused path vs the sequence-major kernels - forward and every parameter gradient."""
+    from gnnqc.models.timelayer import TimeLayer
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    from gnnqc.ops.optim import FlatAdam
+    torch.manual_seed(0)
+    tl = TimeLayer(18, 16, 2, "lstm", pool_size=3).to(cuda_device)
+    x = torch.randn(128, 181, 18, device=cuda_device)
+
+    def run(no_tm, direct):
+        monkeypatch.setenv("GNNQC_NO_TM", "1" if no_tm else "0")
+        xi = x.clone().requires_grad_(True)
+        for p in tl.parameters():
+            p.grad = None
+        opt = FlatAdam(tl.parameters()) if direct else None
+        out = tl(xi)
+        with direct_grad_accumulation(direct):
+            out.pow(2).sum().backward()
+        if opt is not None:
+            opt.relink_grads()
+        return out.detach(), xi.grad.clone(), [p.grad.clone() for p in tl.parameters()]
+
+    o1, dx1, g1 = run(True, False)
+    o2, dx2, g2 = run(False, False)
+    o3, dx3, g3 = run(False, True)
+    torch.testing.assert_close(o2, o1, atol=2e-2, rtol=2e-2)
+    for a, b_ in zip([dx2] + g2, [dx1] + g1):
+        err = (a - b_).abs().max().item() / (b_.abs().max().item() + 1e-6)
+        assert err < 6e-2, err
+    for a, b_ in zip([dx3] + g3, [dx2] + g2):
+        torch.testing.assert_close(a, b_, atol=1e-5, rtol=1e-4)
