@@ -14,7 +14,9 @@ namespace gq {
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ lr_p, const float* __restrict__ step_p,
-                            long n, float b1, float b2, float eps, float gscale, float wd) {
+                            long n, float b1, float b2, float eps, float gscale, float wd,
+                            const int* __restrict__ ok_p) {
+  if (ok_p != nullptr && *ok_p == 0) return;   // non-finite gradients: skip the whole update
   const float step = *step_p;
   const float lr = *lr_p;
   const float bc1 = 1.0f - powf(b1, step);
@@ -58,10 +60,65 @@ __global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* out) 
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(out, bad);
 }
 
+// Non-finite gradient guard, graph-capturable: every workgroup counts
+// non-finite entries of g into state[0]; the last workgroup to finish (ticket state[1])
+// publishes ok = (count == 0) in state[2], advances the optimiser step counter only for
+// a good step, counts skipped steps in state[3] and re-arms state[0..1] for the next
+// launch. The Adam kernel then reads state[2]. No host synchronisation anywhere.
+__global__ void grad_guard_kernel(const float* __restrict__ g, long n, int* __restrict__ state,
+                                  float* __restrict__ step) {
+  int bad = 0;
+  const long n4 = n / 4, stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    bad += !isfinite(v.x) + !isfinite(v.y) + !isfinite(v.z) + !isfinite(v.w);
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) bad += !isfinite(g[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+  __shared__ int wsum[16];
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += wsum[w];
+    if (tot) atomicAdd(&state[0], tot);
+    __threadfence();
+    const int ticket = atomicAdd(&state[1], 1);
+    if (ticket == (int)gridDim.x - 1) {          // last workgroup: all counts are in
+      const int cnt = atomicAdd(&state[0], 0);
+      const int ok = cnt == 0;
+      state[2] = ok;
+      if (ok) step[0] += 1.0f;
+      else state[3] += 1;
+      state[0] = 0;
+      state[1] = 0;
+      __threadfence();
+    }
+  }
+}
+
+void grad_guard(const at::Tensor& g, at::Tensor state, at::Tensor step) {
+  check_f32_cuda(g, "g");
+  check_f32_cuda(step, "step");
+  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kInt && state.numel() >= 4 && state.is_contiguous(),
+              "grad_guard: state must be int32[4] on the device");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr()) % 16) == 0, "grad_guard: g must be 16-byte aligned");
+  c10::DeviceGuard guard(g.device());
+  const long n = g.numel();
+  const int grid = (int)std::max<long>(1, std::min<long>((n / 4 + 255) / 256, 128));
+  hipLaunchKernelGGL(grad_guard_kernel, dim3(grid), dim3(256), 0, stream(), g.data_ptr<float>(), n,
+                     state.data_ptr<int>(), step.data_ptr<float>());
+  GQ_LAUNCH_CHECK();
+}
+
 void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, const at::Tensor& lr,
-               const at::Tensor& step, double b1, double b2, double eps, double gscale, double wd) {
+               const at::Tensor& step, double b1, double b2, double eps, double gscale, double wd,
+               const c10::optional<at::Tensor>& ok) {
   const at::Tensor* ops[] = {&p, &g, &m, &v, &lr, &step};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "adam operand");
+  if (ok.has_value())
+    TORCH_CHECK(ok->is_cuda() && ok->scalar_type() == at::kInt && ok->numel() >= 4, "adam: guard state int32[4]");
   const long n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) % 16) == 0,
@@ -71,7 +128,8 @@ void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, co
   const int grid = (int)std::max<long>(1, std::min<long>((n / 4 + block - 1) / block, 1024));
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(block), 0, stream(), p.data_ptr<float>(), g.data_ptr<float>(),
                      m.data_ptr<float>(), v.data_ptr<float>(), lr.data_ptr<float>(), step.data_ptr<float>(), n,
-                     (float)b1, (float)b2, (float)eps, (float)gscale, (float)wd);
+                     (float)b1, (float)b2, (float)eps, (float)gscale, (float)wd,
+                     ok.has_value() ? ok->data_ptr<int>() + 2 : nullptr);
   GQ_LAUNCH_CHECK();
 }
 
@@ -92,4 +150,5 @@ at::Tensor nonfinite_count(const at::Tensor& x) {
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("adam_step", &gq::adam_step);
   m.impl("nonfinite_count", &gq::nonfinite_count);
+  m.impl("grad_guard", &gq::grad_guard);
 }

@@ -26,7 +26,7 @@ template <int H, int DT>            // DT = ceil((Din + 1) / 16) din tiles (incl
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ dU,
-    float* __restrict__ db, int M, int T, int Din, int ldx, long dx_cb_stride) {
+    float* __restrict__ db, long rows, long period, long hshift, int Din, int ldx, long dx_cb_stride) {
   constexpr int G4 = 4 * H;
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
@@ -42,7 +42,6 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
   const int quad = lane >> 4;
   const int cb = blockIdx.x;               // column block: gate-units [cb*64, cb*64+64)
   const int gu0 = cb * GR_CB;
-  const long rows = (long)M * T;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
 
   f32x4_t accW[DT], accU[HT];
@@ -95,8 +94,7 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
       const long r = r0 + rr;
       const bool ok = r < rows;
       const long rc = min(r, rows - 1);
-      const long sq = rc / T, t = rc % T;
-      float v = x[((size_t)sq * T + t) * ldx + min(d, Din - 1)];
+      float v = x[(size_t)rc * ldx + min(d, Din - 1)];
       v = d < Din ? v : (d == Din ? 1.f : 0.f);
       xT[d][rr] = (__bf16)(ok ? v : 0.f);
     }
@@ -105,9 +103,8 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
       const int k = e % H;
       const long r = r0 + rr;
       const long rc = min(r, rows - 1);
-      const long t = rc % T;
-      const float v = hseq[(size_t)max(rc - 1, 0L) * H + k];
-      hT[k][rr] = (__bf16)((r < rows && t > 0) ? v : 0.f);
+      const float v = hseq[(size_t)max(rc - hshift, 0L) * H + k];   // h_{t-1}: hshift rows back
+      hT[k][rr] = (__bf16)((r < rows && rc % period >= hshift) ? v : 0.f);
     }
     __syncthreads();
     // ---- dW^T (wave w: gate-units [16w,16w+16) of the block) and dU^T
@@ -137,8 +134,7 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
           }
           const long r = r0 + 16 * rt + col;
           if (r < rows) {
-            const long sq = r / T, t = r % T;
-            float* o = dx + cb * dx_cb_stride + ((size_t)sq * T + t) * Din;
+            float* o = dx + cb * dx_cb_stride + (size_t)r * Din;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int din = dtile * 16 + 4 * quad + q;
@@ -177,13 +173,13 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
 
 template <int H>
 void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const float* x, const float* h,
-                    const float* W, float* dx, float* dW, float* dU, float* db, int M, int T, int Din, int ldx,
-                    long dx_cb_stride) {
+                    const float* W, float* dx, float* dW, float* dU, float* db, long rows, long period, long hshift,
+                    int Din, int ldx, long dx_cb_stride) {
   switch (DT) {
 #define GQ_DT(D)                                                                                              \
   case D:                                                                                                     \
-    hipLaunchKernelGGL((lstm_grads_kernel<H, D>), grid, dim3(256), 0, st, dz, x, h, W, dx, dW, dU, db, M, T, \
-                       Din, ldx, dx_cb_stride);                                                                  \
+    hipLaunchKernelGGL((lstm_grads_kernel<H, D>), grid, dim3(256), 0, st, dz, x, h, W, dx, dW, dU, db, rows, period, \
+                       hshift, Din, ldx, dx_cb_stride);                                                                 \
     break;
     GQ_DT(1) GQ_DT(2) GQ_DT(3) GQ_DT(4) GQ_DT(5) GQ_DT(6) GQ_DT(7) GQ_DT(8) GQ_DT(9)
 #undef GQ_DT
@@ -191,6 +187,33 @@ void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const fl
       TORCH_CHECK(false, "gnnqc lstm_grads: input width ", Din, " too large (max 143)");
   }
 }
+
+// Flat-row launcher shared by the sequence-major (lstm_grads) and time-major (lstm_tm_bwd)
+// paths: row r of dz / x / dx has h_{t-1} at row r - hshift when r % period >= hshift.
+//   sequence-major [M,T,C]: period = T, hshift = 1;  time-major [T,Mp,C]: period = T*Mp, hshift = Mp.
+void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
+                     float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
+                     long dx_cb_stride, hipStream_t st) {
+  if (rows == 0) return;
+  const int ncb = (4 * H) / GR_CB;
+  const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
+  // enough workgroups to fill the chip, few enough that the final atomics stay cheap
+  const int splits = (int)std::max<long>(1, std::min<long>(ntiles, std::max(32, 256 / ncb)));
+  dim3 grid(ncb, splits);
+  const int DT = (Din + 1 + 15) / 16;
+#define GQ_GR_H(HH)                                                                                              \
+  case HH:                                                                                                       \
+    launch_grads_h<HH>(DT, grid, st, dz, x, hseq, W, dx, dW, dU, db, rows, period, hshift, Din, ldx, dx_cb_stride); \
+    break;
+  switch (H) {
+    GQ_GR_H(16) GQ_GR_H(32) GQ_GR_H(64) GQ_GR_H(128)
+    default: TORCH_CHECK(false, "gnnqc lstm_grads: unsupported hidden size ", H);
+  }
+#undef GQ_GR_H
+  GQ_LAUNCH_CHECK();
+}
+
+int lstm_grads_col_blocks(int H) { return (4 * H) / GR_CB; }
 
 // dz [M(p),T,4H] from lstm_bwd; x [M,T,Din] (unit inner stride, row stride ldx);
 // hseq [M,T,H]; W [Din,4H]. dW/dU/db are ACCUMULATED into (pass zeroed or existing
@@ -211,29 +234,17 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   TORCH_CHECK(hseq.size(0) == M && hseq.size(1) == T, "hseq shape");
   TORCH_CHECK(W.size(0) == Din && W.size(1) == 4 * H && dW.sizes() == W.sizes() && dU.size(0) == H &&
                   dU.size(1) == 4 * H && db.numel() == 4 * H, "gradient buffer shapes");
+  TORCH_CHECK(Din + 1 <= 9 * 16, "gnnqc lstm_grads: input width ", Din, " too large (max 143)");
   c10::DeviceGuard guard(x.device());
-  const int ncb = (4 * H) / GR_CB;
+  const int ncb = lstm_grads_col_blocks(H);
   // dx = dz W^T contracts over all 4H gate-units: with several column blocks each
   // block writes its partial product to its own slab (plain stores), summed below
   at::Tensor dx = need_dx ? at::empty({ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
-  const long dx_cb_stride = (long)M * T * Din;
   const long rows = (long)M * T;
   if (rows == 0) return need_dx ? dx.sum(0) : dx;
-  const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
-  // enough workgroups to fill the chip, few enough that the final atomics stay cheap
-  const int splits = (int)std::max<long>(1, std::min<long>(ntiles, std::max(32, 256 / ncb)));
-  dim3 grid(ncb, splits);
-  const int DT = (Din + 1 + 15) / 16;
-  auto st = stream();
-  float* dxp = need_dx ? dx.data_ptr<float>() : nullptr;
-  switch (H) {
-    case 16: launch_grads_h<16>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
-    case 32: launch_grads_h<32>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
-    case 64: launch_grads_h<64>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
-    case 128: launch_grads_h<128>(DT, grid, st, dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(), dxp, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), M, T, Din, x.stride(1), dx_cb_stride); break;
-    default: TORCH_CHECK(false, "gnnqc lstm_grads: unsupported hidden size ", H);
-  }
-  GQ_LAUNCH_CHECK();
+  lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
+                  need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                  db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, stream());
   if (!need_dx) return dx;
   return ncb == 1 ? dx[0] : dx.sum(0);
 }

@@ -29,6 +29,12 @@
 
 namespace gq {
 
+// lstm_grads.hip: weight gradients (+ dx) over flat rows, h_{t-1} hshift rows back
+void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
+                     float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
+                     long dx_cb_stride, hipStream_t st);
+int lstm_grads_col_blocks(int H);
+
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
 // A wave-uniform predicate the compiler can SEE is uniform (an SGPR): branches on it are
@@ -202,42 +208,32 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
 }
 
 // =====================================================================================
-// backward (fused recurrence + weight gradients + input gradient)
-// dhout: [T][Mp][H] (or [Mp][H] for the last step only)  x: [T][Mp][Din]  hout: [T][Mp][H]
-// dx: [T][Mp][Din]  dW: [Din][4H]  dU: [H][4H]  db: [4H]   (dW/dU/db accumulated with atomics)
-template <int H, int KX, int GR, int D, bool WGRAD, bool DX, bool LAST>
+// backward recurrence. Per reverse step: cell phase (dz_t of the lane's own cells), then
+// dh_{t-1} = U dz_t on MFMA (the serial chain) and, off the chain,
+//   DZ: the dz_t tile -> HBM (fp32 [T+1][Mp][4H]); the weight gradients and dx are then ONE
+//       parallel pass over all T*Mp rows (lstm_grads_rows): folding them into this kernel
+//       lengthens every step of the serial chain and pushes H = 32 past the VGPR budget.
+//   DX: dx^T = W dz_t^T tile -> HBM (frozen-weight input gradients, e.g. integrated gradients).
+// dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
-    const float* __restrict__ x, const float* __restrict__ hout, const float* __restrict__ W,
-    const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ dU,
-    float* __restrict__ db, int Mp, int T, int Din) {
+    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
+    int Mp, int T, int Din) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
-  constexpr int NDB = KX * 2;                     // 16-wide din blocks incl. the bias row (<= 32 KX)
-  constexpr int NRB = G4 / 16;                    // 16-row blocks of the gate dimension
-  constexpr int NHB = H / 16;
-  constexpr int TW = (NRB * NDB + NW - 1) / NW;   // dW^T tiles per wave
-  constexpr int TU = (NRB * NHB + NW - 1) / NW;   // dU^T tiles per wave
   constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
   constexpr int TX = (NXB + NW - 1) / NW;         // dx tiles per wave
+  static_assert(16 * G4 / 4 == NT, "one dz float4 granule per thread");
   __shared__ __attribute__((aligned(16))) __bf16 zs[2][16][G4 + 8];     // dz row-major (B of U dz^T, W dz^T)
-  __shared__ __attribute__((aligned(16))) __bf16 zt[2][G4][16 + 4];     // dz^T (A of dW^T, dU^T)
-  __shared__ __attribute__((aligned(16))) __bf16 xt[2][32 * KX][16 + 4]; // [x_t | 1]^T (B of dW^T)
-  __shared__ __attribute__((aligned(16))) __bf16 ht[2][H][16 + 4];      // h_{t-1}^T (B of dU^T)
   __shared__ __attribute__((aligned(16))) float dhs[2][16][H];          // dh_out tile
-  __shared__ __attribute__((aligned(16))) float dxs[2][16][32 * KX];    // dx tile
+  __shared__ __attribute__((aligned(16))) float dxs[2][16][DX ? 32 * KX : 1];   // dx tile
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in an SGPR
   const int col = lane & 15, quad = lane >> 4;
   const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
 
-  for (int i = tid; i < 2 * G4 * 20; i += NT) (&zt[0][0][0])[i] = (__bf16)0.0f;
-  for (int i = tid; i < 2 * 32 * KX * 20; i += NT) {
-    const int r = (i / 20) % (32 * KX);
-    (&xt[0][0][0])[i] = (__bf16)(r == Din ? 1.0f : 0.0f);      // ones row: db as a column of dW^T
-  }
-  for (int i = tid; i < 2 * H * 20; i += NT) (&ht[0][0][0])[i] = (__bf16)0.0f;
   for (int i = tid; i < 2 * 16 * H; i += NT) (&dhs[0][0][0])[i] = 0.f;
 
   // A fragments of U (dh_rec) and W (dx^T): tile row `col` of cell group gi is unit
@@ -276,11 +272,6 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
       }
     }
   }
-  f32x4_t accW[WGRAD ? TW : 1], accU[WGRAD ? TU : 1];
-#pragma unroll
-  for (int q = 0; q < (WGRAD ? TW : 1); ++q) accW[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < (WGRAD ? TU : 1); ++q) accU[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // ---- streams. internal state (per lane, ring over reverse steps): gates, c_t
   float4 rg[CPL][D];
@@ -299,21 +290,18 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   // branch around memory ops, see the forward). dh: [16][H] float4 granules.
   constexpr int n_gd = 16 * H / 4;
   const int gd = (tid % n_gd) * 4;
-  const int gd_seq = gd / H, gd_k = gd % H;
   const float* dbase = dhout + (size_t)row0 * H + gd;
   const size_t dstep = LAST ? 0 : (size_t)Mp * H;
   float4 rd[D];
-  // x and h_{t-1} tiles (weight gradients)
+  // dz storer: one float4 granule of the [16][4H] tile per thread
+  const int gz_seq = tid / (G4 / 4), gz_c = (tid % (G4 / 4)) * 4;
+  float* zbase = dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
+  const size_t zstep = (size_t)Mp * G4;
+  // dx storer over [16][Din] granules of GR floats (lanes past the tile rewrite granule 0)
   const int n_gx = 16 * Din / GR;
   const int gx = (tid % n_gx) * GR;
   const int gx_seq = gx / Din, gx_k = gx % Din;
-  const float* xbase = x + (size_t)row0 * Din + gx;
   const size_t xstep = (size_t)Mp * Din;
-  Granule<GR> rx[D];
-  const float* hbase = hout + (size_t)row0 * H + gd;
-  const size_t hstep = (size_t)Mp * H;
-  float4 rh[D];
-  // dx storer (same granule map as x); skipped stores go to the scratch time row T
   float* sbase = dx + (size_t)row0 * Din + gx;
 
   // reverse step s <-> time t = T-1-s. Streams for step s are loaded D steps ahead.
@@ -327,33 +315,15 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     }                                                                                       \
     rd[J] = v_;                                                                             \
   }
-#define GQ_TMB_LOAD_XH(J, SS)                                                               \
-  if constexpr (WGRAD) {                                                                    \
-    const int tt_ = max(T - 1 - (SS), 0);                                                   \
-    rx[J].load(xbase + (size_t)tt_ * xstep);                                                \
-    rh[J] = *reinterpret_cast<const float4*>(hbase + (size_t)max(tt_ - 1, 0) * hstep);      \
-  }
-#define GQ_TMB_STAGE_XH(J, BUF, TT)                                                         \
-  if constexpr (WGRAD) {                                                                    \
-    _Pragma("unroll") for (int q = 0; q < GR; ++q) xt[BUF][gx_k + q][gx_seq] = (__bf16)rx[J].v[q]; \
-    const float hm_ = (TT) > 0 ? 1.f : 0.f;    /* h_{-1} = 0 */                             \
-    ht[BUF][gd_k + 0][gd_seq] = (__bf16)(rh[J].x * hm_);                                    \
-    ht[BUF][gd_k + 1][gd_seq] = (__bf16)(rh[J].y * hm_);                                    \
-    ht[BUF][gd_k + 2][gd_seq] = (__bf16)(rh[J].z * hm_);                                    \
-    ht[BUF][gd_k + 3][gd_seq] = (__bf16)(rh[J].w * hm_);                                    \
-  }
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     GQ_TMB_LOAD_STATE(j, j)
     GQ_TMB_LOAD_D(j, j)
-    GQ_TMB_LOAD_XH(j, j)
   }
   __syncthreads();
   // stage step 0 (t = T-1) tiles
   *reinterpret_cast<float4*>(&dhs[0][0][0] + gd) = rd[0];
   GQ_TMB_LOAD_D(0, D)
-  GQ_TMB_STAGE_XH(0, 0, T - 1)
-  GQ_TMB_LOAD_XH(0, D)
   float dc[CPL], dhr[CPL];
 #pragma unroll
   for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
@@ -376,20 +346,10 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
         const float tc = tanhf_fast(rc[cc][j]);
         const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
         dc[cc] = dct * g4.y;
-        const float zi = dct * g4.z * g4.x * (1.f - g4.x);
-        const float zf = dct * cp * g4.y * (1.f - g4.y);
-        const float zg = dct * g4.x * (1.f - g4.z * g4.z);
-        const float zo = dh * tc * g4.w * (1.f - g4.w);
-        zs[p][col][0 * H + u] = (__bf16)zi;
-        zs[p][col][1 * H + u] = (__bf16)zf;
-        zs[p][col][2 * H + u] = (__bf16)zg;
-        zs[p][col][3 * H + u] = (__bf16)zo;
-        if constexpr (WGRAD) {
-          zt[p][0 * H + u][col] = (__bf16)zi;
-          zt[p][1 * H + u][col] = (__bf16)zf;
-          zt[p][2 * H + u][col] = (__bf16)zg;
-          zt[p][3 * H + u][col] = (__bf16)zo;
-        }
+        zs[p][col][0 * H + u] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
+        zs[p][col][1 * H + u] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
+        zs[p][col][2 * H + u] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
+        zs[p][col][3 * H + u] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
       }
       GQ_TMB_LOAD_STATE(j, s + D)
       *reinterpret_cast<float4*>(&dhs[p ^ 1][0][0] + gd) = rd[jn];   // dh tile of step s+1
@@ -408,20 +368,27 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
         }
         dhr[cc] = a0[0] + a1[0];
       }
-      // (b) previous step's dx tile -> HBM (written by all waves before this barrier)
+      // (b) dz tile of this step -> HBM (steps past t = 0 pad the unrolled chunk: scratch row)
+      if constexpr (DZ) {
+        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[p][gz_seq][gz_c]);
+        const int tz = t >= 0 ? t : T;
+        *reinterpret_cast<float4*>(zbase + (size_t)tz * zstep) =
+            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+      }
+      // (c) previous step's dx tile -> HBM (written by all waves before this barrier)
       if constexpr (DX) {
         const int ts = (s >= 1 && s <= T) ? t + 1 : T;
 #pragma unroll
         for (int q = 0; q < GR; ++q) sbase[(size_t)ts * xstep + q] = dxs[p ^ 1][gx_seq][gx_k + q];
       }
-      // (c) dx^T = W dz^T for this step (steps past t = 0 only pad the unrolled chunk)
-      if (DX && t >= 0) {
+      // (d) dx^T = W dz^T for this step
+      if constexpr (DX) {
 #pragma unroll
         for (int q = 0; q < TX; ++q) {
           const int xb = w + NW * q;
           if (xb < NXB) {                           // wave-uniform
             f32x4_t a = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (!DX) continue;
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
               const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
@@ -432,32 +399,6 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
           }
         }
       }
-      // (d) weight gradients: dW^T += dz^T [x|1], dU^T += dz^T h_{t-1}   (K = 16 sequences)
-      if (WGRAD && t >= 0) {
-#pragma unroll
-        for (int q = 0; q < TW; ++q) {
-          const int tq = w + NW * q;
-          if (tq < NRB * NDB) {
-            const int rb = tq / NDB, dbk = tq % NDB;
-            const bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(&zt[p][16 * rb + col][4 * quad]);
-            const bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(&xt[p][16 * dbk + col][4 * quad]);
-            accW[q] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, accW[q], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < TU; ++q) {
-          const int tq = w + NW * q;
-          if (tq < NRB * NHB) {
-            const int rb = tq / NHB, hb = tq % NHB;
-            const bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(&zt[p][16 * rb + col][4 * quad]);
-            const bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(&ht[p][16 * hb + col][4 * quad]);
-            accU[q] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, accU[q], 0, 0, 0);
-          }
-        }
-      }
-      // stage x_{t-1} / h_{t-2} tiles for the next reverse step (garbage past t = 0: unused)
-      GQ_TMB_STAGE_XH(jn, p ^ 1, t - 1)
-      GQ_TMB_LOAD_XH(jn, s + 1 + D)
     }
   }
   __syncthreads();
@@ -466,36 +407,8 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < GR; ++q) sbase[q] = dxs[pl][gx_seq][gx_k + q];
   }
-  if constexpr (WGRAD) {
-    // C layout: lane (col = n, quad) holds rows 4 quad + r of the tile
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      const int tq = w + NW * q;
-      if (tq < NRB * NDB) {
-        const int rb = tq / NDB, dbk = tq % NDB;
-        const int din = 16 * dbk + col;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gr = 16 * rb + 4 * quad + r;
-          if (din < Din) atomicAdd(&dW[(size_t)din * G4 + gr], accW[q][r]);
-          else if (din == Din) atomicAdd(&db[gr], accW[q][r]);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < TU; ++q) {
-      const int tq = w + NW * q;
-      if (tq < NRB * NHB) {
-        const int rb = tq / NHB, hb = tq % NHB;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(&dU[(size_t)(16 * hb + col) * G4 + 16 * rb + 4 * quad + r], accU[q][r]);
-      }
-    }
-  }
 #undef GQ_TMB_LOAD_STATE
 #undef GQ_TMB_LOAD_D
-#undef GQ_TMB_LOAD_XH
-#undef GQ_TMB_STAGE_XH
 }
 
 // =====================================================================================
@@ -525,13 +438,12 @@ static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* 
                      h, g, c, Mp, T, Din);
 }
 
-template <int H, int KX, int GR, bool WG, bool DXF, bool LAST>
-static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* x, const float* h,
-                       const float* W, const float* U, float* dx, float* dW, float* dU, float* db, int Mp, int T,
-                       int Din, hipStream_t st) {
+template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
+static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* W, const float* U,
+                       float* dx, float* dz, int Mp, int T, int Din, hipStream_t st) {
   constexpr int D = 4;
-  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, WG, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh,
-                     g, c, x, h, W, U, dx, dW, dU, db, Mp, T, Din);
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh,
+                     g, c, W, U, dx, dz, Mp, T, Din);
 }
 
 #define GQ_TM_H_DISPATCH(HV, ...)                                  \
@@ -610,25 +522,37 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   const int gr = tm_granule(Din, x.data_ptr());
   TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm_bwd: unsupported shape");
   c10::DeviceGuard guard(x.device());
-  at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, x.options()) : at::empty({0}, x.options());
-  TORCH_CHECK(!need_dx || tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
   const int ntiles = Mp / 16;
   auto st = stream();
-  float* dxp = need_dx ? dx.data_ptr<float>() : nullptr;
-  float* dWp = wg ? dW.data_ptr<float>() : nullptr;
-  float* dUp = wg ? dU.data_ptr<float>() : nullptr;
-  float* dbp = wg ? db.data_ptr<float>() : nullptr;
-#define GQ_TM_BWD_CALL(WGV, DXV, LASTV)                                                                    \
-  tm_bwd_cfg<HH, KXX, GRR, WGV, DXV, LASTV>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(), c.data_ptr<float>(), \
-                                             x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),     \
-                                             U.data_ptr<float>(), dxp, dWp, dUp, dbp, Mp, T, Din, st)
-  GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 1 + 31) / 32, GQ_TM_GR_DISPATCH(gr,
-      if (wg && need_dx) { if (last) GQ_TM_BWD_CALL(true, true, true); else GQ_TM_BWD_CALL(true, true, false); }
-      else if (wg) { if (last) GQ_TM_BWD_CALL(true, false, true); else GQ_TM_BWD_CALL(true, false, false); }
-      else { if (last) GQ_TM_BWD_CALL(false, true, true); else GQ_TM_BWD_CALL(false, true, false); })));
+  if (wg) {
+    // recurrence -> dz (fp32, bf16-exact), then dW/dU/db (+ dx) in one pass over T*Mp rows
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options());
+    GQ_TM_H_DISPATCH(H,
+        if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, st);
+        else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, st));
+    GQ_LAUNCH_CHECK();
+    const long rows = (long)T * Mp;
+    const int ncb = lstm_grads_col_blocks(H);
+    at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
+    lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
+                    need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                    db.data_ptr<float>(), rows, rows, Mp, H, Din, Din, rows * Din, st);
+    if (!need_dx) return dx;
+    return ncb == 1 ? dx[0] : dx.sum(0);
+  }
+  at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
+  TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
+#define GQ_TM_BWD_CALL(LASTV)                                                                               \
+  tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),          \
+                                               c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
+                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, st)
+  GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
+      if (last) GQ_TM_BWD_CALL(true); else GQ_TM_BWD_CALL(false))));
 #undef GQ_TM_BWD_CALL
   GQ_LAUNCH_CHECK();
-  return need_dx ? dx.narrow(0, 0, T) : dx;
+  return dx.narrow(0, 0, T);
 }
 
 }  // namespace gq

@@ -30,8 +30,9 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor(b!) db, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) dalpha) -> Tensor");
   // flat-buffer optimiser (adam.hip)
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
-        "float beta2, float eps, float grad_scale, float weight_decay) -> ()");
+        "float beta2, float eps, float grad_scale, float weight_decay, Tensor? guard=None) -> ()");
   m.def("nonfinite_count(Tensor x) -> Tensor");
+  m.def("grad_guard(Tensor g, Tensor(a!) state, Tensor(b!) step) -> ()");
   // metrics (metrics.hip)
   m.def("score_histogram(Tensor scores, Tensor labels, Tensor mask, int bins) -> Tensor");
   // fused dense head + weighted BCE + metrics (head.hip)

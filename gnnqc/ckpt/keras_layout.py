@@ -55,7 +55,7 @@ def keras_tensors(model, optimizer=None) -> Dict[str, object]:
         out["model_type" + SUFFIX] = str(getattr(model, "model_type", model.ds_type))
         out["model_normalization" + SUFFIX] = str(model.model_normalization)
     if optimizer is not None:
-        out["optimizer/_iterations" + SUFFIX] = np.asarray(optimizer.iterations, dtype=np.int64)
+        out["optimizer/_iterations" + SUFFIX] = np.asarray(int(optimizer.step_t.item()), dtype=np.int64)
         out["optimizer/_learning_rate" + SUFFIX] = np.asarray(optimizer.lr, dtype=np.float32)
         slots = optimizer.slots() if hasattr(optimizer, "slots") else []
         if len(slots) == 2:

@@ -77,7 +77,9 @@ def cmd_train(args):
         out_dir = (mc.baseline_model.model_path if baseline else mc.model_path)
         hist, model = train_model(model, mc, pc, tl, vl if len(va) else None, baseline=baseline, store=store,
                                   checkpoint_path=os.path.join(out_dir, "checkpoint"),
-                                  log_path=os.path.join(out_dir, "train_log.jsonl"))
+                                  log_path=os.path.join(out_dir, "train_log.jsonl"),
+                                  resume_dir=os.path.join(out_dir, "resume") if args.resume_every else None,
+                                  resume=args.resume)
         if D.is_main():
             save_model(model, out_dir, preproc_config=pc)
         if len(te):
@@ -170,6 +172,9 @@ def main(argv=None):
     p = add_common(sub.add_parser("train", help="train GCN (or baseline), save, evaluate on test"))
     p.add_argument("--baseline", action="store_true")
     p.add_argument("--both", action="store_true")
+    p.add_argument("--resume", action="store_true",
+                   help="continue from <model_path>/resume/resume.pt if present (e.g. under torchrun --max-restarts)")
+    p.add_argument("--resume-every", type=int, default=1, help="full-state checkpoint every K epochs (0: off)")
     p.set_defaults(fn=cmd_train)
     p = add_common(sub.add_parser("evaluate", help="threshold on val + test metrics of a saved model"))
     p.add_argument("--model-dir", required=True)

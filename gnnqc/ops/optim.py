@@ -8,7 +8,13 @@ a second one. Consequences on MI355X:
   753 KB buffer (no per-tensor launches, no bucketing metadata);
 * the Adam update is one HIP kernel over the whole buffer;
 * lr / step live on the device, so the optimiser launch can be captured in a HIP
-  graph and replayed while the LR schedule changes.
+  graph and replayed while the LR schedule changes;
+* non-finite guard (on by default): one extra kernel checks the
+  (all-reduced) gradient buffer; a step with NaN/Inf gradients is skipped on the
+  device - parameters, slots and the bias-correction step stay untouched - and
+  counted in ``skipped_steps``. It lives inside the captured graph, so it costs no
+  host synchronisation. In DP the all-reduce spreads a NaN to every rank, so all
+  ranks skip the same step.
 
 Optimisers by name like ``libs/fit_model.py:71-74``: adam (Keras eps 1e-7,
 "epsilon-hat" update), sgd, rmsprop (Keras defaults rho .9, eps 1e-7).
@@ -44,12 +50,38 @@ def flatten_parameters(params: Iterable[torch.nn.Parameter], align: int = 4):
 class FlatOptimizer:
     """Base: owns the flat buffers of a module's trainables."""
 
-    def __init__(self, params, lr: float):
+    def __init__(self, params, lr: float, guard: bool = True):
         self.flat_p, self.flat_g, self.params = flatten_parameters(params)
         dev = self.flat_p.device
         self.lr_t = torch.tensor([float(lr)], device=dev, dtype=torch.float32)
-        self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
-        self.iterations = 0
+        self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)   # applied steps (bias correction)
+        self.iterations = 0                                              # attempted steps (host)
+        self.guard = bool(guard)
+        # [nonfinite count, ticket, ok flag, skipped steps] (see adam.hip grad_guard)
+        self.guard_state = torch.zeros(4, device=dev, dtype=torch.int32)
+        self.guard_state[2] = 1
+
+    @property
+    def skipped_steps(self) -> int:
+        return int(self.guard_state[3].item())
+
+    def _begin_step(self):
+        """Advance the step counter; with the guard, only if the gradients are finite.
+        Returns the device ok flag (bool tensor) for eager updates, or None."""
+        self.iterations += 1
+        if not self.guard:
+            self.step_t.add_(1.0)
+            return None
+        from . import use_hip
+        if use_hip(self.flat_g):
+            from ..utils.native import hip_ops
+            hip_ops().grad_guard(self.flat_g, self.guard_state, self.step_t)
+            return self.guard_state[2:3].bool()
+        ok = torch.isfinite(self.flat_g).all().reshape(1)
+        self.step_t.add_(ok.float())
+        self.guard_state[2:3].copy_(ok.int())
+        self.guard_state[3:4].add_((~ok).int())
+        return ok
 
     @property
     def lr(self) -> float:
@@ -85,40 +117,43 @@ class FlatOptimizer:
         return out
 
     def state_dict(self):
-        return {"lr": self.lr, "iterations": self.iterations}
+        return {"lr": self.lr, "iterations": self.iterations, "step": float(self.step_t.item()),
+                "skipped_steps": self.skipped_steps}
 
     def load_state_dict(self, sd):
         self.lr = sd["lr"]
         self.iterations = int(sd["iterations"])
-        self.step_t.fill_(float(self.iterations))
+        self.step_t.fill_(float(sd.get("step", self.iterations)))
+        self.guard_state[3] = int(sd.get("skipped_steps", 0))
 
 
 class FlatAdam(FlatOptimizer):
     def __init__(self, params, lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-7,
-                 weight_decay: float = 0.0):
-        super().__init__(params, lr)
+                 weight_decay: float = 0.0, guard: bool = True):
+        super().__init__(params, lr, guard)
         self.beta1, self.beta2, self.eps, self.wd = beta1, beta2, eps, weight_decay
         self.m = torch.zeros_like(self.flat_p)
         self.v = torch.zeros_like(self.flat_p)
 
     def step(self, grad_scale: float = 1.0):
         from . import use_hip
-        self.step_t.add_(1.0)
-        self.iterations += 1
+        ok = self._begin_step()
         if use_hip(self.flat_p):
             from ..utils.native import hip_ops
             hip_ops().adam_step(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
-                                self.beta2, self.eps, float(grad_scale), self.wd)
+                                self.beta2, self.eps, float(grad_scale), self.wd,
+                                self.guard_state if self.guard else None)
             return
         with torch.no_grad():
             g = self.flat_g * grad_scale
             if self.wd:
                 g = g + self.wd * self.flat_p
-            self.m.mul_(self.beta1).add_(g * (1 - self.beta1))
-            self.v.mul_(self.beta2).add_(g * g * (1 - self.beta2))
+            m = self.m * self.beta1 + g * (1 - self.beta1)
+            v = self.v * self.beta2 + g * g * (1 - self.beta2)
             t = self.step_t
             alpha = self.lr_t * torch.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
-            self.flat_p.sub_(alpha * self.m / (torch.sqrt(self.v) + self.eps))
+            p = self.flat_p - alpha * m / (torch.sqrt(v) + self.eps)
+            _commit(ok, (self.m, m), (self.v, v), (self.flat_p, p))
 
     def state_dict(self):
         sd = super().state_dict()
@@ -141,15 +176,14 @@ class FlatSGD(FlatOptimizer):
         self.buf = torch.zeros_like(self.flat_p) if momentum else None
 
     def step(self, grad_scale: float = 1.0):
-        self.step_t.add_(1.0)
-        self.iterations += 1
+        ok = self._begin_step()
         with torch.no_grad():
             g = self.flat_g * grad_scale
             if self.buf is not None:
-                self.buf.mul_(self.momentum).sub_(self.lr_t * g)
-                self.flat_p.add_(self.buf)
+                buf = self.buf * self.momentum - self.lr_t * g
+                _commit(ok, (self.buf, buf), (self.flat_p, self.flat_p + buf))
             else:
-                self.flat_p.sub_(self.lr_t * g)
+                _commit(ok, (self.flat_p, self.flat_p - self.lr_t * g))
 
     def slots(self):
         return [self.buf] if self.buf is not None else []
@@ -162,26 +196,37 @@ class FlatRMSprop(FlatOptimizer):
         self.ms = torch.zeros_like(self.flat_p)
 
     def step(self, grad_scale: float = 1.0):
-        self.step_t.add_(1.0)
-        self.iterations += 1
+        ok = self._begin_step()
         with torch.no_grad():
             g = self.flat_g * grad_scale
-            self.ms.mul_(self.rho).add_(g * g * (1 - self.rho))
-            self.flat_p.sub_(self.lr_t * g / (torch.sqrt(self.ms) + self.eps))
+            ms = self.ms * self.rho + g * g * (1 - self.rho)
+            _commit(ok, (self.ms, ms), (self.flat_p, self.flat_p - self.lr_t * g / (torch.sqrt(ms) + self.eps)))
 
     def slots(self):
         return [self.ms]
 
 
-def make_optimizer(name: str, params, lr: float):
+def _commit(ok, *pairs):
+    """dst <- new for each (dst, new) pair, unless the device flag ``ok`` is False."""
+    for dst, new in pairs:
+        if ok is None:
+            dst.copy_(new)
+        else:
+            dst.copy_(torch.where(ok, new, dst))
+
+
+def make_optimizer(name: str, params, lr: float, guard: bool = True):
     name = (name or "adam").lower()
     if name == "adam":
-        return FlatAdam(params, lr)
+        return FlatAdam(params, lr, guard=guard)
     if name == "sgd":
-        return FlatSGD(params, lr)
-    if name == "rmsprop":
-        return FlatRMSprop(params, lr)
-    raise ValueError(f"unknown optimizer {name}")
+        o = FlatSGD(params, lr)
+    elif name == "rmsprop":
+        o = FlatRMSprop(params, lr)
+    else:
+        raise ValueError(f"unknown optimizer {name}")
+    o.guard = bool(guard)
+    return o
 
 
 __all__ = ["flatten_parameters", "FlatAdam", "FlatSGD", "FlatRMSprop", "make_optimizer"]

@@ -22,6 +22,9 @@ from ..ops.lstm import direct_grad_accumulation
 from ..ops.metrics import score_histogram
 from ..parallel import dist as D
 from .loss import weighted_bce_with_logits
+from .resilience import FaultInjector
+
+_rf = torch.autograd.profiler.record_function
 
 HIST_BINS = 1001
 
@@ -87,13 +90,20 @@ class Trainer:
         self.graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
         self.last_loss = torch.zeros((), device=self.device)
+        self.global_step = 0
+        self.fault = FaultInjector.from_env()
+        # NaN poisoning of the gradient (fault injection only: no extra kernel otherwise)
+        self.poison = torch.zeros(1, device=self.device) if (self.fault and self.fault.poisons) else None
+        # HIP-event timing of the DP all-reduce (read once per epoch)
+        self._comm_events = []
 
     # ---------------------------------------------------------------- body
     def _loss(self, wids, metrics: Optional["MetricAccumulator"] = None):
         """(total, loss, logits, batch). With a fused-head model the loss, logits and
         the metric update come out of one HIP kernel (``gnnqc.ops.head``)."""
-        b = self.store.gather(wids)
-        inputs = b.model_inputs(self.ds_type, self.baseline)
+        with _rf("gnnqc.gather"):
+            b = self.store.gather(wids)
+            inputs = b.model_inputs(self.ds_type, self.baseline)
         spec = self.model.head_spec() if hasattr(self.model, "head_spec") else None
         if spec is not None:
             dense, dense2, dense_out, a1, a2 = spec
@@ -111,12 +121,16 @@ class Trainer:
 
     def _body(self, wids, with_opt: bool):
         self.opt.zero_grad()
-        total, loss, z, b = self._loss(wids, self.train_metrics)
-        with direct_grad_accumulation(True):
+        with _rf("gnnqc.forward"):
+            total, loss, z, b = self._loss(wids, self.train_metrics)
+        with _rf("gnnqc.backward"), direct_grad_accumulation(True):
             total.backward()
+        if self.poison is not None:
+            self.opt.flat_g[:1].add_(self.poison)
         self.last_loss.copy_(loss.detach())
         if with_opt:
-            self.opt.step(grad_scale=1.0)
+            with _rf("gnnqc.optimizer"):
+                self.opt.step(grad_scale=1.0)
 
     def _capture(self):
         # warm up on a side stream (allocator + lazy init), then capture
@@ -129,8 +143,10 @@ class Trainer:
                 self._body(self.static_wids, with_opt=False)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
+        it0 = self.opt.iterations
         with torch.cuda.graph(self.graph):
             self._body(self.static_wids, with_opt=with_opt)
+        self.opt.iterations = it0          # capture runs nothing; replays count steps
         # undo warm-up side effects (BN running stats, metric sums)
         with torch.no_grad():
             for k, v in self.model.state_dict().items():
@@ -140,6 +156,16 @@ class Trainer:
 
     def train_step(self, wids: torch.Tensor):
         self.model.train()
+        step = self.global_step + 1
+        if self.poison is not None:
+            self.poison.fill_(float("nan") if self.fault.nan_now(step) else 0.0)
+        self._step(wids)
+        self.global_step = step
+        if self.fault is not None:
+            self.fault.after_step(step)
+        return self.last_loss
+
+    def _step(self, wids):
         if self.use_graph:
             if self.graph is None:
                 self._capture()
@@ -147,23 +173,43 @@ class Trainer:
             self.graph.replay()
             if self.world == 1:
                 self.opt.iterations += 1
-                return self.last_loss
+                return
         else:
             self._body(wids.to(self.device), with_opt=self.world == 1)
             if self.world == 1:
-                return self.last_loss
+                return
         # data parallel: one all-reduce of the flat gradient buffer, then Adam
-        D.all_reduce_(self.opt.flat_g)
-        self.opt.step(grad_scale=1.0 / self.world)
-        return self.last_loss
+        with _rf("gnnqc.allreduce"):
+            if self.device.type == "cuda":
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                D.all_reduce_(self.opt.flat_g)
+                e1.record()
+                self._comm_events.append((e0, e1))
+            else:
+                D.all_reduce_(self.opt.flat_g)
+        with _rf("gnnqc.optimizer"):
+            self.opt.step(grad_scale=1.0 / self.world)
 
     # ---------------------------------------------------------------- epoch helpers
     def train_epoch(self, loader, epoch: int) -> Dict[str, float]:
+        import time
         loader.set_epoch(epoch)
         self.train_metrics.reset()
+        self._comm_events = []
+        skipped0 = self.opt.skipped_steps
+        steps0 = self.global_step
+        t0 = time.perf_counter()
         for row in loader.batch_ids():
             self.train_step(row)
-        return self.train_metrics.result()
+        logs = self.train_metrics.result()            # device -> host: synchronises the epoch
+        dt = time.perf_counter() - t0
+        nsteps = self.global_step - steps0
+        logs["skipped_steps"] = float(self.opt.skipped_steps - skipped0)
+        logs["windows_per_sec"] = nsteps * loader.batch_size * self.world / max(dt, 1e-9)
+        if self._comm_events:
+            logs["allreduce_us"] = 1e3 * sum(a.elapsed_time(b) for a, b in self._comm_events) / len(self._comm_events)
+        return logs
 
     @torch.no_grad()
     def evaluate(self, loader, prefix: str = "val_") -> Dict[str, float]:

@@ -89,6 +89,27 @@ class EarlyStopping(Callback):
                 if self.restore and self.best_state is not None:
                     state["model"].load_state_dict(self.best_state)
 
+    def state_dict(self):
+        return {"best": float(self.best), "wait": int(self.wait),
+                "best_state": {k: v.cpu() for k, v in self.best_state.items()} if self.best_state else None}
+
+    def load_state_dict(self, sd):
+        self.best, self.wait = float(sd["best"]), int(sd["wait"])
+        self.best_state = sd.get("best_state")
+
+
+class ResumeCallback(Callback):
+    """Per-epoch full-state checkpoint for ``train_model(resume=...)``."""
+
+    def __init__(self, path: str, every: int = 1):
+        self.path, self.every = path, max(1, int(every))
+
+    def on_epoch_end(self, epoch, logs, state):
+        if (epoch + 1) % self.every == 0:
+            from .resilience import save_resume
+            save_resume(self.path, state["model"], state["optimizer"], epoch, state.get("history"),
+                        state.get("callbacks", ()))
+
 
 class ModelCheckpoint(Callback):
     def __init__(self, path: str, monitor: str = "val_loss", save_best_only: bool = True, preproc_config=None):
@@ -180,17 +201,20 @@ def train_model(model, model_config, preproc_config, train_dataset_batched, val_
                 baseline: bool = False, classes_weights=None, labels=None, CV: bool = False,
                 split_numb: Optional[int] = None, store=None, callbacks: Optional[List[Callback]] = None,
                 checkpoint_path: Optional[str] = None, log_path: Optional[str] = None, use_graph: Optional[bool] = None,
-                verbose: int = 1):
-    """Fit ``model`` on a :class:`~gnnqc.data.store.DeviceLoader` (reference signature + extras)."""
+                verbose: int = 1, resume_dir: Optional[str] = None, resume: bool = False):
+    """Fit ``model`` on a :class:`~gnnqc.data.store.DeviceLoader` (reference signature + extras).
+
+    ``resume_dir``: write a full-state ``resume.pt`` there after every epoch;
+    ``resume=True``: continue from it if present (see :mod:`gnnqc.train.resilience`)."""
     store = store or train_dataset_batched.store
     if classes_weights is None:
         if labels is None and model_config.get("weight_classes", {}).get("calculate", False):
             labels = store.labels(train_dataset_batched.ids).cpu().numpy()
         classes_weights = calculate_weights(model_config, labels)
-    opt = make_optimizer(model_config.get("optimizer", "adam"), model.parameters(),
-                         model_config.get("learning_rate", 1e-3))
-    D.broadcast_module(model)
     runtime = model_config.get("runtime") or {}
+    opt = make_optimizer(model_config.get("optimizer", "adam"), model.parameters(),
+                         model_config.get("learning_rate", 1e-3), guard=bool(runtime.get("nonfinite_guard", True)))
+    D.broadcast_module(model)
     if use_graph is None:
         use_graph = bool(runtime.get("hip_graphs", True))
     trainer = Trainer(model, store, opt, classes_weights, baseline, use_graph=use_graph,
@@ -214,11 +238,23 @@ def train_model(model, model_config, preproc_config, train_dataset_batched, val_
             if verbose:
                 print(f"wandb disabled: {e}")
     cbs += list(callbacks or [])
+    resume_dir = resume_dir or runtime.get("resume_dir")
+    saver = ResumeCallback(resume_dir, runtime.get("resume_every", 1)) if resume_dir else None
     history = History()
-    state = {"model": model, "optimizer": opt, "stop": False, "trainer": trainer}
+    state = {"model": model, "optimizer": opt, "stop": False, "trainer": trainer, "history": history,
+             "callbacks": cbs}
+    start_epoch = 0
+    if resume and resume_dir:
+        from .resilience import load_resume, restore
+        rs = load_resume(resume_dir)
+        if rs is not None:
+            start_epoch = restore(rs, model, opt, history, cbs)
+            trainer.global_step = opt.iterations
+            if verbose and D.is_main():
+                print(f"resumed from {resume_dir} at epoch {start_epoch + 1}", flush=True)
     for cb in cbs:
         cb.on_train_begin(state)
-    for epoch in range(int(model_config.get("epochs", 10))):
+    for epoch in range(start_epoch, int(model_config.get("epochs", 10))):
         for cb in cbs:
             cb.on_epoch_begin(epoch, state)
         t0 = time.time()
@@ -230,6 +266,8 @@ def train_model(model, model_config, preproc_config, train_dataset_batched, val_
         for cb in cbs:
             cb.on_epoch_end(epoch, logs, state)
         history.append(epoch, logs)
+        if saver is not None:     # after every callback and the history: a consistent snapshot
+            saver.on_epoch_end(epoch, logs, state)
         if verbose and D.is_main():
             shown = " - ".join(f"{k}: {v:.4f}" for k, v in logs.items() if k in
                                ("loss", "auc", "recall", "precision", "val_loss", "val_auc", "lr", "epoch_time_s"))
@@ -243,4 +281,4 @@ def train_model(model, model_config, preproc_config, train_dataset_batched, val_
 
 
 __all__ = ["train_model", "calculate_weights", "History", "Callback", "EarlyStopping", "ModelCheckpoint",
-           "LearningRateScheduler", "JSONLLogger", "WandbCallback", "MCCCustom"]
+           "LearningRateScheduler", "JSONLLogger", "WandbCallback", "MCCCustom", "ResumeCallback"]

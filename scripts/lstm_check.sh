@@ -11,3 +11,7 @@ GNNQC_NO_TM=1 timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $OUT/be
 tail -1 $OUT/bench_notm.log | cut -c1-200
 tail -1 $OUT/bench.log | cut -c1-250
 cat $OUT/micro_new.jsonl | grep '"M": 128'
+ROOT=$(pwd)
+export TMPDIR=/tmp
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5) > $OUT/prof.log 2>&1
+echo "prof rc=$?"
