@@ -38,6 +38,15 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// Deterministic mode: kernels whose cross-workgroup reductions use float
+// atomics launch a single workgroup per output block instead, so every gradient element
+// receives exactly one atomic (onto zero) and training is bitwise reproducible.
+// Slower; for debugging / reproducibility runs. Set via gnnqc.ops.set_deterministic.
+inline bool& deterministic_mode() {
+  static bool v = false;
+  return v;
+}
+
 #define GQ_CHECK(cond, msg) TORCH_CHECK(cond, "gnnqc: ", msg)
 #define GQ_LAUNCH_CHECK() do { hipError_t e__ = hipGetLastError(); TORCH_CHECK(e__ == hipSuccess, "gnnqc kernel launch failed: ", hipGetErrorString(e__)); } while (0)
 

@@ -222,7 +222,7 @@ at::Tensor gcn_stats(const at::Tensor& x, const at::Tensor& mask) {
   c10::DeviceGuard guard(x.device());
   at::Tensor out = at::zeros({Cin + Cin * Cin + 1}, x.options().dtype(at::kDouble));
   const long rows = (long)B * T * N;
-  GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_stats_kernel<CIN>, dim3(grid_for(rows, 256, 512)), dim3(256), 0,
+  GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_stats_kernel<CIN>, dim3(deterministic_mode() ? 1 : grid_for(rows, 256, 512)), dim3(256), 0,
                                           stream(), x.data_ptr<float>(), mask.data_ptr<float>(),
                                           out.data_ptr<double>(), B, T, N));
   GQ_LAUNCH_CHECK();

@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 
 static int head_grid(int R) {
   const int nt = (R + HT - 1) / HT;
-  return std::max(1, std::min(nt, 256));
+  return deterministic_mode() ? 1 : std::max(1, std::min(nt, 256));
 }
 
 #define GQ_HEAD_F_DISPATCH(F_, ...)                                 \

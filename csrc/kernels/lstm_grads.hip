@@ -198,7 +198,7 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
   const int ncb = (4 * H) / GR_CB;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
   // enough workgroups to fill the chip, few enough that the final atomics stay cheap
-  const int splits = (int)std::max<long>(1, std::min<long>(ntiles, std::max(32, 256 / ncb)));
+  const int splits = deterministic_mode() ? 1 : (int)std::max<long>(1, std::min<long>(ntiles, std::max(32, 256 / ncb)));
   dim3 grid(ncb, splits);
   const int DT = (Din + 1 + 15) / 16;
 #define GQ_GR_H(HH)                                                                                              \

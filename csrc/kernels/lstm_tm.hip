@@ -382,8 +382,9 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < GR; ++q) sbase[(size_t)ts * xstep + q] = dxs[p ^ 1][gx_seq][gx_k + q];
       }
-      // (d) dx^T = W dz^T for this step
-      if constexpr (DX) {
+      // (d) dx^T = W dz^T for this step (steps past t = 0 only pad the unrolled chunk and
+      // must not overwrite the t = 0 tile the epilogue stores; no memory op in the branch)
+      if (DX && t >= 0) {
 #pragma unroll
         for (int q = 0; q < TX; ++q) {
           const int xb = w + NW * q;

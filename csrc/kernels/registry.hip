@@ -4,7 +4,20 @@
 #include <ATen/ATen.h>
 #include <torch/library.h>
 
+#include "common.h"
+
+namespace gq {
+// returns the previous value (see deterministic_mode in common.h)
+static bool set_deterministic(bool flag) {
+  const bool old = deterministic_mode();
+  deterministic_mode() = flag;
+  return old;
+}
+}  // namespace gq
+
 TORCH_LIBRARY(gnnqc, m) {
+  // process-wide switches (catch-all kernels: no tensor arguments)
+  m.def("set_deterministic(bool flag) -> bool", &gq::set_deterministic);
   // persistent LSTM recurrence (lstm.hip)
   m.def("lstm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train, bool bf16) -> Tensor[]");
   m.def("lstm_bwd(Tensor dh, Tensor gates, Tensor cseq, Tensor U, bool bf16) -> Tensor");
@@ -28,6 +41,10 @@ TORCH_LIBRARY(gnnqc, m) {
         "bool training, float momentum, float eps) -> Tensor");
   m.def("gcn_bwd_finalize(Tensor acc, Tensor S, Tensor W, Tensor b, Tensor st, bool training, Tensor(a!) dW, "
         "Tensor(b!) db, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) dalpha) -> Tensor");
+  // Conv1D + LeakyReLU (+ GAP) implicit GEMM (conv1d.hip)
+  m.def("conv1d_fwd(Tensor x, Tensor W, Tensor b, float alpha, bool gap, bool store_y) -> Tensor[]");
+  m.def("conv1d_bwd(Tensor dy, Tensor y, Tensor x, Tensor W, float alpha, bool gap, Tensor(a!) dW, "
+        "Tensor(b!) db, bool need_dx) -> Tensor");
   // flat-buffer optimiser (adam.hip)
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
         "float beta2, float eps, float grad_scale, float weight_decay, Tensor? guard=None) -> ()");

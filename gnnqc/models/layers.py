@@ -125,27 +125,35 @@ class LSTM(nn.Module):
 
 
 class Conv1D(nn.Module):
-    """Keras Conv1D(filters, kernel_size, padding='same') on [M, T, in] (channels last)."""
+    """Keras Conv1D(filters, kernel_size, padding='same') on [M, T, in] (channels last).
+
+    ``forward_act`` fuses the following LeakyReLU (and optionally the
+    GlobalAveragePooling1D) into one HIP kernel on the GPU (``gnnqc.ops.conv``)."""
 
     def __init__(self, in_features: int, filters: int, kernel_size: int, padding: str = "same",
-                 regularizer: Optional[float] = None):
+                 regularizer: Optional[float] = None, compute_bf16: bool = True):
         super().__init__()
         self.kernel_size = int(kernel_size)
         self.padding = padding
         self.regularizer = regularizer
+        self.compute_bf16 = compute_bf16
         self.kernel = nn.Parameter(torch.empty(self.kernel_size, in_features, filters))
         self.bias = nn.Parameter(torch.zeros(filters))
         glorot_uniform_(self.kernel, self.kernel_size * in_features, self.kernel_size * filters)
 
     def forward(self, x):
-        k = self.kernel_size
-        xt = x.transpose(1, 2)                      # [M, in, T]
+        return self.forward_act(x, 1.0)
+
+    def forward_act(self, x, alpha: float = 1.0, gap: bool = False):
+        from ..ops.conv import conv1d_act, conv1d_act_eager
+        if self.padding == "same" and self.compute_bf16:
+            return conv1d_act(x, self.kernel, self.bias, alpha, gap)
         if self.padding == "same":
-            left = (k - 1) // 2
-            xt = F.pad(xt, (left, k - 1 - left))
-        w = self.kernel.permute(2, 1, 0)            # [out, in, k]
-        y = F.conv1d(xt, w, self.bias)
-        return y.transpose(1, 2)
+            return conv1d_act_eager(x, self.kernel, self.bias, alpha, gap)
+        y = F.conv1d(x.transpose(1, 2), self.kernel.permute(2, 1, 0), self.bias).transpose(1, 2)  # 'valid'
+        if alpha != 1.0:
+            y = F.leaky_relu(y, alpha)
+        return y.mean(1) if gap else y
 
     def reg_loss(self):
         return self.regularizer * (self.kernel ** 2).sum() if self.regularizer else None

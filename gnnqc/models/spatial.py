@@ -55,7 +55,7 @@ class SensorsTimeLayer(nn.Module):
         if layer_type == "lstm":
             self.time_layer = LSTM(in_features, units, activation, True, regularizer, compute_bf16)
         else:
-            self.time_layer = Conv1D(in_features, units, kernel_size, regularizer=regularizer)
+            self.time_layer = Conv1D(in_features, units, kernel_size, regularizer=regularizer, compute_bf16=compute_bf16)
             self.activation = PReLU(units)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

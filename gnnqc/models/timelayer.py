@@ -47,8 +47,8 @@ class TimeLayer(nn.Module):
         else:
             if kernel_size is None:
                 raise ValueError("CNN TimeLayer needs kernel_size")
-            self.time1 = Conv1D(in_features, f, kernel_size, regularizer=regularizer)
-            self.time2 = Conv1D(f, f, kernel_size, regularizer=regularizer)
+            self.time1 = Conv1D(in_features, f, kernel_size, regularizer=regularizer, compute_bf16=compute_bf16)
+            self.time2 = Conv1D(f, f, kernel_size, regularizer=regularizer, compute_bf16=compute_bf16)
             self.leakyrelu1 = LeakyReLU(alpha)
             self.leakyrelu2 = LeakyReLU(alpha)
             self.max_pooling = MaxPooling1D(pool_size)
@@ -56,13 +56,14 @@ class TimeLayer(nn.Module):
             prev = f
             for i in range(n_stacks):
                 u = f * 2 ** (i + 1)
-                self.time_layers.append(Conv1D(prev, u, kernel_size, regularizer=regularizer))
+                self.time_layers.append(Conv1D(prev, u, kernel_size, regularizer=regularizer, compute_bf16=compute_bf16))
                 self.leakyrelu_layers.append(LeakyReLU(alpha))
-                self.time_layers.append(Conv1D(u, u, kernel_size, regularizer=regularizer))
+                self.time_layers.append(Conv1D(u, u, kernel_size, regularizer=regularizer, compute_bf16=compute_bf16))
                 self.leakyrelu_layers.append(LeakyReLU(alpha))
                 self.pooling_layers.append(MaxPooling1D(cnn_stack_pool or pool_size))
                 prev = u
-            self.time4 = Conv1D(prev, f * 2 ** (n_stacks + 1), kernel_size, regularizer=regularizer)
+            self.time4 = Conv1D(prev, f * 2 ** (n_stacks + 1), kernel_size, regularizer=regularizer,
+                               compute_bf16=compute_bf16)
             self.leakyrelu3 = LeakyReLU(alpha)
             self.global_pooling = GlobalAveragePooling1D()
 
@@ -105,6 +106,18 @@ class TimeLayer(nn.Module):
             h = mod(h)
         return h
 
+    def _forward_cnn(self, x: torch.Tensor) -> torch.Tensor:
+        """CNN branch (``create_model.py:80-101``): every Conv1D + LeakyReLU pair is one fused
+        kernel on the GPU, and the last one also folds in the GlobalAveragePooling1D."""
+        x1 = self.time1.forward_act(x, self.leakyrelu1.alpha)
+        x1 = self.time2.forward_act(x1, self.leakyrelu2.alpha)
+        x1 = self.max_pooling(x1)
+        for i in range(len(self.pooling_layers)):
+            x1 = self.time_layers[2 * i].forward_act(x1, self.leakyrelu_layers[2 * i].alpha)
+            x1 = self.time_layers[2 * i + 1].forward_act(x1, self.leakyrelu_layers[2 * i + 1].alpha)
+            x1 = self.pooling_layers[i](x1)
+        return self.time4.forward_act(x1, self.leakyrelu3.alpha, gap=True)
+
     def _tm_ok(self, x: torch.Tensor) -> bool:
         from ..ops.lstm import tm_eligible
         return (self.layer_type == "lstm" and self.time1.activation == "tanh"
@@ -114,26 +127,16 @@ class TimeLayer(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._tm_ok(x):
             return self._forward_tm(x)
-        cnn = self.layer_type != "lstm"
+        if self.layer_type != "lstm":
+            return self._forward_cnn(x)
         x1 = self.time1(x)
-        if cnn:
-            x1 = self.leakyrelu1(x1)
         x1 = self.time2(x1)
-        if cnn:
-            x1 = self.leakyrelu2(x1)
         x1 = self.max_pooling(x1)
         for i in range(len(self.pooling_layers)):
             x1 = self.time_layers[2 * i](x1)
-            if cnn:
-                x1 = self.leakyrelu_layers[2 * i](x1)
             x1 = self.time_layers[2 * i + 1](x1)
-            if cnn:
-                x1 = self.leakyrelu_layers[2 * i + 1](x1)
             x1 = self.pooling_layers[i](x1)
         x1 = self.time4(x1)
-        if cnn:
-            x1 = self.leakyrelu3(x1)
-            x1 = self.global_pooling(x1)
         return x1
 
 

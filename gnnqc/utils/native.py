@@ -59,6 +59,8 @@ def hip_available() -> bool:
             if os.path.exists(HIP_LIB):
                 torch.ops.load_library(HIP_LIB)
                 _hip_loaded = True
+                if os.environ.get("GNNQC_DETERMINISTIC", "0") == "1":
+                    torch.ops.gnnqc.set_deterministic(True)
             else:
                 _hip_loaded = False
     return _hip_loaded

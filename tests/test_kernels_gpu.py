@@ -362,3 +362,54 @@ def test_timelayer_time_major_matches_sequence_major(cuda_device, monkeypatch):
         assert err < 6e-2, err
     for a, b_ in zip([dx3] + g3, [dx2] + g2):
         torch.testing.assert_close(a, b_, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("k,cin,cout,T,gap", [(5, 18, 16, 181, False), (3, 16, 32, 60, False), (5, 32, 64, 20, False),
+                                              (5, 64, 128, 6, True), (1, 7, 16, 13, False), (4, 16, 16, 9, True),
+                                              (7, 3, 24, 50, False)])
+def test_conv1d_act_matches_eager(cuda_device, k, cin, cout, T, gap):
+    """Fused Conv1D(same)+LeakyReLU(+GAP) HIP kernels vs fp64 eager: output, dx, dW, db."""
+    from gnnqc.ops.conv import conv1d_act, conv1d_act_eager, hip_conv_supported
+    assert hip_conv_supported(k, cin, cout)
+    gen = torch.Generator().manual_seed(k * 1000 + cin * 10 + cout)
+    M = 37
+    x = torch.randn(M, T, cin, generator=gen)
+    W = torch.randn(k, cin, cout, generator=gen) * (1.0 / (k * cin) ** 0.5)
+    b = torch.randn(cout, generator=gen) * 0.1
+    xs = [t.to(cuda_device).requires_grad_(True) for t in (x, W, b)]
+    out = conv1d_act(*xs, alpha=0.3, gap=gap)
+    ref_in = [t.double().requires_grad_(True) for t in (x, W, b)]
+    ref = conv1d_act_eager(*ref_in, alpha=0.3, gap=gap)
+    assert out.shape == ref.shape
+    err = (out.double().cpu() - ref).abs().max().item()
+    assert err < 3e-2 * (ref.abs().max().item() + 1e-3), err
+    g = torch.randn(ref.shape, generator=gen)
+    out.backward(g.to(cuda_device))
+    ref.backward(g.double())
+    for got, r, name in zip(xs, ref_in, ("x", "W", "b")):
+        e = (got.grad.double().cpu() - r.grad).abs().max().item()
+        scale = r.grad.abs().max().item() + 1e-6
+        assert e / scale < 3e-2, f"grad {name}: rel err {e / scale}"
+
+
+def test_timelayer_cnn_branch_hip_vs_eager(cuda_device, monkeypatch):
+    """CNN TimeLayer: fused HIP conv kernels vs the eager path on the same weights."""
+    from gnnqc.models.timelayer import TimeLayer
+    torch.manual_seed(0)
+    tl = TimeLayer(18, 16, 2, "cnn", kernel_size=5, pool_size=3).to(cuda_device)
+    x = torch.randn(64, 181, 18, device=cuda_device)
+
+    def run(eager):
+        monkeypatch.setenv("GNNQC_FORCE_EAGER", "1" if eager else "0")
+        for p in tl.parameters():
+            p.grad = None
+        out = tl(x)
+        out.pow(2).sum().backward()
+        return out.detach(), [p.grad.detach().clone() for p in tl.parameters()]
+
+    o1, g1 = run(False)
+    o0, g0 = run(True)
+    assert o1.shape == o0.shape == (64, 64)
+    assert (o1 - o0).abs().max().item() < 3e-2 * (o0.abs().max().item() + 1e-3)
+    for a, b in zip(g1, g0):
+        assert (a - b).abs().max().item() < 5e-2 * (b.abs().max().item() + 1e-6)

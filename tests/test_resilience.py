@@ -152,3 +152,38 @@ def test_guard_kernel_matches_eager(cuda_device):
         assert torch.equal(p.detach(), before) == bad
     assert opt.skipped_steps == 1 and opt.step_t.item() == 2
     assert opt.guard_state[0].item() == 0 and opt.guard_state[1].item() == 0
+
+
+def _gcn_train_state(device, steps=6, det=True):
+    from gnnqc.data.store import DeviceLoader
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops import set_deterministic
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    from gnnqc.data.preprocessing import create_windows_dataset
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.data.synthetic import make_cml_raw
+    prev = set_deterministic(det)
+    try:
+        pc = C.normalize_preproc(C.default("preprocessing_cml"))
+        ws = create_windows_dataset(pc, raw=make_cml_raw(n_sensors=10, n_minutes=4 * 1440, seed=3))
+        st = DeviceStore(ws, "rolling_median", pc.graph, device=torch.device(device))
+        mc = C.default("model_cml")
+        torch.manual_seed(0)
+        m = GCNClassifier(mc, pc).to(device)
+        opt = make_optimizer("adam", m.parameters(), 1e-3)
+        t = Trainer(m, st, opt, {0: 1.0, 1: 5.0}, use_graph=True, batch_size=128)
+        L = DeviceLoader(st, np.arange(min(st.n_windows, 128 * steps)), 128)
+        t.train_epoch(L, 0)
+        torch.cuda.synchronize()
+        return {k: v.detach().clone() for k, v in m.state_dict().items()}
+    finally:
+        set_deterministic(prev)
+
+
+@pytest.mark.gpu
+def test_deterministic_mode_bitwise_reproducible(cuda_device):
+    a = _gcn_train_state("cuda")
+    b = _gcn_train_state("cuda")
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
