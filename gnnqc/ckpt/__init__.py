@@ -5,9 +5,9 @@
 * ``gnnqc_state.pt``   - tensors only (parameters, BN statistics, optimiser slots,
   step counters); loaded with ``torch.load(weights_only=True)``;
 * ``gnnqc_meta.json``  - model/preprocessing config, class, epoch, RNG cursor;
-* ``variables/variables.{index,data-00000-of-00001}`` + ``keras_metadata.pb``-style
-  JSON - the Keras SavedModel variable layout (TensorBundle), see
-  :mod:`gnnqc.ckpt.tensorbundle` and :mod:`gnnqc.ckpt.keras_layout`.
+* ``variables/variables.{index,data-00000-of-00001}`` + ``keras_metadata.pb`` - the
+  Keras SavedModel variable layout (TensorBundle) and per-layer JSON, see
+  :mod:`gnnqc.ckpt.tensorbundle`, :mod:`gnnqc.ckpt.keras_layout`, :mod:`gnnqc.ckpt.keras_meta`.
 
 ``load_model(path)`` rebuilds the model from the metadata and restores the state;
 ``load_keras_weights`` imports the reference's trained ``model_*`` directories.
@@ -57,7 +57,9 @@ def save_model(model, path: str, optimizer=None, epoch: Optional[int] = None, pr
         json.dump(meta, f, indent=1, default=str)
     if keras_layout:
         from .keras_layout import write_keras_variables
+        from .keras_meta import write_keras_metadata
         write_keras_variables(model, path, optimizer)
+        write_keras_metadata(model, path, optimizer)
 
 
 def load_model(path: str, device="cpu", with_optimizer: bool = False):

@@ -117,3 +117,36 @@ def test_save_load_resume(tmp_path):
     assert opt3.iterations == 1 and abs(opt3.lr - 1e-3) < 1e-9
     torch.testing.assert_close(opt3.m, opt.m)
     torch.testing.assert_close(opt3.v, opt.v)
+
+
+@needs_ref
+@pytest.mark.parametrize("name", ["model_cml", "model_cml_baseline", "model_soilnet", "model_soilnet_baseline"])
+def test_keras_metadata_matches_reference_structure(name, tmp_path):
+    """keras_metadata.pb written for a model built from the reference checkpoint has the
+    reference's node paths, identifiers, class names and the key layer configs."""
+    from gnnqc.ckpt.keras_meta import read_keras_metadata_pb, write_keras_metadata
+    model, pc, mc = build_from_keras(os.path.join(REF, name))
+    write_keras_metadata(model, str(tmp_path))
+    ours = {n["node_path"]: n for n in read_keras_metadata_pb(str(tmp_path))}
+    ref = {n["node_path"]: n for n in read_keras_metadata_pb(os.path.join(REF, name))}
+    assert set(ours) == set(ref)
+
+    def strip(v):   # shared_object_id numbering depends on Keras' global object counter
+        if isinstance(v, dict):
+            return {k: strip(x) for k, x in v.items() if k != "shared_object_id"}
+        if isinstance(v, list):
+            return [strip(x) for x in v]
+        return v
+
+    for path, r in ref.items():
+        o = ours[path]
+        assert o["identifier"] == r["identifier"], path
+        rm, om = r["metadata"], o["metadata"]
+        assert om["class_name"] == rm["class_name"], path
+        for key in ("units", "return_sequences", "activation", "channels", "aggregate", "filter_1_size",
+                    "n_stacks", "layer_type", "pool_size", "momentum", "epsilon", "num_thresholds"):
+            if key in rm.get("config", {}):
+                assert strip(om["config"].get(key)) == strip(rm["config"][key]), (path, key)
+        if "build_input_shape" in rm and path != "root":
+            assert om["build_input_shape"] == rm["build_input_shape"], path
+    assert ours["root"]["metadata"]["training_config"]["loss"] == "binary_crossentropy"
