@@ -28,6 +28,7 @@ struct ConvArgs {
   float* g;            // [M][Cout] GAP accumulator (pre-zeroed) or null
   long rows;
   int T, Cin, Cout, k, left, lda, Kp;
+  int KCH;             // K chunk staged per pass (multiple of 32; = Kp keeps W^T resident)
   float alpha;         // output activation slope (1 = identity)
   float gate_alpha;    // slope of the gating leaky'
   float a_scale;       // multiplier of A (1/T for the GAP backward)
@@ -38,21 +39,15 @@ struct ConvArgs {
 template <int NT>      // NT = ceil(Cout / 16) output tiles
 __global__ __launch_bounds__(256) void conv1d_fwd_kernel(ConvArgs p) {
   extern __shared__ __attribute__((aligned(16))) __bf16 smem[];
-  const int Kp = p.Kp, LD = Kp + CV_PAD;
-  __bf16* Wt = smem;                          // [NT*16][LD]
-  __bf16* As = smem + NT * 16 * LD;           // [CV_RT][LD]
+  const int Kp = p.Kp, KCH = p.KCH, LD = KCH + CV_PAD;
+  __bf16* Wt = smem;                          // [NT*16][LD]   W^T chunk
+  __bf16* As = smem + NT * 16 * LD;           // [CV_RT][LD]   im2col chunk
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, quad = lane >> 4;
   const int KC = p.k * p.Cin;
+  const int nch = (Kp + KCH - 1) / KCH;       // kernel-uniform
 
-  // W^T into LDS: Wt[n][tap*Cin + i] = W[tap][i][n]  (zero padded)
-  for (int e = tid; e < NT * 16 * Kp; e += 256) {
-    const int n = e / Kp, kk = e % Kp;
-    const float m_ = (n < p.Cout && kk < KC) ? 1.f : 0.f;
-    const float v = p.W[(size_t)min(kk, KC - 1) * p.Cout + min(n, p.Cout - 1)];
-    Wt[n * LD + kk] = (__bf16)(v * m_);
-  }
   float bias[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -61,37 +56,51 @@ __global__ __launch_bounds__(256) void conv1d_fwd_kernel(ConvArgs p) {
   }
 
   const long ntiles = (p.rows + CV_RT - 1) / CV_RT;
+  bool w_staged = false;
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const long r0 = tile * CV_RT;
-    __syncthreads();   // previous tile's A reads done (and Wt staged on the first pass)
-    // ---- im2col A tile [64][Kp]
-    for (int e = tid; e < CV_RT * Kp; e += 256) {
-      const int rr = e / Kp, kk = e % Kp;
-      const long r = r0 + rr;
-      const long rc = min(r, p.rows - 1);
-      const long m = rc / p.T;
-      const int t = (int)(rc - m * p.T);
-      const int tap = kk / p.Cin, i = kk - tap * p.Cin;
-      const int ts = t + tap - p.left;
-      const bool ok = r < p.rows && kk < KC && ts >= 0 && ts < p.T;
-      const int tsc = min(max(ts, 0), p.T - 1);
-      const int ic = min(i, p.Cin - 1);
-      const long src = p.bcast ? m : m * p.T + tsc;
-      // unconditional loads (the forward passes gate = x with slope 1): no branch around VMEM
-      const float v = p.a[(size_t)src * p.lda + ic];
-      const float gy = p.gate[(size_t)(m * p.T + tsc) * p.Cin + ic];
-      As[rr * LD + kk] = (__bf16)(ok ? v * (gy > 0.f ? 1.f : p.gate_alpha) * p.a_scale : 0.f);
-    }
-    __syncthreads();
     f32x4_t acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < Kp; ks += 32) {
-      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[(16 * w + col) * LD + ks + 8 * quad]);
+    for (int ch = 0; ch < nch; ++ch) {
+      const int k0 = ch * KCH;
+      __syncthreads();   // previous chunk / tile reads of As (and Wt) are done
+      if (!w_staged) {   // W^T chunk: Wt[n][kk - k0] = W[tap][i][n]  (zero padded); once if resident
+        for (int e = tid; e < NT * 16 * KCH; e += 256) {
+          const int n = e / KCH, kk = k0 + e % KCH;
+          const float m_ = (n < p.Cout && kk < KC) ? 1.f : 0.f;
+          const float v = p.W[(size_t)min(kk, KC - 1) * p.Cout + min(n, p.Cout - 1)];
+          Wt[n * LD + (kk - k0)] = (__bf16)(v * m_);
+        }
+        w_staged = nch == 1;
+      }
+      // ---- im2col A chunk [64][KCH]
+      for (int e = tid; e < CV_RT * KCH; e += 256) {
+        const int rr = e / KCH, kk = k0 + e % KCH;
+        const long r = r0 + rr;
+        const long rc = min(r, p.rows - 1);
+        const long m = rc / p.T;
+        const int t = (int)(rc - m * p.T);
+        const int tap = kk / p.Cin, i = kk - tap * p.Cin;
+        const int ts = t + tap - p.left;
+        const bool ok = r < p.rows && kk < KC && ts >= 0 && ts < p.T;
+        const int tsc = min(max(ts, 0), p.T - 1);
+        const int ic = min(i, p.Cin - 1);
+        const long src = p.bcast ? m : m * p.T + tsc;
+        // unconditional loads (the forward passes gate = x with slope 1): no branch around VMEM
+        const float v = p.a[(size_t)src * p.lda + ic];
+        const float gy = p.gate[(size_t)(m * p.T + tsc) * p.Cin + ic];
+        As[rr * LD + (kk - k0)] = (__bf16)(ok ? v * (gy > 0.f ? 1.f : p.gate_alpha) * p.a_scale : 0.f);
+      }
+      __syncthreads();
+      const int kw = min(KCH, Kp - k0);
+      for (int ks = 0; ks < kw; ks += 32) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[(16 * w + col) * LD + ks + 8 * quad]);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Wt[(16 * nt + col) * LD + ks + 8 * quad]);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
+        for (int nt = 0; nt < NT; ++nt) {
+          const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Wt[(16 * nt + col) * LD + ks + 8 * quad]);
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
+        }
       }
     }
     // ---- epilogue: lane holds rows 16w + 4quad + q of column 16nt + col
@@ -193,19 +202,30 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
 // ----------------------------------------------------------------------------- host
 static int conv_kp(int k, int Cin) { return (k * Cin + 31) / 32 * 32; }
 
-static size_t conv_lds(int NT, int Kp) { return (size_t)(NT * 16 + CV_RT) * (Kp + CV_PAD) * sizeof(__bf16); }
-
-bool conv1d_supported(int k, int Cin, int Cout) {
-  if (k < 1 || Cin < 1 || Cout < 1 || Cout > 128 || Cin > 128) return false;
+static int conv_ntp(int Cout) {
   const int NT = (Cout + 15) / 16;
-  const int NTp = NT <= 1 ? 1 : NT <= 2 ? 2 : NT <= 4 ? 4 : 8;
-  return conv_lds(NTp, conv_kp(k, Cin)) <= 150 * 1024 && (k * Cin + 1 + 15) / 16 <= 24;
+  return NT <= 1 ? 1 : NT <= 2 ? 2 : NT <= 4 ? 4 : 8;
 }
 
-static void launch_conv_fwd(const ConvArgs& a) {
-  const int NT = (a.Cout + 15) / 16;
-  const int NTp = NT <= 1 ? 1 : NT <= 2 ? 2 : NT <= 4 ? 4 : 8;
-  const size_t lds = conv_lds(NTp, a.Kp);
+static size_t conv_lds(int NTp, int KCH) { return (size_t)(NTp * 16 + CV_RT) * (KCH + CV_PAD) * sizeof(__bf16); }
+
+// K chunk: all of K (W^T resident) when it fits 80 KB (two workgroups per CU), else the
+// largest multiple of 32 that does
+static int conv_kch(int NTp, int Kp) {
+  int kch = Kp;
+  while (kch > 32 && conv_lds(NTp, kch) > 80 * 1024) kch -= 32;
+  return kch;
+}
+
+bool conv1d_supported(int k, int Cin, int Cout) {
+  // forward / dx: any K (chunked); dW: the im2col tile (k*Cin + 1 ones row) must fit 24 column tiles
+  return k >= 1 && Cin >= 1 && Cout >= 1 && Cout <= 128 && Cin <= 128 && (k * Cin + 1 + 15) / 16 <= 24;
+}
+
+static void launch_conv_fwd(ConvArgs& a) {
+  const int NTp = conv_ntp(a.Cout);
+  a.KCH = conv_kch(NTp, a.Kp);
+  const size_t lds = conv_lds(NTp, a.KCH);
   const long ntiles = (a.rows + CV_RT - 1) / CV_RT;
   const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024) / lds)));
   const int grid = (int)std::max<long>(1, std::min<long>(ntiles, 256L * per_cu));
@@ -265,7 +285,7 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
   TORCH_CHECK(y.dim() == 3 && y.size(0) == M && y.size(1) == T && y.size(2) == Cout, "conv1d_bwd: y shape");
   TORCH_CHECK(gap ? (dy.dim() == 2 && dy.size(0) == M && dy.size(1) == Cout) : dy.sizes() == y.sizes(),
               "conv1d_bwd: dy shape");
-  TORCH_CHECK(conv1d_supported(k, Cin, Cout) && conv1d_supported(k, Cout, Cin), "conv1d_bwd: unsupported shape");
+  TORCH_CHECK(conv1d_supported(k, Cin, Cout), "conv1d_bwd: unsupported shape");
   c10::DeviceGuard guard(x.device());
   const long rows = (long)M * T;
   at::Tensor dx = need_dx ? at::empty({M, T, Cin}, x.options()) : at::empty({0}, x.options());

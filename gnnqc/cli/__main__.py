@@ -193,6 +193,7 @@ def main(argv=None):
     p.add_argument("--xai-config", default=None)
     p.add_argument("--out-dir", default=None)
     p.add_argument("--max-batches", type=int, default=None)
+    p.add_argument("--shard", default=None, help="i/n: process every n-th batch starting at i (like a SLURM array task)")
     p.set_defaults(fn=cmd_explain)
     p = add_common(sub.add_parser("analyse", help="aggregate / plot saved IG attributions"))
     p.add_argument("--xai-dir", required=True)

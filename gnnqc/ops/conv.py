@@ -56,11 +56,9 @@ class _HipConv1dAct(torch.autograd.Function):
 
 
 def hip_conv_supported(k: int, cin: int, cout: int) -> bool:
-    kp = lambda c: (k * c + 31) // 32 * 32  # noqa: E731
-    ntp = lambda c: 1 if c <= 16 else 2 if c <= 32 else 4 if c <= 64 else 8  # noqa: E731
-    ok = lambda ci, co: (1 <= co <= 128 and 1 <= ci <= 128 and (ntp(co) * 16 + 64) * (kp(ci) + 8) * 2 <= 150 * 1024
-                         and (k * ci + 1 + 15) // 16 <= 24)  # noqa: E731
-    return ok(cin, cout) and ok(cout, cin)
+    """Shapes the HIP kernels take (``conv1d_supported`` in conv1d.hip): channels <= 128 and
+    the weight-gradient im2col tile k*Cin + 1 within 24 column tiles of 16."""
+    return 1 <= k and 1 <= cin <= 128 and 1 <= cout <= 128 and (k * cin + 1 + 15) // 16 <= 24
 
 
 def conv1d_act(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, alpha: float = 1.0, gap: bool = False):

@@ -180,7 +180,7 @@ class IntegratedGradientsExplainer:
     """
 
     def __init__(self, preproc_config, model_config, xai_config, model=None, windows=None, device=None,
-                 raw=None):
+                 raw=None, shard: Optional[str] = None):
         load = lambda c: C.load(c) if isinstance(c, str) else c  # noqa: E731
         self.preproc_config = C.normalize_preproc(load(preproc_config))
         self.model_config = load(model_config)
@@ -190,8 +190,14 @@ class IntegratedGradientsExplainer:
         from ..parallel import dist as D
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
-        # SLURM array job sharding (``:190-199``) or one rank per GPU
-        if "SLURM_ARRAY_TASK_ID" in os.environ:
+        # explicit shard ("i/n"), SLURM array job sharding (``:190-199``) or one rank per GPU
+        shard = shard or os.environ.get("GNNQC_IG_SHARD")
+        if shard:
+            i, n = (int(v) for v in str(shard).split("/"))
+            if not 0 <= i < n:
+                raise ValueError(f"shard {shard!r}: need 0 <= i < n")
+            self.workerid, self.n_worker = i, n
+        elif "SLURM_ARRAY_TASK_ID" in os.environ:
             self.workerid = int(os.environ["SLURM_ARRAY_TASK_ID"])
             self.n_worker = int(os.environ["SLURM_ARRAY_TASK_COUNT"])
         elif D.world_size() > 1:
@@ -407,7 +413,7 @@ def run_explainer(args):
         xc["output_dir"] = args.out_dir
     mc["model_path"] = args.model_dir
     raw = make_raw(args, pc)
-    ex = IntegratedGradientsExplainer(pc, mc, xc, device=dev, raw=raw)
+    ex = IntegratedGradientsExplainer(pc, mc, xc, device=dev, raw=raw, shard=getattr(args, "shard", None))
     ex.prepare_data()
     res = ex.get_gradients(max_batches=args.max_batches)
     print(json.dumps({"samples": len(res), "output_dir": ex.output_dir}))

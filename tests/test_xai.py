@@ -160,3 +160,35 @@ def test_roc_and_result_plots(cml_small, tmp_path):
     paths = plot_results(sids, dates, (rng.random(len(ids)) > 0.5).astype(int), flags, rng.random(len(ids)), pc, mc,
                          windows=ws)
     assert paths and all(os.path.exists(q) for q in paths)
+
+
+def test_explainer_shards_partition_batches(cml_small, tmp_path):
+    """--shard i/n splits the batches round-robin like the SLURM array path; the shards
+    together cover exactly the unsharded sample set."""
+    from gnnqc.ckpt import save_model
+    pc, ws, _ = cml_small
+    torch.manual_seed(3)
+    mc = C.default("model_cml")
+    model = _sharp(create_model(mc, pc))
+    mdir = str(tmp_path / "model")
+    save_model(model, mdir, preproc_config=pc)
+    mc["model_path"] = mdir
+    pc2 = C.Config(dict(pc))
+    pc2["batch_size"] = 8
+
+    def run(shard, out):
+        xc = C.default("xai_ig")
+        xc["output_dir"] = str(tmp_path / out)
+        ig = xc.integrated_gradients
+        ig["m_steps"], ig["dataset"], ig["threshold"] = 2, "all", 0.5
+        ex = IntegratedGradientsExplainer(pc2, mc, xc, windows=ws, device="cpu", shard=shard)
+        ex.prepare_data()
+        ex.sample_ids = ex.sample_ids[:24]
+        return {(r["sensor"], r["file_stem"]) for r in ex.get_gradients()}
+
+    full = run(None, "all")
+    a, b = run("0/2", "s0"), run("1/2", "s1")
+    assert a and b and not (a & b)
+    assert a | b == full
+    with pytest.raises(ValueError):
+        run("2/2", "bad")
