@@ -33,19 +33,22 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=128, help="windows per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="windows per GPU per step (default: config batch_size,"
+                    " CML 128 / SoilNet 32)")
     ap.add_argument("--model", choices=["gcn", "baseline"], default="gcn")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-graph", action="store_true", help="disable HIP-graph capture of the step")
-    ap.add_argument("--sensors", type=int, default=23)
-    ap.add_argument("--days", type=int, default=28)
+    ap.add_argument("--ds", choices=["cml", "soilnet"], default="cml",
+                    help="cml = the headline config; soilnet = diagnostic (T=337, per-node sequences)")
+    ap.add_argument("--sensors", type=int, default=None, help="default: 23 CML links / 40 SoilNet boxes")
+    ap.add_argument("--days", type=int, default=None, help="default: 28 (CML) / 89 (SoilNet)")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from gnnqc import config as C
     from gnnqc.data.preprocessing import create_windows_dataset
     from gnnqc.data.store import DeviceLoader, DeviceStore
-    from gnnqc.data.synthetic import make_cml_raw
+    from gnnqc.data.synthetic import make_cml_raw, make_soilnet_raw
     from gnnqc.models import BaselineClassifier, GCNClassifier
     from gnnqc.ops.optim import make_optimizer
     from gnnqc.parallel import dist as D
@@ -55,13 +58,22 @@ def main(argv=None):
     dev = D.init_distributed()
     world, rank = D.world_size(), D.rank()
     torch.manual_seed(1234)
-    pc = C.normalize_preproc(C.default("preprocessing_cml"))
+    soil = args.ds == "soilnet"
+    args.sensors = args.sensors or (40 if soil else 23)
+    args.days = args.days or (89 if soil else 28)
+    pc = C.normalize_preproc(C.default(f"preprocessing_{args.ds}"))
+    args.batch = args.batch or int(pc.batch_size)
     pc.batch_size = args.batch
-    mc = C.default("model_cml")
+    mc = C.default(f"model_{args.ds}")
     mc.runtime.compute_dtype = args.dtype
-    raw = make_cml_raw(n_sensors=args.sensors, n_minutes=args.days * 1440, seed=7)
+    if soil:
+        raw = make_soilnet_raw(n_boxes=args.sensors, n_time=args.days * 96, seed=7)
+    else:
+        raw = make_cml_raw(n_sensors=args.sensors, n_minutes=args.days * 1440, seed=7)
+    if soil:
+        pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
     ws = create_windows_dataset(pc, raw=raw)
-    store = DeviceStore(ws, "rolling_median", pc.graph, device=dev)
+    store = DeviceStore(ws, "scale_range" if soil else "rolling_median", pc.graph, device=dev)
     tr = list(range(ws.n_windows))          # throughput: every window is a training window
     loader = DeviceLoader(store, tr, args.batch, shuffle=True, seed=44, rank=rank, world_size=world,
                           drop_last=True)
@@ -108,11 +120,13 @@ def main(argv=None):
             "vs_baseline_basis": "reference GCN predict() 350 windows/s on V100 (BASELINE.md nb:321); "
                                  "reference training windows/s is not published",
             "dtype": args.dtype,
-            "data": "synthetic (CML example shape: %d links x %d days @1min, T=181), random-init weights"
-                    % (args.sensors, args.days),
+            "data": ("synthetic (SoilNet: %d boxes x %d days @15min, T=%d), random-init weights" if soil else
+                     "synthetic (CML example shape: %d links x %d days @1min, T=%d), random-init weights")
+                    % (args.sensors, args.days, ws.seq_len),
             "config": {
-                "model": "CML GCN (GeneralConv16+mean pool+LSTM TimeLayer f16 n_stacks2+dense64)" if not baseline
-                else "CML baseline LSTM",
+                "model": ("%s GCN (GeneralConv16+%s+LSTM TimeLayer f16 n_stacks2+dense64)"
+                          % ("SoilNet" if soil else "CML", "per-node sequences" if soil else "mean pool"))
+                if not baseline else ("SoilNet" if soil else "CML") + " baseline LSTM",
                 "global_batch": args.batch * world,
                 "seq_len": ws.seq_len,
                 "parallelism": f"dp{world}",

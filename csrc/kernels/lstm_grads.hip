@@ -26,7 +26,7 @@ template <int H, int DT>            // DT = ceil((Din + 1) / 16) din tiles (incl
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ dU,
-    float* __restrict__ db, long rows, long period, long hshift, int Din, int ldx, long dx_cb_stride) {
+    float* __restrict__ db, long rows, long period, long hshift, int Din, int ldx, long dx_cb_stride, int lddx) {
   constexpr int G4 = 4 * H;
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
           }
           const long r = r0 + 16 * rt + col;
           if (r < rows) {
-            float* o = dx + cb * dx_cb_stride + (size_t)r * Din;
+            float* o = dx + cb * dx_cb_stride + (size_t)r * lddx;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int din = dtile * 16 + 4 * quad + q;
@@ -174,12 +174,12 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
 template <int H>
 void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const float* x, const float* h,
                     const float* W, float* dx, float* dW, float* dU, float* db, long rows, long period, long hshift,
-                    int Din, int ldx, long dx_cb_stride) {
+                    int Din, int ldx, long dx_cb_stride, int lddx) {
   switch (DT) {
 #define GQ_DT(D)                                                                                              \
   case D:                                                                                                     \
     hipLaunchKernelGGL((lstm_grads_kernel<H, D>), grid, dim3(256), 0, st, dz, x, h, W, dx, dW, dU, db, rows, period, \
-                       hshift, Din, ldx, dx_cb_stride);                                                                 \
+                       hshift, Din, ldx, dx_cb_stride, lddx);                                                           \
     break;
     GQ_DT(1) GQ_DT(2) GQ_DT(3) GQ_DT(4) GQ_DT(5) GQ_DT(6) GQ_DT(7) GQ_DT(8) GQ_DT(9)
 #undef GQ_DT
@@ -190,10 +190,11 @@ void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const fl
 
 // Flat-row launcher shared by the sequence-major (lstm_grads) and time-major (lstm_tm_bwd)
 // paths: row r of dz / x / dx has h_{t-1} at row r - hshift when r % period >= hshift.
+// x rows have pitch ldx, dx rows pitch lddx; only the first Din (= rows of W) channels are used.
 //   sequence-major [M,T,C]: period = T, hshift = 1;  time-major [T,Mp,C]: period = T*Mp, hshift = Mp.
 void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
-                     long dx_cb_stride, hipStream_t st) {
+                     long dx_cb_stride, int lddx, hipStream_t st) {
   if (rows == 0) return;
   const int ncb = (4 * H) / GR_CB;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
@@ -203,7 +204,8 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
   const int DT = (Din + 1 + 15) / 16;
 #define GQ_GR_H(HH)                                                                                              \
   case HH:                                                                                                       \
-    launch_grads_h<HH>(DT, grid, st, dz, x, hseq, W, dx, dW, dU, db, rows, period, hshift, Din, ldx, dx_cb_stride); \
+    launch_grads_h<HH>(DT, grid, st, dz, x, hseq, W, dx, dW, dU, db, rows, period, hshift, Din, ldx, dx_cb_stride, \
+                       lddx);                                                                                    \
     break;
   switch (H) {
     GQ_GR_H(16) GQ_GR_H(32) GQ_GR_H(64) GQ_GR_H(128)
@@ -244,7 +246,7 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   if (rows == 0) return need_dx ? dx.sum(0) : dx;
   lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
                   need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
-                  db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, stream());
+                  db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, Din, stream());
   if (!need_dx) return dx;
   return ncb == 1 ? dx[0] : dx.sum(0);
 }

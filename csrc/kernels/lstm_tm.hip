@@ -32,7 +32,7 @@ namespace gq {
 // lstm_grads.hip: weight gradients (+ dx) over flat rows, h_{t-1} hshift rows back
 void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
-                     long dx_cb_stride, hipStream_t st);
+                     long dx_cb_stride, int lddx, hipStream_t st);
 int lstm_grads_col_blocks(int H);
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -78,7 +78,8 @@ template <int H, bool TRAIN, int KX, int GR, int D>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hout, float* __restrict__ gbuf,
-    float* __restrict__ cbuf, int Mp, int T, int Din) {
+    float* __restrict__ cbuf, int Mp, int T, int Din, int Dw) {
+  // Din: channels of the x layout (row pitch); Dw <= Din: rows of W (padding channels of x are zero)
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
   constexpr int KPX = 32 * KX;
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 32 * s + 8 * quad + j;
-        v[j] = (__bf16)(W[min(k, Din - 1) * G4 + ag * H + au] * (k < Din ? 1.0f : 0.0f));
+        v[j] = (__bf16)(W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
       }
       wfr[cc][s] = v;
     }
@@ -219,7 +220,7 @@ template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
-    int Mp, int T, int Din) {
+    int Mp, int T, int Din, int Dw) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
   constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
         bf16x8_t v;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          v[j] = (__bf16)(W[(size_t)min(din, Din - 1) * G4 + 32 * s + 8 * quad + j] * ((xb < NXB && din < Din) ? 1.0f : 0.0f));
+          v[j] = (__bf16)(W[(size_t)min(din, Dw - 1) * G4 + 32 * s + 8 * quad + j] * ((xb < NXB && din < Dw) ? 1.0f : 0.0f));
         wfr[q][s] = v;
       }
     }
@@ -433,18 +434,18 @@ static bool tm_supported(int H, int Din, int gr) {
 
 template <int H, bool TRAIN, int KX, int GR>
 static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, float* g,
-                       float* c, int Mp, int T, int Din, hipStream_t st) {
+                       float* c, int Mp, int T, int Din, int Dw, hipStream_t st) {
   constexpr int D = 6;
   hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W, U, b,
-                     h, g, c, Mp, T, Din);
+                     h, g, c, Mp, T, Din, Dw);
 }
 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
 static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* W, const float* U,
-                       float* dx, float* dz, int Mp, int T, int Din, hipStream_t st) {
+                       float* dx, float* dz, int Mp, int T, int Din, int Dw, hipStream_t st) {
   constexpr int D = 4;
   hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh,
-                     g, c, W, U, dx, dz, Mp, T, Din);
+                     g, c, W, U, dx, dz, Mp, T, Din, Dw);
 }
 
 #define GQ_TM_H_DISPATCH(HV, ...)                                  \
@@ -467,7 +468,8 @@ static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float*
     else { constexpr int GRR = 1; __VA_ARGS__; }                   \
   }
 
-// x: [T, Mp, Din] time-major. Returns [h (T,Mp,H), gates (state), c (state)].
+// x: [T, Mp, Din] time-major; W: [Dw, 4H] with Dw <= Din (x channels >= Dw must be zero, e.g. the
+// alignment padding of a 19-channel input to 20). Returns [h (T,Mp,H), gates (state), c (state)].
 std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
                                     const at::Tensor& b, bool train) {
   check_f32_cuda(x, "x");
@@ -477,7 +479,8 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   TORCH_CHECK(x.dim() == 3, "lstm_tm_fwd: x must be [T, Mp, Din]");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
   TORCH_CHECK(Mp % 16 == 0 && Mp > 0 && T > 0, "lstm_tm_fwd: Mp must be a positive multiple of 16");
-  TORCH_CHECK(U.size(1) == 4 * H && W.size(0) == Din && W.size(1) == 4 * H && b.numel() == 4 * H,
+  const int Dw = (int)W.size(0);
+  TORCH_CHECK(U.size(1) == 4 * H && Dw >= 1 && Dw <= Din && W.size(1) == 4 * H && b.numel() == 4 * H,
               "lstm_tm_fwd: weight shapes");
   const int gr = tm_granule(Din, x.data_ptr());
   TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
@@ -493,9 +496,9 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   float* cp = train ? c.data_ptr<float>() : nullptr;
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (train) tm_fwd_cfg<HH, true, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, st);
+                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st);
       else tm_fwd_cfg<HH, false, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, st))));
+                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st))));
   GQ_LAUNCH_CHECK();
   return {h.narrow(0, 0, T), g, c};
 }
@@ -508,6 +511,8 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   const at::Tensor* ops[] = {&dh, &g, &c, &x, &h, &W, &U};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
+  const int Dw = (int)W.size(0);
+  TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H, "lstm_tm_bwd: W shape");
   const bool last = dh.dim() == 2;
   TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H) : (dh.size(0) == T && dh.size(1) == Mp && dh.size(2) == H),
               "lstm_tm_bwd: dh shape");
@@ -517,7 +522,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   if (wg) {
     const at::Tensor* gs[] = {&dW, &dU, &db};
     for (const at::Tensor* t : gs) check_f32_cuda(*t, "lstm_tm_bwd grad");
-    TORCH_CHECK(dW.numel() == (long)Din * 4 * H && dU.numel() == (long)H * 4 * H && db.numel() == 4 * H,
+    TORCH_CHECK(dW.numel() == (long)Dw * 4 * H && dU.numel() == (long)H * 4 * H && db.numel() == 4 * H,
                 "lstm_tm_bwd: gradient buffer shapes");
   }
   const int gr = tm_granule(Din, x.data_ptr());
@@ -530,16 +535,18 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options());
     GQ_TM_H_DISPATCH(H,
         if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, st);
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st);
         else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, st));
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st));
     GQ_LAUNCH_CHECK();
     const long rows = (long)T * Mp;
     const int ncb = lstm_grads_col_blocks(H);
-    at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
+    // dx keeps the x layout (Din channels); padding channels (>= Dw) get zero gradient
+    at::Tensor dx = need_dx ? (Dw < Din ? at::zeros({ncb, T, Mp, Din}, x.options()) : at::empty({ncb, T, Mp, Din}, x.options()))
+                            : at::empty({0}, x.options());
     lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                     need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
-                    db.data_ptr<float>(), rows, rows, Mp, H, Din, Din, rows * Din, st);
+                    db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, st);
     if (!need_dx) return dx;
     return ncb == 1 ? dx[0] : dx.sum(0);
   }
@@ -548,7 +555,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #define GQ_TM_BWD_CALL(LASTV)                                                                               \
   tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),          \
                                                c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
-                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, st)
+                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st)
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (last) GQ_TM_BWD_CALL(true); else GQ_TM_BWD_CALL(false))));
 #undef GQ_TM_BWD_CALL

@@ -35,6 +35,14 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor alpha, int c_off) -> Tensor");
   m.def("gcn_pool_bwd_input(Tensor x, Tensor w, Tensor mask, Tensor dout, Tensor W, Tensor b, Tensor scale, "
         "Tensor shift, Tensor alpha, Tensor dzcoef, int c_off) -> Tensor");
+  // per-node GeneralConv writing the time-major LSTM input (gcn_node.hip)
+  m.def("gcn_adj_bits(Tensor adj, bool agg_mean) -> Tensor[]");
+  m.def("gcn_node_fwd(Tensor x, Tensor bits, Tensor rs, Tensor mask, Tensor W, Tensor b, Tensor scale, "
+        "Tensor shift, Tensor alpha, int Mp, int Cp) -> Tensor");
+  m.def("gcn_node_bwd(Tensor x, Tensor bitsT, Tensor rs, Tensor mask, Tensor dout, Tensor W, Tensor b, "
+        "Tensor scale, Tensor shift, Tensor alpha) -> Tensor");
+  m.def("gcn_node_bwd_input(Tensor x, Tensor bitsT, Tensor rs, Tensor mask, Tensor dout, Tensor W, Tensor b, "
+        "Tensor scale, Tensor shift, Tensor alpha, Tensor coef) -> Tensor");
   // GCN glue: pooling weights, BN statistics, closed-form backward (gcn_glue.hip)
   m.def("gcn_pool_weights(Tensor adj, Tensor mask, Tensor anom_pos, bool agg_mean, int pool) -> Tensor");
   m.def("gcn_bn_prep(Tensor S, Tensor W, Tensor b, Tensor gamma, Tensor beta, Tensor(a!) rmean, Tensor(b!) rvar, "

@@ -136,7 +136,8 @@ def cmd_cv(args):
     out = {}
     for baseline in kinds:
         s = run_cv(pc, mc, ws, folds=args.folds, baseline=baseline, store=store, seed=args.seed,
-                   gap_days=args.gap_days, log_path=args.log, max_folds=args.max_folds)
+                   gap_days=args.gap_days, log_path=args.log, max_folds=args.max_folds,
+                   fold_ids=[int(v) for v in args.fold_ids.split(",")] if args.fold_ids else None)
         out[s["model"]] = s
         if D.is_main():
             print(json.dumps({"model": s["model"], "mean_auc": round(s["mean_auc"], 4), "std_auc": round(s["std_auc"], 4),
@@ -185,6 +186,7 @@ def main(argv=None):
     p.add_argument("--both", action="store_true")
     p.add_argument("--gap-days", type=int, default=None)
     p.add_argument("--max-folds", type=int, default=None, help="only run the first K folds")
+    p.add_argument("--fold-ids", default=None, help="comma list: only run these folds (e.g. 0,1)")
     p.add_argument("--out", default=None)
     p.add_argument("--log", default=None)
     p.set_defaults(fn=cmd_cv)

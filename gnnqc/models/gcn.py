@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from ..config import freq_minutes
-from ..ops.gcn import gcn_pool, pool_nodes
+from ..ops.gcn import gcn_node_tm, gcn_node_tm_ok, gcn_pool, pool_nodes
 from .graphconv import GeneralConv, make_graph_layer
 from .layers import Dense, Dropout, LeakyReLU
 from .spatial import SensorsTimeLayer, SpatialTransformer
@@ -154,6 +154,17 @@ class GCNClassifier(nn.Module):
         h = self.gcn_layer(feats, adj, mask)
         return graph_reshape(torch.cat([h, x], -1))
 
+    def _soil_fused(self, inputs) -> bool:
+        """SoilNet fast path: fused per-node GCN kernel writing the time-major LSTM input."""
+        if self.ds_type != "soilnet" or not self._fused_ok():
+            return False
+        if self.sensors_time_layer is not None or self.spatial_transformer is not None:
+            return False
+        x = inputs[0]
+        g = self.gcn_layer
+        return (gcn_node_tm_ok(x, g.kernel, g.aggregate, g.dropout, self.training)
+                and self.time_layer.time_major_ok(x, g.out_features + x.shape[-1]))
+
     def head(self, ts: torch.Tensor) -> torch.Tensor:
         d = self.dropout1(ts)
         d = self.leakyrelu4(self.dense(d))
@@ -163,6 +174,12 @@ class GCNClassifier(nn.Module):
 
     def features(self, inputs) -> torch.Tensor:
         """TimeLayer output rows [R, F] (CML: R = B; SoilNet: R = B*N) - the head's input."""
+        if self._soil_fused(inputs):
+            x, adj, mask = inputs[:3]
+            g = self.gcn_layer
+            h, M = gcn_node_tm(x, adj, mask, g.kernel, g.bias, g.bn_gamma, g.bn_beta, g.prelu_alpha,
+                               g.bn_moving_mean, g.bn_moving_variance, self.training, g.aggregate, g.momentum, g.eps)
+            return self.time_layer.forward_time_major(h, M)
         return self.time_layer(self.temporal_input(inputs))
 
     def head_spec(self):
@@ -175,7 +192,7 @@ class GCNClassifier(nn.Module):
         return self.dense, self.dense2, self.dense_out, self.leakyrelu4.alpha, self.leakyrelu5.alpha
 
     def logits(self, inputs) -> torch.Tensor:
-        z = self.head(self.time_layer(self.temporal_input(inputs)))
+        z = self.head(self.features(inputs))
         if self.ds_type == "soilnet":
             B, N = inputs[0].shape[0], inputs[0].shape[2]
             z = z.view(B, N)

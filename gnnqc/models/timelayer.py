@@ -82,14 +82,21 @@ class TimeLayer(nn.Module):
         """GPU LSTM branch: the leading H <= 32 layers (and their pools) run time-major
         ([T, Mp, C], fused-backward kernels); the rest continues sequence-major."""
         import torch.nn.functional as F
-        from ..ops.lstm import lstm_layer_tm, tm_eligible
-        from ..ops.pool import max_pool1d_tm
         M = x.shape[0]
         Mp = (M + 15) // 16 * 16
+        cpad = (-x.shape[-1]) % 4          # float4 loader granules: zero channels up to a multiple of 4
         h = x.float().transpose(0, 1)
-        if Mp != M:
-            h = F.pad(h, (0, 0, 0, Mp - M))
-        h = h.contiguous()
+        if Mp != M or cpad:
+            h = F.pad(h, (0, cpad, 0, Mp - M))
+        return self.forward_time_major(h.contiguous(), M)
+
+    def forward_time_major(self, h: torch.Tensor, M: int) -> torch.Tensor:
+        """LSTM branch on a time-major input ``[T, Mp, C]`` (Mp = M rounded up to 16, zero
+        rows past M; C may carry zero channels past the first layer's input width).
+        Returns ``[M, out_features]``. Producers that can write this layout directly (the
+        SoilNet GCN kernel) skip the transpose/pad copy of :meth:`_forward_tm`."""
+        from ..ops.lstm import lstm_layer_tm, tm_eligible
+        from ..ops.pool import max_pool1d_tm
         tm = True
         for mod in self._sequence():
             if isinstance(mod, MaxPooling1D):
@@ -101,7 +108,10 @@ class TimeLayer(nn.Module):
                     return h[:M]
                 continue
             if tm:                                   # leave time-major: [T, Mp, C] -> [M, T, C]
-                h = h.transpose(0, 1)[:M].contiguous()
+                h = h.transpose(0, 1)[:M]
+                if h.shape[-1] != mod.kernel.shape[0]:   # (only if the first layer is not time-major)
+                    h = h[..., : mod.kernel.shape[0]]
+                h = h.contiguous()
                 tm = False
             h = mod(h)
         return h
@@ -118,10 +128,16 @@ class TimeLayer(nn.Module):
             x1 = self.pooling_layers[i](x1)
         return self.time4.forward_act(x1, self.leakyrelu3.alpha, gap=True)
 
-    def _tm_ok(self, x: torch.Tensor) -> bool:
+    def time_major_ok(self, x: torch.Tensor, channels: int) -> bool:
+        """Whether :meth:`forward_time_major` can take a ``channels``-wide input on x's device."""
+        return self._tm_ok(x, channels)
+
+    def _tm_ok(self, x: torch.Tensor, channels: Optional[int] = None) -> bool:
         from ..ops.lstm import tm_eligible
+        c = x.shape[-1] if channels is None else int(channels)
         return (self.layer_type == "lstm" and self.time1.activation == "tanh"
-                and tm_eligible(x, self.time1.units, x.shape[-1], self.time1.activation, self.time1.compute_bf16)
+                and tm_eligible(x, self.time1.units, c + (-c) % 4, self.time1.activation,
+                                self.time1.compute_bf16)
                 and os.environ.get("GNNQC_NO_TM", "0") != "1")
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

@@ -168,6 +168,95 @@ def gcn_pool(x, adj, mask, anom, anom_pos, W, b, gamma, beta, alpha, running_mea
     return pooled if anom is None else torch.cat([anom, pooled], dim=-1)
 
 
+class _HipGCNNodeTM(torch.autograd.Function):
+    """Per-node GeneralConv -> time-major LSTM input ``[T, Mp, Cp]`` (``gcn_node.hip``).
+
+    Forward: gcn_stats, gcn_bn_prep, gcn_node_fwd; backward: gcn_node_bwd,
+    gcn_bwd_finalize (+ gcn_node_bwd_input when dx is needed, e.g. integrated gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, bits, bitsT, rs, mask, W, b, gamma, beta, alpha, running_mean, running_var,
+                training: bool, momentum: float, eps: float, Mp: int, Cp: int):
+        from ..utils.native import hip_ops
+        ops = hip_ops()
+        S = ops.gcn_stats(x, mask) if training else x.new_zeros(0, dtype=torch.float64)
+        st = ops.gcn_bn_prep(S, W.contiguous(), b.contiguous(), gamma.contiguous(), beta.contiguous(),
+                             running_mean, running_var, bool(training), float(momentum), float(eps))
+        out = ops.gcn_node_fwd(x, bits, rs, mask, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous(),
+                               int(Mp), int(Cp))
+        ctx.training = training
+        ctx.params = (W, b, gamma, beta, alpha)
+        ctx.save_for_backward(x, bitsT, rs, mask, W, b, alpha, st, S)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..utils.native import hip_ops
+        from .lstm import _grad_sink
+        ops = hip_ops()
+        x, bitsT, rs, mask, W, b, alpha, st, S = ctx.saved_tensors
+        dout = dout.contiguous()
+        need = ctx.needs_input_grad
+        empty = x.new_zeros(0)
+        acc = empty
+        if ctx.training or any(need[5:10]):
+            acc = ops.gcn_node_bwd(x, bitsT, rs, mask, dout, W.contiguous(), b.contiguous(), st[2], st[3],
+                                   alpha.contiguous())
+        sinks = [(_grad_sink(p) if n else (empty, True)) for p, n in zip(ctx.params, need[5:10])]
+        coef = ops.gcn_bwd_finalize(acc, S, W.contiguous(), b.contiguous(), st, bool(ctx.training),
+                                    *[s[0] for s in sinks])
+        dx = None
+        if need[0]:
+            dx = ops.gcn_node_bwd_input(x, bitsT, rs, mask, dout, W.contiguous(), b.contiguous(), st[2], st[3],
+                                        alpha.contiguous(), coef)
+        grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need[5:10])]
+        return (dx, None, None, None, None, *grads, None, None, None, None, None, None, None)
+
+
+def gcn_node_tm_ok(x: torch.Tensor, W: torch.Tensor, aggregate: str, dropout: float, training: bool) -> bool:
+    """Whether :func:`gcn_node_tm` runs the HIP kernels for this input."""
+    from . import use_hip
+    F_ = W.shape[1]
+    N = x.shape[2]
+    lds = N * ((N + 31) // 32) * 4 + N * F_ * 4 + N * 8
+    return (use_hip(x) and aggregate in ("mean", "sum") and not (dropout and training) and x.shape[-1] <= 4
+            and F_ <= 64 and 64 % F_ == 0 and lds <= 150 * 1024)
+
+
+def gcn_node_tm(x, adj, mask, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
+                aggregate: str = "mean", momentum: float = 0.99, eps: float = 1e-3, cpad_to: int = 4):
+    """SoilNet GeneralConv + ``Concatenate([gcn, x])`` + ``graph_reshape`` as ONE time-major tensor.
+
+    Returns ``(h [T, Mp, Cp], M)`` with row ``m = b*N + i`` (the reference's
+    per-node sequence order), channels ``[F gcn | Cin raw | 0 pad]`` (Cp a multiple
+    of ``cpad_to``) and zero rows past ``M = B*N`` - the input layout of
+    :meth:`gnnqc.models.timelayer.TimeLayer.forward_time_major`.
+    """
+    from ..utils.native import hip_ops
+    B, T, N, Cin = x.shape
+    M = B * N
+    Mp = (M + 15) // 16 * 16
+    Cp = W.shape[1] + Cin
+    Cp += (-Cp) % cpad_to
+    bits, bitsT, rs = hip_ops().gcn_adj_bits(adj.float().contiguous(), aggregate == "mean")
+    h = _HipGCNNodeTM.apply(x.float().contiguous(), bits, bitsT, rs, mask.float().contiguous(), W, b, gamma, beta,
+                            alpha, running_mean, running_var, bool(training), float(momentum), float(eps), Mp, Cp)
+    return h, M
+
+
+def gcn_node_tm_eager(x, adj, mask, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
+                      aggregate: str = "mean", momentum: float = 0.99, eps: float = 1e-3, cpad_to: int = 4):
+    """Eager oracle of :func:`gcn_node_tm` (same output layout)."""
+    B, T, N, Cin = x.shape
+    M = B * N
+    Mp = (M + 15) // 16 * 16
+    h = general_conv_eager(x, adj, mask, W, b, gamma, beta, running_mean, running_var, alpha, training, aggregate,
+                           0.0, momentum, eps)
+    seq = torch.cat([h, x], -1).permute(1, 0, 2, 3).reshape(T, M, -1)
+    C = seq.shape[-1]
+    return F.pad(seq, (0, (-C) % cpad_to, 0, Mp - M)), M
+
+
 def pool_nodes(h: torch.Tensor, mask: torch.Tensor, anom_pos, pooling: str = "mean") -> torch.Tensor:
     """``timeseries_pooling`` over valid nodes: [B,T,N,F] -> [B,T,F]."""
     m = mask[:, None, :, None].to(h.dtype)
@@ -184,5 +273,5 @@ def pool_nodes(h: torch.Tensor, mask: torch.Tensor, anom_pos, pooling: str = "me
     raise ValueError(pooling)
 
 
-__all__ = ["gcn_pool", "node_pool_weights", "masked_batchnorm", "general_conv_eager", "pool_nodes",
+__all__ = ["gcn_pool", "gcn_node_tm", "gcn_node_tm_eager", "gcn_node_tm_ok", "node_pool_weights", "masked_batchnorm", "general_conv_eager", "pool_nodes",
            "normalized_adjacency", "prelu"]

@@ -28,7 +28,10 @@ from .fit import train_model
 
 def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, baseline: bool = False,
            device="cpu", seed: int = 0, store: Optional[DeviceStore] = None, gap_days: Optional[int] = None,
-           verbose: int = 1, log_path: Optional[str] = None, max_folds: Optional[int] = None) -> Dict:
+           verbose: int = 1, log_path: Optional[str] = None, max_folds: Optional[int] = None,
+           fold_ids: Optional[List[int]] = None) -> Dict:
+    """``fold_ids`` runs only those folds (e.g. to spread a CV over several jobs; merge
+    the per-fold JSONL lines with :func:`summarize_folds`)."""
     pc = preproc_config
     mc = model_config
     k = int(folds or pc.get("split_numb", 5))
@@ -38,7 +41,10 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
     store = store or DeviceStore(windows, norm, pc.graph, device=device)
     rank, world = D.rank(), D.world_size()
     results: List[Dict] = []
-    for fold in range(min(k, int(max_folds)) if max_folds else k):
+    todo = list(range(min(k, int(max_folds)) if max_folds else k))
+    if fold_ids is not None:
+        todo = [int(f) for f in fold_ids if 0 <= int(f) < k]
+    for fold in todo:
         t0 = time.time()
         tr, te, pcf = load_dataset_CV(pc, windows, fold, gap_days=gap_days)
         torch.manual_seed(seed + fold)
@@ -66,13 +72,19 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
         if log_path and D.is_main():
             with open(log_path, "a") as f:
                 f.write(json.dumps(res) + "\n")
-    aucs = np.array([r["auc"] for r in results])
-    summary = {
-        "model": "baseline" if baseline else "gcn", "ds_type": windows.ds_type, "folds": k,
-        "mean_auc": float(np.nanmean(aucs)), "std_auc": float(np.nanstd(aucs)),
-        "mean_mcc": float(np.mean([r["mcc"] for r in results])), "per_fold": results,
+    return summarize_folds(results, "baseline" if baseline else "gcn", windows.ds_type, k)
+
+
+def summarize_folds(results: List[Dict], model: str, ds_type: str, folds: int) -> Dict:
+    """Headline summary (mean / std ROC-AUC, mean MCC) of per-fold result dicts."""
+    aucs = np.array([r["auc"] for r in results], dtype=np.float64)
+    return {
+        "model": model, "ds_type": ds_type, "folds": folds, "folds_run": sorted(int(r["fold"]) for r in results),
+        "mean_auc": float(np.nanmean(aucs)) if aucs.size else float("nan"),
+        "std_auc": float(np.nanstd(aucs)) if aucs.size else float("nan"),
+        "mean_mcc": float(np.mean([r["mcc"] for r in results])) if results else float("nan"),
+        "per_fold": results,
     }
-    return summary
 
 
-__all__ = ["run_cv"]
+__all__ = ["run_cv", "summarize_folds"]

@@ -8,6 +8,7 @@
 #           see profiles/r1_soil_diag.md)
 # Usage (GPU box; writes gpurun_out/cv/):
 #   DATASETS="cml soilnet" MODELS="gcn baseline" bash scripts/cv_headline.sh [extra cli args]
+#   FOLD_IDS=0,1,2 TAG=_a ...   (run a subset of folds; per-fold lines append to cv_<ds>_<model>.jsonl)
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=${OUT:-$ROOT/gpurun_out/cv}
 mkdir -p "$OUT"
@@ -21,8 +22,9 @@ for ds in ${DATASETS:-cml soilnet}; do
     m=""; [ "$mm" = "baseline" ] && m="--baseline"
     echo "== $ds $mm CV"; date
     timeout -k 10 ${CV_TIMEOUT:-1000} python3 -m gnnqc.cli cv --ds $ds --synthetic $args $m --folds 5 \
-        --out "$OUT/cv_${ds}_${mm}.json" --log "$OUT/cv_${ds}_${mm}.jsonl" "$@" > "$OUT/cv_${ds}_${mm}.log" 2>&1
-    rc=$?; echo "$ds $mm rc=$rc"; tail -1 "$OUT/cv_${ds}_${mm}.log"
+        ${FOLD_IDS:+--fold-ids $FOLD_IDS} --out "$OUT/cv_${ds}_${mm}${TAG}.json" --log "$OUT/cv_${ds}_${mm}.jsonl" "$@" \
+        > "$OUT/cv_${ds}_${mm}${TAG}.log" 2>&1
+    rc=$?; echo "$ds $mm rc=$rc"; tail -1 "$OUT/cv_${ds}_${mm}${TAG}.log"
     [ $rc -ne 0 ] && exit $rc
   done
 done

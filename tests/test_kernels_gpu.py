@@ -421,3 +421,118 @@ def test_timelayer_cnn_branch_hip_vs_eager(cuda_device, monkeypatch):
     assert (o1 - o0).norm().item() < 2e-2 * o0.norm().item()
     for a, b in zip(g1, g0):
         assert (a - b).norm().item() < 5e-2 * (b.norm().item() + 1e-6)
+
+
+@pytest.mark.parametrize("H", [16, 32])
+@pytest.mark.parametrize("wgrad", [True, False])
+def test_lstm_time_major_padded_channels(cuda_device, H, wgrad):
+    """x with zero channels past W's rows (19 -> 20, float4 loader granules) == unpadded eager."""
+    from gnnqc.ops.lstm import lstm_eager, lstm_layer_tm
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(H + 11)
+    M, T, Din = 37, 14, 19
+    x = torch.randn(M, T, Din, generator=gen).to(dev)
+    W, U, b = _lstm_params(Din, H, gen, dev)
+    xt = torch.zeros(T, 48, 20, device=dev)
+    xt[:, :M, :Din] = x.transpose(0, 1)
+    xt.requires_grad_(True)
+    Wp, Up, bp = (t.clone().requires_grad_(wgrad) for t in (W, U, b))
+    out = lstm_layer_tm(xt, Wp, Up, bp, True)
+    out_m = out[:, :M].transpose(0, 1)
+    ref_params = [t.clone().double().requires_grad_(True) for t in (x, W, U, b)]
+    ref = lstm_eager(*ref_params)
+    assert torch.allclose(out_m.double(), ref, atol=3e-2, rtol=3e-2), (out_m.double() - ref).abs().max()
+    g = torch.randn(ref.shape, generator=gen).to(dev)
+    out_m.backward(g)
+    ref.backward(g.double())
+    got = [xt.grad[:, :M, :Din].transpose(0, 1)] + ([Wp.grad, Up.grad, bp.grad] if wgrad else [])
+    for p, r, name in zip(got, ref_params, "xWUb"):
+        err = (p.double() - r.grad).abs().max().item()
+        scale = r.grad.abs().max().item() + 1e-6
+        assert err / scale < 5e-2, f"grad {name}: rel err {err / scale}"
+    assert float(xt.grad[..., Din:].abs().max()) == 0.0        # padding channel: no gradient
+
+
+def _soil_graph(B, N, gen, dev):
+    """Random symmetric radius-like graphs with self loops and padded (masked) nodes."""
+    n_valid = [N - 3 * b for b in range(B)]
+    adj = torch.zeros(B, N, N)
+    mask = torch.zeros(B, N)
+    for b, nv in enumerate(n_valid):
+        mask[b, :nv] = 1
+        a = (torch.rand(nv, nv, generator=gen) < 0.12).float()
+        a = ((a + a.t()) > 0).float()
+        a.fill_diagonal_(1.0)
+        adj[b, :nv, :nv] = a
+    return adj.to(dev), mask.to(dev)
+
+
+@pytest.mark.parametrize("training", [True, False])
+@pytest.mark.parametrize("aggregate", ["mean", "sum"])
+def test_gcn_node_tm_matches_eager(cuda_device, training, aggregate):
+    """Per-node GeneralConv kernel (SoilNet): time-major output and every gradient vs fp64 eager."""
+    from gnnqc.ops.gcn import gcn_node_tm, gcn_node_tm_eager
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(5 + training + 2 * (aggregate == "sum"))
+    B, T, N, Cin, F = 3, 9, 45, 3, 16
+    adj, mask = _soil_graph(B, N, gen, dev)
+    x = (torch.randn(B, T, N, Cin, generator=gen).to(dev)) * mask[:, None, :, None]
+    W = (torch.randn(Cin, F, generator=gen) * 0.5).to(dev)
+    b = (torch.randn(F, generator=gen) * 0.1).to(dev)
+    gamma = (1 + 0.1 * torch.randn(F, generator=gen)).to(dev)
+    beta = (0.1 * torch.randn(F, generator=gen)).to(dev)
+    alpha = (0.2 * torch.rand(F, generator=gen)).to(dev)
+    rm0 = (0.1 * torch.randn(F, generator=gen)).to(dev)
+    rv0 = (1 + 0.1 * torch.rand(F, generator=gen)).to(dev)
+    ps = [t.clone().requires_grad_(True) for t in (x, W, b, gamma, beta, alpha)]
+    rps = [t.clone().double().requires_grad_(True) for t in (x, W, b, gamma, beta, alpha)]
+    rm, rv, rrm, rrv = rm0.clone(), rv0.clone(), rm0.clone().double(), rv0.clone().double()
+    h, M = gcn_node_tm(ps[0], adj, mask, *ps[1:5], ps[5], rm, rv, training, aggregate)
+    ref, Mr = gcn_node_tm_eager(rps[0], adj.double(), mask.double(), *rps[1:5], rps[5], rrm, rrv, training,
+                                aggregate)
+    assert M == Mr and h.shape == ref.shape, (h.shape, ref.shape)
+    torch.testing.assert_close(h.double(), ref, atol=2e-4, rtol=2e-4)
+    torch.testing.assert_close(rm.double(), rrm, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rv.double(), rrv, atol=1e-5, rtol=1e-5)
+    g = torch.randn(ref.shape, generator=gen).to(dev)
+    g[:, M:] = 0
+    h.backward(g)
+    ref.backward(g.double())
+    for p, r, name in zip(ps, rps, ("x", "W", "b", "gamma", "beta", "alpha")):
+        if r.grad is None:
+            continue
+        err = (p.grad.double() - r.grad).abs().max().item()
+        scale = r.grad.abs().max().item() + 1e-6
+        assert err / scale < 1e-3, f"grad {name}: rel err {err / scale}"
+
+
+def test_soilnet_gcn_fused_path_matches_eager(cuda_device, monkeypatch):
+    """SoilNet GCNClassifier: fused GCN + time-major LSTM vs the all-eager path (same weights)."""
+    from gnnqc import config as C
+    from gnnqc.models import GCNClassifier
+    torch.manual_seed(0)
+    pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
+    mc = C.default("model_soilnet")
+    model = GCNClassifier(mc, pc).to(cuda_device)
+    gen = torch.Generator().manual_seed(1)
+    B, T, N = 4, 337, 29
+    adj, mask = _soil_graph(B, N, gen, cuda_device)
+    x = torch.rand(B, T, N, 3, generator=gen).to(cuda_device) * mask[:, None, :, None]
+    inputs = (x, adj, mask)
+    assert model._soil_fused(inputs)
+
+    def run(eager):
+        monkeypatch.setenv("GNNQC_FORCE_EAGER", "1" if eager else "0")
+        for p in model.parameters():
+            p.grad = None
+        z = model.logits(inputs)
+        (z * mask).pow(2).sum().backward()
+        return z.detach(), {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+
+    z1, g1 = run(False)
+    z0, g0 = run(True)
+    assert z1.shape == z0.shape == (B, N)
+    assert (z1 - z0).norm().item() < 3e-2 * z0.norm().item()
+    assert set(g1) == set(g0)
+    for k in g0:
+        assert (g1[k] - g0[k]).norm().item() < 8e-2 * (g0[k].norm().item() + 1e-6), k
