@@ -264,7 +264,7 @@ at::Tensor gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
   c10::DeviceGuard guard(x.device());
   const int nacc = 3 + Cin;
   const int rows_per_blk = 256 / F;
-  const int nblk = grid_for((long)B * T, rows_per_blk, 256);
+  const int nblk = grid_for((long)B * T, rows_per_blk, 2048);
   at::Tensor partial = at::empty({nblk, nacc, F}, x.options());
   GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_pool_bwd_kernel<CIN>, dim3(nblk), dim3(256), 0, stream(), x.data_ptr<float>(),
                      w.data_ptr<float>(), dout.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(),

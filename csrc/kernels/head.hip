@@ -12,7 +12,7 @@
 // histogram) and ONE backward kernel (all weight gradients + d features).
 //
 // Layout: rows are tiled by 64; 256 threads = 4 waves; thread (j = tid & 63,
-// g = tid >> 6) owns output column j of rows g*16 .. g*16+15. Input tiles and
+// g = tid >> 6) owns output column j of rows g*RPG .. g*RPG+RPG-1. Input tiles and
 // activations live in LDS; inner products read LDS with wave-uniform addresses
 // (broadcast, conflict free) and weights with lane-contiguous addresses. The
 // backward kernel is persistent over row tiles and keeps its weight-gradient
@@ -22,8 +22,11 @@
 
 namespace gq {
 
-constexpr int HT = 64;     // rows per tile
+constexpr int HT = 16;     // rows per tile: 8 workgroups for a CML batch of 128 (LDS-bound loops
+                           // spread over 8 CUs; 64-row tiles left 2 CUs doing 4x the work each)
 constexpr int HU = 64;     // dense units (model_config dense.units)
+constexpr int RPG = HT / 4;  // rows per wave group
+constexpr int UPG = HU / 4;  // dense units per wave group (dW2 rows per thread)
 
 __device__ __forceinline__ float leaky(float z, float a) { return z > 0.f ? z : a * z; }
 __device__ __forceinline__ float dleaky(float z, float a) { return z > 0.f ? 1.f : a; }
@@ -100,51 +103,51 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
       *reinterpret_cast<float4*>(&sf[r][4 * c4]) = v;
     }
     __syncthreads();
-    float acc[16];
+    float acc[RPG];
     const float bj1 = b1[j];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = bj1;
+    for (int i = 0; i < RPG; ++i) acc[i] = bj1;
     #pragma unroll 4
     for (int k = 0; k < F; ++k) {
-      const float w = W1[k * HU + j];
+      const float w = sW1[k][j];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] += sf[g * 16 + i][k] * w;
+      for (int i = 0; i < RPG; ++i) acc[i] += sf[g * RPG + i][k] * w;
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = g * 16 + i;
+    for (int i = 0; i < RPG; ++i) {
+      const int r = g * RPG + i;
       if (row0 + r < R) z1o[(long)(row0 + r) * HU + j] = acc[i];
       sa1[r][j] = leaky(acc[i], alpha1);
     }
     __syncthreads();
     const float bj2 = b2[j];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = bj2;
+    for (int i = 0; i < RPG; ++i) acc[i] = bj2;
     #pragma unroll 4
     for (int k = 0; k < HU; ++k) {
-      const float w = W2[k * HU + j];
+      const float w = sW2[k][j];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] += sa1[g * 16 + i][k] * w;
+      for (int i = 0; i < RPG; ++i) acc[i] += sa1[g * RPG + i][k] * w;
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = g * 16 + i;
+    for (int i = 0; i < RPG; ++i) {
+      const int r = g * RPG + i;
       if (row0 + r < R) z2o[(long)(row0 + r) * HU + j] = acc[i];
       sa2[r][j] = leaky(acc[i], alpha2);
     }
     __syncthreads();
-    // output unit: wave g reduces its 16 rows; lane i < 16 keeps row g*16+i
+    // output unit: wave g reduces its RPG rows; lane i < RPG keeps row g*RPG+i
     float zr = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float v = wave_sum(sa2[g * 16 + i][j] * w3);
+    for (int i = 0; i < RPG; ++i) {
+      const float v = wave_sum(sa2[g * RPG + i][j] * w3);
       if (j == i) zr = v;
     }
     {
-      const int row = row0 + g * 16 + (j & 15);
+      const int row = row0 + g * RPG + (j % RPG);
       const int rc = min(row, R - 1);
       const float yy_ = y[rc], m_ = mask[rc];        // loads outside any per-lane branch
-      if (j < 16 && row < R) {
+      if (j < RPG && row < R) {
         const float z = zr + b3v;
         logits[row] = z;
         const float yy = yy_, m = m_;
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     }
     __syncthreads();
   }
-  // block reduction of the loss / metric partials (lanes >= 16 hold zeros)
+  // block reduction of the loss / metric partials (lanes >= RPG hold zeros)
   float v[6] = {m_loss, m_n, m_tp, m_tn, m_fp, m_fn};
 #pragma unroll
   for (int q = 0; q < 6; ++q) v[q] = wave_sum(v[q]);
@@ -211,11 +214,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   stage_lds<F * HU, HU, HU + 1>(&sW1[0][0], W1);
   stage_lds<HU * HU, HU, HU + 1>(&sW2[0][0], W2);
   const float w3j = W3[j];
-  float aW1[KPT], aW2[16], aW3 = 0.f, ab1 = 0.f, ab2 = 0.f, ab3 = 0.f;
+  float aW1[KPT], aW2[UPG], aW3 = 0.f, ab1 = 0.f, ab2 = 0.f, ab3 = 0.f;
 #pragma unroll
   for (int q = 0; q < KPT; ++q) aW1[q] = 0.f;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) aW2[q] = 0.f;
+  for (int q = 0; q < UPG; ++q) aW2[q] = 0.f;
   const int ntiles = (R + HT - 1) / HT;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int row0 = tile * HT;
@@ -229,8 +232,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       *reinterpret_cast<float4*>(&sf[r][4 * c4]) = v;
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = g * 16 + i, row = row0 + r;
+    for (int i = 0; i < RPG; ++i) {
+      const int r = g * RPG + i, row = row0 + r;
       const float rm = row < R ? 1.f : 0.f;
       const float a = z1[(long)min(row, R - 1) * HU + j] * rm;
       const float b = z2[(long)min(row, R - 1) * HU + j] * rm;
@@ -252,8 +255,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     __syncthreads();
     // dW3 / db... and dz2 = dz3 * W3 * leaky'(z2) (in place)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = g * 16 + i;
+    for (int i = 0; i < RPG; ++i) {
+      const int r = g * RPG + i;
       const float z = sz2[r][j], d3 = sdz3[r];
       aW3 += leaky(z, alpha2) * d3;
       sz2[r][j] = d3 * w3j * dleaky(z, alpha2);
@@ -264,23 +267,23 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     for (int r = 0; r < HT; ++r) {
       const float d = sz2[r][j];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) aW2[q] += sa1[r][g * 16 + q] * d;
+      for (int q = 0; q < UPG; ++q) aW2[q] += sa1[r][g * UPG + q] * d;
       if (g == 0) ab2 += d;
     }
-    float da[16];
+    float da[RPG];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) da[q] = 0.f;
-    // thread owns unit i = j of rows g*16..: da1[r][i] = sum_k dz2[r][k] W2[i][k]
+    for (int q = 0; q < RPG; ++q) da[q] = 0.f;
+    // thread owns unit i = j of rows g*RPG..: da1[r][i] = sum_k dz2[r][k] W2[i][k]
     #pragma unroll 4
     for (int k = 0; k < HU; ++k) {
       const float w = sW2[j][k];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) da[q] += sz2[g * 16 + q][k] * w;
+      for (int q = 0; q < RPG; ++q) da[q] += sz2[g * RPG + q][k] * w;
     }
     __syncthreads();     // all reads of sz1 (raw z1) by other threads are per-owner: safe, but sz2 reads end here
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int r = g * 16 + q;
+    for (int q = 0; q < RPG; ++q) {
+      const int r = g * RPG + q;
       sz1[r][j] = da[q] * dleaky(sz1[r][j], alpha1);
     }
     __syncthreads();
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 #pragma unroll
   for (int q = 0; q < KPT; ++q) atomicAdd(&dW1[(g * KPT + q) * HU + j], aW1[q]);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) atomicAdd(&dW2[(g * 16 + q) * HU + j], aW2[q]);
+  for (int q = 0; q < UPG; ++q) atomicAdd(&dW2[(g * UPG + q) * HU + j], aW2[q]);
   red[g][j] = aW3;
   __syncthreads();
   if (g == 0) {

@@ -4,13 +4,13 @@
 // all remaining LSTM gradients are contractions over those rows:
 //   dW = x^T dz   [Din, 4H]      dU = h_{t-1}^T dz  [H, 4H]      db = 1^T dz  [4H]
 //   dx = dz W^T   [rows, Din]
-// hipBLASLt runs the first three as K = B*T (~23k) skinny GEMMs with poor tile
-// choices; here ONE kernel streams each 32-row tile of (dz, x, h_{t-1}) through
+// hipBLASLt runs the first three as K = B*T (~23k CML, ~2.3M SoilNet) skinny GEMMs with
+// poor tile choices; here ONE kernel streams each 32-row tile of (dz, x, h_{t-1}) through
 // LDS once and feeds all four products to v_mfma_f32_16x16x32_bf16:
 //   * grid = (gate-unit column blocks of 64) x (row splits); a workgroup keeps its
-//     dW^T / dU^T / db partial tiles in registers across all its row tiles and adds
-//     them to the gradient buffers with one fp32 atomic per element at the end
-//     (these can be the optimiser's flat gradient views: no AccumulateGrad pass);
+//     dW^T / dU^T / db partial tiles in registers across all its row tiles, writes them
+//     once to a workspace, and a reduce kernel adds the split sums to the gradient
+//     buffers (these can be the optimiser's flat gradient views: no AccumulateGrad pass);
 //   * db rides along as an extra constant-1 input channel of x (row Din of dW^T);
 //   * dx^T = W dz^T uses W as register-resident A fragments; with one column
 //     block (H <= 16) dx is stored directly, otherwise accumulated atomically.
@@ -22,14 +22,24 @@ constexpr int GR_ROWS = 32;         // rows (sequence, step) per tile = MFMA K
 constexpr int GR_CB = 64;           // gate-units per column block (4 waves x 16)
 constexpr int GR_LDR = GR_ROWS + 8; // padded LDS row length (bf16) of transposed images
 
-template <int H, int DT>            // DT = ceil((Din + 1) / 16) din tiles (incl. the bias channel)
+// One workgroup = (column block cb of 64 gate-units, row split s); it walks the row tiles
+// s, s + splits, ... with a one-tile register prefetch: tile i+1's dz / x / h_{t-1} loads are
+// issued before tile i's MFMAs and only waited for when tile i+1 is staged (LDS-only
+// barriers, so the loads stay in flight across them). Every tile's x and h rows are ONE
+// contiguous span (flat rows), streamed in GRX-float granules. The weight-gradient partial
+// tiles stay in VGPRs and are written once per workgroup, in MFMA-fragment order, to a
+// workspace that lstm_grads_reduce_kernel sums over the splits (fixed order, plain
+// read-modify-write into the gradient buffers: deterministic, no float atomics).
+template <int H, int DT, int GRX>
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
-    const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ dU,
-    float* __restrict__ db, long rows, long period, long hshift, int Din, int ldx, long dx_cb_stride, int lddx) {
+    const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
+    long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems) {
   constexpr int G4 = 4 * H;
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
+  constexpr int XGM = (GR_ROWS * 144 / GRX + 255) / 256;   // max x granules per thread
+  constexpr int HG = (GR_ROWS * H / 4 + 255) / 256;        // h float4 granules per thread
   __shared__ __attribute__((aligned(16))) __bf16 dzT[GR_CB][GR_LDR];          // [gu][row]
   __shared__ __attribute__((aligned(16))) __bf16 dzR[GR_ROWS][GR_CB + 8];     // [row][gu]
   __shared__ __attribute__((aligned(16))) __bf16 xT[DP][GR_LDR];             // [din][row]
@@ -41,8 +51,12 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
   const int col = lane & 15;
   const int quad = lane >> 4;
   const int cb = blockIdx.x;               // column block: gate-units [cb*64, cb*64+64)
+  const int split = blockIdx.y, splits = gridDim.y;
   const int gu0 = cb * GR_CB;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
+  const long nmine = split < ntiles ? (ntiles - 1 - split) / splits + 1 : 0;
+
+  for (int e = tid; e < DP * GR_LDR; e += 256) (&xT[0][0])[e] = (__bf16)0.f;   // channels > Din stay 0
 
   f32x4_t accW[DT], accU[HT];
 #pragma unroll
@@ -52,7 +66,6 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
 
   // dx work items of this wave: (din tile, row tile) pairs, 2 row tiles per 32 rows
   constexpr int DXT = (DP + 15) / 16 * 2;
-  // A fragments of W for dx^T = W dz^T: rows = din, k = gate-units of this block
   bf16x8_t wa[(DXT + 3) / 4][2];
 #pragma unroll
   for (int i = 0; i < (DXT + 3) / 4; ++i) {
@@ -71,42 +84,92 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
     }
   }
 
-  for (long tile = blockIdx.y; tile < ntiles; tile += gridDim.y) {
+  // ---- per-tile register images (prefetch ring of depth 1)
+  float4 rz[2];                     // dz: rows tid/16 and tid/16 + 16, gate-units 4*(tid%16) ..
+  float rx[XGM][GRX];               // x granules of the contiguous [32][ldx] span
+  float4 rh[HG];                    // h_{t-1} granules of the contiguous [32][H] span
+  const int zr = tid >> 4, zc = (tid & 15) * 4;
+  const long xspan = (long)GR_ROWS * ldx;
+  const long hspan = (long)GR_ROWS * H;
+  // x_elems: floats readable from x (a strided view may end before rows * ldx)
+  const long xlast = (x_elems - GRX) / GRX * GRX, hlast = rows * (long)H - 4;
+  auto load_tile = [&](long tile) {
     const long r0 = tile * GR_ROWS;
-    // ---- stage dz (both orientations), x^T (+ ones channel) and h_{t-1}^T as bf16
-    for (int e = tid; e < GR_ROWS * (GR_CB / 4); e += 256) {
-      const int rr = e / (GR_CB / 4);
-      const int c4 = (e % (GR_CB / 4)) * 4;
-      const long r = min(r0 + rr, rows - 1);
-      float4 v = *reinterpret_cast<const float4*>(dz + (size_t)r * G4 + gu0 + c4);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const long r = min(r0 + zr + 16 * q, rows - 1);
+      rz[q] = *reinterpret_cast<const float4*>(dz + (size_t)r * G4 + gu0 + zc);
+    }
+    // granule offsets are clamped into the tile's span (idle lanes re-read a line already
+    // being fetched instead of the next tile's data) and into the array (rows past the end
+    // and h_{t-1} of a period's first step are masked when staged)
+#pragma unroll
+    for (int i = 0; i < XGM; ++i) {
+      if (i < xg) {                               // kernel argument: a scalar (uniform) branch
+        const long o = min(r0 * ldx + min((long)(tid + 256 * i) * GRX, xspan - GRX), xlast);
+        if constexpr (GRX == 4) {
+          const float4 v = *reinterpret_cast<const float4*>(x + o);
+          rx[i][0] = v.x; rx[i][1] = v.y; rx[i][2] = v.z; rx[i][3] = v.w;
+        } else {
+          rx[i][0] = x[o];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < HG; ++i) {
+      const long o = min(max((r0 - hshift) * H + min((long)(tid + 256 * i) * 4, hspan - 4), 0L), hlast);
+      rh[i] = *reinterpret_cast<const float4*>(hseq + o);
+    }
+  };
+  auto stage_tile = [&](long tile) {
+    const long r0 = tile * GR_ROWS;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int rr = zr + 16 * q;
       const float m = (r0 + rr < rows) ? 1.f : 0.f;
-      const __bf16 b0 = (__bf16)(v.x * m), b1 = (__bf16)(v.y * m), b2 = (__bf16)(v.z * m), b3 = (__bf16)(v.w * m);
+      const __bf16 b0 = (__bf16)(rz[q].x * m), b1 = (__bf16)(rz[q].y * m), b2 = (__bf16)(rz[q].z * m),
+                   b3 = (__bf16)(rz[q].w * m);
       typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      *reinterpret_cast<bf16x4_t*>(&dzR[rr][c4]) = bf16x4_t{b0, b1, b2, b3};
-      dzT[c4 + 0][rr] = b0;
-      dzT[c4 + 1][rr] = b1;
-      dzT[c4 + 2][rr] = b2;
-      dzT[c4 + 3][rr] = b3;
+      *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = bf16x4_t{b0, b1, b2, b3};
+      dzT[zc + 0][rr] = b0;
+      dzT[zc + 1][rr] = b1;
+      dzT[zc + 2][rr] = b2;
+      dzT[zc + 3][rr] = b3;
     }
-    for (int e = tid; e < GR_ROWS * DP; e += 256) {
-      const int rr = e / DP;
-      const int d = e % DP;
-      const long r = r0 + rr;
-      const bool ok = r < rows;
-      const long rc = min(r, rows - 1);
-      float v = x[(size_t)rc * ldx + min(d, Din - 1)];
-      v = d < Din ? v : (d == Din ? 1.f : 0.f);
-      xT[d][rr] = (__bf16)(ok ? v : 0.f);
+#pragma unroll
+    for (int i = 0; i < XGM; ++i) {
+      const long g = (long)(tid + 256 * i) * GRX;
+      if (i < xg && g < xspan) {                  // xg: wave-uniform (kernel argument)
+        const int rr = (int)(g / ldx), d0 = (int)(g % ldx);
+        const float m = (r0 + rr < rows) ? 1.f : 0.f;
+#pragma unroll
+        for (int q = 0; q < GRX; ++q)
+          if (d0 + q < Din) xT[d0 + q][rr] = (__bf16)(rx[i][q] * m);
+      }
     }
-    for (int e = tid; e < GR_ROWS * H; e += 256) {
-      const int rr = e / H;
-      const int k = e % H;
-      const long r = r0 + rr;
-      const long rc = min(r, rows - 1);
-      const float v = hseq[(size_t)max(rc - hshift, 0L) * H + k];   // h_{t-1}: hshift rows back
-      hT[k][rr] = (__bf16)((r < rows && rc % period >= hshift) ? v : 0.f);
+    if (tid < GR_ROWS) xT[Din][tid] = (__bf16)((r0 + tid < rows) ? 1.f : 0.f);   // bias channel
+#pragma unroll
+    for (int i = 0; i < HG; ++i) {
+      const int g = (tid + 256 * i) * 4;
+      if (g < GR_ROWS * H) {
+        const int rr = g / H, k0 = g % H;
+        const long r = r0 + rr;
+        const float m = (r < rows && r % period >= hshift) ? 1.f : 0.f;
+        hT[k0 + 0][rr] = (__bf16)(rh[i].x * m);
+        hT[k0 + 1][rr] = (__bf16)(rh[i].y * m);
+        hT[k0 + 2][rr] = (__bf16)(rh[i].z * m);
+        hT[k0 + 3][rr] = (__bf16)(rh[i].w * m);
+      }
     }
-    __syncthreads();
+  };
+
+  if (nmine > 0) load_tile(split);
+  for (long i = 0; i < nmine; ++i) {
+    const long tile = split + i * splits;
+    lds_barrier();                                // previous tile's LDS reads are done
+    stage_tile(tile);
+    load_tile(min(tile + splits, ntiles - 1));    // prefetch (the last one is a harmless reload)
+    lds_barrier();
     // ---- dW^T (wave w: gate-units [16w,16w+16) of the block) and dU^T
     const bf16x8_t az = *reinterpret_cast<const bf16x8_t*>(&dzT[16 * w + col][8 * quad]);
 #pragma unroll
@@ -121,16 +184,17 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
     }
     // ---- dx^T tiles: item = (din tile, row tile)
     if (dx != nullptr) {
+      const long r0 = tile * GR_ROWS;
 #pragma unroll
-      for (int i = 0; i < (DXT + 3) / 4; ++i) {
-        const int item = w + 4 * i;
+      for (int ii = 0; ii < (DXT + 3) / 4; ++ii) {
+        const int item = w + 4 * ii;
         if (item < DXT) {   // wave-uniform
           const int dtile = item >> 1, rt = item & 1;
           f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
             const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&dzR[16 * rt + col][32 * ks + 8 * quad]);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks], bz, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ii][ks], bz, acc, 0, 0, 0);
           }
           const long r = r0 + 16 * rt + col;
           if (r < rows) {
@@ -138,48 +202,102 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int din = dtile * 16 + 4 * quad + q;
-              if (din < Din) {
-                o[din] = acc[q];
-              }
+              if (din < Din) o[din] = acc[q];
             }
           }
         }
       }
     }
-    __syncthreads();
   }
-  // ---- flush partial weight gradients. The C tiles hold [gate-unit][din|k] with
-  // the gate-unit on 4 rows per lane; transpose them through LDS so that every
-  // atomic wave-instruction adds 64 consecutive gate-units (256 contiguous bytes:
-  // the full-rate shape; one lane per row would run ~17x slower).
-  __shared__ float fl[DP + H][GR_CB + 1];
+  // ---- partial tiles -> workspace record of this workgroup, fragment order (float4 per lane)
+  float* rec = ws + ((size_t)split * gridDim.x + cb) * (size_t)(DT + HT) * 1024;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 16 * w + 4 * quad + q;
+  for (int d = 0; d < DT; ++d)
+    *reinterpret_cast<f32x4_t*>(rec + ((size_t)(d * 4 + w) * 64 + lane) * 4) = accW[d];
 #pragma unroll
-    for (int d = 0; d < DT; ++d) fl[16 * d + col][c] = accW[d][q];
-#pragma unroll
-    for (int k = 0; k < HT; ++k) fl[DP + 16 * k + col][c] = accU[k][q];
+  for (int k = 0; k < HT; ++k)
+    *reinterpret_cast<f32x4_t*>(rec + ((size_t)((DT + k) * 4 + w) * 64 + lane) * 4) = accU[k];
+}
+
+// Reduction of the per-split records in a fixed order (deterministic):
+//   reduce: workgroup = 16 consecutive record slots x 16 split lanes (x NG split groups in
+//           grid.y); split lane l of group g sums splits g*16 + l, + 16*NG, ...; the 16 lane
+//           partials are combined through LDS. With NG == 1 (up to 512 splits) the result is
+//           added to the gradient buffers directly, else it goes to ws2[g][slot] and
+//   final:  thread = record slot sums its NG group sums and adds them.
+// Adding: one writer per element, plain read-modify-write into dW [Din,4H] / db / dU [H,4H].
+__device__ __forceinline__ void grads_add(float s, int e, int ncb, int DT, int HT, int Din, int H,
+                                          float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dU) {
+  const int R = (DT + HT) * 1024;
+  const int G4 = 4 * H;
+  // record layout: [split][cb][DT + HT fragments][4 waves][64 lanes][4]
+  const int cb = e / R, slot = e % R;
+  const int q = slot & 3, lane = (slot >> 2) & 63, w = (slot >> 8) & 3, j = slot >> 10;
+  const int colr = lane & 15, quad = lane >> 4;
+  const int gu = cb * GR_CB + 16 * w + 4 * quad + q;
+  if (j < DT) {
+    const int din = 16 * j + colr;
+    if (din < Din) dW[(size_t)din * G4 + gu] += s;
+    else if (din == Din) db[gu] += s;
+  } else {
+    const int k = 16 * (j - DT) + colr;
+    if (k < H) dU[(size_t)k * G4 + gu] += s;
   }
+}
+
+__global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __restrict__ ws, int splits, int RC,
+                                                                float* __restrict__ ws2, int ncb, int DT, int HT,
+                                                                int Din, int H, float* __restrict__ dW,
+                                                                float* __restrict__ db, float* __restrict__ dU) {
+  __shared__ float red[16][17];
+  const int sl = threadIdx.x & 15, l = threadIdx.x >> 4;
+  const int slot = min(blockIdx.x * 16 + sl, RC - 1);
+  const int g = blockIdx.y, NG = gridDim.y;
+  const int stride = 16 * NG;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int sp = g * 16 + l;
+  for (; sp + 3 * stride < splits; sp += 4 * stride) {
+    a0 += ws[(size_t)sp * RC + slot];
+    a1 += ws[(size_t)(sp + stride) * RC + slot];
+    a2 += ws[(size_t)(sp + 2 * stride) * RC + slot];
+    a3 += ws[(size_t)(sp + 3 * stride) * RC + slot];
+  }
+  for (; sp < splits; sp += stride) a0 += ws[(size_t)sp * RC + slot];
+  red[l][sl] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  for (int e = tid; e < (DP + H) * GR_CB; e += 256) {
-    const int row = e / GR_CB, c = e % GR_CB;
-    const float v = fl[row][c];
-    if (row < Din) atomicAdd(dW + (size_t)row * G4 + gu0 + c, v);
-    else if (row == Din) atomicAdd(db + gu0 + c, v);
-    else if (row >= DP) atomicAdd(dU + (size_t)(row - DP) * G4 + gu0 + c, v);
+  if (threadIdx.x < 16 && blockIdx.x * 16 + sl < RC) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][sl];
+    if (NG == 1) grads_add(s, slot, ncb, DT, HT, Din, H, dW, db, dU);
+    else ws2[(size_t)g * RC + slot] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void lstm_grads_reduce_final_kernel(const float* __restrict__ ws2, int NG, int RC,
+                                                                      int ncb, int DT, int HT, int Din, int H,
+                                                                      float* __restrict__ dW, float* __restrict__ db,
+                                                                      float* __restrict__ dU) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < RC; e += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int g = 0; g < NG; ++g) s += ws2[(size_t)g * RC + e];
+    grads_add(s, e, ncb, DT, HT, Din, H, dW, db, dU);
   }
 }
 
 template <int H>
-void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const float* x, const float* h,
-                    const float* W, float* dx, float* dW, float* dU, float* db, long rows, long period, long hshift,
-                    int Din, int ldx, long dx_cb_stride, int lddx) {
+void launch_grads_h(int DT, int grx, dim3 grid, hipStream_t st, const float* dz, const float* x, const float* h,
+                    const float* W, float* dx, float* ws, long rows, long period, long hshift, int Din, int ldx,
+                    long dx_cb_stride, int lddx, int xg, long x_elems) {
   switch (DT) {
 #define GQ_DT(D)                                                                                              \
   case D:                                                                                                     \
-    hipLaunchKernelGGL((lstm_grads_kernel<H, D>), grid, dim3(256), 0, st, dz, x, h, W, dx, dW, dU, db, rows, period, \
-                       hshift, Din, ldx, dx_cb_stride, lddx);                                                           \
+    if (grx == 4)                                                                                             \
+      hipLaunchKernelGGL((lstm_grads_kernel<H, D, 4>), grid, dim3(256), 0, st, dz, x, h, W, dx, ws, rows,     \
+                         period, hshift, Din, ldx, dx_cb_stride, lddx, xg, x_elems);                          \
+    else                                                                                                      \
+      hipLaunchKernelGGL((lstm_grads_kernel<H, D, 1>), grid, dim3(256), 0, st, dz, x, h, W, dx, ws, rows,     \
+                         period, hshift, Din, ldx, dx_cb_stride, lddx, xg, x_elems);                          \
     break;
     GQ_DT(1) GQ_DT(2) GQ_DT(3) GQ_DT(4) GQ_DT(5) GQ_DT(6) GQ_DT(7) GQ_DT(8) GQ_DT(9)
 #undef GQ_DT
@@ -194,18 +312,30 @@ void launch_grads_h(int DT, dim3 grid, hipStream_t st, const float* dz, const fl
 //   sequence-major [M,T,C]: period = T, hshift = 1;  time-major [T,Mp,C]: period = T*Mp, hshift = Mp.
 void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
-                     long dx_cb_stride, int lddx, hipStream_t st) {
+                     long dx_cb_stride, int lddx, long x_elems, hipStream_t st) {
   if (rows == 0) return;
+  TORCH_CHECK(ldx >= Din && ldx <= 144, "gnnqc lstm_grads: x row pitch ", ldx, " (Din ", Din, ")");
   const int ncb = (4 * H) / GR_CB;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
-  // enough workgroups to fill the chip, few enough that the final atomics stay cheap
-  const int splits = deterministic_mode() ? 1 : (int)std::max<long>(1, std::min<long>(ntiles, std::max(32, 256 / ncb)));
-  dim3 grid(ncb, splits);
+  // ~2 tiles per workgroup for small row counts (latency: everything in flight at once),
+  // up to ~8 workgroups per CU for large ones. The split count depends only on the shape
+  // and the reduce kernel sums in a fixed order: bitwise reproducible in every mode.
+  const int splits = (int)std::max<long>(1, std::min<long>((ntiles + 1) / 2, std::max(64, 2048 / ncb)));
   const int DT = (Din + 1 + 15) / 16;
+  const int HT = H / 16;
+  const int grx = (ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) ? 4 : 1;
+  const int xg = (int)((GR_ROWS * (long)ldx / grx + 255) / 256);
+  const int RC = (DT + HT) * 1024 * ncb;          // floats per split record (all column blocks)
+  const int NG = std::max(1, splits / 512);       // split groups of the reduction
+  auto ws_t = at::empty({(long)splits * RC + (NG > 1 ? (long)NG * RC : 0L)},
+                        at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, c10::hip::current_device()));
+  float* ws = ws_t.data_ptr<float>();
+  float* ws2 = ws + (size_t)splits * RC;
+  dim3 grid(ncb, splits);
 #define GQ_GR_H(HH)                                                                                              \
   case HH:                                                                                                       \
-    launch_grads_h<HH>(DT, grid, st, dz, x, hseq, W, dx, dW, dU, db, rows, period, hshift, Din, ldx, dx_cb_stride, \
-                       lddx);                                                                                    \
+    launch_grads_h<HH>(DT, grx, grid, st, dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride,  \
+                       lddx, xg, x_elems);                                                                       \
     break;
   switch (H) {
     GQ_GR_H(16) GQ_GR_H(32) GQ_GR_H(64) GQ_GR_H(128)
@@ -213,6 +343,14 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
   }
 #undef GQ_GR_H
   GQ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(lstm_grads_reduce_kernel, dim3((RC + 15) / 16, NG), dim3(256), 0, st, ws, splits, RC, ws2, ncb,
+                     DT, HT, Din, H, dW, db, dU);
+  GQ_LAUNCH_CHECK();
+  if (NG > 1) {
+    hipLaunchKernelGGL(lstm_grads_reduce_final_kernel, dim3(std::min((RC + 255) / 256, 1024)), dim3(256), 0, st, ws2,
+                       NG, RC, ncb, DT, HT, Din, H, dW, db, dU);
+    GQ_LAUNCH_CHECK();
+  }
 }
 
 int lstm_grads_col_blocks(int H) { return (4 * H) / GR_CB; }
@@ -246,7 +384,8 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   if (rows == 0) return need_dx ? dx.sum(0) : dx;
   lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
                   need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
-                  db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, Din, stream());
+                  db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, Din,
+                  (long)(x.storage().nbytes() / sizeof(float)) - x.storage_offset(), stream());
   if (!need_dx) return dx;
   return ncb == 1 ? dx[0] : dx.sum(0);
 }

@@ -32,7 +32,7 @@ namespace gq {
 // lstm_grads.hip: weight gradients (+ dx) over flat rows, h_{t-1} hshift rows back
 void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
-                     long dx_cb_stride, int lddx, hipStream_t st);
+                     long dx_cb_stride, int lddx, long x_elems, hipStream_t st);
 int lstm_grads_col_blocks(int H);
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -201,6 +201,158 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
           const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
           *reinterpret_cast<float4*>(gbuf + o * 4) = make_float4(iv, fv, gv, ov);
           cbuf[o] = c[cc];
+        }
+      }
+      lds_barrier();
+    }
+  }
+}
+
+// =====================================================================================
+// forward of a layer PAIR (layer A: Din -> H, layer B: H -> H, both return_sequences),
+// wavefront-pipelined inside one workgroup: waves [0, NW) run layer A at step s while waves
+// [NW, 2 NW) run layer B at step s - 1, fed from A's bf16 h tile in LDS (no HBM round trip,
+// no second launch). One LDS barrier per step for both layers, so the pair costs ~one
+// recurrence of T + 1 steps instead of two of T. Outputs and saved state are exactly those
+// of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
+// (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
+template <int H, bool TRAIN, int KX, int GR, int D>
+__global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
+    const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
+    const float* __restrict__ bB, float* __restrict__ hA, float* __restrict__ gA, float* __restrict__ cA,
+    float* __restrict__ hB, float* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw) {
+  using C = TMC<H>;
+  static_assert(C::CPL == 1, "pair kernel: one cell per lane (H <= 64)");
+  constexpr int NW = C::NW, NTL = C::NT, G4 = C::G4;
+  constexpr int KPX = 32 * KX;
+  constexpr int KS = C::KSH;                       // K steps over an H-wide operand
+  constexpr int KW = KX > KS ? KX : KS;
+  __shared__ __attribute__((aligned(16))) __bf16 hsA[2][16][C::KPH + 8];
+  __shared__ __attribute__((aligned(16))) __bf16 hsB[2][16][C::KPH + 8];
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
+  __shared__ __attribute__((aligned(16))) float hfA[2][16][H];
+  __shared__ __attribute__((aligned(16))) float hfB[2][16][H];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool layerB = wv >= NW;                     // SGPR: branches on it are scalar
+  const int w = layerB ? wv - NW : wv;
+  const int tl = tid - (layerB ? NTL : 0);          // thread index within the layer
+  const int col = lane & 15, quad = lane >> 4;
+  const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
+
+  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += 2 * NTL) {
+    (&hsA[0][0][0])[i] = (__bf16)0.0f;
+    (&hsB[0][0][0])[i] = (__bf16)0.0f;
+  }
+  for (int i = tid; i < 2 * 16 * (KPX + 8); i += 2 * NTL) (&xs[0][0][0])[i] = (__bf16)0.0f;
+
+  // A fragments (rows permuted as in lstm_tm_fwd_kernel): U and W of this wave's layer
+  const float* Ul = layerB ? UB : UA;
+  const float* Wl = layerB ? WB : WA;
+  const float* bl = layerB ? bB : bA;
+  const int Dl = layerB ? H : Dw;                   // rows of this layer's W
+  bf16x8_t ufr[KS], wfr[KW];
+  const int au = 4 * w + (col >> 2), ag = col & 3;
+  const int unit = 4 * w + quad;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * s + 8 * quad + j;
+      v[j] = (__bf16)(Ul[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+    }
+    ufr[s] = v;
+  }
+#pragma unroll
+  for (int s = 0; s < KW; ++s) {
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * s + 8 * quad + j;
+      v[j] = (__bf16)(Wl[min(k, Dl - 1) * G4 + ag * H + au] * (k < Dl ? 1.0f : 0.0f));
+    }
+    wfr[s] = v;
+  }
+  const f32x4_t bias4 = f32x4_t{bl[unit], bl[H + unit], bl[2 * H + unit], bl[3 * H + unit]};
+
+  // x loader (all threads, granule tid mod n; duplicates are identical) and h storers
+  const int n_gx = 16 * Din / GR;
+  const int gx = (tid % n_gx) * GR;
+  const int gx_seq = gx / Din, gx_k = gx % Din;
+  const float* xbase = x + (size_t)row0 * Din + gx;
+  const size_t xstep = (size_t)Mp * Din;
+  Granule<GR> xr[D];
+  constexpr int n_gh = 16 * H / 4;
+  const int gh = (tl % n_gh) * 4;
+  float* hbase = (layerB ? hB : hA) + (size_t)row0 * H + gh;
+  const size_t hstep = (size_t)Mp * H;
+  float* gbuf = layerB ? gB : gA;
+  float* cbuf = layerB ? cB : cA;
+  __bf16(*hsW)[16][C::KPH + 8] = layerB ? hsB : hsA;    // this layer's recurrent tile
+  float(*hfW)[16][H] = layerB ? hfB : hfA;
+
+#pragma unroll
+  for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < GR; ++q) xs[0][gx_seq][gx_k + q] = (__bf16)xr[0].v[q];
+  xr[0].load(xbase + (size_t)min(D, T - 1) * xstep);
+  float c = 0.f;
+  __syncthreads();
+
+  // steps 0 .. T+1: A computes t = s (s < T), B computes t = s - 1 (1 <= s <= T); each layer
+  // stores the h tile of its previous step (A: s - 1, B: s - 2; invalid -> scratch row T)
+  for (int t0 = 0; t0 <= T + 1; t0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int s = t0 + j;
+      const int p = s & 1;
+      const int jn = (j + 1 == D) ? 0 : j + 1;
+      const int tc = layerB ? s - 1 : s;             // time step this layer computes
+      {
+        const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
+        const float4 v = *reinterpret_cast<const float4*>(&hfW[p ^ 1][0][0] + gh);
+        *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+      }
+      f32x4_t acc = bias4;
+      if (layerB) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&hsA[p][col][32 * k + 8 * quad]);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, acc, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {
+          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * k + 8 * quad]);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, acc, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hsW[p][col][32 * k + 8 * quad]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bh, acc, 0, 0, 0);
+      }
+      // stage x_{s+1}, refill the slot with x_{s+1+D}
+#pragma unroll
+      for (int q = 0; q < GR; ++q) xs[p ^ 1][gx_seq][gx_k + q] = (__bf16)xr[jn].v[q];
+      xr[jn].load(xbase + (size_t)min(s + 1 + D, T - 1) * xstep);
+      if (tc >= 0) {                                 // B idles at s = 0 (keeps c = 0, h = 0)
+        const float iv = sigmoidf_fast(acc[0]);
+        const float fv = sigmoidf_fast(acc[1]);
+        const float gv = tanhf_fast(acc[2]);
+        const float ov = sigmoidf_fast(acc[3]);
+        c = fv * c + iv * gv;
+        const float hv = ov * tanhf_fast(c);
+        hsW[p ^ 1][col][unit] = (__bf16)hv;
+        hfW[p][col][unit] = hv;
+        if constexpr (TRAIN) {                       // steps past T-1 write the scratch row T
+          const size_t o = (((size_t)min(tc, T) * ntiles + tile) * NW + w) * 64 + lane;
+          *reinterpret_cast<float4*>(gbuf + o * 4) = make_float4(iv, fv, gv, ov);
+          cbuf[o] = c;
         }
       }
       lds_barrier();
@@ -503,6 +655,47 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   return {h.narrow(0, 0, T), g, c};
 }
 
+// Pair forward (lstm_tm2_fwd_kernel): x [T, Mp, Din]; A: W [Dw <= Din, 4H], B: W [H, 4H].
+// Returns [hA, gA, cA, hB, gB, cB] with the layouts of lstm_tm_fwd.
+std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, const at::Tensor& UA,
+                                     const at::Tensor& bA, const at::Tensor& WB, const at::Tensor& UB,
+                                     const at::Tensor& bB, bool train) {
+  for (const at::Tensor* t : {&x, &WA, &UA, &bA, &WB, &UB, &bB}) check_f32_cuda(*t, "lstm_tm2_fwd operand");
+  TORCH_CHECK(x.dim() == 3, "lstm_tm2_fwd: x must be [T, Mp, Din]");
+  const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)UA.size(0);
+  const int Dw = (int)WA.size(0);
+  TORCH_CHECK(Mp % 16 == 0 && Mp > 0 && T > 0, "lstm_tm2_fwd: Mp must be a positive multiple of 16");
+  TORCH_CHECK(UA.size(1) == 4 * H && Dw >= 1 && Dw <= Din && WA.size(1) == 4 * H && bA.numel() == 4 * H,
+              "lstm_tm2_fwd: layer A weight shapes");
+  TORCH_CHECK(UB.size(0) == H && UB.size(1) == 4 * H && WB.size(0) == H && WB.size(1) == 4 * H && bB.numel() == 4 * H,
+              "lstm_tm2_fwd: layer B must be H -> H with the same H");
+  const int gr = tm_granule(Din, x.data_ptr());
+  TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm2_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
+  c10::DeviceGuard guard(x.device());
+  auto opt = x.options();
+  auto mk = [&](bool state, int last) {
+    return state ? (train ? at::empty({T + 1, Mp, H, last}, opt) : at::empty({0}, opt)) : at::empty({T + 1, Mp, H}, opt);
+  };
+  at::Tensor hA = mk(false, 0), hB = mk(false, 0);
+  at::Tensor gA = mk(true, 4), gB = mk(true, 4);
+  at::Tensor cA = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
+  at::Tensor cB = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
+  const int ntiles = Mp / 16;
+  auto st = stream();
+  float* P[4] = {train ? gA.data_ptr<float>() : nullptr, train ? cA.data_ptr<float>() : nullptr,
+                 train ? gB.data_ptr<float>() : nullptr, train ? cB.data_ptr<float>() : nullptr};
+#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR)                                                                         \
+  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,        \
+                     x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
+                     WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), P[0], \
+                     P[1], hB.data_ptr<float>(), P[2], P[3], Mp, T, Din, Dw)
+  GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
+      if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR); else GQ_TM2_LAUNCH(HH, false, KXX, GRR))));
+#undef GQ_TM2_LAUNCH
+  GQ_LAUNCH_CHECK();
+  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB};
+}
+
 // dh: [T, Mp, H] (or [Mp, H] when only the last step has a gradient). Returns dx [T, Mp, Din]
 // (empty if !need_dx) and accumulates dW, dU, db when they are non-empty.
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
@@ -546,7 +739,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
                             : at::empty({0}, x.options());
     lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                     need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
-                    db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, st);
+                    db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, st);
     if (!need_dx) return dx;
     return ncb == 1 ? dx[0] : dx.sum(0);
   }
@@ -567,5 +760,6 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_tm_fwd", &gq::lstm_tm_fwd);
+  m.impl("lstm_tm2_fwd", &gq::lstm_tm2_fwd);
   m.impl("lstm_tm_bwd", &gq::lstm_tm_bwd);
 }

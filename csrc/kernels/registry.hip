@@ -25,6 +25,8 @@ TORCH_LIBRARY(gnnqc, m) {
         "bool need_dx) -> Tensor");
   // time-major LSTM with fused backward (lstm_tm.hip)
   m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train) -> Tensor[]");
+  m.def("lstm_tm2_fwd(Tensor x, Tensor WA, Tensor UA, Tensor bA, Tensor WB, Tensor UB, Tensor bB, bool train) "
+        "-> Tensor[]");
   m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor(a!) dW, "
         "Tensor(b!) dU, Tensor(c!) db, bool need_dx) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)

@@ -20,6 +20,11 @@ import torch.nn as nn
 from .layers import LSTM, Conv1D, GlobalAveragePooling1D, LeakyReLU, MaxPooling1D
 
 
+def _pair_fusion() -> bool:
+    """Layer-pair forward fusion (``lstm_tm2_fwd``); ``GNNQC_NO_PAIR=1`` disables it."""
+    return os.environ.get("GNNQC_NO_PAIR", "0") != "1"
+
+
 class TimeLayer(nn.Module):
     def __init__(self, in_features: int, filter_1_size: int = 8, n_stacks: int = 2, layer_type: str = "lstm",
                  activation: str = "tanh", kernel_size: Optional[int] = 5, regularizer: Optional[float] = None,
@@ -95,12 +100,24 @@ class TimeLayer(nn.Module):
         rows past M; C may carry zero channels past the first layer's input width).
         Returns ``[M, out_features]``. Producers that can write this layout directly (the
         SoilNet GCN kernel) skip the transpose/pad copy of :meth:`_forward_tm`."""
-        from ..ops.lstm import lstm_layer_tm, tm_eligible
+        from ..ops.lstm import lstm_layer_tm, lstm_pair_tm, tm_eligible
         from ..ops.pool import max_pool1d_tm
         tm = True
-        for mod in self._sequence():
+        seq = self._sequence()
+        i = 0
+        while i < len(seq):
+            mod = seq[i]
+            i += 1
             if isinstance(mod, MaxPooling1D):
                 h = max_pool1d_tm(h, mod.pool_size) if tm else mod(h)
+                continue
+            nxt = seq[i] if i < len(seq) else None
+            if (tm and isinstance(nxt, LSTM) and mod.return_sequences and nxt.return_sequences
+                    and nxt.units == mod.units and nxt.kernel.shape[0] == mod.units and _pair_fusion()
+                    and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16)
+                    and nxt.activation == mod.activation and nxt.compute_bf16 == mod.compute_bf16):
+                h = lstm_pair_tm(h, mod, nxt)            # two layers, one pipelined forward kernel
+                i += 1
                 continue
             if tm and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16):
                 h = lstm_layer_tm(h, mod.kernel, mod.recurrent_kernel, mod.bias, mod.return_sequences)

@@ -166,6 +166,55 @@ class _HipLSTMTM(torch.autograd.Function):
         return (dx if need_dx else None, *grads, None)
 
 
+class _HipLSTMTMPair(torch.autograd.Function):
+    """Two stacked time-major layers A (Din -> H) and B (H -> H), both returning sequences:
+    ONE wavefront-pipelined forward kernel (``lstm_tm2_fwd``); the backward runs the
+    per-layer fused kernels (B first, its dx is A's dh)."""
+
+    @staticmethod
+    def forward(ctx, x, WA, UA, bA, WB, UB, bB):
+        from ..utils.native import hip_ops
+        x = x.contiguous()
+        need = any(ctx.needs_input_grad[:7])
+        hA, gA, cA, hB, gB, cB = hip_ops().lstm_tm2_fwd(x, WA.contiguous(), UA.contiguous(), bA.contiguous(),
+                                                        WB.contiguous(), UB.contiguous(), bB.contiguous(), need)
+        ctx.params = (WA, UA, bA, WB, UB, bB)
+        if need:
+            ctx.save_for_backward(x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB)
+        return hB
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..utils.native import hip_ops
+        ops = hip_ops()
+        x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        e = x.new_zeros(0)
+
+        def sinks(params, flags):
+            if any(flags):
+                return [_grad_sink(p) for p in params]
+            return [(e, True)] * 3
+
+        sB = sinks(ctx.params[3:], need[4:7])
+        dhA = ops.lstm_tm_bwd(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
+                              sB[0][0], sB[1][0], sB[2][0], True)
+        sA = sinks(ctx.params[:3], need[1:4])
+        need_dx = bool(need[0])
+        dx = None
+        if need_dx or any(need[1:4]):
+            dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0], sA[2][0],
+                                 need_dx)
+        gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
+        gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
+        return (dx if need_dx else None, *gA_, *gB_)
+
+
+def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:
+    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``)."""
+    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias)
+
+
 def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf16: bool = True) -> bool:
     """Whether the time-major fused kernels handle this layer (GPU, bf16, tanh, H in {16, 32})."""
     from . import use_hip
@@ -188,4 +237,4 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     return lstm_eager(x, W, U, b, return_sequences, activation)
 
 
-__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "tm_eligible"]
+__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "tm_eligible"]

@@ -536,3 +536,56 @@ def test_soilnet_gcn_fused_path_matches_eager(cuda_device, monkeypatch):
     assert set(g1) == set(g0)
     for k in g0:
         assert (g1[k] - g0[k]).norm().item() < 8e-2 * (g0[k].norm().item() + 1e-6), k
+
+
+@pytest.mark.parametrize("H,Din", [(16, 20), (16, 16), (32, 16), (32, 32)])
+@pytest.mark.parametrize("wgrad", [True, False])
+def test_lstm_pair_fused_forward_matches_two_layers(cuda_device, H, Din, wgrad):
+    """lstm_tm2_fwd (layer pair, one pipelined kernel) == two lstm_tm_fwd layers, incl. gradients."""
+    from gnnqc.ops.lstm import _HipLSTMTMPair, lstm_layer_tm
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(H * 7 + Din)
+    T, M = 23, 40
+    x = torch.zeros(T, 48, Din, device=dev)
+    x[:, :M, : Din - 1] = torch.randn(T, M, Din - 1, generator=gen).to(dev)   # last channel: zero pad
+    WA, UA, bA = _lstm_params(Din - 1 if Din == 20 else Din, H, gen, dev)
+    WB, UB, bB = _lstm_params(H, H, gen, dev)
+    ps1 = [t.clone().requires_grad_(wgrad) for t in (WA, UA, bA, WB, UB, bB)]
+    ps2 = [t.clone().requires_grad_(wgrad) for t in (WA, UA, bA, WB, UB, bB)]
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.clone().requires_grad_(True)
+    out1 = _HipLSTMTMPair.apply(x1, *ps1)
+    out2 = lstm_layer_tm(lstm_layer_tm(x2, *ps2[:3], True), *ps2[3:], True)
+    # same bf16 operands and accumulation order, but the compiler may contract the fp32 cell
+    # update differently in the two kernels: a 1-ulp difference can flip a bf16 rounding of h
+    torch.testing.assert_close(out1, out2, atol=2e-3, rtol=1e-2)
+    g = torch.randn(out1.shape, generator=gen).to(dev)
+    g[:, M:] = 0
+    out1.backward(g)
+    out2.backward(g)
+    for a, b_ in zip([x1.grad] + ([p.grad for p in ps1] if wgrad else []),
+                     [x2.grad] + ([p.grad for p in ps2] if wgrad else [])):
+        assert (a - b_).norm().item() <= 1e-2 * (b_.norm().item() + 1e-6)
+
+
+def test_timelayer_pair_fusion_matches_unfused(cuda_device, monkeypatch):
+    """CML TimeLayer: pair-fused forward vs per-layer kernels (outputs and all gradients)."""
+    from gnnqc.models.timelayer import TimeLayer
+    torch.manual_seed(0)
+    tl = TimeLayer(18, 16, 2, "lstm", pool_size=3).to(cuda_device)
+    x = torch.randn(128, 181, 18, device=cuda_device)
+
+    def run(no_pair):
+        monkeypatch.setenv("GNNQC_NO_PAIR", "1" if no_pair else "0")
+        xi = x.clone().requires_grad_(True)
+        for p in tl.parameters():
+            p.grad = None
+        out = tl(xi)
+        out.pow(2).sum().backward()
+        return out.detach(), [xi.grad.clone()] + [p.grad.clone() for p in tl.parameters()]
+
+    o0, g0 = run(True)
+    o1, g1 = run(False)
+    torch.testing.assert_close(o1, o0, atol=2e-3, rtol=1e-2)
+    for a, b_ in zip(g1, g0):
+        assert (a - b_).norm().item() <= 2e-2 * (b_.norm().item() + 1e-6)
