@@ -69,6 +69,103 @@ at::Tensor window_gather(const at::Tensor& series, const at::Tensor& shift, cons
   return out;
 }
 
+// Everything else a batch needs, one workgroup per sample (replaces ~12 small indexing /
+// masking launches): node mask, masked adjacency, flagged-node position, labels and label
+// mask, and (CML) the flagged sensor's series cut from the gathered x.
+//   vm[b,n]    = (w >= 0) * win_valid[w,n]
+//   adj[b,i,j] = group_adj[g,i,j] * vm[b,i] * vm[b,j]
+//   CML:     y[b] = win_label[w] * ok, y_mask[b] = ok, anom[b,t,c] = x[b,t,max(ap,0),c]
+//   SoilNet: y[b,n] = win_label[w,n] * vm[b,n], y_mask[b,n] = win_label_valid[w,n] * ok
+// with w = max(wids[b], 0), g = win_group[w], ok = (wids[b] >= 0) * valid_sample[b].
+__global__ __launch_bounds__(256) void batch_meta_kernel(
+    const long* __restrict__ wids, const long* __restrict__ wg, const uint8_t* __restrict__ wv,
+    const float* __restrict__ gadj, const long* __restrict__ gap, const float* __restrict__ wlab,
+    const float* __restrict__ wlabv, const float* __restrict__ vsample, const float* __restrict__ x,
+    float* __restrict__ vm, float* __restrict__ adj, long* __restrict__ ap, float* __restrict__ y,
+    float* __restrict__ ym, float* __restrict__ anom, int N, int T, int C, int soil) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long wraw = wids[b];
+  const long w = wraw < 0 ? 0 : wraw;
+  const float ok = (wraw >= 0 ? 1.f : 0.f) * (vsample != nullptr ? vsample[b] : 1.f);
+  const long g = wg[w];
+  const float live = wraw >= 0 ? 1.f : 0.f;
+  __shared__ float svm[1024];
+  for (int n = tid; n < N; n += 256) {
+    const float v = live * (wv[w * N + n] ? 1.f : 0.f);
+    svm[n] = v;
+    vm[(long)b * N + n] = v;
+    if (soil) {
+      y[(long)b * N + n] = wlab[w * N + n] * v;
+      ym[(long)b * N + n] = wlabv[w * N + n] * ok;
+    }
+  }
+  __syncthreads();
+  const float* A = gadj + g * (long)N * N;
+  float* out = adj + (long)b * N * N;
+  for (int e = tid; e < N * N; e += 256) out[e] = A[e] * svm[e / N] * svm[e % N];
+  const long a = gap[g];
+  if (tid == 0) {
+    ap[b] = a;
+    if (!soil) {
+      y[b] = wlab[w] * ok;
+      ym[b] = ok;
+    }
+  }
+  if (!soil) {
+    const long n0 = a < 0 ? 0 : a;
+    for (int e = tid; e < T * C; e += 256) {
+      const int t = e / C, c = e % C;
+      anom[((long)b * T + t) * C + c] = x[(((long)b * T + t) * N + n0) * C + c];
+    }
+  }
+}
+
+// returns [vm, adj, anom_pos, y, y_mask, anom (CML; empty for SoilNet)]
+std::vector<at::Tensor> batch_meta(const at::Tensor& wids, const at::Tensor& win_group, const at::Tensor& win_valid,
+                                   const at::Tensor& group_adj, const at::Tensor& group_anom_pos,
+                                   const at::Tensor& win_label, const at::Tensor& win_label_valid,
+                                   const at::Tensor& valid_sample, const at::Tensor& x) {
+  TORCH_CHECK(wids.scalar_type() == at::kLong && win_group.scalar_type() == at::kLong &&
+                  group_anom_pos.scalar_type() == at::kLong, "batch_meta: index tensors must be int64");
+  TORCH_CHECK(win_valid.scalar_type() == at::kByte && win_valid.is_contiguous(), "batch_meta: win_valid uint8");
+  check_f32_cuda(group_adj, "group_adj");
+  check_f32_cuda(win_label, "win_label");
+  check_f32_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 4, "batch_meta: x must be [B,T,N,C]");
+  const int B = wids.size(0), T = x.size(1), N = x.size(2), C = x.size(3);
+  TORCH_CHECK(N <= 1024 && win_valid.size(1) == N && group_adj.size(1) == N && group_adj.size(2) == N,
+              "batch_meta: node dimension");
+  const bool soil = win_label.dim() == 2;
+  if (soil) {
+    check_f32_cuda(win_label_valid, "win_label_valid");
+    TORCH_CHECK(win_label.size(1) == N && win_label_valid.sizes() == win_label.sizes(), "batch_meta: label shapes");
+  }
+  const float* vs = nullptr;
+  if (valid_sample.numel() > 0) {
+    check_f32_cuda(valid_sample, "valid_sample");
+    TORCH_CHECK(valid_sample.numel() == B, "batch_meta: valid_sample must be [B]");
+    vs = valid_sample.data_ptr<float>();
+  }
+  c10::DeviceGuard guard(x.device());
+  auto fo = x.options();
+  at::Tensor vm = at::empty({B, N}, fo), adj = at::empty({B, N, N}, fo);
+  at::Tensor ap = at::empty({B}, wids.options());
+  at::Tensor y = soil ? at::empty({B, N}, fo) : at::empty({B}, fo);
+  at::Tensor ym = soil ? at::empty({B, N}, fo) : at::empty({B}, fo);
+  at::Tensor anom = soil ? at::empty({0}, fo) : at::empty({B, T, C}, fo);
+  hipLaunchKernelGGL(batch_meta_kernel, dim3(B), dim3(256), 0, stream(), wids.data_ptr<long>(),
+                     win_group.data_ptr<long>(), win_valid.data_ptr<uint8_t>(), group_adj.data_ptr<float>(),
+                     group_anom_pos.data_ptr<long>(), win_label.data_ptr<float>(),
+                     soil ? win_label_valid.data_ptr<float>() : nullptr, vs, x.data_ptr<float>(),
+                     vm.data_ptr<float>(), adj.data_ptr<float>(), ap.data_ptr<long>(), y.data_ptr<float>(),
+                     ym.data_ptr<float>(), soil ? nullptr : anom.data_ptr<float>(), N, T, C, soil ? 1 : 0);
+  GQ_LAUNCH_CHECK();
+  return {vm, adj, ap, y, ym, anom};
+}
+
 }  // namespace gq
 
-TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) { m.impl("window_gather", &gq::window_gather); }
+TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("window_gather", &gq::window_gather);
+  m.impl("batch_meta", &gq::batch_meta);
+}

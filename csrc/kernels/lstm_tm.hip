@@ -228,24 +228,21 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
   constexpr int KPX = 32 * KX;
   constexpr int KS = C::KSH;                       // K steps over an H-wide operand
   constexpr int KW = KX > KS ? KX : KS;
-  __shared__ __attribute__((aligned(16))) __bf16 hsA[2][16][C::KPH + 8];
-  __shared__ __attribute__((aligned(16))) __bf16 hsB[2][16][C::KPH + 8];
+  // [layer][parity]: indexed (not pointer-selected) so every access stays a DS instruction
+  __shared__ __attribute__((aligned(16))) __bf16 hs[2][2][16][C::KPH + 8];
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
-  __shared__ __attribute__((aligned(16))) float hfA[2][16][H];
-  __shared__ __attribute__((aligned(16))) float hfB[2][16][H];
+  __shared__ __attribute__((aligned(16))) float hf[2][2][16][H];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool layerB = wv >= NW;                     // SGPR: branches on it are scalar
+  const int L = layerB ? 1 : 0;
   const int w = layerB ? wv - NW : wv;
   const int tl = tid - (layerB ? NTL : 0);          // thread index within the layer
   const int col = lane & 15, quad = lane >> 4;
   const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
 
-  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += 2 * NTL) {
-    (&hsA[0][0][0])[i] = (__bf16)0.0f;
-    (&hsB[0][0][0])[i] = (__bf16)0.0f;
-  }
+  for (int i = tid; i < 2 * 2 * 16 * (C::KPH + 8); i += 2 * NTL) (&hs[0][0][0][0])[i] = (__bf16)0.0f;
   for (int i = tid; i < 2 * 16 * (KPX + 8); i += 2 * NTL) (&xs[0][0][0])[i] = (__bf16)0.0f;
 
   // A fragments (rows permuted as in lstm_tm_fwd_kernel): U and W of this wave's layer
@@ -291,8 +288,6 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
   const size_t hstep = (size_t)Mp * H;
   float* gbuf = layerB ? gB : gA;
   float* cbuf = layerB ? cB : cA;
-  __bf16(*hsW)[16][C::KPH + 8] = layerB ? hsB : hsA;    // this layer's recurrent tile
-  float(*hfW)[16][H] = layerB ? hfB : hfA;
 
 #pragma unroll
   for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
@@ -314,14 +309,14 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
       const int tc = layerB ? s - 1 : s;             // time step this layer computes
       {
         const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
-        const float4 v = *reinterpret_cast<const float4*>(&hfW[p ^ 1][0][0] + gh);
+        const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][0][0] + gh);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
       }
       f32x4_t acc = bias4;
       if (layerB) {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
-          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&hsA[p][col][32 * k + 8 * quad]);
+          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&hs[0][p][col][32 * k + 8 * quad]);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, acc, 0, 0, 0);
         }
       } else {
@@ -333,24 +328,27 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
       }
 #pragma unroll
       for (int k = 0; k < KS; ++k) {
-        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hsW[p][col][32 * k + 8 * quad]);
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[L][p][col][32 * k + 8 * quad]);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bh, acc, 0, 0, 0);
       }
       // stage x_{s+1}, refill the slot with x_{s+1+D}
 #pragma unroll
       for (int q = 0; q < GR; ++q) xs[p ^ 1][gx_seq][gx_k + q] = (__bf16)xr[jn].v[q];
       xr[jn].load(xbase + (size_t)min(s + 1 + D, T - 1) * xstep);
-      if (tc >= 0) {                                 // B idles at s = 0 (keeps c = 0, h = 0)
+      {
+        // branch-free (a branch here makes the compiler drain the x prefetch ring at the join):
+        // B's step s = 0 is masked to keep c = 0, h = 0
+        const float m = tc >= 0 ? 1.f : 0.f;
         const float iv = sigmoidf_fast(acc[0]);
         const float fv = sigmoidf_fast(acc[1]);
         const float gv = tanhf_fast(acc[2]);
         const float ov = sigmoidf_fast(acc[3]);
-        c = fv * c + iv * gv;
-        const float hv = ov * tanhf_fast(c);
-        hsW[p ^ 1][col][unit] = (__bf16)hv;
-        hfW[p][col][unit] = hv;
-        if constexpr (TRAIN) {                       // steps past T-1 write the scratch row T
-          const size_t o = (((size_t)min(tc, T) * ntiles + tile) * NW + w) * 64 + lane;
+        c = (fv * c + iv * gv) * m;
+        const float hv = ov * tanhf_fast(c) * m;
+        hs[L][p ^ 1][col][unit] = (__bf16)hv;
+        hf[L][p][col][unit] = hv;
+        if constexpr (TRAIN) {                       // invalid steps write the scratch row T
+          const size_t o = (((size_t)(tc >= 0 ? min(tc, T) : T) * ntiles + tile) * NW + w) * 64 + lane;
           *reinterpret_cast<float4*>(gbuf + o * 4) = make_float4(iv, fv, gv, ov);
           cbuf[o] = c;
         }
@@ -566,6 +564,173 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 }
 
 // =====================================================================================
+// backward of a layer PAIR (A: Din -> H, B: H -> H), wavefront-pipelined like the pair
+// forward: waves [0, NW) run B's reverse recurrence at time t = T-1-s, waves [NW, 2 NW) run
+// A's at t + 2, taking dh_A = W_B dz_B from LDS (written in B's MFMA phase two steps back:
+// the one barrier per step orders it before A's cell phase). Per step:
+// cell phase (dz of both layers -> LDS), one LDS barrier, MFMA phase (U dz for both chains,
+// W_B dz_B -> A's dh tile; both dz tiles -> HBM for the weight-gradient passes).
+// Replaces two lstm_tm_bwd_kernel launches (and B's dx round trip through HBM).
+template <int H, int D>
+__global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
+    const float* __restrict__ dhout, const float* __restrict__ gB, const float* __restrict__ cB,
+    const float* __restrict__ gA, const float* __restrict__ cA, const float* __restrict__ WB,
+    const float* __restrict__ UB, const float* __restrict__ UA, float* __restrict__ dzB, float* __restrict__ dzA,
+    int Mp, int T) {
+  using C = TMC<H>;
+  static_assert(C::CPL == 1, "pair kernel: one cell per lane");
+  constexpr int NW = C::NW, NTL = C::NT, G4 = C::G4, KB = C::KB;
+  constexpr int NXB = H / 16;                     // 16-row blocks of dx_B^T (din = H)
+  constexpr int TX = (NXB + NW - 1) / NW;
+  static_assert(16 * G4 / 4 == NTL, "one dz float4 granule per layer thread");
+  // [layer L (0 = B, 1 = A)][parity]; dd[0] = B's dh_out tile, dd[1] = W_B dz_B = A's dh tile.
+  // Indexed by the (uniform) layer, never pointer-selected: all accesses stay DS instructions.
+  __shared__ __attribute__((aligned(16))) __bf16 zs[2][2][16][G4 + 8];
+  __shared__ __attribute__((aligned(16))) float dd[2][2][16][H];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool layerA = wv >= NW;                   // SGPR
+  const int L = layerA ? 1 : 0;
+  const int w = layerA ? wv - NW : wv;
+  const int tl = tid - (layerA ? NTL : 0);
+  const int col = lane & 15, quad = lane >> 4;
+  const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
+
+  for (int i = tid; i < 2 * 2 * 16 * H; i += 2 * NTL) (&dd[0][0][0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * 2 * 16 * (G4 + 8); i += 2 * NTL) (&zs[0][0][0][0])[i] = (__bf16)0.f;
+  const int unit = 4 * w + quad;
+  const int au = 4 * w + (col >> 2);
+  const float* Ul = layerA ? UA : UB;
+  bf16x8_t ufr[KB];
+#pragma unroll
+  for (int s = 0; s < KB; ++s) {
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float val = Ul[(size_t)au * G4 + 32 * s + 8 * quad + j];
+      v[j] = (__bf16)(val * ((col & 3) == 0 ? 1.0f : 0.0f));
+    }
+    ufr[s] = v;
+  }
+  bf16x8_t wfr[TX][KB];                           // B waves: W_B rows (din) for dx_B^T
+#pragma unroll
+  for (int q = 0; q < TX; ++q) {
+    const int xb = w + NW * q;
+    const int din = 16 * xb + col;
+#pragma unroll
+    for (int s = 0; s < KB; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (__bf16)(WB[(size_t)min(din, H - 1) * G4 + 32 * s + 8 * quad + j] * ((xb < NXB && din < H) ? 1.0f : 0.0f));
+      wfr[q][s] = v;
+    }
+  }
+
+  // state rings: B at step s uses t = T-1-s, A uses t = T+1-s (clamped; invalid steps skip compute)
+  const float* gl = layerA ? gA : gB;
+  const float* cl = layerA ? cA : cB;
+  const int Tl = layerA ? T + 2 : T;              // this layer's t = Tl - 1 - s
+  float4 rg[D];
+  float rc[D];
+  auto idx = [&](int tt) { return (((size_t)tt * ntiles + tile) * NW + w) * 64 + lane; };
+#define GQ_TM2B_STATE(J, SS)                                        \
+  {                                                                 \
+    const int tt_ = min(max(Tl - 1 - (SS), 0), T - 1);              \
+    const size_t o_ = idx(tt_);                                     \
+    rg[J] = *reinterpret_cast<const float4*>(gl + o_ * 4);          \
+    rc[J] = cl[o_];                                                 \
+  }
+  constexpr int n_gd = 16 * H / 4;
+  const int gd = (tid % n_gd) * 4;
+  const float* dbase = dhout + (size_t)row0 * H + gd;
+  const size_t dstep = (size_t)Mp * H;
+  float4 rd[D];
+#define GQ_TM2B_D(J, SS)                                                                   \
+  rd[J] = *reinterpret_cast<const float4*>(dbase + (size_t)max(T - 1 - (SS), 0) * dstep);
+  const int gz_seq = tl / (G4 / 4), gz_c = (tl % (G4 / 4)) * 4;
+  float* zbase = (layerA ? dzA : dzB) + (size_t)(row0 + gz_seq) * G4 + gz_c;
+  const size_t zstep = (size_t)Mp * G4;
+
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    GQ_TM2B_STATE(j, j)
+    GQ_TM2B_D(j, j)
+  }
+  __syncthreads();
+  *reinterpret_cast<float4*>(&dd[0][0][0][0] + gd) = rd[0];
+  GQ_TM2B_D(0, D)
+  float dc = 0.f, dhr = 0.f;
+  __syncthreads();
+
+  for (int s0 = 0; s0 <= T + 1; s0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int s = s0 + j;
+      const int t = Tl - 1 - s;                    // this layer's time step
+      const int p = s & 1;
+      const int jn = (j + 1 == D) ? 0 : j + 1;
+      // ---------------- cell phase
+      {   // branch-free: invalid steps (B past t = 0, A before its first step) are masked to 0
+        const float m = (t >= 0 && t < T) ? 1.f : 0.f;
+        const float cp = rc[jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
+        const float dh = (dd[L][p][col][unit] + dhr) * m;
+        const float4 g4 = rg[j];
+        const float tc = tanhf_fast(rc[j]);
+        const float dct = (dc + dh * g4.w * (1.f - tc * tc)) * m;
+        dc = dct * g4.y;
+        zs[L][p][col][0 * H + unit] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
+        zs[L][p][col][1 * H + unit] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
+        zs[L][p][col][2 * H + unit] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
+        zs[L][p][col][3 * H + unit] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
+      }
+      GQ_TM2B_STATE(j, s + D)
+      *reinterpret_cast<float4*>(&dd[0][p ^ 1][0][0] + gd) = rd[jn];   // B's dh tile of step s+1
+      GQ_TM2B_D(jn, s + 1 + D)
+      lds_barrier();
+      // ---------------- MFMA phase: dh_{t-1} = U dz_t (both chains)
+      {
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[L][p][col][32 * k + 8 * quad]);
+          if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a1, 0, 0, 0);
+          else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a0, 0, 0, 0);
+        }
+        dhr = a0[0] + a1[0];
+      }
+      // this step's dz tile -> HBM (invalid steps write the scratch row T)
+      {
+        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[L][p][gz_seq][gz_c]);
+        const int tz = (t >= 0 && t < T) ? t : T;
+        *reinterpret_cast<float4*>(zbase + (size_t)tz * zstep) =
+            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+      }
+      // B: dx_B^T = W_B dz_B^T -> A's dh tile (read two steps later, same parity)
+      if (!layerA) {
+#pragma unroll
+        for (int q = 0; q < TX; ++q) {
+          const int xb = w + NW * q;
+          if (xb < NXB) {                          // wave-uniform
+            f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[0][p][col][32 * k + 8 * quad]);
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q][k], bz, a, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dd[1][p][col][16 * xb + 4 * quad + r] = a[r];
+          }
+        }
+      }
+    }
+  }
+#undef GQ_TM2B_STATE
+#undef GQ_TM2B_D
+}
+
+// =====================================================================================
 // host side
 static int tm_granule(int Din, const void* x) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(x);
@@ -696,6 +861,55 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB};
 }
 
+// Pair backward recurrences (lstm_tm2_bwd_kernel): dh [T, Mp, H] of B's output sequence;
+// returns [dzA, dzB] (fp32 [T+1, Mp, 4H], row T scratch) for the weight-gradient passes.
+std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB, const at::Tensor& cB,
+                                     const at::Tensor& gA, const at::Tensor& cA, const at::Tensor& WB,
+                                     const at::Tensor& UB, const at::Tensor& UA) {
+  for (const at::Tensor* t : {&dh, &gB, &cB, &gA, &cA, &WB, &UB, &UA}) check_f32_cuda(*t, "lstm_tm2_bwd operand");
+  TORCH_CHECK(dh.dim() == 3, "lstm_tm2_bwd: dh must be [T, Mp, H]");
+  const int T = (int)dh.size(0), Mp = (int)dh.size(1), H = (int)dh.size(2);
+  TORCH_CHECK(Mp % 16 == 0 && (H == 16 || H == 32), "lstm_tm2_bwd: H must be 16 or 32, Mp a multiple of 16");
+  TORCH_CHECK(UA.size(0) == H && UB.size(0) == H && WB.size(0) == H && WB.size(1) == 4 * H, "lstm_tm2_bwd: weights");
+  const long st_n = (long)(T + 1) * Mp * H;
+  TORCH_CHECK(gA.numel() == 4 * st_n && gB.numel() == 4 * st_n && cA.numel() == st_n && cB.numel() == st_n,
+              "lstm_tm2_bwd: saved state shapes");
+  c10::DeviceGuard guard(dh.device());
+  at::Tensor dzA = at::empty({T + 1, Mp, 4 * H}, dh.options()), dzB = at::empty({T + 1, Mp, 4 * H}, dh.options());
+  const int ntiles = Mp / 16;
+  GQ_TM_H_DISPATCH(H, hipLaunchKernelGGL((lstm_tm2_bwd_kernel<HH, 4>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,
+                                         stream(), dh.data_ptr<float>(), gB.data_ptr<float>(), cB.data_ptr<float>(),
+                                         gA.data_ptr<float>(), cA.data_ptr<float>(), WB.data_ptr<float>(),
+                                         UB.data_ptr<float>(), UA.data_ptr<float>(), dzB.data_ptr<float>(),
+                                         dzA.data_ptr<float>(), Mp, T));
+  GQ_LAUNCH_CHECK();
+  return {dzA, dzB};
+}
+
+// Weight gradients (+ dx) of one time-major layer from its dz (lstm_grads_rows): accumulates
+// dW, dU, db; returns dx [T, Mp, Din] if need_dx.
+at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
+                         at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx) {
+  for (const at::Tensor* t : {&dz, &x, &h, &W}) check_f32_cuda(*t, "lstm_tm_grads operand");
+  for (const at::Tensor* t : {&dW, &dU, &db}) check_f32_cuda(*t, "lstm_tm_grads gradient");
+  const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)h.size(2);
+  const int Dw = (int)W.size(0);
+  TORCH_CHECK(dz.size(0) >= T && dz.size(1) == Mp && dz.size(2) == 4 * H && h.size(0) == T && h.size(1) == Mp,
+              "lstm_tm_grads: shapes");
+  TORCH_CHECK(Dw <= Din && dW.numel() == (long)Dw * 4 * H && dU.numel() == (long)H * 4 * H && db.numel() == 4 * H,
+              "lstm_tm_grads: gradient buffer shapes");
+  c10::DeviceGuard guard(x.device());
+  const long rows = (long)T * Mp;
+  const int ncb = lstm_grads_col_blocks(H);
+  at::Tensor dx = need_dx ? (Dw < Din ? at::zeros({ncb, T, Mp, Din}, x.options()) : at::empty({ncb, T, Mp, Din}, x.options()))
+                          : at::empty({0}, x.options());
+  lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
+                  need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                  db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, stream());
+  if (!need_dx) return dx;
+  return ncb == 1 ? dx[0] : dx.sum(0);
+}
+
 // dh: [T, Mp, H] (or [Mp, H] when only the last step has a gradient). Returns dx [T, Mp, Din]
 // (empty if !need_dx) and accumulates dW, dU, db when they are non-empty.
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
@@ -761,5 +975,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_tm_fwd", &gq::lstm_tm_fwd);
   m.impl("lstm_tm2_fwd", &gq::lstm_tm2_fwd);
+  m.impl("lstm_tm2_bwd", &gq::lstm_tm2_bwd);
+  m.impl("lstm_tm_grads", &gq::lstm_tm_grads);
   m.impl("lstm_tm_bwd", &gq::lstm_tm_bwd);
 }

@@ -27,6 +27,10 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train) -> Tensor[]");
   m.def("lstm_tm2_fwd(Tensor x, Tensor WA, Tensor UA, Tensor bA, Tensor WB, Tensor UB, Tensor bB, bool train) "
         "-> Tensor[]");
+  m.def("lstm_tm2_bwd(Tensor dh, Tensor gB, Tensor cB, Tensor gA, Tensor cA, Tensor WB, Tensor UB, Tensor UA) "
+        "-> Tensor[]");
+  m.def("lstm_tm_grads(Tensor dz, Tensor x, Tensor h, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
+        "bool need_dx) -> Tensor");
   m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor(a!) dW, "
         "Tensor(b!) dU, Tensor(c!) db, bool need_dx) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)
@@ -74,4 +78,6 @@ TORCH_LIBRARY(gnnqc, m) {
   // window gather (gather.hip)
   m.def("window_gather(Tensor series, Tensor shift, Tensor scale, Tensor win_group, Tensor win_center, "
         "Tensor win_valid, Tensor wids, int tb, int seq_len, bool time_norm) -> Tensor");
+  m.def("batch_meta(Tensor wids, Tensor win_group, Tensor win_valid, Tensor group_adj, Tensor group_anom_pos, "
+        "Tensor win_label, Tensor win_label_valid, Tensor valid_sample, Tensor x) -> Tensor[]");
 }

@@ -183,25 +183,33 @@ class DeviceStore:
         """
         dev = self.device
         wids = wids.to(dev)
+        from ..ops import use_hip
+        if use_hip(self.series) and self.series.dtype == torch.float32 and self.group_adj.dtype == torch.float32:
+            # two launches: the normalised window cut + everything else (masks, adjacency, labels, anom)
+            from ..utils.native import hip_ops
+            ops = hip_ops()
+            wl = wids.long().contiguous()
+            x = ops.window_gather(self.series, self.shift, self.scale, self.win_group, self.win_center,
+                                  self.win_valid_u8, wl, self.tb, self.seq_len, self.time_varying_norm)
+            vs = (valid_sample.to(dev, torch.float32).contiguous() if valid_sample is not None
+                  else x.new_zeros(0))
+            lv = self.win_label_valid if self.win_label_valid is not None else x.new_zeros(0)
+            vm, adj, ap, y, y_mask, anom = ops.batch_meta(wl, self.win_group, self.win_valid_u8, self.group_adj,
+                                                          self.group_anom_pos, self.win_label, lv, vs, x)
+            return Batch(x=x, adj=adj, node_mask=vm, anom=anom if self.ds_type == "cml" else None, anom_pos=ap,
+                         y=y, y_mask=y_mask, wid=wids)
         pad = wids < 0
         w = wids.clamp(min=0)
         g = self.win_group[w]
         c = self.win_center[w]
         valid = self.win_valid[w] & ~pad[:, None]                    # [B, N]
         vm = valid.to(torch.float32)
-        from ..ops import use_hip
-        if use_hip(self.series) and self.series.dtype == torch.float32:
-            from ..utils.native import hip_ops
-            x = hip_ops().window_gather(self.series, self.shift, self.scale, self.win_group, self.win_center,
-                                        self.win_valid_u8, wids.long().contiguous(), self.tb, self.seq_len,
-                                        self.time_varying_norm)
-        else:
-            t = c[:, None] + self.t_offsets[None, :]                 # [B, T]
-            x = self.series[g[:, None], t].float()                   # [B, T, N, C]
-            tc = c if self.time_varying_norm else torch.zeros_like(c)
-            sh = self.shift[g, tc]                                   # [B, N, C]
-            sc = self.scale[g, tc]
-            x = (x - sh[:, None]) * sc[:, None] * vm[:, None, :, None]
+        t = c[:, None] + self.t_offsets[None, :]                     # [B, T]
+        x = self.series[g[:, None], t].float()                       # [B, T, N, C]
+        tc = c if self.time_varying_norm else torch.zeros_like(c)
+        sh = self.shift[g, tc]                                       # [B, N, C]
+        sc = self.scale[g, tc]
+        x = (x - sh[:, None]) * sc[:, None] * vm[:, None, :, None]
         adj = self.group_adj[g] * vm[:, :, None] * vm[:, None, :]
         ap = self.group_anom_pos[g]
         sample_ok = (~pad).to(x.dtype)

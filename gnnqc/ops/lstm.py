@@ -197,17 +197,36 @@ class _HipLSTMTMPair(torch.autograd.Function):
             return [(e, True)] * 3
 
         sB = sinks(ctx.params[3:], need[4:7])
-        dhA = ops.lstm_tm_bwd(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
-                              sB[0][0], sB[1][0], sB[2][0], True)
         sA = sinks(ctx.params[:3], need[1:4])
         need_dx = bool(need[0])
         dx = None
-        if need_dx or any(need[1:4]):
-            dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0], sA[2][0],
-                                 need_dx)
+        if any(need[1:7]) and _pair_bwd():
+            # training: both reverse recurrences in one pipelined kernel (B's dx stays in LDS),
+            # then one weight-gradient pass per layer (+ dx of A)
+            dzA, dzB = ops.lstm_tm2_bwd(dout.contiguous(), gB, cB, gA, cA, WB.contiguous(), UB.contiguous(),
+                                        UA.contiguous())
+            ops.lstm_tm_grads(dzB, hA, hB, WB.contiguous(), sB[0][0], sB[1][0], sB[2][0], False)
+            dx = ops.lstm_tm_grads(dzA, x, hA, WA.contiguous(), sA[0][0], sA[1][0], sA[2][0], need_dx)
+        else:
+            dhA = ops.lstm_tm_bwd(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
+                                  sB[0][0], sB[1][0], sB[2][0], True)
+            if need_dx or any(need[1:4]):
+                dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0],
+                                     sA[2][0], need_dx)
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
         return (dx if need_dx else None, *gA_, *gB_)
+
+
+def _pair_bwd() -> bool:
+    """Pipelined pair backward (``lstm_tm2_bwd``), opt-in with ``GNNQC_PAIR_BWD=1``.
+
+    Measured slower than two per-layer kernels on MI355X (CML 148 vs 118 us for the H=16
+    pair, 103 vs 62 us for H=32; SoilNet likewise): B's in-loop dx MFMAs and the second
+    layer's waves sharing each SIMD's MFMA pipe lengthen every step more than the fusion
+    saves, unlike the forward pair where both layers' per-step work is symmetric."""
+    import os
+    return os.environ.get("GNNQC_PAIR_BWD", "0") == "1"
 
 
 def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:

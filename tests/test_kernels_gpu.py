@@ -540,9 +540,11 @@ def test_soilnet_gcn_fused_path_matches_eager(cuda_device, monkeypatch):
 
 @pytest.mark.parametrize("H,Din", [(16, 20), (16, 16), (32, 16), (32, 32)])
 @pytest.mark.parametrize("wgrad", [True, False])
-def test_lstm_pair_fused_forward_matches_two_layers(cuda_device, H, Din, wgrad):
-    """lstm_tm2_fwd (layer pair, one pipelined kernel) == two lstm_tm_fwd layers, incl. gradients."""
+@pytest.mark.parametrize("pair_bwd", [True, False])
+def test_lstm_pair_fused_forward_matches_two_layers(cuda_device, monkeypatch, H, Din, wgrad, pair_bwd):
+    """lstm_tm2_fwd / lstm_tm2_bwd (layer pair, pipelined kernels) == two single layers, incl. gradients."""
     from gnnqc.ops.lstm import _HipLSTMTMPair, lstm_layer_tm
+    monkeypatch.setenv("GNNQC_PAIR_BWD", "1" if pair_bwd else "0")
     dev = cuda_device
     gen = torch.Generator().manual_seed(H * 7 + Din)
     T, M = 23, 40
@@ -589,3 +591,36 @@ def test_timelayer_pair_fusion_matches_unfused(cuda_device, monkeypatch):
     torch.testing.assert_close(o1, o0, atol=2e-3, rtol=1e-2)
     for a, b_ in zip(g1, g0):
         assert (a - b_).norm().item() <= 2e-2 * (b_.norm().item() + 1e-6)
+
+
+def _soil_small_windows():
+    from gnnqc import config as C
+    from gnnqc.data.preprocessing import create_windows_dataset
+    from gnnqc.data.synthetic import make_soilnet_raw
+    pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
+    raw = make_soilnet_raw(n_boxes=6, n_time=10 * 96, seed=2)
+    pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
+    return pc, create_windows_dataset(pc, raw=raw)
+
+
+@pytest.mark.parametrize("ds", ["cml", "soilnet"])
+def test_batch_meta_matches_torch_gather(cuda_device, cml_windows, ds):
+    """Fused batch assembly (window_gather + batch_meta) == the eager gather, every field."""
+    from gnnqc.data.store import DeviceStore
+    pc, ws = cml_windows if ds == "cml" else _soil_small_windows()
+    norm = "rolling_median" if ds == "cml" else "scale_range"
+    st = DeviceStore(ws, norm, pc.graph, device=cuda_device)
+    st_cpu = DeviceStore(ws, norm, pc.graph, device="cpu")
+    n = st.n_windows
+    wids = torch.tensor([0, min(5, n - 1), -1, n // 2, n - 1])
+    vs = torch.tensor([1.0, 0.0, 1.0, 1.0, 1.0])
+    for valid_sample in (None, vs):
+        ref = st_cpu.gather(wids, valid_sample)
+        got = st.gather(wids.to(cuda_device), None if valid_sample is None else valid_sample.to(cuda_device))
+        for name in ("x", "adj", "node_mask", "anom", "anom_pos", "y", "y_mask", "wid"):
+            a, b_ = getattr(got, name), getattr(ref, name)
+            if b_ is None:
+                assert a is None, name
+                continue
+            assert a.shape == b_.shape and a.dtype == b_.dtype, (name, a.shape, b_.shape, a.dtype, b_.dtype)
+            assert torch.allclose(a.cpu().double(), b_.double(), atol=1e-5), name
