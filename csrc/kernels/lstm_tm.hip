@@ -744,7 +744,7 @@ static int tm_granule(int Din, const void* x) {
 // hidden sizes keep the seq-major kernels of lstm.hip / lstm_grads.hip. The per-step
 // x tile must fit the loader lanes and Din + 1 (bias row) must fit 128.
 static bool tm_supported(int H, int Din, int gr) {
-  if (H != 16 && H != 32) return false;
+  if (H != 16 && H != 32 && H != 64) return false;
   if (Din < 1 || Din > 127) return false;
   return 16 * Din / gr <= 16 * H;
 }
@@ -760,7 +760,7 @@ static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
 static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* W, const float* U,
                        float* dx, float* dz, int Mp, int T, int Din, int Dw, hipStream_t st) {
-  constexpr int D = 4;
+  constexpr int D = H >= 64 ? 2 : 4;        // H = 64: 16 waves x 128 VGPRs, shorter state rings
   hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh,
                      g, c, W, U, dx, dz, Mp, T, Din, Dw);
 }
@@ -769,7 +769,15 @@ static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float*
   switch (HV) {                                                    \
     case 16: { constexpr int HH = 16; __VA_ARGS__; break; }        \
     case 32: { constexpr int HH = 32; __VA_ARGS__; break; }        \
-    default: TORCH_CHECK(false, "lstm_tm: hidden size must be 16 or 32");  \
+    case 64: { constexpr int HH = 64; __VA_ARGS__; break; }        \
+    default: TORCH_CHECK(false, "lstm_tm: hidden size must be 16, 32 or 64");  \
+  }
+// layer pairs run 2 x H/4 waves in one workgroup: H <= 32
+#define GQ_TM2_H_DISPATCH(HV, ...)                                 \
+  switch (HV) {                                                    \
+    case 16: { constexpr int HH = 16; __VA_ARGS__; break; }        \
+    case 32: { constexpr int HH = 32; __VA_ARGS__; break; }        \
+    default: TORCH_CHECK(false, "lstm_tm2: hidden size must be 16 or 32");  \
   }
 #define GQ_TM_KX_DISPATCH(KXN, ...)                                \
   {                                                                \
@@ -835,7 +843,7 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   TORCH_CHECK(UB.size(0) == H && UB.size(1) == 4 * H && WB.size(0) == H && WB.size(1) == 4 * H && bB.numel() == 4 * H,
               "lstm_tm2_fwd: layer B must be H -> H with the same H");
   const int gr = tm_granule(Din, x.data_ptr());
-  TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm2_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
+  TORCH_CHECK(H <= 32 && tm_supported(H, Din, gr), "lstm_tm2_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
   c10::DeviceGuard guard(x.device());
   auto opt = x.options();
   auto mk = [&](bool state, int last) {
@@ -854,7 +862,7 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
                      x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
                      WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), P[0], \
                      P[1], hB.data_ptr<float>(), P[2], P[3], Mp, T, Din, Dw)
-  GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
+  GQ_TM2_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR); else GQ_TM2_LAUNCH(HH, false, KXX, GRR))));
 #undef GQ_TM2_LAUNCH
   GQ_LAUNCH_CHECK();
@@ -877,7 +885,7 @@ std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB,
   c10::DeviceGuard guard(dh.device());
   at::Tensor dzA = at::empty({T + 1, Mp, 4 * H}, dh.options()), dzB = at::empty({T + 1, Mp, 4 * H}, dh.options());
   const int ntiles = Mp / 16;
-  GQ_TM_H_DISPATCH(H, hipLaunchKernelGGL((lstm_tm2_bwd_kernel<HH, 4>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,
+  GQ_TM2_H_DISPATCH(H, hipLaunchKernelGGL((lstm_tm2_bwd_kernel<HH, 4>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,
                                          stream(), dh.data_ptr<float>(), gB.data_ptr<float>(), cB.data_ptr<float>(),
                                          gA.data_ptr<float>(), cA.data_ptr<float>(), WB.data_ptr<float>(),
                                          UB.data_ptr<float>(), UA.data_ptr<float>(), dzB.data_ptr<float>(),

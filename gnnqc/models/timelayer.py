@@ -113,7 +113,7 @@ class TimeLayer(nn.Module):
                 continue
             nxt = seq[i] if i < len(seq) else None
             if (tm and isinstance(nxt, LSTM) and mod.return_sequences and nxt.return_sequences
-                    and nxt.units == mod.units and nxt.kernel.shape[0] == mod.units and _pair_fusion()
+                    and mod.units <= 32 and nxt.units == mod.units and nxt.kernel.shape[0] == mod.units and _pair_fusion()
                     and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16)
                     and nxt.activation == mod.activation and nxt.compute_bf16 == mod.compute_bf16):
                 h = lstm_pair_tm(h, mod, nxt)            # two layers, one pipelined forward kernel

@@ -79,7 +79,8 @@ class _HipLSTM(torch.autograd.Function):
         ops = hip_ops()
         # rows may be padded (e.g. a channel-padded producer): only unit inner stride needed
         if not (x.stride(2) == 1 and x.stride(0) == x.shape[1] * x.stride(1)):
-            x = x.contiguous()
+            # (.contiguous() keeps odd strides on size-1 dims, e.g. T = 1 cut from a time-major view)
+            x = x.clone(memory_format=torch.contiguous_format)
         need = any(ctx.needs_input_grad[:4])
         h, c, g = ops.lstm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need, bf16)
         ctx.bf16 = bf16
@@ -235,9 +236,9 @@ def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:
 
 
 def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf16: bool = True) -> bool:
-    """Whether the time-major fused kernels handle this layer (GPU, bf16, tanh, H in {16, 32})."""
+    """Whether the time-major kernels handle this layer (GPU, bf16, tanh, H in {16, 32, 64})."""
     from . import use_hip
-    return (use_hip(x) and bf16 and activation == "tanh" and H in (16, 32) and 1 <= Din <= 127
+    return (use_hip(x) and bf16 and activation == "tanh" and H in (16, 32, 64) and 1 <= Din <= 127
             and (16 * Din) // (4 if Din % 4 == 0 else (2 if Din % 2 == 0 else 1)) <= 16 * H)
 
 

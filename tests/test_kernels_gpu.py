@@ -296,8 +296,8 @@ def test_gcn_pool_weights_matches_eager(cuda_device, aggregate, pooling):
     torch.testing.assert_close(got, ref, atol=1e-6, rtol=1e-5)
 
 
-@pytest.mark.parametrize("H", [16, 32])
-@pytest.mark.parametrize("Din", [18, 16, 2, 32])
+@pytest.mark.parametrize("H", [16, 32, 64])
+@pytest.mark.parametrize("Din", [18, 16, 2, 32, 64])
 @pytest.mark.parametrize("ret_seq", [True, False])
 @pytest.mark.parametrize("wgrad", [True, False])
 def test_lstm_time_major_fused_bwd_matches_eager(cuda_device, H, Din, ret_seq, wgrad):
