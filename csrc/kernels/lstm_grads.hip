@@ -353,6 +353,102 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// dx = dz W^T on its own (no LDS): for a 16-row tile and a 16-wide din tile, the MFMA B
+// operand (rows x gate-units, K-contiguous per lane) is 8 consecutive floats of one dz row
+// and the A operand (din x gate-units) 8 consecutive floats of one W row, so both come
+// straight from global memory / registers; the C tile's 4 consecutive din values per lane
+// leave as one float4. All 4H gate-units are contracted in one workgroup: no per-column-
+// block slabs and no slab sum. Used when the weight-gradient pass runs on a side stream
+// (off the critical path) while this kernel feeds the next layer's recurrence.
+template <int H, int NDT>          // NDT: 16-wide din tiles per wave
+__global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ dz, const float* __restrict__ W,
+                                                      float* __restrict__ dx, long rows, int Dw, int lddx) {
+  constexpr int G4 = 4 * H, KS = G4 / 32;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, quad = lane >> 4;
+  bf16x8_t wa[NDT][KS];
+#pragma unroll
+  for (int d = 0; d < NDT; ++d) {
+    const int din = 16 * (w + 4 * d) + col;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const float4 a = *reinterpret_cast<const float4*>(W + (size_t)min(din, Dw - 1) * G4 + 32 * ks + 8 * quad);
+      const float4 b = *reinterpret_cast<const float4*>(W + (size_t)min(din, Dw - 1) * G4 + 32 * ks + 8 * quad + 4);
+      const float m = din < Dw ? 1.f : 0.f;
+      wa[d][ks] = bf16x8_t{(__bf16)(a.x * m), (__bf16)(a.y * m), (__bf16)(a.z * m), (__bf16)(a.w * m),
+                           (__bf16)(b.x * m), (__bf16)(b.y * m), (__bf16)(b.z * m), (__bf16)(b.w * m)};
+    }
+  }
+  const long ntiles = (rows + 15) / 16;
+  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long r = t * 16 + col;
+    const long rc = min(r, rows - 1);
+    bf16x8_t bz[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const float4 a = *reinterpret_cast<const float4*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad);
+      const float4 b = *reinterpret_cast<const float4*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad + 4);
+      bz[ks] = bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                        (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+    }
+#pragma unroll
+    for (int d = 0; d < NDT; ++d) {
+      const int din0 = 16 * (w + 4 * d) + 4 * quad;
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[d][ks], bz[ks], acc, 0, 0, 0);
+      // lane holds dx[r][din0 .. din0+3]; columns Dw .. lddx-1 (layout padding) get zeros
+      if (r < rows && din0 < lddx) {
+        float* o = dx + (size_t)r * lddx + din0;
+        if (din0 + 4 <= lddx) {
+          *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        } else {
+          for (int q = 0; q < lddx - din0; ++q) o[q] = acc[q];
+        }
+      }
+    }
+  }
+}
+
+// dz: [>= rows, 4H] fp32 rows; W: [Dw, 4H]; out: [rows, lddx] (lddx >= Dw, multiple of 4).
+void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, int Dw, int lddx, hipStream_t st) {
+  if (rows == 0) return;
+  const int ndin = (lddx + 15) / 16;
+  const int ndt = (ndin + 3) / 4;
+  const long ntiles = (rows + 15) / 16;
+  const int grid = (int)std::max<long>(1, std::min<long>(ntiles, 2048));
+#define GQ_DX(HH, ND) hipLaunchKernelGGL((lstm_dx_kernel<HH, ND>), dim3(grid), dim3(256), 0, st, dz, W, dx, rows, Dw, lddx)
+#define GQ_DX_H(HH)                                                         \
+  case HH:                                                                  \
+    if (ndt == 1) GQ_DX(HH, 1); else if (ndt == 2) GQ_DX(HH, 2);           \
+    else TORCH_CHECK(false, "lstm_dx: input width ", lddx, " > 128");       \
+    break;
+  switch (H) {
+    GQ_DX_H(16) GQ_DX_H(32) GQ_DX_H(64) GQ_DX_H(128)
+    default: TORCH_CHECK(false, "lstm_dx: unsupported hidden size ", H);
+  }
+#undef GQ_DX_H
+#undef GQ_DX
+  GQ_LAUNCH_CHECK();
+}
+
+// dx = dz[:rows] W^T into a fresh [rows / lead, lead, lddx] tensor (shape taken from `like`).
+at::Tensor lstm_dx(const at::Tensor& dz, const at::Tensor& W, const at::Tensor& like) {
+  check_f32_cuda(dz, "dz");
+  check_f32_cuda(W, "W");
+  const int G4 = (int)W.size(1), H = G4 / 4, Dw = (int)W.size(0);
+  TORCH_CHECK(dz.size(-1) == G4, "lstm_dx: dz / W gate widths differ");
+  const int lddx = (int)like.size(-1);
+  TORCH_CHECK(lddx >= Dw && lddx % 4 == 0, "lstm_dx: output width must be >= W rows and a multiple of 4");
+  const long rows = like.numel() / lddx;
+  TORCH_CHECK(dz.numel() / G4 >= rows, "lstm_dx: dz has too few rows");
+  c10::DeviceGuard guard(dz.device());
+  at::Tensor dx = at::empty(like.sizes(), like.options().dtype(at::kFloat));
+  lstm_dx_rows(dz.data_ptr<float>(), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, lddx, stream());
+  return dx;
+}
+
 int lstm_grads_col_blocks(int H) { return (4 * H) / GR_CB; }
 
 // dz [M(p),T,4H] from lstm_bwd; x [M,T,Din] (unit inner stride, row stride ldx);
@@ -392,4 +488,7 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
 
 }  // namespace gq
 
-TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) { m.impl("lstm_grads", &gq::lstm_grads); }
+TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("lstm_grads", &gq::lstm_grads);
+  m.impl("lstm_dx", &gq::lstm_dx);
+}

@@ -894,6 +894,33 @@ std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB,
   return {dzA, dzB};
 }
 
+// Backward recurrence only: dz [T+1, Mp, 4H] (row T scratch) for the split backward (dx and
+// the weight-gradient pass are then launched separately, the latter on a side stream).
+at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& W,
+                          const at::Tensor& U, int64_t T) {
+  for (const at::Tensor* t : {&dh, &g, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_dz operand");
+  const int H = (int)U.size(0);
+  const bool last = dh.dim() == 2;
+  const int Mp = (int)(last ? dh.size(0) : dh.size(1));
+  TORCH_CHECK(last ? dh.size(1) == H : (dh.size(0) == T && dh.size(2) == H), "lstm_tm_bwd_dz: dh shape");
+  TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H,
+              "lstm_tm_bwd_dz: saved state shapes");
+  TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_tm_bwd_dz: hidden size");
+  c10::DeviceGuard guard(dh.device());
+  at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, dh.options());
+  const int ntiles = Mp / 16;
+  auto st = stream();
+  GQ_TM_H_DISPATCH(H,
+      if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
+            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, (int)T,
+            (int)W.size(0), (int)W.size(0), st);
+      else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
+            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, (int)T,
+            (int)W.size(0), (int)W.size(0), st));
+  GQ_LAUNCH_CHECK();
+  return dz;
+}
+
 // Weight gradients (+ dx) of one time-major layer from its dz (lstm_grads_rows): accumulates
 // dW, dU, db; returns dx [T, Mp, Din] if need_dx.
 at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
@@ -985,5 +1012,6 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_tm2_fwd", &gq::lstm_tm2_fwd);
   m.impl("lstm_tm2_bwd", &gq::lstm_tm2_bwd);
   m.impl("lstm_tm_grads", &gq::lstm_tm_grads);
+  m.impl("lstm_tm_bwd_dz", &gq::lstm_tm_bwd_dz);
   m.impl("lstm_tm_bwd", &gq::lstm_tm_bwd);
 }

@@ -31,6 +31,8 @@ TORCH_LIBRARY(gnnqc, m) {
         "-> Tensor[]");
   m.def("lstm_tm_grads(Tensor dz, Tensor x, Tensor h, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
         "bool need_dx) -> Tensor");
+  m.def("lstm_tm_bwd_dz(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T) -> Tensor");
+  m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
   m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor(a!) dW, "
         "Tensor(b!) dU, Tensor(c!) db, bool need_dx) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)

@@ -46,13 +46,68 @@ def lstm_eager(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
 
 
 class _DirectGrad:
-    """When enabled (by the training engine), LSTM weight gradients are atomically
-    accumulated by the ``lstm_grads`` kernel straight into ``param.grad`` (the
-    optimiser's flat gradient buffer views) instead of being returned to autograd
-    - no separate AccumulateGrad add per parameter. Off by default so that
-    ``torch.autograd.grad`` (e.g. integrated gradients) never touches ``.grad``."""
+    """When enabled (by the training engine), LSTM weight gradients are accumulated by the
+    ``lstm_grads`` kernels straight into ``param.grad`` (the optimiser's flat gradient
+    buffer views) instead of being returned to autograd - no separate AccumulateGrad add
+    per parameter. Off by default so that ``torch.autograd.grad`` (e.g. integrated
+    gradients) never touches ``.grad``.
+
+    In this mode the weight-gradient passes can also leave the critical path: each layer's
+    backward recurrence is followed by a small dx kernel on the current stream (what the
+    next layer's recurrence waits for), while dW/dU/db run on a side stream that the
+    current stream re-joins when the context exits (HIP-graph capture turns this into
+    parallel graph branches). Opt-in, see :func:`_split_mode`."""
 
     enabled = False
+    streams = {}          # device index -> side stream
+    pending = set()       # devices with side-stream work not yet joined
+    keep = []             # tensors the side stream reads: held until the join (allocator safety)
+
+
+def _split_mode() -> str:
+    """Backward of a direct-accumulation LSTM layer: ``fused`` (default: one weight-gradient
+    kernel also producing dx), ``split`` (dx kernel + weight-gradient kernel, one stream) or
+    ``side`` (weight gradients on a side stream). Env ``GNNQC_LSTM_BWD``.
+
+    Measured on MI355X (CML bench, ms/step, HIP graph / eager): fused 0.757 / 1.238,
+    side 0.885 / 2.037 - cross-stream event waits cost more than the overlap wins here."""
+    import os
+    return os.environ.get("GNNQC_LSTM_BWD", "fused")
+
+
+def _side_stream(device: torch.device):
+    if _split_mode() != "side" or device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _DirectGrad.streams.get(idx)
+    if st is None:
+        st = torch.cuda.Stream(device=idx)
+        _DirectGrad.streams[idx] = st
+    return st
+
+
+def join_side_streams():
+    """Make the current stream wait for all pending weight-gradient side-stream work."""
+    for idx in list(_DirectGrad.pending):
+        torch.cuda.current_stream(idx).wait_stream(_DirectGrad.streams[idx])
+    _DirectGrad.pending.clear()
+    # freed only now: later reuse of their memory on the current stream is ordered after the
+    # side-stream kernels (no record_stream, which does not mix with graph capture)
+    _DirectGrad.keep.clear()
+
+
+def _off_critical_path(device: torch.device, tensors, fn):
+    """Run ``fn()`` (weight-gradient kernels) on the side stream after the current stream's
+    work so far; ``tensors`` stay referenced until :func:`join_side_streams`."""
+    st = _side_stream(device) if _DirectGrad.enabled else None
+    if st is None:
+        fn()
+        return
+    st.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(st):
+        fn()
+    _DirectGrad.keep.extend(tensors)
+    _DirectGrad.pending.add(device.index if device.index is not None else torch.cuda.current_device())
 
 
 @contextlib.contextmanager
@@ -63,6 +118,8 @@ def direct_grad_accumulation(flag: bool = True):
         yield
     finally:
         _DirectGrad.enabled = prev
+        if _DirectGrad.pending and torch.cuda.is_available():
+            join_side_streams()
 
 
 def _grad_sink(p: torch.Tensor):
@@ -122,12 +179,32 @@ class _HipLSTM(torch.autograd.Function):
         gU, dU_in = _grad_sink(Up)
         gb, db_in = _grad_sink(bp)
         need_dx = bool(ctx.needs_input_grad[0])
-        dx = ops.lstm_grads(dz, x, h, W.contiguous(), gW, gU, gb, need_dx)
+        Wc = W.contiguous()
+        if dW_in and dU_in and db_in and _split_mode() != "fused" and x.shape[-1] % 4 == 0:
+            # critical path: dx only; dW/dU/db on the side stream
+            dx = ops.lstm_dx(dz, Wc, x) if need_dx else None
+            _off_critical_path(dz.device, (dz, x, h, Wc),
+                               lambda: ops.lstm_grads(dz, x, h, Wc, gW, gU, gb, False))
+            return dx, None, None, None, None, None
+        dx = ops.lstm_grads(dz, x, h, Wc, gW, gU, gb, need_dx)
         return (dx if need_dx else None,
                 None if dW_in or not ctx.needs_input_grad[1] else gW,
                 None if dU_in or not ctx.needs_input_grad[2] else gU,
                 None if db_in or not ctx.needs_input_grad[3] else gb,
                 None, None)
+
+
+def _tm_split_backward(dh, g, c, x, h, W, U, sinks, need_dx):
+    """Time-major layer backward in direct-accumulation mode: recurrence -> dz, dx = dz W^T
+    on the current stream; the weight-gradient pass on the side stream."""
+    from ..utils.native import hip_ops
+    ops = hip_ops()
+    T = x.shape[0]
+    dz = ops.lstm_tm_bwd_dz(dh, g, c, W, U, T)
+    dx = ops.lstm_dx(dz, W, x) if need_dx else None
+    _off_critical_path(x.device, (dz, x, h, W),
+                       lambda: ops.lstm_tm_grads(dz, x, h, W, sinks[0][0], sinks[1][0], sinks[2][0], False))
+    return dx
 
 
 class _HipLSTMTM(torch.autograd.Function):
@@ -161,8 +238,11 @@ class _HipLSTMTM(torch.autograd.Function):
         else:
             e = x.new_zeros(0)
             sinks = [(e, True)] * 3
-        dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
-                                   sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
+        if wgrad and all(d for _, d in sinks) and _split_mode() != "fused":
+            dx = _tm_split_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
+        else:
+            dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
+                                       sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
         grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
         return (dx if need_dx else None, *grads, None)
 
@@ -208,6 +288,10 @@ class _HipLSTMTMPair(torch.autograd.Function):
                                         UA.contiguous())
             ops.lstm_tm_grads(dzB, hA, hB, WB.contiguous(), sB[0][0], sB[1][0], sB[2][0], False)
             dx = ops.lstm_tm_grads(dzA, x, hA, WA.contiguous(), sA[0][0], sA[1][0], sA[2][0], need_dx)
+        elif (any(need[4:7]) and all(d for _, d in sB) and any(need[1:4]) and all(d for _, d in sA)
+              and _split_mode() != "fused"):
+            dhA = _tm_split_backward(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
+            dx = _tm_split_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
             dhA = ops.lstm_tm_bwd(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
                                   sB[0][0], sB[1][0], sB[2][0], True)
@@ -257,4 +341,5 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     return lstm_eager(x, W, U, b, return_sequences, activation)
 
 
-__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "tm_eligible"]
+__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "tm_eligible", "direct_grad_accumulation",
+           "join_side_streams"]

@@ -624,3 +624,35 @@ def test_batch_meta_matches_torch_gather(cuda_device, cml_windows, ds):
                 continue
             assert a.shape == b_.shape and a.dtype == b_.dtype, (name, a.shape, b_.shape, a.dtype, b_.dtype)
             assert torch.allclose(a.cpu().double(), b_.double(), atol=1e-5), name
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+@pytest.mark.parametrize("mode", ["side", "split"])
+def test_split_lstm_backward_matches_fused(cuda_device, cml_windows, monkeypatch, use_graph, mode):
+    """Training steps with the weight-gradient passes on a side stream (graph branches when
+    captured) == the same steps with everything on one stream."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceLoader, DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    pc, ws = cml_windows
+    mc = C.default("model_cml")
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+
+    def run(side):
+        monkeypatch.setenv("GNNQC_LSTM_BWD", mode if side else "fused")
+        torch.manual_seed(0)
+        model = GCNClassifier(mc, pc).to(cuda_device)
+        opt = make_optimizer("adam", model.parameters(), 1e-3)
+        tr = Trainer(model, st, opt, {0: 1.0, 1: 5.0}, use_graph=use_graph, batch_size=64)
+        loader = DeviceLoader(st, list(range(st.n_windows)), 64, shuffle=True)
+        for row in list(loader.batch_ids())[:6]:
+            tr.train_step(row)
+        torch.cuda.synchronize()
+        return torch.cat([p.detach().reshape(-1) for p in model.parameters()]), float(tr.last_loss.item())
+
+    p1, l1 = run(True)
+    p0, l0 = run(False)
+    assert abs(l1 - l0) < 2e-2 * abs(l0) + 1e-4, (l1, l0)
+    assert (p1 - p0).norm().item() < 2e-3 * p0.norm().item()
