@@ -170,17 +170,20 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
       f32x4_t acc[CPL];
 #pragma unroll
       for (int cc = 0; cc < CPL; ++cc) {
-        acc[cc] = bias4[cc];
+        // x and h parts in independent accumulators: their MFMA chains overlap instead of
+        // the h part waiting for the x part's result
+        f32x4_t accx = bias4[cc], acch = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KX; ++s) {
           const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
-          acc[cc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, acc[cc], 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, accx, 0, 0, 0);
         }
 #pragma unroll
         for (int s = 0; s < C::KSH; ++s) {
           const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
-          acc[cc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acc[cc], 0, 0, 0);
+          acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acch, 0, 0, 0);
         }
+        acc[cc] = accx + acch;
       }
       // stage x_{t+1}, refill the slot with x_{t+1+D}
 #pragma unroll
@@ -312,25 +315,26 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
         const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][0][0] + gh);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
       }
-      f32x4_t acc = bias4;
+      f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};   // independent MFMA chains
       if (layerB) {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
           const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&hs[0][p][col][32 * k + 8 * quad]);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, acc, 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, accx, 0, 0, 0);
         }
       } else {
 #pragma unroll
         for (int k = 0; k < KX; ++k) {
           const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * k + 8 * quad]);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, acc, 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k], bx, accx, 0, 0, 0);
         }
       }
 #pragma unroll
       for (int k = 0; k < KS; ++k) {
         const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[L][p][col][32 * k + 8 * quad]);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bh, acc, 0, 0, 0);
+        acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bh, acch, 0, 0, 0);
       }
+      const f32x4_t acc = accx + acch;
       // stage x_{s+1}, refill the slot with x_{s+1+D}
 #pragma unroll
       for (int q = 0; q < GR; ++q) xs[p ^ 1][gx_seq][gx_k + q] = (__bf16)xr[jn].v[q];
@@ -475,10 +479,14 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   // stage step 0 (t = T-1) tiles
   *reinterpret_cast<float4*>(&dhs[0][0][0] + gd) = rd[0];
   GQ_TMB_LOAD_D(0, D)
-  float dc[CPL], dhr[CPL];
+  float dc[CPL], dhr[CPL], dhn[CPL];
 #pragma unroll
   for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
   __syncthreads();
+  // dh_out of the step to come, read from LDS one step early (right after the barrier that
+  // published it) so the cell phase does not wait on an LDS round trip
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) dhn[cc] = dhs[0][col][unit[cc]];
 
   for (int s0 = 0; s0 < T; s0 += D) {
 #pragma unroll
@@ -492,7 +500,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
       for (int cc = 0; cc < CPL; ++cc) {
         const int u = unit[cc];
         const float cp = rc[cc][jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
-        const float dh = dhs[p][col][u] + dhr[cc];
+        const float dh = dhn[cc] + dhr[cc];
         const float4 g4 = rg[cc][j];
         const float tc = tanhf_fast(rc[cc][j]);
         const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
@@ -506,6 +514,8 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
       *reinterpret_cast<float4*>(&dhs[p ^ 1][0][0] + gd) = rd[jn];   // dh tile of step s+1
       GQ_TMB_LOAD_D(jn, s + 1 + D)
       lds_barrier();
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) dhn[cc] = dhs[p ^ 1][col][unit[cc]];   // next step's dh_out
       // ---------------- MFMA phase
       // (a) serial chain: dh_{t-1} = U dz_t
 #pragma unroll
