@@ -64,39 +64,101 @@ __global__ void gcn_stats_kernel(const float* __restrict__ x, const float* __res
 }
 
 // ------------------------------------------------------------------ forward
-// thread = (row=(b,t), f); loops over the N nodes of its sample.
-template <int Cin>
-__global__ void gcn_pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                    const float* __restrict__ anom, const float* __restrict__ W,
-                                    const float* __restrict__ bias, const float* __restrict__ scale,
-                                    const float* __restrict__ shift, const float* __restrict__ alpha,
-                                    float* __restrict__ out, int B, int T, int N, int F, int Ca) {
-  const int Fo = Ca + F;
-  const long total = (long)B * T * Fo;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int f = i % Fo;
-    const long row = i / Fo;          // b*T + t
-    const int b = row / T;
-    if (f < Ca) {
-      out[i] = anom[row * Ca + f];
-      continue;
+// thread = one (b,t) row, all F channels in registers. A workgroup's 256 rows are ONE
+// contiguous span of x ([B,T,N,Cin] with (b,t) consecutive), staged through LDS with
+// coalesced float4 loads when it fits (N*Cin <= GCN_STAGE_MAX); each thread then walks its
+// row's N nodes once (the old channel-per-thread layout re-read every row F times).
+// Channel parameters live in LDS (wave-uniform broadcast reads).
+constexpr int GCN_STAGE_MAX = 48;           // floats per row staged in LDS (48 KiB / 256 rows)
+
+template <int Cin, int F>
+__device__ __forceinline__ void gcn_load_params(const float* W, const float* bias, const float* scale,
+                                                const float* shift, const float* alpha, float* sp) {
+  // sp: [Cin+4][F] = W rows, bias, scale, shift, alpha
+  for (int i = threadIdx.x; i < (Cin + 4) * F; i += blockDim.x) {
+    const int r = i / F, f = i % F;
+    float v;
+    if (r < Cin) v = W[r * F + f];
+    else if (r == Cin) v = bias[f];
+    else if (r == Cin + 1) v = scale[f];
+    else if (r == Cin + 2) v = shift[f];
+    else v = alpha[f];
+    sp[i] = v;
+  }
+}
+
+// stage rows [row0, row0 + nrow) of a [rows, L] fp32 array into LDS (zero past `rows`)
+__device__ __forceinline__ void gcn_stage_rows(const float* __restrict__ src, float* dst, long row0, int nrow,
+                                               long rows, int L) {
+  const long beg = row0 * L;
+  const long end = min(rows, row0 + nrow) * (long)L;
+  const int n = nrow * L;
+  if ((beg & 3) == 0 && (L & 3) == 0) {
+    for (int i = threadIdx.x * 4; i < n; i += blockDim.x * 4) {
+      float4 v = beg + i < end ? *reinterpret_cast<const float4*>(src + beg + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(dst + i) = v;
     }
-    const int ff = f - Ca;
-    float wk[Cin];
-    _Pragma("unroll") for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + ff];
-    const float bb = bias[ff], sc = scale[ff], sh = shift[ff], al = alpha[ff];
-    const float* xr = x + row * (long)N * Cin;
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = beg + i < end ? src[beg + i] : 0.f;
+  }
+}
+
+// 4 threads per row (adjacent lanes), each owning F/4 channels whose parameters sit in VGPRs.
+template <int Cin, int F>
+__global__ __launch_bounds__(256) void gcn_pool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ anom, const float* __restrict__ W,
+                                                           const float* __restrict__ bias, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, const float* __restrict__ alpha,
+                                                           float* __restrict__ out, int B, int T, int N, int Ca) {
+  constexpr int FQ = F / 4, RPB = 64;             // channels per thread, rows per workgroup
+  extern __shared__ __attribute__((aligned(16))) float sx[];   // RPB * N * Cin (if staged)
+  const int L = N * Cin;
+  const bool staged = L <= GCN_STAGE_MAX;
+  const int Fo = Ca + F;
+  const long rows = (long)B * T;
+  const int r = threadIdx.x >> 2, q = threadIdx.x & 3, f0 = q * FQ;
+  float pw[Cin][FQ], pb[FQ], psc[FQ], psh[FQ], pal[FQ];
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) pw[k][j] = W[k * F + f0 + j];
+    pb[j] = bias[f0 + j];
+    psc[j] = scale[f0 + j];
+    psh[j] = shift[f0 + j];
+    pal[j] = alpha[f0 + j];
+  }
+  for (long row0 = (long)blockIdx.x * RPB; row0 < rows; row0 += (long)gridDim.x * RPB) {
+    if (staged) {
+      __syncthreads();
+      gcn_stage_rows(x, sx, row0, RPB, rows, L);
+      __syncthreads();
+    }
+    const long row = row0 + r;
+    if (row >= rows) continue;
+    const int b = (int)(row / T);
+    const float* xr = staged ? sx + r * L : x + row * (long)L;
     const float* wr = w + (long)b * N;
-    float acc = 0.f;
+    float acc[FQ];
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) acc[j] = 0.f;
     for (int n = 0; n < N; ++n) {
       const float wn = wr[n];
-      if (wn == 0.f) continue;
-      float z = bb;
-      _Pragma("unroll") for (int k = 0; k < Cin; ++k) z += xr[n * Cin + k] * wk[k];
-      const float y = z * sc + sh;
-      acc += wn * (y > 0.f ? y : al * y);
+      float xv[Cin];
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) {
+        float z = pb[j];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) z += xv[k] * pw[k][j];
+        const float y = z * psc[j] + psh[j];
+        acc[j] += wn * (y > 0.f ? y : pal[j] * y);
+      }
     }
-    out[i] = acc;
+    float* o = out + row * Fo;
+    for (int c = q; c < Ca; c += 4) o[c] = anom[row * Ca + c];
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) o[Ca + f0 + j] = acc[j];
   }
 }
 
@@ -158,39 +220,71 @@ __global__ void gcn_pool_bwd_kernel(const float* __restrict__ x, const float* __
 }
 
 // ------------------------------------------------------------------ backward (input)
-// thread = node row (b,t,n): dz_f = c1_f*dy_f + c0_f + c2_f*z_f (valid rows), dx_k = sum_f W[k,f] dz_f
-template <int Cin>
-__global__ void gcn_pool_bwd_input_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                          const float* __restrict__ mask, const float* __restrict__ dout,
-                                          const float* __restrict__ W, const float* __restrict__ bias,
-                                          const float* __restrict__ scale, const float* __restrict__ shift,
-                                          const float* __restrict__ alpha, const float* __restrict__ coef,
-                                          float* __restrict__ dx, int B, int T, int N, int F, int c_off,
-                                          int dstride) {
-  const long rows = (long)B * T * N;
-  for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < rows; r += (long)gridDim.x * blockDim.x) {
-    const int n = r % N;
-    const long bt = r / N;
-    const int b = bt / T;
-    float xv[Cin], dxv[Cin];
-    _Pragma("unroll") for (int k = 0; k < Cin; ++k) {
-      xv[k] = x[r * Cin + k];
-      dxv[k] = 0.f;
-    }
-    const float m = mask[b * N + n];
-    if (m != 0.f) {
+// thread = one (b,t) row: its F upstream gradients are read once, then per node n
+// dz_f = c1_f*dy_f + c0_f + c2_f*z_f (valid nodes), dx_k = sum_f W[k,f] dz_f.
+// 4 adjacent lanes per row, F/4 channels each; dx_k reduced over the 4 lanes by shuffles.
+template <int Cin, int F>
+__global__ __launch_bounds__(256) void gcn_pool_bwd_input_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                                 const float* __restrict__ mask, const float* __restrict__ dout,
+                                                                 const float* __restrict__ W, const float* __restrict__ bias,
+                                                                 const float* __restrict__ scale, const float* __restrict__ shift,
+                                                                 const float* __restrict__ alpha, const float* __restrict__ coef,
+                                                                 float* __restrict__ dx, int B, int T, int N, int c_off,
+                                                                 int dstride) {
+  constexpr int FQ = F / 4;
+  const int q = threadIdx.x & 3, f0 = q * FQ;
+  float pw[Cin][FQ], pb[FQ], psc[FQ], psh[FQ], pal[FQ], c0[FQ], c1[FQ], c2[FQ];
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) pw[k][j] = W[k * F + f0 + j];
+    pb[j] = bias[f0 + j];
+    psc[j] = scale[f0 + j];
+    psh[j] = shift[f0 + j];
+    pal[j] = alpha[f0 + j];
+    c0[j] = coef[f0 + j];
+    c1[j] = coef[F + f0 + j];
+    c2[j] = coef[2 * F + f0 + j];
+  }
+  const long rows = (long)B * T;
+  const long nthr = (long)gridDim.x * blockDim.x / 4;
+  for (long row = (blockIdx.x * (long)blockDim.x + threadIdx.x) / 4; row < rows + 0; row += nthr) {
+    // (all 4 lanes of a row take the same trip count: the shuffles below stay converged)
+    const int b = (int)(row / T);
+    float g[FQ];
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) g[j] = dout[row * dstride + c_off + f0 + j];
+    const float* xr = x + row * (long)N * Cin;
+    float* dxr = dx + row * (long)N * Cin;
+    for (int n = 0; n < N; ++n) {
+      float xv[Cin], dxv[Cin];
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) {
+        xv[k] = xr[n * Cin + k];
+        dxv[k] = 0.f;
+      }
+      const float m = mask[b * N + n] != 0.f ? 1.f : 0.f;
       const float wn = w[b * N + n];
-      for (int f = 0; f < F; ++f) {
-        float z = bias[f];
-        _Pragma("unroll") for (int k = 0; k < Cin; ++k) z += xv[k] * W[k * F + f];
-        const float y = z * scale[f] + shift[f];
-        const float da = wn * dout[bt * dstride + c_off + f];
-        const float dy = y > 0.f ? da : alpha[f] * da;
-        const float dz = coef[F + f] * dy + coef[f] + coef[2 * F + f] * z;
-        _Pragma("unroll") for (int k = 0; k < Cin; ++k) dxv[k] += W[k * F + f] * dz;
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) {
+        float z = pb[j];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) z += xv[k] * pw[k][j];
+        const float y = z * psc[j] + psh[j];
+        const float da = wn * g[j];
+        const float dy = y > 0.f ? da : pal[j] * da;
+        const float dz = m * (c1[j] * dy + c0[j] + c2[j] * z);
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) dxv[k] += pw[k][j] * dz;
+      }
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) {
+        float v = dxv[k];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        if (q == (k & 3)) dxr[n * Cin + k] = v;
       }
     }
-    _Pragma("unroll") for (int k = 0; k < Cin; ++k) dx[r * Cin + k] = dxv[k];
   }
 }
 
@@ -229,6 +323,14 @@ at::Tensor gcn_stats(const at::Tensor& x, const at::Tensor& mask) {
   return out;
 }
 
+#define GQ_GCN_F_DISPATCH(F_RT, ...)                                   \
+  switch (F_RT) {                                                      \
+    case 8: { constexpr int FF = 8; __VA_ARGS__; } break;              \
+    case 16: { constexpr int FF = 16; __VA_ARGS__; } break;            \
+    case 32: { constexpr int FF = 32; __VA_ARGS__; } break;            \
+    default: TORCH_CHECK(false, "gcn: 8, 16 or 32 output channels");  \
+  }
+
 at::Tensor gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& anom, const at::Tensor& W,
                         const at::Tensor& b, const at::Tensor& scale, const at::Tensor& shift,
                         const at::Tensor& alpha) {
@@ -244,12 +346,15 @@ at::Tensor gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
   }
   c10::DeviceGuard guard(x.device());
   at::Tensor out = at::empty({B, T, Ca + F}, x.options());
-  const long total = (long)B * T * (Ca + F);
+  const long rows = (long)B * T;
   const float* anom_p = Ca ? anom.data_ptr<float>() : nullptr;
-  GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_pool_fwd_kernel<CIN>, dim3(grid_for(total, 256, 4096)), dim3(256), 0,
-                     stream(), x.data_ptr<float>(), w.data_ptr<float>(), anom_p,
-                     W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                     alpha.data_ptr<float>(), out.data_ptr<float>(), B, T, N, F, Ca));
+  const bool staged = N * Cin <= GCN_STAGE_MAX;
+  const size_t smem = staged ? (size_t)64 * N * Cin * sizeof(float) : 0;
+  GQ_CIN_DISPATCH(Cin, GQ_GCN_F_DISPATCH(F,
+      hipLaunchKernelGGL((gcn_pool_fwd_kernel<CIN, FF>), dim3(grid_for(rows, 64, 8192)), dim3(256), smem, stream(),
+                         x.data_ptr<float>(), w.data_ptr<float>(), anom_p, W.data_ptr<float>(), b.data_ptr<float>(),
+                         scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
+                         out.data_ptr<float>(), B, T, N, Ca)));
   GQ_LAUNCH_CHECK();
   return out;
 }
@@ -283,12 +388,13 @@ at::Tensor gcn_pool_bwd_input(const at::Tensor& x, const at::Tensor& w, const at
   TORCH_CHECK(coef.numel() == 3 * F, "coef must be [3,F]");
   c10::DeviceGuard guard(x.device());
   at::Tensor dx = at::empty_like(x);
-  const long rows = (long)B * T * N;
-  GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_pool_bwd_input_kernel<CIN>, dim3(grid_for(rows, 256, 4096)), dim3(256), 0, stream(),
-                     x.data_ptr<float>(), w.data_ptr<float>(), mask.data_ptr<float>(), dout.data_ptr<float>(),
-                     W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                     alpha.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr<float>(), B, T, N, F,
-                     (int)c_off, (int)dout.size(2)));
+  const long rows = (long)B * T;
+  GQ_CIN_DISPATCH(Cin, GQ_GCN_F_DISPATCH(F,
+      hipLaunchKernelGGL((gcn_pool_bwd_input_kernel<CIN, FF>), dim3(grid_for(rows, 64, 8192)), dim3(256), 0, stream(),
+                         x.data_ptr<float>(), w.data_ptr<float>(), mask.data_ptr<float>(), dout.data_ptr<float>(),
+                         W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                         alpha.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr<float>(), B, T, N,
+                         (int)c_off, (int)dout.size(2))));
   GQ_LAUNCH_CHECK();
   return dx;
 }
