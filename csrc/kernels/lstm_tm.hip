@@ -51,6 +51,9 @@ struct TMC {
   static constexpr int KPH = ((H + 31) / 32) * 32;
   static constexpr int KSH = KPH / 32;              // K = H steps (forward recurrent part)
   static constexpr int KB = G4 / 32;                // K = 4H steps (backward)
+  static constexpr int HP = H + 4;                  // row pitch of fp32 [16][H] LDS tiles: the
+                                                    // per-cell accesses (16 rows x 4 units per
+                                                    // wave) then hit 64 distinct banks
 };
 
 // ---- tile streamer: granules of GR floats of one contiguous tile, wave-uniform loaders
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
   constexpr int KPX = 32 * KX;
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][16][C::KPH + 8];
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
-  __shared__ __attribute__((aligned(16))) float hf[2][16][H];
+  __shared__ __attribute__((aligned(16))) float hf[2][16][C::HP];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in an SGPR
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
       const int jn = (j + 1 == D) ? 0 : j + 1;
       {                                             // h_{t-1}: one contiguous tile
         const int ts = (t >= 1 && t <= T) ? t - 1 : T;
-        const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][0][0] + gh);
+        const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
       }
       f32x4_t acc[CPL];
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
   // [layer][parity]: indexed (not pointer-selected) so every access stays a DS instruction
   __shared__ __attribute__((aligned(16))) __bf16 hs[2][2][16][C::KPH + 8];
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
-  __shared__ __attribute__((aligned(16))) float hf[2][2][16][H];
+  __shared__ __attribute__((aligned(16))) float hf[2][2][16][C::HP];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
       const int tc = layerB ? s - 1 : s;             // time step this layer computes
       {
         const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
-        const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][0][0] + gh);
+        const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
       }
       f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};   // independent MFMA chains
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   constexpr int TX = (NXB + NW - 1) / NW;         // dx tiles per wave
   static_assert(16 * G4 / 4 == NT, "one dz float4 granule per thread");
   __shared__ __attribute__((aligned(16))) __bf16 zs[2][16][G4 + 8];     // dz row-major (B of U dz^T, W dz^T)
-  __shared__ __attribute__((aligned(16))) float dhs[2][16][H];          // dh_out tile
+  __shared__ __attribute__((aligned(16))) float dhs[2][16][C::HP];      // dh_out tile
   __shared__ __attribute__((aligned(16))) float dxs[2][16][DX ? 32 * KX : 1];   // dx tile
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -389,7 +392,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   const int col = lane & 15, quad = lane >> 4;
   const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
 
-  for (int i = tid; i < 2 * 16 * H; i += NT) (&dhs[0][0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * 16 * C::HP; i += NT) (&dhs[0][0][0])[i] = 0.f;
 
   // A fragments of U (dh_rec) and W (dx^T): tile row `col` of cell group gi is unit
   // 4 gi + (col >> 2) when col % 4 == 0 and zero otherwise -> acc[0] is the lane's own cell
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   }
   __syncthreads();
   // stage step 0 (t = T-1) tiles
-  *reinterpret_cast<float4*>(&dhs[0][0][0] + gd) = rd[0];
+  *reinterpret_cast<float4*>(&dhs[0][gd / H][gd % H]) = rd[0];
   GQ_TMB_LOAD_D(0, D)
   float dc[CPL], dhr[CPL], dhn[CPL];
 #pragma unroll
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
         zs[p][col][3 * H + u] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
       }
       GQ_TMB_LOAD_STATE(j, s + D)
-      *reinterpret_cast<float4*>(&dhs[p ^ 1][0][0] + gd) = rd[jn];   // dh tile of step s+1
+      *reinterpret_cast<float4*>(&dhs[p ^ 1][gd / H][gd % H]) = rd[jn];   // dh tile of step s+1
       GQ_TMB_LOAD_D(jn, s + 1 + D)
       lds_barrier();
 #pragma unroll
@@ -596,7 +599,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
   // [layer L (0 = B, 1 = A)][parity]; dd[0] = B's dh_out tile, dd[1] = W_B dz_B = A's dh tile.
   // Indexed by the (uniform) layer, never pointer-selected: all accesses stay DS instructions.
   __shared__ __attribute__((aligned(16))) __bf16 zs[2][2][16][G4 + 8];
-  __shared__ __attribute__((aligned(16))) float dd[2][2][16][H];
+  __shared__ __attribute__((aligned(16))) float dd[2][2][16][C::HP];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
   const int col = lane & 15, quad = lane >> 4;
   const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
 
-  for (int i = tid; i < 2 * 2 * 16 * H; i += 2 * NTL) (&dd[0][0][0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * 2 * 16 * C::HP; i += 2 * NTL) (&dd[0][0][0][0])[i] = 0.f;
   for (int i = tid; i < 2 * 2 * 16 * (G4 + 8); i += 2 * NTL) (&zs[0][0][0][0])[i] = (__bf16)0.f;
   const int unit = 4 * w + quad;
   const int au = 4 * w + (col >> 2);
@@ -669,7 +672,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
     GQ_TM2B_D(j, j)
   }
   __syncthreads();
-  *reinterpret_cast<float4*>(&dd[0][0][0][0] + gd) = rd[0];
+  *reinterpret_cast<float4*>(&dd[0][0][gd / H][gd % H]) = rd[0];
   GQ_TM2B_D(0, D)
   float dc = 0.f, dhr = 0.f;
   __syncthreads();
@@ -696,7 +699,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
         zs[L][p][col][3 * H + unit] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
       }
       GQ_TM2B_STATE(j, s + D)
-      *reinterpret_cast<float4*>(&dd[0][p ^ 1][0][0] + gd) = rd[jn];   // B's dh tile of step s+1
+      *reinterpret_cast<float4*>(&dd[0][p ^ 1][gd / H][gd % H]) = rd[jn];   // B's dh tile of step s+1
       GQ_TM2B_D(jn, s + 1 + D)
       lds_barrier();
       // ---------------- MFMA phase: dh_{t-1} = U dz_t (both chains)
