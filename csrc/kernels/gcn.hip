@@ -109,7 +109,10 @@ __global__ __launch_bounds__(256) void gcn_pool_fwd_kernel(const float* __restri
                                                            const float* __restrict__ anom, const float* __restrict__ W,
                                                            const float* __restrict__ bias, const float* __restrict__ scale,
                                                            const float* __restrict__ shift, const float* __restrict__ alpha,
-                                                           float* __restrict__ out, int B, int T, int N, int Ca) {
+                                                           float* __restrict__ out, int B, int T, int N, int Ca,
+                                                           int Mp, int Cp) {
+  // Mp > 0: write the time-major LSTM input [T][Mp][Cp] directly (rows b >= B and channels
+  // >= Ca + F zero), else [B][T][Ca + F]
   constexpr int FQ = F / 4, RPB = 64;             // channels per thread, rows per workgroup
   extern __shared__ __attribute__((aligned(16))) float sx[];   // RPB * N * Cin (if staged)
   const int L = N * Cin;
@@ -127,15 +130,21 @@ __global__ __launch_bounds__(256) void gcn_pool_fwd_kernel(const float* __restri
     psh[j] = shift[f0 + j];
     pal[j] = alpha[f0 + j];
   }
-  for (long row0 = (long)blockIdx.x * RPB; row0 < rows; row0 += (long)gridDim.x * RPB) {
+  const long vrows = Mp > 0 ? (long)Mp * T : rows;        // virtual rows incl. zero padding rows
+  for (long row0 = (long)blockIdx.x * RPB; row0 < vrows; row0 += (long)gridDim.x * RPB) {
     if (staged) {
       __syncthreads();
-      gcn_stage_rows(x, sx, row0, RPB, rows, L);
+      if (row0 < rows) gcn_stage_rows(x, sx, row0, RPB, rows, L);
       __syncthreads();
     }
     const long row = row0 + r;
-    if (row >= rows) continue;
-    const int b = (int)(row / T);
+    if (row >= vrows) continue;
+    const int b = (int)(row / T), t = (int)(row % T);
+    float* o = Mp > 0 ? out + ((long)t * Mp + b) * Cp : out + row * Fo;
+    if (row >= rows) {                            // (time-major only) padding row
+      for (int c = q; c < Cp; c += 4) o[c] = 0.f;
+      continue;
+    }
     const float* xr = staged ? sx + r * L : x + row * (long)L;
     const float* wr = w + (long)b * N;
     float acc[FQ];
@@ -155,10 +164,11 @@ __global__ __launch_bounds__(256) void gcn_pool_fwd_kernel(const float* __restri
         acc[j] += wn * (y > 0.f ? y : pal[j] * y);
       }
     }
-    float* o = out + row * Fo;
     for (int c = q; c < Ca; c += 4) o[c] = anom[row * Ca + c];
 #pragma unroll
     for (int j = 0; j < FQ; ++j) o[Ca + f0 + j] = acc[j];
+    if (Mp > 0)
+      for (int c = Fo + q; c < Cp; c += 4) o[c] = 0.f;
   }
 }
 
@@ -170,7 +180,8 @@ __global__ void gcn_pool_bwd_kernel(const float* __restrict__ x, const float* __
                                     const float* __restrict__ bias, const float* __restrict__ scale,
                                     const float* __restrict__ shift, const float* __restrict__ alpha,
                                     float* __restrict__ partial, int B, int T, int N, int F, int c_off,
-                                    int dstride) {
+                                    int dstride, int dmp) {
+  // dmp > 0: dout is time-major [T][dmp][dstride] (row (b,t) at (t*dmp + b)*dstride)
   // block = 256 threads = (256/F) rows x F channels (F divides 256)
   const int f = threadIdx.x % F;
   const int rsub = threadIdx.x / F;
@@ -184,7 +195,8 @@ __global__ void gcn_pool_bwd_kernel(const float* __restrict__ x, const float* __
   const long nrows = (long)B * T;
   for (long row = (long)blockIdx.x * rows_per_blk + rsub; row < nrows; row += (long)gridDim.x * rows_per_blk) {
     const int b = row / T;
-    const float g = dout[row * dstride + c_off + f];
+    const long dro = dmp > 0 ? ((row % T) * dmp + row / T) * (long)dstride : row * (long)dstride;
+    const float g = dout[dro + c_off + f];
     const float* xr = x + row * (long)N * Cin;
     const float* wr = w + (long)b * N;
     for (int n = 0; n < N; ++n) {
@@ -230,7 +242,7 @@ __global__ __launch_bounds__(256) void gcn_pool_bwd_input_kernel(const float* __
                                                                  const float* __restrict__ scale, const float* __restrict__ shift,
                                                                  const float* __restrict__ alpha, const float* __restrict__ coef,
                                                                  float* __restrict__ dx, int B, int T, int N, int c_off,
-                                                                 int dstride) {
+                                                                 int dstride, int dmp) {
   constexpr int FQ = F / 4;
   const int q = threadIdx.x & 3, f0 = q * FQ;
   float pw[Cin][FQ], pb[FQ], psc[FQ], psh[FQ], pal[FQ], c0[FQ], c1[FQ], c2[FQ];
@@ -251,9 +263,10 @@ __global__ __launch_bounds__(256) void gcn_pool_bwd_input_kernel(const float* __
   for (long row = (blockIdx.x * (long)blockDim.x + threadIdx.x) / 4; row < rows + 0; row += nthr) {
     // (all 4 lanes of a row take the same trip count: the shuffles below stay converged)
     const int b = (int)(row / T);
+    const long dro = dmp > 0 ? ((row % T) * dmp + b) * (long)dstride : row * (long)dstride;
     float g[FQ];
 #pragma unroll
-    for (int j = 0; j < FQ; ++j) g[j] = dout[row * dstride + c_off + f0 + j];
+    for (int j = 0; j < FQ; ++j) g[j] = dout[dro + c_off + f0 + j];
     const float* xr = x + row * (long)N * Cin;
     float* dxr = dx + row * (long)N * Cin;
     for (int n = 0; n < N; ++n) {
@@ -286,6 +299,47 @@ __global__ __launch_bounds__(256) void gcn_pool_bwd_input_kernel(const float* __
       }
     }
   }
+}
+
+// Deterministic column sums of a [R, C] fp32 matrix (per-workgroup partials, R large, C
+// small): workgroup = 8 columns x 32 row lanes, fixed-order LDS combine. (A torch sum over
+// dim 0 of a [1448, 80] partial matrix took ~20 us on the backward critical path.)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ in, long R, int C,
+                                                     float* __restrict__ out) {
+  __shared__ float red[32][9];
+  const int c8 = threadIdx.x & 7, l = threadIdx.x >> 3;
+  const int c = min(blockIdx.x * 8 + c8, C - 1);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  long r = l;
+  for (; r + 96 < R; r += 128) {
+    a0 += in[r * C + c];
+    a1 += in[(r + 32) * C + c];
+    a2 += in[(r + 64) * C + c];
+    a3 += in[(r + 96) * C + c];
+  }
+  for (; r < R; r += 32) a0 += in[r * C + c];
+  red[l][c8] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (threadIdx.x < 8 && blockIdx.x * 8 + c8 < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) s += red[k][c8];
+    out[c] = s;
+  }
+}
+
+// sum over the leading dim of a contiguous [R, ...] fp32 tensor
+at::Tensor colsum(const at::Tensor& partial) {
+  check_f32_cuda(partial, "partial");
+  const long R = partial.size(0);
+  const int C = (int)(partial.numel() / std::max<long>(R, 1));
+  std::vector<int64_t> shape(partial.sizes().begin() + 1, partial.sizes().end());
+  at::Tensor out = at::empty(shape, partial.options());
+  if (R == 0) return out.zero_();
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 7) / 8), dim3(256), 0, stream(), partial.data_ptr<float>(), R, C,
+                     out.data_ptr<float>());
+  GQ_LAUNCH_CHECK();
+  return out;
 }
 
 #define GQ_CIN_DISPATCH(CIN_RT, ...)                        \
@@ -333,7 +387,7 @@ at::Tensor gcn_stats(const at::Tensor& x, const at::Tensor& mask) {
 
 at::Tensor gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& anom, const at::Tensor& W,
                         const at::Tensor& b, const at::Tensor& scale, const at::Tensor& shift,
-                        const at::Tensor& alpha) {
+                        const at::Tensor& alpha, int64_t Mp, int64_t Cp) {
   for (auto* p : {&x, &w, &W, &b, &scale, &shift, &alpha}) check_f32_cuda(*p, "gcn input");
   const int B = x.size(0), T = x.size(1), N = x.size(2), Cin = x.size(3), F = W.size(1);
   TORCH_CHECK(W.size(0) == Cin && Cin <= GCN_MAX_CIN, "W must be [Cin,F], Cin<=8");
@@ -344,9 +398,10 @@ at::Tensor gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
     TORCH_CHECK(anom.size(0) == B && anom.size(1) == T, "anom must be [B,T,Ca]");
     Ca = anom.size(2);
   }
+  TORCH_CHECK(Mp == 0 || (Mp >= B && Mp % 16 == 0 && Cp >= Ca + F), "gcn_pool_fwd: time-major Mp / Cp");
   c10::DeviceGuard guard(x.device());
-  at::Tensor out = at::empty({B, T, Ca + F}, x.options());
-  const long rows = (long)B * T;
+  at::Tensor out = Mp > 0 ? at::empty({T, Mp, Cp}, x.options()) : at::empty({B, T, Ca + F}, x.options());
+  const long rows = Mp > 0 ? (long)Mp * T : (long)B * T;
   const float* anom_p = Ca ? anom.data_ptr<float>() : nullptr;
   const bool staged = N * Cin <= GCN_STAGE_MAX;
   const size_t smem = staged ? (size_t)64 * N * Cin * sizeof(float) : 0;
@@ -354,18 +409,19 @@ at::Tensor gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
       hipLaunchKernelGGL((gcn_pool_fwd_kernel<CIN, FF>), dim3(grid_for(rows, 64, 8192)), dim3(256), smem, stream(),
                          x.data_ptr<float>(), w.data_ptr<float>(), anom_p, W.data_ptr<float>(), b.data_ptr<float>(),
                          scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
-                         out.data_ptr<float>(), B, T, N, Ca)));
+                         out.data_ptr<float>(), B, T, N, Ca, (int)Mp, (int)Cp)));
   GQ_LAUNCH_CHECK();
   return out;
 }
 
 at::Tensor gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dout, const at::Tensor& W,
                         const at::Tensor& b, const at::Tensor& scale, const at::Tensor& shift,
-                        const at::Tensor& alpha, int64_t c_off) {
+                        const at::Tensor& alpha, int64_t c_off, bool time_major) {
   for (auto* p : {&x, &w, &dout, &W, &b, &scale, &shift, &alpha}) check_f32_cuda(*p, "gcn bwd input");
   const int B = x.size(0), T = x.size(1), N = x.size(2), Cin = x.size(3), F = W.size(1);
   TORCH_CHECK(256 % F == 0, "gcn_pool_bwd: F must divide 256");
-  TORCH_CHECK(dout.size(0) == B && dout.size(1) == T && dout.size(2) >= c_off + F, "dout shape");
+  TORCH_CHECK(time_major ? (dout.size(0) == T && dout.size(1) >= B && dout.size(2) >= c_off + F)
+                         : (dout.size(0) == B && dout.size(1) == T && dout.size(2) >= c_off + F), "dout shape");
   c10::DeviceGuard guard(x.device());
   const int nacc = 3 + Cin;
   const int rows_per_blk = 256 / F;
@@ -374,15 +430,16 @@ at::Tensor gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
   GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_pool_bwd_kernel<CIN>, dim3(nblk), dim3(256), 0, stream(), x.data_ptr<float>(),
                      w.data_ptr<float>(), dout.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(),
                      scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
-                     partial.data_ptr<float>(), B, T, N, F, (int)c_off, (int)dout.size(2)));
+                     partial.data_ptr<float>(), B, T, N, F, (int)c_off, (int)dout.size(2),
+                     time_major ? (int)dout.size(1) : 0));
   GQ_LAUNCH_CHECK();
-  return partial.sum(0);   // [3+Cin, F], fixed-order (deterministic) reduction
+  return colsum(partial);   // [3+Cin, F], fixed-order (deterministic) reduction
 }
 
 at::Tensor gcn_pool_bwd_input(const at::Tensor& x, const at::Tensor& w, const at::Tensor& mask,
                               const at::Tensor& dout, const at::Tensor& W, const at::Tensor& b,
                               const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& alpha,
-                              const at::Tensor& coef, int64_t c_off) {
+                              const at::Tensor& coef, int64_t c_off, bool time_major) {
   for (auto* p : {&x, &w, &mask, &dout, &W, &b, &scale, &shift, &alpha, &coef}) check_f32_cuda(*p, "gcn bwd_input");
   const int B = x.size(0), T = x.size(1), N = x.size(2), Cin = x.size(3), F = W.size(1);
   TORCH_CHECK(coef.numel() == 3 * F, "coef must be [3,F]");
@@ -394,7 +451,7 @@ at::Tensor gcn_pool_bwd_input(const at::Tensor& x, const at::Tensor& w, const at
                          x.data_ptr<float>(), w.data_ptr<float>(), mask.data_ptr<float>(), dout.data_ptr<float>(),
                          W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
                          alpha.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr<float>(), B, T, N,
-                         (int)c_off, (int)dout.size(2))));
+                         (int)c_off, (int)dout.size(2), time_major ? (int)dout.size(1) : 0)));
   GQ_LAUNCH_CHECK();
   return dx;
 }

@@ -27,6 +27,8 @@
 
 namespace gq {
 
+at::Tensor colsum(const at::Tensor& partial);     // gcn.hip
+
 // bits[b][i][w]: bit q of word w set iff A[b,i,32w+q] != 0 ; bitsT the same for A^T.
 // rs[b][i] = 1/deg_i (mean aggregation; 0 for an isolated node) or 1 (sum).
 __global__ void gcn_adj_bits_kernel(const float* __restrict__ adj, unsigned* __restrict__ bits,
@@ -381,7 +383,7 @@ at::Tensor gcn_node_bwd(const at::Tensor& x, const at::Tensor& bitsT, const at::
                          partial.data_ptr<float>(), g.B, g.T, g.N, g.F, (int)dout.size(2), (int)dout.size(1), g.NWd,
                          g.tchunk));
   GQ_LAUNCH_CHECK();
-  return partial.sum(0);
+  return colsum(partial);
 }
 
 at::Tensor gcn_node_bwd_input(const at::Tensor& x, const at::Tensor& bitsT, const at::Tensor& rs,

@@ -249,6 +249,7 @@ __global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __r
                                                                 float* __restrict__ ws2, int ncb, int DT, int HT,
                                                                 int Din, int H, float* __restrict__ dW,
                                                                 float* __restrict__ db, float* __restrict__ dU) {
+  // 16 consecutive slots (64 B per split row) x 16 split lanes (measured faster than 8 x 32)
   __shared__ float red[16][17];
   const int sl = threadIdx.x & 15, l = threadIdx.x >> 4;
   const int slot = min(blockIdx.x * 16 + sl, RC - 1);

@@ -38,11 +38,11 @@ TORCH_LIBRARY(gnnqc, m) {
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)
   m.def("gcn_stats(Tensor x, Tensor mask) -> Tensor");
   m.def("gcn_pool_fwd(Tensor x, Tensor w, Tensor anom, Tensor W, Tensor b, Tensor scale, Tensor shift, "
-        "Tensor alpha) -> Tensor");
+        "Tensor alpha, int Mp=0, int Cp=0) -> Tensor");
   m.def("gcn_pool_bwd(Tensor x, Tensor w, Tensor dout, Tensor W, Tensor b, Tensor scale, Tensor shift, "
-        "Tensor alpha, int c_off) -> Tensor");
+        "Tensor alpha, int c_off, bool time_major=False) -> Tensor");
   m.def("gcn_pool_bwd_input(Tensor x, Tensor w, Tensor mask, Tensor dout, Tensor W, Tensor b, Tensor scale, "
-        "Tensor shift, Tensor alpha, Tensor dzcoef, int c_off) -> Tensor");
+        "Tensor shift, Tensor alpha, Tensor dzcoef, int c_off, bool time_major=False) -> Tensor");
   // per-node GeneralConv writing the time-major LSTM input (gcn_node.hip)
   m.def("gcn_adj_bits(Tensor adj, bool agg_mean) -> Tensor[]");
   m.def("gcn_node_fwd(Tensor x, Tensor bits, Tensor rs, Tensor mask, Tensor W, Tensor b, Tensor scale, "

@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from ..config import freq_minutes
-from ..ops.gcn import gcn_node_tm, gcn_node_tm_ok, gcn_pool, pool_nodes
+from ..ops.gcn import gcn_node_tm, gcn_node_tm_ok, gcn_pool, gcn_pool_hip_ok, pool_nodes
 from .graphconv import GeneralConv, make_graph_layer
 from .layers import Dense, Dropout, LeakyReLU
 from .spatial import SensorsTimeLayer, SpatialTransformer
@@ -172,8 +172,28 @@ class GCNClassifier(nn.Module):
         d = self.leakyrelu5(self.dense2(d))
         return self.dense_out(d).squeeze(-1)
 
+    def _cml_time_major(self, inputs) -> bool:
+        """CML fast path: the fused GCN + pooling kernel writes the time-major LSTM input."""
+        if self.ds_type != "cml" or not self._fused_ok() or self.sensors_time_layer is not None:
+            return False
+        if self.spatial_transformer is not None or len(inputs) > 5:
+            return False
+        x, anom = inputs[0], inputs[1]
+        g = self.gcn_layer
+        pooling = "selection" if self.pooling_type == "selection" else self.aggregation_type
+        return (gcn_pool_hip_ok(x, g.kernel, g.aggregate, pooling, g.dropout, self.training)
+                and self.time_layer.time_major_ok(x, g.out_features + anom.shape[-1]))
+
     def features(self, inputs) -> torch.Tensor:
         """TimeLayer output rows [R, F] (CML: R = B; SoilNet: R = B*N) - the head's input."""
+        if self._cml_time_major(inputs):
+            x, anom, adj, mask, anom_pos = inputs[:5]
+            g = self.gcn_layer
+            pooling = "selection" if self.pooling_type == "selection" else self.aggregation_type
+            h, M = gcn_pool(x, adj, mask, anom, anom_pos, g.kernel, g.bias, g.bn_gamma, g.bn_beta, g.prelu_alpha,
+                            g.bn_moving_mean, g.bn_moving_variance, self.training, g.aggregate, pooling, g.momentum,
+                            g.eps, g.dropout, time_major=True)
+            return self.time_layer.forward_time_major(h, M)
         if self._soil_fused(inputs):
             x, adj, mask = inputs[:3]
             g = self.gcn_layer

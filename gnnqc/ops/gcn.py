@@ -104,14 +104,16 @@ class _HipGCNPool(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, mask, anom, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
-                momentum: float, eps: float):
+                momentum: float, eps: float, Mp: int = 0, Cp: int = 0):
         from ..utils.native import hip_ops
         ops = hip_ops()
         S = ops.gcn_stats(x, mask) if training else x.new_zeros(0, dtype=torch.float64)
         st = ops.gcn_bn_prep(S, W.contiguous(), b.contiguous(), gamma.contiguous(), beta.contiguous(),
                              running_mean, running_var, bool(training), float(momentum), float(eps))
         anom_t = anom.contiguous() if anom is not None else x.new_zeros(0)
-        out = ops.gcn_pool_fwd(x, w, anom_t, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous())
+        out = ops.gcn_pool_fwd(x, w, anom_t, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous(),
+                               int(Mp), int(Cp))
+        ctx.tm = Mp > 0
         ctx.training = training
         ctx.ca = 0 if anom is None else anom.shape[-1]
         ctx.has_anom = anom is not None
@@ -132,36 +134,54 @@ class _HipGCNPool(torch.autograd.Function):
         acc = empty
         if ctx.training or need_w:
             acc = ops.gcn_pool_bwd(x, w, dout, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous(),
-                                   ctx.ca)
+                                   ctx.ca, ctx.tm)
         sinks = [(_grad_sink(p) if n else (empty, True)) for p, n in zip(ctx.params, need[4:9])]
         coef = ops.gcn_bwd_finalize(acc, S, W.contiguous(), b.contiguous(), st, bool(ctx.training),
                                     *[s[0] for s in sinks])
         dx = None
         if need[0]:
             dx = ops.gcn_pool_bwd_input(x, w, mask, dout, W.contiguous(), b.contiguous(), st[2], st[3],
-                                        alpha.contiguous(), coef, ctx.ca)
-        danom = dout[..., : ctx.ca] if (ctx.has_anom and need[3]) else None
+                                        alpha.contiguous(), coef, ctx.ca, ctx.tm)
+        danom = None
+        if ctx.has_anom and need[3]:
+            danom = dout[:, : x.shape[0], : ctx.ca].transpose(0, 1) if ctx.tm else dout[..., : ctx.ca]
         grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need[4:9])]
-        return (dx, None, None, danom, *grads, None, None, None, None, None)
+        return (dx, None, None, danom, *grads, None, None, None, None, None, None, None)
+
+
+def gcn_pool_hip_ok(x, W, aggregate: str, pooling: str, dropout: float, training: bool) -> bool:
+    from . import use_hip
+    linear = aggregate in ("mean", "sum") and pooling in ("mean", "sum", "selection")
+    return bool(use_hip(x) and linear and not (dropout and training) and x.shape[-1] <= 8
+                and W.shape[1] in (8, 16, 32))
 
 
 def gcn_pool(x, adj, mask, anom, anom_pos, W, b, gamma, beta, alpha, running_mean, running_var,
              training: bool, aggregate: str = "mean", pooling: str = "mean", momentum: float = 0.99,
-             eps: float = 1e-3, dropout: float = 0.0):
+             eps: float = 1e-3, dropout: float = 0.0, time_major: bool = False):
     """GeneralConv + node pooling + concat -> LSTM input ``[B, T, Ca + F]``.
 
     Uses the fused HIP kernels for linear aggregation/pooling on GPU; otherwise the
-    eager per-node path.
+    eager per-node path. ``time_major=True`` (HIP path only) returns ``(h [T, Mp, Cp], B)``:
+    the time-major, row- and channel-padded input of
+    :meth:`gnnqc.models.timelayer.TimeLayer.forward_time_major`, written by the kernel itself.
     """
-    from . import use_hip
-    linear = aggregate in ("mean", "sum") and pooling in ("mean", "sum", "selection")
-    if use_hip(x) and linear and not (dropout and training) and x.shape[-1] <= 8 and 256 % W.shape[1] == 0:
+    if gcn_pool_hip_ok(x, W, aggregate, pooling, dropout, training):
         from ..utils.native import hip_ops
         ap = anom_pos.long().contiguous() if (pooling == "selection" and anom_pos is not None) else x.new_zeros(0)
         w = hip_ops().gcn_pool_weights(adj.float().contiguous(), mask.float().contiguous(), ap,
                                        aggregate == "mean", {"mean": 0, "sum": 1, "selection": 2}[pooling])
-        return _HipGCNPool.apply(x.contiguous(), w, mask.contiguous().float(), anom, W, b, gamma, beta, alpha,
-                                 running_mean, running_var, bool(training), float(momentum), float(eps))
+        Mp = Cp = 0
+        if time_major:
+            B = x.shape[0]
+            Mp = (B + 15) // 16 * 16
+            Cp = W.shape[1] + (anom.shape[-1] if anom is not None else 0)
+            Cp += (-Cp) % 4
+        out = _HipGCNPool.apply(x.contiguous(), w, mask.contiguous().float(), anom, W, b, gamma, beta, alpha,
+                                running_mean, running_var, bool(training), float(momentum), float(eps), Mp, Cp)
+        return (out, x.shape[0]) if time_major else out
+    if time_major:
+        raise ValueError("gcn_pool(time_major=True) needs the HIP path")
     h = general_conv_eager(x, adj, mask, W, b, gamma, beta, running_mean, running_var, alpha, training,
                            aggregate, dropout, momentum, eps)
     pooled = pool_nodes(h, mask, anom_pos, pooling)
@@ -273,5 +293,5 @@ def pool_nodes(h: torch.Tensor, mask: torch.Tensor, anom_pos, pooling: str = "me
     raise ValueError(pooling)
 
 
-__all__ = ["gcn_pool", "gcn_node_tm", "gcn_node_tm_eager", "gcn_node_tm_ok", "node_pool_weights", "masked_batchnorm", "general_conv_eager", "pool_nodes",
+__all__ = ["gcn_pool", "gcn_pool_hip_ok", "gcn_node_tm", "gcn_node_tm_eager", "gcn_node_tm_ok", "node_pool_weights", "masked_batchnorm", "general_conv_eager", "pool_nodes",
            "normalized_adjacency", "prelu"]

@@ -656,3 +656,35 @@ def test_split_lstm_backward_matches_fused(cuda_device, cml_windows, monkeypatch
     p0, l0 = run(False)
     assert abs(l1 - l0) < 2e-2 * abs(l0) + 1e-4, (l1, l0)
     assert (p1 - p0).norm().item() < 2e-3 * p0.norm().item()
+
+
+def test_cml_time_major_gcn_output_matches_batch_major(cuda_device, cml_windows, monkeypatch):
+    """CML GCN: kernel-written time-major LSTM input == batch-major kernel output + transpose/pad,
+    for logits, every parameter gradient and the input gradients (integrated gradients)."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    pc, ws = cml_windows
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    torch.manual_seed(0)
+    model = GCNClassifier(C.default("model_cml"), pc).to(cuda_device)
+    b = st.gather(torch.arange(40, device=cuda_device))
+
+    def run(tm):
+        monkeypatch.setattr(GCNClassifier, "_cml_time_major",
+                            (lambda self, i: GCNClassifier.__dict__["_cml_time_major_orig"](self, i)) if tm
+                            else (lambda self, i: False))
+        for p in model.parameters():
+            p.grad = None
+        x = b.x.clone().requires_grad_(True)
+        anom = b.anom.clone().requires_grad_(True)
+        z = model.logits((x, anom, b.adj, b.node_mask, b.anom_pos))
+        z.pow(2).sum().backward()
+        return [z.detach(), x.grad, anom.grad] + [p.grad.clone() for p in model.parameters()]
+
+    monkeypatch.setattr(GCNClassifier, "_cml_time_major_orig", GCNClassifier._cml_time_major, raising=False)
+    assert model._cml_time_major((b.x, b.anom, b.adj, b.node_mask, b.anom_pos))
+    r1 = run(True)
+    r0 = run(False)
+    for a, b_ in zip(r1, r0):
+        assert (a - b_).norm().item() <= 1e-4 * (b_.norm().item() + 1e-6)
