@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int din = dtile * 16 + 4 * quad + q;
-              if (din < Din) o[din] = acc[q];
+              if (din < lddx) o[din] = acc[q];   // columns Din .. lddx-1: zero (W rows masked)
             }
           }
         }

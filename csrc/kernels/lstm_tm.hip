@@ -949,8 +949,8 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
   c10::DeviceGuard guard(x.device());
   const long rows = (long)T * Mp;
   const int ncb = lstm_grads_col_blocks(H);
-  at::Tensor dx = need_dx ? (Dw < Din ? at::zeros({ncb, T, Mp, Din}, x.options()) : at::empty({ncb, T, Mp, Din}, x.options()))
-                          : at::empty({0}, x.options());
+  // padding channels (>= Dw) are written as zeros by the kernel (their W rows are masked)
+  at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
   lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                   need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                   db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, stream());
@@ -997,8 +997,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     const long rows = (long)T * Mp;
     const int ncb = lstm_grads_col_blocks(H);
     // dx keeps the x layout (Din channels); padding channels (>= Dw) get zero gradient
-    at::Tensor dx = need_dx ? (Dw < Din ? at::zeros({ncb, T, Mp, Din}, x.options()) : at::empty({ncb, T, Mp, Din}, x.options()))
-                            : at::empty({0}, x.options());
+    at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
     lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                     need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                     db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, st);

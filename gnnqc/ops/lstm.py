@@ -157,8 +157,8 @@ class _HipLSTM(torch.autograd.Function):
         if ctx.return_sequences:
             dh = dout.contiguous()
         else:
-            dh = dout.new_zeros(M, T, H)
-            dh[:, -1] = dout
+            # gradient only at the last step: one constant-pad launch (not zeros + slice copy)
+            dh = torch.nn.functional.pad(dout.unsqueeze(1), (0, 0, T - 1, 0))
         dz = ops.lstm_bwd(dh, g, c, U.contiguous(), ctx.bf16)
         if not ctx.bf16:
             # fp32 numerics-reference mode: exact fp32 GEMMs for the weight gradients
