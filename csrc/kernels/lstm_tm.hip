@@ -74,14 +74,56 @@ struct Granule {
   __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
 };
 
+// ---- fused MaxPooling1D(P) (valid, stride P) of a stored h sequence. Each storer lane owns
+// one float4 granule of the [16][H] tile for the whole sequence, so the running max and the
+// byte argmax (first maximum wins, like TF's MaxPoolGrad) stay in its registers; the pooled
+// granule and its 4 argmax bytes are written when a window closes. Layout = maxpool1d_fwd's
+// on the time-major tensor: pooled [T/P][Mp][H] fp32, argmax [T/P][Mp][H] uint8.
+struct PoolAcc {
+  float4 m;
+  unsigned idx;
+  __device__ __forceinline__ void step(const float4& v, int t, int P, int To, float* __restrict__ pout,
+                                       unsigned* __restrict__ iout, size_t off, size_t pstep) {
+    const int r = t % P;                            // t, P wave-uniform: scalar branches
+    if (r == 0) {
+      m = v;
+      idx = 0u;
+    } else {
+      const unsigned rb = (unsigned)r;
+      if (v.x > m.x) { m.x = v.x; idx = (idx & 0xffffff00u) | rb; }
+      if (v.y > m.y) { m.y = v.y; idx = (idx & 0xffff00ffu) | (rb << 8); }
+      if (v.z > m.z) { m.z = v.z; idx = (idx & 0xff00ffffu) | (rb << 16); }
+      if (v.w > m.w) { m.w = v.w; idx = (idx & 0x00ffffffu) | (rb << 24); }
+    }
+    if (r == P - 1 && t / P < To) {
+      const size_t k = (size_t)(t / P);
+      *reinterpret_cast<float4*>(pout + k * pstep + off) = m;
+      iout[(k * pstep + off) / 4] = idx;
+    }
+  }
+};
+
+// inverse for the backward: dh_t = dpool[t / P] where the argmax byte == t % P, else 0
+__device__ __forceinline__ float4 unpool4(const float4& v, unsigned idx, int t, int P, int To) {
+  const bool ok = t >= 0 && t < To * P;
+  const unsigned r = ok ? (unsigned)(t % P) : 0xffu;
+  float4 o;
+  o.x = ((idx & 0xffu) == r) ? v.x : 0.f;
+  o.y = (((idx >> 8) & 0xffu) == r) ? v.y : 0.f;
+  o.z = (((idx >> 16) & 0xffu) == r) ? v.z : 0.f;
+  o.w = ((idx >> 24) == r) ? v.w : 0.f;
+  return o;
+}
+
 // =====================================================================================
 // forward
 // x: [T][Mp][Din]  hout: [T][Mp][H]  gbuf: [T][tiles][NW][CPL][64][4]  cbuf: [..][64]
-template <int H, bool TRAIN, int KX, int GR, int D>
+template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hout, float* __restrict__ gbuf,
-    float* __restrict__ cbuf, int Mp, int T, int Din, int Dw) {
+    float* __restrict__ cbuf, int Mp, int T, int Din, int Dw, float* __restrict__ pout,
+    unsigned* __restrict__ iout, int P) {
   // Din: channels of the x layout (row pitch); Dw <= Din: rows of W (padding channels of x are zero)
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
@@ -146,6 +188,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
   const int gh = (tid % n_gh) * 4;
   float* hbase = hout + (size_t)row0 * H + gh;
   const size_t hstep = (size_t)Mp * H;
+  PoolAcc pool;
 
 #pragma unroll
   for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
@@ -169,6 +212,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
         const int ts = (t >= 1 && t <= T) ? t - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+        if (POOL && t >= 1 && t <= T) pool.step(v, t - 1, P, T / P, pout, iout, (size_t)row0 * H + gh, hstep);
       }
       f32x4_t acc[CPL];
 #pragma unroll
@@ -222,12 +266,13 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
 // recurrence of T + 1 steps instead of two of T. Outputs and saved state are exactly those
 // of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
 // (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
-template <int H, bool TRAIN, int KX, int GR, int D>
+template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
 __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
     const float* __restrict__ bB, float* __restrict__ hA, float* __restrict__ gA, float* __restrict__ cA,
-    float* __restrict__ hB, float* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw) {
+    float* __restrict__ hB, float* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw,
+    float* __restrict__ pout, unsigned* __restrict__ iout, int P) {
   using C = TMC<H>;
   static_assert(C::CPL == 1, "pair kernel: one cell per lane (H <= 64)");
   constexpr int NW = C::NW, NTL = C::NT, G4 = C::G4;
@@ -294,6 +339,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
   const size_t hstep = (size_t)Mp * H;
   float* gbuf = layerB ? gB : gA;
   float* cbuf = layerB ? cB : cA;
+  PoolAcc pool;
 
 #pragma unroll
   for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
@@ -317,6 +363,9 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
         const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+        // layer B's output feeds the MaxPooling1D that follows the pair
+        if (POOL && layerB && tc >= 1 && tc <= T)
+          pool.step(v, tc - 1, P, T / P, pout, iout, (size_t)row0 * H + gh, hstep);
       }
       f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};   // independent MFMA chains
       if (layerB) {
@@ -373,11 +422,13 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
 //       lengthens every step of the serial chain and pushes H = 32 past the VGPR budget.
 //   DX: dx^T = W dz_t^T tile -> HBM (frozen-weight input gradients, e.g. integrated gradients).
 // dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
-    int Mp, int T, int Din, int Dw) {
+    int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P) {
+  // UNPOOL: dhout is the gradient of the fused MaxPooling1D output [T/P][Mp][H] and pidx its
+  // argmax bytes; the scatter back to [T][Mp][H] happens as the dh tiles are staged
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
   constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
@@ -451,6 +502,14 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   const float* dbase = dhout + (size_t)row0 * H + gd;
   const size_t dstep = LAST ? 0 : (size_t)Mp * H;
   float4 rd[D];
+  unsigned ri[UNPOOL ? D : 1];
+  const int To = UNPOOL ? T / P : 0;
+  const unsigned* pbase = UNPOOL ? pidx + ((size_t)row0 * H + gd) / 4 : nullptr;
+  // stage the dh tile of time t (UNPOOL: scatter the pooled gradient by its argmax)
+  auto dh_tile = [&](int j, int t) -> float4 {
+    if constexpr (UNPOOL) return unpool4(rd[j], ri[j], t, P, To);
+    else return rd[j];
+  };
   // dz storer: one float4 granule of the [16][4H] tile per thread
   const int gz_seq = tid / (G4 / 4), gz_c = (tid % (G4 / 4)) * 4;
   float* zbase = dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
@@ -466,12 +525,18 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 #define GQ_TMB_LOAD_D(J, SS)                                                                \
   {                                                                                         \
     const int tt_ = max(T - 1 - (SS), 0);                                                   \
-    float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)tt_ * dstep);              \
-    if (LAST) {                                                                             \
-      const float m_ = (SS) == 0 ? 1.f : 0.f;                                               \
-      v_.x *= m_; v_.y *= m_; v_.z *= m_; v_.w *= m_;                                       \
+    if (UNPOOL) {                                                                           \
+      const size_t k_ = (size_t)min(tt_ / P, To - 1) * dstep;                               \
+      rd[J] = *reinterpret_cast<const float4*>(dbase + k_);                                 \
+      ri[J] = pbase[k_ / 4];                                                                \
+    } else {                                                                                \
+      float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)tt_ * dstep);            \
+      if (LAST) {                                                                           \
+        const float m_ = (SS) == 0 ? 1.f : 0.f;                                             \
+        v_.x *= m_; v_.y *= m_; v_.z *= m_; v_.w *= m_;                                     \
+      }                                                                                     \
+      rd[J] = v_;                                                                           \
     }                                                                                       \
-    rd[J] = v_;                                                                             \
   }
 #pragma unroll
   for (int j = 0; j < D; ++j) {
@@ -480,7 +545,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   }
   __syncthreads();
   // stage step 0 (t = T-1) tiles
-  *reinterpret_cast<float4*>(&dhs[0][gd / H][gd % H]) = rd[0];
+  *reinterpret_cast<float4*>(&dhs[0][gd / H][gd % H]) = dh_tile(0, T - 1);
   GQ_TMB_LOAD_D(0, D)
   float dc[CPL], dhr[CPL], dhn[CPL];
 #pragma unroll
@@ -514,7 +579,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
         zs[p][col][3 * H + u] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
       }
       GQ_TMB_LOAD_STATE(j, s + D)
-      *reinterpret_cast<float4*>(&dhs[p ^ 1][gd / H][gd % H]) = rd[jn];   // dh tile of step s+1
+      *reinterpret_cast<float4*>(&dhs[p ^ 1][gd / H][gd % H]) = dh_tile(jn, t - 1);   // dh tile of step s+1
       GQ_TMB_LOAD_D(jn, s + 1 + D)
       lds_barrier();
 #pragma unroll
@@ -762,20 +827,70 @@ static bool tm_supported(int H, int Din, int gr) {
   return 16 * Din / gr <= 16 * H;
 }
 
+// fused MaxPooling1D of the layer output: pooled [T/P, Mp, H] fp32 + argmax uint8 (P = 0: none)
+struct TmPool {
+  int P = 0;
+  float* out = nullptr;
+  unsigned* idx = nullptr;
+  const unsigned* cidx = nullptr;   // backward: argmax of the pooled gradient given as dh
+};
+
+static TmPool tm_pool_outputs(int P, int T, int Mp, int H, const at::TensorOptions& opt, at::Tensor& pooled,
+                              at::Tensor& pidx) {
+  TmPool pl;
+  if (P <= 0) {
+    pooled = at::empty({0}, opt);
+    pidx = at::empty({0}, opt.dtype(at::kByte));
+    return pl;
+  }
+  TORCH_CHECK(P <= 255 && T / P >= 1, "lstm_tm: pool size must be 1..255 and <= T");
+  pooled = at::empty({T / P, Mp, H}, opt);
+  pidx = at::empty({T / P, Mp, H}, opt.dtype(at::kByte));
+  pl.P = P;
+  pl.out = pooled.data_ptr<float>();
+  pl.idx = reinterpret_cast<unsigned*>(pidx.data_ptr<uint8_t>());
+  return pl;
+}
+
 template <int H, bool TRAIN, int KX, int GR>
 static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, float* g,
-                       float* c, int Mp, int T, int Din, int Dw, hipStream_t st) {
+                       float* c, int Mp, int T, int Din, int Dw, const TmPool& pl, hipStream_t st) {
   constexpr int D = 6;
-  hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W, U, b,
-                     h, g, c, Mp, T, Din, Dw);
+  if (pl.P > 0)
+    hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D, true>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W,
+                       U, b, h, g, c, Mp, T, Din, Dw, pl.out, pl.idx, pl.P);
+  else
+    hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D, false>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W,
+                       U, b, h, g, c, Mp, T, Din, Dw, nullptr, nullptr, 1);
 }
 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
 static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* W, const float* U,
-                       float* dx, float* dz, int Mp, int T, int Din, int Dw, hipStream_t st) {
+                       float* dx, float* dz, int Mp, int T, int Din, int Dw, hipStream_t st,
+                       const TmPool& pl = TmPool()) {
   constexpr int D = H >= 64 ? 2 : 4;        // H = 64: 16 waves x 128 VGPRs, shorter state rings
-  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh,
-                     g, c, W, U, dx, dz, Mp, T, Din, Dw);
+  if constexpr (!LAST) {
+    if (pl.P > 0) {
+      hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST, true>), dim3(ntiles), dim3(TMC<H>::NT), 0,
+                         st, dh, g, c, W, U, dx, dz, Mp, T, Din, Dw, pl.cidx, pl.P);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST, false>), dim3(ntiles), dim3(TMC<H>::NT), 0, st,
+                     dh, g, c, W, U, dx, dz, Mp, T, Din, Dw, nullptr, 1);
+}
+
+static TmPool tm_pool_input(const c10::optional<at::Tensor>& pidx, int64_t P, const at::Tensor& dh, int T, int Mp,
+                            int H) {
+  TmPool pl;
+  if (P <= 0) return pl;
+  TORCH_CHECK(pidx.has_value() && pidx->scalar_type() == at::kByte && pidx->is_contiguous() && pidx->is_cuda(),
+              "lstm_tm_bwd: pool_idx must be the uint8 argmax of the fused pooling");
+  TORCH_CHECK(dh.dim() == 3 && dh.size(0) == T / P && dh.size(1) == Mp && dh.size(2) == H &&
+                  pidx->sizes() == dh.sizes(), "lstm_tm_bwd: pooled gradient shape");
+  pl.P = (int)P;
+  pl.cidx = reinterpret_cast<const unsigned*>(pidx->data_ptr<uint8_t>());
+  return pl;
 }
 
 #define GQ_TM_H_DISPATCH(HV, ...)                                  \
@@ -809,7 +924,7 @@ static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float*
 // x: [T, Mp, Din] time-major; W: [Dw, 4H] with Dw <= Din (x channels >= Dw must be zero, e.g. the
 // alignment padding of a 19-channel input to 20). Returns [h (T,Mp,H), gates (state), c (state)].
 std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
-                                    const at::Tensor& b, bool train) {
+                                    const at::Tensor& b, bool train, int64_t pool) {
   check_f32_cuda(x, "x");
   check_f32_cuda(W, "W");
   check_f32_cuda(U, "U");
@@ -832,20 +947,22 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   auto st = stream();
   float* gp = train ? g.data_ptr<float>() : nullptr;
   float* cp = train ? c.data_ptr<float>() : nullptr;
+  at::Tensor pooled, pidx;
+  const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (train) tm_fwd_cfg<HH, true, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st);
+                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, pl, st);
       else tm_fwd_cfg<HH, false, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st))));
+                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, pl, st))));
   GQ_LAUNCH_CHECK();
-  return {h.narrow(0, 0, T), g, c};
+  return {h.narrow(0, 0, T), g, c, pooled, pidx};
 }
 
 // Pair forward (lstm_tm2_fwd_kernel): x [T, Mp, Din]; A: W [Dw <= Din, 4H], B: W [H, 4H].
 // Returns [hA, gA, cA, hB, gB, cB] with the layouts of lstm_tm_fwd.
 std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, const at::Tensor& UA,
                                      const at::Tensor& bA, const at::Tensor& WB, const at::Tensor& UB,
-                                     const at::Tensor& bB, bool train) {
+                                     const at::Tensor& bB, bool train, int64_t pool) {
   for (const at::Tensor* t : {&x, &WA, &UA, &bA, &WB, &UB, &bB}) check_f32_cuda(*t, "lstm_tm2_fwd operand");
   TORCH_CHECK(x.dim() == 3, "lstm_tm2_fwd: x must be [T, Mp, Din]");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)UA.size(0);
@@ -870,16 +987,19 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   auto st = stream();
   float* P[4] = {train ? gA.data_ptr<float>() : nullptr, train ? cA.data_ptr<float>() : nullptr,
                  train ? gB.data_ptr<float>() : nullptr, train ? cB.data_ptr<float>() : nullptr};
-#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR)                                                                         \
-  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,        \
+  at::Tensor pooled, pidx;
+  const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
+#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, PL)                                                                     \
+  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, PL>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,    \
                      x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
                      WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), P[0], \
-                     P[1], hB.data_ptr<float>(), P[2], P[3], Mp, T, Din, Dw)
+                     P[1], hB.data_ptr<float>(), P[2], P[3], Mp, T, Din, Dw, pl.out, pl.idx, pl.P > 0 ? pl.P : 1)
   GQ_TM2_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
-      if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR); else GQ_TM2_LAUNCH(HH, false, KXX, GRR))));
+      if (pl.P > 0) { if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, true); else GQ_TM2_LAUNCH(HH, false, KXX, GRR, true); }
+      else { if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, false); else GQ_TM2_LAUNCH(HH, false, KXX, GRR, false); })));
 #undef GQ_TM2_LAUNCH
   GQ_LAUNCH_CHECK();
-  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB};
+  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB, pooled, pidx};
 }
 
 // Pair backward recurrences (lstm_tm2_bwd_kernel): dh [T, Mp, H] of B's output sequence;
@@ -910,12 +1030,13 @@ std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB,
 // Backward recurrence only: dz [T+1, Mp, 4H] (row T scratch) for the split backward (dx and
 // the weight-gradient pass are then launched separately, the latter on a side stream).
 at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& W,
-                          const at::Tensor& U, int64_t T) {
+                          const at::Tensor& U, int64_t T, const c10::optional<at::Tensor>& pool_idx, int64_t pool) {
   for (const at::Tensor* t : {&dh, &g, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_dz operand");
   const int H = (int)U.size(0);
   const bool last = dh.dim() == 2;
   const int Mp = (int)(last ? dh.size(0) : dh.size(1));
-  TORCH_CHECK(last ? dh.size(1) == H : (dh.size(0) == T && dh.size(2) == H), "lstm_tm_bwd_dz: dh shape");
+  TORCH_CHECK(last ? dh.size(1) == H : ((pool > 0 || dh.size(0) == T) && dh.size(2) == H), "lstm_tm_bwd_dz: dh shape");
+  const TmPool pl = tm_pool_input(pool_idx, last ? 0 : pool, dh, (int)T, Mp, H);
   TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H,
               "lstm_tm_bwd_dz: saved state shapes");
   TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_tm_bwd_dz: hidden size");
@@ -929,7 +1050,7 @@ at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::T
             (int)W.size(0), (int)W.size(0), st);
       else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
             c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, (int)T,
-            (int)W.size(0), (int)W.size(0), st));
+            (int)W.size(0), (int)W.size(0), st, pl));
   GQ_LAUNCH_CHECK();
   return dz;
 }
@@ -962,15 +1083,16 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
 // (empty if !need_dx) and accumulates dW, dU, db when they are non-empty.
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
                        const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, at::Tensor dW, at::Tensor dU,
-                       at::Tensor db, bool need_dx) {
+                       at::Tensor db, bool need_dx, const c10::optional<at::Tensor>& pool_idx, int64_t pool) {
   const at::Tensor* ops[] = {&dh, &g, &c, &x, &h, &W, &U};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
   const int Dw = (int)W.size(0);
   TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H, "lstm_tm_bwd: W shape");
   const bool last = dh.dim() == 2;
-  TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H) : (dh.size(0) == T && dh.size(1) == Mp && dh.size(2) == H),
-              "lstm_tm_bwd: dh shape");
+  TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H)
+                   : ((pool > 0 || dh.size(0) == T) && dh.size(1) == Mp && dh.size(2) == H), "lstm_tm_bwd: dh shape");
+  const TmPool pl = tm_pool_input(pool_idx, last ? 0 : pool, dh, T, Mp, H);
   TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H &&
                   h.numel() == (long)T * Mp * H, "lstm_tm_bwd: saved state shapes");
   const bool wg = dW.numel() > 0;
@@ -992,7 +1114,8 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
         if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
               c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st);
         else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st));
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st,
+              pl));
     GQ_LAUNCH_CHECK();
     const long rows = (long)T * Mp;
     const int ncb = lstm_grads_col_blocks(H);
@@ -1009,7 +1132,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #define GQ_TM_BWD_CALL(LASTV)                                                                               \
   tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),          \
                                                c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
-                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st)
+                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st, pl)
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (last) GQ_TM_BWD_CALL(true); else GQ_TM_BWD_CALL(false))));
 #undef GQ_TM_BWD_CALL

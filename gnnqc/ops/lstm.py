@@ -194,13 +194,13 @@ class _HipLSTM(torch.autograd.Function):
                 None, None)
 
 
-def _tm_split_backward(dh, g, c, x, h, W, U, sinks, need_dx):
+def _tm_split_backward(dh, g, c, x, h, W, U, sinks, need_dx, pool_idx=None, pool: int = 0):
     """Time-major layer backward in direct-accumulation mode: recurrence -> dz, dx = dz W^T
     on the current stream; the weight-gradient pass on the side stream."""
     from ..utils.native import hip_ops
     ops = hip_ops()
     T = x.shape[0]
-    dz = ops.lstm_tm_bwd_dz(dh, g, c, W, U, T)
+    dz = ops.lstm_tm_bwd_dz(dh, g, c, W, U, T, pool_idx, int(pool))
     dx = ops.lstm_dx(dz, W, x) if need_dx else None
     _off_critical_path(x.device, (dz, x, h, W),
                        lambda: ops.lstm_tm_grads(dz, x, h, W, sinks[0][0], sinks[1][0], sinks[2][0], False))
@@ -213,38 +213,45 @@ class _HipLSTMTM(torch.autograd.Function):
     accumulated straight into the gradient buffers (direct mode) or returned."""
 
     @staticmethod
-    def forward(ctx, x, W, U, b, return_sequences: bool):
+    def forward(ctx, x, W, U, b, return_sequences: bool, pool: int = 0):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:4])
-        h, g, c = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need)
+        h, g, c, pooled, pidx = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need,
+                                                      int(pool))
         ctx.params = (W, U, b)
         ctx.return_sequences = return_sequences
+        ctx.pool = int(pool)
         if need:
-            ctx.save_for_backward(x, W, U, h, g, c)
+            ctx.save_for_backward(x, W, U, h, g, c, pidx)
+        if pool:
+            return pooled
         return h if return_sequences else h[-1]
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
-        x, W, U, h, g, c = ctx.saved_tensors
+        x, W, U, h, g, c, pidx = ctx.saved_tensors
         need = ctx.needs_input_grad
         wgrad = any(need[1:4])
         need_dx = bool(need[0])
+        pool = ctx.pool
         if not wgrad and not need_dx:
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         if wgrad:
             sinks = [_grad_sink(p) for p in ctx.params]
         else:
             e = x.new_zeros(0)
             sinks = [(e, True)] * 3
+        pi = pidx if pool else None
         if wgrad and all(d for _, d in sinks) and _split_mode() != "fused":
-            dx = _tm_split_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
+            dx = _tm_split_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx,
+                                    pi, pool)
         else:
             dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
-                                       sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
+                                       sinks[0][0], sinks[1][0], sinks[2][0], need_dx, pi, pool)
         grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
-        return (dx if need_dx else None, *grads, None)
+        return (dx if need_dx else None, *grads, None, None)
 
 
 class _HipLSTMTMPair(torch.autograd.Function):
@@ -253,24 +260,29 @@ class _HipLSTMTMPair(torch.autograd.Function):
     per-layer fused kernels (B first, its dx is A's dh)."""
 
     @staticmethod
-    def forward(ctx, x, WA, UA, bA, WB, UB, bB):
+    def forward(ctx, x, WA, UA, bA, WB, UB, bB, pool: int = 0):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:7])
-        hA, gA, cA, hB, gB, cB = hip_ops().lstm_tm2_fwd(x, WA.contiguous(), UA.contiguous(), bA.contiguous(),
-                                                        WB.contiguous(), UB.contiguous(), bB.contiguous(), need)
+        hA, gA, cA, hB, gB, cB, pooled, pidx = hip_ops().lstm_tm2_fwd(
+            x, WA.contiguous(), UA.contiguous(), bA.contiguous(), WB.contiguous(), UB.contiguous(), bB.contiguous(),
+            need, int(pool))
         ctx.params = (WA, UA, bA, WB, UB, bB)
+        ctx.pool = int(pool)
         if need:
-            ctx.save_for_backward(x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB)
-        return hB
+            ctx.save_for_backward(x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB, pidx)
+        return pooled if pool else hB
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB = ctx.saved_tensors
+        x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB, pidx = ctx.saved_tensors
         need = ctx.needs_input_grad
         e = x.new_zeros(0)
+        pool = ctx.pool
+        pi = pidx if pool else None
+        dout = dout.contiguous()
 
         def sinks(params, flags):
             if any(flags):
@@ -284,23 +296,26 @@ class _HipLSTMTMPair(torch.autograd.Function):
         if any(need[1:7]) and _pair_bwd():
             # training: both reverse recurrences in one pipelined kernel (B's dx stays in LDS),
             # then one weight-gradient pass per layer (+ dx of A)
-            dzA, dzB = ops.lstm_tm2_bwd(dout.contiguous(), gB, cB, gA, cA, WB.contiguous(), UB.contiguous(),
+            if pool:      # (this kernel takes the unpooled gradient)
+                T, Mp, H = hB.shape
+                dout = ops.maxpool1d_bwd(dout.view(1, -1, Mp * H), pidx.view(1, -1, Mp * H), T, pool).view(T, Mp, H)
+            dzA, dzB = ops.lstm_tm2_bwd(dout, gB, cB, gA, cA, WB.contiguous(), UB.contiguous(),
                                         UA.contiguous())
             ops.lstm_tm_grads(dzB, hA, hB, WB.contiguous(), sB[0][0], sB[1][0], sB[2][0], False)
             dx = ops.lstm_tm_grads(dzA, x, hA, WA.contiguous(), sA[0][0], sA[1][0], sA[2][0], need_dx)
         elif (any(need[4:7]) and all(d for _, d in sB) and any(need[1:4]) and all(d for _, d in sA)
               and _split_mode() != "fused"):
-            dhA = _tm_split_backward(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
+            dhA = _tm_split_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True, pi, pool)
             dx = _tm_split_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
-            dhA = ops.lstm_tm_bwd(dout.contiguous(), gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
-                                  sB[0][0], sB[1][0], sB[2][0], True)
+            dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
+                                  sB[0][0], sB[1][0], sB[2][0], True, pi, pool)
             if need_dx or any(need[1:4]):
                 dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0],
                                      sA[2][0], need_dx)
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
-        return (dx if need_dx else None, *gA_, *gB_)
+        return (dx if need_dx else None, *gA_, *gB_, None)
 
 
 def _pair_bwd() -> bool:
@@ -314,9 +329,11 @@ def _pair_bwd() -> bool:
     return os.environ.get("GNNQC_PAIR_BWD", "0") == "1"
 
 
-def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:
-    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``)."""
-    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias)
+def lstm_pair_tm(x_tm, A, B, pool: int = 0) -> torch.Tensor:
+    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``); ``pool`` > 0
+    also fuses the following MaxPooling1D (returns the pooled sequence)."""
+    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias,
+                                int(pool))
 
 
 def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf16: bool = True) -> bool:
@@ -327,8 +344,9 @@ def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf1
 
 
 def lstm_layer_tm(x_tm: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
-                  return_sequences: bool = True) -> torch.Tensor:
-    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences))
+                  return_sequences: bool = True, pool: int = 0) -> torch.Tensor:
+    """Time-major layer; ``pool`` > 0 fuses a following MaxPooling1D(pool) into the kernels."""
+    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences), int(pool))
 
 
 def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
