@@ -5,8 +5,9 @@
 * ``gnnqc_state.pt``   - tensors only (parameters, BN statistics, optimiser slots,
   step counters); loaded with ``torch.load(weights_only=True)``;
 * ``gnnqc_meta.json``  - model/preprocessing config, class, epoch, RNG cursor;
-* ``variables/variables.{index,data-00000-of-00001}`` + ``keras_metadata.pb`` - the
-  Keras SavedModel variable layout (TensorBundle) and per-layer JSON, see
+* ``variables/variables.{index,data-00000-of-00001}`` (+ ``_CHECKPOINTABLE_OBJECT_GRAPH``),
+  ``keras_metadata.pb`` and ``fingerprint.pb`` - the Keras SavedModel variable layout
+  (TensorBundle), object graph, per-layer JSON and content fingerprint, see
   :mod:`gnnqc.ckpt.tensorbundle`, :mod:`gnnqc.ckpt.keras_layout`, :mod:`gnnqc.ckpt.keras_meta`.
 
 ``load_model(path)`` rebuilds the model from the metadata and restores the state;
@@ -58,8 +59,10 @@ def save_model(model, path: str, optimizer=None, epoch: Optional[int] = None, pr
     if keras_layout:
         from .keras_layout import write_keras_variables
         from .keras_meta import write_keras_metadata
+        from .keras_layout import write_fingerprint
         write_keras_variables(model, path, optimizer)
         write_keras_metadata(model, path, optimizer)
+        write_fingerprint(path)
 
 
 def load_model(path: str, device="cpu", with_optimizer: bool = False):

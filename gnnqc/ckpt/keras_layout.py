@@ -66,9 +66,79 @@ def keras_tensors(model, optimizer=None) -> Dict[str, object]:
     return out
 
 
+OBJECT_GRAPH_KEY = "_CHECKPOINTABLE_OBJECT_GRAPH"
+
+
+def object_graph(keys, full_names: Optional[Dict[str, str]] = None) -> bytes:
+    """``TrackableObjectGraph`` proto for a set of ``<path>/.ATTRIBUTES/VARIABLE_VALUE`` keys.
+
+    Node 0 is the root; every path prefix (``variables``, ``variables/3``, ``optimizer/_variables``,
+    ...) becomes a node whose ``children`` reference the next component by local name, and each
+    variable node carries one ``SerializedTensor`` attribute (name ``VARIABLE_VALUE``, the
+    checkpoint key) - the part of the reference's 600-node Keras graph
+    (``model_cml/variables``, decoded in SURVEY §5.4) that object-based restore uses to map
+    checkpoint keys to objects. Function / signature nodes are not emitted (no graph is saved).
+    Field numbers follow tensorflow/core/protobuf/trackable_object_graph.proto."""
+    from .tensorbundle import _pb_bytes, _pb_varint
+    full_names = full_names or {}
+    nodes = [{"children": [], "attrs": []}]
+    index = {(): 0}
+    for key in sorted(keys):
+        if not key.endswith(SUFFIX):
+            continue
+        parts = tuple(key[: -len(SUFFIX)].split("/"))
+        for d in range(1, len(parts) + 1):
+            pre = parts[:d]
+            if pre not in index:
+                index[pre] = len(nodes)
+                nodes.append({"children": [], "attrs": []})
+                nodes[index[parts[: d - 1]]]["children"].append((index[pre], parts[d - 1]))
+        nodes[index[parts]]["attrs"].append(("VARIABLE_VALUE", full_names.get(key, "/".join(parts)), key))
+    out = b""
+    for n in nodes:
+        body = b"".join(_pb_bytes(1, _pb_varint(1, nid) + _pb_bytes(2, name.encode())) for nid, name in n["children"])
+        body += b"".join(_pb_bytes(2, _pb_bytes(1, a.encode()) + _pb_bytes(2, f.encode()) + _pb_bytes(3, k.encode()))
+                         for a, f, k in n["attrs"])
+        out += _pb_bytes(1, body)
+    return out
+
+
+def write_fingerprint(path: str):
+    """``fingerprint.pb`` (``FingerprintDef``): 64-bit content hashes of what the directory holds
+    (fields 1-5: saved-model checksum, graph hash, signature hash, object-graph hash, checkpoint
+    hash; 6: version). Our hashes are blake2b-64 of the files, not TF's farmhash; no saved
+    graph exists, so the graph / signature hashes are of empty inputs."""
+    import hashlib
+    from .tensorbundle import _pb_bytes, _pb_varint
+
+    def h(*blobs):
+        d = hashlib.blake2b(digest_size=8)
+        for b in blobs:
+            d.update(b)
+        return int.from_bytes(d.digest(), "little")
+
+    var = os.path.join(path, "variables", "variables")
+    with open(var + ".index", "rb") as f:
+        idx = f.read()
+    with open(var + ".data-00000-of-00001", "rb") as f:
+        data = f.read()
+    meta = b""
+    mp = os.path.join(path, "keras_metadata.pb")
+    if os.path.exists(mp):
+        with open(mp, "rb") as f:
+            meta = f.read()
+    ck = h(idx, data)
+    fp = (_pb_varint(1, h(idx, data, meta)) + _pb_varint(2, h(b"")) + _pb_varint(3, h(b"")) + _pb_varint(4, h(idx))
+          + _pb_varint(5, ck) + _pb_bytes(6, b""))
+    with open(os.path.join(path, "fingerprint.pb"), "wb") as f:
+        f.write(fp)
+
+
 def write_keras_variables(model, path: str, optimizer=None):
-    """Write ``<path>/variables/variables.{index,data-00000-of-00001}``."""
-    write_bundle(os.path.join(path, "variables", "variables"), keras_tensors(model, optimizer))
+    """Write ``<path>/variables/variables.{index,data-00000-of-00001}`` (with the object graph)."""
+    t = keras_tensors(model, optimizer)
+    t[OBJECT_GRAPH_KEY] = object_graph(list(t))
+    write_bundle(os.path.join(path, "variables", "variables"), t)
 
 
 def _bundle_prefix(path: str) -> str:

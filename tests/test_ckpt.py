@@ -67,7 +67,7 @@ def test_reference_checkpoint_layout(name, tmp_path):
     ours = read_bundle(str(tmp_path / "variables" / "variables"))
     ref = read_bundle(os.path.join(REF, name, "variables", "variables"))
     for k, v in ours.items():
-        if k.startswith("model_info"):
+        if k.startswith("model_info") or k == "_CHECKPOINTABLE_OBJECT_GRAPH":   # (graph: own test)
             continue
         if isinstance(v, bytes):
             assert v == ref[k]
@@ -150,3 +150,65 @@ def test_keras_metadata_matches_reference_structure(name, tmp_path):
         if "build_input_shape" in rm and path != "root":
             assert om["build_input_shape"] == rm["build_input_shape"], path
     assert ours["root"]["metadata"]["training_config"]["loss"] == "binary_crossentropy"
+
+
+def _graph_nodes(raw: bytes):
+    from gnnqc.ckpt.tensorbundle import _proto_fields
+    nodes = []
+    for f, _, v in _proto_fields(raw):
+        if f != 1:
+            continue
+        ch, at = [], []
+        for f2, _, v2 in _proto_fields(v):
+            if f2 == 1:
+                d = {a: b for a, _, b in _proto_fields(v2)}
+                ch.append((d.get(1, 0), d[2].decode()))
+            elif f2 == 2:
+                d = {a: b.decode() for a, _, b in _proto_fields(v2)}
+                at.append(d)
+        nodes.append((ch, at))
+    return nodes
+
+
+def _resolve(nodes, key):
+    """Walk the object graph along the key's path; return the leaf's attribute keys."""
+    node = 0
+    for part in key.split("/.ATTRIBUTES/")[0].split("/"):
+        node = dict((n, i) for i, n in nodes[node][0])[part]
+    return [a[3] for a in nodes[node][1]]
+
+
+def test_object_graph_and_fingerprint(tmp_path):
+    """Saved checkpoints carry a TrackableObjectGraph resolving every key, and fingerprint.pb."""
+    model, pc, mc = _model()
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    save_model(model, str(tmp_path), optimizer=opt, epoch=0, preproc_config=pc)
+    b = read_bundle(str(tmp_path / "variables" / "variables"))
+    nodes = _graph_nodes(b["_CHECKPOINTABLE_OBJECT_GRAPH"])
+    keys = [k for k in b if k.endswith("/.ATTRIBUTES/VARIABLE_VALUE")]
+    assert len(keys) > 34
+    for k in keys:
+        assert _resolve(nodes, k) == [k]
+    root_children = {n for _, n in nodes[0][0]}
+    assert {"variables", "model_info", "optimizer"} <= root_children
+    fp = (tmp_path / "fingerprint.pb").read_bytes()
+    assert len(fp) > 40 and fp[0] == 0x08
+
+
+@needs_ref
+def test_object_graph_paths_match_reference():
+    """Every variable key of the reference's own object graph resolves along the same path in
+    the graph we write for the same architecture (the variable-bearing part of the graph)."""
+    import tempfile
+    ref = read_bundle(os.path.join(REF, "model_cml", "variables", "variables"))
+    ref_nodes = _graph_nodes(ref["_CHECKPOINTABLE_OBJECT_GRAPH"])
+    model, pc, mc = _model()
+    with tempfile.TemporaryDirectory() as d:
+        save_model(model, d, preproc_config=pc)
+        ours = read_bundle(os.path.join(d, "variables", "variables"))
+    nodes = _graph_nodes(ours["_CHECKPOINTABLE_OBJECT_GRAPH"])
+    ref_keys = [k for k in ref if k.startswith(("variables/", "model_")) and k.endswith("VARIABLE_VALUE")]
+    assert len(ref_keys) >= 34
+    for k in ref_keys:
+        assert _resolve(ref_nodes, k) == [k]
+        assert _resolve(nodes, k) == [k]
