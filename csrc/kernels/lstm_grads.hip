@@ -15,264 +15,24 @@
 //   * dx^T = W dz^T uses W as register-resident A fragments; with one column
 //     block (H <= 16) dx is stored directly, otherwise accumulated atomically.
 #include "common.h"
+#include "lstm_grads_body.h"
 
 namespace gq {
 
-constexpr int GR_ROWS = 32;         // rows (sequence, step) per tile = MFMA K
-constexpr int GR_CB = 64;           // gate-units per column block (4 waves x 16)
-constexpr int GR_LDR = GR_ROWS + 8; // padded LDS row length (bf16) of transposed images
-
-// One workgroup = (column block cb of 64 gate-units, row split s); it walks the row tiles
-// s, s + splits, ... with a one-tile register prefetch: tile i+1's dz / x / h_{t-1} loads are
-// issued before tile i's MFMAs and only waited for when tile i+1 is staged (LDS-only
-// barriers, so the loads stay in flight across them). Every tile's x and h rows are ONE
-// contiguous span (flat rows), streamed in GRX-float granules. The weight-gradient partial
-// tiles stay in VGPRs and are written once per workgroup, in MFMA-fragment order, to a
-// workspace that lstm_grads_reduce_kernel sums over the splits (fixed order, plain
-// read-modify-write into the gradient buffers: deterministic, no float atomics).
 template <int H, int DT, int GRX>
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
     long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems) {
-  constexpr int G4 = 4 * H;
-  constexpr int HT = H / 16;        // k tiles of dU
-  constexpr int DP = DT * 16;       // padded din (incl. bias channel)
-  constexpr int XGM = (GR_ROWS * 144 / GRX + 255) / 256;   // max x granules per thread
-  constexpr int HG = (GR_ROWS * H / 4 + 255) / 256;        // h float4 granules per thread
-  __shared__ __attribute__((aligned(16))) __bf16 dzT[GR_CB][GR_LDR];          // [gu][row]
-  __shared__ __attribute__((aligned(16))) __bf16 dzR[GR_ROWS][GR_CB + 8];     // [row][gu]
-  __shared__ __attribute__((aligned(16))) __bf16 xT[DP][GR_LDR];             // [din][row]
-  __shared__ __attribute__((aligned(16))) __bf16 hT[H][GR_LDR];              // [k][row]
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = tid >> 6;
-  const int col = lane & 15;
-  const int quad = lane >> 4;
-  const int cb = blockIdx.x;               // column block: gate-units [cb*64, cb*64+64)
-  const int split = blockIdx.y, splits = gridDim.y;
-  const int gu0 = cb * GR_CB;
-  const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
-  const long nmine = split < ntiles ? (ntiles - 1 - split) / splits + 1 : 0;
-
-  for (int e = tid; e < DP * GR_LDR; e += 256) (&xT[0][0])[e] = (__bf16)0.f;   // channels > Din stay 0
-
-  f32x4_t accW[DT], accU[HT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d) accW[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < HT; ++k) accU[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // dx work items of this wave: (din tile, row tile) pairs, 2 row tiles per 32 rows
-  constexpr int DXT = (DP + 15) / 16 * 2;
-  bf16x8_t wa[(DXT + 3) / 4][2];
-#pragma unroll
-  for (int i = 0; i < (DXT + 3) / 4; ++i) {
-    const int item = w + 4 * i;
-    const int dtile = item >> 1;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int din = dtile * 16 + col;
-        const int gu = gu0 + 32 * ks + 8 * quad + j;
-        v[j] = (__bf16)(W[(size_t)min(din, Din - 1) * G4 + gu] * ((item < DXT && din < Din) ? 1.f : 0.f));
-      }
-      wa[i][ks] = v;
-    }
-  }
-
-  // ---- per-tile register images (prefetch ring of depth 1)
-  float4 rz[2];                     // dz: rows tid/16 and tid/16 + 16, gate-units 4*(tid%16) ..
-  float rx[XGM][GRX];               // x granules of the contiguous [32][ldx] span
-  float4 rh[HG];                    // h_{t-1} granules of the contiguous [32][H] span
-  const int zr = tid >> 4, zc = (tid & 15) * 4;
-  const long xspan = (long)GR_ROWS * ldx;
-  const long hspan = (long)GR_ROWS * H;
-  // x_elems: floats readable from x (a strided view may end before rows * ldx)
-  const long xlast = (x_elems - GRX) / GRX * GRX, hlast = rows * (long)H - 4;
-  auto load_tile = [&](long tile) {
-    const long r0 = tile * GR_ROWS;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const long r = min(r0 + zr + 16 * q, rows - 1);
-      rz[q] = *reinterpret_cast<const float4*>(dz + (size_t)r * G4 + gu0 + zc);
-    }
-    // granule offsets are clamped into the tile's span (idle lanes re-read a line already
-    // being fetched instead of the next tile's data) and into the array (rows past the end
-    // and h_{t-1} of a period's first step are masked when staged)
-#pragma unroll
-    for (int i = 0; i < XGM; ++i) {
-      if (i < xg) {                               // kernel argument: a scalar (uniform) branch
-        const long o = min(r0 * ldx + min((long)(tid + 256 * i) * GRX, xspan - GRX), xlast);
-        if constexpr (GRX == 4) {
-          const float4 v = *reinterpret_cast<const float4*>(x + o);
-          rx[i][0] = v.x; rx[i][1] = v.y; rx[i][2] = v.z; rx[i][3] = v.w;
-        } else {
-          rx[i][0] = x[o];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < HG; ++i) {
-      const long o = min(max((r0 - hshift) * H + min((long)(tid + 256 * i) * 4, hspan - 4), 0L), hlast);
-      rh[i] = *reinterpret_cast<const float4*>(hseq + o);
-    }
-  };
-  auto stage_tile = [&](long tile) {
-    const long r0 = tile * GR_ROWS;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int rr = zr + 16 * q;
-      const float m = (r0 + rr < rows) ? 1.f : 0.f;
-      const __bf16 b0 = (__bf16)(rz[q].x * m), b1 = (__bf16)(rz[q].y * m), b2 = (__bf16)(rz[q].z * m),
-                   b3 = (__bf16)(rz[q].w * m);
-      typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = bf16x4_t{b0, b1, b2, b3};
-      dzT[zc + 0][rr] = b0;
-      dzT[zc + 1][rr] = b1;
-      dzT[zc + 2][rr] = b2;
-      dzT[zc + 3][rr] = b3;
-    }
-#pragma unroll
-    for (int i = 0; i < XGM; ++i) {
-      const long g = (long)(tid + 256 * i) * GRX;
-      if (i < xg && g < xspan) {                  // xg: wave-uniform (kernel argument)
-        const int rr = (int)(g / ldx), d0 = (int)(g % ldx);
-        const float m = (r0 + rr < rows) ? 1.f : 0.f;
-#pragma unroll
-        for (int q = 0; q < GRX; ++q)
-          if (d0 + q < Din) xT[d0 + q][rr] = (__bf16)(rx[i][q] * m);
-      }
-    }
-    if (tid < GR_ROWS) xT[Din][tid] = (__bf16)((r0 + tid < rows) ? 1.f : 0.f);   // bias channel
-#pragma unroll
-    for (int i = 0; i < HG; ++i) {
-      const int g = (tid + 256 * i) * 4;
-      if (g < GR_ROWS * H) {
-        const int rr = g / H, k0 = g % H;
-        const long r = r0 + rr;
-        const float m = (r < rows && r % period >= hshift) ? 1.f : 0.f;
-        hT[k0 + 0][rr] = (__bf16)(rh[i].x * m);
-        hT[k0 + 1][rr] = (__bf16)(rh[i].y * m);
-        hT[k0 + 2][rr] = (__bf16)(rh[i].z * m);
-        hT[k0 + 3][rr] = (__bf16)(rh[i].w * m);
-      }
-    }
-  };
-
-  if (nmine > 0) load_tile(split);
-  for (long i = 0; i < nmine; ++i) {
-    const long tile = split + i * splits;
-    lds_barrier();                                // previous tile's LDS reads are done
-    stage_tile(tile);
-    load_tile(min(tile + splits, ntiles - 1));    // prefetch (the last one is a harmless reload)
-    lds_barrier();
-    // ---- dW^T (wave w: gate-units [16w,16w+16) of the block) and dU^T
-    const bf16x8_t az = *reinterpret_cast<const bf16x8_t*>(&dzT[16 * w + col][8 * quad]);
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xT[16 * d + col][8 * quad]);
-      accW[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az, bx, accW[d], 0, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < HT; ++k) {
-      const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hT[16 * k + col][8 * quad]);
-      accU[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az, bh, accU[k], 0, 0, 0);
-    }
-    // ---- dx^T tiles: item = (din tile, row tile)
-    if (dx != nullptr) {
-      const long r0 = tile * GR_ROWS;
-#pragma unroll
-      for (int ii = 0; ii < (DXT + 3) / 4; ++ii) {
-        const int item = w + 4 * ii;
-        if (item < DXT) {   // wave-uniform
-          const int dtile = item >> 1, rt = item & 1;
-          f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&dzR[16 * rt + col][32 * ks + 8 * quad]);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ii][ks], bz, acc, 0, 0, 0);
-          }
-          const long r = r0 + 16 * rt + col;
-          if (r < rows) {
-            float* o = dx + cb * dx_cb_stride + (size_t)r * lddx;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int din = dtile * 16 + 4 * quad + q;
-              if (din < lddx) o[din] = acc[q];   // columns Din .. lddx-1: zero (W rows masked)
-            }
-          }
-        }
-      }
-    }
-  }
-  // ---- partial tiles -> workspace record of this workgroup, fragment order (float4 per lane)
-  float* rec = ws + ((size_t)split * gridDim.x + cb) * (size_t)(DT + HT) * 1024;
-#pragma unroll
-  for (int d = 0; d < DT; ++d)
-    *reinterpret_cast<f32x4_t*>(rec + ((size_t)(d * 4 + w) * 64 + lane) * 4) = accW[d];
-#pragma unroll
-  for (int k = 0; k < HT; ++k)
-    *reinterpret_cast<f32x4_t*>(rec + ((size_t)((DT + k) * 4 + w) * 64 + lane) * 4) = accU[k];
-}
-
-// Reduction of the per-split records in a fixed order (deterministic):
-//   reduce: workgroup = 16 consecutive record slots x 16 split lanes (x NG split groups in
-//           grid.y); split lane l of group g sums splits g*16 + l, + 16*NG, ...; the 16 lane
-//           partials are combined through LDS. With NG == 1 (up to 512 splits) the result is
-//           added to the gradient buffers directly, else it goes to ws2[g][slot] and
-//   final:  thread = record slot sums its NG group sums and adds them.
-// Adding: one writer per element, plain read-modify-write into dW [Din,4H] / db / dU [H,4H].
-__device__ __forceinline__ void grads_add(float s, int e, int ncb, int DT, int HT, int Din, int H,
-                                          float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dU) {
-  const int R = (DT + HT) * 1024;
-  const int G4 = 4 * H;
-  // record layout: [split][cb][DT + HT fragments][4 waves][64 lanes][4]
-  const int cb = e / R, slot = e % R;
-  const int q = slot & 3, lane = (slot >> 2) & 63, w = (slot >> 8) & 3, j = slot >> 10;
-  const int colr = lane & 15, quad = lane >> 4;
-  const int gu = cb * GR_CB + 16 * w + 4 * quad + q;
-  if (j < DT) {
-    const int din = 16 * j + colr;
-    if (din < Din) dW[(size_t)din * G4 + gu] += s;
-    else if (din == Din) db[gu] += s;
-  } else {
-    const int k = 16 * (j - DT) + colr;
-    if (k < H) dU[(size_t)k * G4 + gu] += s;
-  }
+  lstm_grads_body<H, DT, GRX>(dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride, lddx, xg,
+                              x_elems, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
 }
 
 __global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __restrict__ ws, int splits, int RC,
                                                                 float* __restrict__ ws2, int ncb, int DT, int HT,
                                                                 int Din, int H, float* __restrict__ dW,
                                                                 float* __restrict__ db, float* __restrict__ dU) {
-  // 16 consecutive slots (64 B per split row) x 16 split lanes (measured faster than 8 x 32)
-  __shared__ float red[16][17];
-  const int sl = threadIdx.x & 15, l = threadIdx.x >> 4;
-  const int slot = min(blockIdx.x * 16 + sl, RC - 1);
-  const int g = blockIdx.y, NG = gridDim.y;
-  const int stride = 16 * NG;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int sp = g * 16 + l;
-  for (; sp + 3 * stride < splits; sp += 4 * stride) {
-    a0 += ws[(size_t)sp * RC + slot];
-    a1 += ws[(size_t)(sp + stride) * RC + slot];
-    a2 += ws[(size_t)(sp + 2 * stride) * RC + slot];
-    a3 += ws[(size_t)(sp + 3 * stride) * RC + slot];
-  }
-  for (; sp < splits; sp += stride) a0 += ws[(size_t)sp * RC + slot];
-  red[l][sl] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (threadIdx.x < 16 && blockIdx.x * 16 + sl < RC) {
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s += red[k][sl];
-    if (NG == 1) grads_add(s, slot, ncb, DT, HT, Din, H, dW, db, dU);
-    else ws2[(size_t)g * RC + slot] = s;
-  }
+  lstm_grads_reduce_body(ws, splits, RC, ws2, ncb, DT, HT, Din, H, dW, db, dU, blockIdx.x, blockIdx.y, gridDim.y);
 }
 
 __global__ __launch_bounds__(256) void lstm_grads_reduce_final_kernel(const float* __restrict__ ws2, int NG, int RC,
@@ -362,16 +122,17 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
 // leave as one float4. All 4H gate-units are contracted in one workgroup: no per-column-
 // block slabs and no slab sum. Used when the weight-gradient pass runs on a side stream
 // (off the critical path) while this kernel feeds the next layer's recurrence.
-template <int H, int NDT>          // NDT: 16-wide din tiles per wave
+template <int H, int RW, int NDT>   // RW: waves sharing one 16-row tile; NDT: 16-wide din tiles per wave
 __global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ dz, const float* __restrict__ W,
                                                       float* __restrict__ dx, long rows, int Dw, int lddx) {
-  constexpr int G4 = 4 * H, KS = G4 / 32;
+  constexpr int G4 = 4 * H, KS = G4 / 32, TPB = 4 / RW;     // row tiles per workgroup pass
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, quad = lane >> 4;
+  const int wr = w / RW, wd = w % RW;                       // row-tile slot, din-tile phase
   bf16x8_t wa[NDT][KS];
 #pragma unroll
   for (int d = 0; d < NDT; ++d) {
-    const int din = 16 * (w + 4 * d) + col;
+    const int din = 16 * (wd + RW * d) + col;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const float4 a = *reinterpret_cast<const float4*>(W + (size_t)min(din, Dw - 1) * G4 + 32 * ks + 8 * quad);
@@ -382,7 +143,7 @@ __global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ 
     }
   }
   const long ntiles = (rows + 15) / 16;
-  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  for (long t = (long)blockIdx.x * TPB + wr; t < ntiles; t += (long)gridDim.x * TPB) {
     const long r = t * 16 + col;
     const long rc = min(r, rows - 1);
     bf16x8_t bz[KS];
@@ -395,7 +156,7 @@ __global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ 
     }
 #pragma unroll
     for (int d = 0; d < NDT; ++d) {
-      const int din0 = 16 * (w + 4 * d) + 4 * quad;
+      const int din0 = 16 * (wd + RW * d) + 4 * quad;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[d][ks], bz[ks], acc, 0, 0, 0);
@@ -413,17 +174,22 @@ __global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ 
 }
 
 // dz: [>= rows, 4H] fp32 rows; W: [Dw, 4H]; out: [rows, lddx] (lddx >= Dw, multiple of 4).
+// Narrow inputs (1-2 din tiles) give each wave its own row tile instead of a din tile that
+// is then thrown away: no redundant dz loads, 2-4 row tiles per workgroup pass.
 void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, int Dw, int lddx, hipStream_t st) {
   if (rows == 0) return;
   const int ndin = (lddx + 15) / 16;
-  const int ndt = (ndin + 3) / 4;
-  const long ntiles = (rows + 15) / 16;
-  const int grid = (int)std::max<long>(1, std::min<long>(ntiles, 2048));
-#define GQ_DX(HH, ND) hipLaunchKernelGGL((lstm_dx_kernel<HH, ND>), dim3(grid), dim3(256), 0, st, dz, W, dx, rows, Dw, lddx)
-#define GQ_DX_H(HH)                                                         \
-  case HH:                                                                  \
-    if (ndt == 1) GQ_DX(HH, 1); else if (ndt == 2) GQ_DX(HH, 2);           \
-    else TORCH_CHECK(false, "lstm_dx: input width ", lddx, " > 128");       \
+  TORCH_CHECK(ndin <= 8, "lstm_dx: input width ", lddx, " > 128");
+  const int rw = ndin >= 3 ? 4 : ndin;
+  const int ndt = (ndin + rw - 1) / rw;
+  const long ngroups = ((rows + 15) / 16 + (4 / rw) - 1) / (4 / rw);
+  const int grid = (int)std::max<long>(1, std::min<long>(ngroups, 2048));
+#define GQ_DX(HH, RWV, ND) \
+  hipLaunchKernelGGL((lstm_dx_kernel<HH, RWV, ND>), dim3(grid), dim3(256), 0, st, dz, W, dx, rows, Dw, lddx)
+#define GQ_DX_H(HH)                                                                            \
+  case HH:                                                                                     \
+    if (rw == 1) GQ_DX(HH, 1, 1); else if (rw == 2) GQ_DX(HH, 2, 1);                           \
+    else if (ndt == 1) GQ_DX(HH, 4, 1); else GQ_DX(HH, 4, 2);                                  \
     break;
   switch (H) {
     GQ_DX_H(16) GQ_DX_H(32) GQ_DX_H(64) GQ_DX_H(128)

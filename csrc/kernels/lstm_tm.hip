@@ -26,6 +26,7 @@
 //                VGPRs for the whole sequence and flushed once with atomics.
 // So dz never goes to HBM and no separate weight-gradient kernel runs.
 #include "common.h"
+#include "lstm_grads_body.h"
 
 namespace gq {
 
@@ -423,10 +424,10 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
 //   DX: dx^T = W dz_t^T tile -> HBM (frozen-weight input gradients, e.g. integrated gradients).
 // dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
 template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
-__global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
+__device__ __forceinline__ void lstm_tm_bwd_body(
     const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
-    int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P) {
+    int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P, int tile, int ntiles) {
   // UNPOOL: dhout is the gradient of the fused MaxPooling1D output [T/P][Mp][H] and pidx its
   // argmax bytes; the scatter back to [T][Mp][H] happens as the dh tiles are staged
   using C = TMC<H>;
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in an SGPR
   const int col = lane & 15, quad = lane >> 4;
-  const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
+  const int row0 = tile * 16;
 
   for (int i = tid; i < 2 * 16 * C::HP; i += NT) (&dhs[0][0][0])[i] = 0.f;
 
@@ -641,6 +642,15 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 #undef GQ_TMB_LOAD_D
 }
 
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
+__global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
+    const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
+    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
+    int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P) {
+  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, UNPOOL>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, pidx, P,
+                                                       blockIdx.x, gridDim.x);
+}
+
 // =====================================================================================
 // backward of a layer PAIR (A: Din -> H, B: H -> H), wavefront-pipelined like the pair
 // forward: waves [0, NW) run B's reverse recurrence at time t = T-1-s, waves [NW, 2 NW) run
@@ -806,6 +816,65 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
   }
 #undef GQ_TM2B_STATE
 #undef GQ_TM2B_D
+}
+
+// =====================================================================================
+// Horizontal fusion of the backward: one launch = the reverse recurrence of layer L (the
+// serial critical path, workgroups [0, ntiles)) + the weight-gradient pass of the layer
+// processed just before it (extra 256-thread workgroups) + the split reduction of the layer
+// before that. The weight-gradient work used to run after each recurrence on the same
+// stream; here it fills the idle CUs while the next recurrence runs (separate streams were
+// measured slower: cross-stream event waits). Extra waves of a recurrence-sized workgroup
+// exit at once (s_barrier only counts live waves).
+static constexpr int PIPE_RED_KB = 8;     // slot blocks per reduce workgroup (lstm_grads_reduce_multi)
+
+struct GradJob {
+  const float* dz;
+  const float* x;
+  const float* h;
+  const float* W;
+  float* ws;
+  long rows, period, hshift, x_elems;
+  int Din, ldx, xg, ncb, splits, nblocks;
+};
+
+struct RedJob {
+  const float* ws;
+  float* dW;
+  float* db;
+  float* dU;
+  int splits, RC, ncb, DT, HT, Din, H, nblocks, kb;
+};
+
+template <int HR, int HG, int DT>
+__global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
+    const float* __restrict__ dh, const float* __restrict__ g, const float* __restrict__ c,
+    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dz, int Mp, int T, int Dw,
+    int ntiles, GradJob gj, RedJob rj) {
+  constexpr int D = HR >= 64 ? 2 : 4;
+  const int b = blockIdx.x;
+  if (b < ntiles) {
+    lstm_tm_bwd_body<HR, 1, 1, D, true, false, false, false>(dh, g, c, W, U, nullptr, dz, Mp, T, Dw, Dw, nullptr, 1,
+                                                             b, ntiles);
+    return;
+  }
+  if (threadIdx.x >= 256) return;
+  const int gb = b - ntiles;
+  if (gb < gj.nblocks) {
+    if constexpr (HG > 0)
+      lstm_grads_body<HG, DT, 4>(gj.dz, gj.x, gj.h, gj.W, nullptr, gj.ws, gj.rows, gj.period, gj.hshift, gj.Din,
+                                 gj.ldx, 0, gj.Din, gj.xg, gj.x_elems, gb % gj.ncb, gb / gj.ncb, gj.ncb, gj.splits);
+    return;
+  }
+  const int rb = gb - gj.nblocks;
+  if (rb < rj.nblocks) {
+    if (rj.kb > 1)     // many slots: KB slot blocks per workgroup
+      lstm_grads_reduce_multi<PIPE_RED_KB>(rj.ws, rj.splits, rj.RC, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
+                                           rj.dU, rb);
+    else               // few slots, many splits: one slot block per workgroup, 4 add chains per lane
+      lstm_grads_reduce_body(rj.ws, rj.splits, rj.RC, nullptr, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
+                             rj.dU, rb, 0, 1);
+  }
 }
 
 // =====================================================================================
@@ -1055,6 +1124,148 @@ at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::T
   return dz;
 }
 
+// ---- pipelined backward (see lstm_tm_bwd_dual_kernel)
+static constexpr int PIPE_MAX_SPLITS = 512;     // one reduction group: the reduce fits one launch
+
+// workspace of a pending weight-gradient job: [splits][ncb][(DT + HT) fragments][1024] fp32
+at::Tensor lstm_grads_job_ws(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& W, int64_t H) {
+  check_f32_cuda(W, "W");
+  const int Dw = (int)W.size(0);
+  const long rows = x.numel() / x.size(-1);
+  const int ncb = lstm_grads_col_blocks((int)H);
+  const long ntiles = (rows + 31) / 32;
+  const int splits = (int)std::max<long>(1, std::min<long>({(ntiles + 1) / 2, (long)std::max(64, 2048 / ncb),
+                                                            (long)PIPE_MAX_SPLITS}));
+  const int DT = (Dw + 1 + 15) / 16, HT = (int)H / 16;
+  c10::DeviceGuard guard(x.device());
+  return at::empty({(long)splits * ncb * (DT + HT) * 1024}, x.options());
+}
+
+static bool grads_job_ok(const at::Tensor& x, int Dw) {
+  const int ldx = (int)x.stride(-2);
+  return ldx % 4 == 0 && ldx >= Dw && ldx <= 144 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+         (Dw + 1 + 15) / 16 <= 5 && x.stride(-1) == 1;
+}
+
+// rec: dh [T, Mp, H] (empty: no recurrence); job (gz empty: none): dz / x / h / W of the layer
+// whose weight gradients to compute, with its row mapping (period, hshift) and workspace;
+// reduce (rws empty: none): a job whose gradient pass already ran. Returns the rec's dz.
+at::Tensor lstm_tm_bwd_pipe(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& W,
+                            const at::Tensor& U, int64_t T, const at::Tensor& gz, const at::Tensor& gx,
+                            const at::Tensor& gh, const at::Tensor& gW, int64_t g_period, int64_t g_hshift,
+                            const at::Tensor& gws, const at::Tensor& rws, const at::Tensor& rW, at::Tensor rdW,
+                            at::Tensor rdU, at::Tensor rdb) {
+  const bool rec = dh.numel() > 0, job = gz.numel() > 0, red = rws.numel() > 0;
+  const at::Tensor& ref = rec ? dh : (job ? gz : rws);
+  c10::DeviceGuard guard(ref.device());
+  int HR = 16, Mp = 0, ntiles = 0, Dw = 1;
+  at::Tensor dz = at::empty({0}, ref.options());
+  if (rec) {
+    for (const at::Tensor* t : {&dh, &g, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_pipe operand");
+    HR = (int)U.size(0);
+    Mp = (int)dh.size(1);
+    TORCH_CHECK(dh.dim() == 3 && dh.size(0) == T && dh.size(2) == HR && Mp % 16 == 0, "lstm_tm_bwd_pipe: dh shape");
+    TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * HR * 4 && c.numel() == (long)(T + 1) * Mp * HR,
+                "lstm_tm_bwd_pipe: saved state shapes");
+    TORCH_CHECK(HR == 16 || HR == 32 || HR == 64, "lstm_tm_bwd_pipe: hidden size");
+    ntiles = Mp / 16;
+    Dw = (int)W.size(0);
+    dz = at::empty({T + 1, Mp, 4 * HR}, dh.options());
+  }
+  GradJob gj{};
+  int HG = 0, DTG = 1;
+  if (job) {
+    for (const at::Tensor* t : {&gz, &gh, &gW, &gws}) check_f32_cuda(*t, "lstm_tm_bwd_pipe job operand");
+    TORCH_CHECK(gx.is_cuda() && gx.scalar_type() == at::kFloat, "lstm_tm_bwd_pipe: job x");
+    HG = (int)gW.size(1) / 4;
+    const int gDw = (int)gW.size(0);
+    TORCH_CHECK(grads_job_ok(gx, gDw), "lstm_tm_bwd_pipe: job x layout");
+    DTG = (gDw + 1 + 15) / 16;
+    gj.dz = gz.data_ptr<float>();
+    gj.x = gx.data_ptr<float>();
+    gj.h = gh.data_ptr<float>();
+    gj.W = gW.data_ptr<float>();
+    gj.ws = gws.data_ptr<float>();
+    gj.ldx = (int)gx.stride(-2);
+    gj.rows = gx.numel() / gx.size(-1);
+    gj.period = g_period;
+    gj.hshift = g_hshift;
+    gj.x_elems = (long)(gx.storage().nbytes() / sizeof(float)) - gx.storage_offset();
+    gj.Din = gDw;
+    gj.xg = (int)((32L * gj.ldx / 4 + 255) / 256);
+    gj.ncb = lstm_grads_col_blocks(HG);
+    const long RC = (long)(DTG + HG / 16) * 1024 * gj.ncb;
+    gj.splits = (int)(gws.numel() / RC);
+    TORCH_CHECK(gj.splits >= 1 && gj.splits <= PIPE_MAX_SPLITS && gws.numel() == gj.splits * RC,
+                "lstm_tm_bwd_pipe: job workspace size");
+    gj.nblocks = gj.ncb * gj.splits;
+  }
+  RedJob rj{};
+  if (red) {
+    for (const at::Tensor* t : {&rws, &rW}) check_f32_cuda(*t, "lstm_tm_bwd_pipe reduce operand");
+    for (at::Tensor* t : {&rdW, &rdU, &rdb}) check_f32_cuda(*t, "lstm_tm_bwd_pipe reduce gradient");
+    rj.H = (int)rW.size(1) / 4;
+    rj.Din = (int)rW.size(0);
+    rj.DT = (rj.Din + 1 + 15) / 16;
+    rj.HT = rj.H / 16;
+    rj.ncb = lstm_grads_col_blocks(rj.H);
+    rj.RC = (rj.DT + rj.HT) * 1024 * rj.ncb;
+    rj.splits = (int)(rws.numel() / rj.RC);
+    TORCH_CHECK(rj.splits >= 1 && rj.splits <= PIPE_MAX_SPLITS && rws.numel() == (long)rj.splits * rj.RC,
+                "lstm_tm_bwd_pipe: reduce workspace size");
+    TORCH_CHECK(rdW.numel() == rW.numel() && rdU.numel() == (long)rj.H * 4 * rj.H && rdb.numel() == 4 * rj.H,
+                "lstm_tm_bwd_pipe: reduce gradient buffers");
+    rj.ws = rws.data_ptr<float>();
+    rj.dW = rdW.data_ptr<float>();
+    rj.dU = rdU.data_ptr<float>();
+    rj.db = rdb.data_ptr<float>();
+    // the wide form once the one-block-per-16-slots grid would exceed a few waves of workgroups
+    rj.kb = (rj.RC + 15) / 16 > 1024 ? PIPE_RED_KB : 1;
+    rj.nblocks = (rj.RC + 16 * rj.kb - 1) / (16 * rj.kb);
+  }
+  const int nblk = ntiles + gj.nblocks + rj.nblocks;
+  if (nblk == 0) return dz;
+  TORCH_CHECK(!job || HG == HR || HG == 2 * HR || !rec, "lstm_tm_bwd_pipe: job hidden size must be H or 2H of the rec");
+  const float* P[5] = {rec ? dh.data_ptr<float>() : nullptr, rec ? g.data_ptr<float>() : nullptr,
+                       rec ? c.data_ptr<float>() : nullptr, rec ? W.data_ptr<float>() : nullptr,
+                       rec ? U.data_ptr<float>() : nullptr};
+  float* dzp = rec ? dz.data_ptr<float>() : nullptr;
+  auto st = stream();
+#define GQ_PIPE_LAUNCH(HRV, HGV, DTV)                                                                          \
+  hipLaunchKernelGGL((lstm_tm_bwd_dual_kernel<HRV, HGV, DTV>), dim3(nblk), dim3(TMC<HRV>::NT), 0, st, P[0], P[1],  \
+                     P[2], P[3], P[4], dzp, Mp, (int)T, Dw, ntiles, gj, rj)
+#define GQ_PIPE_DT(HRV, HGV)                                                                                   \
+  switch (DTG) {                                                                                               \
+    case 1: GQ_PIPE_LAUNCH(HRV, HGV, 1); break;                                                                \
+    case 2: GQ_PIPE_LAUNCH(HRV, HGV, 2); break;                                                                \
+    case 3: GQ_PIPE_LAUNCH(HRV, HGV, 3); break;                                                                \
+    case 4: GQ_PIPE_LAUNCH(HRV, HGV, 4); break;                                                                \
+    default: GQ_PIPE_LAUNCH(HRV, HGV, 5); break;                                                               \
+  }
+#define GQ_PIPE_H(HRV)                                                                                         \
+  if (!job) GQ_PIPE_LAUNCH(HRV, 0, 1);                                                                         \
+  else if (HG == HRV) { GQ_PIPE_DT(HRV, HRV) }                                                                 \
+  else { GQ_PIPE_DT(HRV, 2 * HRV) }
+  if (!rec) {                   // flush launch: 256-thread workgroups; job of any hidden size
+    if (!job) GQ_PIPE_LAUNCH(16, 0, 1);
+    else if (HG == 16) { GQ_PIPE_DT(16, 16) }
+    else if (HG == 32) { GQ_PIPE_DT(16, 32) }
+    else if (HG == 64) { GQ_PIPE_DT(32, 64) }
+    else { GQ_PIPE_DT(64, 128) }
+  } else if (HR == 16) {
+    GQ_PIPE_H(16)
+  } else if (HR == 32) {
+    GQ_PIPE_H(32)
+  } else {
+    GQ_PIPE_H(64)
+  }
+#undef GQ_PIPE_H
+#undef GQ_PIPE_DT
+#undef GQ_PIPE_LAUNCH
+  GQ_LAUNCH_CHECK();
+  return dz;
+}
+
 // Weight gradients (+ dx) of one time-major layer from its dz (lstm_grads_rows): accumulates
 // dW, dU, db; returns dx [T, Mp, Din] if need_dx.
 at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
@@ -1148,5 +1359,7 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_tm2_bwd", &gq::lstm_tm2_bwd);
   m.impl("lstm_tm_grads", &gq::lstm_tm_grads);
   m.impl("lstm_tm_bwd_dz", &gq::lstm_tm_bwd_dz);
+  m.impl("lstm_tm_bwd_pipe", &gq::lstm_tm_bwd_pipe);
+  m.impl("lstm_grads_job_ws", &gq::lstm_grads_job_ws);
   m.impl("lstm_tm_bwd", &gq::lstm_tm_bwd);
 }

@@ -34,6 +34,10 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_tm_bwd_dz(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T, Tensor? pool_idx=None, "
         "int pool=0) -> Tensor");
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
+  m.def("lstm_tm_bwd_pipe(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T, Tensor gz, Tensor gx, "
+        "Tensor gh, Tensor gW, int g_period, int g_hshift, Tensor gws, Tensor rws, Tensor rW, Tensor(a!) rdW, "
+        "Tensor(b!) rdU, Tensor(c!) rdb) -> Tensor");
+  m.def("lstm_grads_job_ws(Tensor dz, Tensor x, Tensor W, int H) -> Tensor");
   m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor(a!) dW, "
         "Tensor(b!) dU, Tensor(c!) db, bool need_dx, Tensor? pool_idx=None, int pool=0) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)

@@ -65,14 +65,18 @@ class _DirectGrad:
 
 
 def _split_mode() -> str:
-    """Backward of a direct-accumulation LSTM layer: ``fused`` (default: one weight-gradient
-    kernel also producing dx), ``split`` (dx kernel + weight-gradient kernel, one stream) or
-    ``side`` (weight gradients on a side stream). Env ``GNNQC_LSTM_BWD``.
+    """Backward of a direct-accumulation LSTM layer: ``pipe`` (default: weight gradients of
+    each layer fused behind the next layer's recurrence, see :class:`_Pipe`; layers with
+    large recurrence grids keep ``fused``), ``fused`` (recurrence, then one weight-gradient
+    kernel also producing dx, then the split reduction), ``split`` (dx kernel +
+    weight-gradient kernel, one stream) or ``side`` (weight gradients on a side stream).
+    Env ``GNNQC_LSTM_BWD``.
 
-    Measured on MI355X (CML bench, ms/step, HIP graph / eager): fused 0.757 / 1.238,
-    side 0.885 / 2.037 - cross-stream event waits cost more than the overlap wins here."""
+    Measured on MI355X (CML bench, ms/step, HIP graph / eager): pipe 0.667 / 0.985,
+    fused 0.709 / 0.986; earlier: fused 0.757 / 1.238 vs side 0.885 / 2.037 - cross-stream
+    event waits cost more than the overlap wins here."""
     import os
-    return os.environ.get("GNNQC_LSTM_BWD", "fused")
+    return os.environ.get("GNNQC_LSTM_BWD", "pipe")
 
 
 def _side_stream(device: torch.device):
@@ -110,6 +114,98 @@ def _off_critical_path(device: torch.device, tensors, fn):
     _DirectGrad.pending.add(device.index if device.index is not None else torch.cuda.current_device())
 
 
+class _Pipe:
+    """Pipelined backward (``GNNQC_LSTM_BWD=pipe``, direct-accumulation mode only).
+
+    A layer's weight-gradient pass does not feed any later recurrence, so it is deferred:
+    each time-major backward recurrence launches ONE kernel (``lstm_tm_bwd_pipe``) whose
+    first workgroups run the recurrence (a handful of tiles - most CUs idle) while the
+    remaining workgroups run the weight-gradient pass of the previously finished layer and
+    the split reduction of the one before. dx of the layer is a separate small kernel
+    (the next recurrence's input). Leftover work is flushed when the direct-accumulation
+    context exits. Single stream: ordering is plain stream order, no events."""
+
+    job = None      # layer whose weight-gradient pass has not run yet
+    red = None      # layer whose gradient pass ran; its split reduction has not
+
+
+# Largest sequence count (rows of 16-sequence tiles) a recurrence may have for its layer to
+# join the pipe: the gradient workgroups only help when the recurrence leaves most CUs idle
+# (CML: 8 tiles). With hundreds of tiles (SoilNet: 418) they compete with the recurrence
+# for the CUs and the step got slower (6.11 vs 5.15 ms), so such layers keep the fused path.
+PIPE_MAX_SEQ = 2048
+
+
+def _pipe_on(sinks, n_seq: int) -> bool:
+    return (_DirectGrad.enabled and _split_mode() == "pipe" and all(d for _, d in sinks)
+            and n_seq <= PIPE_MAX_SEQ)
+
+
+def _pipe_job(dz, x, h, W, sinks, period: int, hshift: int):
+    from ..utils.native import hip_ops
+    H = W.shape[1] // 4
+    return dict(dz=dz, x=x, h=h, W=W, period=int(period), hshift=int(hshift),
+                ws=hip_ops().lstm_grads_job_ws(dz, x, W, H), g=[s for s, _ in sinks])
+
+
+def _pipe_launch(dh=None, g=None, c=None, W=None, U=None, T: int = 0, job=None, red=None):
+    """One pipe kernel: [recurrence] + [grads of ``job``] + [reduce of ``red``]. Returns dz."""
+    from ..utils.native import hip_ops
+    ref = dh if dh is not None else (job or red)["dz"]
+    e = ref.new_zeros(0)
+    rec = (dh, g, c, W, U) if dh is not None else (e, e, e, e, e)
+    jb = (job["dz"], job["x"], job["h"], job["W"], job["period"], job["hshift"], job["ws"]) if job else \
+        (e, e, e, e, 1, 1, e)
+    rd = (red["ws"], red["W"], *red["g"]) if red else (e, e, e, e, e)
+    return hip_ops().lstm_tm_bwd_pipe(*rec, int(T), *jb, *rd)
+
+
+def _pipe_drain_one():
+    """Advance the pending jobs by one stage without a recurrence."""
+    job, red = _Pipe.job, _Pipe.red
+    if job is None and red is None:
+        return
+    _pipe_launch(job=job, red=red)
+    _Pipe.job, _Pipe.red = None, job
+
+
+def pipe_flush():
+    """Run all pending weight-gradient / reduction work (end of the backward)."""
+    while _Pipe.job is not None or _Pipe.red is not None:
+        _pipe_drain_one()
+
+
+def _pipe_push(job):
+    """Queue ``job``: if a job is still pending (no recurrence consumed it), advance first."""
+    if _Pipe.job is not None:
+        _pipe_drain_one()
+    _Pipe.job = job
+
+
+def _pipe_tm_backward(dh, g, c, x, h, W, U, sinks, need_dx):
+    """Time-major layer backward in pipe mode: one pipe launch (recurrence + pending grads +
+    pending reduce), dx = dz W^T, then this layer's own weight-gradient job is queued."""
+    from ..utils.native import hip_ops
+    T, Mp = x.shape[0], x.shape[1]
+    HR = U.shape[0]
+    if dh.dim() == 2:        # gradient only at the last step
+        dh = torch.nn.functional.pad(dh.unsqueeze(0), (0, 0, 0, 0, T - 1, 0))
+    job, red = _Pipe.job, _Pipe.red
+    if job is not None and job["W"].shape[1] // 4 not in (HR, 2 * HR):
+        _pipe_drain_one()              # shape the fused kernel does not take: run it alone
+        job, red = _Pipe.job, _Pipe.red
+    dz = _pipe_launch(dh, g, c, W, U, T, job, red)
+    _Pipe.job, _Pipe.red = None, job
+    dx = hip_ops().lstm_dx(dz, W, x) if need_dx else None
+    _pipe_push(_pipe_job(dz, x, h, W, sinks, T * Mp, Mp))
+    return dx
+
+
+def _pipe_x_ok(x: torch.Tensor, Dw: int) -> bool:
+    return (x.stride(-1) == 1 and x.stride(-2) % 4 == 0 and x.data_ptr() % 16 == 0 and (Dw + 16) // 16 <= 5
+            and x.shape[-1] % 4 == 0)
+
+
 @contextlib.contextmanager
 def direct_grad_accumulation(flag: bool = True):
     prev = _DirectGrad.enabled
@@ -118,6 +214,8 @@ def direct_grad_accumulation(flag: bool = True):
         yield
     finally:
         _DirectGrad.enabled = prev
+        if _Pipe.job is not None or _Pipe.red is not None:
+            pipe_flush()
         if _DirectGrad.pending and torch.cuda.is_available():
             join_side_streams()
 
@@ -180,7 +278,12 @@ class _HipLSTM(torch.autograd.Function):
         gb, db_in = _grad_sink(bp)
         need_dx = bool(ctx.needs_input_grad[0])
         Wc = W.contiguous()
-        if dW_in and dU_in and db_in and _split_mode() != "fused" and x.shape[-1] % 4 == 0:
+        if (dW_in and dU_in and db_in and _pipe_on(((gW, True),), M) and _pipe_x_ok(x, W.shape[0])):
+            # sequence-major recurrence (H = 128); the weight-gradient job joins the pipe
+            dx = ops.lstm_dx(dz, Wc, x) if need_dx else None
+            _pipe_push(_pipe_job(dz, x, h, Wc, ((gW, True), (gU, True), (gb, True)), T, 1))
+            return dx, None, None, None, None, None
+        if dW_in and dU_in and db_in and _split_mode() not in ("fused", "pipe") and x.shape[-1] % 4 == 0:
             # critical path: dx only; dW/dU/db on the side stream
             dx = ops.lstm_dx(dz, Wc, x) if need_dx else None
             _off_critical_path(dz.device, (dz, x, h, Wc),
@@ -244,7 +347,9 @@ class _HipLSTMTM(torch.autograd.Function):
             e = x.new_zeros(0)
             sinks = [(e, True)] * 3
         pi = pidx if pool else None
-        if wgrad and all(d for _, d in sinks) and _split_mode() != "fused":
+        if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+            dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
+        elif wgrad and all(d for _, d in sinks) and _split_mode() not in ("fused", "pipe"):
             dx = _tm_split_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx,
                                     pi, pool)
         else:
@@ -303,8 +408,12 @@ class _HipLSTMTMPair(torch.autograd.Function):
                                         UA.contiguous())
             ops.lstm_tm_grads(dzB, hA, hB, WB.contiguous(), sB[0][0], sB[1][0], sB[2][0], False)
             dx = ops.lstm_tm_grads(dzA, x, hA, WA.contiguous(), sA[0][0], sA[1][0], sA[2][0], need_dx)
+        elif (any(need[4:7]) and any(need[1:4]) and not pool and _pipe_on(sB, x.shape[1]) and _pipe_on(sA, x.shape[1])
+              and _pipe_x_ok(x, WA.shape[0]) and _pipe_x_ok(hA, WB.shape[0])):
+            dhA = _pipe_tm_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
+            dx = _pipe_tm_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         elif (any(need[4:7]) and all(d for _, d in sB) and any(need[1:4]) and all(d for _, d in sA)
-              and _split_mode() != "fused"):
+              and _split_mode() not in ("fused", "pipe")):
             dhA = _tm_split_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True, pi, pool)
             dx = _tm_split_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:

@@ -65,6 +65,23 @@ def test_lstm_direct_grad_accumulation_and_padded_rows(cuda_device, Din, H):
         assert err < 5e-2, f"{name}: {err}"
 
 
+@pytest.mark.parametrize("H", [16, 32, 64, 128])
+@pytest.mark.parametrize("Dw,lddx", [(16, 16), (18, 20), (32, 32), (40, 44), (64, 64), (100, 100)])
+def test_lstm_dx_matches_matmul(cuda_device, H, Dw, lddx):
+    """Standalone dx = dz W^T kernel (all row-tile / din-tile layouts) vs an fp32 matmul of the
+    bf16-rounded operands; layout-padding columns come out as zeros."""
+    from gnnqc.utils.native import hip_ops
+    gen = torch.Generator().manual_seed(H + Dw)
+    rows = 16 * 37 + 5
+    dz = torch.randn(rows + 3, 4 * H, generator=gen).to(cuda_device)
+    W = torch.randn(Dw, 4 * H, generator=gen).to(cuda_device) * 0.2
+    like = torch.empty(rows, lddx, device=cuda_device)
+    dx = hip_ops().lstm_dx(dz, W, like)
+    ref = dz[:rows].bfloat16().float() @ W.bfloat16().float().t()
+    torch.testing.assert_close(dx[:, :Dw], ref, atol=1e-3, rtol=1e-3)
+    assert torch.count_nonzero(dx[:, Dw:]).item() == 0
+
+
 def test_lstm_long_sequence_fp32_exact(cuda_device):
     from gnnqc.ops.lstm import _HipLSTM, lstm_eager
     gen = torch.Generator().manual_seed(3)
@@ -627,7 +644,7 @@ def test_batch_meta_matches_torch_gather(cuda_device, cml_windows, ds):
 
 
 @pytest.mark.parametrize("use_graph", [True, False])
-@pytest.mark.parametrize("mode", ["side", "split"])
+@pytest.mark.parametrize("mode", ["side", "split", "pipe"])
 def test_split_lstm_backward_matches_fused(cuda_device, cml_windows, monkeypatch, use_graph, mode):
     """Training steps with the weight-gradient passes on a side stream (graph branches when
     captured) == the same steps with everything on one stream."""
@@ -656,6 +673,37 @@ def test_split_lstm_backward_matches_fused(cuda_device, cml_windows, monkeypatch
     p0, l0 = run(False)
     assert abs(l1 - l0) < 2e-2 * abs(l0) + 1e-4, (l1, l0)
     assert (p1 - p0).norm().item() < 2e-3 * p0.norm().item()
+
+
+@pytest.mark.parametrize("ds", ["cml", "soilnet"])
+def test_pipe_lstm_backward_gradients(cuda_device, cml_windows, monkeypatch, ds):
+    """One backward with the pipelined LSTM backward (weight-gradient passes fused behind the
+    next layer's recurrence, flushed at context exit) == the fused per-layer backward, for
+    every parameter gradient."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops.lstm import _Pipe, direct_grad_accumulation
+    pc, ws = cml_windows if ds == "cml" else _soil_small_windows()
+    st = DeviceStore(ws, "rolling_median" if ds == "cml" else "scale_range", pc.graph, device=cuda_device)
+    torch.manual_seed(0)
+    model = GCNClassifier(C.default(f"model_{ds}"), pc).to(cuda_device)
+    b = st.gather(torch.arange(min(40, st.n_windows), device=cuda_device))
+    inputs = b.model_inputs(ds, False)
+
+    def run(mode):
+        monkeypatch.setenv("GNNQC_LSTM_BWD", mode)
+        for p in model.parameters():
+            p.grad = torch.zeros_like(p)
+        with direct_grad_accumulation(True):
+            model.logits(inputs).float().square().mean().backward()
+        assert _Pipe.job is None and _Pipe.red is None
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in model.parameters()]
+
+    g0, g1 = run("fused"), run("pipe")
+    for (n, _), a, r in zip(model.named_parameters(), g1, g0):
+        assert (a - r).norm().item() <= 1e-4 * r.norm().item() + 1e-7, n
 
 
 def test_cml_time_major_gcn_output_matches_batch_major(cuda_device, cml_windows, monkeypatch):
