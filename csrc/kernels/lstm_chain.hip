@@ -1,0 +1,395 @@
+// Cross-CU layer pipeline for the forward of a time-major LSTM stack (gfx950).
+//
+// The per-layer forward kernels (lstm_tm.hip) run one after another: with the CML batch a
+// recurrence occupies 8 of the 256 CUs, and the stack's six recurrences (plus three pool
+// launches) are a serial sum. Sequences never mix across layers, so tile j of layer k+1
+// only needs tile j of layer k - and only up to the step it is at. This kernel runs all
+// layers of the stack at once: workgroup (stage s, tile j) computes layer s of tile j on
+// its own CU and consumes layer s-1's output AS IT IS PRODUCED, a few steps behind.
+//
+// Hand-off (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility", R2
+// granules): the producer writes every output element a second time as an 8-byte
+// {value, tag} granule with an agent-scope (sc1, write-through) store; the consumer's
+// prefetch ring loads granules with agent-scope (sc1, L1-bypassing) loads and checks the
+// tag (launch epoch | time index) when it stages x_t into LDS; a wave whose granules are not
+// there yet re-polls (bounded; a timeout sets a flag instead of hanging). The producer
+// never waits, the consumer only when it catches up. An 8-byte granule is written and read
+// untorn, so no fence or flag ordering is needed.
+//
+// The launch epoch lives in device memory (ctl[0]) and is advanced by the last workgroup
+// to finish, so HIP-graph replays get fresh tags and stale granules of an earlier launch
+// at the same address never match. All workgroups must be co-resident (grid <= 256 of
+// 1024-thread workgroups, checked on the host): a consumer spins only on producers that
+// are already running. Workgroups of stage s for tile j have the same blockIdx % 8, so
+// under the observed round-robin placement one tile's whole stack shares an XCD (speed only).
+//
+// Each stage also writes everything the per-layer kernels write (h, gate / cell state for
+// the backward, the fused MaxPooling1D output + argmax bytes), so the backward is unchanged.
+#include "common.h"
+#include "lstm_tm_common.h"
+
+namespace gq {
+
+static constexpr int CHAIN_MAX = 8;
+static constexpr int CHAIN_SPIN = 1 << 20;
+
+struct ChainStage {
+  const float* x;                    // stage 0: fp32 input [T][Mp][Din]
+  const unsigned long long* xin;     // stages > 0: tagged input stream [T][Mp][Din]
+  const float* W;
+  const float* U;
+  const float* b;
+  float* h;                          // [T+1][Mp][H] (row T: scratch)
+  float* g;                          // train: [T+1][tiles][NW][CPL][64][4]
+  float* c;
+  unsigned long long* sout;          // tagged output stream [To][Mp][H] (nullptr: last stage)
+  float* pout;                       // pooled output [T/P][Mp][H] (P > 0)
+  unsigned* iout;
+  int H, T, Din, Dw, KX, P;
+};
+
+struct ChainArgs {
+  ChainStage st[CHAIN_MAX];
+  int ns, ntiles, nt8, Mp;
+  int* ctl;                          // [0] epoch, [1] finished workgroups, [2] spin timeout seen
+};
+
+__device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_granule(unsigned long long* p, float v, unsigned tag) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// slow path: the wave re-polls its granule until every lane sees the wanted tag
+__device__ __noinline__ unsigned long long chain_wait(const unsigned long long* p, unsigned want, int* ctl) {
+  unsigned long long v = 0;
+  for (int it = 0; it < CHAIN_SPIN; ++it) {
+    v = ld_granule(p);
+    if (__builtin_amdgcn_ballot_w64((unsigned)(v >> 32) != want) == 0) return v;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
+// One layer of one tile: lstm_tm_fwd_kernel's step loop with the x ring fed either from
+// global memory (stage 0) or from the previous stage's granule stream (SRC), and the
+// output (optionally max-pooled) also published as granules.
+template <int H, bool TRAIN, int KX, int D, bool SRC>
+__device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
+                                            int* ctl) {
+  using C = TMC<H>;
+  constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
+  constexpr int KPX = 32 * KX;
+  constexpr int GR = SRC ? 1 : 4;
+  __shared__ __attribute__((aligned(16))) __bf16 hs[2][16][C::KPH + 8];
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
+  __shared__ __attribute__((aligned(16))) float hf[2][16][C::HP];
+
+  const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, quad = lane >> 4;
+  const int row0 = tile * 16;
+
+  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += NT) (&hs[0][0][0])[i] = (__bf16)0.0f;
+  for (int i = tid; i < 2 * 16 * (KPX + 8); i += NT) (&xs[0][0][0])[i] = (__bf16)0.0f;
+
+  bf16x8_t ufr[CPL][C::KSH], wfr[CPL][KX];
+  f32x4_t bias4[CPL];
+  int unit[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) {
+    const int gi = w + NW * cc;
+    const int au = 4 * gi + (col >> 2), ag = col & 3;
+    unit[cc] = 4 * gi + quad;
+#pragma unroll
+    for (int s = 0; s < C::KSH; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(S.U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+      }
+      ufr[cc][s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
+      }
+      wfr[cc][s] = v;
+    }
+    const int u = unit[cc];
+    bias4[cc] = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
+  }
+
+  // x ring: granule (tid mod n_gx) of the contiguous [16][Din] tile (duplicates across lanes)
+  const int n_gx = 16 * Din / GR;
+  const int gx = (tid % n_gx) * GR;
+  const int gx_seq = gx / Din, gx_k = gx % Din;
+  const size_t xstep = (size_t)Mp * Din;
+  const size_t xoff = (size_t)row0 * Din + gx;
+  Granule<GR> xr[D];
+  unsigned long long xq[D];
+  auto load_x = [&](int j, int tx) {
+    if constexpr (SRC) xq[j] = ld_granule(S.xin + xoff + (size_t)tx * xstep);
+    else xr[j].load(S.x + xoff + (size_t)tx * xstep);
+  };
+  auto stage_x = [&](int buf, int j, int tx) {
+    if constexpr (SRC) {
+      const unsigned want = tagb | (unsigned)tx;
+      unsigned long long v = xq[j];
+      if (__builtin_amdgcn_ballot_w64((unsigned)(v >> 32) != want) != 0)
+        v = chain_wait(S.xin + xoff + (size_t)tx * xstep, want, ctl);
+      xs[buf][gx_seq][gx_k] = (__bf16)__uint_as_float((unsigned)v);
+    } else {
+#pragma unroll
+      for (int q = 0; q < GR; ++q) xs[buf][gx_seq][gx_k + q] = (__bf16)xr[j].v[q];
+    }
+  };
+
+  // h storer: granule (tid mod n_gh) of the [16][H] tile; lane group tid / n_gh (0..3)
+  // publishes element `el` of that float4 to the stream (no duplicate granule stores)
+  constexpr int n_gh = 16 * H / 4;
+  const int gh = (tid % n_gh) * 4;
+  const int el = tid / n_gh;
+  float* hbase = S.h + (size_t)row0 * H + gh;
+  const size_t hstep = (size_t)Mp * H;
+  unsigned long long* sbase = S.sout ? S.sout + (size_t)row0 * H + gh + el : nullptr;
+  const bool publish = S.sout != nullptr;
+  const int To = P > 0 ? T / P : T;
+  PoolAcc pool;
+
+#pragma unroll
+  for (int j = 0; j < D; ++j) load_x(j, min(j, T - 1));
+  __syncthreads();
+  stage_x(0, 0, 0);
+  load_x(0, min(D, T - 1));
+  float c[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) c[cc] = 0.f;
+  __syncthreads();
+
+  for (int t0 = 0; t0 <= T; t0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int t = t0 + j;
+      const int p = t & 1;
+      const int jn = (j + 1 == D) ? 0 : j + 1;
+      {
+        const int ts = (t >= 1 && t <= T) ? t - 1 : T;
+        const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
+        *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+        if (t >= 1 && t <= T) {
+          if (P > 0) {
+            pool.step(v, t - 1, P, To, S.pout, S.iout, (size_t)row0 * H + gh, hstep);
+            if (publish && (t - 1) % P == P - 1 && (t - 1) / P < To) {
+              const float m = el == 0 ? pool.m.x : el == 1 ? pool.m.y : el == 2 ? pool.m.z : pool.m.w;
+              st_granule(sbase + (size_t)((t - 1) / P) * hstep, m, tagb | (unsigned)((t - 1) / P));
+            }
+          } else if (publish) {
+            const float m = el == 0 ? v.x : el == 1 ? v.y : el == 2 ? v.z : v.w;
+            st_granule(sbase + (size_t)(t - 1) * hstep, m, tagb | (unsigned)(t - 1));
+          }
+        }
+      }
+      f32x4_t acc[CPL];
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) {
+        f32x4_t accx = bias4[cc], acch = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KX; ++s) {
+          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
+          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, accx, 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < C::KSH; ++s) {
+          const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
+          acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acch, 0, 0, 0);
+        }
+        acc[cc] = accx + acch;
+      }
+      stage_x(p ^ 1, jn, min(t + 1, T - 1));
+      load_x(jn, min(t + 1 + D, T - 1));
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc) {
+        const float iv = sigmoidf_fast(acc[cc][0]);
+        const float fv = sigmoidf_fast(acc[cc][1]);
+        const float gv = tanhf_fast(acc[cc][2]);
+        const float ov = sigmoidf_fast(acc[cc][3]);
+        c[cc] = fv * c[cc] + iv * gv;
+        const float hv = ov * tanhf_fast(c[cc]);
+        const int u = unit[cc];
+        hs[p ^ 1][col][u] = (__bf16)hv;
+        hf[p][col][u] = hv;
+        if constexpr (TRAIN) {
+          const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
+          *reinterpret_cast<float4*>(S.g + o * 4) = make_float4(iv, fv, gv, ov);
+          S.c[o] = c[cc];
+        }
+      }
+      lds_barrier();
+    }
+  }
+}
+
+__device__ __forceinline__ void chain_finish(const ChainArgs& A, int nblk) {
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(A.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nblk - 1) {            // last workgroup: next launch gets a new epoch
+      __hip_atomic_store(A.ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(A.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <bool TRAIN>
+__global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
+  const int nblk = gridDim.x;
+  const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
+  if (s >= A.ns || tile >= A.ntiles) {
+    chain_finish(A, nblk);
+    return;
+  }
+  const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned tagb = (E & 0xFFFFFu) << 12;
+  const ChainStage& S = A.st[s];
+  const int H = S.H, KX = S.KX;
+  const bool src = s > 0;
+#define GQ_CHAIN_BODY(HH, KXX, DD, SRCV)                                                \
+  {                                                                                     \
+    if (threadIdx.x >= TMC<HH>::NT) return;                                             \
+    chain_stage<HH, TRAIN, KXX, DD, SRCV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl);        \
+  }
+#define GQ_CHAIN_KX(HH)                                                                 \
+  if (src) { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 8, true) else GQ_CHAIN_BODY(HH, 2, 8, true) } \
+  else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false) else GQ_CHAIN_BODY(HH, 2, 6, false) }
+  if (H == 16) GQ_CHAIN_KX(16)
+  else if (H == 32) GQ_CHAIN_KX(32)
+  else GQ_CHAIN_KX(64)
+#undef GQ_CHAIN_KX
+#undef GQ_CHAIN_BODY
+  __syncthreads();
+  chain_finish(A, nblk);
+}
+
+// ---------------------------------------------------------------------------------------
+// host
+static int* chain_ctl(int dev) {
+  static int* ctl[64] = {nullptr};
+  TORCH_CHECK(dev >= 0 && dev < 64, "lstm_chain: device index");
+  if (!ctl[dev]) {
+    hipStreamCaptureStatus cs;
+    TORCH_CHECK(hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
+                "lstm_chain: first use must not be inside a graph capture");
+    int* p = nullptr;
+    TORCH_CHECK(hipMalloc(&p, 4 * sizeof(int)) == hipSuccess, "lstm_chain: control word allocation");
+    const int init[4] = {1, 0, 0, 0};     // epoch 1: zeroed memory never carries a valid tag
+    TORCH_CHECK(hipMemcpy(p, init, sizeof(init), hipMemcpyHostToDevice) == hipSuccess, "lstm_chain: init");
+    ctl[dev] = p;
+  }
+  return ctl[dev];
+}
+
+// x [T, Mp, Din] (Din % 4 == 0, 16-B aligned); per stage W [Dw, 4H], U [H, 4H], b [4H];
+// pool[s] > 0: MaxPooling1D(pool[s]) after stage s. Returns per stage [h, g, c, pooled, idx].
+std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U, at::TensorList b,
+                                       at::IntArrayRef pool, bool train) {
+  check_f32_cuda(x, "x");
+  const int ns = (int)W.size();
+  TORCH_CHECK(ns >= 1 && ns <= CHAIN_MAX && (int)U.size() == ns && (int)b.size() == ns && (int)pool.size() == ns,
+              "lstm_chain: stage lists");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "lstm_chain: x must be a contiguous [T, Mp, Din]");
+  const int Mp = (int)x.size(1);
+  TORCH_CHECK(Mp % 16 == 0, "lstm_chain: Mp must be a multiple of 16");
+  const int ntiles = Mp / 16, nt8 = (ntiles + 7) / 8 * 8;
+  TORCH_CHECK(ns * nt8 <= 256, "lstm_chain: ", ns * nt8, " workgroups cannot all be resident");
+  TORCH_CHECK(x.size(2) % 4 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "lstm_chain: x channels must be float4 granules");
+  c10::DeviceGuard guard(x.device());
+  auto opt = x.options();
+  ChainArgs A{};
+  A.ns = ns;
+  A.ntiles = ntiles;
+  A.nt8 = nt8;
+  A.Mp = Mp;
+  A.ctl = chain_ctl(x.get_device());
+  std::vector<at::Tensor> out;
+  at::Tensor prev_stream;
+  int T = (int)x.size(0), Din = (int)x.size(2);
+  for (int s = 0; s < ns; ++s) {
+    for (const at::Tensor* t : {&W[s], &U[s], &b[s]}) check_f32_cuda(*t, "lstm_chain weight");
+    const int H = (int)U[s].size(0), Dw = (int)W[s].size(0);
+    TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_chain: hidden size ", H);
+    TORCH_CHECK(W[s].size(1) == 4 * H && U[s].size(1) == 4 * H && b[s].numel() == 4 * H, "lstm_chain: weights");
+    TORCH_CHECK(Dw <= Din && Din <= 64 && (s == 0 || Din <= H), "lstm_chain: stage ", s, " input width ", Din);
+    TORCH_CHECK(T >= 1 && T < 4096, "lstm_chain: sequence length");
+    const int P = (int)pool[s];
+    ChainStage& S = A.st[s];
+    S.x = s == 0 ? x.data_ptr<float>() : nullptr;
+    S.xin = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev_stream.data_ptr<int64_t>());
+    S.W = W[s].data_ptr<float>();
+    S.U = U[s].data_ptr<float>();
+    S.b = b[s].data_ptr<float>();
+    at::Tensor h = at::empty({T + 1, Mp, H}, opt);
+    at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt) : at::empty({0}, opt);
+    at::Tensor c = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
+    at::Tensor pooled, pidx;
+    const TmPool pl = tm_pool_outputs(P, T, Mp, H, opt, pooled, pidx);
+    const int To = P > 0 ? T / P : T;
+    TORCH_CHECK(To >= 1, "lstm_chain: pooled length");
+    at::Tensor so = s + 1 < ns ? at::empty({To, Mp, H}, opt.dtype(at::kLong)) : at::Tensor();
+    S.h = h.data_ptr<float>();
+    S.g = train ? g.data_ptr<float>() : nullptr;
+    S.c = train ? c.data_ptr<float>() : nullptr;
+    S.sout = so.defined() ? reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>()) : nullptr;
+    S.pout = pl.out;
+    S.iout = pl.idx;
+    S.H = H;
+    S.T = T;
+    S.Din = Din;
+    S.Dw = Dw;
+    S.KX = (Din + 31) / 32;
+    S.P = P;
+    out.insert(out.end(), {h.narrow(0, 0, T), g, c, pooled, pidx});
+    if (so.defined()) out.push_back(so);        // kept alive until the launch is enqueued
+    prev_stream = so;
+    T = To;
+    Din = H;
+  }
+  const int nblk = ns * nt8;
+  if (train)
+    hipLaunchKernelGGL(lstm_chain_fwd_kernel<true>, dim3(nblk), dim3(1024), 0, stream(), A);
+  else
+    hipLaunchKernelGGL(lstm_chain_fwd_kernel<false>, dim3(nblk), dim3(1024), 0, stream(), A);
+  GQ_LAUNCH_CHECK();
+  // drop the stream buffers from the result (the caching allocator orders their reuse)
+  std::vector<at::Tensor> res;
+  for (auto& t : out)
+    if (t.scalar_type() != at::kLong) res.push_back(t);
+  return res;
+}
+
+// [epoch, finished, timeout flag, 0] of this device's chain control words (tests)
+at::Tensor lstm_chain_status(const at::Tensor& like) {
+  c10::DeviceGuard guard(like.device());
+  int* p = chain_ctl(like.get_device());
+  at::Tensor o = at::empty({4}, like.options().dtype(at::kInt));
+  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int>(), p, 4 * sizeof(int), hipMemcpyDeviceToDevice, stream()) == hipSuccess,
+              "lstm_chain_status");
+  return o;
+}
+
+}  // namespace gq
+
+TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("lstm_chain_fwd", &gq::lstm_chain_fwd);
+  m.impl("lstm_chain_status", &gq::lstm_chain_status);
+}

@@ -27,6 +27,7 @@
 // So dz never goes to HBM and no separate weight-gradient kernel runs.
 #include "common.h"
 #include "lstm_grads_body.h"
+#include "lstm_tm_common.h"
 
 namespace gq {
 
@@ -35,86 +36,6 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
                      long dx_cb_stride, int lddx, long x_elems, hipStream_t st);
 int lstm_grads_col_blocks(int H);
-
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-
-// A wave-uniform predicate the compiler can SEE is uniform (an SGPR): branches on it are
-// scalar, so no exec-mask join -> no conservative s_waitcnt vmcnt(0) around the loads
-// inside (measured: with threadIdx-derived predicates every step drained the load ring).
-__device__ __forceinline__ bool wave_uniform(bool p) { return __builtin_amdgcn_readfirstlane((int)p) != 0; }
-
-template <int H>
-struct TMC {
-  static constexpr int CPL = H > 64 ? H / 64 : 1;   // cells per lane
-  static constexpr int NW = H / (4 * CPL);          // waves per 16-sequence tile (<= 16)
-  static constexpr int NT = 64 * NW;
-  static constexpr int G4 = 4 * H;
-  static constexpr int KPH = ((H + 31) / 32) * 32;
-  static constexpr int KSH = KPH / 32;              // K = H steps (forward recurrent part)
-  static constexpr int KB = G4 / 32;                // K = 4H steps (backward)
-  static constexpr int HP = H + 4;                  // row pitch of fp32 [16][H] LDS tiles: the
-                                                    // per-cell accesses (16 rows x 4 units per
-                                                    // wave) then hit 64 distinct banks
-};
-
-// ---- tile streamer: granules of GR floats of one contiguous tile, wave-uniform loaders
-template <int GR>
-struct Granule {
-  float v[4];
-  __device__ __forceinline__ void load(const float* p) {
-    if constexpr (GR == 4) {
-      const float4 a = *reinterpret_cast<const float4*>(p);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    } else if constexpr (GR == 2) {
-      const float2 a = *reinterpret_cast<const float2*>(p);
-      v[0] = a.x; v[1] = a.y;
-    } else {
-      v[0] = *p;
-    }
-  }
-  __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
-};
-
-// ---- fused MaxPooling1D(P) (valid, stride P) of a stored h sequence. Each storer lane owns
-// one float4 granule of the [16][H] tile for the whole sequence, so the running max and the
-// byte argmax (first maximum wins, like TF's MaxPoolGrad) stay in its registers; the pooled
-// granule and its 4 argmax bytes are written when a window closes. Layout = maxpool1d_fwd's
-// on the time-major tensor: pooled [T/P][Mp][H] fp32, argmax [T/P][Mp][H] uint8.
-struct PoolAcc {
-  float4 m;
-  unsigned idx;
-  __device__ __forceinline__ void step(const float4& v, int t, int P, int To, float* __restrict__ pout,
-                                       unsigned* __restrict__ iout, size_t off, size_t pstep) {
-    const int r = t % P;                            // t, P wave-uniform: scalar branches
-    if (r == 0) {
-      m = v;
-      idx = 0u;
-    } else {
-      const unsigned rb = (unsigned)r;
-      if (v.x > m.x) { m.x = v.x; idx = (idx & 0xffffff00u) | rb; }
-      if (v.y > m.y) { m.y = v.y; idx = (idx & 0xffff00ffu) | (rb << 8); }
-      if (v.z > m.z) { m.z = v.z; idx = (idx & 0xff00ffffu) | (rb << 16); }
-      if (v.w > m.w) { m.w = v.w; idx = (idx & 0x00ffffffu) | (rb << 24); }
-    }
-    if (r == P - 1 && t / P < To) {
-      const size_t k = (size_t)(t / P);
-      *reinterpret_cast<float4*>(pout + k * pstep + off) = m;
-      iout[(k * pstep + off) / 4] = idx;
-    }
-  }
-};
-
-// inverse for the backward: dh_t = dpool[t / P] where the argmax byte == t % P, else 0
-__device__ __forceinline__ float4 unpool4(const float4& v, unsigned idx, int t, int P, int To) {
-  const bool ok = t >= 0 && t < To * P;
-  const unsigned r = ok ? (unsigned)(t % P) : 0xffu;
-  float4 o;
-  o.x = ((idx & 0xffu) == r) ? v.x : 0.f;
-  o.y = (((idx >> 8) & 0xffu) == r) ? v.y : 0.f;
-  o.z = (((idx >> 16) & 0xffu) == r) ? v.z : 0.f;
-  o.w = ((idx >> 24) == r) ? v.w : 0.f;
-  return o;
-}
 
 // =====================================================================================
 // forward
@@ -897,30 +818,6 @@ static bool tm_supported(int H, int Din, int gr) {
 }
 
 // fused MaxPooling1D of the layer output: pooled [T/P, Mp, H] fp32 + argmax uint8 (P = 0: none)
-struct TmPool {
-  int P = 0;
-  float* out = nullptr;
-  unsigned* idx = nullptr;
-  const unsigned* cidx = nullptr;   // backward: argmax of the pooled gradient given as dh
-};
-
-static TmPool tm_pool_outputs(int P, int T, int Mp, int H, const at::TensorOptions& opt, at::Tensor& pooled,
-                              at::Tensor& pidx) {
-  TmPool pl;
-  if (P <= 0) {
-    pooled = at::empty({0}, opt);
-    pidx = at::empty({0}, opt.dtype(at::kByte));
-    return pl;
-  }
-  TORCH_CHECK(P <= 255 && T / P >= 1, "lstm_tm: pool size must be 1..255 and <= T");
-  pooled = at::empty({T / P, Mp, H}, opt);
-  pidx = at::empty({T / P, Mp, H}, opt.dtype(at::kByte));
-  pl.P = P;
-  pl.out = pooled.data_ptr<float>();
-  pl.idx = reinterpret_cast<unsigned*>(pidx.data_ptr<uint8_t>());
-  return pl;
-}
-
 template <int H, bool TRAIN, int KX, int GR>
 static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, float* g,
                        float* c, int Mp, int T, int Din, int Dw, const TmPool& pl, hipStream_t st) {

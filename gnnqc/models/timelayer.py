@@ -100,11 +100,15 @@ class TimeLayer(nn.Module):
         rows past M; C may carry zero channels past the first layer's input width).
         Returns ``[M, out_features]``. Producers that can write this layout directly (the
         SoilNet GCN kernel) skip the transpose/pad copy of :meth:`_forward_tm`."""
-        from ..ops.lstm import lstm_layer_tm, lstm_pair_tm, tm_eligible
+        from ..ops.lstm import _chain_on, lstm_chain_tm, lstm_layer_tm, lstm_pair_tm, tm_eligible
         from ..ops.pool import max_pool1d_tm
         tm = True
         seq = self._sequence()
         i = 0
+        plan = self._chain_plan(seq, h) if _chain_on() else None
+        if plan is not None:                      # leading layers + pools: one pipelined launch
+            mods, pools, i = plan
+            h = lstm_chain_tm(h, mods, pools)
         while i < len(seq):
             mod = seq[i]
             i += 1
@@ -136,6 +140,42 @@ class TimeLayer(nn.Module):
                 tm = False
             h = mod(h)
         return h
+
+    @staticmethod
+    def _chain_plan(seq, h: torch.Tensor):
+        """Leading run of time-major LSTM layers (returning sequences, each optionally followed
+        by a MaxPooling1D) that the cross-CU chain kernel takes: ``(modules, pools, next index)``
+        or None. Constraints of ``lstm_chain.hip``: H in {16, 32, 64}, inputs <= 64 channels and
+        no wider than the layer, all workgroups co-resident (``chain_fits``)."""
+        from ..ops import use_hip
+        from ..ops.lstm import chain_fits
+        T, Mp, din = h.shape
+        if not use_hip(h) or din % 4 or h.data_ptr() % 16:
+            return None
+        mods, pools = [], []
+        i = 0
+        while i < len(seq):
+            mod = seq[i]
+            if not (isinstance(mod, LSTM) and mod.return_sequences and mod.activation == "tanh" and mod.compute_bf16
+                    and mod.units in (16, 32, 64)):
+                break
+            Dw = mod.kernel.shape[0]
+            if din > 64 or Dw > din or (mods and din > mod.units) or T >= 4096:
+                break
+            j, pool = i + 1, 0
+            if j < len(seq) and isinstance(seq[j], MaxPooling1D):
+                P = seq[j].pool_size
+                if not (1 <= P <= 255 and T // P >= 1):
+                    break
+                pool, j = P, j + 1
+            mods.append(mod)
+            pools.append(pool)
+            T = T // pool if pool else T
+            din = mod.units
+            i = j
+        if not chain_fits(Mp, len(mods)):
+            return None
+        return mods, pools, i
 
     @staticmethod
     def _fusable_pool(seq, i: int, T: int) -> int:

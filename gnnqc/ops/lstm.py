@@ -310,6 +310,103 @@ def _tm_split_backward(dh, g, c, x, h, W, U, sinks, need_dx, pool_idx=None, pool
     return dx
 
 
+def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx, pidx=None, pool: int = 0):
+    """Backward of one time-major layer (pipe / split / fused, see :func:`_split_mode`).
+    Returns dx (or None) and the three weight gradients to hand to autograd (None where they
+    were accumulated directly into ``.grad``)."""
+    from ..utils.native import hip_ops
+    wgrad = any(need_w)
+    if not wgrad and not need_dx:
+        return None, [None, None, None]
+    if wgrad:
+        sinks = [_grad_sink(p) for p in params]
+    else:
+        e = x.new_zeros(0)
+        sinks = [(e, True)] * 3
+    pi = pidx if pool else None
+    Wc, Uc = W.contiguous(), U.contiguous()
+    if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+        dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx)
+    elif wgrad and all(d for _, d in sinks) and _split_mode() not in ("fused", "pipe"):
+        dx = _tm_split_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx, pi, pool)
+    else:
+        dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, sinks[0][0], sinks[1][0], sinks[2][0],
+                                   need_dx, pi, pool)
+    grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need_w)]
+    return (dx if need_dx else None), grads
+
+
+class _HipLSTMChain(torch.autograd.Function):
+    """A stack of time-major layers (with MaxPooling1D between some of them) whose forward
+    runs as ONE cross-CU pipelined kernel (``lstm_chain.hip``: every layer of a 16-sequence
+    tile on its own CU, consuming the previous layer's output as it is produced). The
+    backward runs the per-layer backward kernels in reverse, un-pooling between them."""
+
+    @staticmethod
+    def forward(ctx, x, pools, *params):
+        from ..utils.native import hip_ops
+        ns = len(pools)
+        Ws = [params[3 * i].contiguous() for i in range(ns)]
+        Us = [params[3 * i + 1].contiguous() for i in range(ns)]
+        bs = [params[3 * i + 2].contiguous() for i in range(ns)]
+        need = any(ctx.needs_input_grad)
+        outs = hip_ops().lstm_chain_fwd(x, Ws, Us, bs, [int(p) for p in pools], need)
+        ctx.pools = tuple(int(p) for p in pools)
+        ctx.params = params
+        if need:
+            ctx.save_for_backward(x, *Ws, *Us, *outs)
+        last = outs[5 * (ns - 1):]
+        return last[3] if pools[-1] else last[0]
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..utils.native import hip_ops
+        ops = hip_ops()
+        pools = ctx.pools
+        ns = len(pools)
+        saved = ctx.saved_tensors
+        x, Ws, Us, outs = saved[0], saved[1:1 + ns], saved[1 + ns:1 + 2 * ns], saved[1 + 2 * ns:]
+        need = ctx.needs_input_grad
+        grads = [None] * (3 * ns)
+        dh = dout.contiguous()
+        dx = None
+        for i in reversed(range(ns)):
+            h, g, c, _, idx = outs[5 * i:5 * i + 5]
+            T, Mp, H = h.shape
+            if pools[i]:
+                dh = ops.maxpool1d_bwd(dh.view(1, -1, Mp * H), idx.view(1, -1, Mp * H), T, pools[i]).view(T, Mp, H)
+            if i == 0:
+                xi = x
+            else:
+                xi = outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)]
+            need_dx = i > 0 or bool(need[0])
+            dx, gr = _tm_layer_backward(dh, xi, Ws[i], Us[i], h, g, c, ctx.params[3 * i:3 * i + 3],
+                                        need[2 + 3 * i:5 + 3 * i], need_dx)
+            grads[3 * i:3 * i + 3] = gr
+            dh = dx
+        return (dx if need[0] else None, None, *grads)
+
+
+def _chain_on() -> bool:
+    """Cross-CU pipelined forward of the time-major LSTM stack (``GNNQC_CHAIN``, default on)."""
+    import os
+    return os.environ.get("GNNQC_CHAIN", "1") == "1"
+
+
+def lstm_chain_tm(x_tm: torch.Tensor, mods, pools) -> torch.Tensor:
+    """Forward of stacked LSTM modules (``gnnqc.models.layers.LSTM``, all returning sequences)
+    with ``pools[i]`` > 0 a MaxPooling1D after module i; returns the last stage's output."""
+    params = []
+    for m in mods:
+        params += [m.kernel, m.recurrent_kernel, m.bias]
+    return _HipLSTMChain.apply(x_tm, tuple(int(p) for p in pools), *params)
+
+
+def chain_fits(Mp: int, n_stages: int) -> bool:
+    """All workgroups of a chain launch must be co-resident (one 1024-thread workgroup per CU)."""
+    return n_stages >= 2 and n_stages * ((Mp // 16 + 7) // 8 * 8) <= 256 and n_stages <= 8
+
+
 class _HipLSTMTM(torch.autograd.Function):
     """Time-major LSTM layer (``lstm_tm.hip``): x [T, Mp, Din] -> h [T, Mp, H] (or the last
     step [Mp, H]). The backward is ONE fused kernel: recurrence, dx, and dW/dU/db
@@ -468,5 +565,6 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     return lstm_eager(x, W, U, b, return_sequences, activation)
 
 
-__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "tm_eligible", "direct_grad_accumulation",
+__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
+           "direct_grad_accumulation",
            "join_side_streams"]

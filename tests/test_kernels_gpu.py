@@ -594,6 +594,8 @@ def test_timelayer_pair_fusion_matches_unfused(cuda_device, monkeypatch):
     tl = TimeLayer(18, 16, 2, "lstm", pool_size=3).to(cuda_device)
     x = torch.randn(128, 181, 18, device=cuda_device)
 
+    monkeypatch.setenv("GNNQC_CHAIN", "0")
+
     def run(no_pair):
         monkeypatch.setenv("GNNQC_NO_PAIR", "1" if no_pair else "0")
         xi = x.clone().requires_grad_(True)
@@ -608,6 +610,46 @@ def test_timelayer_pair_fusion_matches_unfused(cuda_device, monkeypatch):
     torch.testing.assert_close(o1, o0, atol=2e-3, rtol=1e-2)
     for a, b_ in zip(g1, g0):
         assert (a - b_).norm().item() <= 2e-2 * (b_.norm().item() + 1e-6)
+
+
+@pytest.mark.parametrize("M", [128, 40, 300])
+def test_chain_forward_matches_per_layer(cuda_device, monkeypatch, M):
+    """CML TimeLayer: the cross-CU pipelined stack forward (lstm_chain.hip) == the per-layer
+    kernels (no pair fusion) for the output and every gradient; repeated launches (fresh
+    epochs over reused stream buffers) stay identical and no consumer spin timed out."""
+    from gnnqc.models.timelayer import TimeLayer
+    from gnnqc.utils.native import hip_ops
+    torch.manual_seed(0)
+    tl = TimeLayer(18, 16, 2, "lstm", pool_size=3).to(cuda_device)
+    x = torch.randn(M, 181, 18, device=cuda_device)
+    monkeypatch.setenv("GNNQC_NO_PAIR", "1")
+
+    def run(chain):
+        monkeypatch.setenv("GNNQC_CHAIN", "1" if chain else "0")
+        xi = x.clone().requires_grad_(True)
+        for p in tl.parameters():
+            p.grad = None
+        out = tl(xi)
+        out.pow(2).sum().backward()
+        return out.detach(), [xi.grad.clone()] + [p.grad.clone() for p in tl.parameters()]
+
+    seq = tl._sequence()
+    h = torch.zeros(181, (M + 15) // 16 * 16, 20, device=cuda_device)
+    plan = tl._chain_plan(seq, h)
+    assert plan is not None and len(plan[0]) == 6 and plan[1] == [0, 3, 0, 3, 0, 3]
+    st0 = hip_ops().lstm_chain_status(x).cpu()
+    o0, g0 = run(False)
+    o1, g1 = run(True)
+    outs = [tl(x).detach() for _ in range(4)]
+    torch.cuda.synchronize()
+    st1 = hip_ops().lstm_chain_status(x).cpu()
+    assert int(st1[2]) == 0, "a consumer spin timed out"
+    assert int(st1[0]) - int(st0[0]) == 5 and int(st1[1]) == 0, (st0, st1)
+    torch.testing.assert_close(o1, o0, atol=1e-5, rtol=1e-5)
+    for o in outs:
+        assert torch.equal(o, o1)
+    for a, b_ in zip(g1, g0):     # (bf16 rounding flips of near-tie values move gradients ~1e-3)
+        assert (a - b_).norm().item() <= 5e-3 * (b_.norm().item() + 1e-6)
 
 
 def _soil_small_windows():
