@@ -23,8 +23,12 @@
 // are already running. Workgroups of stage s for tile j have the same blockIdx % 8, so
 // under the observed round-robin placement one tile's whole stack shares an XCD (speed only).
 //
+// A MaxPooling1D(3) between two stages is done by the CONSUMER while staging its input
+// (three granules per element, max + first-max argmax byte): the producer's own per-step
+// pooling lengthened its serial chain by ~110 ns per step (58 -> 78 us for the first pooled
+// CML layer), while the consumer, running at a third of the producer's step rate, has slack.
 // Each stage also writes everything the per-layer kernels write (h, gate / cell state for
-// the backward, the fused MaxPooling1D output + argmax bytes), so the backward is unchanged.
+// the backward, pooled output + argmax bytes), so the backward is unchanged.
 #include "common.h"
 #include "lstm_tm_common.h"
 
@@ -32,6 +36,20 @@ namespace gq {
 
 static constexpr int CHAIN_MAX = 8;
 static constexpr int CHAIN_SPIN = 1 << 20;
+// granule ring depth of a non-pooling consumer: an sc1 load of a line another CU wrote
+// through to memory takes microseconds under load, D steps of ~0.33 us each must cover it
+#ifndef CHAIN_D
+#define CHAIN_D 6
+#endif
+#ifndef CHAIN_D3
+#define CHAIN_D3 3           // ring of a pooling (PIN = 3) consumer: it runs at a third of the rate
+#endif
+#ifndef CHAIN_LEAD1
+#define CHAIN_LEAD1 2
+#endif
+#ifndef CHAIN_LEAD3
+#define CHAIN_LEAD3 1
+#endif
 
 struct ChainStage {
   const float* x;                    // stage 0: fp32 input [T][Mp][Din]
@@ -43,15 +61,18 @@ struct ChainStage {
   float* g;                          // train: [T+1][tiles][NW][CPL][64][4]
   float* c;
   unsigned long long* sout;          // tagged output stream [To][Mp][H] (nullptr: last stage)
-  float* pout;                       // pooled output [T/P][Mp][H] (P > 0)
+  float* pout;                       // last stage only: own pooled output [T/P][Mp][H] (P > 0)
   unsigned* iout;
-  int H, T, Din, Dw, KX, P;
+  float* pin_out;                    // PIN > 1: the pooled input [T][Mp][Din] + argmax bytes,
+  unsigned char* pin_idx;            //   written here (the producer publishes unpooled h)
+  int H, T, Din, Dw, KX, P, PIN;
 };
 
 struct ChainArgs {
   ChainStage st[CHAIN_MAX];
   int ns, ntiles, nt8, Mp;
   int* ctl;                          // [0] epoch, [1] finished workgroups, [2] spin timeout seen
+  long long* trace;                  // [blocks][2] start / end s_memrealtime (100 MHz) of the last launch
 };
 
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
@@ -78,16 +99,29 @@ __device__ __noinline__ unsigned long long chain_wait(const unsigned long long* 
 // One layer of one tile: lstm_tm_fwd_kernel's step loop with the x ring fed either from
 // global memory (stage 0) or from the previous stage's granule stream (SRC), and the
 // output (optionally max-pooled) also published as granules.
-template <int H, bool TRAIN, int KX, int D, bool SRC>
+// LDS of one stage (carved from the kernel's one buffer: the stage bodies must not each
+// reserve their own static arrays)
+template <int H, int KX>
+struct ChainLds {
+  static constexpr int HS = 2 * 16 * (TMC<H>::KPH + 8) * 2;
+  static constexpr int XS = 2 * 16 * (32 * KX + 8) * 2;
+  static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
+  static constexpr int BYTES = HS + XS + HF;
+};
+static constexpr int CHAIN_LDS = ChainLds<64, 2>::BYTES;
+
+template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN>
 __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
-                                            int* ctl) {
+                                            int* ctl, char* smem) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
   constexpr int KPX = 32 * KX;
   constexpr int GR = SRC ? 1 : 4;
-  __shared__ __attribute__((aligned(16))) __bf16 hs[2][16][C::KPH + 8];
-  __shared__ __attribute__((aligned(16))) __bf16 xs[2][16][KPX + 8];
-  __shared__ __attribute__((aligned(16))) float hf[2][16][C::HP];
+  using L = ChainLds<H, KX>;
+  static_assert(L::BYTES <= CHAIN_LDS && L::HS % 16 == 0 && L::XS % 16 == 0, "chain LDS layout");
+  auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
+  auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
+  auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
 
   const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -136,19 +170,40 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   const int gx_seq = gx / Din, gx_k = gx % Din;
   const size_t xstep = (size_t)Mp * Din;
   const size_t xoff = (size_t)row0 * Din + gx;
+  // SRC: x_t = MaxPool(PIN) of the producer's h at PIN t .. PIN t + PIN - 1 (PIN == 1: h_t),
+  // pooled here from PIN granules (value + first-max argmax byte also stored for the backward)
   Granule<GR> xr[D];
-  unsigned long long xq[D];
+  unsigned long long xq[D][PIN];
   auto load_x = [&](int j, int tx) {
-    if constexpr (SRC) xq[j] = ld_granule(S.xin + xoff + (size_t)tx * xstep);
-    else xr[j].load(S.x + xoff + (size_t)tx * xstep);
+    if constexpr (SRC) {
+#pragma unroll
+      for (int r = 0; r < PIN; ++r) xq[j][r] = ld_granule(S.xin + xoff + (size_t)(PIN * tx + r) * xstep);
+    } else {
+      xr[j].load(S.x + xoff + (size_t)tx * xstep);
+    }
   };
   auto stage_x = [&](int buf, int j, int tx) {
     if constexpr (SRC) {
-      const unsigned want = tagb | (unsigned)tx;
-      unsigned long long v = xq[j];
-      if (__builtin_amdgcn_ballot_w64((unsigned)(v >> 32) != want) != 0)
-        v = chain_wait(S.xin + xoff + (size_t)tx * xstep, want, ctl);
-      xs[buf][gx_seq][gx_k] = (__bf16)__uint_as_float((unsigned)v);
+      bool bad = false;
+#pragma unroll
+      for (int r = 0; r < PIN; ++r) bad |= (unsigned)(xq[j][r] >> 32) != (tagb | (unsigned)(PIN * tx + r));
+      if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+#pragma unroll
+        for (int r = 0; r < PIN; ++r)
+          xq[j][r] = chain_wait(S.xin + xoff + (size_t)(PIN * tx + r) * xstep, tagb | (unsigned)(PIN * tx + r), ctl);
+      }
+      float m = __uint_as_float((unsigned)xq[j][0]);
+      if constexpr (PIN > 1) {
+        unsigned arg = 0;
+#pragma unroll
+        for (int r = 1; r < PIN; ++r) {
+          const float v = __uint_as_float((unsigned)xq[j][r]);
+          if (v > m) { m = v; arg = r; }
+        }
+        S.pin_out[xoff + (size_t)tx * xstep] = m;
+        S.pin_idx[xoff + (size_t)tx * xstep] = (unsigned char)arg;
+      }
+      xs[buf][gx_seq][gx_k] = (__bf16)m;
     } else {
 #pragma unroll
       for (int q = 0; q < GR; ++q) xs[buf][gx_seq][gx_k + q] = (__bf16)xr[j].v[q];
@@ -164,9 +219,17 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   const size_t hstep = (size_t)Mp * H;
   unsigned long long* sbase = S.sout ? S.sout + (size_t)row0 * H + gh + el : nullptr;
   const bool publish = S.sout != nullptr;
-  const int To = P > 0 ? T / P : T;
+  const int To = P > 0 ? T / P : T;      // (P > 0 only without a consumer stage)
   PoolAcc pool;
 
+  if constexpr (SRC) {
+    // start once the producer is D + LEAD (input) steps ahead: the ring's loads then find
+    // their granules. (Starting at once left every ring slot stale: each of the first D
+    // steps then paid a full re-poll round trip, ~12 us of lag per stage.)
+    constexpr int LEAD = PIN > 1 ? CHAIN_LEAD3 : CHAIN_LEAD1;
+    const int tw = min(D + LEAD, T - 1);
+    (void)chain_wait(S.xin + xoff + (size_t)(PIN * tw + PIN - 1) * xstep, tagb | (unsigned)(PIN * tw + PIN - 1), ctl);
+  }
 #pragma unroll
   for (int j = 0; j < D; ++j) load_x(j, min(j, T - 1));
   __syncthreads();
@@ -188,12 +251,8 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
         if (t >= 1 && t <= T) {
-          if (P > 0) {
+          if (P > 0) {              // last stage: pools its own output (the consumer pools otherwise)
             pool.step(v, t - 1, P, To, S.pout, S.iout, (size_t)row0 * H + gh, hstep);
-            if (publish && (t - 1) % P == P - 1 && (t - 1) / P < To) {
-              const float m = el == 0 ? pool.m.x : el == 1 ? pool.m.y : el == 2 ? pool.m.z : pool.m.w;
-              st_granule(sbase + (size_t)((t - 1) / P) * hstep, m, tagb | (unsigned)((t - 1) / P));
-            }
           } else if (publish) {
             const float m = el == 0 ? v.x : el == 1 ? v.y : el == 2 ? v.z : v.w;
             st_granule(sbase + (size_t)(t - 1) * hstep, m, tagb | (unsigned)(t - 1));
@@ -258,30 +317,42 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
     chain_finish(A, nblk);
     return;
   }
+  if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned tagb = (E & 0xFFFFFu) << 12;
+  __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS];
   const ChainStage& S = A.st[s];
   const int H = S.H, KX = S.KX;
   const bool src = s > 0;
-#define GQ_CHAIN_BODY(HH, KXX, DD, SRCV)                                                \
+#define GQ_CHAIN_BODY(HH, KXX, DD, SRCV, PINV)                                          \
   {                                                                                     \
     if (threadIdx.x >= TMC<HH>::NT) return;                                             \
-    chain_stage<HH, TRAIN, KXX, DD, SRCV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl);        \
+    chain_stage<HH, TRAIN, KXX, DD, SRCV, PINV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
   }
+#define GQ_CHAIN_SRC(HH, PINV, DD)                                                      \
+  if (KX == 1) GQ_CHAIN_BODY(HH, 1, DD, true, PINV) else GQ_CHAIN_BODY(HH, 2, DD, true, PINV)
 #define GQ_CHAIN_KX(HH)                                                                 \
-  if (src) { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 8, true) else GQ_CHAIN_BODY(HH, 2, 8, true) } \
-  else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false) else GQ_CHAIN_BODY(HH, 2, 6, false) }
+  if (src) { if (S.PIN == 3) { GQ_CHAIN_SRC(HH, 3, CHAIN_D3) } else { GQ_CHAIN_SRC(HH, 1, CHAIN_D) } } \
+  else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false, 1) else GQ_CHAIN_BODY(HH, 2, 6, false, 1) }
   if (H == 16) GQ_CHAIN_KX(16)
   else if (H == 32) GQ_CHAIN_KX(32)
   else GQ_CHAIN_KX(64)
 #undef GQ_CHAIN_KX
+#undef GQ_CHAIN_SRC
 #undef GQ_CHAIN_BODY
   __syncthreads();
+  if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
   chain_finish(A, nblk);
 }
 
 // ---------------------------------------------------------------------------------------
 // host
+static long long* chain_trace_buf(int dev) {
+  static long long* tr[64] = {nullptr};
+  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], 2 * 256 * sizeof(long long)) == hipSuccess, "lstm_chain: trace");
+  return tr[dev];
+}
+
 static int* chain_ctl(int dev) {
   static int* ctl[64] = {nullptr};
   TORCH_CHECK(dev >= 0 && dev < 64, "lstm_chain: device index");
@@ -321,6 +392,7 @@ std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at
   A.nt8 = nt8;
   A.Mp = Mp;
   A.ctl = chain_ctl(x.get_device());
+  A.trace = chain_trace_buf(x.get_device());
   std::vector<at::Tensor> out;
   at::Tensor prev_stream;
   int T = (int)x.size(0), Din = (int)x.size(2);
@@ -332,6 +404,8 @@ std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at
     TORCH_CHECK(Dw <= Din && Din <= 64 && (s == 0 || Din <= H), "lstm_chain: stage ", s, " input width ", Din);
     TORCH_CHECK(T >= 1 && T < 4096, "lstm_chain: sequence length");
     const int P = (int)pool[s];
+    const bool last = s + 1 == ns;
+    TORCH_CHECK(last || P == 0 || P == 3, "lstm_chain: pools between stages must be 3 (got ", P, ")");
     ChainStage& S = A.st[s];
     S.x = s == 0 ? x.data_ptr<float>() : nullptr;
     S.xin = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev_stream.data_ptr<int64_t>());
@@ -345,19 +419,25 @@ std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at
     const TmPool pl = tm_pool_outputs(P, T, Mp, H, opt, pooled, pidx);
     const int To = P > 0 ? T / P : T;
     TORCH_CHECK(To >= 1, "lstm_chain: pooled length");
-    at::Tensor so = s + 1 < ns ? at::empty({To, Mp, H}, opt.dtype(at::kLong)) : at::Tensor();
+    // the stream carries the UNPOOLED h: a pooling consumer pools it (and writes pooled / pidx)
+    at::Tensor so = !last ? at::empty({T, Mp, H}, opt.dtype(at::kLong)) : at::Tensor();
     S.h = h.data_ptr<float>();
     S.g = train ? g.data_ptr<float>() : nullptr;
     S.c = train ? c.data_ptr<float>() : nullptr;
     S.sout = so.defined() ? reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>()) : nullptr;
-    S.pout = pl.out;
-    S.iout = pl.idx;
+    S.pout = last ? pl.out : nullptr;
+    S.iout = last ? pl.idx : nullptr;
+    S.P = last ? P : 0;
+    if (!last && P > 0) {          // the next stage pools this stage's output
+      A.st[s + 1].pin_out = pooled.data_ptr<float>();
+      A.st[s + 1].pin_idx = pidx.data_ptr<uint8_t>();
+    }
     S.H = H;
     S.T = T;
     S.Din = Din;
     S.Dw = Dw;
     S.KX = (Din + 31) / 32;
-    S.P = P;
+    S.PIN = s > 0 ? std::max(1, (int)pool[s - 1]) : 1;
     out.insert(out.end(), {h.narrow(0, 0, T), g, c, pooled, pidx});
     if (so.defined()) out.push_back(so);        // kept alive until the launch is enqueued
     prev_stream = so;
@@ -387,9 +467,20 @@ at::Tensor lstm_chain_status(const at::Tensor& like) {
   return o;
 }
 
+// [blocks, 2] start / end timestamps (s_memrealtime ticks) of the last chain launch (profiling)
+at::Tensor lstm_chain_trace(const at::Tensor& like) {
+  c10::DeviceGuard guard(like.device());
+  long long* p = chain_trace_buf(like.get_device());
+  at::Tensor o = at::empty({256, 2}, like.options().dtype(at::kLong));
+  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, 512 * sizeof(long long), hipMemcpyDeviceToDevice, stream()) ==
+                  hipSuccess, "lstm_chain_trace");
+  return o;
+}
+
 }  // namespace gq
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_fwd", &gq::lstm_chain_fwd);
   m.impl("lstm_chain_status", &gq::lstm_chain_status);
+  m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
 }

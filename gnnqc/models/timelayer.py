@@ -173,6 +173,8 @@ class TimeLayer(nn.Module):
             T = T // pool if pool else T
             din = mod.units
             i = j
+            if pool not in (0, 3):       # consumer-side pooling takes 3; others end the chain
+                break
         if not chain_fits(Mp, len(mods)):
             return None
         return mods, pools, i
