@@ -299,12 +299,12 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   }
 }
 
-__device__ __forceinline__ void chain_finish(const ChainArgs& A, int nblk) {
+__device__ __forceinline__ void chain_finish(int* ctl, int nblk) {
   if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(A.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int old = __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == nblk - 1) {            // last workgroup: next launch gets a new epoch
-      __hip_atomic_store(A.ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(A.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const int nblk = gridDim.x;
   const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
   if (s >= A.ns || tile >= A.ntiles) {
-    chain_finish(A, nblk);
+    chain_finish(A.ctl, nblk);
     return;
   }
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -342,7 +342,292 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
 #undef GQ_CHAIN_BODY
   __syncthreads();
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-  chain_finish(A, nblk);
+  chain_finish(A.ctl, nblk);
+}
+
+// =====================================================================================
+// backward chain: the layers' reverse recurrences, top layer first. Stage k's dx (the
+// gradient of the layer below's output, un-pooled by the CONSUMER with the forward's argmax
+// bytes when a MaxPooling1D sits between them) is handed off as granules like the forward's
+// h; every stage also writes its dz [T+1][Mp][4H] for the weight-gradient pass. The last
+// stage writes its dx as plain fp32 (the GCN backward's input).
+struct ChainBStage {
+  const float* dh;                   // stage 0: fp32 gradient of the layer's (pooled) output [Ts][Mp][H]
+  const unsigned long long* din;     // stages > 0: tagged dx stream of the stage above [Ts][Mp][H]
+  const unsigned char* pidx;         // P > 0: argmax bytes of the pool after this layer [Ts][Mp][H]
+  const float* g;
+  const float* c;
+  const float* W;
+  const float* U;
+  float* dz;                         // [T+1][Mp][4H]
+  unsigned long long* sout;          // tagged dx stream [T+1][Mp][Din] (nullptr: last stage)
+  float* dx;                         // last stage: fp32 dx [T][Mp][Din]
+  int H, T, Din, Dw, KX, P, Ts;
+};
+
+struct ChainBArgs {
+  ChainBStage st[CHAIN_MAX];
+  int ns, ntiles, nt8, Mp;
+  int* ctl;
+  long long* trace;
+};
+
+template <int H, int KX>
+struct ChainBLds {
+  static constexpr bool WL = H >= 32;             // W^T fragments of dx from LDS (VGPR budget)
+  static constexpr int ZS = 2 * 16 * (4 * H + 8) * 2;
+  static constexpr int DH = 2 * 16 * TMC<H>::HP * 4;
+  static constexpr int DX = 2 * 16 * 32 * KX * 4;
+  static constexpr int WB = WL ? 2 * KX * 16 * (4 * H + 8) * 2 : 0;
+  static constexpr int BYTES = ZS + DH + DX + WB;
+};
+static constexpr int CHAINB_LDS = ChainBLds<64, 2>::BYTES;
+
+#ifndef CHAINB_LEAD
+#define CHAINB_LEAD 2
+#endif
+
+// lstm_tm_bwd_body (DZ + DX) with one dh element per lane from the stage above's stream
+// (or, stage 0, from global memory), un-pooled on load, and dx published element-wise.
+template <int H, int KX, int D>
+__device__ __forceinline__ void chain_bwd_stage(const ChainBStage& S, int tile, int ntiles, int Mp, unsigned tagb,
+                                                int* ctl, char* smem, bool src) {
+  using C = TMC<H>;
+  constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
+  constexpr int NXB = KX * 2;
+  constexpr int TX = (NXB + NW - 1) / NW;
+  static_assert(CPL == 1 && 16 * H == NT, "one dh element per lane");
+  using L = ChainBLds<H, KX>;
+  static_assert(L::BYTES <= CHAINB_LDS && L::ZS % 16 == 0 && L::DH % 16 == 0, "chain bwd LDS layout");
+  auto zs = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem);
+  auto dhs = reinterpret_cast<float (*)[16][C::HP]>(smem + L::ZS);
+  auto dxs = reinterpret_cast<float (*)[16][32 * KX]>(smem + L::ZS + L::DH);
+  auto wl = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem + L::ZS + L::DH + L::DX);
+
+  const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P, Ts = S.Ts;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, quad = lane >> 4;
+  const int row0 = tile * 16;
+
+  for (int i = tid; i < 2 * 16 * C::HP; i += NT) (&dhs[0][0][0])[i] = 0.f;
+
+  bf16x8_t ufr[KB];
+  const int unit = 4 * w + quad;
+  {
+    const int au = 4 * w + (col >> 2);
+#pragma unroll
+    for (int s = 0; s < KB; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float val = S.U[(size_t)au * G4 + 32 * s + 8 * quad + j];
+        v[j] = (__bf16)(val * ((col & 3) == 0 ? 1.f : 0.f));
+      }
+      ufr[s] = v;
+    }
+  }
+  bf16x8_t wfr[L::WL ? 1 : TX][L::WL ? 1 : KB];
+  if constexpr (L::WL) {     // W^T blocks [NXB][16 din][4H] in LDS
+    for (int i = tid; i < NXB * 16 * G4; i += NT) {
+      const int xb = i / (16 * G4), r = (i / G4) % 16, k = i % G4;
+      const int din = 16 * xb + r;
+      wl[xb][r][k] = (__bf16)(din < Dw ? S.W[(size_t)din * G4 + k] : 0.f);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < TX; ++q) {
+      const int xb = w + NW * q;
+      const int din = 16 * xb + col;
+#pragma unroll
+      for (int s = 0; s < KB; ++s) {
+        bf16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = (__bf16)(S.W[(size_t)min(din, Dw - 1) * G4 + 32 * s + 8 * quad + j] *
+                          ((xb < NXB && din < Dw) ? 1.f : 0.f));
+        wfr[q][s] = v;
+      }
+    }
+  }
+
+  // forward state ring (gates, c_t) and the dh element ring, D reverse steps ahead
+  float4 rg[D];
+  float rc[D];
+  unsigned long long rq[D];
+  unsigned ri[D];
+  auto sidx = [&](int tt) { return ((((size_t)tt * ntiles + tile) * NW + w)) * 64 + lane; };
+  // source time of the dh of time tt (-1: past the last pooling window -> zero gradient)
+  auto src_t = [&](int tt) { return P > 0 ? (tt < Ts * P ? tt / P : -1) : tt; };
+  const size_t eoff = (size_t)row0 * H + tid;        // this lane's dh element in a [Mp][H] row block
+  const size_t hstep = (size_t)Mp * H;
+  auto load = [&](int J, int SS) {
+    const int tt = max(T - 1 - SS, 0);
+    const size_t o = sidx(tt);
+    rg[J] = *reinterpret_cast<const float4*>(S.g + o * 4);
+    rc[J] = S.c[o];
+    const int st = max(src_t(tt), 0);
+    if (src) rq[J] = ld_granule(S.din + eoff + (size_t)st * hstep);
+    else rq[J] = (unsigned long long)__float_as_uint(S.dh[eoff + (size_t)st * hstep]);
+    ri[J] = P > 0 ? (unsigned)S.pidx[eoff + (size_t)st * hstep] : 0u;
+  };
+  // dh of time tt from ring slot J (tag-checked for a stream source)
+  auto stage_dh = [&](int J, int tt) -> float {
+    const int st = tt >= 0 ? src_t(tt) : -1;
+    if (src) {
+      const bool bad = st >= 0 && (unsigned)(rq[J] >> 32) != (tagb | (unsigned)st);
+      if (__builtin_amdgcn_ballot_w64(bad) != 0)
+        rq[J] = chain_wait(S.din + eoff + (size_t)max(st, 0) * hstep, tagb | (unsigned)max(st, 0), ctl);
+    }
+    const float v = __uint_as_float((unsigned)rq[J]);
+    const bool keep = st >= 0 && (P == 0 || ri[J] == (unsigned)(tt % P));
+    return keep ? v : 0.f;
+  };
+  // dz storer (one float4 granule of the [16][4H] tile per thread)
+  const int gz_seq = tid / (G4 / 4), gz_c = (tid % (G4 / 4)) * 4;
+  float* zbase = S.dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
+  const size_t zstep = (size_t)Mp * G4;
+  // dx: element e of the [16][Din] tile per lane (NQ passes, clamped duplicates: no branch)
+  const int nx = 16 * Din;
+  const size_t xstep = (size_t)Mp * Din;
+  const bool publish = S.sout != nullptr;
+  auto store_dx = [&](int buf, int ts, unsigned tag) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q * NT >= nx) break;                            // uniform
+      const int e = min(tid + q * NT, nx - 1);
+      const float v = dxs[buf][e / Din][e % Din];
+      const size_t o = (size_t)row0 * Din + e + (size_t)ts * xstep;
+      if (publish) st_granule(S.sout + o, v, tag);
+      else S.dx[o] = v;
+    }
+  };
+
+  if (src) {    // start once the stage above is D + LEAD steps ahead (see the forward)
+    int tw = T - 1 - (D + CHAINB_LEAD);
+    tw = max(tw, 0);
+    const int st = src_t(tw);
+    if (st >= 0) (void)chain_wait(S.din + eoff + (size_t)st * hstep, tagb | (unsigned)st, ctl);
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) load(j, j);
+  __syncthreads();
+  dhs[0][tid / H][tid % H] = stage_dh(0, T - 1);
+  load(0, D);
+  float dc = 0.f, dhr = 0.f, dhn;
+  __syncthreads();
+  dhn = dhs[0][col][unit];
+
+  for (int s0 = 0; s0 < T; s0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int s = s0 + j;
+      const int t = T - 1 - s;
+      const int p = s & 1;
+      const int jn = (j + 1 == D) ? 0 : j + 1;
+      {
+        const float cp = rc[jn] * (t > 0 ? 1.f : 0.f);
+        const float dh = dhn + dhr;
+        const float4 g4 = rg[j];
+        const float tc = tanhf_fast(rc[j]);
+        const float dct = dc + dh * g4.w * (1.f - tc * tc);
+        dc = dct * g4.y;
+        zs[p][col][0 * H + unit] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
+        zs[p][col][1 * H + unit] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
+        zs[p][col][2 * H + unit] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
+        zs[p][col][3 * H + unit] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
+      }
+      {   // state of step s + D and the dh of step s + 1 (time t - 1)
+        const int tt = max(T - 1 - (s + D), 0);
+        const size_t o = sidx(tt);
+        rg[j] = *reinterpret_cast<const float4*>(S.g + o * 4);
+        rc[j] = S.c[o];
+      }
+      dhs[p ^ 1][tid / H][tid % H] = stage_dh(jn, t - 1);
+      {
+        const int tt = max(T - 1 - (s + 1 + D), 0);
+        const int st = max(src_t(tt), 0);
+        if (src) rq[jn] = ld_granule(S.din + eoff + (size_t)st * hstep);
+        else rq[jn] = (unsigned long long)__float_as_uint(S.dh[eoff + (size_t)st * hstep]);
+        ri[jn] = P > 0 ? (unsigned)S.pidx[eoff + (size_t)st * hstep] : 0u;
+      }
+      lds_barrier();
+      dhn = dhs[p ^ 1][col][unit];
+      {   // serial chain: dh_{t-1} = U dz_t
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+          if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a1, 0, 0, 0);
+          else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a0, 0, 0, 0);
+        }
+        dhr = a0[0] + a1[0];
+      }
+      {   // dz tile -> HBM (weight-gradient pass)
+        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[p][gz_seq][gz_c]);
+        const int tz = t >= 0 ? t : T;
+        *reinterpret_cast<float4*>(zbase + (size_t)tz * zstep) =
+            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+      }
+      {   // previous step's dx tile (time t + 1) -> stream / HBM; steps outside write row T
+        const int ts = (s >= 1 && s <= T) ? t + 1 : T;
+        store_dx(p ^ 1, ts, tagb | (unsigned)ts);
+      }
+      if (t >= 0) {   // dx^T = W dz^T of this step
+#pragma unroll
+        for (int q = 0; q < TX; ++q) {
+          const int xb = w + NW * q;
+          if (xb < NXB) {
+            f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+              bf16x8_t wa;
+              if constexpr (L::WL) wa = *reinterpret_cast<const bf16x8_t*>(&wl[xb][col][32 * k + 8 * quad]);
+              else wa = wfr[q][k];
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bz, a, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dxs[p][col][16 * xb + 4 * quad + r] = a[r];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  store_dx((T - 1) & 1, 0, tagb);     // dx tile of t = 0
+}
+
+__global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
+  const int nblk = gridDim.x;
+  const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
+  if (s >= A.ns || tile >= A.ntiles) {
+    chain_finish(A.ctl, nblk);
+    return;
+  }
+  if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
+  const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned tagb = (E & 0xFFFFFu) << 12;
+  __shared__ __attribute__((aligned(16))) char smem[CHAINB_LDS];
+  const ChainBStage& S = A.st[s];
+  const int H = S.H, KX = S.KX;
+  const bool src = s > 0;
+#define GQ_CHAINB_BODY(HH, KXX, DD)                                                     \
+  {                                                                                     \
+    if (threadIdx.x >= TMC<HH>::NT) return;                                             \
+    chain_bwd_stage<HH, KXX, DD>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem, src);      \
+  }
+#ifdef CHAINB_ONLY
+  { GQ_CHAINB_BODY(CHAINB_ONLY, CHAINB_KX, (CHAINB_ONLY == 64 ? 2 : 4)) }
+#else
+  if (H == 16) { if (KX == 1) GQ_CHAINB_BODY(16, 1, 4) else GQ_CHAINB_BODY(16, 2, 4) }
+  else if (H == 32) { if (KX == 1) GQ_CHAINB_BODY(32, 1, 4) else GQ_CHAINB_BODY(32, 2, 4) }
+  else { if (KX == 1) GQ_CHAINB_BODY(64, 1, 2) else GQ_CHAINB_BODY(64, 2, 2) }
+#endif
+#undef GQ_CHAINB_BODY
+  __syncthreads();
+  if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+  chain_finish(A.ctl, nblk);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -457,6 +742,90 @@ std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at
   return res;
 }
 
+// Backward of a chain, stages listed TOP layer first. dh: gradient of the top layer's output
+// (pooled if pool[0] > 0); per stage the forward's g / c, W, U, the argmax bytes of the pool
+// after the layer (empty if none) and pool size; x_width[s]: channels of the layer's input
+// layout. Returns [dz_0 .. dz_{n-1}, dx of the bottom layer].
+std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, at::TensorList c, at::TensorList W,
+                                       at::TensorList U, at::TensorList pidx, at::IntArrayRef pool,
+                                       at::IntArrayRef x_width, at::IntArrayRef T_in) {
+  check_f32_cuda(dh, "dh");
+  const int ns = (int)W.size();
+  TORCH_CHECK(ns >= 2 && ns <= CHAIN_MAX && (int)U.size() == ns && (int)g.size() == ns && (int)c.size() == ns &&
+                  (int)pidx.size() == ns && (int)pool.size() == ns && (int)x_width.size() == ns &&
+                  (int)T_in.size() == ns, "lstm_chain_bwd: stage lists");
+  TORCH_CHECK(dh.dim() == 3 && dh.is_contiguous(), "lstm_chain_bwd: dh must be a contiguous [Ts, Mp, H]");
+  const int Mp = (int)dh.size(1);
+  TORCH_CHECK(Mp % 16 == 0, "lstm_chain_bwd: Mp");
+  const int ntiles = Mp / 16, nt8 = (ntiles + 7) / 8 * 8;
+  TORCH_CHECK(ns * nt8 <= 256, "lstm_chain_bwd: ", ns * nt8, " workgroups cannot all be resident");
+  c10::DeviceGuard guard(dh.device());
+  auto opt = dh.options();
+  ChainBArgs A{};
+  A.ns = ns;
+  A.ntiles = ntiles;
+  A.nt8 = nt8;
+  A.Mp = Mp;
+  A.ctl = chain_ctl(dh.get_device());
+  A.trace = chain_trace_buf(dh.get_device());
+  std::vector<at::Tensor> dzs, keep;
+  at::Tensor dx, prev;
+  for (int s = 0; s < ns; ++s) {
+    const int H = (int)U[s].size(0), Dw = (int)W[s].size(0), T = (int)T_in[s], Din = (int)x_width[s];
+    const int P = (int)pool[s];
+    TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_chain_bwd: hidden size ", H);
+    TORCH_CHECK(Dw <= Din && Din <= 64 && Din % 4 == 0 && T >= 1 && T < 4096, "lstm_chain_bwd: stage ", s, " shape");
+    for (const at::Tensor* t : {&g[s], &c[s], &W[s], &U[s]}) check_f32_cuda(*t, "lstm_chain_bwd operand");
+    TORCH_CHECK(g[s].numel() == (long)(T + 1) * Mp * H * 4 && c[s].numel() == (long)(T + 1) * Mp * H,
+                "lstm_chain_bwd: saved state shapes");
+    const int Ts = P > 0 ? T / P : T;
+    if (s == 0) {
+      TORCH_CHECK(dh.size(0) == Ts && dh.size(2) == H, "lstm_chain_bwd: dh shape");
+    } else {
+      TORCH_CHECK((int)x_width[s - 1] == H, "lstm_chain_bwd: stage ", s, " output width");
+      TORCH_CHECK((int)T_in[s - 1] == Ts, "lstm_chain_bwd: lengths");
+    }
+    if (P > 0) {
+      TORCH_CHECK(pidx[s].numel() == (long)Ts * Mp * H && pidx[s].scalar_type() == at::kByte,
+                  "lstm_chain_bwd: argmax bytes");
+    }
+    ChainBStage& S = A.st[s];
+    S.dh = s == 0 ? dh.data_ptr<float>() : nullptr;
+    S.din = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev.data_ptr<int64_t>());
+    S.pidx = P > 0 ? pidx[s].data_ptr<uint8_t>() : nullptr;
+    S.g = g[s].data_ptr<float>();
+    S.c = c[s].data_ptr<float>();
+    S.W = W[s].data_ptr<float>();
+    S.U = U[s].data_ptr<float>();
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, opt);
+    S.dz = dz.data_ptr<float>();
+    dzs.push_back(dz);
+    const bool last = s + 1 == ns;
+    if (!last) {
+      at::Tensor so = at::empty({T + 1, Mp, Din}, opt.dtype(at::kLong));
+      S.sout = reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>());
+      S.dx = nullptr;
+      keep.push_back(so);
+      prev = so;
+    } else {
+      dx = at::empty({T + 1, Mp, Din}, opt);
+      S.sout = nullptr;
+      S.dx = dx.data_ptr<float>();
+    }
+    S.H = H;
+    S.T = T;
+    S.Din = Din;
+    S.Dw = Dw;
+    S.KX = (Din + 31) / 32;
+    S.P = P;
+    S.Ts = Ts;
+  }
+  hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(ns * nt8), dim3(1024), 0, stream(), A);
+  GQ_LAUNCH_CHECK();
+  dzs.push_back(dx.narrow(0, 0, (int)T_in[ns - 1]));
+  return dzs;
+}
+
 // [epoch, finished, timeout flag, 0] of this device's chain control words (tests)
 at::Tensor lstm_chain_status(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
@@ -483,4 +852,5 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_fwd", &gq::lstm_chain_fwd);
   m.impl("lstm_chain_status", &gq::lstm_chain_status);
   m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
+  m.impl("lstm_chain_bwd", &gq::lstm_chain_bwd);
 }

@@ -370,6 +370,36 @@ class _HipLSTMChain(torch.autograd.Function):
         grads = [None] * (3 * ns)
         dh = dout.contiguous()
         dx = None
+
+        def layer_x(i):
+            if i == 0:
+                return x
+            return outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)]
+
+        if _chain_bwd_on() and chain_fits(dh.shape[1], ns) and all(layer_x(i).shape[-1] % 4 == 0 for i in range(ns)):
+            # all reverse recurrences in ONE cross-CU pipelined launch (dz of every layer + dx
+            # of the bottom one), then the weight-gradient passes
+            order = list(reversed(range(ns)))
+            e8 = x.new_zeros(0, dtype=torch.uint8)
+            res = ops.lstm_chain_bwd(dh, [outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
+                                     [Ws[i] for i in order], [Us[i] for i in order],
+                                     [outs[5 * i + 4] if pools[i] else e8 for i in order],
+                                     [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
+                                     [outs[5 * i].shape[0] for i in order])
+            for k, i in enumerate(order):
+                nw = need[2 + 3 * i:5 + 3 * i]
+                if not any(nw):
+                    continue
+                h = outs[5 * i]
+                xi = layer_x(i)
+                sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
+                if _pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0]):
+                    _pipe_push(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
+                else:
+                    ops.lstm_tm_grads(res[k], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
+                grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]
+            dx = res[ns]
+            return (dx if need[0] else None, None, *grads)
         for i in reversed(range(ns)):
             h, g, c, _, idx = outs[5 * i:5 * i + 5]
             T, Mp, H = h.shape
@@ -385,6 +415,12 @@ class _HipLSTMChain(torch.autograd.Function):
             grads[3 * i:3 * i + 3] = gr
             dh = dx
         return (dx if need[0] else None, None, *grads)
+
+
+def _chain_bwd_on() -> bool:
+    """Cross-CU pipelined backward of the chain (``GNNQC_CHAIN_BWD``, default on)."""
+    import os
+    return os.environ.get("GNNQC_CHAIN_BWD", "1") == "1"
 
 
 def _chain_on() -> bool:

@@ -612,8 +612,9 @@ def test_timelayer_pair_fusion_matches_unfused(cuda_device, monkeypatch):
         assert (a - b_).norm().item() <= 2e-2 * (b_.norm().item() + 1e-6)
 
 
+@pytest.mark.parametrize("bwd", ["chain", "per_layer"])
 @pytest.mark.parametrize("M", [128, 40, 300])
-def test_chain_forward_matches_per_layer(cuda_device, monkeypatch, M):
+def test_chain_forward_matches_per_layer(cuda_device, monkeypatch, M, bwd):
     """CML TimeLayer: the cross-CU pipelined stack forward (lstm_chain.hip) == the per-layer
     kernels (no pair fusion) for the output and every gradient; repeated launches (fresh
     epochs over reused stream buffers) stay identical and no consumer spin timed out."""
@@ -623,6 +624,7 @@ def test_chain_forward_matches_per_layer(cuda_device, monkeypatch, M):
     tl = TimeLayer(18, 16, 2, "lstm", pool_size=3).to(cuda_device)
     x = torch.randn(M, 181, 18, device=cuda_device)
     monkeypatch.setenv("GNNQC_NO_PAIR", "1")
+    monkeypatch.setenv("GNNQC_CHAIN_BWD", "1" if bwd == "chain" else "0")
 
     def run(chain):
         monkeypatch.setenv("GNNQC_CHAIN", "1" if chain else "0")
@@ -644,7 +646,7 @@ def test_chain_forward_matches_per_layer(cuda_device, monkeypatch, M):
     torch.cuda.synchronize()
     st1 = hip_ops().lstm_chain_status(x).cpu()
     assert int(st1[2]) == 0, "a consumer spin timed out"
-    assert int(st1[0]) - int(st0[0]) == 5 and int(st1[1]) == 0, (st0, st1)
+    assert int(st1[0]) - int(st0[0]) == (6 if bwd == "chain" else 5) and int(st1[1]) == 0, (st0, st1)
     torch.testing.assert_close(o1, o0, atol=1e-5, rtol=1e-5)
     for o in outs:
         assert torch.equal(o, o1)
