@@ -24,8 +24,9 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
     long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems) {
+  __shared__ __attribute__((aligned(16))) char smem[GradsLds<H, DT>::BYTES];
   lstm_grads_body<H, DT, GRX>(dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride, lddx, xg,
-                              x_elems, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
+                              x_elems, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, smem);
 }
 
 __global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __restrict__ ws, int splits, int RC,

@@ -19,21 +19,34 @@ constexpr int GR_LDR = GR_ROWS + 8; // padded LDS row length (bf16) of transpose
 // read-modify-write into the gradient buffers: deterministic, no float atomics).
 // (device body: cb / split / ncbv / splits are the virtual block coordinates, so the same code
 // runs as its own kernel or as extra workgroups of a recurrence launch; needs 256 threads)
+// LDS of one body instance (the caller owns the buffer: a kernel holding several instances
+// then reserves the largest one instead of their sum)
+template <int H, int DT>
+struct GradsLds {
+  static constexpr int DZT = GR_CB * GR_LDR * 2;
+  static constexpr int DZR = GR_ROWS * (GR_CB + 8) * 2;
+  static constexpr int XT = DT * 16 * GR_LDR * 2;
+  static constexpr int HT = H * GR_LDR * 2;
+  static constexpr int BYTES = DZT + DZR + XT + HT;
+};
+
 template <int H, int DT, int GRX>
 __device__ __forceinline__ void lstm_grads_body(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
     long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems, int cb, int split,
-    int ncbv, int splits) {
+    int ncbv, int splits, char* __restrict__ smem) {
   constexpr int G4 = 4 * H;
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
   constexpr int XGM = (GR_ROWS * 144 / GRX + 255) / 256;   // max x granules per thread
   constexpr int HG = (GR_ROWS * H / 4 + 255) / 256;        // h float4 granules per thread
-  __shared__ __attribute__((aligned(16))) __bf16 dzT[GR_CB][GR_LDR];          // [gu][row]
-  __shared__ __attribute__((aligned(16))) __bf16 dzR[GR_ROWS][GR_CB + 8];     // [row][gu]
-  __shared__ __attribute__((aligned(16))) __bf16 xT[DP][GR_LDR];             // [din][row]
-  __shared__ __attribute__((aligned(16))) __bf16 hT[H][GR_LDR];              // [k][row]
+  using L = GradsLds<H, DT>;
+  static_assert(L::DZT % 16 == 0 && L::DZR % 16 == 0 && L::XT % 16 == 0, "grads LDS layout");
+  auto dzT = reinterpret_cast<__bf16 (*)[GR_LDR]>(smem);                              // [gu][row]
+  auto dzR = reinterpret_cast<__bf16 (*)[GR_CB + 8]>(smem + L::DZT);                  // [row][gu]
+  auto xT = reinterpret_cast<__bf16 (*)[GR_LDR]>(smem + L::DZT + L::DZR);             // [din][row]
+  auto hT = reinterpret_cast<__bf16 (*)[GR_LDR]>(smem + L::DZT + L::DZR + L::XT);     // [k][row]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

@@ -783,8 +783,11 @@ __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
   const int gb = b - ntiles;
   if (gb < gj.nblocks) {
     if constexpr (HG > 0)
+      {
+      __shared__ __attribute__((aligned(16))) char gsm[GradsLds<HG, DT>::BYTES];
       lstm_grads_body<HG, DT, 4>(gj.dz, gj.x, gj.h, gj.W, nullptr, gj.ws, gj.rows, gj.period, gj.hshift, gj.Din,
-                                 gj.ldx, 0, gj.Din, gj.xg, gj.x_elems, gb % gj.ncb, gb / gj.ncb, gj.ncb, gj.splits);
+                                 gj.ldx, 0, gj.Din, gj.xg, gj.x_elems, gb % gj.ncb, gb / gj.ncb, gj.ncb, gj.splits, gsm);
+    }
     return;
   }
   const int rb = gb - gj.nblocks;
@@ -1163,6 +1166,135 @@ at::Tensor lstm_tm_bwd_pipe(const at::Tensor& dh, const at::Tensor& g, const at:
   return dz;
 }
 
+// ---- all pending weight-gradient jobs in ONE launch, then all reductions in ONE launch
+// (after the chain backward, whose recurrences leave no per-layer launch to hide them in)
+static constexpr int MULTI_MAX = 12;
+struct MultiGrad {
+  GradJob j[MULTI_MAX];
+  int start[MULTI_MAX + 1];
+  int key[MULTI_MAX];              // HG * 8 + DT
+  int n;
+};
+struct MultiRed {
+  RedJob j[MULTI_MAX];
+  int start[MULTI_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void lstm_grads_multi_kernel(MultiGrad M) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < M.n && b >= M.start[k + 1]) ++k;        // uniform
+  const GradJob gj = M.j[k];                              // by value: scalar loads, no scratch copy
+  const int gb = b - M.start[k];
+  __shared__ __attribute__((aligned(16))) char smem[GradsLds<128, 5>::BYTES];   // the largest instance
+#define GQ_MG(HG, DT)                                                                                    \
+  case HG * 8 + DT:                                                                                      \
+    lstm_grads_body<HG, DT, 4>(gj.dz, gj.x, gj.h, gj.W, nullptr, gj.ws, gj.rows, gj.period, gj.hshift, gj.Din, \
+                               gj.ldx, 0, gj.Din, gj.xg, gj.x_elems, gb % gj.ncb, gb / gj.ncb, gj.ncb, gj.splits, \
+                               smem);                                                                    \
+    break;
+#define GQ_MG_H(HG) GQ_MG(HG, 1) GQ_MG(HG, 2) GQ_MG(HG, 3) GQ_MG(HG, 4) GQ_MG(HG, 5)
+  switch (M.key[k]) {
+    GQ_MG_H(16) GQ_MG_H(32) GQ_MG_H(64) GQ_MG_H(128)
+    default: break;
+  }
+#undef GQ_MG_H
+#undef GQ_MG
+}
+
+__global__ __launch_bounds__(256) void lstm_grads_reduce_multi_kernel(MultiRed M) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < M.n && b >= M.start[k + 1]) ++k;
+  const RedJob rj = M.j[k];
+  lstm_grads_reduce_body(rj.ws, rj.splits, rj.RC, nullptr, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db, rj.dU,
+                         b - M.start[k], 0, 1);
+}
+
+// grads of jobs (dz, x, h, W, period, hshift, ws) then reductions of rjobs (ws, W, dW, dU, db):
+// a reduce job may be one of this call's grads jobs (stream order runs the grads first)
+void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, at::TensorList gW,
+                      at::IntArrayRef period, at::IntArrayRef hshift, at::TensorList gws, at::TensorList rws,
+                      at::TensorList rW, at::TensorList rdW, at::TensorList rdU, at::TensorList rdb) {
+  const int ng = (int)gz.size(), nr = (int)rws.size();
+  TORCH_CHECK(ng <= MULTI_MAX && nr <= MULTI_MAX && (int)gx.size() == ng && (int)gh.size() == ng &&
+                  (int)gW.size() == ng && (int)period.size() == ng && (int)hshift.size() == ng &&
+                  (int)gws.size() == ng && (int)rW.size() == nr && (int)rdW.size() == nr && (int)rdU.size() == nr &&
+                  (int)rdb.size() == nr, "lstm_grads_multi: job lists");
+  if (ng + nr == 0) return;
+  c10::DeviceGuard guard(ng ? gz[0].device() : rws[0].device());
+  auto st = stream();
+  if (ng) {
+    MultiGrad M{};
+    M.n = ng;
+    int nb = 0;
+    for (int k = 0; k < ng; ++k) {
+      for (const at::Tensor* t : {&gz[k], &gh[k], &gW[k], &gws[k]}) check_f32_cuda(*t, "lstm_grads_multi operand");
+      TORCH_CHECK(gx[k].is_cuda() && gx[k].scalar_type() == at::kFloat, "lstm_grads_multi: x");
+      const int HG = (int)gW[k].size(1) / 4, Dw = (int)gW[k].size(0);
+      TORCH_CHECK(HG == 16 || HG == 32 || HG == 64 || HG == 128, "lstm_grads_multi: hidden size");
+      TORCH_CHECK(grads_job_ok(gx[k], Dw), "lstm_grads_multi: x layout");
+      const int DT = (Dw + 1 + 15) / 16;
+      GradJob& j = M.j[k];
+      j.dz = gz[k].data_ptr<float>();
+      j.x = gx[k].data_ptr<float>();
+      j.h = gh[k].data_ptr<float>();
+      j.W = gW[k].data_ptr<float>();
+      j.ws = gws[k].data_ptr<float>();
+      j.ldx = (int)gx[k].stride(-2);
+      j.rows = gx[k].numel() / gx[k].size(-1);
+      j.period = period[k];
+      j.hshift = hshift[k];
+      j.x_elems = (long)(gx[k].storage().nbytes() / sizeof(float)) - gx[k].storage_offset();
+      j.Din = Dw;
+      j.xg = (int)((32L * j.ldx / 4 + 255) / 256);
+      j.ncb = lstm_grads_col_blocks(HG);
+      const long RC = (long)(DT + HG / 16) * 1024 * j.ncb;
+      j.splits = (int)(gws[k].numel() / RC);
+      TORCH_CHECK(j.splits >= 1 && j.splits <= PIPE_MAX_SPLITS && gws[k].numel() == j.splits * RC,
+                  "lstm_grads_multi: workspace size");
+      j.nblocks = j.ncb * j.splits;
+      M.key[k] = HG * 8 + DT;
+      M.start[k] = nb;
+      nb += j.nblocks;
+    }
+    M.start[ng] = nb;
+    hipLaunchKernelGGL(lstm_grads_multi_kernel, dim3(nb), dim3(256), 0, st, M);
+    GQ_LAUNCH_CHECK();
+  }
+  if (nr) {
+    MultiRed R{};
+    R.n = nr;
+    int nb = 0;
+    for (int k = 0; k < nr; ++k) {
+      RedJob& r = R.j[k];
+      r.H = (int)rW[k].size(1) / 4;
+      r.Din = (int)rW[k].size(0);
+      r.DT = (r.Din + 1 + 15) / 16;
+      r.HT = r.H / 16;
+      r.ncb = lstm_grads_col_blocks(r.H);
+      r.RC = (r.DT + r.HT) * 1024 * r.ncb;
+      r.splits = (int)(rws[k].numel() / r.RC);
+      TORCH_CHECK(r.splits >= 1 && r.splits <= PIPE_MAX_SPLITS && rws[k].numel() == (long)r.splits * r.RC,
+                  "lstm_grads_multi: reduce workspace size");
+      TORCH_CHECK(rdW[k].numel() == rW[k].numel() && rdU[k].numel() == (long)r.H * 4 * r.H &&
+                      rdb[k].numel() == 4 * r.H, "lstm_grads_multi: gradient buffers");
+      r.ws = rws[k].data_ptr<float>();
+      r.dW = rdW[k].data_ptr<float>();
+      r.dU = rdU[k].data_ptr<float>();
+      r.db = rdb[k].data_ptr<float>();
+      r.nblocks = (r.RC + 15) / 16;
+      r.kb = 1;
+      R.start[k] = nb;
+      nb += r.nblocks;
+    }
+    R.start[nr] = nb;
+    hipLaunchKernelGGL(lstm_grads_reduce_multi_kernel, dim3(nb), dim3(256), 0, st, R);
+    GQ_LAUNCH_CHECK();
+  }
+}
+
 // Weight gradients (+ dx) of one time-major layer from its dz (lstm_grads_rows): accumulates
 // dW, dU, db; returns dx [T, Mp, Din] if need_dx.
 at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
@@ -1258,5 +1390,6 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_tm_bwd_dz", &gq::lstm_tm_bwd_dz);
   m.impl("lstm_tm_bwd_pipe", &gq::lstm_tm_bwd_pipe);
   m.impl("lstm_grads_job_ws", &gq::lstm_grads_job_ws);
+  m.impl("lstm_grads_multi", &gq::lstm_grads_multi);
   m.impl("lstm_tm_bwd", &gq::lstm_tm_bwd);
 }

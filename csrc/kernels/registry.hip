@@ -36,6 +36,8 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
   m.def("lstm_chain_fwd(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train) -> Tensor[]");
   m.def("lstm_chain_status(Tensor like) -> Tensor");
+  m.def("lstm_grads_multi(Tensor[] gz, Tensor[] gx, Tensor[] gh, Tensor[] gW, int[] period, int[] hshift, "
+        "Tensor[] gws, Tensor[] rws, Tensor[] rW, Tensor(a!)[] rdW, Tensor(b!)[] rdU, Tensor(c!)[] rdb) -> ()");
   m.def("lstm_chain_trace(Tensor like) -> Tensor");
   m.def("lstm_chain_bwd(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");

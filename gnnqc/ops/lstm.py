@@ -127,6 +127,7 @@ class _Pipe:
 
     job = None      # layer whose weight-gradient pass has not run yet
     red = None      # layer whose gradient pass ran; its split reduction has not
+    batch = []      # jobs of a chain backward: all gradient passes in one launch at the flush
 
 
 # Largest sequence count (rows of 16-sequence tiles) a recurrence may have for its layer to
@@ -134,6 +135,9 @@ class _Pipe:
 # (CML: 8 tiles). With hundreds of tiles (SoilNet: 418) they compete with the recurrence
 # for the CUs and the step got slower (6.11 vs 5.15 ms), so such layers keep the fused path.
 PIPE_MAX_SEQ = 2048
+
+
+_MULTI_MAX = 12        # jobs per lstm_grads_multi launch (lstm_tm.hip MULTI_MAX)
 
 
 def _pipe_on(sinks, n_seq: int) -> bool:
@@ -170,7 +174,18 @@ def _pipe_drain_one():
 
 
 def pipe_flush():
-    """Run all pending weight-gradient / reduction work (end of the backward)."""
+    """Run all pending weight-gradient / reduction work (end of the backward). With a chain
+    backward's batch: every pending gradient pass in ONE launch, every reduction in one more."""
+    if _Pipe.batch:
+        from ..utils.native import hip_ops
+        grads = ([_Pipe.job] if _Pipe.job is not None else []) + _Pipe.batch
+        reds = ([_Pipe.red] if _Pipe.red is not None else []) + grads
+        hip_ops().lstm_grads_multi([j["dz"] for j in grads], [j["x"] for j in grads], [j["h"] for j in grads],
+                                   [j["W"] for j in grads], [j["period"] for j in grads],
+                                   [j["hshift"] for j in grads], [j["ws"] for j in grads],
+                                   [r["ws"] for r in reds], [r["W"] for r in reds], [r["g"][0] for r in reds],
+                                   [r["g"][1] for r in reds], [r["g"][2] for r in reds])
+        _Pipe.job, _Pipe.red, _Pipe.batch = None, None, []
     while _Pipe.job is not None or _Pipe.red is not None:
         _pipe_drain_one()
 
@@ -214,7 +229,7 @@ def direct_grad_accumulation(flag: bool = True):
         yield
     finally:
         _DirectGrad.enabled = prev
-        if _Pipe.job is not None or _Pipe.red is not None:
+        if _Pipe.job is not None or _Pipe.red is not None or _Pipe.batch:
             pipe_flush()
         if _DirectGrad.pending and torch.cuda.is_available():
             join_side_streams()
@@ -393,8 +408,9 @@ class _HipLSTMChain(torch.autograd.Function):
                 h = outs[5 * i]
                 xi = layer_x(i)
                 sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
-                if _pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0]):
-                    _pipe_push(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
+                if (_pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
+                        and len(_Pipe.batch) < _MULTI_MAX - 2):
+                    _Pipe.batch.append(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
                 else:
                     ops.lstm_tm_grads(res[k], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
                 grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]

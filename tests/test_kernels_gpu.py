@@ -741,7 +741,7 @@ def test_pipe_lstm_backward_gradients(cuda_device, cml_windows, monkeypatch, ds)
             p.grad = torch.zeros_like(p)
         with direct_grad_accumulation(True):
             model.logits(inputs).float().square().mean().backward()
-        assert _Pipe.job is None and _Pipe.red is None
+        assert _Pipe.job is None and _Pipe.red is None and not _Pipe.batch
         torch.cuda.synchronize()
         return [p.grad.clone() for p in model.parameters()]
 
