@@ -1208,8 +1208,12 @@ __global__ __launch_bounds__(256) void lstm_grads_reduce_multi_kernel(MultiRed M
   int k = 0;
   while (k + 1 < M.n && b >= M.start[k + 1]) ++k;
   const RedJob rj = M.j[k];
-  lstm_grads_reduce_body(rj.ws, rj.splits, rj.RC, nullptr, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db, rj.dU,
-                         b - M.start[k], 0, 1);
+  if (rj.kb > 1)
+    lstm_grads_reduce_multi<PIPE_RED_KB>(rj.ws, rj.splits, rj.RC, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
+                                         rj.dU, b - M.start[k]);
+  else
+    lstm_grads_reduce_body(rj.ws, rj.splits, rj.RC, nullptr, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
+                           rj.dU, b - M.start[k], 0, 1);
 }
 
 // grads of jobs (dz, x, h, W, period, hshift, ws) then reductions of rjobs (ws, W, dW, dU, db):
@@ -1284,8 +1288,8 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
       r.dW = rdW[k].data_ptr<float>();
       r.dU = rdU[k].data_ptr<float>();
       r.db = rdb[k].data_ptr<float>();
-      r.nblocks = (r.RC + 15) / 16;
-      r.kb = 1;
+      r.kb = (r.RC + 15) / 16 > 1024 ? PIPE_RED_KB : 1;    // wide jobs: KB slot blocks per workgroup
+      r.nblocks = (r.RC + 16 * r.kb - 1) / (16 * r.kb);
       R.start[k] = nb;
       nb += r.nblocks;
     }
