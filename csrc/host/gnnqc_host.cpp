@@ -76,11 +76,13 @@ void rolling_row(const float* x, int64_t n, int64_t w, int64_t minp, float* mean
   }
 }
 
-uint32_t crc_table[8][256];
-bool crc_init_done = false;
+struct CrcTable {
+  uint32_t v[8][256];
+  CrcTable();
+};
 
-void crc_init() {
-  if (crc_init_done) return;
+CrcTable::CrcTable() {
+  uint32_t (&crc_table)[8][256] = v;
   const uint32_t poly = 0x82F63B78u;
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
@@ -90,11 +92,17 @@ void crc_init() {
   for (uint32_t i = 0; i < 256; ++i)
     for (int t = 1; t < 8; ++t)
       crc_table[t][i] = (crc_table[t - 1][i] >> 8) ^ crc_table[0][crc_table[t - 1][i] & 0xFF];
-  crc_init_done = true;
+}
+
+// slicing-by-8 tables, built once (thread-safe function-local static: the record
+// readers may call in from several Python threads)
+const uint32_t (&crc_tables())[8][256] {
+  static const CrcTable tab;
+  return tab.v;
 }
 
 uint32_t crc32c_sw(uint32_t crc, const uint8_t* p, size_t n) {
-  crc_init();
+  const uint32_t (&crc_table)[8][256] = crc_tables();
   crc = ~crc;
   while (n >= 8) {
     uint64_t v;
@@ -115,6 +123,9 @@ uint32_t crc32c_sw(uint32_t crc, const uint8_t* p, size_t n) {
 extern "C" {
 
 int gq_version() { return 1; }
+
+// portable slicing-by-8 path (used where SSE4.2 is absent; tested against the hardware path)
+uint32_t gq_crc32c_sw(const uint8_t* data, uint64_t n, uint32_t init) { return crc32c_sw(init, data, n); }
 
 // x: [rows, n] row-major. Any output pointer may be null.
 void gq_rolling_stats(const float* x, int64_t rows, int64_t n, int64_t window, int64_t min_periods,
