@@ -76,6 +76,30 @@ __device__ __forceinline__ float row_gather(const unsigned* __restrict__ row, in
   return acc;
 }
 
+// V consecutive channels c0..c0+V-1 at once (one ds_read_b128 per neighbour when V == 4;
+// vals 16-byte aligned, F and c0 multiples of V): one bit walk per V channels
+template <int V>
+__device__ __forceinline__ void row_gather_v(const unsigned* __restrict__ row, int NWd, const float* __restrict__ vals,
+                                             int F, int c0, float (&acc)[V]) {
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.f;
+  for (int w = 0; w < NWd; ++w) {
+    unsigned m = row[w];
+    while (m) {
+      const int q = __builtin_ctz(m);
+      m &= m - 1u;
+      const float* p = vals + (32 * w + q) * F + c0;
+      if constexpr (V == 4) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += p[v];
+      }
+    }
+  }
+}
+
 struct NodeSmem {
   unsigned* bits;
   float* vals;
@@ -83,18 +107,18 @@ struct NodeSmem {
   float* mk;
   __device__ NodeSmem(unsigned char* base, int N, int NWd, int F) {
     bits = reinterpret_cast<unsigned*>(base);
-    vals = reinterpret_cast<float*>(bits + (size_t)N * NWd);
+    vals = reinterpret_cast<float*>(bits + ((size_t)N * NWd + 3) / 4 * 4);   // 16-byte aligned rows
     rs = vals + (size_t)N * F;
     mk = rs + N;
   }
 };
 
 static size_t node_smem_bytes(int N, int NWd, int F) {
-  return (size_t)N * NWd * 4 + (size_t)N * F * 4 + (size_t)N * 8;
+  return ((size_t)N * NWd + 3) / 4 * 16 + (size_t)N * F * 4 + (size_t)N * 8;
 }
 
 // ------------------------------------------------------------------ forward
-template <int Cin>
+template <int Cin, int V>
 __global__ __launch_bounds__(256) void gcn_node_fwd_kernel(
     const float* __restrict__ x, const unsigned* __restrict__ bits, const float* __restrict__ rs,
     const float* __restrict__ mask, const float* __restrict__ W, const float* __restrict__ bias,
@@ -127,12 +151,26 @@ __global__ __launch_bounds__(256) void gcn_node_fwd_kernel(
     }
     __syncthreads();
     float* ot = out + ((long)t * Mp + (long)b * N) * Cp;
-    for (int e = tid; e < N * Cp; e += 256) {
-      const int i = e / Cp, c = e % Cp;
-      float v = 0.f;
-      if (c < F) v = row_gather(sm.bits + (size_t)i * NWd, NWd, sm.vals, F, c) * sm.rs[i];
-      else if (c < F + Cin) v = xt[i * Cin + (c - F)];
-      ot[e] = v;
+    // V output channels per item (F, Cp multiples of V): aggregated groups walk the row mask once
+    const int G = Cp / V;
+    for (int e = tid; e < N * G; e += 256) {
+      const int i = e / G, c0 = (e - i * G) * V;
+      float v[V];
+      if (c0 < F) {
+        row_gather_v<V>(sm.bits + (size_t)i * NWd, NWd, sm.vals, F, c0, v);
+        const float r = sm.rs[i];
+#pragma unroll
+        for (int u = 0; u < V; ++u) v[u] *= r;
+      } else {
+#pragma unroll
+        for (int u = 0; u < V; ++u) v[u] = c0 + u < F + Cin ? xt[i * Cin + (c0 + u - F)] : 0.f;
+      }
+      if constexpr (V == 4) {
+        *reinterpret_cast<float4*>(ot + (long)i * Cp + c0) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < V; ++u) ot[(long)i * Cp + c0 + u] = v[u];
+      }
     }
   }
   if (b == B - 1) {                            // zero the padding rows B*N .. Mp-1
@@ -144,7 +182,7 @@ __global__ __launch_bounds__(256) void gcn_node_fwd_kernel(
 
 // ------------------------------------------------------------------ backward (params)
 // partial[blk][q][f], q: 0 = sum dy, 1 = sum dy*z, 2 = sum da*y[y<=0], 3+k = sum x_k dy
-template <int Cin>
+template <int Cin, int V>
 __global__ __launch_bounds__(256) void gcn_node_bwd_kernel(
     const float* __restrict__ x, const unsigned* __restrict__ bitsT, const float* __restrict__ rs,
     const float* __restrict__ mask, const float* __restrict__ dout, const float* __restrict__ W,
@@ -161,13 +199,23 @@ __global__ __launch_bounds__(256) void gcn_node_bwd_kernel(
     sm.mk[i] = mask[(long)b * N + i];
   }
   const int f = tid % F;
-  float wk[Cin];
+  // gather phase: V channels c0..c0+V-1 per item (G = F / V groups; 256 % G == 0, so fixed per thread)
+  const int G = F / V, c0 = (tid % G) * V;
+  float wk[V][Cin], bb[V], sc[V], sh[V], al[V];
 #pragma unroll
-  for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + f];
-  const float bb = bias[f], sc = scale[f], sh = shift[f], al = alpha[f];
-  float acc[NACC];
+  for (int v = 0; v < V; ++v) {
 #pragma unroll
-  for (int q = 0; q < NACC; ++q) acc[q] = 0.f;
+    for (int k = 0; k < Cin; ++k) wk[v][k] = W[k * F + c0 + v];
+    bb[v] = bias[c0 + v];
+    sc[v] = scale[c0 + v];
+    sh[v] = shift[c0 + v];
+    al[v] = alpha[c0 + v];
+  }
+  float acc[V][NACC];
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) acc[v][q] = 0.f;
   const int t1 = min(t0 + tchunk, T);
   for (int t = t0; t < t1; ++t) {
     __syncthreads();
@@ -178,34 +226,39 @@ __global__ __launch_bounds__(256) void gcn_node_bwd_kernel(
     }
     __syncthreads();
     const float* xt = x + ((long)b * T + t) * (long)N * Cin;
-    for (int e = tid; e < N * F; e += 256) {
-      const int j = e / F;
+    for (int e = tid; e < N * G; e += 256) {
+      const int j = e / G;
       if (sm.mk[j] == 0.f) continue;               // masked node: activation forced to 0
-      const float da = row_gather(sm.bits + (size_t)j * NWd, NWd, sm.vals, F, f);
+      float da[V];
+      row_gather_v<V>(sm.bits + (size_t)j * NWd, NWd, sm.vals, F, c0, da);
       float xv[Cin];
-      float z = bb;
 #pragma unroll
-      for (int k = 0; k < Cin; ++k) {
-        xv[k] = xt[j * Cin + k];
-        z += xv[k] * wk[k];
+      for (int k = 0; k < Cin; ++k) xv[k] = xt[j * Cin + k];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float z = bb[v];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) z += xv[k] * wk[v][k];
+        const float y = z * sc[v] + sh[v];
+        const float dy = y > 0.f ? da[v] : al[v] * da[v];
+        acc[v][0] += dy;
+        acc[v][1] += dy * z;
+        acc[v][2] += y > 0.f ? 0.f : da[v] * y;
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) acc[v][3 + k] += xv[k] * dy;
       }
-      const float y = z * sc + sh;
-      const float dy = y > 0.f ? da : al * da;
-      acc[0] += dy;
-      acc[1] += dy * z;
-      acc[2] += y > 0.f ? 0.f : da * y;
-#pragma unroll
-      for (int k = 0; k < Cin; ++k) acc[3 + k] += xv[k] * dy;
     }
   }
   __shared__ float red[4][NACC][64];
   const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
-  for (int q = 0; q < NACC; ++q) {
-    float v = acc[q];
-    for (int o = 32; o >= F; o >>= 1) v += __shfl_xor(v, o, 64);
-    red[wv][q][lane] = v;
-  }
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) {
+      float a = acc[v][q];
+      for (int o = 32; o >= G; o >>= 1) a += __shfl_xor(a, o, 64);
+      if (lane < G) red[wv][q][lane * V + v] = a;  // lane g holds channels g*V .. g*V+V-1
+    }
   __syncthreads();
   const long blk = (long)blockIdx.y * gridDim.x + blockIdx.x;
   for (int e = tid; e < NACC * F; e += 256) {
@@ -283,6 +336,15 @@ __global__ __launch_bounds__(256) void gcn_node_bwd_input_kernel(
     default: TORCH_CHECK(false, "gcn_node: 1..4 input channels"); \
   }
 
+#define GQ_NODE_V_DISPATCH(VEC, ...)                   \
+  if (VEC) {                                           \
+    constexpr int VV = 4;                              \
+    __VA_ARGS__;                                       \
+  } else {                                             \
+    constexpr int VV = 1;                              \
+    __VA_ARGS__;                                       \
+  }
+
 struct NodeGeom {
   int B, T, N, Cin, F, NWd, tchunk;
   size_t smem;
@@ -352,13 +414,14 @@ at::Tensor gcn_node_fwd(const at::Tensor& x, const at::Tensor& bits, const at::T
   TORCH_CHECK(rs.numel() == (long)g.B * g.N && mask.numel() == (long)g.B * g.N, "gcn_node_fwd: rs/mask shape");
   c10::DeviceGuard guard(x.device());
   at::Tensor out = at::empty({g.T, Mp, Cp}, x.options());
-  GQ_NODE_CIN_DISPATCH(g.Cin,
-      allow_smem(gcn_node_fwd_kernel<CIN>, g.smem);
-      hipLaunchKernelGGL(gcn_node_fwd_kernel<CIN>, g.grid, dim3(256), g.smem, stream(), x.data_ptr<float>(),
+  const bool vec = g.F % 4 == 0 && Cp % 4 == 0;
+  GQ_NODE_CIN_DISPATCH(g.Cin, GQ_NODE_V_DISPATCH(vec,
+      allow_smem(gcn_node_fwd_kernel<CIN, VV>, g.smem);
+      hipLaunchKernelGGL((gcn_node_fwd_kernel<CIN, VV>), g.grid, dim3(256), g.smem, stream(), x.data_ptr<float>(),
                          reinterpret_cast<const unsigned*>(bits.data_ptr<int>()), rs.data_ptr<float>(),
                          mask.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(),
                          shift.data_ptr<float>(), alpha.data_ptr<float>(), out.data_ptr<float>(), g.B, g.T, g.N, g.F,
-                         (int)Cp, (int)Mp, g.NWd, g.tchunk));
+                         (int)Cp, (int)Mp, g.NWd, g.tchunk)));
   GQ_LAUNCH_CHECK();
   return out;
 }
@@ -374,14 +437,14 @@ at::Tensor gcn_node_bwd(const at::Tensor& x, const at::Tensor& bitsT, const at::
   c10::DeviceGuard guard(x.device());
   const int nacc = 3 + g.Cin;
   at::Tensor partial = at::empty({(long)g.grid.x * g.grid.y, nacc, g.F}, x.options());
-  GQ_NODE_CIN_DISPATCH(g.Cin,
-      allow_smem(gcn_node_bwd_kernel<CIN>, g.smem);
-      hipLaunchKernelGGL(gcn_node_bwd_kernel<CIN>, g.grid, dim3(256), g.smem, stream(), x.data_ptr<float>(),
+  GQ_NODE_CIN_DISPATCH(g.Cin, GQ_NODE_V_DISPATCH(g.F % 4 == 0,
+      allow_smem(gcn_node_bwd_kernel<CIN, VV>, g.smem);
+      hipLaunchKernelGGL((gcn_node_bwd_kernel<CIN, VV>), g.grid, dim3(256), g.smem, stream(), x.data_ptr<float>(),
                          reinterpret_cast<const unsigned*>(bitsT.data_ptr<int>()), rs.data_ptr<float>(),
                          mask.data_ptr<float>(), dout.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(),
                          scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
                          partial.data_ptr<float>(), g.B, g.T, g.N, g.F, (int)dout.size(2), (int)dout.size(1), g.NWd,
-                         g.tchunk));
+                         g.tchunk)));
   GQ_LAUNCH_CHECK();
   return colsum(partial);
 }

@@ -238,7 +238,7 @@ def gcn_node_tm_ok(x: torch.Tensor, W: torch.Tensor, aggregate: str, dropout: fl
     from . import use_hip
     F_ = W.shape[1]
     N = x.shape[2]
-    lds = N * ((N + 31) // 32) * 4 + N * F_ * 4 + N * 8
+    lds = (N * ((N + 31) // 32) + 3) // 4 * 16 + N * F_ * 4 + N * 8     # gcn_node.hip node_smem_bytes
     return (use_hip(x) and aggregate in ("mean", "sum") and not (dropout and training) and x.shape[-1] <= 4
             and F_ <= 64 and 64 % F_ == 0 and lds <= 150 * 1024)
 

@@ -486,12 +486,13 @@ def _soil_graph(B, N, gen, dev):
 
 @pytest.mark.parametrize("training", [True, False])
 @pytest.mark.parametrize("aggregate", ["mean", "sum"])
-def test_gcn_node_tm_matches_eager(cuda_device, training, aggregate):
+@pytest.mark.parametrize("F", [16, 2])      # 16: 4-channel vector gather path, 2: scalar path
+def test_gcn_node_tm_matches_eager(cuda_device, training, aggregate, F):
     """Per-node GeneralConv kernel (SoilNet): time-major output and every gradient vs fp64 eager."""
     from gnnqc.ops.gcn import gcn_node_tm, gcn_node_tm_eager
     dev = cuda_device
     gen = torch.Generator().manual_seed(5 + training + 2 * (aggregate == "sum"))
-    B, T, N, Cin, F = 3, 9, 45, 3, 16
+    B, T, N, Cin = 3, 9, 45, 3
     adj, mask = _soil_graph(B, N, gen, dev)
     x = (torch.randn(B, T, N, Cin, generator=gen).to(dev)) * mask[:, None, :, None]
     W = (torch.randn(Cin, F, generator=gen) * 0.5).to(dev)
