@@ -11,6 +11,7 @@ on the device and are only read at epoch end - no host sync per step.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -88,6 +89,10 @@ class Trainer:
         self.batch_size = int(batch_size)
         self.train_metrics = MetricAccumulator(self.device)
         self.graph = None
+        # DP (or GNNQC_SPLIT_OPT_GRAPH=1): the optimizer runs after the all-reduce, so it
+        # is captured as a second small graph instead of being launched eagerly each step
+        self.split_opt = self.world > 1 or os.environ.get("GNNQC_SPLIT_OPT_GRAPH", "0") == "1"
+        self.opt_graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
         self.last_loss = torch.zeros((), device=self.device)
         self.global_step = 0
@@ -135,7 +140,7 @@ class Trainer:
     def _capture(self):
         # warm up on a side stream (allocator + lazy init), then capture
         snap = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
-        with_opt = self.world == 1
+        with_opt = not self.split_opt
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -146,6 +151,10 @@ class Trainer:
         it0 = self.opt.iterations
         with torch.cuda.graph(self.graph):
             self._body(self.static_wids, with_opt=with_opt)
+        if self.split_opt:
+            self.opt_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.opt_graph):
+                self.opt.step(grad_scale=1.0 / self.world)
         self.opt.iterations = it0          # capture runs nothing; replays count steps
         # undo warm-up side effects (BN running stats, metric sums)
         with torch.no_grad():
@@ -171,25 +180,31 @@ class Trainer:
                 self._capture()
             self.static_wids.copy_(wids, non_blocking=True)
             self.graph.replay()
-            if self.world == 1:
-                self.opt.iterations += 1
-                return
         else:
-            self._body(wids.to(self.device), with_opt=self.world == 1)
-            if self.world == 1:
-                return
+            self._body(wids.to(self.device), with_opt=not self.split_opt)
+        if not self.split_opt:
+            self.opt.iterations += int(self.use_graph)
+            return
         # data parallel: one all-reduce of the flat gradient buffer, then Adam
-        with _rf("gnnqc.allreduce"):
-            if self.device.type == "cuda":
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                D.all_reduce_(self.opt.flat_g)
-                e1.record()
-                self._comm_events.append((e0, e1))
-            else:
-                D.all_reduce_(self.opt.flat_g)
+        if self.world > 1:
+            with _rf("gnnqc.allreduce"):
+                if self.device.type == "cuda":
+                    if len(self._comm_events) < 64:      # sample the first steps of an epoch
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        D.all_reduce_(self.opt.flat_g)
+                        e1.record()
+                        self._comm_events.append((e0, e1))
+                    else:
+                        D.all_reduce_(self.opt.flat_g)
+                else:
+                    D.all_reduce_(self.opt.flat_g)
         with _rf("gnnqc.optimizer"):
-            self.opt.step(grad_scale=1.0 / self.world)
+            if self.opt_graph is not None:
+                self.opt_graph.replay()
+                self.opt.iterations += 1
+            else:
+                self.opt.step(grad_scale=1.0 / self.world)
 
     # ---------------------------------------------------------------- epoch helpers
     def train_epoch(self, loader, epoch: int) -> Dict[str, float]:

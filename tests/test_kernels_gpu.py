@@ -818,3 +818,37 @@ def test_lstm_fused_maxpool_matches_separate_pool(cuda_device, H, pair, T):
     y0.backward(g)
     for a, b_ in zip([x1.grad] + [p.grad for p in p1], [x0.grad] + [p.grad for p in p0]):
         assert (a - b_).norm().item() <= 2e-2 * (b_.norm().item() + 1e-6)
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_split_optimizer_graph_matches_fused(cuda_device, cml_windows, monkeypatch, use_graph):
+    """The data-parallel step layout (forward/backward graph, then a separate optimizer graph
+    replayed after the all-reduce) gives the same parameters as the one-graph step."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceLoader, DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    pc, ws = cml_windows
+    mc = C.default("model_cml")
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+
+    def run(split):
+        monkeypatch.setenv("GNNQC_SPLIT_OPT_GRAPH", "1" if split else "0")
+        torch.manual_seed(0)
+        model = GCNClassifier(mc, pc).to(cuda_device)
+        opt = make_optimizer("adam", model.parameters(), 1e-3)
+        tr = Trainer(model, st, opt, {0: 1.0, 1: 5.0}, use_graph=use_graph, batch_size=64)
+        assert tr.split_opt == split
+        loader = DeviceLoader(st, list(range(st.n_windows)), 64, shuffle=True)
+        for row in list(loader.batch_ids())[:6]:
+            tr.train_step(row)
+        torch.cuda.synchronize()
+        assert (tr.opt_graph is not None) == (split and use_graph)
+        assert opt.iterations == 6 and float(opt.step_t.item()) == 6.0
+        return torch.cat([p.detach().reshape(-1) for p in model.parameters()]), float(tr.last_loss.item())
+
+    p1, l1 = run(True)
+    p0, l0 = run(False)
+    assert abs(l1 - l0) < 1e-3 * abs(l0) + 1e-5, (l1, l0)
+    assert (p1 - p0).norm().item() < 1e-4 * p0.norm().item()
