@@ -114,3 +114,30 @@ def test_training_reduces_loss_cpu():
         res = t.train_epoch(L, ep)
         first = first or res["loss"]
     assert res["loss"] < first
+
+
+def test_split_optimizer_step_matches_fused_cpu(monkeypatch):
+    """The data-parallel step layout (backward, then a separate optimizer step after the
+    all-reduce point) == the fused step, on CPU (eager; no graphs)."""
+    from gnnqc.data.store import DeviceLoader
+    from gnnqc.models import BaselineClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    pc, ws, st = _small_cml(seed=6)
+    mc = C.default("model_cml")
+    mc.baseline_model.filter_1_size = 8
+
+    def run(split):
+        monkeypatch.setenv("GNNQC_SPLIT_OPT_GRAPH", "1" if split else "0")
+        torch.manual_seed(0)
+        m = BaselineClassifier(mc, pc)
+        opt = make_optimizer("adam", m.parameters(), 3e-3)
+        t = Trainer(m, st, opt, {0: 1.0, 1: 5.0}, baseline=True, use_graph=False, batch_size=32)
+        assert t.split_opt == split
+        L = DeviceLoader(st, np.arange(min(st.n_windows, 128)), 32)
+        for row in L.batch_ids():
+            t.train_step(row)
+        assert opt.iterations == 4
+        return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+
+    assert torch.equal(run(True), run(False))
