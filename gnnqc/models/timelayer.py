@@ -133,7 +133,9 @@ class TimeLayer(nn.Module):
                     return h[:M]
                 continue
             if tm:                                   # leave time-major: [T, Mp, C] -> [M, T, C]
-                h = h.transpose(0, 1)[:M]
+                h = h.transpose(0, 1)
+                if h.shape[0] != M:                  # (a no-op slice would still cost a zero-fill + copy in backward)
+                    h = h[:M]
                 if h.shape[-1] != mod.kernel.shape[0]:   # (only if the first layer is not time-major)
                     h = h[..., : mod.kernel.shape[0]]
                 h = h.contiguous()

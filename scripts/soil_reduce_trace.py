@@ -1,4 +1,6 @@
-"""Attribute the aten reductions of one SoilNet GCN training step (eager, no graph).
+"""Attribute the aten reductions / fills / copies of one GCN training step (eager, no graph).
+
+Usage: python scripts/soil_reduce_trace.py [soilnet|cml]
 
 Prints the top aten ops by device time with their input shapes and Python stacks,
 so a stray PyTorch reduction in the SoilNet path can be traced to its call site.
@@ -21,13 +23,18 @@ def main():
     from gnnqc.train.engine import Trainer
     from gnnqc.train.loss import calculate_weights
 
+    from gnnqc.data.synthetic import make_cml_raw
+    ds = sys.argv[1] if len(sys.argv) > 1 else "soilnet"
     dev = torch.device("cuda:0")
-    pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
-    mc = C.default("model_soilnet")
-    raw = make_soilnet_raw(n_boxes=40, n_time=89 * 96, seed=7)
-    pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
+    pc = C.normalize_preproc(C.default(f"preprocessing_{ds}"))
+    mc = C.default(f"model_{ds}")
+    if ds == "soilnet":
+        raw = make_soilnet_raw(n_boxes=40, n_time=89 * 96, seed=7)
+        pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
+    else:
+        raw = make_cml_raw(n_sensors=23, n_minutes=28 * 1440, seed=7)
     ws = create_windows_dataset(pc, raw=raw)
-    store = DeviceStore(ws, "scale_range", pc.graph, device=dev)
+    store = DeviceStore(ws, "scale_range" if ds == "soilnet" else "rolling_median", pc.graph, device=dev)
     loader = DeviceLoader(store, list(range(ws.n_windows)), int(pc.batch_size), shuffle=True, seed=44,
                           drop_last=True)
     model = GCNClassifier(mc, pc).to(dev)
@@ -51,6 +58,12 @@ def main():
             print("==", ev.name, ev.input_shapes)
             for fr in (ev.stack or [])[:8]:
                 print("   ", fr)
+        if ev.name in ("aten::fill_", "aten::zero_", "aten::copy_", "aten::clone", "aten::zeros", "aten::contiguous"):
+            chain, p = [], ev.cpu_parent
+            while p is not None and len(chain) < 6:
+                chain.append(p.name)
+                p = p.cpu_parent
+            print("==", ev.name, ev.input_shapes, "<-", " <- ".join(chain))
 
 
 if __name__ == "__main__":
