@@ -65,8 +65,12 @@ __global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* out) 
 // publishes ok = (count == 0) in state[2], advances the optimiser step counter only for
 // a good step, counts skipped steps in state[3] and re-arms state[0..1] for the next
 // launch. The Adam kernel then reads state[2]. No host synchronisation anywhere.
+// ext (optional): the LSTM chain kernels' control words (lstm_chain.hip). ext[2] is set when a
+// chain consumer's bounded spin timed out in this step - its activations / gradients then came
+// from stale data, so the step is rejected like a non-finite one; the flag is cleared and
+// counted in ext[3] (the host raises on it at epoch end).
 __global__ void grad_guard_kernel(const float* __restrict__ g, long n, int* __restrict__ state,
-                                  float* __restrict__ step) {
+                                  float* __restrict__ step, int* __restrict__ ext) {
   int bad = 0;
   const long n4 = n / 4, stride = (long)gridDim.x * blockDim.x;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -87,7 +91,12 @@ __global__ void grad_guard_kernel(const float* __restrict__ g, long n, int* __re
     const int ticket = atomicAdd(&state[1], 1);
     if (ticket == (int)gridDim.x - 1) {          // last workgroup: all counts are in
       const int cnt = atomicAdd(&state[0], 0);
-      const int ok = cnt == 0;
+      int stale = 0;
+      if (ext != nullptr) {
+        stale = atomicExch(&ext[2], 0);
+        if (stale) atomicAdd(&ext[3], 1);
+      }
+      const int ok = cnt == 0 && stale == 0;
       state[2] = ok;
       if (ok) step[0] += 1.0f;
       else state[3] += 1;
@@ -98,7 +107,7 @@ __global__ void grad_guard_kernel(const float* __restrict__ g, long n, int* __re
   }
 }
 
-void grad_guard(const at::Tensor& g, at::Tensor state, at::Tensor step) {
+void grad_guard(const at::Tensor& g, at::Tensor state, at::Tensor step, const c10::optional<at::Tensor>& ext) {
   check_f32_cuda(g, "g");
   check_f32_cuda(step, "step");
   TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kInt && state.numel() >= 4 && state.is_contiguous(),
@@ -107,8 +116,14 @@ void grad_guard(const at::Tensor& g, at::Tensor state, at::Tensor step) {
   c10::DeviceGuard guard(g.device());
   const long n = g.numel();
   const int grid = (int)std::max<long>(1, std::min<long>((n / 4 + 255) / 256, 128));
+  int* ep = nullptr;
+  if (ext.has_value() && ext->defined()) {
+    TORCH_CHECK(ext->is_cuda() && ext->scalar_type() == at::kInt && ext->numel() >= 4 && ext->get_device() == g.get_device(),
+                "grad_guard: ext must be int32[4] on the gradient's device");
+    ep = ext->data_ptr<int>();
+  }
   hipLaunchKernelGGL(grad_guard_kernel, dim3(grid), dim3(256), 0, stream(), g.data_ptr<float>(), n,
-                     state.data_ptr<int>(), step.data_ptr<float>());
+                     state.data_ptr<int>(), step.data_ptr<float>(), ep);
   GQ_LAUNCH_CHECK();
 }
 

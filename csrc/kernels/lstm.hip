@@ -411,21 +411,6 @@ void launch_bwd(int H, const float* dh, const float* g, const float* c, const fl
   }
 }
 
-// cell-per-lane kernels for H <= 64 (lstm_v3.hip), opt-in with GNNQC_LSTM_V3=1: 2x faster
-// inference forward, but per-cell scattered stores make its training forward/backward slower
-// than this file's kernels on the CML shapes (profiles/r1_lstm_microbench.md).
-// v3 stores gates interleaved per cell and returns them as a 4-D [M, T, H, 4] tensor, so
-// lstm_bwd picks the matching backward from the tensor it is given.
-bool v3_supports(int H, int Din, int ldx, const void* x);
-void launch_fwd_v3(int H, bool train, int M, int T, int Din, int ldx, const float* x, const float* W, const float* U,
-                   const float* b, float* h, float* c, float* g, hipStream_t st);
-bool launch_bwd_v3(int H, int M, int T, const float* dh, const float* gates, const float* c, const float* U,
-                   float* dz, hipStream_t st);
-static bool use_v3() {
-  static const bool v = [] { const char* e = std::getenv("GNNQC_LSTM_V3"); return e && e[0] == '1'; }();
-  return v;
-}
-
 std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
                                  bool train, bool bf16) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be a float32 GPU tensor");
@@ -444,8 +429,7 @@ std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const
   const int Mp = (M + 15) / 16 * 16;   // stores go to whole 16-row tiles
   at::Tensor h = at::empty({Mp, T, H}, opt);
   at::Tensor c = train ? at::empty({Mp, T, H}, opt) : at::empty({0}, opt);
-  const bool v3 = bf16 && use_v3() && v3_supports(H, Din, ldx, x.data_ptr());
-  at::Tensor g = train ? (v3 ? at::empty({Mp, T, H, 4}, opt) : at::empty({Mp, T, 4 * H}, opt)) : at::empty({0}, opt);
+  at::Tensor g = train ? at::empty({Mp, T, 4 * H}, opt) : at::empty({0}, opt);
   auto cut = [&](at::Tensor t) { return (train && Mp != M) ? t.narrow(0, 0, M) : t; };
   if (M == 0 || T == 0) return {h.narrow(0, 0, M), cut(c), cut(g)};
   auto st = stream();
@@ -453,9 +437,7 @@ std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const
   float* hp = h.data_ptr<float>();
   float* cp = train ? c.data_ptr<float>() : nullptr;
   float* gp = train ? g.data_ptr<float>() : nullptr;
-  if (v3) {
-    launch_fwd_v3(H, train, M, T, Din, ldx, xp, Wp, Up, bp, hp, cp, gp, st);
-  } else if (bf16) {
+  if (bf16) {
     if (train) launch_fwd<true, true>(H, xp, Wp, Up, bp, hp, cp, gp, M, T, Din, ldx, st);
     else launch_fwd<true, false>(H, xp, Wp, Up, bp, hp, cp, gp, M, T, Din, ldx, st);
   } else {
@@ -473,20 +455,14 @@ at::Tensor lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Ten
   check_f32_cuda(cseq, "cseq");
   check_f32_cuda(U, "U");
   const int M = dh.size(0), T = dh.size(1), H = U.size(0);
-  const bool v3 = gates.dim() == 4;    // interleaved layout written by the v3 forward
-  TORCH_CHECK(dh.size(2) == H && gates.size(0) == M && gates.size(1) == T &&
-                  (v3 ? (gates.size(2) == H && gates.size(3) == 4) : gates.size(2) == 4 * H) &&
+  TORCH_CHECK(dh.size(2) == H && gates.size(0) == M && gates.size(1) == T && gates.size(2) == 4 * H &&
                   cseq.size(0) == M && cseq.size(1) == T && cseq.size(2) == H, "lstm_bwd: shape mismatch");
-  TORCH_CHECK(!v3 || bf16, "lstm_bwd: interleaved (v3) gates come from the bf16 forward");
   c10::DeviceGuard guard(dh.device());
   const int Mp = (M + 15) / 16 * 16;
   at::Tensor dz = at::empty({Mp, T, 4 * H}, dh.options());
   if (M == 0 || T == 0) return dz.narrow(0, 0, M);
   auto st = stream();
-  if (v3) {
-    TORCH_CHECK(launch_bwd_v3(H, M, T, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(),
-                              U.data_ptr<float>(), dz.data_ptr<float>(), st), "lstm_bwd: v3 hidden size");
-  } else if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
+  if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
   else launch_bwd<false>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
   GQ_LAUNCH_CHECK();
   return Mp == M ? dz : dz.narrow(0, 0, M);

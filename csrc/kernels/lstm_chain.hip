@@ -105,6 +105,11 @@ __device__ __noinline__ unsigned long long chain_wait(const unsigned long long* 
   return v;
 }
 
+// Tag base of a launch: (epoch mod (2^20 - 1)) + 1 in the high 20 bits of the 32-bit tag, the
+// time index (< 4096) in the low 12. Never 0, so a zeroed granule (fresh or reused memory)
+// can never pass as a valid one, whatever the epoch counter has wrapped to.
+__device__ __forceinline__ unsigned chain_tag_base(unsigned E) { return ((E % 0xFFFFFu) + 1u) << 12; }
+
 // One layer of one tile: lstm_tm_fwd_kernel's step loop with the x ring fed either from
 // global memory (stage 0) or from the previous stage's granule stream (SRC), and the
 // output (optionally max-pooled) also published as granules.
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   }
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned tagb = (E & 0xFFFFFu) << 12;
+  const unsigned tagb = chain_tag_base(E);
   __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS];
   const ChainStage& S = A.st[s];
   const int H = S.H, KX = S.KX;
@@ -682,7 +687,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   }
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned tagb = (E & 0xFFFFFu) << 12;
+  const unsigned tagb = chain_tag_base(E);
   __shared__ __attribute__((aligned(16))) char smem[CHAINB_LDS];
   // the stage record is loaded field by field from the kernel arguments (scalar loads): a
   // reference into the by-value argument array made the compiler copy the whole array to
@@ -744,6 +749,46 @@ static int* chain_ctl(int dev) {
   return ctl[dev];
 }
 
+// Workgroups of the chain kernels that can be resident at once on this device: the CU count
+// of the device (a partitioned MI355X exposes fewer) times the occupancy of the 1024-thread
+// chain kernels (with their LDS and VGPR use). Every workgroup of a chain launch must be
+// resident, or consumers spin on producers that are never scheduled.
+static int chain_capacity(int dev) {
+  static int cap[64] = {0};
+  TORCH_CHECK(dev >= 0 && dev < 64, "lstm_chain: device index");
+  if (cap[dev] == 0) {
+    hipDeviceProp_t prop;
+    TORCH_CHECK(hipGetDeviceProperties(&prop, dev) == hipSuccess, "lstm_chain: device properties");
+    int occ = 1 << 30;
+    const void* kernels[] = {reinterpret_cast<const void*>(&lstm_chain_fwd_kernel<true>),
+                             reinterpret_cast<const void*>(&lstm_chain_fwd_kernel<false>),
+                             reinterpret_cast<const void*>(&lstm_chain_bwd_kernel)};
+    for (const void* k : kernels) {
+      int n = 0;
+      TORCH_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 1024, 0) == hipSuccess,
+                  "lstm_chain: occupancy query");
+      occ = std::min(occ, n);
+    }
+    cap[dev] = std::max(0, occ) * prop.multiProcessorCount;
+  }
+  return cap[dev];
+}
+
+int64_t lstm_chain_capacity(const at::Tensor& like) {
+  TORCH_CHECK(like.is_cuda(), "lstm_chain_capacity: a GPU tensor names the device");
+  return chain_capacity(like.get_device());
+}
+
+// The device's chain control words as an int32[4] view (no copy): [epoch, finished workgroups,
+// spin-timeout flag, timeouts consumed by the gradient guard]. The optimiser's grad_guard reads
+// and clears the flag inside the captured step (a timed-out step is skipped, never applied).
+at::Tensor lstm_chain_ctl(const at::Tensor& like) {
+  TORCH_CHECK(like.is_cuda(), "lstm_chain_ctl: a GPU tensor names the device");
+  c10::DeviceGuard guard(like.device());
+  int* p = chain_ctl(like.get_device());
+  return at::from_blob(p, {4}, like.options().dtype(at::kInt));
+}
+
 // x [T, Mp, Din] (Din % 4 == 0, 16-B aligned); per stage W [Dw, 4H], U [H, 4H], b [4H];
 // pool[s] > 0: MaxPooling1D(pool[s]) after stage s. Returns per stage [h, g, c, pooled, idx].
 std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U, at::TensorList b,
@@ -756,7 +801,8 @@ std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at
   const int Mp = (int)x.size(1);
   TORCH_CHECK(Mp % 16 == 0, "lstm_chain: Mp must be a multiple of 16");
   const int ntiles = Mp / 16, nt8 = (ntiles + 7) / 8 * 8;
-  TORCH_CHECK(ns * nt8 <= 256, "lstm_chain: ", ns * nt8, " workgroups cannot all be resident");
+  TORCH_CHECK(ns * nt8 <= chain_capacity(x.get_device()), "lstm_chain: ", ns * nt8,
+              " workgroups cannot all be resident on this device");
   TORCH_CHECK(x.size(2) % 4 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "lstm_chain: x channels must be float4 granules");
   c10::DeviceGuard guard(x.device());
@@ -848,7 +894,8 @@ std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, a
   const int Mp = (int)dh.size(1);
   TORCH_CHECK(Mp % 16 == 0, "lstm_chain_bwd: Mp");
   const int ntiles = Mp / 16, nt8 = (ntiles + 7) / 8 * 8;
-  TORCH_CHECK(ns * nt8 <= 256, "lstm_chain_bwd: ", ns * nt8, " workgroups cannot all be resident");
+  TORCH_CHECK(ns * nt8 <= chain_capacity(dh.get_device()), "lstm_chain_bwd: ", ns * nt8,
+              " workgroups cannot all be resident on this device");
   c10::DeviceGuard guard(dh.device());
   auto opt = dh.options();
   ChainBArgs A{};
@@ -942,6 +989,8 @@ at::Tensor lstm_chain_trace(const at::Tensor& like) {
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_fwd", &gq::lstm_chain_fwd);
   m.impl("lstm_chain_status", &gq::lstm_chain_status);
+  m.impl("lstm_chain_capacity", &gq::lstm_chain_capacity);
+  m.impl("lstm_chain_ctl", &gq::lstm_chain_ctl);
   m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
   m.impl("lstm_chain_bwd", &gq::lstm_chain_bwd);
 }

@@ -36,6 +36,8 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
   m.def("lstm_chain_fwd(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train) -> Tensor[]");
   m.def("lstm_chain_status(Tensor like) -> Tensor");
+  m.def("lstm_chain_capacity(Tensor like) -> int");
+  m.def("lstm_chain_ctl(Tensor like) -> Tensor");
   m.def("lstm_grads_multi(Tensor[] gz, Tensor[] gx, Tensor[] gh, Tensor[] gW, int[] period, int[] hshift, "
         "Tensor[] gws, Tensor[] rws, Tensor[] rW, Tensor(a!)[] rdW, Tensor(b!)[] rdU, Tensor(c!)[] rdb) -> ()");
   m.def("lstm_chain_trace(Tensor like) -> Tensor");
@@ -77,7 +79,7 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
         "float beta2, float eps, float grad_scale, float weight_decay, Tensor? guard=None) -> ()");
   m.def("nonfinite_count(Tensor x) -> Tensor");
-  m.def("grad_guard(Tensor g, Tensor(a!) state, Tensor(b!) step) -> ()");
+  m.def("grad_guard(Tensor g, Tensor(a!) state, Tensor(b!) step, Tensor(c!)? ext=None) -> ()");
   // metrics (metrics.hip)
   m.def("score_histogram(Tensor scores, Tensor labels, Tensor mask, int bins) -> Tensor");
   // fused dense head + weighted BCE + metrics (head.hip)

@@ -57,10 +57,6 @@ def graph_reshape(h: torch.Tensor) -> torch.Tensor:
     return h.permute(0, 2, 1, 3).reshape(B * N, T, Fdim)
 
 
-class _Head(nn.Module):
-    pass
-
-
 class GCNClassifier(nn.Module):
     def __init__(self, model_config, preprocessing_config):
         super().__init__()

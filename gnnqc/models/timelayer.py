@@ -177,7 +177,7 @@ class TimeLayer(nn.Module):
             i = j
             if pool not in (0, 3):       # consumer-side pooling takes 3; others end the chain
                 break
-        if not chain_fits(Mp, len(mods)):
+        if not chain_fits(Mp, len(mods), h.device):
             return None
         return mods, pools, i
 

@@ -12,6 +12,7 @@ plain GEMMs over all (sequence, step) rows.
 from __future__ import annotations
 
 import contextlib
+from typing import Optional
 
 import torch
 
@@ -391,7 +392,7 @@ class _HipLSTMChain(torch.autograd.Function):
                 return x
             return outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)]
 
-        if _chain_bwd_on() and chain_fits(dh.shape[1], ns) and all(layer_x(i).shape[-1] % 4 == 0 for i in range(ns)):
+        if _chain_bwd_on() and chain_fits(dh.shape[1], ns, dh.device) and all(layer_x(i).shape[-1] % 4 == 0 for i in range(ns)):
             # all reverse recurrences in ONE cross-CU pipelined launch (dz of every layer + dx
             # of the bottom one), then the weight-gradient passes
             order = list(reversed(range(ns)))
@@ -454,9 +455,71 @@ def lstm_chain_tm(x_tm: torch.Tensor, mods, pools) -> torch.Tensor:
     return _HipLSTMChain.apply(x_tm, tuple(int(p) for p in pools), *params)
 
 
-def chain_fits(Mp: int, n_stages: int) -> bool:
+_CHAIN_CAP = {}
+
+
+def chain_capacity(device) -> int:
+    """Chain workgroups that can be resident at once on ``device``: its CU count (queried: a
+    partitioned MI355X exposes 32 or 64) times the occupancy of the 1024-thread chain kernels."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return 0
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    cap = _CHAIN_CAP.get(idx)
+    if cap is None:
+        from ..utils.native import hip_ops
+        cap = int(hip_ops().lstm_chain_capacity(torch.empty(0, device=torch.device("cuda", idx))))
+        _CHAIN_CAP[idx] = cap
+    return cap
+
+
+def chain_fits(Mp: int, n_stages: int, device=None) -> bool:
     """All workgroups of a chain launch must be co-resident (one 1024-thread workgroup per CU)."""
-    return n_stages >= 2 and n_stages * ((Mp // 16 + 7) // 8 * 8) <= 256 and n_stages <= 8
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    return (2 <= n_stages <= 8 and n_stages * ((Mp // 16 + 7) // 8 * 8) <= chain_capacity(device))
+
+
+_CHAIN_CTL = {}
+
+
+def chain_ctl(device) -> Optional[torch.Tensor]:
+    """The device's chain control words ``[epoch, finished, timeout flag, rejected steps]`` as an
+    int32[4] view (``lstm_chain.hip``); None off the GPU. The optimiser's non-finite guard reads
+    and clears the timeout flag inside the captured step."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _CHAIN_CTL.get(idx)
+    if t is None:
+        from ..utils.native import hip_ops
+        t = hip_ops().lstm_chain_ctl(torch.empty(0, device=torch.device("cuda", idx)))
+        _CHAIN_CTL[idx] = t
+    return t
+
+
+class ChainTimeoutError(RuntimeError):
+    """A chain consumer gave up waiting for its producer (not all workgroups were resident, or
+    another kernel held the CUs): the affected results were computed from stale data."""
+
+
+def check_chain(device, rejected_before: Optional[int] = None) -> int:
+    """Raise :class:`ChainTimeoutError` if a chain spin timed out since the last check (forward-only
+    use: evaluation, prediction) or if training steps were rejected for it since
+    ``rejected_before``. Synchronises. Returns the current rejected-step count."""
+    ctl = chain_ctl(device)
+    if ctl is None:
+        return 0
+    v = ctl.cpu().tolist()
+    if v[2]:
+        ctl[2:3].zero_()
+        raise ChainTimeoutError("LSTM chain kernel: a consumer spin timed out; results of this pass are invalid "
+                                "(is another kernel sharing the GPU, or is the device partitioned?)")
+    if rejected_before is not None and v[3] > rejected_before:
+        raise ChainTimeoutError(f"LSTM chain kernel: {v[3] - rejected_before} training step(s) rejected after a "
+                                "consumer spin timeout (skipped on the device, parameters untouched)")
+    return int(v[3])
 
 
 class _HipLSTMTM(torch.autograd.Function):
@@ -618,5 +681,6 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
 
 
 __all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
+           "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError",
            "direct_grad_accumulation",
            "join_side_streams"]

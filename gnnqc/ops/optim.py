@@ -14,7 +14,8 @@ a second one. Consequences on MI355X:
   device - parameters, slots and the bias-correction step stay untouched - and
   counted in ``skipped_steps``. It lives inside the captured graph, so it costs no
   host synchronisation. In DP the all-reduce spreads a NaN to every rank, so all
-  ranks skip the same step.
+  ranks skip the same step. The same guard rejects a step in which an LSTM chain kernel's
+  bounded spin timed out (``gnnqc.ops.lstm.check_chain`` raises on it at epoch end).
 
 Optimisers by name like ``libs/fit_model.py:71-74``: adam (Keras eps 1e-7,
 "epsilon-hat" update), sgd, rmsprop (Keras defaults rho .9, eps 1e-7).
@@ -75,7 +76,9 @@ class FlatOptimizer:
         from . import use_hip
         if use_hip(self.flat_g):
             from ..utils.native import hip_ops
-            hip_ops().grad_guard(self.flat_g, self.guard_state, self.step_t)
+            from .lstm import chain_ctl
+            # a step whose LSTM chain kernel timed out (stale hand-off data) is rejected too
+            hip_ops().grad_guard(self.flat_g, self.guard_state, self.step_t, chain_ctl(self.flat_g.device))
             return self.guard_state[2:3].bool()
         ok = torch.isfinite(self.flat_g).all().reshape(1)
         self.step_t.add_(ok.float())

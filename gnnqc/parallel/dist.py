@@ -7,6 +7,7 @@ collectives; the ones this framework needs are:
 
 * ``all_reduce`` of the flat gradient buffer every step (one 753 KB collective),
 * ``broadcast`` of parameters + BN statistics at start / resume,
+* ``all_reduce`` (mean) of the BN moving statistics at every epoch end,
 * ``all_reduce`` of metric accumulators (loss sums, confusion counts, histograms),
 * ``all_gather`` of predictions / labels for global AUC/MCC and of IG attributions,
 * ``barrier`` around checkpointing.
@@ -95,6 +96,29 @@ def broadcast_module(module: torch.nn.Module, src: int = 0):
             dist.broadcast(t.data, src)
 
 
+def average_buffers(module: torch.nn.Module):
+    """Mean of every floating-point buffer (BatchNorm moving mean / variance) over the ranks.
+
+    Each rank updates the BN statistics from its own shard of the batch; Keras'
+    MirroredStrategy mean-aggregates such variables, so they are averaged once per epoch,
+    before evaluation, checkpointing or a resume snapshot read them. One collective over
+    all buffers flattened together."""
+    if not (is_initialized() and world_size() > 1):
+        return
+    bufs = [b for b in module.buffers() if b.is_floating_point()]
+    if not bufs:
+        return
+    with torch.no_grad():
+        flat = torch.cat([b.reshape(-1).to(torch.float64) for b in bufs])
+        dist.all_reduce(flat)
+        flat /= world_size()
+        off = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off:off + n].view_as(b).to(b.dtype))
+            off += n
+
+
 def all_gather_var(t: torch.Tensor) -> torch.Tensor:
     """All-gather tensors whose first dim differs per rank; concatenated in rank order."""
     if not (is_initialized() and world_size() > 1):
@@ -120,5 +144,5 @@ def max_over_ranks(x: float) -> float:
     return float(t.item())
 
 
-__all__ = ["init_distributed", "destroy", "barrier", "all_reduce_", "broadcast_", "broadcast_module",
+__all__ = ["init_distributed", "destroy", "barrier", "all_reduce_", "broadcast_", "broadcast_module", "average_buffers",
            "all_gather_var", "max_over_ranks", "world_size", "rank", "is_main", "is_initialized", "env_world"]

@@ -213,18 +213,31 @@ class Trainer:
         self.train_metrics.reset()
         self._comm_events = []
         skipped0 = self.opt.skipped_steps
+        rejected0 = self._chain_rejected()
         steps0 = self.global_step
         t0 = time.perf_counter()
         for row in loader.batch_ids():
             self.train_step(row)
+        D.average_buffers(self.model)                 # DP: BN moving statistics agree on every rank
         logs = self.train_metrics.result()            # device -> host: synchronises the epoch
         dt = time.perf_counter() - t0
         nsteps = self.global_step - steps0
         logs["skipped_steps"] = float(self.opt.skipped_steps - skipped0)
+        if rejected0 is not None:
+            # steps rejected on the device after an LSTM chain spin timeout: fail loudly
+            from ..ops.lstm import check_chain
+            check_chain(self.device, rejected0)
         logs["windows_per_sec"] = nsteps * loader.batch_size * self.world / max(dt, 1e-9)
         if self._comm_events:
             logs["allreduce_us"] = 1e3 * sum(a.elapsed_time(b) for a, b in self._comm_events) / len(self._comm_events)
         return logs
+
+    def _chain_rejected(self) -> Optional[int]:
+        """Training steps rejected so far for an LSTM chain spin timeout (None off the GPU)."""
+        if self.device.type != "cuda":
+            return None
+        from ..ops.lstm import chain_ctl
+        return int(chain_ctl(self.device)[3].item())
 
     @torch.no_grad()
     def evaluate(self, loader, prefix: str = "val_") -> Dict[str, float]:
@@ -233,7 +246,11 @@ class Trainer:
         for row in loader.batch_ids():
             self._loss(row, acc)
         self.model.train()
-        return acc.result(prefix)
+        out = acc.result(prefix)
+        if self.device.type == "cuda":
+            from ..ops.lstm import check_chain
+            check_chain(self.device)
+        return out
 
 
 @torch.no_grad()
@@ -256,6 +273,9 @@ def predict(model, store, loader, baseline: bool = False, gather_all: bool = Tru
         ws.append(b.wid)
     if was_training:
         model.train()
+    if store.device.type == "cuda":
+        from ..ops.lstm import check_chain
+        check_chain(store.device)
     p = torch.cat(ps)
     y = torch.cat(ys)
     m = torch.cat(ms)
