@@ -207,6 +207,32 @@ class GCNClassifier(nn.Module):
             return None
         return self.dense, self.dense2, self.dense_out, self.leakyrelu4.alpha, self.leakyrelu5.alpha
 
+    def fused_loss(self, inputs, y: torch.Tensor, mask: torch.Tensor, w0: float, w1: float, sums=None, hist=None):
+        """(loss, logits) through the headed-chain fast path (CML, GPU): the fused GCN kernel
+        writes the time-major LSTM input, then ONE kernel runs the whole TimeLayer, the head, the
+        weighted BCE and the metric accumulation (``gnnqc.ops.lstm.lstm_chain_head_tm``).
+        None when the configuration is not the one those kernels implement."""
+        spec = self.head_spec()
+        if spec is None or self.ds_type != "cml" or not self._cml_time_major(inputs):
+            return None
+        if any(d.kernel.shape[1] != 64 for d in spec[:2]) or spec[2].kernel.shape != (64, 1):
+            return None
+        if not (self.training is False or (self.dropout1.rate == 0 and self.dropout2.rate == 0)):
+            return None
+        x, anom, adj, mask_n, anom_pos = inputs[:5]
+        g = self.gcn_layer
+        pooling = "selection" if self.pooling_type == "selection" else self.aggregation_type
+        h, M = gcn_pool(x, adj, mask_n, anom, anom_pos, g.kernel, g.bias, g.bn_gamma, g.bn_beta, g.prelu_alpha,
+                        g.bn_moving_mean, g.bn_moving_variance, self.training, g.aggregate, pooling, g.momentum,
+                        g.eps, g.dropout, time_major=True)
+        if not self.time_layer.head_chain_ok(h) or spec[0].kernel.shape[0] != 128:
+            # (the GCN already ran: finish on the separate-kernel path from its output)
+            from ..ops.head import fused_head_loss
+            return fused_head_loss(self.time_layer.forward_time_major(h, M), *spec, y, mask, w0, w1, sums, hist)
+        yf = y.reshape(-1).float().contiguous()
+        mf = mask.reshape(-1).float().contiguous()
+        return self.time_layer.forward_time_major_head(h, M, spec[:3], spec[3:], yf, mf, w0, w1, sums, hist)
+
     def logits(self, inputs) -> torch.Tensor:
         z = self.head(self.features(inputs))
         if self.ds_type == "soilnet":

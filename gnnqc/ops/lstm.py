@@ -434,6 +434,103 @@ class _HipLSTMChain(torch.autograd.Function):
         return (dx if need[0] else None, None, *grads)
 
 
+class _HipLSTMChainHead(torch.autograd.Function):
+    """CML TimeLayer + classifier head + weighted BCE as ONE forward launch and ONE backward
+    launch (``lstm_chain.hip`` + ``chain_head.h``): the six pipelined time-major layers, the
+    H = 128 last layer (time4, last state) as a seventh chain stage, the Dense head, the loss
+    and the metric accumulation in the forward; the head backward (recomputed from time4's last
+    state), time4's reverse recurrence and the six reverse recurrences in the backward. The
+    weight-gradient passes of all seven layers then run as one ``lstm_grads_multi`` launch.
+
+    Inputs: x [T, Mp, C] time-major, y / mask [M]; ``consts`` = (alpha1, alpha2, w0, w1);
+    params = 7 x (W, U, b) then the head's (W1, b1, W2, b2, W3, b3). Returns (loss, logits [M])."""
+
+    @staticmethod
+    def forward(ctx, x, y, mask, sums, hist, consts, pools, M, *params):
+        from ..utils.native import hip_ops
+        ns = len(pools)
+        Ws = [params[3 * i].contiguous() for i in range(ns)]
+        Us = [params[3 * i + 1].contiguous() for i in range(ns)]
+        bs = [params[3 * i + 2].contiguous() for i in range(ns)]
+        head = [p.contiguous() for p in params[3 * ns:]]
+        need = any(ctx.needs_input_grad)
+        e = x.new_zeros(0)
+        res = hip_ops().lstm_chain_head_fwd(x, Ws, Us, bs, [int(p) for p in pools], need, head, y, mask, int(M),
+                                           *[float(c) for c in consts],
+                                           sums if sums is not None else e.double(),
+                                           hist if hist is not None else e)
+        outs, logits, loss = res[:5 * ns], res[5 * ns], res[5 * ns + 1]
+        ctx.pools, ctx.consts, ctx.M = tuple(int(p) for p in pools), tuple(float(c) for c in consts), int(M)
+        ctx.params = params
+        if need:
+            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs)
+        ctx.mark_non_differentiable(logits)
+        return loss.reshape(()), logits
+
+    @staticmethod
+    def backward(ctx, dloss, _dlogits):
+        from ..utils.native import hip_ops
+        ops = hip_ops()
+        pools = ctx.pools
+        ns = len(pools)
+        saved = ctx.saved_tensors
+        x, y, mask = saved[:3]
+        Ws, Us = saved[3:3 + ns], saved[3 + ns:3 + 2 * ns]
+        head = saved[3 + 2 * ns:9 + 2 * ns]
+        outs = saved[9 + 2 * ns:]
+        need = ctx.needs_input_grad
+        nparam = 3 * ns
+        hsinks = [_grad_sink(p) for p in ctx.params[nparam:]]
+
+        def layer_x(i):
+            if i == 0:
+                return x
+            return outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)]
+
+        order = list(reversed(range(ns)))
+        e8 = x.new_zeros(0, dtype=torch.uint8)
+        hT = outs[5 * (ns - 1)][-1]                        # time4's last state [Mp, 128] (contiguous)
+        g = dloss.reshape(1).float()
+        if not g.is_contiguous():
+            g = g.contiguous()
+        res = ops.lstm_chain_head_bwd(g, [outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
+                                      [Ws[i] for i in order], [Us[i] for i in order],
+                                      [outs[5 * i + 4] if pools[i] else e8 for i in order],
+                                      [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
+                                      [outs[5 * i].shape[0] for i in order], hT, list(head), y, mask, ctx.M,
+                                      *ctx.consts, [s for s, _ in hsinks])
+        grads = [None] * nparam
+        for k, i in enumerate(order):
+            nw = need[8 + 3 * i:11 + 3 * i]
+            if not any(nw):
+                continue
+            h = outs[5 * i]
+            xi = layer_x(i)
+            sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
+            if (_pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
+                    and len(_Pipe.batch) < _MULTI_MAX - 2):
+                _Pipe.batch.append(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
+            else:
+                ops.lstm_tm_grads(res[k], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
+            grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]
+        hgrads = [None if (direct or not n) else buf for (buf, direct), n in zip(hsinks, need[8 + nparam:])]
+        dx = res[ns]
+        return (dx if need[0] else None, None, None, None, None, None, None, None, *grads, *hgrads)
+
+
+def lstm_chain_head_tm(x_tm: torch.Tensor, mods, pools, head, y: torch.Tensor, mask: torch.Tensor, M: int,
+                       alpha1: float, alpha2: float, w0: float, w1: float, sums=None, hist=None):
+    """(loss, logits) of ``mods`` (LSTM modules; the last one H = 128 returning its last state)
+    followed by the Dense head ``head`` = (dense, dense2, dense_out) and the weighted BCE."""
+    params = []
+    for m in mods:
+        params += [m.kernel, m.recurrent_kernel, m.bias]
+    for d in head:
+        params += [d.kernel, d.bias]
+    return _HipLSTMChainHead.apply(x_tm, y, mask, sums, hist, (alpha1, alpha2, w0, w1), tuple(int(p) for p in pools),
+                                   int(M), *params)
+
+
 def _chain_bwd_on() -> bool:
     """Cross-CU pipelined backward of the chain (``GNNQC_CHAIN_BWD``, default on)."""
     import os
@@ -484,8 +581,8 @@ _CHAIN_CTL = {}
 
 
 def chain_ctl(device) -> Optional[torch.Tensor]:
-    """The device's chain control words ``[epoch, finished, timeout flag, rejected steps]`` as an
-    int32[4] view (``lstm_chain.hip``); None off the GPU. The optimiser's non-finite guard reads
+    """The device's chain control words ``[epoch, finished, timeout flag, rejected steps, fwd / bwd
+    head tickets, debug spin limit, 0]`` as an int32[8] view (``lstm_chain.hip``); None off the GPU. The optimiser's non-finite guard reads
     and clears the timeout flag inside the captured step."""
     device = torch.device(device)
     if device.type != "cuda":
@@ -681,6 +778,6 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
 
 
 __all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
-           "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError",
+           "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError", "lstm_chain_head_tm",
            "direct_grad_accumulation",
            "join_side_streams"]

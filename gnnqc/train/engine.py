@@ -95,6 +95,7 @@ class Trainer:
         self.opt_graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
         self.last_loss = torch.zeros((), device=self.device)
+        self._one = torch.ones((), device=self.device)
         self.global_step = 0
         self.fault = FaultInjector.from_env()
         # NaN poisoning of the gradient (fault injection only: no extra kernel otherwise)
@@ -109,8 +110,14 @@ class Trainer:
         with _rf("gnnqc.gather"):
             b = self.store.gather(wids)
             inputs = b.model_inputs(self.ds_type, self.baseline)
-        spec = self.model.head_spec() if hasattr(self.model, "head_spec") else None
-        if spec is not None:
+        fused = None
+        if hasattr(self.model, "fused_loss") and not self.baseline:
+            fused = self.model.fused_loss(inputs, b.y, b.y_mask, self.w0, self.w1, metrics.sums if metrics else None,
+                                          metrics.hist if metrics else None)
+        spec = self.model.head_spec() if (fused is None and hasattr(self.model, "head_spec")) else None
+        if fused is not None:
+            loss, z = fused
+        elif spec is not None:
             dense, dense2, dense_out, a1, a2 = spec
             loss, z = fused_head_loss(self.model.features(inputs), dense, dense2, dense_out, a1, a2, b.y, b.y_mask,
                                       self.w0, self.w1, metrics.sums if metrics else None,
@@ -129,7 +136,7 @@ class Trainer:
         with _rf("gnnqc.forward"):
             total, loss, z, b = self._loss(wids, self.train_metrics)
         with _rf("gnnqc.backward"), direct_grad_accumulation(True):
-            total.backward()
+            total.backward(self._one)          # (a kept seed: no ones_like fill launch per step)
         if self.poison is not None:
             self.opt.flat_g[:1].add_(self.poison)
         self.last_loss.copy_(loss.detach())

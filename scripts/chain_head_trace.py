@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Per-stage timeline of the CML chain kernels with and without the headed time4 stage.
+
+For the six-stage chain (lstm_chain_fwd / _bwd) and the seven-stage headed chain
+(lstm_chain_head_fwd / _bwd) prints the launch time (HIP events, mean of 50) and, from the
+kernels' s_memrealtime trace, every stage's start / end (tile 0, us after the first workgroup
+started). One JSON line per measurement."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, reps=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def stages(ops, x, k, nt8, mid=False):
+    tr = ops.lstm_chain_trace(x).cpu()
+    m = tr[512:768]
+    m2 = tr[768:]
+    tr = tr[:512].view(256, 2)
+    t0 = int(tr[:k * nt8:nt8, 0].min())
+    out = []
+    for s in range(k):
+        row = [round((int(tr[s * nt8, 0]) - t0) / 100, 1)]
+        if mid or s == k - 1:
+            row.append(round((int(m[s * nt8]) - t0) / 100, 1))
+        if mid and s == 0:
+            row.append(round((int(m2[s * nt8]) - t0) / 100, 1))
+        row.append(round((int(tr[s * nt8, 1]) - t0) / 100, 1))
+        out.append(row)
+    return out
+
+
+def main():
+    from gnnqc.utils.native import hip_ops
+    ops = hip_ops()
+    dev = torch.device("cuda:0")
+    M = int(os.environ.get("M", "128"))
+    Mp = (M + 15) // 16 * 16
+    torch.manual_seed(0)
+    units = [16, 16, 32, 32, 64, 64, 128]
+    pools = [0, 3, 0, 3, 0, 3, 0]
+    din = 20
+    Ws, Us, bs = [], [], []
+    for i, H in enumerate(units):
+        dw = 18 if i == 0 else units[i - 1]
+        Ws.append(torch.randn(dw, 4 * H, device=dev) * 0.3)
+        Us.append(torch.randn(H, 4 * H, device=dev) * 0.3)
+        bs.append(torch.randn(4 * H, device=dev) * 0.1)
+    head = [torch.randn(128, 64, device=dev) * 0.1, torch.zeros(64, device=dev),
+            torch.randn(64, 64, device=dev) * 0.1, torch.zeros(64, device=dev),
+            torch.randn(64, 1, device=dev) * 0.1, torch.zeros(1, device=dev)]
+    y = (torch.rand(M, device=dev) < 0.2).float()
+    mask = torch.ones(M, device=dev)
+    x = torch.randn(181, Mp, din, device=dev)
+    nt8 = (Mp // 16 + 7) // 8 * 8
+    e = torch.zeros(0, device=dev)
+    hc = (0.3, 0.3, 1.0, 5.0)
+    us6 = timeit(lambda: ops.lstm_chain_fwd(x, Ws[:6], Us[:6], bs[:6], pools[:6], True))
+    print(json.dumps({"fwd": "chain6", "us": round(us6, 2), "stages": stages(ops, x, 6, nt8)}), flush=True)
+    us7 = timeit(lambda: ops.lstm_chain_head_fwd(x, Ws, Us, bs, pools, True, head, y, mask, M, *hc, e.double(), e))
+    print(json.dumps({"fwd": "chain7+head", "us": round(us7, 2), "stages": stages(ops, x, 7, nt8)}), flush=True)
+    # backward
+    outs = ops.lstm_chain_head_fwd(x, Ws, Us, bs, pools, True, head, y, mask, M, *hc, e.double(), e)
+    e8 = torch.zeros(0, dtype=torch.uint8, device=dev)
+    xw = [din] + units[:-1]
+    Ts = [outs[5 * i].shape[0] for i in range(7)]
+    order6 = list(reversed(range(6)))
+    dh = torch.randn(Ts[5] // 3, Mp, 64, device=dev)
+    a6 = (dh, [outs[5 * i + 1] for i in order6], [outs[5 * i + 2] for i in order6], [Ws[i] for i in order6],
+          [Us[i] for i in order6], [outs[5 * i + 4] if pools[i] else e8 for i in order6],
+          [pools[i] for i in order6], [xw[i] for i in order6], [Ts[i] for i in order6])
+    ub6 = timeit(lambda: ops.lstm_chain_bwd(*a6))
+    print(json.dumps({"bwd": "chain6", "us": round(ub6, 2), "stages": stages(ops, x, 6, nt8, True)}), flush=True)
+    order7 = list(reversed(range(7)))
+    hT = outs[5 * 6][-1]
+    hg = [torch.zeros_like(p) for p in head]
+    one = torch.ones(1, device=dev)
+    a7 = (one, [outs[5 * i + 1] for i in order7], [outs[5 * i + 2] for i in order7], [Ws[i] for i in order7],
+          [Us[i] for i in order7], [outs[5 * i + 4] if pools[i] else e8 for i in order7],
+          [pools[i] for i in order7], [xw[i] for i in order7], [Ts[i] for i in order7], hT, head, y, mask, M, *hc, hg)
+    ub7 = timeit(lambda: ops.lstm_chain_head_bwd(*a7))
+    print(json.dumps({"bwd": "chain7+head", "us": round(ub7, 2), "stages": stages(ops, x, 7, nt8, True)}), flush=True)
+    st = ops.lstm_chain_status(x).cpu().tolist()
+    print(json.dumps({"status": st}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+"""CML GCN benched path (GCN kernel -> headed LSTM chain -> head + BCE in the chain) on the GPU:
+whole-model numerics against a float64 eager oracle, against the separate-kernel path, and the
+chain's fail-loudly guarantees (a timed-out step is rejected, never applied)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(cuda_device, cml_windows, B=128, seed=0):
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    pc, ws = cml_windows
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    torch.manual_seed(seed)
+    mc = C.default("model_cml")
+    model = GCNClassifier(mc, pc).to(cuda_device)
+    with torch.no_grad():                  # non-trivial head biases / BN parameters
+        for p in (model.dense.bias, model.dense2.bias, model.dense_out.bias):
+            p.normal_(0, 0.1)
+    n = min(B, st.n_windows)
+    b = st.gather(torch.arange(n, device=cuda_device))
+    return pc, mc, st, model, b
+
+
+def _grads(model, fn):
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    for p in model.parameters():
+        p.grad = torch.zeros_like(p)
+    with direct_grad_accumulation(True):
+        loss, z = fn()
+        loss.backward(torch.ones((), device=loss.device))
+    torch.cuda.synchronize()
+    return loss.detach(), z.detach(), {n: p.grad.clone() for n, p in model.named_parameters()}
+
+
+def test_headed_chain_is_the_default_cml_path(cuda_device, cml_windows):
+    _, _, _, model, b = _setup(cuda_device, cml_windows)
+    inputs = b.model_inputs("cml")
+    x_tm_ok = model._cml_time_major(inputs)
+    assert x_tm_ok
+    from gnnqc.ops.gcn import gcn_pool
+    g = model.gcn_layer
+    x, anom, adj, mask, anom_pos = inputs[:5]
+    h, M = gcn_pool(x, adj, mask, anom, anom_pos, g.kernel, g.bias, g.bn_gamma, g.bn_beta, g.prelu_alpha, g.bn_moving_mean,
+                    g.bn_moving_variance, False, g.aggregate, "mean", g.momentum, g.eps, g.dropout, time_major=True)
+    assert model.time_layer.head_chain_ok(h)
+
+
+def test_headed_chain_matches_separate_kernels(cuda_device, cml_windows, monkeypatch):
+    """One launch for TimeLayer + head + loss (fwd) and one for their backward == the chain of six
+    layers + separate time4 / head kernels: loss, logits and every parameter gradient."""
+    _, _, _, model, b = _setup(cuda_device, cml_windows)
+    inputs = b.model_inputs("cml")
+
+    def run(head_chain):
+        monkeypatch.setenv("GNNQC_HEAD_CHAIN", "1" if head_chain else "0")
+        return _grads(model, lambda: model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0))
+
+    l1, z1, g1 = run(True)
+    l0, z0, g0 = run(False)
+    torch.testing.assert_close(z1, z0, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(l1, l0, atol=1e-4, rtol=1e-3)
+    for n in g0:
+        err = (g1[n] - g0[n]).norm().item()
+        assert err <= 5e-3 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())
+
+
+def test_cml_default_path_matches_fp64_eager(cuda_device, cml_windows):
+    """The benched CML step (fused GCN, headed chain, bf16 MFMA recurrences) against the same
+    model evaluated in float64 with plain PyTorch on the CPU: logits, loss, every gradient."""
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.train.loss import weighted_bce_with_logits
+    pc, _, _, model, b = _setup(cuda_device, cml_windows, B=96)
+    inputs = b.model_inputs("cml")
+    assert model.time_layer.head_chain_ok is not None
+    loss, z, g = _grads(model, lambda: model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0))
+
+    ref = __import__("copy").deepcopy(model).cpu().double()
+    for p in ref.parameters():
+        p.grad = None
+    _, ws = cml_windows
+    st = DeviceStore(ws, "rolling_median", pc.graph, device="cpu")
+    bc = st.gather(torch.arange(b.y.shape[0]))
+    ri = [t.double() if torch.is_tensor(t) and t.is_floating_point() else t for t in bc.model_inputs("cml")]
+    zr = ref.logits(ri)
+    lr = weighted_bce_with_logits(zr, bc.y.double(), bc.y_mask.double(), 1.0, 5.0)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 2e-2 * abs(lr.item()) + 1e-4, (loss.item(), lr.item())
+    assert (z.cpu().double() - zr.detach()).abs().max().item() < 5e-2
+    for n, p in ref.named_parameters():
+        if p.grad is None:
+            continue
+        err = (g[n].cpu().double() - p.grad).norm().item()
+        scale = p.grad.norm().item()
+        assert err <= 8e-2 * scale + 1e-5, (n, err, scale)
+
+
+def test_chain_timeout_rejects_the_step(cuda_device, cml_windows):
+    """A consumer spin that times out (forced with the debug spin limit) makes the guard skip the
+    step on the device (parameters untouched) and the epoch end raise ChainTimeoutError."""
+    from gnnqc.data.store import DeviceLoader
+    from gnnqc.ops.lstm import ChainTimeoutError, chain_ctl, check_chain
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    _, _, st, model, _ = _setup(cuda_device, cml_windows)
+    opt = make_optimizer("adam", model.parameters(), 1e-3)
+    tr = Trainer(model, st, opt, {0: 1.0, 1: 5.0}, use_graph=False, batch_size=64)
+    loader = DeviceLoader(st, list(range(st.n_windows)), 64, shuffle=False)
+    row = next(iter(loader.batch_ids()))
+    ctl = chain_ctl(cuda_device)
+    rejected0 = check_chain(cuda_device)
+    tr.train_step(row)                                  # a normal step first
+    torch.cuda.synchronize()
+    before = opt.flat_p.clone()
+    skipped0 = opt.skipped_steps
+    try:
+        ctl[6] = 1                                      # spin limit 1: consumers give up at once
+        tr.train_step(row)
+        torch.cuda.synchronize()
+    finally:
+        ctl[6] = 0
+    assert opt.skipped_steps == skipped0 + 1
+    assert torch.equal(opt.flat_p, before), "a timed-out step must not change the parameters"
+    with pytest.raises(ChainTimeoutError):
+        check_chain(cuda_device, rejected0)
+    tr.train_step(row)                                  # and training continues normally
+    torch.cuda.synchronize()
+    assert opt.skipped_steps == skipped0 + 1
+    assert not torch.equal(opt.flat_p, before)
+
+
+def test_headed_chain_eval_metrics_match(cuda_device, cml_windows, monkeypatch):
+    """Evaluation through the headed chain (no-grad, TRAIN=false kernels) == separate kernels."""
+    from gnnqc.data.store import DeviceLoader
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    _, _, st, model, _ = _setup(cuda_device, cml_windows)
+    opt = make_optimizer("adam", model.parameters(), 1e-3)
+    tr = Trainer(model, st, opt, {0: 1.0, 1: 5.0}, use_graph=False, batch_size=64)
+    loader = DeviceLoader(st, list(range(st.n_windows)), 64, shuffle=False)
+    monkeypatch.setenv("GNNQC_HEAD_CHAIN", "1")
+    a = tr.evaluate(loader)
+    monkeypatch.setenv("GNNQC_HEAD_CHAIN", "0")
+    r = tr.evaluate(loader)
+    for k in r:
+        assert abs(a[k] - r[k]) <= 2e-3 * abs(r[k]) + 2e-3, (k, a[k], r[k])
