@@ -29,7 +29,6 @@
 // CML layer), while the consumer, running at a third of the producer's step rate, has slack.
 // Each stage also writes everything the per-layer kernels write (h, gate / cell state for
 // the backward, pooled output + argmax bytes), so the backward is unchanged.
-#include "chain_head.h"
 #include "common.h"
 #include "lstm_tm_common.h"
 
@@ -72,11 +71,14 @@ struct ChainStage {
 struct ChainArgs {
   ChainStage st[CHAIN_MAX];
   int ns, ntiles, nt8, Mp;
-  int* ctl;                          // [0] epoch, [1] finished workgroups, [2] spin timeout seen,
-                                     // [3] timeouts rejected by the guard, [4] / [5] head tickets
+  int* ctl;                          // [0] epoch, [1] finished workgroups, [2] spin timeout seen
   long long* trace;                  // [blocks][2] start / end s_memrealtime (100 MHz) of the last launch
-  ChainHead hd;                      // head != 0: the last stage (H = 128) runs the classifier head
-  int head;
+  // extra workgroups past the stages (the chain leaves most CUs idle): build the time4 kernel's
+  // A-fragment image (lstm_tm_common.h t4_pack_one) from pkU / pkW into pk
+  const float* pkU;
+  const float* pkW;
+  bf16x8_t* pk;
+  int pkDw;
 };
 
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
@@ -129,31 +131,20 @@ struct ChainLds {
   static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
   static constexpr int BYTES = HS + XS + HF;
 };
-// the last stage of a headed chain (time4, H = 128): [h_{T-1} tile for the head][stage LDS, then
-// the head's scratch over it]
-static constexpr int CH_HL_BYTES = 16 * (128 + 4) * 4;
-static constexpr int cmax(int a, int b) { return a > b ? a : b; }
-// H = 128: the input-projection fragments (W, 2 cells x KX x 16 waves x 64 lanes x 16 B) live in
-// LDS after the stage's tiles - resident in VGPRs they pushed the stage past 128 registers
-static constexpr int CH_WL_BYTES = 2 * 2 * 16 * 64 * 16 + 2 * 16 * 64 * 16;   // + bias fragments
-static constexpr int CHAIN_LDS =
-    cmax(ChainLds<64, 2>::BYTES,
-         CH_HL_BYTES + cmax(ChainLds<128, 2>::BYTES + CH_WL_BYTES, ChainHeadFwdLds<128>::BYTES));
+static constexpr int CHAIN_LDS = ChainLds<64, 2>::BYTES;
 
-template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN, bool HEAD = false>
+template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN>
 __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
-                                            int* ctl, char* smem, float* hl = nullptr) {
+                                            int* ctl, char* smem) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
   constexpr int KPX = 32 * KX;
   constexpr int GR = SRC ? 1 : 4;
   using L = ChainLds<H, KX>;
-  constexpr bool WL = H > 64;                 // W fragments from LDS (see CH_WL_BYTES)
   static_assert(L::BYTES <= CHAIN_LDS && L::HS % 16 == 0 && L::XS % 16 == 0, "chain LDS layout");
   auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
   auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
   auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
-  bf16x8_t* wl = reinterpret_cast<bf16x8_t*>(smem + L::BYTES);   // WL: [CPL][KX][NW][64]
 
   const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -164,9 +155,8 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += NT) (&hs[0][0][0])[i] = (__bf16)0.0f;
   for (int i = tid; i < 2 * 16 * (KPX + 8); i += NT) (&xs[0][0][0])[i] = (__bf16)0.0f;
 
-  bf16x8_t ufr[CPL][C::KSH], wfr[WL ? 1 : CPL][WL ? 1 : KX];
-  f32x4_t bias4[WL ? 1 : CPL];
-  f32x4_t* bl = reinterpret_cast<f32x4_t*>(smem + L::BYTES + (WL ? CPL * KX * NW * 64 * 16 : 0));   // WL: [CPL][NW][64]
+  bf16x8_t ufr[CPL][C::KSH], wfr[CPL][KX];
+  f32x4_t bias4[CPL];
   int unit[CPL];
 #pragma unroll
   for (int cc = 0; cc < CPL; ++cc) {
@@ -191,13 +181,10 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         const int k = 32 * s + 8 * quad + j;
         v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
       }
-      if constexpr (WL) wl[((cc * KX + s) * NW + w) * 64 + lane] = v;
-      else wfr[cc][s] = v;
+      wfr[cc][s] = v;
     }
     const int u = unit[cc];
-    const f32x4_t bv = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
-    if constexpr (WL) bl[(cc * NW + w) * 64 + lane] = bv;
-    else bias4[cc] = bv;
+    bias4[cc] = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
   }
 
   // x ring: granule (tid mod n_gx) of the contiguous [16][Din] tile (duplicates across lanes)
@@ -298,16 +285,11 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
       f32x4_t acc[CPL];
 #pragma unroll
       for (int cc = 0; cc < CPL; ++cc) {
-        f32x4_t accx, acch = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (WL) accx = bl[(cc * NW + w) * 64 + lane];
-        else accx = bias4[cc];
+        f32x4_t accx = bias4[cc], acch = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KX; ++s) {
           const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
-          bf16x8_t wa;
-          if constexpr (WL) wa = wl[((cc * KX + s) * NW + w) * 64 + lane];
-          else wa = wfr[cc][s];
-          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bx, accx, 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, accx, 0, 0, 0);
         }
 #pragma unroll
         for (int s = 0; s < C::KSH; ++s) {
@@ -329,9 +311,6 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         const int u = unit[cc];
         hs[p ^ 1][col][u] = (__bf16)hv;
         hf[p][col][u] = hv;
-        if constexpr (HEAD) {
-          if (t == T - 1) hl[col * (H + 4) + u] = hv;    // (t, T uniform: scalar branch)
-        }
         if constexpr (TRAIN) {
           const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
           *reinterpret_cast<float4*>(S.g + o * 4) = make_float4(iv, fv, gv, ov);
@@ -341,29 +320,6 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
       lds_barrier();
     }
   }
-}
-
-// H = 128 last stage (+ head): its own (non-inlined) function, so its register allocation does
-// not raise the pressure of the H <= 64 stage bodies sharing the kernel
-template <bool TRAIN>
-__device__ __noinline__ void chain_stage128(const ChainArgs* __restrict__ Ap, int s, int tile, unsigned tagb,
-                                            char* smem) {
-  // (a separate function: inlined, its register pressure made the allocator spill inside the
-  // step loops of every other stage of the kernel)
-  const int si = __builtin_amdgcn_readfirstlane(s);
-  const ChainStage& S = Ap->st[si];
-  const ChainHead& hd = Ap->hd;
-  const bool head = Ap->head != 0;
-  const int ntiles = Ap->ntiles, Mp = Ap->Mp;
-  int* ctl = Ap->ctl;
-  float* hl = reinterpret_cast<float*>(smem);
-  if (S.PIN == 3)
-    chain_stage<128, TRAIN, 2, 2, true, 3, true>(S, tile, ntiles, Mp, tagb, ctl, smem + CH_HL_BYTES, hl);
-  else
-    chain_stage<128, TRAIN, 2, 4, true, 1, true>(S, tile, ntiles, Mp, tagb, ctl, smem + CH_HL_BYTES, hl);
-  __syncthreads();
-  if (threadIdx.x == 0) Ap->trace[512 + blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();   // loop done
-  if (head) chain_head_fwd<128>(hd, tile, ntiles, hl, smem + CH_HL_BYTES);
 }
 
 __device__ __forceinline__ void chain_finish(int* ctl, int nblk) {
@@ -379,6 +335,12 @@ __device__ __forceinline__ void chain_finish(int* ctl, int nblk) {
 template <bool TRAIN>
 __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const int nblk = gridDim.x;
+  if ((int)blockIdx.x >= A.ns * A.nt8) {          // packing workgroups
+    const int f = ((int)blockIdx.x - A.ns * A.nt8) * 1024 + (int)threadIdx.x;
+    if (A.pk != nullptr && f < T4PK_N) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
+    chain_finish(A.ctl, nblk);
+    return;
+  }
   const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
   if (s >= A.ns || tile >= A.ntiles) {
     chain_finish(A.ctl, nblk);
@@ -403,15 +365,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false, 1) else GQ_CHAIN_BODY(HH, 2, 6, false, 1) }
   if (H == 16) GQ_CHAIN_KX(16)
   else if (H == 32) GQ_CHAIN_KX(32)
-  else if (H == 64) GQ_CHAIN_KX(64)
-  else {
-    // H = 128: only as the last stage, fed by a stage of <= 64 channels (host-checked), and
-    // (A.head) followed by the classifier head on the tile's h_{T-1}
-    // (A.hd is read in place, after the recurrence: a by-value copy taken here kept its fields
-    // live across the whole stage loop and spilled)
-    // the argument block in place (kernarg segment): no by-value copy of it into scratch
-    chain_stage128<TRAIN>((const ChainArgs*)__builtin_amdgcn_kernarg_segment_ptr(), s, tile, tagb, smem);
-  }
+  else GQ_CHAIN_KX(64)
 #undef GQ_CHAIN_KX
 #undef GQ_CHAIN_SRC
 #undef GQ_CHAIN_BODY
@@ -446,8 +400,6 @@ struct ChainBArgs {
   int ns, ntiles, nt8, Mp;
   int* ctl;
   long long* trace;
-  ChainHead hd;                      // head != 0: stage 0 is time4 (H = 128) behind the classifier head
-  int head;
 };
 
 template <int H, int KX>
@@ -459,10 +411,7 @@ struct ChainBLds {
   static constexpr int WB = WL ? 2 * KX * 16 * (4 * H + 8) * 2 : 0;
   static constexpr int BYTES = ZS + DH + DX + WB;
 };
-// time4 stage of a headed chain: dh_{T-1} tile, then the head scratch / the step tiles over it
-static constexpr int CHB_HEAD_REC = 16 * (512 + 8) * 2 + 2 * 16 * (128 + 4) * 4 + 4 * 16 * (64 + 4) * 4;
-static constexpr int CHAINB_LDS =
-    cmax(ChainBLds<64, 2>::BYTES, 16 * (128 + 4) * 4 + cmax(CHB_HEAD_REC, ChainHeadBwdLds<128>::BYTES));
+static constexpr int CHAINB_LDS = ChainBLds<64, 2>::BYTES;
 
 #ifndef CHAINB_LEAD
 #define CHAINB_LEAD 2
@@ -744,144 +693,6 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   if constexpr (!PUBW) store_dx((T - 1) & 1, 0, tagb);     // dx tile of t = 0
 }
 
-// Top stage of a headed backward chain: time4 (H = 128, return_sequences = False) under the
-// classifier head. Prologue: the head backward of the tile's 16 rows (chain_head.h) leaves
-// dh_{T-1} in LDS. Then T reverse steps with two cells per lane (the forward's gate layout):
-//   cell phase   dz of both cells -> zs (bf16 LDS tile [16][4H])
-//   MFMA phase   dh_rec^T = U dz^T: wave w owns unit tile w % 8 over gate-column half w / 8
-//                (8 MFMA 16x16x32, U fragments resident: 32 VGPRs); dx^T = W dz^T: din tile
-//                w % 4 over gate-column quarter w / 4 (4 MFMAs); partials summed through LDS
-//   publish      dx_t (16 x Din) as tagged granules for the layer below (un-pooled there),
-//                dz_t -> HBM for the weight-gradient pass
-// Two LDS barriers per step; T is 6 on the CML shapes, so the stage is a short prologue of
-// the chain rather than a pipeline stage of its own.
-template <int KX>
-__device__ __noinline__ void chain_bwd_head_stage(const ChainBArgs* __restrict__ Ap, int tile, unsigned tagb,
-                                                  char* smem) {
-  // (own function, argument block read in place: see chain_stage128)
-  const ChainBStage& S = Ap->st[0];
-  const ChainHead& hd = Ap->hd;
-  const int ntiles = Ap->ntiles, Mp = Ap->Mp;
-  constexpr int H = 128;
-  using C = TMC<H>;
-  constexpr int CPL = C::CPL, NW = C::NW, G4 = C::G4, HP = C::HP;
-  static_assert(C::NT == 1024 && CPL == 2 && NW == 16, "time4 stage mapping");
-  constexpr int ZP = G4 + 8;                 // bf16 pitch of the dz tile
-  constexpr int DXP = 32 * KX + 4;           // fp32 pitch of the dx partial tiles
-  float* dhT = reinterpret_cast<float*>(smem);                                 // [16][HP]
-  char* rs = smem + 16 * HP * 4;
-  auto zs = reinterpret_cast<__bf16 (*)[ZP]>(rs);                             // [16][ZP]
-  auto dhp = reinterpret_cast<float (*)[16][HP]>(rs + 16 * ZP * 2);            // [2][16][HP]
-  auto dxp = reinterpret_cast<float (*)[16][DXP]>(rs + 16 * ZP * 2 + 2 * 16 * HP * 4);   // [4][16][DXP]
-
-  const bool reducer = chain_head_bwd<H>(hd, tile, ntiles, dhT, rs);
-  __syncthreads();                           // the head scratch (rs) becomes the step tiles
-  if (threadIdx.x == 0) Ap->trace[512 + blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();  // head done
-
-  const int T = S.T, Din = S.Din, Dw = S.Dw;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int col = lane & 15, quad = lane >> 4;
-  const int row0 = tile * 16;
-  const int ut = w & 7, kh = w >> 3;         // dh_rec: unit tile, gate-column half
-  const int dt = w & 3, kq = w >> 2;         // dx: din tile, gate-column quarter
-  bf16x8_t ufr[8], wfr[4];
-#pragma unroll
-  for (int s8 = 0; s8 < 8; ++s8) {
-    const float* src = S.U + (size_t)(16 * ut + col) * G4 + 256 * kh + 32 * s8 + 8 * quad;
-    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-    ufr[s8] = bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
-                       (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
-  }
-  {
-    const int din = 16 * dt + col;
-    const float m = (dt < 2 * KX && din < Dw) ? 1.f : 0.f;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const float* src = S.W + (size_t)min(din, Dw - 1) * G4 + 128 * kq + 32 * s4 + 8 * quad;
-      const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-      wfr[s4] = bf16x8_t{(__bf16)(a.x * m), (__bf16)(a.y * m), (__bf16)(a.z * m), (__bf16)(a.w * m),
-                         (__bf16)(b.x * m), (__bf16)(b.y * m), (__bf16)(b.z * m), (__bf16)(b.w * m)};
-    }
-  }
-  int unit[CPL];
-#pragma unroll
-  for (int cc = 0; cc < CPL; ++cc) unit[cc] = 4 * (w + NW * cc) + quad;
-  auto gidx = [&](int t, int cc) { return ((((size_t)t * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane; };
-  float4 g4[CPL];
-  float ct[CPL], cp[CPL], dc[CPL], dhr[CPL];
-  auto load_state = [&](int t) {
-#pragma unroll
-    for (int cc = 0; cc < CPL; ++cc) {
-      g4[cc] = *reinterpret_cast<const float4*>(S.g + gidx(t, cc) * 4);
-      ct[cc] = S.c[gidx(t, cc)];
-      cp[cc] = S.c[gidx(max(t - 1, 0), cc)] * (t > 0 ? 1.f : 0.f);
-    }
-  };
-  load_state(T - 1);
-#pragma unroll
-  for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
-  const size_t xstep = (size_t)Mp * Din;
-  const int nx = 16 * Din;
-  const int xr = tid / Din, xk = tid % Din;
-  const size_t zstep = (size_t)Mp * G4;
-
-  for (int s = 0; s < T; ++s) {
-    const int t = T - 1 - s;
-#pragma unroll
-    for (int cc = 0; cc < CPL; ++cc) {
-      const int u = unit[cc];
-      const float dh = dhr[cc] + (s == 0 ? dhT[col * HP + u] : 0.f);
-      const float4 g = g4[cc];
-      const float tc = tanhf_fast(ct[cc]);
-      const float dct = dc[cc] + dh * g.w * (1.f - tc * tc);
-      dc[cc] = dct * g.y;
-      zs[col][0 * H + u] = (__bf16)(dct * g.z * g.x * (1.f - g.x));
-      zs[col][1 * H + u] = (__bf16)(dct * cp[cc] * g.y * (1.f - g.y));
-      zs[col][2 * H + u] = (__bf16)(dct * g.x * (1.f - g.z * g.z));
-      zs[col][3 * H + u] = (__bf16)(dh * tc * g.w * (1.f - g.w));
-    }
-    if (t >= 1) load_state(t - 1);           // (uniform) next step's gates / cell states in flight
-    lds_barrier();
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {            // dz_t tile -> HBM, as the bf16 values the MFMAs use
-      const int e = tid + 1024 * q, sq = e >> 7, c4 = (e & 127) * 4;
-      const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[sq][c4]);
-      *reinterpret_cast<float4*>(S.dz + (size_t)t * zstep + (size_t)(row0 + sq) * G4 + c4) =
-          make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
-    }
-    {
-      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) {
-        const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[col][256 * kh + 32 * s8 + 8 * quad]);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[s8], bz, a, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dhp[kh][col][16 * ut + 4 * quad + r] = a[r];
-    }
-    if (dt < 2 * KX) {                       // (uniform)
-      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[col][128 * kq + 32 * s4 + 8 * quad]);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[s4], bz, a, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dxp[kq][col][16 * dt + 4 * quad + r] = a[r];
-    }
-    lds_barrier();
-#pragma unroll
-    for (int cc = 0; cc < CPL; ++cc) dhr[cc] = dhp[0][col][unit[cc]] + dhp[1][col][unit[cc]];
-    if (tid < nx) {
-      const float v = (dxp[0][xr][xk] + dxp[1][xr][xk]) + (dxp[2][xr][xk] + dxp[3][xr][xk]);
-      st_granule(S.sout + (size_t)t * xstep + (size_t)row0 * Din + tid, v, tagb | (unsigned)t);
-    }
-  }
-  if (threadIdx.x == 0) Ap->trace[768 + blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();    // loop done
-  if (reducer) chain_head_bwd_reduce<H>(hd, ntiles);
-}
-
 __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   const int nblk = gridDim.x;
   const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
@@ -899,15 +710,6 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   const ChainBStage S = A.st[s];
   const int H = S.H, KX = S.KX;
   const bool src = s > 0;
-  if (s == 0 && A.head) {
-    const ChainBArgs* Ap = (const ChainBArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    if (KX == 1) chain_bwd_head_stage<1>(Ap, tile, tagb, smem);
-    else chain_bwd_head_stage<2>(Ap, tile, tagb, smem);
-    __syncthreads();
-    if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-    chain_finish(A.ctl, nblk);
-    return;
-  }
 #define GQ_CHAINB_BODY3(HH, KXX, DD, SRCV, UPV, XOV)                                    \
   {                                                                                     \
     if (threadIdx.x >= TMC<HH>::NT + (TMC<HH>::NT + 64 <= 1024 ? 64 : 0)) return;       \
@@ -942,11 +744,11 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
 // host
 static long long* chain_trace_buf(int dev) {
   static long long* tr[64] = {nullptr};
-  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], 4 * 256 * sizeof(long long)) == hipSuccess, "lstm_chain: trace");
+  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], 3 * 256 * sizeof(long long)) == hipSuccess, "lstm_chain: trace");
   return tr[dev];
 }
 
-static int* chain_ctl(int dev) {
+int* chain_ctl(int dev) {
   static int* ctl[64] = {nullptr};
   TORCH_CHECK(dev >= 0 && dev < 64, "lstm_chain: device index");
   if (!ctl[dev]) {
@@ -993,8 +795,8 @@ int64_t lstm_chain_capacity(const at::Tensor& like) {
 }
 
 // The device's chain control words as an int32[8] view (no copy): [epoch, finished workgroups,
-// spin-timeout flag, timeouts consumed by the gradient guard, head tickets (2), debug spin limit
-// (0: default), 0]. The optimiser's grad_guard reads
+// spin-timeout flag, timeouts consumed by the gradient guard, time4/head kernel tickets (2),
+// debug spin limit (0: default), 0]. The optimiser's grad_guard reads
 // and clears the flag inside the captured step (a timed-out step is skipped, never applied).
 at::Tensor lstm_chain_ctl(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "lstm_chain_ctl: a GPU tensor names the device");
@@ -1003,47 +805,28 @@ at::Tensor lstm_chain_ctl(const at::Tensor& like) {
   return at::from_blob(p, {8}, like.options().dtype(at::kInt));
 }
 
-// Classifier head operands of a headed chain (host side)
-struct HeadIn {
-  at::TensorList p;                  // W1 [F,64], b1 [64], W2 [64,64], b2 [64], W3 [64,1], b3 [1]
-  const at::Tensor* y;
-  const at::Tensor* mask;
-  int M;
-  float alpha1, alpha2, w0, w1;
-};
-
-static void head_args(ChainHead& hd, const HeadIn& hi, int F, int Mp) {
-  TORCH_CHECK(hi.p.size() == 6, "lstm_chain head: expected W1, b1, W2, b2, W3, b3");
-  for (const at::Tensor& t : hi.p) check_f32_cuda(t, "lstm_chain head weight");
-  TORCH_CHECK(hi.p[0].numel() == (long)F * CH_HU && hi.p[1].numel() == CH_HU && hi.p[2].numel() == CH_HU * CH_HU &&
-                  hi.p[3].numel() == CH_HU && hi.p[4].numel() == CH_HU && hi.p[5].numel() == 1,
-              "lstm_chain head: expected Dense(", F, ",64)-Dense(64,64)-Dense(64,1)");
-  check_f32_cuda(*hi.y, "y");
-  check_f32_cuda(*hi.mask, "mask");
-  TORCH_CHECK(hi.M >= 1 && hi.M <= Mp && hi.y->numel() >= hi.M && hi.mask->numel() >= hi.M,
-              "lstm_chain head: y / mask rows");
-  hd.W1 = hi.p[0].data_ptr<float>();
-  hd.b1 = hi.p[1].data_ptr<float>();
-  hd.W2 = hi.p[2].data_ptr<float>();
-  hd.b2 = hi.p[3].data_ptr<float>();
-  hd.W3 = hi.p[4].data_ptr<float>();
-  hd.b3 = hi.p[5].data_ptr<float>();
-  hd.y = hi.y->data_ptr<float>();
-  hd.mask = hi.mask->data_ptr<float>();
-  hd.M = hi.M;
-  hd.alpha1 = hi.alpha1;
-  hd.alpha2 = hi.alpha2;
-  hd.w0 = hi.w0;
-  hd.w1 = hi.w1;
-}
-
 // x [T, Mp, Din] (Din % 4 == 0, 16-B aligned); per stage W [Dw, 4H], U [H, 4H], b [4H];
 // pool[s] > 0: MaxPooling1D(pool[s]) after stage s. Returns per stage [h, g, c, pooled, idx].
-// With a head (hi): the last stage is H = 128 without pool, followed by the classifier head and
-// the weighted BCE; [logits (M), loss (1)] are appended.
 static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorList W, at::TensorList U,
-                                              at::TensorList b, at::IntArrayRef pool, bool train, const HeadIn* hi,
-                                              at::Tensor sums, at::Tensor hist) {
+                                              at::TensorList b, at::IntArrayRef pool, bool train, const at::Tensor* pkW,
+                                              const at::Tensor* pkU);
+
+std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U, at::TensorList b,
+                                       at::IntArrayRef pool, bool train) {
+  return chain_fwd_impl(x, W, U, b, pool, train, nullptr, nullptr);
+}
+
+// The chain forward, whose spare workgroups also build the time4 kernel's fragment image of
+// (Wt4 [Din, 512], Ut4 [128, 512]); the image is appended to the result.
+std::vector<at::Tensor> lstm_chain_fwd_pack(const at::Tensor& x, at::TensorList W, at::TensorList U,
+                                            at::TensorList b, at::IntArrayRef pool, bool train, const at::Tensor& Wt4,
+                                            const at::Tensor& Ut4) {
+  return chain_fwd_impl(x, W, U, b, pool, train, &Wt4, &Ut4);
+}
+
+static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorList W, at::TensorList U,
+                                              at::TensorList b, at::IntArrayRef pool, bool train, const at::Tensor* pkW,
+                                              const at::Tensor* pkU) {
   check_f32_cuda(x, "x");
   const int ns = (int)W.size();
   TORCH_CHECK(ns >= 1 && ns <= CHAIN_MAX && (int)U.size() == ns && (int)b.size() == ns && (int)pool.size() == ns,
@@ -1071,16 +854,13 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   for (int s = 0; s < ns; ++s) {
     for (const at::Tensor* t : {&W[s], &U[s], &b[s]}) check_f32_cuda(*t, "lstm_chain weight");
     const int H = (int)U[s].size(0), Dw = (int)W[s].size(0);
-    const bool last = s + 1 == ns;
-    const bool head_stage = hi != nullptr && last;
-    TORCH_CHECK(H == 16 || H == 32 || H == 64 || (head_stage && H == 128 && s > 0), "lstm_chain: hidden size ", H);
+    TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_chain: hidden size ", H);
     TORCH_CHECK(W[s].size(1) == 4 * H && U[s].size(1) == 4 * H && b[s].numel() == 4 * H, "lstm_chain: weights");
     TORCH_CHECK(Dw <= Din && Din <= 64 && (s == 0 || Din <= H), "lstm_chain: stage ", s, " input width ", Din);
-    TORCH_CHECK(H < 128 || (Din > 32 && Din % 4 == 0), "lstm_chain: the H = 128 stage takes 33..64 input channels");
     TORCH_CHECK(T >= 1 && T < 4096, "lstm_chain: sequence length");
     const int P = (int)pool[s];
+    const bool last = s + 1 == ns;
     TORCH_CHECK(last || P == 0 || P == 3, "lstm_chain: pools between stages must be 3 (got ", P, ")");
-    TORCH_CHECK(!head_stage || P == 0, "lstm_chain: the head stage returns its last state (no pool)");
     ChainStage& S = A.st[s];
     S.x = s == 0 ? x.data_ptr<float>() : nullptr;
     S.xin = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev_stream.data_ptr<int64_t>());
@@ -1119,114 +899,75 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     T = To;
     Din = H;
   }
-  if (hi != nullptr) {
-    head_args(A.hd, *hi, (int)U[ns - 1].size(0), Mp);
-    at::Tensor logits = at::empty({hi->M}, opt), loss = at::empty({1}, opt);
-    at::Tensor part = at::empty({ntiles * 8}, opt);
-    A.hd.logits = logits.data_ptr<float>();
-    A.hd.loss = loss.data_ptr<float>();
-    A.hd.part = part.data_ptr<float>();
-    A.hd.ticket = A.ctl + 4;
-    if (sums.numel() > 0) {
-      TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.numel() == 6, "sums: 6 float64");
-      A.hd.sums = sums.data_ptr<double>();
-    }
-    if (hist.numel() > 0) {
-      check_f32_cuda(hist, "hist");
-      TORCH_CHECK(hist.dim() == 2 && hist.size(0) == 2, "hist must be [2, bins]");
-      A.hd.hist = hist.data_ptr<float>();
-      A.hd.bins = (int)hist.size(1);
-    }
-    A.head = 1;
-    out.push_back(part);
-    out.push_back(logits);
-    out.push_back(loss);
+  int nblk = ns * nt8;
+  at::Tensor pk;
+  if (pkW != nullptr) {
+    check_f32_cuda(*pkW, "Wt4");
+    check_f32_cuda(*pkU, "Ut4");
+    TORCH_CHECK(pkU->size(0) == 128 && pkU->size(1) == 512 && pkW->size(1) == 512 && pkW->size(0) <= 64,
+                "lstm_chain_fwd_pack: time4 weights must be [<=64, 512] and [128, 512]");
+    pk = at::empty({(long)T4PK_N * 4}, opt);                  // 16 B per fragment
+    A.pkU = pkU->data_ptr<float>();
+    A.pkW = pkW->data_ptr<float>();
+    A.pkDw = (int)pkW->size(0);
+    A.pk = reinterpret_cast<bf16x8_t*>(pk.data_ptr<float>());
+    nblk += (T4PK_N + 1023) / 1024;
+    TORCH_CHECK(nblk <= chain_capacity(x.get_device()), "lstm_chain: ", nblk,
+                " workgroups cannot all be resident on this device");
   }
-  const int nblk = ns * nt8;
   if (train)
     hipLaunchKernelGGL(lstm_chain_fwd_kernel<true>, dim3(nblk), dim3(1024), 0, stream(), A);
   else
     hipLaunchKernelGGL(lstm_chain_fwd_kernel<false>, dim3(nblk), dim3(1024), 0, stream(), A);
   GQ_LAUNCH_CHECK();
-  // drop the stream buffers / head partials from the result (the caching allocator orders their reuse)
+  // drop the stream buffers from the result (the caching allocator orders their reuse)
   std::vector<at::Tensor> res;
-  for (size_t i = 0; i < out.size(); ++i) {
-    const bool part_buf = hi != nullptr && i + 3 == out.size();
-    if (out[i].scalar_type() != at::kLong && !part_buf) res.push_back(out[i]);
-  }
+  for (auto& t : out)
+    if (t.scalar_type() != at::kLong) res.push_back(t);
+  if (pk.defined()) res.push_back(pk);
   return res;
-}
-
-std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U, at::TensorList b,
-                                       at::IntArrayRef pool, bool train) {
-  return chain_fwd_impl(x, W, U, b, pool, train, nullptr, at::Tensor(), at::Tensor());
-}
-
-// Headed chain forward (CML GCN: the six pipelined layers + time4 + classifier head + weighted
-// BCE + metric accumulation in ONE launch). head = [W1, b1, W2, b2, W3, b3]; y / mask [M].
-// Returns the per-stage tensors of lstm_chain_fwd, then logits [M] and loss [1].
-std::vector<at::Tensor> lstm_chain_head_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U,
-                                            at::TensorList b, at::IntArrayRef pool, bool train, at::TensorList head,
-                                            const at::Tensor& y, const at::Tensor& mask, int64_t M, double alpha1,
-                                            double alpha2, double w0, double w1, at::Tensor sums, at::Tensor hist) {
-  const HeadIn hi{head, &y, &mask, (int)M, (float)alpha1, (float)alpha2, (float)w0, (float)w1};
-  return chain_fwd_impl(x, W, U, b, pool, train, &hi, sums, hist);
 }
 
 // Backward of a chain, stages listed TOP layer first. dh: gradient of the top layer's output
 // (pooled if pool[0] > 0); per stage the forward's g / c, W, U, the argmax bytes of the pool
 // after the layer (empty if none) and pool size; x_width[s]: channels of the layer's input
 // layout. Returns [dz_0 .. dz_{n-1}, dx of the bottom layer].
-// With a head (hi, hT, dloss): stage 0 is the H = 128 layer under the classifier head; its dh
-// comes from the head backward (hT: the layer's output at its last step, [Mp, 128]), and the
-// head's weight gradients are added to hgrads = [dW1, db1, dW2, db2, dW3, db3].
-static std::vector<at::Tensor> chain_bwd_impl(const at::Tensor* dh, at::TensorList g, at::TensorList c,
-                                              at::TensorList W, at::TensorList U, at::TensorList pidx,
-                                              at::IntArrayRef pool, at::IntArrayRef x_width, at::IntArrayRef T_in,
-                                              const HeadIn* hi, const at::Tensor* hT, const at::Tensor* dloss,
-                                              at::TensorList hgrads) {
+std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, at::TensorList c, at::TensorList W,
+                                       at::TensorList U, at::TensorList pidx, at::IntArrayRef pool,
+                                       at::IntArrayRef x_width, at::IntArrayRef T_in) {
+  check_f32_cuda(dh, "dh");
   const int ns = (int)W.size();
   TORCH_CHECK(ns >= 1 && ns <= CHAIN_MAX && (int)U.size() == ns && (int)g.size() == ns && (int)c.size() == ns &&
                   (int)pidx.size() == ns && (int)pool.size() == ns && (int)x_width.size() == ns &&
                   (int)T_in.size() == ns, "lstm_chain_bwd: stage lists");
-  const at::Tensor& ref = hi ? *hT : *dh;
-  check_f32_cuda(ref, hi ? "hT" : "dh");
-  int Mp;
-  if (hi) {
-    TORCH_CHECK(hT->dim() == 2 && hT->size(1) == 128, "lstm_chain_bwd: hT must be [Mp, 128]");
-    Mp = (int)hT->size(0);
-  } else {
-    TORCH_CHECK(dh->dim() == 3 && dh->is_contiguous(), "lstm_chain_bwd: dh must be a contiguous [Ts, Mp, H]");
-    Mp = (int)dh->size(1);
-  }
+  TORCH_CHECK(dh.dim() == 3 && dh.is_contiguous(), "lstm_chain_bwd: dh must be a contiguous [Ts, Mp, H]");
+  const int Mp = (int)dh.size(1);
   TORCH_CHECK(Mp % 16 == 0, "lstm_chain_bwd: Mp");
   const int ntiles = Mp / 16, nt8 = (ntiles + 7) / 8 * 8;
-  TORCH_CHECK(ns * nt8 <= chain_capacity(ref.get_device()), "lstm_chain_bwd: ", ns * nt8,
+  TORCH_CHECK(ns * nt8 <= chain_capacity(dh.get_device()), "lstm_chain_bwd: ", ns * nt8,
               " workgroups cannot all be resident on this device");
-  c10::DeviceGuard guard(ref.device());
-  auto opt = ref.options();
+  c10::DeviceGuard guard(dh.device());
+  auto opt = dh.options();
   ChainBArgs A{};
   A.ns = ns;
   A.ntiles = ntiles;
   A.nt8 = nt8;
   A.Mp = Mp;
-  A.ctl = chain_ctl(ref.get_device());
-  A.trace = chain_trace_buf(ref.get_device());
+  A.ctl = chain_ctl(dh.get_device());
+  A.trace = chain_trace_buf(dh.get_device());
   std::vector<at::Tensor> dzs, keep;
   at::Tensor dx, prev;
   for (int s = 0; s < ns; ++s) {
     const int H = (int)U[s].size(0), Dw = (int)W[s].size(0), T = (int)T_in[s], Din = (int)x_width[s];
     const int P = (int)pool[s];
-    const bool head_stage = hi != nullptr && s == 0;
-    TORCH_CHECK(H == 16 || H == 32 || H == 64 || (head_stage && H == 128), "lstm_chain_bwd: hidden size ", H);
+    TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_chain_bwd: hidden size ", H);
     TORCH_CHECK(Dw <= Din && Din <= 64 && Din % 4 == 0 && T >= 1 && T < 4096, "lstm_chain_bwd: stage ", s, " shape");
-    TORCH_CHECK(!head_stage || (P == 0 && ns > 1), "lstm_chain_bwd: the head stage has no pool and a stage below");
     for (const at::Tensor* t : {&g[s], &c[s], &W[s], &U[s]}) check_f32_cuda(*t, "lstm_chain_bwd operand");
     TORCH_CHECK(g[s].numel() == (long)(T + 1) * Mp * H * 4 && c[s].numel() == (long)(T + 1) * Mp * H,
                 "lstm_chain_bwd: saved state shapes");
     const int Ts = P > 0 ? T / P : T;
     if (s == 0) {
-      if (!hi) TORCH_CHECK(dh->size(0) == Ts && dh->size(2) == H, "lstm_chain_bwd: dh shape");
+      TORCH_CHECK(dh.size(0) == Ts && dh.size(2) == H, "lstm_chain_bwd: dh shape");
     } else {
       TORCH_CHECK((int)x_width[s - 1] == H, "lstm_chain_bwd: stage ", s, " output width");
       TORCH_CHECK((int)T_in[s - 1] == Ts, "lstm_chain_bwd: lengths");
@@ -1236,7 +977,7 @@ static std::vector<at::Tensor> chain_bwd_impl(const at::Tensor* dh, at::TensorLi
                   "lstm_chain_bwd: argmax bytes");
     }
     ChainBStage& S = A.st[s];
-    S.dh = (s == 0 && !hi) ? dh->data_ptr<float>() : nullptr;
+    S.dh = s == 0 ? dh.data_ptr<float>() : nullptr;
     S.din = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev.data_ptr<int64_t>());
     S.pidx = P > 0 ? pidx[s].data_ptr<uint8_t>() : nullptr;
     S.g = g[s].data_ptr<float>();
@@ -1267,50 +1008,10 @@ static std::vector<at::Tensor> chain_bwd_impl(const at::Tensor* dh, at::TensorLi
     S.Ts = Ts;
     S.trace_mid = A.trace + 512;
   }
-  at::Tensor gpart;
-  if (hi) {
-    head_args(A.hd, *hi, 128, Mp);
-    check_f32_cuda(*dloss, "dloss");
-    TORCH_CHECK(dloss->numel() == 1, "lstm_chain_bwd: dloss must be a scalar");
-    TORCH_CHECK(hgrads.size() == 6, "lstm_chain_bwd: head gradient list");
-    for (size_t i = 0; i < 6; ++i) {
-      check_f32_cuda(hgrads[i], "head gradient");
-      TORCH_CHECK(hgrads[i].numel() == hi->p[i].numel(), "lstm_chain_bwd: head gradient ", i, " size");
-    }
-    TORCH_CHECK(hT->is_contiguous(), "lstm_chain_bwd: hT rows must be contiguous");
-    gpart = at::empty({(long)ntiles * ChainHeadRec<128>::PITCH}, opt);
-    A.hd.hT = hT->data_ptr<float>();
-    A.hd.dloss = dloss->data_ptr<float>();
-    A.hd.gpart = gpart.data_ptr<float>();
-    A.hd.dW1 = hgrads[0].data_ptr<float>();
-    A.hd.db1 = hgrads[1].data_ptr<float>();
-    A.hd.dW2 = hgrads[2].data_ptr<float>();
-    A.hd.db2 = hgrads[3].data_ptr<float>();
-    A.hd.dW3 = hgrads[4].data_ptr<float>();
-    A.hd.db3 = hgrads[5].data_ptr<float>();
-    A.hd.ticket = A.ctl + 5;
-    A.head = 1;
-  }
   hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(ns * nt8), dim3(1024), 0, stream(), A);
   GQ_LAUNCH_CHECK();
   dzs.push_back(dx.defined() ? dx.narrow(0, 0, (int)T_in[ns - 1]) : at::empty({0}, opt));
   return dzs;
-}
-
-std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, at::TensorList c, at::TensorList W,
-                                       at::TensorList U, at::TensorList pidx, at::IntArrayRef pool,
-                                       at::IntArrayRef x_width, at::IntArrayRef T_in) {
-  return chain_bwd_impl(&dh, g, c, W, U, pidx, pool, x_width, T_in, nullptr, nullptr, nullptr, {});
-}
-
-std::vector<at::Tensor> lstm_chain_head_bwd(const at::Tensor& dloss, at::TensorList g, at::TensorList c,
-                                            at::TensorList W, at::TensorList U, at::TensorList pidx,
-                                            at::IntArrayRef pool, at::IntArrayRef x_width, at::IntArrayRef T_in,
-                                            const at::Tensor& hT, at::TensorList head, const at::Tensor& y,
-                                            const at::Tensor& mask, int64_t M, double alpha1, double alpha2, double w0,
-                                            double w1, at::TensorList hgrads) {
-  const HeadIn hi{head, &y, &mask, (int)M, (float)alpha1, (float)alpha2, (float)w0, (float)w1};
-  return chain_bwd_impl(nullptr, g, c, W, U, pidx, pool, x_width, T_in, &hi, &hT, &dloss, hgrads);
 }
 
 // [epoch, finished, timeout flag, 0] of this device's chain control words (tests)
@@ -1327,8 +1028,8 @@ at::Tensor lstm_chain_status(const at::Tensor& like) {
 at::Tensor lstm_chain_trace(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
   long long* p = chain_trace_buf(like.get_device());
-  at::Tensor o = at::empty({4 * 256}, like.options().dtype(at::kLong));
-  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, 1024 * sizeof(long long), hipMemcpyDeviceToDevice, stream()) ==
+  at::Tensor o = at::empty({3 * 256}, like.options().dtype(at::kLong));
+  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, 768 * sizeof(long long), hipMemcpyDeviceToDevice, stream()) ==
                   hipSuccess, "lstm_chain_trace");
   return o;
 }
@@ -1337,11 +1038,10 @@ at::Tensor lstm_chain_trace(const at::Tensor& like) {
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_fwd", &gq::lstm_chain_fwd);
+  m.impl("lstm_chain_fwd_pack", &gq::lstm_chain_fwd_pack);
   m.impl("lstm_chain_status", &gq::lstm_chain_status);
   m.impl("lstm_chain_capacity", &gq::lstm_chain_capacity);
   m.impl("lstm_chain_ctl", &gq::lstm_chain_ctl);
   m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
   m.impl("lstm_chain_bwd", &gq::lstm_chain_bwd);
-  m.impl("lstm_chain_head_fwd", &gq::lstm_chain_head_fwd);
-  m.impl("lstm_chain_head_bwd", &gq::lstm_chain_head_bwd);
 }

@@ -109,4 +109,33 @@ inline TmPool tm_pool_outputs(int P, int T, int Mp, int H, const at::TensorOptio
   return pl;
 }
 
+// ---- time4 (H = 128, Din <= 64) forward A-fragment image (time4_head.hip's 512-thread layout:
+// wave w of 8, cell cc of 4, lane = (quad, col)): U fragments [w][cc][s < 4][lane], then W
+// fragments [w][cc][s < 2][lane], each 8 bf16. Gathering them from the [K][4H] weights touches 16
+// cache lines per load instruction, so the chain forward's idle workgroups build this image once per
+// step and the time4 kernel reads it with lane-contiguous 16-B loads.
+constexpr int T4PK_U = 8 * 4 * 4 * 64;
+constexpr int T4PK_W = 8 * 4 * 2 * 64;
+constexpr int T4PK_N = T4PK_U + T4PK_W;
+
+__device__ __forceinline__ void t4_pack_one(int f, const float* __restrict__ U, const float* __restrict__ W, int Dw,
+                                            bf16x8_t* __restrict__ out) {
+  const bool isU = f < T4PK_U;
+  const int f2 = isU ? f : f - T4PK_U;
+  const int lane = f2 & 63;
+  const int s = isU ? (f2 >> 6) & 3 : (f2 >> 6) & 1;
+  const int cc = isU ? (f2 >> 8) & 3 : (f2 >> 7) & 3;
+  const int w = isU ? f2 >> 10 : f2 >> 9;
+  const int col = lane & 15, quad = lane >> 4;
+  const int gi = w + 8 * cc, au = 4 * gi + (col >> 2), ag = col & 3;
+  bf16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * s + 8 * quad + j;
+    if (isU) v[j] = (__bf16)U[(size_t)k * 512 + ag * 128 + au];
+    else v[j] = (__bf16)(W[(size_t)min(k, Dw - 1) * 512 + ag * 128 + au] * (k < Dw ? 1.f : 0.f));
+  }
+  out[f] = v;
+}
+
 }  // namespace gq

@@ -35,6 +35,8 @@ TORCH_LIBRARY(gnnqc, m) {
         "int pool=0) -> Tensor");
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
   m.def("lstm_chain_fwd(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train) -> Tensor[]");
+  m.def("lstm_chain_fwd_pack(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train, Tensor Wt4, "
+        "Tensor Ut4) -> Tensor[]");
   m.def("lstm_chain_status(Tensor like) -> Tensor");
   m.def("lstm_chain_capacity(Tensor like) -> int");
   m.def("lstm_chain_ctl(Tensor like) -> Tensor");
@@ -43,12 +45,11 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_chain_trace(Tensor like) -> Tensor");
   m.def("lstm_chain_bwd(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");
-  m.def("lstm_chain_head_fwd(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train, Tensor[] head, "
-        "Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, "
-        "Tensor(b!) hist) -> Tensor[]");
-  m.def("lstm_chain_head_bwd(Tensor dloss, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
-        "int[] x_width, int[] T_in, Tensor hT, Tensor[] head, Tensor y, Tensor mask, int M, float alpha1, "
-        "float alpha2, float w0, float w1, Tensor(a!)[] hgrads) -> Tensor[]");
+  m.def("time4_head_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor pk, bool train, Tensor[] head, Tensor y, Tensor mask, "
+        "int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");
+  m.def("time4_head_bwd(Tensor dloss, Tensor x, Tensor h, Tensor g, Tensor c, Tensor W, Tensor U, Tensor[] head, "
+        "Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!)[] hgrads) -> Tensor[]");
+  m.def("time4_trace(Tensor like) -> Tensor");
   m.def("lstm_tm_bwd_pipe(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T, Tensor gz, Tensor gx, "
         "Tensor gh, Tensor gW, int g_period, int g_hshift, Tensor gws, Tensor rws, Tensor rW, Tensor(a!) rdW, "
         "Tensor(b!) rdU, Tensor(c!) rdb) -> Tensor");

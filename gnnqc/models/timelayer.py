@@ -144,10 +144,10 @@ class TimeLayer(nn.Module):
         return h
 
     def head_chain_ok(self, h: torch.Tensor) -> bool:
-        """Whether the whole LSTM branch of a time-major input ``h`` [T, Mp, C] runs as one headed
-        chain (:func:`gnnqc.ops.lstm.lstm_chain_head_tm`): every layer but the last in the chain
-        plan, the last one H = 128 returning its last state on a 33..64-channel input."""
-        from ..ops.lstm import _chain_on, chain_fits
+        """Whether the whole LSTM branch of a time-major input ``h`` [T, Mp, C] runs as the chain +
+        time4/head kernels (:func:`gnnqc.ops.lstm.lstm_chain_head_tm`): every layer but the last in
+        the chain plan, the last one H = 128 returning its last state after <= 16 steps."""
+        from ..ops.lstm import _chain_on
         if self.layer_type != "lstm" or not _chain_on() or os.environ.get("GNNQC_HEAD_CHAIN", "1") != "1":
             return False
         seq = self._sequence()
@@ -156,10 +156,12 @@ class TimeLayer(nn.Module):
             return False
         last = seq[-1]
         mods, pools, _ = plan
+        T = h.shape[0]
+        for p in pools:
+            T = T // p if p else T
         return (isinstance(last, LSTM) and not last.return_sequences and last.units == 128
-                and last.activation == "tanh" and last.compute_bf16 and pools[-1] in (0, 3)
-                and 32 < mods[-1].units <= 64 and last.kernel.shape[0] == mods[-1].units
-                and chain_fits(h.shape[1], len(mods) + 1, h.device))
+                and last.activation == "tanh" and last.compute_bf16 and 1 <= T <= 16
+                and mods[-1].units % 4 == 0 and mods[-1].units <= 64 and last.kernel.shape[0] == mods[-1].units)
 
     def forward_time_major_head(self, h: torch.Tensor, M: int, head, alphas, y: torch.Tensor, mask: torch.Tensor,
                                 w0: float, w1: float, sums=None, hist=None):
@@ -167,7 +169,7 @@ class TimeLayer(nn.Module):
         input (see :meth:`head_chain_ok`), one launch forward and one backward."""
         from ..ops.lstm import lstm_chain_head_tm
         mods, pools, _ = self._chain_plan(self._sequence(), h)
-        return lstm_chain_head_tm(h, list(mods) + [self.time4], list(pools) + [0], head, y, mask, M,
+        return lstm_chain_head_tm(h, list(mods) + [self.time4], list(pools), head, y, mask, M,
                                   alphas[0], alphas[1], w0, w1, sums, hist)
 
     @staticmethod

@@ -435,11 +435,11 @@ class _HipLSTMChain(torch.autograd.Function):
 
 
 class _HipLSTMChainHead(torch.autograd.Function):
-    """CML TimeLayer + classifier head + weighted BCE as ONE forward launch and ONE backward
-    launch (``lstm_chain.hip`` + ``chain_head.h``): the six pipelined time-major layers, the
-    H = 128 last layer (time4, last state) as a seventh chain stage, the Dense head, the loss
-    and the metric accumulation in the forward; the head backward (recomputed from time4's last
-    state), time4's reverse recurrence and the six reverse recurrences in the backward. The
+    """CML TimeLayer + classifier head + weighted BCE in two forward and two backward launches:
+    the six pipelined time-major layers as ONE chain kernel (``lstm_chain.hip``), then time4
+    (H = 128, last state) with the Dense head, the loss and the metric accumulation as ONE
+    kernel (``time4_head.hip``); backward: the head backward + time4's reverse recurrence as ONE
+    kernel, whose dx (gradient of the chain's pooled output) feeds ONE chain backward. The
     weight-gradient passes of all seven layers then run as one ``lstm_grads_multi`` launch.
 
     Inputs: x [T, Mp, C] time-major, y / mask [M]; ``consts`` = (alpha1, alpha2, w0, w1);
@@ -448,22 +448,26 @@ class _HipLSTMChainHead(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, mask, sums, hist, consts, pools, M, *params):
         from ..utils.native import hip_ops
-        ns = len(pools)
-        Ws = [params[3 * i].contiguous() for i in range(ns)]
-        Us = [params[3 * i + 1].contiguous() for i in range(ns)]
-        bs = [params[3 * i + 2].contiguous() for i in range(ns)]
-        head = [p.contiguous() for p in params[3 * ns:]]
+        ops = hip_ops()
+        ns = len(pools)                    # chain stages (time4 follows)
+        Ws = [params[3 * i].contiguous() for i in range(ns + 1)]
+        Us = [params[3 * i + 1].contiguous() for i in range(ns + 1)]
+        bs = [params[3 * i + 2].contiguous() for i in range(ns + 1)]
+        head = [p.contiguous() for p in params[3 * (ns + 1):]]
         need = any(ctx.needs_input_grad)
         e = x.new_zeros(0)
-        res = hip_ops().lstm_chain_head_fwd(x, Ws, Us, bs, [int(p) for p in pools], need, head, y, mask, int(M),
-                                           *[float(c) for c in consts],
-                                           sums if sums is not None else e.double(),
-                                           hist if hist is not None else e)
-        outs, logits, loss = res[:5 * ns], res[5 * ns], res[5 * ns + 1]
+        # (the chain's spare workgroups build time4's weight-fragment image on the way)
+        outs = ops.lstm_chain_fwd_pack(x, Ws[:ns], Us[:ns], bs[:ns], [int(p) for p in pools], need, Ws[ns], Us[ns])
+        pk = outs.pop()
+        xt = outs[5 * (ns - 1) + 3] if pools[-1] else outs[5 * (ns - 1)]      # time4's input [T4, Mp, C]
+        h4, g4, c4, logits, loss = ops.time4_head_fwd(xt, Ws[ns], Us[ns], bs[ns], pk, need, head, y, mask, int(M),
+                                                      *[float(c) for c in consts],
+                                                      sums if sums is not None else e.double(),
+                                                      hist if hist is not None else e)
         ctx.pools, ctx.consts, ctx.M = tuple(int(p) for p in pools), tuple(float(c) for c in consts), int(M)
         ctx.params = params
         if need:
-            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs)
+            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs, h4, g4, c4)
         ctx.mark_non_differentiable(logits)
         return loss.reshape(()), logits
 
@@ -475,53 +479,61 @@ class _HipLSTMChainHead(torch.autograd.Function):
         ns = len(pools)
         saved = ctx.saved_tensors
         x, y, mask = saved[:3]
-        Ws, Us = saved[3:3 + ns], saved[3 + ns:3 + 2 * ns]
-        head = saved[3 + 2 * ns:9 + 2 * ns]
-        outs = saved[9 + 2 * ns:]
+        Ws, Us = saved[3:4 + ns], saved[4 + ns:5 + 2 * ns]
+        head = saved[5 + 2 * ns:11 + 2 * ns]
+        outs = saved[11 + 2 * ns:11 + 7 * ns]
+        h4, g4, c4 = saved[11 + 7 * ns:]
         need = ctx.needs_input_grad
-        nparam = 3 * ns
-        hsinks = [_grad_sink(p) for p in ctx.params[nparam:]]
+        npar = 3 * (ns + 1)
 
         def layer_x(i):
             if i == 0:
                 return x
             return outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)]
 
-        order = list(reversed(range(ns)))
-        e8 = x.new_zeros(0, dtype=torch.uint8)
-        hT = outs[5 * (ns - 1)][-1]                        # time4's last state [Mp, 128] (contiguous)
         g = dloss.reshape(1).float()
         if not g.is_contiguous():
             g = g.contiguous()
-        res = ops.lstm_chain_head_bwd(g, [outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
-                                      [Ws[i] for i in order], [Us[i] for i in order],
-                                      [outs[5 * i + 4] if pools[i] else e8 for i in order],
-                                      [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
-                                      [outs[5 * i].shape[0] for i in order], hT, list(head), y, mask, ctx.M,
-                                      *ctx.consts, [s for s, _ in hsinks])
-        grads = [None] * nparam
+        hsinks = [_grad_sink(p) for p in ctx.params[npar:]]
+        xt = layer_x(ns)
+        dz4, dxt = ops.time4_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], list(head), y, mask, ctx.M, *ctx.consts,
+                                      [s for s, _ in hsinks])
+        order = list(reversed(range(ns)))
+        e8 = x.new_zeros(0, dtype=torch.uint8)
+        res = ops.lstm_chain_bwd(dxt, [outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
+                                 [Ws[i] for i in order], [Us[i] for i in order],
+                                 [outs[5 * i + 4] if pools[i] else e8 for i in order],
+                                 [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
+                                 [outs[5 * i].shape[0] for i in order])
+        dzs = {ns: dz4}
+        hs = {ns: h4}
         for k, i in enumerate(order):
+            dzs[i] = res[k]
+            hs[i] = outs[5 * i]
+        grads = [None] * npar
+        for i in [ns] + order:
             nw = need[8 + 3 * i:11 + 3 * i]
             if not any(nw):
                 continue
-            h = outs[5 * i]
+            h = hs[i]
             xi = layer_x(i)
             sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
             if (_pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
                     and len(_Pipe.batch) < _MULTI_MAX - 2):
-                _Pipe.batch.append(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
+                _Pipe.batch.append(_pipe_job(dzs[i], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
             else:
-                ops.lstm_tm_grads(res[k], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
+                ops.lstm_tm_grads(dzs[i], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
             grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]
-        hgrads = [None if (direct or not n) else buf for (buf, direct), n in zip(hsinks, need[8 + nparam:])]
+        hgrads = [None if (direct or not n) else buf for (buf, direct), n in zip(hsinks, need[8 + npar:])]
         dx = res[ns]
         return (dx if need[0] else None, None, None, None, None, None, None, None, *grads, *hgrads)
 
 
 def lstm_chain_head_tm(x_tm: torch.Tensor, mods, pools, head, y: torch.Tensor, mask: torch.Tensor, M: int,
                        alpha1: float, alpha2: float, w0: float, w1: float, sums=None, hist=None):
-    """(loss, logits) of ``mods`` (LSTM modules; the last one H = 128 returning its last state)
-    followed by the Dense head ``head`` = (dense, dense2, dense_out) and the weighted BCE."""
+    """(loss, logits) of ``mods`` (LSTM modules: the chain layers, then time4 - H = 128 returning its
+    last state) followed by the Dense head ``head`` = (dense, dense2, dense_out) and the weighted
+    BCE. ``pools``: the chain layers' pools (time4 has none)."""
     params = []
     for m in mods:
         params += [m.kernel, m.recurrent_kernel, m.bias]

@@ -1,10 +1,8 @@
 #!/usr/bin/env python3
-"""Per-stage timeline of the CML chain kernels with and without the headed time4 stage.
-
-For the six-stage chain (lstm_chain_fwd / _bwd) and the seven-stage headed chain
-(lstm_chain_head_fwd / _bwd) prints the launch time (HIP events, mean of 50) and, from the
-kernels' s_memrealtime trace, every stage's start / end (tile 0, us after the first workgroup
-started). One JSON line per measurement."""
+"""Timeline of the CML TimeLayer kernels: the six-stage chain (lstm_chain_fwd / _bwd, per-stage
+start / end from the kernels' s_memrealtime trace, tile 0, us after the first workgroup started)
+and the time4 + head kernels (time4_head_fwd / _bwd); launch times are HIP-event means of 50.
+One JSON line per measurement."""
 import json
 import os
 import sys
@@ -30,19 +28,23 @@ def timeit(fn, reps=50):
 def stages(ops, x, k, nt8, mid=False):
     tr = ops.lstm_chain_trace(x).cpu()
     m = tr[512:768]
-    m2 = tr[768:]
     tr = tr[:512].view(256, 2)
     t0 = int(tr[:k * nt8:nt8, 0].min())
     out = []
     for s in range(k):
         row = [round((int(tr[s * nt8, 0]) - t0) / 100, 1)]
-        if mid or s == k - 1:
+        if mid:
             row.append(round((int(m[s * nt8]) - t0) / 100, 1))
-        if mid and s == 0:
-            row.append(round((int(m2[s * nt8]) - t0) / 100, 1))
         row.append(round((int(tr[s * nt8, 1]) - t0) / 100, 1))
         out.append(row)
     return out
+
+
+def t4marks(ops, x, ntiles=8):
+    """time4 kernel marks per tile (us after the first tile started): start, prologue, steps..., end."""
+    tr = ops.time4_trace(x).cpu()[:16 * ntiles].view(ntiles, 16)
+    t0 = int(tr[:, 0].min())
+    return [[round((int(v) - t0) / 100, 1) for v in row if int(v) >= t0] for row in tr]
 
 
 def main():
@@ -72,29 +74,33 @@ def main():
     hc = (0.3, 0.3, 1.0, 5.0)
     us6 = timeit(lambda: ops.lstm_chain_fwd(x, Ws[:6], Us[:6], bs[:6], pools[:6], True))
     print(json.dumps({"fwd": "chain6", "us": round(us6, 2), "stages": stages(ops, x, 6, nt8)}), flush=True)
-    us7 = timeit(lambda: ops.lstm_chain_head_fwd(x, Ws, Us, bs, pools, True, head, y, mask, M, *hc, e.double(), e))
-    print(json.dumps({"fwd": "chain7+head", "us": round(us7, 2), "stages": stages(ops, x, 7, nt8)}), flush=True)
-    # backward
-    outs = ops.lstm_chain_head_fwd(x, Ws, Us, bs, pools, True, head, y, mask, M, *hc, e.double(), e)
+    outs = ops.lstm_chain_fwd_pack(x, Ws[:6], Us[:6], bs[:6], pools[:6], True, Ws[6], Us[6])
+    pk = outs.pop()
+    up = timeit(lambda: ops.lstm_chain_fwd_pack(x, Ws[:6], Us[:6], bs[:6], pools[:6], True, Ws[6], Us[6]))
+    print(json.dumps({"fwd": "chain6+pack", "us": round(up, 2)}), flush=True)
+    xt = outs[5 * 5 + 3]
+    ut = timeit(lambda: ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e))
+    print(json.dumps({"fwd": "time4+head", "us": round(ut, 2), "marks": t4marks(ops, x)}), flush=True)
+    ue = timeit(lambda: ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, False, head, y, mask, M, *hc, e.double(), e))
+    print(json.dumps({"fwd": "time4+head eval", "us": round(ue, 2), "marks": t4marks(ops, x)}), flush=True)
+    h4, g4, c4, logits, loss = ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e)
+    hg = [torch.zeros_like(p) for p in head]
+    one = torch.ones(1, device=dev)
+    ub = timeit(lambda: ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], head, y, mask, M, *hc, hg))
+    print(json.dumps({"bwd": "head+time4", "us": round(ub, 2), "marks": t4marks(ops, x)}), flush=True)
+    dz4, dxt = ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], head, y, mask, M, *hc, hg)
     e8 = torch.zeros(0, dtype=torch.uint8, device=dev)
     xw = [din] + units[:-1]
-    Ts = [outs[5 * i].shape[0] for i in range(7)]
+    Ts = [outs[5 * i].shape[0] for i in range(6)]
     order6 = list(reversed(range(6)))
-    dh = torch.randn(Ts[5] // 3, Mp, 64, device=dev)
-    a6 = (dh, [outs[5 * i + 1] for i in order6], [outs[5 * i + 2] for i in order6], [Ws[i] for i in order6],
+    a6 = (dxt, [outs[5 * i + 1] for i in order6], [outs[5 * i + 2] for i in order6], [Ws[i] for i in order6],
           [Us[i] for i in order6], [outs[5 * i + 4] if pools[i] else e8 for i in order6],
           [pools[i] for i in order6], [xw[i] for i in order6], [Ts[i] for i in order6])
     ub6 = timeit(lambda: ops.lstm_chain_bwd(*a6))
     print(json.dumps({"bwd": "chain6", "us": round(ub6, 2), "stages": stages(ops, x, 6, nt8, True)}), flush=True)
-    order7 = list(reversed(range(7)))
-    hT = outs[5 * 6][-1]
-    hg = [torch.zeros_like(p) for p in head]
-    one = torch.ones(1, device=dev)
-    a7 = (one, [outs[5 * i + 1] for i in order7], [outs[5 * i + 2] for i in order7], [Ws[i] for i in order7],
-          [Us[i] for i in order7], [outs[5 * i + 4] if pools[i] else e8 for i in order7],
-          [pools[i] for i in order7], [xw[i] for i in order7], [Ts[i] for i in order7], hT, head, y, mask, M, *hc, hg)
-    ub7 = timeit(lambda: ops.lstm_chain_head_bwd(*a7))
-    print(json.dumps({"bwd": "chain7+head", "us": round(ub7, 2), "stages": stages(ops, x, 7, nt8, True)}), flush=True)
+    both = timeit(lambda: (ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e),
+                           ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], head, y, mask, M, *hc, hg)))
+    print(json.dumps({"time4_head_fwd_bwd_us": round(both, 2)}), flush=True)
     st = ops.lstm_chain_status(x).cpu().tolist()
     print(json.dumps({"status": st}), flush=True)
 
