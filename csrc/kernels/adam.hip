@@ -12,20 +12,30 @@
 
 namespace gq {
 
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// zero_g: the gradient buffer is cleared once read (the next step's backward accumulates onto
+// zeros; the trainer then launches no separate zero-fill per step), also for a skipped step.
+__global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ lr_p, const float* __restrict__ step_p,
                             long n, float b1, float b2, float eps, float gscale, float wd,
-                            const int* __restrict__ ok_p) {
-  if (ok_p != nullptr && *ok_p == 0) return;   // non-finite gradients: skip the whole update
+                            const int* __restrict__ ok_p, int zero_g) {
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (ok_p != nullptr && *ok_p == 0) {         // non-finite gradients: skip the whole update
+    if (zero_g) {
+      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
+        reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) g[i] = 0.f;
+    }
+    return;
+  }
   const float step = *step_p;
   const float lr = *lr_p;
   const float bc1 = 1.0f - powf(b1, step);
   const float bc2 = 1.0f - powf(b2, step);
   const float alpha = lr * sqrtf(bc2) / bc1;
-  const long n4 = n / 4;
-  const long stride = (long)gridDim.x * blockDim.x;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 gg = reinterpret_cast<const float4*>(g)[i];
+    if (zero_g) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 pp = reinterpret_cast<float4*>(p)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
@@ -44,6 +54,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
   for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
     float gc = g[i] * gscale + wd * p[i];
+    if (zero_g) g[i] = 0.f;
     m[i] = b1 * m[i] + (1.f - b1) * gc;
     v[i] = b2 * v[i] + (1.f - b2) * gc * gc;
     p[i] -= alpha * m[i] / (sqrtf(v[i]) + eps);
@@ -127,9 +138,9 @@ void grad_guard(const at::Tensor& g, at::Tensor state, at::Tensor step, const c1
   GQ_LAUNCH_CHECK();
 }
 
-void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, const at::Tensor& lr,
+void adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at::Tensor& lr,
                const at::Tensor& step, double b1, double b2, double eps, double gscale, double wd,
-               const c10::optional<at::Tensor>& ok) {
+               const c10::optional<at::Tensor>& ok, bool zero_grad) {
   const at::Tensor* ops[] = {&p, &g, &m, &v, &lr, &step};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "adam operand");
   if (ok.has_value())
@@ -144,7 +155,7 @@ void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, co
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(block), 0, stream(), p.data_ptr<float>(), g.data_ptr<float>(),
                      m.data_ptr<float>(), v.data_ptr<float>(), lr.data_ptr<float>(), step.data_ptr<float>(), n,
                      (float)b1, (float)b2, (float)eps, (float)gscale, (float)wd,
-                     ok.has_value() ? ok->data_ptr<int>() + 2 : nullptr);
+                     ok.has_value() ? ok->data_ptr<int>() + 2 : nullptr, zero_grad ? 1 : 0);
   GQ_LAUNCH_CHECK();
 }
 

@@ -131,10 +131,18 @@ __global__ __launch_bounds__(256) void gcn_pool_fwd_kernel(const float* __restri
     pal[j] = alpha[f0 + j];
   }
   const long vrows = Mp > 0 ? (long)Mp * T : rows;        // virtual rows incl. zero padding rows
+  float* sw = sx + RPB * L;                         // staged: the node weights of the block's samples
   for (long row0 = (long)blockIdx.x * RPB; row0 < vrows; row0 += (long)gridDim.x * RPB) {
+    const int b0 = (int)(row0 / T);
     if (staged) {
       __syncthreads();
-      if (row0 < rows) gcn_stage_rows(x, sx, row0, RPB, rows, L);
+      if (row0 < rows) {
+        gcn_stage_rows(x, sx, row0, RPB, rows, L);
+        // samples b0 .. of rows row0 .. row0 + RPB - 1 (<= RPB / T + 2 of them): the per-node
+        // weight loads then leave the node loop (they were its serial memory round trips)
+        const int nb = min((int)((min(row0 + RPB, rows) - 1) / T) - b0 + 1, RPB / T + 2);
+        for (int i = threadIdx.x; i < nb * N; i += blockDim.x) sw[i] = w[(long)b0 * N + i];
+      }
       __syncthreads();
     }
     const long row = row0 + r;
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(256) void gcn_pool_fwd_kernel(const float* __restri
       continue;
     }
     const float* xr = staged ? sx + r * L : x + row * (long)L;
-    const float* wr = w + (long)b * N;
+    const float* wr = staged ? sw + (long)(b - b0) * N : w + (long)b * N;
     float acc[FQ];
 #pragma unroll
     for (int j = 0; j < FQ; ++j) acc[j] = 0.f;
@@ -193,24 +201,42 @@ __global__ void gcn_pool_bwd_kernel(const float* __restrict__ x, const float* __
   _Pragma("unroll") for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + f];
   const float bb = bias[f], sc = scale[f], sh = shift[f], al = alpha[f];
   const long nrows = (long)B * T;
-  for (long row = (long)blockIdx.x * rows_per_blk + rsub; row < nrows; row += (long)gridDim.x * rows_per_blk) {
+  // staged (N * Cin <= GCN_STAGE_MAX): the pass's x rows and its samples' node weights are
+  // copied to LDS with coalesced loads first, so the node loop makes no memory round trips
+  // (its per-node global loads, behind a data-dependent branch, were ~all of the kernel's time)
+  extern __shared__ __attribute__((aligned(16))) float sbx[];
+  const int L = N * Cin;
+  const bool staged = L <= GCN_STAGE_MAX;
+  float* sbw = sbx + rows_per_blk * L;
+  for (long r0 = (long)blockIdx.x * rows_per_blk; r0 < nrows; r0 += (long)gridDim.x * rows_per_blk) {
+    const long row = r0 + rsub;
+    const int b0 = (int)(r0 / T);
+    if (staged) {
+      __syncthreads();
+      gcn_stage_rows(x, sbx, r0, rows_per_blk, nrows, L);
+      const int nb = min((int)((min(r0 + rows_per_blk, nrows) - 1) / T) - b0 + 1, rows_per_blk / T + 2);
+      for (int i = threadIdx.x; i < nb * N; i += blockDim.x) sbw[i] = w[(long)b0 * N + i];
+      __syncthreads();
+    }
+    if (row >= nrows) continue;
     const int b = row / T;
     const long dro = dmp > 0 ? ((row % T) * dmp + row / T) * (long)dstride : row * (long)dstride;
     const float g = dout[dro + c_off + f];
-    const float* xr = x + row * (long)N * Cin;
-    const float* wr = w + (long)b * N;
+    const float* xr = staged ? sbx + rsub * L : x + row * (long)L;
+    const float* wr = staged ? sbw + (long)(b - b0) * N : w + (long)b * N;
     for (int n = 0; n < N; ++n) {
-      const float wn = wr[n];
-      if (wn == 0.f) continue;
+      const float wn = wr[n];                     // wn == 0 (masked / unpooled node): da = 0
+      float xv[Cin];
+      _Pragma("unroll") for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
       float z = bb;
-      _Pragma("unroll") for (int k = 0; k < Cin; ++k) z += xr[n * Cin + k] * wk[k];
+      _Pragma("unroll") for (int k = 0; k < Cin; ++k) z += xv[k] * wk[k];
       const float y = z * sc + sh;
       const float da = wn * g;
       const float dy = y > 0.f ? da : al * da;
       acc[0] += dy;
       acc[1] += dy * z;
       acc[2] += y > 0.f ? 0.f : da * y;
-      _Pragma("unroll") for (int k = 0; k < Cin; ++k) acc[3 + k] += xr[n * Cin + k] * dy;
+      _Pragma("unroll") for (int k = 0; k < Cin; ++k) acc[3 + k] += xv[k] * dy;
     }
   }
   // reduce over the rows of the block (threads with equal f): shuffles inside the
@@ -404,7 +430,7 @@ at::Tensor gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
   const long rows = Mp > 0 ? (long)Mp * T : (long)B * T;
   const float* anom_p = Ca ? anom.data_ptr<float>() : nullptr;
   const bool staged = N * Cin <= GCN_STAGE_MAX;
-  const size_t smem = staged ? (size_t)64 * N * Cin * sizeof(float) : 0;
+  const size_t smem = staged ? ((size_t)64 * N * Cin + (size_t)(64 / T + 2) * N) * sizeof(float) : 0;
   GQ_CIN_DISPATCH(Cin, GQ_GCN_F_DISPATCH(F,
       hipLaunchKernelGGL((gcn_pool_fwd_kernel<CIN, FF>), dim3(grid_for(rows, 64, 8192)), dim3(256), smem, stream(),
                          x.data_ptr<float>(), w.data_ptr<float>(), anom_p, W.data_ptr<float>(), b.data_ptr<float>(),
@@ -425,15 +451,19 @@ at::Tensor gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tens
   c10::DeviceGuard guard(x.device());
   const int nacc = 3 + Cin;
   const int rows_per_blk = 256 / F;
-  const int nblk = grid_for((long)B * T, rows_per_blk, 2048);
+  // a few passes per workgroup: fewer partial rows for gcn_bwd_finalize to sum
+  const int nblk = grid_for((long)B * T, rows_per_blk, 512);
   at::Tensor partial = at::empty({nblk, nacc, F}, x.options());
-  GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_pool_bwd_kernel<CIN>, dim3(nblk), dim3(256), 0, stream(), x.data_ptr<float>(),
+  const bool staged = N * Cin <= GCN_STAGE_MAX;
+  const size_t smem = staged ? ((size_t)rows_per_blk * N * Cin + (size_t)(rows_per_blk / T + 2) * N) * sizeof(float) : 0;
+  GQ_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_pool_bwd_kernel<CIN>, dim3(nblk), dim3(256), smem, stream(), x.data_ptr<float>(),
                      w.data_ptr<float>(), dout.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(),
                      scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
                      partial.data_ptr<float>(), B, T, N, F, (int)c_off, (int)dout.size(2),
                      time_major ? (int)dout.size(1) : 0));
   GQ_LAUNCH_CHECK();
-  return colsum(partial);   // [3+Cin, F], fixed-order (deterministic) reduction
+  // [nblk, 3+Cin, F]: gcn_bwd_finalize sums the blocks in fixed order (deterministic)
+  return partial;
 }
 
 at::Tensor gcn_pool_bwd_input(const at::Tensor& x, const at::Tensor& w, const at::Tensor& mask,

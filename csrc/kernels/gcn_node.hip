@@ -446,7 +446,7 @@ at::Tensor gcn_node_bwd(const at::Tensor& x, const at::Tensor& bitsT, const at::
                          partial.data_ptr<float>(), g.B, g.T, g.N, g.F, (int)dout.size(2), (int)dout.size(1), g.NWd,
                          g.tchunk)));
   GQ_LAUNCH_CHECK();
-  return colsum(partial);
+  return partial;      // [blocks, 3+Cin, F]: gcn_bwd_finalize sums the blocks (fixed order)
 }
 
 at::Tensor gcn_node_bwd_input(const at::Tensor& x, const at::Tensor& bitsT, const at::Tensor& rs,

@@ -30,6 +30,7 @@
 // Each stage also writes everything the per-layer kernels write (h, gate / cell state for
 // the backward, pooled output + argmax bytes), so the backward is unchanged.
 #include "common.h"
+#include "lstm_grads_body.h"
 #include "lstm_tm_common.h"
 
 namespace gq {
@@ -322,14 +323,38 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   }
 }
 
-__device__ __forceinline__ void chain_finish(int* ctl, int nblk) {
+__device__ __forceinline__ void chain_finish(int* ctl, int nblk, int* sync = nullptr) {
   if (threadIdx.x == 0) {
     const int old = __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == nblk - 1) {            // last workgroup: next launch gets a new epoch
+      if (sync != nullptr)            // (every waiter of this launch is past its wait)
+        for (int i = 0; i < 16; ++i) __hip_atomic_store(sync + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+// Lane 0 polls an arrival counter (sc1 loads, short naps) until it reaches `want`, then the
+// workgroup barrier releases the other waves. Bounded like chain_wait: a timeout (or one seen
+// elsewhere in the launch) sets / honours ctl[2] and the step is rejected by the guard.
+template <bool LONG = false>
+__device__ __forceinline__ void chain_wait_count(const int* p, int want, int* ctl) {
+  if (threadIdx.x == 0) {
+    const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lim = lim0 > 0 ? lim0 : CHAIN_SPIN;
+    for (int it = 0;; ++it) {
+      if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+      if (it >= lim || ((it & 63) == 63 && __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      if (LONG) __builtin_amdgcn_s_sleep(40);
+      else if (it < 64) __builtin_amdgcn_s_sleep(2);
+      else __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __syncthreads();
 }
 
 template <bool TRAIN>
@@ -395,11 +420,26 @@ struct ChainBStage {
   int H, T, Din, Dw, KX, P, Ts;
 };
 
+// A weight-gradient pass run by the backward chain's spare workgroups (lstm_chain_bwd_grads):
+// it starts when the stage whose dz it reads has finished (or at once: wait < 0), and its split
+// records are reduced into the gradient buffers by the same workgroups.
+struct ChainGJ {
+  GradJob g;
+  RedJob r;          // r.kb: slot lanes of the in-launch reduction (16 .. 256)
+  int key;           // HG * 8 + DT
+  int wait;          // chain stage producing dz (-1: ready at launch)
+  int wait_n;        // that stage's workgroups
+};
+
 struct ChainBArgs {
   ChainBStage st[CHAIN_MAX];
   int ns, ntiles, nt8, Mp;
   int* ctl;
   long long* trace;
+  ChainGJ gj[CHAIN_MAX];
+  int njobs;
+  int* sync;         // [0, 8): stage-done counters, [8, 16): job arrival tickets (reset by the last workgroup)
+  long long* gtrace; // profiling: [job][256 workgroups][3] = pass start, arrival, reduction end (s_memrealtime)
 };
 
 template <int H, int KX>
@@ -693,17 +733,109 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   if constexpr (!PUBW) store_dx((T - 1) & 1, 0, tagb);     // dx tile of t = 0
 }
 
+// In-launch split reduction of job r by workgroup `part` of `nparts`: slots [s0, s1) of the
+// record, SL slot lanes x (256 / SL) split lanes, every split summed in a fixed order, records
+// read with sc1 loads (they were stored sc1). One writer per gradient element: deterministic.
+__device__ __forceinline__ void chain_grads_reduce(const RedJob& r, int part, int nparts, float* red) {
+  const int SL = r.kb, NL = 256 / SL;
+  const int tid = threadIdx.x, sl = tid % SL, l = tid / SL;
+  const int per = (r.RC + nparts - 1) / nparts;
+  const int s0 = part * per, s1 = min(r.RC, s0 + per);
+  for (int base = s0; base < s1; base += SL) {
+    const int slot = min(base + sl, s1 - 1);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int sp = l;
+    for (; sp + 3 * NL < r.splits; sp += 4 * NL) {
+      a0 += ld_sc1(r.ws + (size_t)sp * r.RC + slot);
+      a1 += ld_sc1(r.ws + (size_t)(sp + NL) * r.RC + slot);
+      a2 += ld_sc1(r.ws + (size_t)(sp + 2 * NL) * r.RC + slot);
+      a3 += ld_sc1(r.ws + (size_t)(sp + 3 * NL) * r.RC + slot);
+    }
+    for (; sp < r.splits; sp += NL) a0 += ld_sc1(r.ws + (size_t)sp * r.RC + slot);
+    red[tid] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (tid < SL && base + tid < s1) {
+      float v = 0.f;
+      for (int k = 0; k < NL; ++k) v += red[k * SL + tid];
+      grads_add(v, base + tid, r.ncb, r.DT, r.HT, r.Din, r.H, r.dW, r.db, r.dU);
+    }
+    __syncthreads();
+  }
+}
+
+// One job's gradient-pass share, one instance per (HG, DT) so each gets its own register
+// allocation (one function holding all twenty spilled in every one of them).
+template <int HG, int DT>
+__device__ __noinline__ void chain_grads_job(const ChainBArgs* A, __attribute__((address_space(3))) char* lds, int gb,
+                                             int k) {
+  const GradJob& g = A->gj[k].g;
+  lstm_grads_body<HG, DT, 4, true>(g.dz, g.x, g.h, g.W, nullptr, g.ws, g.rows, g.period, g.hshift, g.Din, g.ldx, 0,
+                                   g.Din, g.xg, g.x_elems, gb % g.ncb, gb / g.ncb, g.ncb, g.splits, (char*)lds);
+}
+
+// The spare workgroups' role (256 of their threads): every job in order - wait for its dz,
+// this workgroup's (column block, split) share of the gradient pass, arrival, then (once all
+// of the job's workgroups arrived) this workgroup's slice of the reduction. A points at the
+// kernel's own argument segment (the kernel passes it: in a called function the kernarg
+// builtin is null), so nothing is copied by value.
+__device__ __noinline__ void chain_grads_role(const ChainBArgs* A, __attribute__((address_space(3))) char* lds, int gb) {
+  int* ctl = A->ctl;
+  // sync[16]: profiling knobs (bit 0: waits and arrivals only; bit 1: long naps in stage waits)
+  const int dbg = __hip_atomic_load(A->sync + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < A->njobs; ++k) {
+    const ChainGJ* J = &A->gj[k];
+    const int nb = J->g.nblocks;
+    if (gb >= nb) continue;                       // (workgroup-uniform)
+    if (J->wait >= 0) {
+      if (dbg & 2) chain_wait_count<true>(A->sync + J->wait, J->wait_n, ctl);
+      else chain_wait_count(A->sync + J->wait, J->wait_n, ctl);
+      // the stage published dz with plain stores + release: acquire before reading them
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    long long* gt = A->gtrace + ((size_t)k * 256 + min(gb, 255)) * 3;
+    if (threadIdx.x == 0) gt[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (!(dbg & 1)) switch (J->key) {
+#define GQ_CG(HG, DT) case HG * 8 + DT: chain_grads_job<HG, DT>(A, lds, gb, k); break;
+#define GQ_CG_H(HG) GQ_CG(HG, 1) GQ_CG(HG, 2) GQ_CG(HG, 3) GQ_CG(HG, 4) GQ_CG(HG, 5)
+      GQ_CG_H(16) GQ_CG_H(32) GQ_CG_H(64) GQ_CG_H(128)
+#undef GQ_CG_H
+#undef GQ_CG
+      default: break;
+    }
+    // records stored sc1: every wave's stores acknowledged, then one arrival per workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(A->sync + 8 + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gt[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+    chain_wait_count(A->sync + 8 + k, nb, ctl);
+    if (!(dbg & 1)) chain_grads_reduce(J->r, gb, nb, reinterpret_cast<float*>((char*)lds));
+    if (threadIdx.x == 0) gt[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
 __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   const int nblk = gridDim.x;
+  __shared__ __attribute__((aligned(16))) char smem[CHAINB_LDS];
+  if ((int)blockIdx.x >= A.ns * A.nt8) {          // spare workgroups: weight-gradient passes
+    if (threadIdx.x >= 256) return;
+    chain_grads_role((const ChainBArgs*)__builtin_amdgcn_kernarg_segment_ptr(),
+                     (__attribute__((address_space(3))) char*)smem, (int)blockIdx.x - A.ns * A.nt8);
+    __syncthreads();
+    chain_finish(A.ctl, nblk, A.sync);
+    return;
+  }
   const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
   if (s >= A.ns || tile >= A.ntiles) {
-    chain_finish(A.ctl, nblk);
+    chain_finish(A.ctl, nblk, A.sync);
     return;
   }
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned tagb = chain_tag_base(E);
-  __shared__ __attribute__((aligned(16))) char smem[CHAINB_LDS];
   // the stage record is loaded field by field from the kernel arguments (scalar loads): a
   // reference into the by-value argument array made the compiler copy the whole array to
   // scratch and read every field from there inside the step loop
@@ -735,16 +867,28 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
 #undef GQ_CHAINB_BODY
 #undef GQ_CHAINB_BODY2
 #undef GQ_CHAINB_BODY3
+  // stage done: every storing wave's dz / dx stores retired, then one lane releases them
+  // (agent fence: written back from this XCD's L2) and counts this tile as finished
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-  chain_finish(A.ctl, nblk);
+  if (threadIdx.x == 0) {
+    A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (A.njobs > 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(A.sync + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  chain_finish(A.ctl, nblk, A.sync);
 }
 
 // ---------------------------------------------------------------------------------------
 // host
 static long long* chain_trace_buf(int dev) {
   static long long* tr[64] = {nullptr};
-  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], 3 * 256 * sizeof(long long)) == hipSuccess, "lstm_chain: trace");
+  // [0, 768): per-workgroup start / end and stage-loop start; then the grads role's [8][256][3]
+  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], (3 * 256 + 8 * 256 * 3) * sizeof(long long)) == hipSuccess,
+                            "lstm_chain: trace");
   return tr[dev];
 }
 
@@ -932,9 +1076,150 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
 // (pooled if pool[0] > 0); per stage the forward's g / c, W, U, the argmax bytes of the pool
 // after the layer (empty if none) and pool size; x_width[s]: channels of the layer's input
 // layout. Returns [dz_0 .. dz_{n-1}, dx of the bottom layer].
+static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Tensor>& keep, const at::Tensor& dh,
+                                               at::TensorList g, at::TensorList c, at::TensorList W, at::TensorList U,
+                                               at::TensorList pidx, at::IntArrayRef pool, at::IntArrayRef x_width,
+                                               at::IntArrayRef T_in, int extra_blocks);
+
 std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, at::TensorList c, at::TensorList W,
                                        at::TensorList U, at::TensorList pidx, at::IntArrayRef pool,
                                        at::IntArrayRef x_width, at::IntArrayRef T_in) {
+  ChainBArgs A{};
+  std::vector<at::Tensor> keep;
+  auto res = chain_bwd_setup(A, keep, dh, g, c, W, U, pidx, pool, x_width, T_in, 0);
+  hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(A.ns * A.nt8), dim3(1024), 0, stream(), A);
+  GQ_LAUNCH_CHECK();
+  return res;
+}
+
+static int* chain_sync(int dev) {
+  static int* p[64] = {nullptr};
+  TORCH_CHECK(dev >= 0 && dev < 64, "lstm_chain: device index");
+  if (!p[dev]) {
+    hipStreamCaptureStatus cs;
+    TORCH_CHECK(hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
+                "lstm_chain: first use must not be inside a graph capture");
+    TORCH_CHECK(hipMalloc(&p[dev], 32 * sizeof(int)) == hipSuccess, "lstm_chain: sync counters");
+    TORCH_CHECK(hipMemset(p[dev], 0, 32 * sizeof(int)) == hipSuccess, "lstm_chain: sync init");
+  }
+  return p[dev];
+}
+
+int lstm_grads_col_blocks(int H);
+
+static bool chain_job_x_ok(const at::Tensor& x, int Dw) {
+  const int ldx = (int)x.stride(-2);
+  return ldx % 4 == 0 && ldx >= Dw && ldx <= 144 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+         (Dw + 1 + 15) / 16 <= 5 && x.stride(-1) == 1;
+}
+
+// one weight-gradient job of the chain backward: dz [>= T*Mp rows, 4H] (time-major), x [T, Mp, ldx]
+// (first Dw channels), h [T, Mp, H]; split count for G spare workgroups; ws: its split records
+static void chain_fill_job(ChainGJ& J, const float* dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
+                           at::Tensor& dW, at::Tensor& dU, at::Tensor& db, int G, int wait, int wait_n,
+                           std::vector<at::Tensor>& keep) {
+  const int Dw = (int)W.size(0), H = (int)W.size(1) / 4;
+  TORCH_CHECK(H == 16 || H == 32 || H == 64 || H == 128, "lstm_chain_bwd_grads: hidden size");
+  TORCH_CHECK(x.dim() == 3 && h.dim() == 3 && h.size(0) == x.size(0) && h.size(1) == x.size(1) && h.size(2) == H &&
+                  h.stride(2) == 1 && h.stride(1) == H && h.stride(0) == (long)H * h.size(1),
+              "lstm_chain_bwd_grads: x [T, Mp, C] / h [T, Mp, H]");
+  TORCH_CHECK(chain_job_x_ok(x, Dw) && x.stride(0) == x.stride(1) * x.size(1), "lstm_chain_bwd_grads: x layout");
+  TORCH_CHECK(dW.numel() == W.numel() && dU.numel() == (long)H * 4 * H && db.numel() == 4 * H,
+              "lstm_chain_bwd_grads: gradient buffers");
+  for (const at::Tensor* t : {&dW, &dU, &db}) check_f32_cuda(*t, "lstm_chain_bwd_grads gradient");
+  const int DT = (Dw + 1 + 15) / 16, HT = H / 16, ncb = lstm_grads_col_blocks(H);
+  const long rows = x.size(0) * x.size(1);
+  const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
+  const int splits = (int)std::max<long>(1, std::min<long>((ntiles + 1) / 2, std::max(1, G / ncb)));
+  const int RC = (DT + HT) * 1024 * ncb;
+  at::Tensor ws = at::empty({(long)splits * RC}, x.options());
+  keep.push_back(ws);
+  GradJob& gj = J.g;
+  gj.dz = dz;
+  gj.x = x.data_ptr<float>();
+  gj.h = h.data_ptr<float>();
+  gj.W = W.data_ptr<float>();
+  gj.ws = ws.data_ptr<float>();
+  gj.rows = rows;
+  gj.period = rows;                 // time-major [T, Mp]: h_{t-1} one Mp block back, none at t = 0
+  gj.hshift = x.size(1);
+  gj.ldx = (int)x.stride(1);
+  gj.x_elems = (long)(x.storage().nbytes() / sizeof(float)) - x.storage_offset();
+  gj.Din = Dw;
+  gj.xg = (int)((32L * gj.ldx / 4 + 255) / 256);
+  gj.ncb = ncb;
+  gj.splits = splits;
+  gj.nblocks = ncb * splits;
+  RedJob& r = J.r;
+  r.ws = gj.ws;
+  r.dW = dW.data_ptr<float>();
+  r.dU = dU.data_ptr<float>();
+  r.db = db.data_ptr<float>();
+  r.splits = splits;
+  r.RC = RC;
+  r.ncb = ncb;
+  r.DT = DT;
+  r.HT = HT;
+  r.Din = Dw;
+  r.H = H;
+  r.nblocks = gj.nblocks;
+  const int per = (RC + gj.nblocks - 1) / gj.nblocks;
+  int sl = 16;
+  while (sl < 256 && sl < per) sl *= 2;
+  r.kb = sl;
+  J.key = H * 8 + DT;
+  J.wait = wait;
+  J.wait_n = wait_n;
+}
+
+// lstm_chain_bwd with the weight-gradient passes of its stages (x_s, h_s, sinks dW_s / dU_s / db_s
+// per stage, top first like W) - and optionally of one more layer whose dz is already known
+// (edz, ex, eh, eW, edW, edU, edb: time4 of the CML stack) - run by the launch's spare workgroups,
+// reduced into the sinks inside the same launch. Returns what lstm_chain_bwd returns.
+std::vector<at::Tensor> lstm_chain_bwd_grads(const at::Tensor& dh, at::TensorList g, at::TensorList c,
+                                             at::TensorList W, at::TensorList U, at::TensorList pidx,
+                                             at::IntArrayRef pool, at::IntArrayRef x_width, at::IntArrayRef T_in,
+                                             at::TensorList gx, at::TensorList gh, at::TensorList gdW,
+                                             at::TensorList gdU, at::TensorList gdb, at::TensorList ext) {
+  const int ns = (int)W.size();
+  TORCH_CHECK((int)gx.size() == ns && (int)gh.size() == ns && (int)gdW.size() == ns && (int)gdU.size() == ns &&
+                  (int)gdb.size() == ns && (ext.size() == 0 || ext.size() == 7),
+              "lstm_chain_bwd_grads: job lists");
+  const int cap = chain_capacity(dh.get_device());
+  const int nt8 = (int)((dh.size(1) / 16 + 7) / 8 * 8);
+  const int G = std::min(cap - ns * nt8, 256);
+  TORCH_CHECK(G >= 8, "lstm_chain_bwd_grads: too few spare workgroups (", G, ")");
+  ChainBArgs A{};
+  std::vector<at::Tensor> keep;
+  auto res = chain_bwd_setup(A, keep, dh, g, c, W, U, pidx, pool, x_width, T_in, G);
+  c10::DeviceGuard guard(dh.device());
+  A.sync = chain_sync(dh.get_device());
+  A.gtrace = A.trace + 3 * 256;
+  int nj = 0;
+  if (ext.size() == 7) {
+    check_f32_cuda(ext[0], "edz");
+    TORCH_CHECK(ext[0].size(-1) == ext[3].size(1) && ext[0].numel() / ext[0].size(-1) >= ext[1].size(0) * ext[1].size(1),
+                "lstm_chain_bwd_grads: edz");
+    at::Tensor dWe = ext[4], dUe = ext[5], dbe = ext[6];
+    chain_fill_job(A.gj[nj++], ext[0].data_ptr<float>(), ext[1], ext[2], ext[3], dWe, dUe, dbe, G, -1, 0, keep);
+  }
+  for (int s = 0; s < ns; ++s) {
+    TORCH_CHECK(gx[s].size(0) == T_in[s] && gx[s].size(1) == dh.size(1), "lstm_chain_bwd_grads: stage x shape");
+    at::Tensor dWs = gdW[s], dUs = gdU[s], dbs = gdb[s];
+    chain_fill_job(A.gj[nj++], res[s].data_ptr<float>(), gx[s], gh[s], W[s], dWs, dUs, dbs, G, s, A.ntiles, keep);
+  }
+  A.njobs = nj;
+  int gmax = 0;
+  for (int k = 0; k < nj; ++k) gmax = std::max(gmax, A.gj[k].g.nblocks);
+  hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(A.ns * A.nt8 + gmax), dim3(1024), 0, stream(), A);
+  GQ_LAUNCH_CHECK();
+  return res;
+}
+
+static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Tensor>& keep, const at::Tensor& dh,
+                                               at::TensorList g, at::TensorList c, at::TensorList W, at::TensorList U,
+                                               at::TensorList pidx, at::IntArrayRef pool, at::IntArrayRef x_width,
+                                               at::IntArrayRef T_in, int extra_blocks) {
   check_f32_cuda(dh, "dh");
   const int ns = (int)W.size();
   TORCH_CHECK(ns >= 1 && ns <= CHAIN_MAX && (int)U.size() == ns && (int)g.size() == ns && (int)c.size() == ns &&
@@ -944,18 +1229,17 @@ std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, a
   const int Mp = (int)dh.size(1);
   TORCH_CHECK(Mp % 16 == 0, "lstm_chain_bwd: Mp");
   const int ntiles = Mp / 16, nt8 = (ntiles + 7) / 8 * 8;
-  TORCH_CHECK(ns * nt8 <= chain_capacity(dh.get_device()), "lstm_chain_bwd: ", ns * nt8,
+  TORCH_CHECK(ns * nt8 + extra_blocks <= chain_capacity(dh.get_device()), "lstm_chain_bwd: ", ns * nt8 + extra_blocks,
               " workgroups cannot all be resident on this device");
   c10::DeviceGuard guard(dh.device());
   auto opt = dh.options();
-  ChainBArgs A{};
   A.ns = ns;
   A.ntiles = ntiles;
   A.nt8 = nt8;
   A.Mp = Mp;
   A.ctl = chain_ctl(dh.get_device());
   A.trace = chain_trace_buf(dh.get_device());
-  std::vector<at::Tensor> dzs, keep;
+  std::vector<at::Tensor> dzs;
   at::Tensor dx, prev;
   for (int s = 0; s < ns; ++s) {
     const int H = (int)U[s].size(0), Dw = (int)W[s].size(0), T = (int)T_in[s], Din = (int)x_width[s];
@@ -1008,10 +1292,15 @@ std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, a
     S.Ts = Ts;
     S.trace_mid = A.trace + 512;
   }
-  hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(ns * nt8), dim3(1024), 0, stream(), A);
-  GQ_LAUNCH_CHECK();
   dzs.push_back(dx.defined() ? dx.narrow(0, 0, (int)T_in[ns - 1]) : at::empty({0}, opt));
   return dzs;
+}
+
+// the backward chain's grads-role counters as an int32[32] view ([16]: profiling knobs)
+at::Tensor lstm_chain_sync(const at::Tensor& like) {
+  TORCH_CHECK(like.is_cuda(), "lstm_chain_sync: a GPU tensor names the device");
+  c10::DeviceGuard guard(like.device());
+  return at::from_blob(chain_sync(like.get_device()), {32}, like.options().dtype(at::kInt));
 }
 
 // [epoch, finished, timeout flag, 0] of this device's chain control words (tests)
@@ -1028,9 +1317,9 @@ at::Tensor lstm_chain_status(const at::Tensor& like) {
 at::Tensor lstm_chain_trace(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
   long long* p = chain_trace_buf(like.get_device());
-  at::Tensor o = at::empty({3 * 256}, like.options().dtype(at::kLong));
-  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, 768 * sizeof(long long), hipMemcpyDeviceToDevice, stream()) ==
-                  hipSuccess, "lstm_chain_trace");
+  at::Tensor o = at::empty({3 * 256 + 8 * 256 * 3}, like.options().dtype(at::kLong));
+  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, o.numel() * sizeof(long long), hipMemcpyDeviceToDevice,
+                             stream()) == hipSuccess, "lstm_chain_trace");
   return o;
 }
 
@@ -1044,4 +1333,6 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_ctl", &gq::lstm_chain_ctl);
   m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
   m.impl("lstm_chain_bwd", &gq::lstm_chain_bwd);
+  m.impl("lstm_chain_bwd_grads", &gq::lstm_chain_bwd_grads);
+  m.impl("lstm_chain_sync", &gq::lstm_chain_sync);
 }

@@ -9,6 +9,25 @@ constexpr int GR_ROWS = 32;         // rows (sequence, step) per tile = MFMA K
 constexpr int GR_CB = 64;           // gate-units per column block (4 waves x 16)
 constexpr int GR_LDR = GR_ROWS + 8; // padded LDS row length (bf16) of transposed images
 
+// a weight-gradient pass (lstm_grads_body) and its split reduction as kernel-argument records
+struct GradJob {
+  const float* dz;
+  const float* x;
+  const float* h;
+  const float* W;
+  float* ws;
+  long rows, period, hshift, x_elems;
+  int Din, ldx, xg, ncb, splits, nblocks;
+};
+
+struct RedJob {
+  const float* ws;
+  float* dW;
+  float* db;
+  float* dU;
+  int splits, RC, ncb, DT, HT, Din, H, nblocks, kb;
+};
+
 // One workgroup = (column block cb of 64 gate-units, row split s); it walks the row tiles
 // s, s + splits, ... with a one-tile register prefetch: tile i+1's dz / x / h_{t-1} loads are
 // issued before tile i's MFMAs and only waited for when tile i+1 is staged (LDS-only
@@ -30,7 +49,23 @@ struct GradsLds {
   static constexpr int BYTES = DZT + DZR + XT + HT;
 };
 
-template <int H, int DT, int GRX>
+// agent-scope (sc1, write-through) store of 16 bytes as two untorn 8-byte halves
+__device__ __forceinline__ void st4_sc1(float* p, f32x4_t v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v[1]) << 32) | __float_as_uint(v[0]), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v[3]) << 32) | __float_as_uint(v[2]), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// CH (chained: extra workgroups of the backward chain kernel): no dx, and the split record is
+// stored write-through (sc1) for a reduction inside the same launch that reads it with sc1 loads
+template <int H, int DT, int GRX, bool CH = false>
 __device__ __forceinline__ void lstm_grads_body(
     const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
@@ -67,9 +102,9 @@ __device__ __forceinline__ void lstm_grads_body(
 
   // dx work items of this wave: (din tile, row tile) pairs, 2 row tiles per 32 rows
   constexpr int DXT = (DP + 15) / 16 * 2;
-  bf16x8_t wa[(DXT + 3) / 4][2];
+  bf16x8_t wa[CH ? 1 : (DXT + 3) / 4][2];
 #pragma unroll
-  for (int i = 0; i < (DXT + 3) / 4; ++i) {
+  for (int i = 0; i < (CH ? 0 : (DXT + 3) / 4); ++i) {
     const int item = w + 4 * i;
     const int dtile = item >> 1;
 #pragma unroll
@@ -131,7 +166,7 @@ __device__ __forceinline__ void lstm_grads_body(
       const __bf16 b0 = (__bf16)(rz[q].x * m), b1 = (__bf16)(rz[q].y * m), b2 = (__bf16)(rz[q].z * m),
                    b3 = (__bf16)(rz[q].w * m);
       typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = bf16x4_t{b0, b1, b2, b3};
+      if constexpr (!CH) *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = bf16x4_t{b0, b1, b2, b3};
       dzT[zc + 0][rr] = b0;
       dzT[zc + 1][rr] = b1;
       dzT[zc + 2][rr] = b2;
@@ -184,7 +219,7 @@ __device__ __forceinline__ void lstm_grads_body(
       accU[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az, bh, accU[k], 0, 0, 0);
     }
     // ---- dx^T tiles: item = (din tile, row tile)
-    if (dx != nullptr) {
+    if constexpr (!CH) if (dx != nullptr) {
       const long r0 = tile * GR_ROWS;
 #pragma unroll
       for (int ii = 0; ii < (DXT + 3) / 4; ++ii) {
@@ -213,11 +248,17 @@ __device__ __forceinline__ void lstm_grads_body(
   // ---- partial tiles -> workspace record of this workgroup, fragment order (float4 per lane)
   float* rec = ws + ((size_t)split * ncbv + cb) * (size_t)(DT + HT) * 1024;
 #pragma unroll
-  for (int d = 0; d < DT; ++d)
-    *reinterpret_cast<f32x4_t*>(rec + ((size_t)(d * 4 + w) * 64 + lane) * 4) = accW[d];
+  for (int d = 0; d < DT; ++d) {
+    float* o = rec + ((size_t)(d * 4 + w) * 64 + lane) * 4;
+    if constexpr (CH) st4_sc1(o, accW[d]);
+    else *reinterpret_cast<f32x4_t*>(o) = accW[d];
+  }
 #pragma unroll
-  for (int k = 0; k < HT; ++k)
-    *reinterpret_cast<f32x4_t*>(rec + ((size_t)((DT + k) * 4 + w) * 64 + lane) * 4) = accU[k];
+  for (int k = 0; k < HT; ++k) {
+    float* o = rec + ((size_t)((DT + k) * 4 + w) * 64 + lane) * 4;
+    if constexpr (CH) st4_sc1(o, accU[k]);
+    else *reinterpret_cast<f32x4_t*>(o) = accU[k];
+  }
 }
 
 // Reduction of the per-split records in a fixed order (deterministic):

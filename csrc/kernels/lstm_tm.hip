@@ -751,23 +751,6 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
 // exit at once (s_barrier only counts live waves).
 static constexpr int PIPE_RED_KB = 8;     // slot blocks per reduce workgroup (lstm_grads_reduce_multi)
 
-struct GradJob {
-  const float* dz;
-  const float* x;
-  const float* h;
-  const float* W;
-  float* ws;
-  long rows, period, hshift, x_elems;
-  int Din, ldx, xg, ncb, splits, nblocks;
-};
-
-struct RedJob {
-  const float* ws;
-  float* dW;
-  float* db;
-  float* dU;
-  int splits, RC, ncb, DT, HT, Din, H, nblocks, kb;
-};
 
 template <int HR, int HG, int DT>
 __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(

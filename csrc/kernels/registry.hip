@@ -40,11 +40,15 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_chain_status(Tensor like) -> Tensor");
   m.def("lstm_chain_capacity(Tensor like) -> int");
   m.def("lstm_chain_ctl(Tensor like) -> Tensor");
+  m.def("lstm_chain_sync(Tensor like) -> Tensor");
   m.def("lstm_grads_multi(Tensor[] gz, Tensor[] gx, Tensor[] gh, Tensor[] gW, int[] period, int[] hshift, "
         "Tensor[] gws, Tensor[] rws, Tensor[] rW, Tensor(a!)[] rdW, Tensor(b!)[] rdU, Tensor(c!)[] rdb) -> ()");
   m.def("lstm_chain_trace(Tensor like) -> Tensor");
   m.def("lstm_chain_bwd(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");
+  m.def("lstm_chain_bwd_grads(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
+        "int[] x_width, int[] T_in, Tensor[] gx, Tensor[] gh, Tensor(a!)[] gdW, Tensor(b!)[] gdU, Tensor(c!)[] gdb, "
+        "Tensor(d!)[] ext) -> Tensor[]");
   m.def("time4_head_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor pk, bool train, Tensor[] head, Tensor y, Tensor mask, "
         "int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");
   m.def("time4_head_bwd(Tensor dloss, Tensor x, Tensor h, Tensor g, Tensor c, Tensor W, Tensor U, Tensor[] head, "
@@ -76,6 +80,8 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("gcn_pool_weights(Tensor adj, Tensor mask, Tensor anom_pos, bool agg_mean, int pool) -> Tensor");
   m.def("gcn_bn_prep(Tensor S, Tensor W, Tensor b, Tensor gamma, Tensor beta, Tensor(a!) rmean, Tensor(b!) rvar, "
         "bool training, float momentum, float eps) -> Tensor");
+  m.def("gcn_prep(Tensor x, Tensor adj, Tensor mask, Tensor anom_pos, bool agg_mean, int pool, Tensor W, Tensor b, "
+        "Tensor gamma, Tensor beta, Tensor(a!) rmean, Tensor(b!) rvar, bool training, float momentum, float eps) -> Tensor[]");
   m.def("gcn_bwd_finalize(Tensor acc, Tensor S, Tensor W, Tensor b, Tensor st, bool training, Tensor(a!) dW, "
         "Tensor(b!) db, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) dalpha) -> Tensor");
   // Conv1D + LeakyReLU (+ GAP) implicit GEMM (conv1d.hip)
@@ -83,8 +89,8 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("conv1d_bwd(Tensor dy, Tensor y, Tensor x, Tensor W, float alpha, bool gap, Tensor(a!) dW, "
         "Tensor(b!) db, bool need_dx) -> Tensor");
   // flat-buffer optimiser (adam.hip)
-  m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
-        "float beta2, float eps, float grad_scale, float weight_decay, Tensor? guard=None) -> ()");
+  m.def("adam_step(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
+        "float beta2, float eps, float grad_scale, float weight_decay, Tensor? guard=None, bool zero_grad=False) -> ()");
   m.def("nonfinite_count(Tensor x) -> Tensor");
   m.def("grad_guard(Tensor g, Tensor(a!) state, Tensor(b!) step, Tensor(c!)? ext=None) -> ()");
   // metrics (metrics.hip)

@@ -97,19 +97,19 @@ def general_conv_eager(x, adj, mask, W, b, gamma, beta, running_mean, running_va
 class _HipGCNPool(torch.autograd.Function):
     """Fused stats -> affine/BN/PReLU -> weighted node sum -> concat (HIP).
 
-    Launches per training step: gcn_stats, gcn_bn_prep, gcn_pool_fwd forward;
-    gcn_pool_bwd, gcn_bwd_finalize (+ gcn_pool_bwd_input when dx is needed)
-    backward. Weight gradients go straight into the optimiser's flat buffer when
+    Launches per training step: gcn_prep (pool weights + batch moments + BN prep) and
+    gcn_pool_fwd forward; gcn_pool_bwd and gcn_bwd_finalize (+ gcn_pool_bwd_input when dx is
+    needed) backward. Weight gradients go straight into the optimiser's flat buffer when
     direct accumulation is on (see ``gnnqc.ops.lstm.direct_grad_accumulation``)."""
 
     @staticmethod
-    def forward(ctx, x, w, mask, anom, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
-                momentum: float, eps: float, Mp: int = 0, Cp: int = 0):
+    def forward(ctx, x, adj, mask, anom, anom_pos, agg_mean: bool, pool: int, W, b, gamma, beta, alpha,
+                running_mean, running_var, training: bool, momentum: float, eps: float, Mp: int = 0, Cp: int = 0):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        S = ops.gcn_stats(x, mask) if training else x.new_zeros(0, dtype=torch.float64)
-        st = ops.gcn_bn_prep(S, W.contiguous(), b.contiguous(), gamma.contiguous(), beta.contiguous(),
-                             running_mean, running_var, bool(training), float(momentum), float(eps))
+        w, S, st = ops.gcn_prep(x, adj, mask, anom_pos, bool(agg_mean), int(pool), W.contiguous(), b.contiguous(),
+                                gamma.contiguous(), beta.contiguous(), running_mean, running_var, bool(training),
+                                float(momentum), float(eps))
         anom_t = anom.contiguous() if anom is not None else x.new_zeros(0)
         out = ops.gcn_pool_fwd(x, w, anom_t, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous(),
                                int(Mp), int(Cp))
@@ -129,13 +129,13 @@ class _HipGCNPool(torch.autograd.Function):
         x, w, mask, W, b, alpha, st, S = ctx.saved_tensors
         dout = dout.contiguous()
         need = ctx.needs_input_grad
-        need_w = any(need[4:9])
+        need_w = any(need[7:12])
         empty = x.new_zeros(0)
         acc = empty
         if ctx.training or need_w:
             acc = ops.gcn_pool_bwd(x, w, dout, W.contiguous(), b.contiguous(), st[2], st[3], alpha.contiguous(),
                                    ctx.ca, ctx.tm)
-        sinks = [(_grad_sink(p) if n else (empty, True)) for p, n in zip(ctx.params, need[4:9])]
+        sinks = [(_grad_sink(p) if n else (empty, True)) for p, n in zip(ctx.params, need[7:12])]
         coef = ops.gcn_bwd_finalize(acc, S, W.contiguous(), b.contiguous(), st, bool(ctx.training),
                                     *[s[0] for s in sinks])
         dx = None
@@ -145,8 +145,8 @@ class _HipGCNPool(torch.autograd.Function):
         danom = None
         if ctx.has_anom and need[3]:
             danom = dout[:, : x.shape[0], : ctx.ca].transpose(0, 1) if ctx.tm else dout[..., : ctx.ca]
-        grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need[4:9])]
-        return (dx, None, None, danom, *grads, None, None, None, None, None, None, None)
+        grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need[7:12])]
+        return (dx, None, None, danom, None, None, None, *grads, None, None, None, None, None, None, None)
 
 
 def gcn_pool_hip_ok(x, W, aggregate: str, pooling: str, dropout: float, training: bool) -> bool:
@@ -167,18 +167,17 @@ def gcn_pool(x, adj, mask, anom, anom_pos, W, b, gamma, beta, alpha, running_mea
     :meth:`gnnqc.models.timelayer.TimeLayer.forward_time_major`, written by the kernel itself.
     """
     if gcn_pool_hip_ok(x, W, aggregate, pooling, dropout, training):
-        from ..utils.native import hip_ops
         ap = anom_pos.long().contiguous() if (pooling == "selection" and anom_pos is not None) else x.new_zeros(0)
-        w = hip_ops().gcn_pool_weights(adj.float().contiguous(), mask.float().contiguous(), ap,
-                                       aggregate == "mean", {"mean": 0, "sum": 1, "selection": 2}[pooling])
         Mp = Cp = 0
         if time_major:
             B = x.shape[0]
             Mp = (B + 15) // 16 * 16
             Cp = W.shape[1] + (anom.shape[-1] if anom is not None else 0)
             Cp += (-Cp) % 4
-        out = _HipGCNPool.apply(x.contiguous(), w, mask.contiguous().float(), anom, W, b, gamma, beta, alpha,
-                                running_mean, running_var, bool(training), float(momentum), float(eps), Mp, Cp)
+        out = _HipGCNPool.apply(x.contiguous(), adj.float().contiguous(), mask.contiguous().float(), anom, ap,
+                                aggregate == "mean", {"mean": 0, "sum": 1, "selection": 2}[pooling], W, b, gamma,
+                                beta, alpha, running_mean, running_var, bool(training), float(momentum), float(eps),
+                                Mp, Cp)
         return (out, x.shape[0]) if time_major else out
     if time_major:
         raise ValueError("gcn_pool(time_major=True) needs the HIP path")

@@ -466,6 +466,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
                                                       hist if hist is not None else e)
         ctx.pools, ctx.consts, ctx.M = tuple(int(p) for p in pools), tuple(float(c) for c in consts), int(M)
         ctx.params = params
+        ctx.set_materialize_grads(False)     # (no zeros tensor for the non-differentiable logits)
         if need:
             ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs, h4, g4, c4)
         ctx.mark_non_differentiable(logits)
@@ -500,30 +501,45 @@ class _HipLSTMChainHead(torch.autograd.Function):
                                       [s for s, _ in hsinks])
         order = list(reversed(range(ns)))
         e8 = x.new_zeros(0, dtype=torch.uint8)
-        res = ops.lstm_chain_bwd(dxt, [outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
-                                 [Ws[i] for i in order], [Us[i] for i in order],
-                                 [outs[5 * i + 4] if pools[i] else e8 for i in order],
-                                 [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
-                                 [outs[5 * i].shape[0] for i in order])
+        chain_args = ([outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
+                      [Ws[i] for i in order], [Us[i] for i in order],
+                      [outs[5 * i + 4] if pools[i] else e8 for i in order],
+                      [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
+                      [outs[5 * i].shape[0] for i in order])
+        grads = [None] * npar
+        sinks = {i: [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]] for i in range(ns + 1)}
+        if (_chain_grads_on() and all(all(need[8 + 3 * i:11 + 3 * i]) for i in range(ns + 1))
+                and all(d for i in range(ns + 1) for _, d in sinks[i])
+                and all(_pipe_x_ok(layer_x(i), Ws[i].shape[0]) for i in range(ns + 1))
+                and chain_fits(x.shape[1], ns, x.device, spare=8)):
+            # the seven weight-gradient passes and their reductions inside the chain backward
+            # launch (its spare workgroups start each pass as soon as its layer's dz is final)
+            res = ops.lstm_chain_bwd_grads(
+                dxt, *chain_args, [layer_x(i) for i in order], [outs[5 * i] for i in order],
+                [sinks[i][0][0] for i in order], [sinks[i][1][0] for i in order], [sinks[i][2][0] for i in order],
+                [dz4, xt, h4, Ws[ns], sinks[ns][0][0], sinks[ns][1][0], sinks[ns][2][0]])
+            hgrads = [None if (direct or not n) else buf for (buf, direct), n in zip(hsinks, need[8 + npar:])]
+            dx = res[ns]
+            return (dx if need[0] else None, None, None, None, None, None, None, None, *grads, *hgrads)
+        res = ops.lstm_chain_bwd(dxt, *chain_args)
         dzs = {ns: dz4}
         hs = {ns: h4}
         for k, i in enumerate(order):
             dzs[i] = res[k]
             hs[i] = outs[5 * i]
-        grads = [None] * npar
         for i in [ns] + order:
             nw = need[8 + 3 * i:11 + 3 * i]
             if not any(nw):
                 continue
             h = hs[i]
             xi = layer_x(i)
-            sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
-            if (_pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
+            sk = sinks[i]
+            if (_pipe_on(sk, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
                     and len(_Pipe.batch) < _MULTI_MAX - 2):
-                _Pipe.batch.append(_pipe_job(dzs[i], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
+                _Pipe.batch.append(_pipe_job(dzs[i], xi, h, Ws[i], sk, h.shape[0] * h.shape[1], h.shape[1]))
             else:
-                ops.lstm_tm_grads(dzs[i], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
-            grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]
+                ops.lstm_tm_grads(dzs[i], xi, h, Ws[i], sk[0][0], sk[1][0], sk[2][0], False)
+            grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sk, nw)]
         hgrads = [None if (direct or not n) else buf for (buf, direct), n in zip(hsinks, need[8 + npar:])]
         dx = res[ns]
         return (dx if need[0] else None, None, None, None, None, None, None, None, *grads, *hgrads)
@@ -582,11 +598,19 @@ def chain_capacity(device) -> int:
     return cap
 
 
-def chain_fits(Mp: int, n_stages: int, device=None) -> bool:
-    """All workgroups of a chain launch must be co-resident (one 1024-thread workgroup per CU)."""
+def chain_fits(Mp: int, n_stages: int, device=None, spare: int = 0) -> bool:
+    """All workgroups of a chain launch must be co-resident (one 1024-thread workgroup per CU);
+    ``spare``: workgroups needed besides the stages' (the weight-gradient role of the backward)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
-    return (2 <= n_stages <= 8 and n_stages * ((Mp // 16 + 7) // 8 * 8) <= chain_capacity(device))
+    return (2 <= n_stages <= 8 and n_stages * ((Mp // 16 + 7) // 8 * 8) + spare <= chain_capacity(device))
+
+
+def _chain_grads_on() -> bool:
+    """Weight-gradient passes inside the chain backward launch (``GNNQC_CHAIN_GRADS``, default off:
+    measured slower - the waiting workgroups slowed the chain itself by ~25%, profiles/r2_chain_grads_trace.jsonl)."""
+    import os
+    return os.environ.get("GNNQC_CHAIN_GRADS", "0") == "1"
 
 
 _CHAIN_CTL = {}

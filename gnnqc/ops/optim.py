@@ -51,6 +51,8 @@ def flatten_parameters(params: Iterable[torch.nn.Parameter], align: int = 4):
 class FlatOptimizer:
     """Base: owns the flat buffers of a module's trainables."""
 
+    grad_zeroed_by_step = False        # subclasses whose update clears flat_g override this
+
     def __init__(self, params, lr: float, guard: bool = True):
         self.flat_p, self.flat_g, self.params = flatten_parameters(params)
         dev = self.flat_p.device
@@ -66,9 +68,9 @@ class FlatOptimizer:
     def skipped_steps(self) -> int:
         return int(self.guard_state[3].item())
 
-    def _begin_step(self):
+    def _begin_step(self, need_flag: bool = True):
         """Advance the step counter; with the guard, only if the gradients are finite.
-        Returns the device ok flag (bool tensor) for eager updates, or None."""
+        Returns the device ok flag (bool tensor) for eager updates (``need_flag``), or None."""
         self.iterations += 1
         if not self.guard:
             self.step_t.add_(1.0)
@@ -79,7 +81,8 @@ class FlatOptimizer:
             from .lstm import chain_ctl
             # a step whose LSTM chain kernel timed out (stale hand-off data) is rejected too
             hip_ops().grad_guard(self.flat_g, self.guard_state, self.step_t, chain_ctl(self.flat_g.device))
-            return self.guard_state[2:3].bool()
+            # (a HIP update kernel reads the guard state itself: no bool conversion launch)
+            return self.guard_state[2:3].bool() if need_flag else None
         ok = torch.isfinite(self.flat_g).all().reshape(1)
         self.step_t.add_(ok.float())
         self.guard_state[2:3].copy_(ok.int())
@@ -137,15 +140,24 @@ class FlatAdam(FlatOptimizer):
         self.beta1, self.beta2, self.eps, self.wd = beta1, beta2, eps, weight_decay
         self.m = torch.zeros_like(self.flat_p)
         self.v = torch.zeros_like(self.flat_p)
+        # the HIP update clears the gradient buffer once it has read it (no separate zero-fill
+        # launch per training step); the trainer then skips zero_grad (grad_zeroed_by_step)
+        self.zero_grad_in_step = self.flat_p.is_cuda
+
+    @property
+    def grad_zeroed_by_step(self) -> bool:
+        from . import use_hip
+        return self.zero_grad_in_step and use_hip(self.flat_p)
 
     def step(self, grad_scale: float = 1.0):
         from . import use_hip
-        ok = self._begin_step()
-        if use_hip(self.flat_p):
+        hip = use_hip(self.flat_p)
+        ok = self._begin_step(need_flag=not hip)
+        if hip:
             from ..utils.native import hip_ops
             hip_ops().adam_step(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
                                 self.beta2, self.eps, float(grad_scale), self.wd,
-                                self.guard_state if self.guard else None)
+                                self.guard_state if self.guard else None, self.zero_grad_in_step)
             return
         with torch.no_grad():
             g = self.flat_g * grad_scale

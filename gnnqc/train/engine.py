@@ -132,14 +132,18 @@ class Trainer:
         return total, loss, z, b
 
     def _body(self, wids, with_opt: bool):
-        self.opt.zero_grad()
+        # every training step ends with the optimizer update (here, or after the DP all-reduce);
+        # a HIP Adam clears the gradient buffer as it reads it, so no zero-fill launch here
+        # (the graph-capture warm-up, which runs no update, zeroes explicitly afterwards)
+        if not self.opt.grad_zeroed_by_step:
+            self.opt.zero_grad()
         with _rf("gnnqc.forward"):
             total, loss, z, b = self._loss(wids, self.train_metrics)
         with _rf("gnnqc.backward"), direct_grad_accumulation(True):
             total.backward(self._one)          # (a kept seed: no ones_like fill launch per step)
         if self.poison is not None:
             self.opt.flat_g[:1].add_(self.poison)
-        self.last_loss.copy_(loss.detach())
+        self.last_loss = loss.detach()       # (a reference, not a copy launch: graph replays refresh it)
         if with_opt:
             with _rf("gnnqc.optimizer"):
                 self.opt.step(grad_scale=1.0)

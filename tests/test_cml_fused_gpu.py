@@ -146,3 +146,24 @@ def test_headed_chain_eval_metrics_match(cuda_device, cml_windows, monkeypatch):
     r = tr.evaluate(loader)
     for k in r:
         assert abs(a[k] - r[k]) <= 2e-3 * abs(r[k]) + 2e-3, (k, a[k], r[k])
+
+
+def test_chain_grads_role_matches_separate_passes(cuda_device, cml_windows, monkeypatch):
+    """Weight gradients computed by the chain backward's spare workgroups (in-launch passes and
+    reductions, GNNQC_CHAIN_GRADS=1) == the separate lstm_grads_multi launches; and run-to-run
+    bitwise identical (fixed-order reductions)."""
+    _, _, _, model, b = _setup(cuda_device, cml_windows)
+    inputs = b.model_inputs("cml")
+
+    def run(flag):
+        monkeypatch.setenv("GNNQC_CHAIN_GRADS", flag)
+        return _grads(model, lambda: model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0))
+
+    l1, _, g1 = run("1")
+    _, _, g1b = run("1")
+    l0, _, g0 = run("0")
+    torch.testing.assert_close(l1, l0)
+    for n in g0:
+        assert torch.equal(g1[n], g1b[n]), n
+        err = (g1[n] - g0[n]).norm().item()
+        assert err <= 1e-4 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())

@@ -93,3 +93,89 @@ def test_bench_runs_with_two_gloo_ranks():
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 256 and out["value"] > 0
+
+
+def _gcn_setup():
+    from gnnqc import config as C
+    from gnnqc.data.preprocessing import create_windows_dataset
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.data.synthetic import make_cml_raw
+    pc = C.normalize_preproc(C.default("preprocessing_cml"))
+    pc.timestep_before, pc.timestep_after = 30, 15
+    ws = create_windows_dataset(pc, raw=make_cml_raw(n_sensors=8, n_minutes=4 * 1440, seed=5))
+    st = DeviceStore(ws, "rolling_median", pc.graph)
+    mc = C.default("model_cml")
+    mc.sequence_layer.filter_1_size = 4          # small TimeLayer: fast on CPU, same structure
+    mc.dense.units = 64
+    return pc, mc, st
+
+
+def _gcn_worker(rank, world, port, out_dir, ids, n_epoch_batches):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from gnnqc.data.store import DeviceLoader
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.parallel import dist as D
+    from gnnqc.train.engine import Trainer
+    D.init_distributed(device="cpu")
+    pc, mc, st = _gcn_setup()
+    torch.manual_seed(rank + 200)             # different init per rank: broadcast must fix it
+    m = GCNClassifier(mc, pc)
+    opt = make_optimizer("adam", m.parameters(), 1e-3)
+    D.broadcast_module(m)
+    np.save(os.path.join(out_dir, f"p0_{rank}.npy"), opt.flat_p.detach().numpy().copy())
+    t = Trainer(m, st, opt, {0: 1.0, 1: 5.0}, baseline=False, use_graph=False, batch_size=len(ids[rank]))
+    # one gradient: this rank's shard, all-reduced mean
+    t._body(torch.tensor(ids[rank]), with_opt=False)
+    D.all_reduce_(opt.flat_g)
+    np.save(os.path.join(out_dir, f"g{rank}.npy"), (opt.flat_g / world).numpy())
+    opt.zero_grad()
+    # an epoch of DP training: parameters and BN statistics must agree on every rank
+    loader = DeviceLoader(st, list(range(n_epoch_batches * 8 * world)), 8, shuffle=True, seed=3, rank=rank,
+                          world_size=world, drop_last=True)
+    t.batch_size = 8
+    t.train_epoch(loader, 0)
+    np.save(os.path.join(out_dir, f"p{rank}.npy"), opt.flat_p.detach().numpy())
+    bufs = torch.cat([b.reshape(-1).double() for b in m.buffers() if b.is_floating_point()])
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), bufs.numpy())
+    D.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world):
+    """GCNClassifier under data parallelism (gloo, the RCCL path by construction): the all-reduced
+    gradient equals the mean of single-process per-shard gradients (BatchNorm batch statistics are
+    per replica, as in Keras MirroredStrategy), and after an epoch parameters and BN moving
+    statistics are identical on every rank (the epoch-end BN average, gnnqc.parallel.dist)."""
+    per = 6
+    ids = [list(range(r * per, (r + 1) * per)) for r in range(world)]
+    port = _free_port()
+    mp.spawn(_gcn_worker, args=(world, port, str(tmp_path), ids, 2), nprocs=world, join=True)
+    p0 = [np.load(tmp_path / f"p0_{r}.npy") for r in range(world)]
+    for r in range(1, world):
+        assert np.array_equal(p0[r], p0[0])
+    gs = [np.load(tmp_path / f"g{r}.npy") for r in range(world)]
+    for r in range(1, world):
+        assert np.allclose(gs[r], gs[0])
+    # reference: one process, the same weights, each shard's gradient, averaged
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops.optim import make_optimizer
+    from gnnqc.train.engine import Trainer
+    pc, mc, st = _gcn_setup()
+    m = GCNClassifier(mc, pc)
+    opt = make_optimizer("adam", m.parameters(), 1e-3)
+    opt.flat_p.copy_(torch.from_numpy(p0[0]))
+    t = Trainer(m, st, opt, {0: 1.0, 1: 5.0}, baseline=False, use_graph=False, batch_size=per)
+    ref = np.zeros_like(gs[0])
+    for r in range(world):
+        t._body(torch.tensor(ids[r]), with_opt=False)
+        ref += opt.flat_g.numpy() / world
+    assert np.allclose(gs[0], ref, rtol=1e-4, atol=1e-6), np.abs(gs[0] - ref).max()
+    ps = [np.load(tmp_path / f"p{r}.npy") for r in range(world)]
+    bs = [np.load(tmp_path / f"b{r}.npy") for r in range(world)]
+    for r in range(1, world):
+        assert np.array_equal(ps[r], ps[0])
+        assert np.allclose(bs[r], bs[0], rtol=0, atol=1e-12)
+    assert not np.array_equal(ps[0], p0[0])

@@ -126,9 +126,9 @@ def test_gcn_pool_matches_eager(cuda_device, training, pooling):
         rm_e.copy_(rm_h); rv_e.copy_(rv_h)
     hp = [t.clone().requires_grad_(True) for t in (x, anom, W, bb, gamma, beta, alpha)]
     ep = [t.clone().double().requires_grad_(True) for t in (x, anom, W, bb, gamma, beta, alpha)]
-    w = G.node_pool_weights(adj, mask, ap, "mean", pooling)
-    out = G._HipGCNPool.apply(hp[0], w, mask, hp[1], hp[2], hp[3], hp[4], hp[5], hp[6], rm_h, rv_h, training,
-                              0.99, 1e-3)
+    out = G._HipGCNPool.apply(hp[0], adj, mask, hp[1], ap.long().contiguous(), True,
+                              {"mean": 0, "sum": 1, "selection": 2}[pooling], hp[2], hp[3], hp[4], hp[5], hp[6],
+                              rm_h, rv_h, training, 0.99, 1e-3)
     h = G.general_conv_eager(ep[0], adj.double(), mask.double(), ep[2], ep[3], ep[4], ep[5], rm_e.double(),
                              rv_e.double(), ep[6], training, "mean")
     ref = torch.cat([ep[1], G.pool_nodes(h, mask.double(), ap, pooling)], -1)
@@ -139,6 +139,36 @@ def test_gcn_pool_matches_eager(cuda_device, training, pooling):
     for p, r, name in zip(hp, ep, ["x", "anom", "W", "b", "gamma", "beta", "alpha"]):
         err = (p.grad.double() - r.grad).abs().max().item()
         assert err < 2e-3 * (1 + r.grad.abs().max().item()), f"{name}: {err}"
+    if training:     # the fused prep's running-statistics update == the eager BatchNorm's
+        z = torch.matmul(x.double(), W.double()) + bb.double()
+        mm = mask.double()[:, None, :, None]
+        n = mm.sum() * x.shape[1]
+        mu = (z * mm).sum((0, 1, 2)) / n
+        var = (((z - mu) ** 2) * mm).sum((0, 1, 2)) / n
+        torch.testing.assert_close(rm_h.double(), 0.01 * mu, atol=1e-5, rtol=1e-4)
+        torch.testing.assert_close(rv_h.double(), 0.99 + 0.01 * var, atol=1e-5, rtol=1e-4)
+
+
+def test_gcn_prep_deterministic_and_eval_mode(cuda_device):
+    """gcn_prep: bitwise-identical batch statistics on repeated launches (fixed-order record
+    sums, no float atomics); eval mode preps BN from the running statistics untouched."""
+    from gnnqc.utils.native import hip_ops
+    gen = torch.Generator().manual_seed(9)
+    x, adj, mask, anom, ap, W, bb, gamma, beta, alpha = _gcn_inputs(gen, cuda_device, B=40, T=30, N=11)
+    F = W.shape[1]
+    outs = []
+    for _ in range(3):
+        rm, rv = torch.zeros(F, device=x.device), torch.ones(F, device=x.device)
+        w, S, st = hip_ops().gcn_prep(x, adj, mask, ap.long(), True, 0, W, bb, gamma, beta, rm, rv, True, 0.99, 1e-3)
+        outs.append((w.clone(), S.clone(), st.clone(), rm.clone()))
+    for o in outs[1:]:
+        for a, b_ in zip(o, outs[0]):
+            assert torch.equal(a, b_)
+    rm, rv = torch.full((F,), 0.3, device=x.device), torch.full((F,), 2.0, device=x.device)
+    w, S, st = hip_ops().gcn_prep(x, adj, mask, ap.long(), True, 0, W, bb, gamma, beta, rm, rv, False, 0.99, 1e-3)
+    assert S.numel() == 0 and torch.all(rm == 0.3) and torch.all(rv == 2.0)
+    torch.testing.assert_close(st[0], rm)
+    torch.testing.assert_close(st[1], torch.rsqrt(rv + 1e-3))
 
 
 def test_adam_kernel_matches_eager(cuda_device):
