@@ -42,6 +42,10 @@ def main(argv=None):
                     help="cml = the headline config; soilnet = diagnostic (T=337, per-node sequences)")
     ap.add_argument("--sensors", type=int, default=None, help="default: 23 CML links / 40 SoilNet boxes")
     ap.add_argument("--days", type=int, default=None, help="default: 28 (CML) / 89 (SoilNet)")
+    ap.add_argument("--adjacency", choices=["radius", "knn"], default="radius",
+                    help="radius = the reference's rule (max_sample_distance, SURVEY 5.11.4); knn = symmetrised "
+                         "k-nearest-neighbour graph (BASELINE.json's 'k=5')")
+    ap.add_argument("--k", type=int, default=5, help="neighbours per node for --adjacency knn")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -64,6 +68,10 @@ def main(argv=None):
     pc = C.normalize_preproc(C.default(f"preprocessing_{args.ds}"))
     args.batch = args.batch or int(pc.batch_size)
     pc.batch_size = args.batch
+    pc.graph["adjacency"] = args.adjacency
+    pc.graph["k"] = int(args.k)
+    adj_desc = (f"knn(k={args.k})" if args.adjacency == "knn" else
+                f"radius(max_sample_distance={pc.graph['max_sample_distance']})")
     mc = C.default(f"model_{args.ds}")
     mc.runtime.compute_dtype = args.dtype
     if soil:
@@ -88,10 +96,12 @@ def main(argv=None):
     nb = rows.shape[0]
 
     def run(k, start):
-        for i in range(k):
-            trainer.train_step(rows[(start + i) % nb])
+        # every one of the k steps is a full training step (gather, forward, backward, guarded
+        # Adam); chunks of trainer.graph_steps of them replay one multi-step HIP graph
+        trainer.train_steps(rows, start, k)
 
     run(args.warmup, 0)
+    trainer._comm_events = []
     D.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -103,11 +113,16 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     dt = D.max_over_ranks(dt)
     loss = float(trainer.last_loss.item())
+    comm_us = None
+    if trainer._comm_events:             # N > 1: HIP events around the first timed all-reduces
+        comm_us = 1e3 * sum(a.elapsed_time(b) for a, b in trainer._comm_events) / len(trainer._comm_events)
+        comm_us = D.max_over_ranks(comm_us)
     windows = args.steps * args.batch * world
     value = windows / dt
     if rank == 0:
         out = {
-            "metric": "ROC-AUC (5-fold CV) + train windows/sec, CML GCN at 1/2/4/8 MI355X",
+            "metric": ("train windows/sec, SoilNet GCN (diagnostic; not the headline metric)" if soil else
+                       "ROC-AUC (5-fold CV) + train windows/sec, CML GCN at 1/2/4/8 MI355X"),
             "value": round(value, 2),
             "unit": "train windows/s (whole job)",
             "n_gpus": world,
@@ -130,11 +145,15 @@ def main(argv=None):
                 "global_batch": args.batch * world,
                 "seq_len": ws.seq_len,
                 "parallelism": f"dp{world}",
+                "adjacency": adj_desc,
+                "graph_steps": trainer.graph_steps if trainer._multi_ok() else 1,
                 "trainable_params": n_params,
                 "hip_graph": trainer.use_graph,
                 "final_loss": round(loss, 5),
             },
         }
+        if comm_us is not None:
+            out["allreduce_us"] = round(comm_us, 2)        # mean RCCL all-reduce of the flat gradients
         print(json.dumps(out), flush=True)
     D.destroy()
 

@@ -159,6 +159,178 @@ void adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at:
   GQ_LAUNCH_CHECK();
 }
 
+// Guard + Adam in ONE launch (was grad_guard then adam_kernel): every workgroup loads its share of
+// g into registers and counts non-finite entries; arrival ticket state[1]; the last arrival
+// decides ok (no non-finite value, no chain timeout in ext[2]), advances the step counter for
+// a good step, re-arms the counters and bumps the generation word state[4]; every workgroup
+// waits for the generation to move (all are co-resident: grid <= resident capacity, checked
+// on the host; bounded spin) and then applies the update from registers, or only clears g.
+// cursor (optional): the device batch cursor of multi-step graphs, advanced mod cursor_mod.
+template <int K>
+__global__ __launch_bounds__(256) void adam_guarded_kernel(
+    float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ lr_p, float* __restrict__ step_p, long n, float b1, float b2, float eps, float gscale,
+    float wd, int* __restrict__ state, int* __restrict__ ext, long* __restrict__ cursor, long cursor_mod) {
+  __shared__ int wsum[4];
+  __shared__ int okf;
+  const int tid = threadIdx.x;
+  const long n4 = n / 4, stride = (long)gridDim.x * blockDim.x;
+  const long i0 = blockIdx.x * (long)blockDim.x + tid;
+  // every workgroup reads these before it arrives and the last arrival changes them only after
+  // all arrived: no ordering needed. state[4] = 2 * generation + ok of the last decision.
+  const int gen0 = __hip_atomic_load(state + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float step0 = __hip_atomic_load(step_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float4 gg[K];
+  float gt = 0.f;
+  int bad = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long i = i0 + k * stride;
+    gg[k] = i < n4 ? reinterpret_cast<const float4*>(g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bad += !isfinite(gg[k].x) + !isfinite(gg[k].y) + !isfinite(gg[k].z) + !isfinite(gg[k].w);
+  }
+  const long it = n4 * 4 + i0;                   // (n % 4 tail: one element per thread at most)
+  if (it < n) {
+    gt = g[it];
+    bad += !isfinite(gt);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+  if ((tid & 63) == 0) wsum[tid >> 6] = bad;
+  __syncthreads();
+  if (tid == 0) {
+    const int tot = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    // ONE atomic carries both the arrival (low 16 bits) and "this workgroup saw a non-finite
+    // value" (high bits): the last arrival learns everything from the value it gets back
+    const int old = __hip_atomic_fetch_add(state + 1, 1 + (tot ? 65536 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok;
+    if ((old & 0xffff) == (int)gridDim.x - 1) {  // last arrival
+      const int nbad = (old >> 16) + (tot ? 1 : 0);
+      int stale = 0;
+      if (ext != nullptr) {
+        stale = __hip_atomic_exchange(ext + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (stale) __hip_atomic_fetch_add(ext + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ok = nbad == 0 && stale == 0;
+      if (ok) step_p[0] = step0 + 1.0f;
+      else __hip_atomic_fetch_add(state + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + 2, ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + 4, ((gen0 >> 1) + 1) * 2 + ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int spins = 0, gv;
+      while ((gv = __hip_atomic_load(state + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == gen0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 22)) break;          // never expected (co-resident grid): skip below
+      }
+      ok = gv != gen0 ? (gv & 1) : 0;
+    }
+    okf = ok;
+  }
+  __syncthreads();
+  if (!okf) {                                    // rejected step: parameters untouched, g cleared
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const long i = i0 + k * stride;
+      if (i < n4) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (it < n) g[it] = 0.f;
+  } else {
+    const float step = step0 + 1.0f;
+    const float lr = *lr_p;
+    const float alpha = lr * sqrtf(1.0f - powf(b2, step)) / (1.0f - powf(b1, step));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const long i = i0 + k * stride;
+      if (i >= n4) break;
+      reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 pp = reinterpret_cast<float4*>(p)[i];
+      float4 mm = reinterpret_cast<float4*>(m)[i];
+      float4 vv = reinterpret_cast<float4*>(v)[i];
+#define GQ_ADAM_LANE(c)                                         \
+      {                                                         \
+        float gc = gg[k].c * gscale + wd * pp.c;                \
+        mm.c = b1 * mm.c + (1.f - b1) * gc;                     \
+        vv.c = b2 * vv.c + (1.f - b2) * gc * gc;                \
+        pp.c -= alpha * mm.c / (sqrtf(vv.c) + eps);             \
+      }
+      GQ_ADAM_LANE(x) GQ_ADAM_LANE(y) GQ_ADAM_LANE(z) GQ_ADAM_LANE(w)
+#undef GQ_ADAM_LANE
+      reinterpret_cast<float4*>(p)[i] = pp;
+      reinterpret_cast<float4*>(m)[i] = mm;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    if (it < n) {
+      g[it] = 0.f;
+      const float gc = gt * gscale + wd * p[it];
+      m[it] = b1 * m[it] + (1.f - b1) * gc;
+      v[it] = b2 * v[it] + (1.f - b2) * gc * gc;
+      p[it] -= alpha * m[it] / (sqrtf(v[it]) + eps);
+    }
+  }
+  if (cursor != nullptr && blockIdx.x == 0 && tid == 0) cursor[0] = (cursor[0] + 1) % cursor_mod;
+}
+
+// capacity of the co-resident grid (blocks of 256 threads) for adam_guarded_kernel<K>
+template <int K>
+static int adam_guarded_capacity(int dev) {
+  static int cap[64] = {0};
+  if (cap[dev] == 0) {
+    hipDeviceProp_t prop;
+    TORCH_CHECK(hipGetDeviceProperties(&prop, dev) == hipSuccess, "adam_guarded: device properties");
+    int occ = 0;
+    TORCH_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&adam_guarded_kernel<K>),
+                                                           256, 0) == hipSuccess, "adam_guarded: occupancy");
+    cap[dev] = std::max(1, occ * prop.multiProcessorCount);
+  }
+  return cap[dev];
+}
+
+// Returns false (nothing launched) when the buffer is too large for one co-resident grid with
+// <= 8 float4 per thread; the caller then runs grad_guard + adam_step.
+bool adam_guarded(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at::Tensor& lr, at::Tensor step,
+                  double b1, double b2, double eps, double gscale, double wd, at::Tensor state,
+                  const c10::optional<at::Tensor>& ext, const c10::optional<at::Tensor>& cursor, int64_t cursor_mod) {
+  const at::Tensor* ops[] = {&p, &g, &m, &v, &lr, &step};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "adam operand");
+  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kInt && state.numel() >= 5 && state.is_contiguous(),
+              "adam_guarded: state must be int32[>=5] on the device");
+  const long n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) % 16) == 0 &&
+                  (reinterpret_cast<uintptr_t>(m.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(v.data_ptr()) % 16) == 0,
+              "adam: buffers must be 16-byte aligned");
+  int* ep = nullptr;
+  if (ext.has_value() && ext->defined()) {
+    TORCH_CHECK(ext->is_cuda() && ext->scalar_type() == at::kInt && ext->numel() >= 4, "adam_guarded: ext int32[4]");
+    ep = ext->data_ptr<int>();
+  }
+  long* cp = nullptr;
+  if (cursor.has_value() && cursor->defined()) {
+    TORCH_CHECK(cursor->is_cuda() && cursor->scalar_type() == at::kLong && cursor->numel() >= 1 && cursor_mod >= 1,
+                "adam_guarded: cursor int64[1], cursor_mod >= 1");
+    cp = cursor->data_ptr<int64_t>();
+  }
+  c10::DeviceGuard guard(p.device());
+  const int dev = p.get_device();
+  const long n4 = std::max<long>(1, (n / 4 + 255) / 256);      // 256-thread blocks at one float4 each
+#define GQ_ADAM_G(KK)                                                                                        \
+  {                                                                                                          \
+    const int grid = (int)((n4 + KK - 1) / KK);                                                              \
+    if (grid <= adam_guarded_capacity<KK>(dev) && (long)grid * 256 > n % 4) {                                \
+      hipLaunchKernelGGL(adam_guarded_kernel<KK>, dim3(grid), dim3(256), 0, stream(), p.data_ptr<float>(),    \
+                         g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), lr.data_ptr<float>(), \
+                         step.data_ptr<float>(), n, (float)b1, (float)b2, (float)eps, (float)gscale, (float)wd, \
+                         state.data_ptr<int>(), ep, cp, cursor_mod);                                          \
+      GQ_LAUNCH_CHECK();                                                                                     \
+      return true;                                                                                           \
+    }                                                                                                        \
+  }
+  GQ_ADAM_G(1) GQ_ADAM_G(2) GQ_ADAM_G(4) GQ_ADAM_G(8)
+#undef GQ_ADAM_G
+  return false;
+}
+
 at::Tensor nonfinite_count(const at::Tensor& x) {
   check_f32_cuda(x, "x");
   c10::DeviceGuard guard(x.device());
@@ -177,4 +349,5 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("adam_step", &gq::adam_step);
   m.impl("nonfinite_count", &gq::nonfinite_count);
   m.impl("grad_guard", &gq::grad_guard);
+  m.impl("adam_guarded", &gq::adam_guarded);
 }

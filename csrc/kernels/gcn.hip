@@ -208,20 +208,55 @@ __global__ void gcn_pool_bwd_kernel(const float* __restrict__ x, const float* __
   const int L = N * Cin;
   const bool staged = L <= GCN_STAGE_MAX;
   float* sbw = sbx + rows_per_blk * L;
-  for (long r0 = (long)blockIdx.x * rows_per_blk; r0 < nrows; r0 += (long)gridDim.x * rows_per_blk) {
+  // staged: a pass's x rows, node weights of its samples and upstream gradients are fetched
+  // into registers one pass AHEAD (coalesced scalar loads), then parked in LDS, so the node loop
+  // makes no memory round trips and each pass's loads overlap the previous pass's compute
+  constexpr int XG = (32 * GCN_STAGE_MAX + 255) / 256, WG = (34 * GCN_STAGE_MAX + 255) / 256;   // F >= 8: <= 32 rows
+  float px[XG], pw[WG], pg = 0.f;
+  const long stride = (long)gridDim.x * rows_per_blk;
+  auto fetch = [&](long r0) {
+    const long xbeg = r0 * L, xend = min(nrows, r0 + rows_per_blk) * (long)L;
+    const int b0 = (int)(r0 / T);
+    const int nb = r0 < nrows ? min((int)((min(r0 + rows_per_blk, nrows) - 1) / T) - b0 + 1, rows_per_blk / T + 2) : 0;
+#pragma unroll
+    for (int j = 0; j < XG; ++j) {
+      const long i = xbeg + threadIdx.x + 256 * j;
+      px[j] = i < xend ? x[i] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < WG; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      pw[j] = i < nb * N ? w[(long)b0 * N + i] : 0.f;
+    }
+    const long row = r0 + rsub;
+    if (row < nrows) {
+      const long dro = dmp > 0 ? ((row % T) * dmp + row / T) * (long)dstride : row * (long)dstride;
+      pg = dout[dro + c_off + f];
+    }
+  };
+  if (staged) fetch((long)blockIdx.x * rows_per_blk);
+  for (long r0 = (long)blockIdx.x * rows_per_blk; r0 < nrows; r0 += stride) {
     const long row = r0 + rsub;
     const int b0 = (int)(r0 / T);
+    float g = 0.f;
     if (staged) {
       __syncthreads();
-      gcn_stage_rows(x, sbx, r0, rows_per_blk, nrows, L);
-      const int nb = min((int)((min(r0 + rows_per_blk, nrows) - 1) / T) - b0 + 1, rows_per_blk / T + 2);
-      for (int i = threadIdx.x; i < nb * N; i += blockDim.x) sbw[i] = w[(long)b0 * N + i];
+#pragma unroll
+      for (int j = 0; j < XG; ++j)
+        if (threadIdx.x + 256 * j < rows_per_blk * L) sbx[threadIdx.x + 256 * j] = px[j];
+#pragma unroll
+      for (int j = 0; j < WG; ++j)
+        if (threadIdx.x + 256 * j < (rows_per_blk / T + 2) * N) sbw[threadIdx.x + 256 * j] = pw[j];
       __syncthreads();
+      g = pg;
+      if (r0 + stride < nrows) fetch(r0 + stride);
     }
     if (row >= nrows) continue;
     const int b = row / T;
-    const long dro = dmp > 0 ? ((row % T) * dmp + row / T) * (long)dstride : row * (long)dstride;
-    const float g = dout[dro + c_off + f];
+    if (!staged) {
+      const long dro = dmp > 0 ? ((row % T) * dmp + row / T) * (long)dstride : row * (long)dstride;
+      g = dout[dro + c_off + f];
+    }
     const float* xr = staged ? sbx + rsub * L : x + row * (long)L;
     const float* wr = staged ? sbw + (long)(b - b0) * N : w + (long)b * N;
     for (int n = 0; n < N; ++n) {

@@ -21,6 +21,7 @@
 namespace gq {
 
 constexpr int GLUE_MAX_CIN = 8;
+constexpr int GLUE_NSTAT_MAX = GLUE_MAX_CIN + GLUE_MAX_CIN * GLUE_MAX_CIN + 1;
 
 // pool: 0 mean over valid nodes, 1 sum, 2 selection of anom_pos ; agg_mean: divide by in-degree
 __global__ __launch_bounds__(256) void gcn_pool_weights_kernel(const float* __restrict__ adj,
@@ -110,8 +111,20 @@ __global__ __launch_bounds__(256) void gcn_bwd_finalize_kernel(
     float* __restrict__ coef) {
   const int f = blockIdx.x;
   const int nacc = 3 + Cin;
-  __shared__ float red[GLUE_MAX_CIN + 3][256];
+  __shared__ float red[4][GLUE_MAX_CIN + 3];
   __shared__ float tot[GLUE_MAX_CIN + 3];
+  // the closed-form epilogue's operands, fetched up front so their loads overlap the reduction's
+  // (thread 0 loading them after it was a chain of dependent memory round trips)
+  __shared__ double sS[GLUE_NSTAT_MAX];
+  __shared__ float sWf[GLUE_MAX_CIN], sst[3], sb;
+  {
+    const int t = threadIdx.x;
+    const int nstat = Cin + Cin * Cin + 1;
+    if (training && acc != nullptr && t < nstat) sS[t] = S[t];
+    if (t >= 96 && t < 96 + Cin) sWf[t - 96] = W[(t - 96) * F + f];
+    if (t >= 128 && t < 131) sst[t - 128] = st[(t - 128) * F + f];
+    if (t == 192) sb = b[f];
+  }
   if (acc != nullptr) {
     float a[GLUE_MAX_CIN + 3];
 #pragma unroll
@@ -121,19 +134,23 @@ __global__ __launch_bounds__(256) void gcn_bwd_finalize_kernel(
       for (int j = 0; j < GLUE_MAX_CIN + 3; ++j)
         if (j < nacc) a[j] += acc[((long)r * nacc + j) * F + f];
     }
+    // fixed-shape reduction: wave shuffles, then the 4 wave partials in order (deterministic)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < GLUE_MAX_CIN + 3; ++j) red[j][threadIdx.x] = a[j];
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o)
-        for (int j = 0; j < nacc; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + o];
-      __syncthreads();
+    for (int j = 0; j < GLUE_MAX_CIN + 3; ++j) {
+      float v = a[j];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) red[wv][j] = v;
     }
-    if ((int)threadIdx.x < nacc) tot[threadIdx.x] = red[threadIdx.x][0];
+    __syncthreads();
+    if ((int)threadIdx.x < nacc)
+      tot[threadIdx.x] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
     __syncthreads();
   }
+  __syncthreads();
   if (threadIdx.x != 0) return;
-  const float mu = st[f], inv = st[F + f], sc = st[2 * F + f];
+  const float mu = sst[0], inv = sst[1], sc = sst[2];
   float c0 = 0.f, c2 = 0.f;
   if (acc != nullptr) {
     const float A = tot[0], Z = tot[1], P = tot[2];
@@ -142,12 +159,12 @@ __global__ __launch_bounds__(256) void gcn_bwd_finalize_kernel(
     if (dgamma) dgamma[f] += dg;
     if (dalpha) dalpha[f] += P;
     if (training) {
-      const double n = fmax(S[Cin + Cin * Cin], 1.0);
+      const double n = fmax(sS[Cin + Cin * Cin], 1.0);
       for (int k = 0; k < Cin; ++k) {
         double s2w = 0.0;
-        for (int l = 0; l < Cin; ++l) s2w += S[Cin + k * Cin + l] * (double)W[l * F + f];
-        const double s1 = S[k];
-        const double sxx = inv * (s2w + s1 * ((double)b[f] - mu));
+        for (int l = 0; l < Cin; ++l) s2w += sS[Cin + k * Cin + l] * (double)sWf[l];
+        const double s1 = sS[k];
+        const double sxx = inv * (s2w + s1 * ((double)sb - mu));
         const double q = tot[3 + k];
         if (dW) dW[k * F + f] += (float)(sc * (q - s1 * A / n - sxx * dg / n));
       }
@@ -169,7 +186,6 @@ __global__ __launch_bounds__(256) void gcn_bwd_finalize_kernel(
 // record with sc1 stores; the workgroup whose arrival-counter add comes last sums the records in
 // sample order (deterministic) and runs the BN prep (batch statistics, Keras running-stat
 // update, scale / shift). Eval: workgroup 0 preps BN from the running statistics.
-constexpr int GLUE_NSTAT_MAX = GLUE_MAX_CIN + GLUE_MAX_CIN * GLUE_MAX_CIN + 1;
 constexpr int GLUE_ADJ_LDS = 8192;      // adjacency floats staged in LDS (32 KiB)
 
 __device__ __forceinline__ void glue_bn(const double* S, int Cin, int F, const float* __restrict__ W,
@@ -231,6 +247,10 @@ __global__ __launch_bounds__(256) void gcn_prep_kernel(
     for (int i = threadIdx.x; i < N * N; i += blockDim.x) sA[i] = A[i];
     A = sA;
   }
+  {
+    float* sM = coef + N + (N * N <= GLUE_ADJ_LDS ? N * N : 0);
+    for (int i = threadIdx.x; i < N; i += blockDim.x) sM[i] = m[i];
+  }
   // pooling weights w[b, j] = sum_i p_i / deg_i * A[i, j]
   float ms = 0.f;
   for (int i = threadIdx.x; i < N; i += blockDim.x) ms += m[i];
@@ -262,24 +282,36 @@ __global__ __launch_bounds__(256) void gcn_prep_kernel(
     if (b == 0) glue_bn(nullptr, Cin, F, W, bias, gamma, beta, rmean, rvar, 0, momentum, eps, st);
     return;
   }
-  // this sample's moments over its T x N node rows (fp64)
+  // this sample's moments over its T x N node rows (fp64), 4 rows per thread per round with all
+  // their loads issued first (a load-then-branch loop made every row a serial memory round trip);
+  // masked rows contribute zeros
   double acc[nstat];
 #pragma unroll
   for (int i = 0; i < nstat; ++i) acc[i] = 0.0;
   const float* xb = x + (long)b * T * N * Cin;
-  for (int r = threadIdx.x; r < T * N; r += blockDim.x) {
-    const float mv = m[r % N];
-    float xv[Cin];
+  const int R = T * N;
+  const float* sM = coef + N + (N * N <= GLUE_ADJ_LDS ? N * N : 0);   // the sample's mask (LDS)
+  for (int r0 = threadIdx.x; r0 < R; r0 += 4 * blockDim.x) {
+    float xv[4][Cin], mv[4];
 #pragma unroll
-    for (int k = 0; k < Cin; ++k) xv[k] = xb[(long)r * Cin + k];
-    if (mv == 0.f) continue;
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u * (int)blockDim.x;
+      const int rc = r < R ? r : 0;
 #pragma unroll
-    for (int k = 0; k < Cin; ++k) {
-      acc[k] += mv * xv[k];
-#pragma unroll
-      for (int l = 0; l < Cin; ++l) acc[Cin + k * Cin + l] += (double)(mv * xv[k]) * xv[l];
+      for (int k = 0; k < Cin; ++k) xv[u][k] = xb[(long)rc * Cin + k];
+      mv[u] = r < R ? sM[rc % N] : 0.f;
     }
-    acc[nstat - 1] += mv;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) {
+        const float mx = mv[u] * xv[u][k];
+        acc[k] += mx;
+#pragma unroll
+        for (int l = 0; l < Cin; ++l) acc[Cin + k * Cin + l] += (double)mx * xv[u][l];
+      }
+      acc[nstat - 1] += mv[u];
+    }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -369,7 +401,7 @@ std::vector<at::Tensor> gcn_prep(const at::Tensor& x, const at::Tensor& adj, con
   TORCH_CHECK(adj.size(0) == B && adj.size(1) == N && adj.size(2) == N && mask.size(0) == B && mask.size(1) == N,
               "gcn_prep: adj / mask shapes");
   TORCH_CHECK(W.size(0) == Cin && Cin >= 1 && Cin <= 4, "gcn_prep: W must be [Cin<=4, F]");
-  TORCH_CHECK(pool >= 0 && pool <= 2 && N <= 16384 && B >= 1, "gcn_prep: pool / sizes");
+  TORCH_CHECK(pool >= 0 && pool <= 2 && N <= 8192 && B >= 1, "gcn_prep: pool / sizes");
   const int64_t* ap = nullptr;
   if (pool == 2) {
     TORCH_CHECK(anom_pos.is_cuda() && anom_pos.scalar_type() == at::kLong && anom_pos.numel() == B &&
@@ -383,7 +415,7 @@ std::vector<at::Tensor> gcn_prep(const at::Tensor& x, const at::Tensor& adj, con
   at::Tensor part = training ? at::empty({(long)B * nstat}, x.options().dtype(at::kDouble)) : S;
   at::Tensor st = at::empty({4, F}, x.options());
   int* tk = glue_ticket(x.get_device());
-  const size_t smem = (N + (N * N <= GLUE_ADJ_LDS ? N * N : 0)) * sizeof(float);
+  const size_t smem = (2 * N + (N * N <= GLUE_ADJ_LDS ? N * N : 0)) * sizeof(float);
   GQ_GLUE_CIN_DISPATCH(Cin, hipLaunchKernelGGL(gcn_prep_kernel<CIN>, dim3(B), dim3(256), smem, stream(),
       x.data_ptr<float>(), adj.data_ptr<float>(), mask.data_ptr<float>(), ap, B, T, N, agg_mean ? 1 : 0, (int)pool,
       w.data_ptr<float>(), training ? part.data_ptr<double>() : nullptr, training ? S.data_ptr<double>() : nullptr,

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const int nblk = gridDim.x;
   if ((int)blockIdx.x >= A.ns * A.nt8) {          // packing workgroups
     const int f = ((int)blockIdx.x - A.ns * A.nt8) * 1024 + (int)threadIdx.x;
-    if (A.pk != nullptr && f < T4PK_N) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
+    if (A.pk != nullptr && f < T4PK_ALL) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
     chain_finish(A.ctl, nblk);
     return;
   }
@@ -1050,12 +1050,12 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     check_f32_cuda(*pkU, "Ut4");
     TORCH_CHECK(pkU->size(0) == 128 && pkU->size(1) == 512 && pkW->size(1) == 512 && pkW->size(0) <= 64,
                 "lstm_chain_fwd_pack: time4 weights must be [<=64, 512] and [128, 512]");
-    pk = at::empty({(long)T4PK_N * 4}, opt);                  // 16 B per fragment
+    pk = at::empty({(long)T4PK_ALL * 4}, opt);                // 16 B per fragment (forward + backward)
     A.pkU = pkU->data_ptr<float>();
     A.pkW = pkW->data_ptr<float>();
     A.pkDw = (int)pkW->size(0);
     A.pk = reinterpret_cast<bf16x8_t*>(pk.data_ptr<float>());
-    nblk += (T4PK_N + 1023) / 1024;
+    nblk += (T4PK_ALL + 1023) / 1024;
     TORCH_CHECK(nblk <= chain_capacity(x.get_device()), "lstm_chain: ", nblk,
                 " workgroups cannot all be resident on this device");
   }

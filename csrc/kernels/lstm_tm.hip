@@ -26,6 +26,8 @@
 //                VGPRs for the whole sequence and flushed once with atomics.
 // So dz never goes to HBM and no separate weight-gradient kernel runs.
 #include "common.h"
+
+#include <cstdlib>
 #include "lstm_grads_body.h"
 #include "lstm_tm_common.h"
 
@@ -1019,7 +1021,13 @@ at::Tensor lstm_grads_job_ws(const at::Tensor& dz, const at::Tensor& x, const at
   const long rows = x.numel() / x.size(-1);
   const int ncb = lstm_grads_col_blocks((int)H);
   const long ntiles = (rows + 31) / 32;
-  const int splits = (int)std::max<long>(1, std::min<long>({(ntiles + 1) / 2, (long)std::max(64, 2048 / ncb),
+  // row tiles per split: each split writes a whole record (all column blocks) once, so few tiles
+  // per split multiply the record traffic (written here, re-read by the reduction)
+  static const int tps = [] {
+    const char* e = std::getenv("GNNQC_GRADS_TPS");
+    return e != nullptr ? std::max(1, std::atoi(e)) : 4;   // 4: best of 2 / 4 / 8 / 16 on the CML step
+  }();
+  const int splits = (int)std::max<long>(1, std::min<long>({(ntiles + tps - 1) / tps, (long)std::max(64, 2048 / ncb),
                                                             (long)PIPE_MAX_SPLITS}));
   const int DT = (Dw + 1 + 15) / 16, HT = (int)H / 16;
   c10::DeviceGuard guard(x.device());

@@ -109,7 +109,7 @@ inline TmPool tm_pool_outputs(int P, int T, int Mp, int H, const at::TensorOptio
   return pl;
 }
 
-// ---- time4 (H = 128, Din <= 64) forward A-fragment image (time4_head.hip's 512-thread layout:
+// ---- time4 (H = 128, Din <= 64) forward and backward A-fragment images (time4_head.hip's 512-thread layout:
 // wave w of 8, cell cc of 4, lane = (quad, col)): U fragments [w][cc][s < 4][lane], then W
 // fragments [w][cc][s < 2][lane], each 8 bf16. Gathering them from the [K][4H] weights touches 16
 // cache lines per load instruction, so the chain forward's idle workgroups build this image once per
@@ -117,9 +117,35 @@ inline TmPool tm_pool_outputs(int P, int T, int Mp, int H, const at::TensorOptio
 constexpr int T4PK_U = 8 * 4 * 4 * 64;
 constexpr int T4PK_W = 8 * 4 * 2 * 64;
 constexpr int T4PK_N = T4PK_U + T4PK_W;
+// backward image (time4_head.hip t4_head_bwd_kernel): U rows [w][s < 16][lane] = U[16w + col][32s + 8quad ..],
+// then W rows [w][s < 8][lane] = W[16 (w & 3) + col][256 (w >> 2) + 32s + 8quad ..] (rows >= Dw zero)
+constexpr int T4PK_BU = 8 * 16 * 64;
+constexpr int T4PK_BW = 8 * 8 * 64;
+constexpr int T4PK_ALL = T4PK_N + T4PK_BU + T4PK_BW;
 
 __device__ __forceinline__ void t4_pack_one(int f, const float* __restrict__ U, const float* __restrict__ W, int Dw,
                                             bf16x8_t* __restrict__ out) {
+  if (f >= T4PK_N) {                       // backward fragments: 8 contiguous floats per lane
+    const int fb = f - T4PK_N;
+    const bool isU = fb < T4PK_BU;
+    const int f2 = isU ? fb : fb - T4PK_BU;
+    const int lane = f2 & 63, col = lane & 15, quad = lane >> 4;
+    const int s = isU ? (f2 >> 6) & 15 : (f2 >> 6) & 7;
+    const int w = isU ? f2 >> 10 : f2 >> 9;
+    const float* src;
+    float m = 1.f;
+    if (isU) {
+      src = U + (size_t)(16 * w + col) * 512 + 32 * s + 8 * quad;
+    } else {
+      const int din = 16 * (w & 3) + col;
+      m = din < Dw ? 1.f : 0.f;
+      src = W + (size_t)min(din, Dw - 1) * 512 + 256 * (w >> 2) + 32 * s + 8 * quad;
+    }
+    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+    out[f] = bf16x8_t{(__bf16)(a.x * m), (__bf16)(a.y * m), (__bf16)(a.z * m), (__bf16)(a.w * m),
+                      (__bf16)(b.x * m), (__bf16)(b.y * m), (__bf16)(b.z * m), (__bf16)(b.w * m)};
+    return;
+  }
   const bool isU = f < T4PK_U;
   const int f2 = isU ? f : f - T4PK_U;
   const int lane = f2 & 63;

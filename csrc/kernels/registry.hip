@@ -51,7 +51,7 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor(d!)[] ext) -> Tensor[]");
   m.def("time4_head_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor pk, bool train, Tensor[] head, Tensor y, Tensor mask, "
         "int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");
-  m.def("time4_head_bwd(Tensor dloss, Tensor x, Tensor h, Tensor g, Tensor c, Tensor W, Tensor U, Tensor[] head, "
+  m.def("time4_head_bwd(Tensor dloss, Tensor x, Tensor h, Tensor g, Tensor c, Tensor W, Tensor U, Tensor pk, Tensor[] head, "
         "Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!)[] hgrads) -> Tensor[]");
   m.def("time4_trace(Tensor like) -> Tensor");
   m.def("lstm_tm_bwd_pipe(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T, Tensor gz, Tensor gx, "
@@ -91,7 +91,13 @@ TORCH_LIBRARY(gnnqc, m) {
   // flat-buffer optimiser (adam.hip)
   m.def("adam_step(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor step, float beta1, "
         "float beta2, float eps, float grad_scale, float weight_decay, Tensor? guard=None, bool zero_grad=False) -> ()");
+  m.def("adam_guarded(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor(e!) step, float beta1, "
+        "float beta2, float eps, float grad_scale, float weight_decay, Tensor(f!) state, Tensor(g!)? ext=None, "
+        "Tensor(h!)? cursor=None, int cursor_mod=1) -> bool");
   m.def("nonfinite_count(Tensor x) -> Tensor");
+  m.def("ig_interp(Tensor v, Tensor alpha) -> Tensor");
+  m.def("ig_accum(Tensor(a!) acc, Tensor g, Tensor w) -> ()");
+  m.def("ig_finalize(Tensor acc, Tensor v, int mode) -> Tensor");
   m.def("grad_guard(Tensor g, Tensor(a!) state, Tensor(b!) step, Tensor(c!)? ext=None) -> ()");
   // metrics (metrics.hip)
   m.def("score_histogram(Tensor scores, Tensor labels, Tensor mask, int bins) -> Tensor");
@@ -109,4 +115,7 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor win_valid, Tensor wids, int tb, int seq_len, bool time_norm) -> Tensor");
   m.def("batch_meta(Tensor wids, Tensor win_group, Tensor win_valid, Tensor group_adj, Tensor group_anom_pos, "
         "Tensor win_label, Tensor win_label_valid, Tensor valid_sample, Tensor x) -> Tensor[]");
+  m.def("batch_gather(Tensor series, Tensor shift, Tensor scale, Tensor win_group, Tensor win_center, "
+        "Tensor win_valid, Tensor wids, Tensor table, Tensor? cursor, Tensor group_adj, Tensor group_anom_pos, "
+        "Tensor win_label, Tensor win_label_valid, Tensor valid_sample, int tb, int seq_len, bool time_norm) -> Tensor[]");
 }

@@ -268,26 +268,6 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
   const int col = lane & 15, quad = lane >> 4;
   const int dt = w & 3, kh = w >> 2;
 
-  // recurrent / input weights as A fragments (loads in flight during the head prologue)
-  bf16x8_t ufr[T4G / 32], wfr[8];
-#pragma unroll
-  for (int s = 0; s < T4G / 32; ++s) {
-    const float* src = A.U + (size_t)(16 * w + col) * T4G + 32 * s + 8 * quad;
-    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-    ufr[s] = bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
-                      (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
-  }
-  {
-    const int din = 16 * dt + col;
-    const float m = (dt < 2 * KX && din < Dw) ? 1.f : 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const float* src = A.W + (size_t)min(din, Dw - 1) * T4G + 256 * kh + 32 * s + 8 * quad;
-      const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-      wfr[s] = bf16x8_t{(__bf16)(a.x * m), (__bf16)(a.y * m), (__bf16)(a.z * m), (__bf16)(a.w * m),
-                        (__bf16)(b.x * m), (__bf16)(b.y * m), (__bf16)(b.z * m), (__bf16)(b.w * m)};
-    }
-  }
   int unit[T4CPL];
 #pragma unroll
   for (int cc = 0; cc < T4CPL; ++cc) unit[cc] = 4 * (w + T4NW * cc) + quad;
@@ -310,6 +290,35 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
 
   t4_mark(A.trace, 0);
   chain_head_bwd<T4H>(A.hd, A.h + (size_t)(T - 1) * Mp * T4H, tile, ntiles, dhT, rs);
+  // recurrent / input weights as A fragments, after the head prologue (live through it they
+  // pushed the kernel past 256 VGPRs into scratch): from the chain forward's backward image
+  // (lane-contiguous 16-B loads), else gathered (16 rows per load instruction: ~10 us)
+  bf16x8_t ufr[T4G / 32], wfr[8];
+  if (A.pk != nullptr) {
+    const bf16x8_t* pu = A.pk + T4PK_N + (size_t)w * 16 * 64 + lane;
+    const bf16x8_t* pw = A.pk + T4PK_N + T4PK_BU + (size_t)w * 8 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < T4G / 32; ++s) ufr[s] = pu[s * 64];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) wfr[s] = pw[s * 64];
+  } else {
+#pragma unroll
+    for (int s = 0; s < T4G / 32; ++s) {
+      const float* src = A.U + (size_t)(16 * w + col) * T4G + 32 * s + 8 * quad;
+      const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+      ufr[s] = bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                        (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+    }
+    const int din = 16 * dt + col;
+    const float m = (dt < 2 * KX && din < Dw) ? 1.f : 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float* src = A.W + (size_t)min(din, Dw - 1) * T4G + 256 * kh + 32 * s + 8 * quad;
+      const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+      wfr[s] = bf16x8_t{(__bf16)(a.x * m), (__bf16)(a.y * m), (__bf16)(a.z * m), (__bf16)(a.w * m),
+                        (__bf16)(b.x * m), (__bf16)(b.y * m), (__bf16)(b.z * m), (__bf16)(b.w * m)};
+    }
+  }
   __syncthreads();                      // the head scratch becomes the step tiles
   t4_mark(A.trace, 1);
 
@@ -356,11 +365,17 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
         for (int q = 0; q < 2; ++q) b[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         const bool dxw = dt < 2 * KX;    // (uniform)
 #pragma unroll
-        for (int k = 0; k < T4G / 32; ++k) {
-          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[col][32 * k + 8 * quad]);
-          a[k & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a[k & 3], 0, 0, 0);
-          if (dxw && (k >> 3) == kh)
-            b[k & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[k & 7], bz, b[k & 1], 0, 0, 0);
+        for (int hh = 0; hh < 2; ++hh) {   // gate-column halves: one uniform branch per half for dx
+          bf16x8_t bz[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bz[j] = *reinterpret_cast<const bf16x8_t*>(&zs[col][32 * (8 * hh + j) + 8 * quad]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            a[j & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[8 * hh + j], bz[j], a[j & 3], 0, 0, 0);
+          if (dxw && hh == kh) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[j], bz[j], b[j & 1], 0, 0, 0);
+          }
         }
         const f32x4_t as = (a[0] + a[1]) + (a[2] + a[3]);
 #pragma unroll
@@ -467,7 +482,7 @@ std::vector<at::Tensor> time4_head_fwd(const at::Tensor& x, const at::Tensor& W,
   A.U = U.data_ptr<float>();
   A.b = b.data_ptr<float>();
   if (pk.numel() > 0) {
-    TORCH_CHECK(pk.is_cuda() && pk.is_contiguous() && pk.nbytes() == (size_t)T4PK_N * 16,
+    TORCH_CHECK(pk.is_cuda() && pk.is_contiguous() && pk.nbytes() >= (size_t)T4PK_N * 16,
                 "time4_head: fragment image size");
     A.pk = reinterpret_cast<const bf16x8_t*>(pk.data_ptr());
   }
@@ -514,7 +529,7 @@ std::vector<at::Tensor> time4_head_fwd(const at::Tensor& x, const at::Tensor& W,
 // hgrads = [dW1, db1, dW2, db2, dW3, db3]; returns [dz [T + 1, Mp, 512], dx [T, Mp, Din]].
 std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor& x, const at::Tensor& h,
                                        const at::Tensor& g, const at::Tensor& c, const at::Tensor& W,
-                                       const at::Tensor& U, at::TensorList head, const at::Tensor& y,
+                                       const at::Tensor& U, const at::Tensor& pk, at::TensorList head, const at::Tensor& y,
                                        const at::Tensor& mask, int64_t M, double alpha1, double alpha2, double w0,
                                        double w1, at::TensorList hgrads) {
   int T, Mp, Din, Dw;
@@ -561,6 +576,11 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   A.hd.ctl = chain_ctl(x.get_device());
   A.head = 1;
   A.trace = t4_trace_buf(x.get_device());
+  if (pk.numel() > 0) {         // the chain forward's image including the backward fragments
+    TORCH_CHECK(pk.is_cuda() && pk.is_contiguous() && pk.nbytes() == (size_t)T4PK_ALL * 16,
+                "time4_head_bwd: pk must be the forward's full fragment image");
+    A.pk = reinterpret_cast<const bf16x8_t*>(pk.data_ptr());
+  }
   TORCH_CHECK(ntiles <= 256, "time4_head: at most 256 tiles");
   if ((Din + 31) / 32 == 1)
     hipLaunchKernelGGL((t4_head_bwd_kernel<1>), dim3(ntiles), dim3(T4NT), 0, stream(), A);

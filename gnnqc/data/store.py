@@ -19,7 +19,7 @@ Normalisations (``parse_*_tfrecord_fn``, ``:566-634,771-857``): ``rolling_median
 from __future__ import annotations
 
 import dataclasses
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import numpy as np
 import torch
@@ -101,6 +101,14 @@ def _norm_arrays(group, normalization: str):
     return shift[None].astype(np.float32), scale[None].astype(np.float32)
 
 
+class CursorIds(NamedTuple):
+    """Batch ids read on the device: row ``cursor[0] % table.shape[0]`` of ``table`` [rows, B]
+    (int64). The optimiser's update advances the cursor, so a HIP graph of several training steps
+    walks the table without any host work between them."""
+    table: torch.Tensor
+    cursor: torch.Tensor
+
+
 class DeviceStore:
     """All windows of a :class:`WindowSet`, resident on one device."""
 
@@ -175,29 +183,37 @@ class DeviceStore:
     def labels(self, ids=None) -> torch.Tensor:
         return self.win_label if ids is None else self.win_label[ids]
 
-    def gather(self, wids: torch.Tensor, valid_sample: Optional[torch.Tensor] = None) -> Batch:
+    def gather(self, wids, valid_sample: Optional[torch.Tensor] = None) -> Batch:
         """Cut a batch of windows out of the resident series (all on device).
 
         ``wids`` may contain -1 for padding slots; those samples get all-zero
-        inputs and zero label masks.
+        inputs and zero label masks. ``wids`` may also be a :class:`CursorIds` (multi-step
+        graphs): the batch is row ``cursor % rows`` of a device id table, read on the device.
         """
         dev = self.device
-        wids = wids.to(dev)
+        cur = wids if isinstance(wids, CursorIds) else None
         from ..ops import use_hip
         if use_hip(self.series) and self.series.dtype == torch.float32 and self.group_adj.dtype == torch.float32:
-            # two launches: the normalised window cut + everything else (masks, adjacency, labels, anom)
+            # ONE launch: the normalised window cut + masks, adjacency, labels, flagged series
             from ..utils.native import hip_ops
             ops = hip_ops()
-            wl = wids.long().contiguous()
-            x = ops.window_gather(self.series, self.shift, self.scale, self.win_group, self.win_center,
-                                  self.win_valid_u8, wl, self.tb, self.seq_len, self.time_varying_norm)
-            vs = (valid_sample.to(dev, torch.float32).contiguous() if valid_sample is not None
-                  else x.new_zeros(0))
-            lv = self.win_label_valid if self.win_label_valid is not None else x.new_zeros(0)
-            vm, adj, ap, y, y_mask, anom = ops.batch_meta(wl, self.win_group, self.win_valid_u8, self.group_adj,
-                                                          self.group_anom_pos, self.win_label, lv, vs, x)
+            e = self.series.new_zeros(0)
+            el = e.long()
+            vs = valid_sample.to(dev, torch.float32).contiguous() if valid_sample is not None else e
+            lv = self.win_label_valid if self.win_label_valid is not None else e
+            if cur is not None:
+                args = (el, cur.table, cur.cursor)
+            else:
+                args = (wids.to(dev).long().contiguous(), el, None)
+            x, vm, adj, ap, y, y_mask, anom, wid = ops.batch_gather(
+                self.series, self.shift, self.scale, self.win_group, self.win_center, self.win_valid_u8, *args,
+                self.group_adj, self.group_anom_pos, self.win_label, lv, vs, self.tb, self.seq_len,
+                self.time_varying_norm)
             return Batch(x=x, adj=adj, node_mask=vm, anom=anom if self.ds_type == "cml" else None, anom_pos=ap,
-                         y=y, y_mask=y_mask, wid=wids)
+                         y=y, y_mask=y_mask, wid=wid)
+        if cur is not None:
+            wids = cur.table[cur.cursor[0] % cur.table.shape[0]]
+        wids = wids.to(dev)
         pad = wids < 0
         w = wids.clamp(min=0)
         g = self.win_group[w]
@@ -282,4 +298,4 @@ class DeviceLoader:
             yield self.store.gather(row)
 
 
-__all__ = ["Batch", "DeviceStore", "DeviceLoader"]
+__all__ = ["Batch", "CursorIds", "DeviceStore", "DeviceLoader"]

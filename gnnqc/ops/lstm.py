@@ -468,7 +468,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
         ctx.params = params
         ctx.set_materialize_grads(False)     # (no zeros tensor for the non-differentiable logits)
         if need:
-            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs, h4, g4, c4)
+            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs, h4, g4, c4, pk)
         ctx.mark_non_differentiable(logits)
         return loss.reshape(()), logits
 
@@ -483,7 +483,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
         Ws, Us = saved[3:4 + ns], saved[4 + ns:5 + 2 * ns]
         head = saved[5 + 2 * ns:11 + 2 * ns]
         outs = saved[11 + 2 * ns:11 + 7 * ns]
-        h4, g4, c4 = saved[11 + 7 * ns:]
+        h4, g4, c4, pk = saved[11 + 7 * ns:]
         need = ctx.needs_input_grad
         npar = 3 * (ns + 1)
 
@@ -497,7 +497,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
             g = g.contiguous()
         hsinks = [_grad_sink(p) for p in ctx.params[npar:]]
         xt = layer_x(ns)
-        dz4, dxt = ops.time4_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], list(head), y, mask, ctx.M, *ctx.consts,
+        dz4, dxt = ops.time4_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], pk, list(head), y, mask, ctx.M, *ctx.consts,
                                       [s for s, _ in hsinks])
         order = list(reversed(range(ns)))
         e8 = x.new_zeros(0, dtype=torch.uint8)

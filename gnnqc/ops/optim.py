@@ -22,7 +22,7 @@ Optimisers by name like ``libs/fit_model.py:71-74``: adam (Keras eps 1e-7,
 """
 from __future__ import annotations
 
-from typing import Iterable, List
+from typing import Optional, Iterable, List
 
 import torch
 
@@ -60,9 +60,13 @@ class FlatOptimizer:
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)   # applied steps (bias correction)
         self.iterations = 0                                              # attempted steps (host)
         self.guard = bool(guard)
-        # [nonfinite count, ticket, ok flag, skipped steps] (see adam.hip grad_guard)
-        self.guard_state = torch.zeros(4, device=dev, dtype=torch.int32)
+        # [nonfinite count, ticket, ok flag, skipped steps, decision generation, -, -, -]
+        # (adam.hip grad_guard / adam_guarded)
+        self.guard_state = torch.zeros(8, device=dev, dtype=torch.int32)
         self.guard_state[2] = 1
+        # multi-step graphs (gnnqc.train.engine): a device batch cursor the update advances
+        self.cursor: Optional[torch.Tensor] = None
+        self.cursor_mod = 1
 
     @property
     def skipped_steps(self) -> int:
@@ -152,6 +156,17 @@ class FlatAdam(FlatOptimizer):
     def step(self, grad_scale: float = 1.0):
         from . import use_hip
         hip = use_hip(self.flat_p)
+        if hip and self.guard and self.zero_grad_in_step:
+            # guard + update (+ batch cursor) as ONE launch when the buffer fits a co-resident grid
+            from ..utils.native import hip_ops
+            from .lstm import chain_ctl
+            if hip_ops().adam_guarded(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
+                                      self.beta2, self.eps, float(grad_scale), self.wd, self.guard_state,
+                                      chain_ctl(self.flat_g.device), self.cursor, int(self.cursor_mod)):
+                self.iterations += 1
+                return
+        if self.cursor is not None:
+            raise RuntimeError("a device batch cursor needs the single-launch HIP Adam")
         ok = self._begin_step(need_flag=not hip)
         if hip:
             from ..utils.native import hip_ops

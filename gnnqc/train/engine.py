@@ -102,6 +102,16 @@ class Trainer:
         self.poison = torch.zeros(1, device=self.device) if (self.fault and self.fault.poisons) else None
         # HIP-event timing of the DP all-reduce (read once per epoch)
         self._comm_events = []
+        # multi-step graphs (train_steps): GNNQC_GRAPH_STEPS training steps per replay, walking a
+        # device batch table with a device cursor the Adam launch advances (no host work, no id
+        # copy and no graph-launch gap between those steps)
+        self.graph_steps = max(1, int(os.environ.get("GNNQC_GRAPH_STEPS", "8")))
+        self.multi_graph = None
+        self._multi_key = None
+        self._table = None
+        self._cursor = torch.zeros(1, dtype=torch.long, device=self.device)
+        self._graph_loss = None
+        self._multi_loss = None
 
     # ---------------------------------------------------------------- body
     def _loss(self, wids, metrics: Optional["MetricAccumulator"] = None):
@@ -167,12 +177,80 @@ class Trainer:
             with torch.cuda.graph(self.opt_graph):
                 self.opt.step(grad_scale=1.0 / self.world)
         self.opt.iterations = it0          # capture runs nothing; replays count steps
+        self._graph_loss = self.last_loss
         # undo warm-up side effects (BN running stats, metric sums)
         with torch.no_grad():
             for k, v in self.model.state_dict().items():
                 v.copy_(snap[k])
         self.train_metrics.reset()
         self.opt.zero_grad()
+
+    def _multi_ok(self) -> bool:
+        return (self.use_graph and not self.split_opt and self.fault is None and self.graph_steps > 1
+                and getattr(self.opt, "zero_grad_in_step", False) and self.opt.guard)
+
+    def _capture_multi(self, nrows: int):
+        """Capture ``graph_steps`` full training steps (gather -> forward -> backward -> guarded
+        Adam, which advances the device cursor) as ONE graph over the static table [nrows, B]."""
+        from ..data.store import CursorIds
+        snap = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+        ids = CursorIds(self._table, self._cursor)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._body(ids, with_opt=False)
+        torch.cuda.current_stream().wait_stream(s)
+        self.opt.zero_grad()
+        self.multi_graph = torch.cuda.CUDAGraph()
+        it0 = self.opt.iterations
+        self.opt.cursor, self.opt.cursor_mod = self._cursor, nrows
+        try:
+            with torch.cuda.graph(self.multi_graph):
+                for _ in range(self.graph_steps):
+                    self._body(ids, with_opt=True)
+        finally:
+            self.opt.cursor, self.opt.cursor_mod = None, 1
+        self.opt.iterations = it0
+        self._multi_loss = self.last_loss
+        self._multi_key = (nrows, self._table.shape[1])
+        with torch.no_grad():
+            for k, v in self.model.state_dict().items():
+                v.copy_(snap[k])
+        self.train_metrics.reset()
+        self.opt.zero_grad()
+
+    def train_steps(self, rows: torch.Tensor, start: int, k: int):
+        """``k`` training steps on batches ``rows[(start + i) % len(rows)]`` (rows: [n, B] device
+        ids). With graphs, full chunks of ``graph_steps`` steps replay one multi-step graph each;
+        the rest (and every step when fault injection or DP is on) go through :meth:`train_step`."""
+        nb = int(rows.shape[0])
+        S = self.graph_steps
+        if not self._multi_ok() or k < S:
+            for i in range(k):
+                self.train_step(rows[(start + i) % nb])
+            return self.last_loss
+        self.model.train()
+        if self._table is None or tuple(self._table.shape) != tuple(rows.shape):
+            self._table = torch.empty_like(rows, dtype=torch.long)
+            self.multi_graph = None
+        if self.multi_graph is not None and self._multi_key != (nb, rows.shape[1]):
+            self.multi_graph = None
+        self._table.copy_(rows, non_blocking=True)
+        if self.multi_graph is None:
+            if self.graph is None:
+                self._capture()              # the single-step graph shares the warm allocator state
+            self._capture_multi(nb)
+        self._cursor.fill_(start % nb)
+        n = k // S
+        for _ in range(n):
+            self.multi_graph.replay()
+        self.opt.iterations += n * S
+        self.global_step += n * S
+        self.last_loss = self._multi_loss
+        for i in range(n * S, k):
+            self.train_step(rows[(start + i) % nb])
+        return self.last_loss
 
     def train_step(self, wids: torch.Tensor):
         self.model.train()
@@ -191,6 +269,7 @@ class Trainer:
                 self._capture()
             self.static_wids.copy_(wids, non_blocking=True)
             self.graph.replay()
+            self.last_loss = self._graph_loss
         else:
             self._body(wids.to(self.device), with_opt=not self.split_opt)
         if not self.split_opt:
@@ -227,8 +306,12 @@ class Trainer:
         rejected0 = self._chain_rejected()
         steps0 = self.global_step
         t0 = time.perf_counter()
-        for row in loader.batch_ids():
-            self.train_step(row)
+        rows = loader.batch_ids()
+        if torch.is_tensor(rows) and rows.dim() == 2 and rows.shape[0] > 0 and rows.shape[1] == self.batch_size:
+            self.train_steps(rows, 0, int(rows.shape[0]))
+        else:
+            for row in rows:
+                self.train_step(row)
         D.average_buffers(self.model)                 # DP: BN moving statistics agree on every rank
         logs = self.train_metrics.result()            # device -> host: synchronises the epoch
         dt = time.perf_counter() - t0

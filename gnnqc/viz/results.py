@@ -7,7 +7,14 @@
 * :func:`timeseries_figure` - one classified window (``:95-149``);
 * :func:`plot_classified_samples` - predict + plot validation windows (``:152-177``);
 * :func:`plot_results` - per-sensor strips of TP/TN/FP/FN along time, optional
-  GCN-vs-baseline comparison (``:180-417``).
+  GCN-vs-baseline comparison (``:180-417``);
+* :func:`classified_timeseries_figure` / :func:`plot_classified_timeseries` - a sensor's raw
+  series over ``plot_time_range``-hour intervals, shaded by outcome at every classified step
+  (``xai/libs/visualize.py:17-69, 72-133``);
+* :func:`classified_timeseries_figure_with_neighbours` /
+  :func:`plot_classified_timeseries_with_neighbours` - the flagged sensor and its neighbours
+  stacked, each with the flagged sensor's outcome shading, neighbour distances in the titles
+  (``xai/libs/visualize.py:243-312``).
 
 All figures are written with the non-interactive Agg backend.
 """
@@ -252,4 +259,233 @@ def plot_results(sensor_ids, anomaly_dates, anomaly_flags_pred, anomaly_flags_tr
     return paths
 
 
-__all__ = ["plot_roc_curves", "extract_target_info", "timeseries_figure", "plot_classified_samples", "plot_results"]
+_OUTCOMES = (((1, 1), "green", "True Positive"), ((0, 0), "blue", "True Negative"),
+             ((0, 1), "red", "False Negative"), ((1, 0), "orange", "False Positive"))
+
+
+def _shade(ax, dates, pred, true, lo, hi, alpha, label=True):
+    """Outcome shading at the steps where both flags are defined (NaN elsewhere)."""
+    pred = np.asarray(pred, np.float64)
+    true = np.asarray(true, np.float64)
+    for (p, t), col, name in _OUTCOMES:
+        ax.fill_between(dates, lo, hi, where=(pred == p) & (true == t), alpha=alpha, color=col,
+                        label=name if label else None)
+
+
+def _stamp(d) -> str:
+    return str(np.datetime64(d, "m")).replace(":", "-")
+
+
+def classified_timeseries_figure(sensor_id, features, dates, anomaly_flags_true, anomaly_flags_pred, model_config,
+                                 probabilities=None, outdir=None):
+    """One sensor over one time range: its raw channels (``features``: list of [T] arrays), shaded
+    TP / TN / FN / FP where a window centred on that step was classified (flags NaN elsewhere),
+    optional probability trace on a twin axis. Returns the PNG path."""
+    pl = (model_config.get("plotting") or {}) if model_config is not None else {}
+    alpha = float(pl.get("alpha", 0.2))
+    outdir = outdir or os.path.join(_outdir(model_config), "classified_timeseries_raw")
+    os.makedirs(outdir, exist_ok=True)
+    d = np.asarray(dates).astype("datetime64[m]")
+    dd = d.astype(object)
+    feats = [np.asarray(f, np.float64) for f in features]
+    allv = np.concatenate([f[np.isfinite(f)] for f in feats]) if feats else np.zeros(1)
+    ymin = float(np.floor(allv.min())) if allv.size else 0.0
+    ymax = float(np.ceil(allv.max())) if allv.size else 1.0
+    if ymax <= ymin:
+        ymax = ymin + 1.0
+    fig, ax = plt.subplots(1, 1, figsize=(20, 4))
+    ax.set_ylim([ymin, ymax])
+    _shade(ax, dd, anomaly_flags_pred, anomaly_flags_true, ymin, ymax, alpha)
+    for j, f in enumerate(feats):
+        ax.plot(dd, f, color=LINE_COLORS[j % len(LINE_COLORS)], linewidth=1.5)
+    if probabilities is not None:
+        ax2 = ax.twinx()
+        ax2.set_ylim([0, 1])
+        ax2.plot(dd, np.asarray(probabilities, np.float64), "k", linewidth=0.5, label="probability")
+    ax.set_title(str(sensor_id), pad=10)
+    ax.legend(loc="upper right")
+    ax.margins(x=0.001)
+    outpath = os.path.join(outdir, f"{sensor_id}_start_{_stamp(d[0])}_end_{_stamp(d[-1])}.png")
+    fig.savefig(outpath, bbox_inches="tight")
+    plt.close(fig)
+    return outpath
+
+
+def _predict_windows(model, store, ids, baseline, batch_size=256):
+    import torch
+    preds = []
+    was = model.training
+    model.eval()
+    with torch.no_grad():
+        for s in range(0, len(ids), batch_size):
+            b = store.gather(torch.as_tensor(ids[s:s + batch_size], device=store.device))
+            preds.append(model(b.model_inputs(store.ds_type, baseline)).reshape(b.y.shape).float().cpu().numpy())
+    if was:
+        model.train()
+    pred = np.concatenate(preds)
+    if store.ds_type != "cml":
+        valid = store.win_valid[torch.as_tensor(ids)].cpu().numpy()
+        pred = np.concatenate([p[m > 0] for p, m in zip(pred, valid)])
+    return pred.reshape(-1)
+
+
+def _node_series(windows, sensor_id):
+    """(group, node position) holding ``sensor_id``'s raw series (CML: the group it is flagged in)."""
+    for g in windows.groups:
+        if windows.ds_type == "cml":
+            if str(g.group_id) == str(sensor_id):
+                return g, max(g.anomalous_pos, 0)
+        else:
+            hit = np.nonzero(np.asarray(g.sensor_ids).astype(str) == str(sensor_id))[0]
+            if len(hit):
+                return g, int(hit[0])
+    return None, -1
+
+
+def plot_classified_timeseries(model, store, window_ids, model_config, predictions=None, start_date=None,
+                               end_date=None, baseline: bool = False, threshold: float = 0.5,
+                               interval: Optional[float] = None, max_figures: Optional[int] = None) -> List[str]:
+    """Classify ``window_ids`` (or use ``predictions``, one per :func:`extract_target_info` row) and
+    write, per sensor and ``plotting.plot_time_range``-hour interval, its raw series with the outcome
+    of every window centred in it (``xai/libs/visualize.py:72-133``)."""
+    ids = np.asarray(window_ids, np.int64)
+    pred = np.asarray(predictions, np.float64).reshape(-1) if predictions is not None else \
+        _predict_windows(model, store, ids, baseline)
+    cls = (pred > threshold).astype(np.float64)
+    sids, adates, flags = extract_target_info(store.windows, ids)
+    pl = (model_config.get("plotting") or {}) if model_config is not None else {}
+    interval = float(interval if interval is not None else pl.get("plot_time_range", 144))
+    step = np.timedelta64(int(interval * 60), "m")
+    out_dir = os.path.join(_outdir(model_config), "classified_timeseries_raw" + ("_baseline" if baseline else ""))
+    paths: List[str] = []
+    for sid in np.unique(sids):
+        g, pos = _node_series(store.windows, sid)
+        if g is None:
+            continue
+        sel = np.nonzero(sids == sid)[0]
+        t_lo = np.datetime64(start_date, "m") if start_date is not None else g.time.min()
+        t_hi = np.datetime64(end_date, "m") if end_date is not None else g.time.max()
+        t0 = t_lo
+        while t0 <= t_hi:
+            t1 = t0 + step
+            m = (g.time >= t0) & (g.time <= t1)
+            cur = sel[(adates[sel] >= t0) & (adates[sel] <= t1)]
+            if len(cur) and m.any():
+                plot_dates = g.time[m]
+                pser = np.full(plot_dates.shape[0], np.nan)
+                tser = pser.copy()
+                _, pi, ai = np.intersect1d(plot_dates, adates[cur], return_indices=True)
+                pser[pi] = cls[cur][ai]
+                tser[pi] = flags[cur][ai]
+                feats = [g.features[pos][c][m] for c in range(g.features.shape[1])]
+                if store.ds_type != "cml":
+                    feats = feats[:1]          # soil moisture (the reference plots moisture only)
+                paths.append(classified_timeseries_figure(sid, feats, plot_dates, tser, pser, model_config,
+                                                          outdir=out_dir))
+                if max_figures is not None and len(paths) >= max_figures:
+                    return paths
+            t0 = t1
+    return paths
+
+
+def classified_timeseries_figure_with_neighbours(sensor_ids, all_features_timeseries, feature_timeseries_dates,
+                                                 anomaly_flags_true, anomaly_flags_pred, model_config, flags,
+                                                 probabilities=None, distances=None, ymin=None, ymax=None,
+                                                 outdir=None):
+    """Stacked panels, one per sensor (``all_features_timeseries`` [S, T, C]): each shaded with the
+    flagged sensor's outcomes, the flagged one titled 'Anomalous sensor', the others 'Neighbouring
+    sensor' with their distance. Per-panel y range min - 1 .. min + 24 unless given
+    (``xai/libs/visualize.py:243-312``). Returns the PNG path."""
+    pl = (model_config.get("plotting") or {}) if model_config is not None else {}
+    alpha = float(pl.get("alpha", 0.2))
+    feats = np.asarray(all_features_timeseries, np.float64)
+    S = feats.shape[0]
+    d = np.asarray(feature_timeseries_dates).astype("datetime64[m]")
+    dd = d.astype(object)
+    fig, axes = plt.subplots(S, 1, figsize=(20, S * 3.5), sharex="all", squeeze=False)
+    axes = axes[:, 0]
+    flagged = str(sensor_ids[int(np.argmax(np.asarray(flags)))]) if np.any(flags) else str(sensor_ids[0])
+    fixed = ymin is not None
+    for i in range(S):
+        f = feats[i]
+        lo, hi = (ymin, ymax) if fixed else (float(np.nanmin(f)) - 1.0, float(np.nanmin(f)) + 24.0)
+        if not np.isfinite(lo):
+            lo, hi = 0.0, 25.0
+        ax = axes[i]
+        ax.set_ylim([lo, hi])
+        _shade(ax, dd, anomaly_flags_pred, anomaly_flags_true, lo, hi, alpha, label=i == S - 1)
+        if flags[i]:
+            ax.set_title(f"Anomalous sensor: {sensor_ids[i]}", pad=10, fontweight="bold")
+        elif distances is not None:
+            ax.set_title(f"Neighbouring sensor: {sensor_ids[i]} distance: {float(distances[i]):.1f}", pad=10)
+        else:
+            ax.set_title(f"Neighbouring sensor: {sensor_ids[i]}", pad=10)
+        if probabilities is not None:
+            ax2 = ax.twinx()
+            ax2.set_ylim([0, 1])
+            ax2.plot(dd, np.asarray(probabilities, np.float64), "k", linewidth=0.5, label="probability")
+        for c in range(f.shape[-1]):
+            ax.plot(dd, f[:, c])
+        ax.xaxis.set_major_formatter(mdates.DateFormatter("%Y-%m-%d %H:%M"))
+        if i == S - 1:
+            ax.legend()
+    outdir = outdir or os.path.join(_outdir(model_config), "classification_with_neighbors")
+    os.makedirs(outdir, exist_ok=True)
+    outpath = os.path.join(outdir, f"{flagged}_start_{_stamp(d[0])}_end_{_stamp(d[-1])}_neighbours.png")
+    fig.savefig(outpath, bbox_inches="tight")
+    plt.close(fig)
+    return outpath
+
+
+def plot_classified_timeseries_with_neighbours(model, store, window_ids, model_config, predictions=None,
+                                               baseline: bool = False, threshold: float = 0.5,
+                                               interval: Optional[float] = None,
+                                               max_figures: Optional[int] = 5) -> List[str]:
+    """CML: per flagged sensor and interval, the flagged link and every neighbour of its graph
+    (channels of the raw series), shaded by the flagged link's outcomes, with the classifier's
+    probability trace and the neighbours' distances to the flagged link."""
+    if store.ds_type != "cml":
+        raise ValueError("neighbour figures follow the CML neighbourhood layout (one flagged link per group)")
+    ids = np.asarray(window_ids, np.int64)
+    pred = np.asarray(predictions, np.float64).reshape(-1) if predictions is not None else \
+        _predict_windows(model, store, ids, baseline)
+    cls = (pred > threshold).astype(np.float64)
+    sids, adates, flags_true = extract_target_info(store.windows, ids)
+    pl = (model_config.get("plotting") or {}) if model_config is not None else {}
+    interval = float(interval if interval is not None else pl.get("plot_time_range", 144))
+    step = np.timedelta64(int(interval * 60), "m")
+    paths: List[str] = []
+    for sid in np.unique(sids):
+        g, pos = _node_series(store.windows, sid)
+        if g is None:
+            continue
+        sel = np.nonzero(sids == sid)[0]
+        t0 = adates[sel].min()
+        while t0 <= adates[sel].max():
+            t1 = t0 + step
+            m = (g.time >= t0) & (g.time <= t1)
+            cur = sel[(adates[sel] >= t0) & (adates[sel] <= t1)]
+            if len(cur) and m.any():
+                plot_dates = g.time[m]
+                pser = np.full(plot_dates.shape[0], np.nan)
+                tser = pser.copy()
+                prob = pser.copy()
+                _, pi, ai = np.intersect1d(plot_dates, adates[cur], return_indices=True)
+                pser[pi] = cls[cur][ai]
+                tser[pi] = flags_true[cur][ai]
+                prob[pi] = pred[cur][ai]
+                feats = np.transpose(g.features[:, :, m], (0, 2, 1))          # [S, T, C]
+                fl = np.zeros(g.n_nodes, dtype=bool)
+                fl[pos] = True
+                paths.append(classified_timeseries_figure_with_neighbours(
+                    [str(s) for s in g.sensor_ids], feats, plot_dates, tser, pser, model_config, fl,
+                    probabilities=prob, distances=np.asarray(g.distances)[pos]))
+                if max_figures is not None and len(paths) >= max_figures:
+                    return paths
+            t0 = t1
+    return paths
+
+
+__all__ = ["plot_roc_curves", "extract_target_info", "timeseries_figure", "plot_classified_samples", "plot_results",
+           "classified_timeseries_figure", "plot_classified_timeseries",
+           "classified_timeseries_figure_with_neighbours", "plot_classified_timeseries_with_neighbours"]

@@ -56,6 +56,18 @@ def _frozen(model):
     return _Ctx()
 
 
+def _ig_hip(t: torch.Tensor) -> bool:
+    """The HIP interpolation / accumulation / finalize kernels (csrc/kernels/ig.hip) run for fp32
+    inputs on the GPU; a missing extension on a GPU box fails loudly in hip_ops()."""
+    from ..ops import use_hip
+    return bool(use_hip(t) and t.dtype == torch.float32)
+
+
+def _ops():
+    from ..utils.native import hip_ops
+    return hip_ops()
+
+
 class IntegratedGradients:
     """Alpha-batched IG engine for the GCN / baseline classifiers.
 
@@ -118,37 +130,53 @@ class IntegratedGradients:
             pred = pred_full.gather(1, target[:, None])[:, 0]
         else:
             pred = pred_full[:, 0]
-        alphas = torch.linspace(0.0, 1.0, self.m_steps + 1, device=vals[0].device)
-        wts = trapezoid_weights(self.m_steps, vals[0].device)
-        acc = [torch.zeros_like(v, dtype=torch.float32) for v in vals]
-        path_pred = torch.empty(self.m_steps + 1, B, device=vals[0].device)
+        dev = vals[0].device
+        dt = torch.float64 if vals[0].dtype == torch.float64 else torch.float32
+        alphas = torch.linspace(0.0, 1.0, self.m_steps + 1, device=dev, dtype=dt)
+        wts = trapezoid_weights(self.m_steps, dev).to(dt)
+        acc = [torch.zeros_like(v, dtype=dt) for v in vals]
+        path_pred = torch.empty(self.m_steps + 1, B, device=dev, dtype=dt)
         k = max(1, min(self.m_steps + 1, self.max_rows // max(B, 1)))
+        hip = _ig_hip(vals[0])
+        vf = [v.to(dt).contiguous() for v in vals]
         with _frozen(model), torch.enable_grad():
             for s in range(0, self.m_steps + 1, k):
                 a = alphas[s:s + k]
                 kk = a.numel()
-                # zero baseline: x_alpha = alpha * x, folded into the batch dimension
+                # zero baseline: x_alpha = alpha * x, folded into the batch dimension (HIP: one
+                # ig_interp launch per input tensor for all kk path points)
                 xs = []
-                for v in vals:
-                    shp = (kk,) + (1,) * v.dim()
-                    xi = (a.view(shp) * v.unsqueeze(0).float()).reshape((kk * B,) + tuple(v.shape[1:]))
+                for v in vf:
+                    if hip:
+                        xi = _ops().ig_interp(v, a.contiguous())
+                    else:
+                        shp = (kk,) + (1,) * v.dim()
+                        xi = (a.view(shp) * v.unsqueeze(0)).reshape((kk * B,) + tuple(v.shape[1:]))
                     xs.append(xi.requires_grad_(True))
                 st = [t.repeat((kk,) + (1,) * (t.dim() - 1)) for t in static]
                 out = model(build(xs, st))
                 y = self._select(out, B, kk, target)
                 grads = torch.autograd.grad(y.sum(), xs)
-                path_pred[s:s + kk] = y.detach().view(kk, B)
-                w = wts[s:s + kk]
+                path_pred[s:s + kk] = y.detach().view(kk, B).to(dt)
+                w = wts[s:s + kk].contiguous()
                 for j, g in enumerate(grads):
-                    g = g.view((kk, B) + tuple(g.shape[1:]))
-                    acc[j] += torch.tensordot(w, g, dims=1)
+                    if hip and g.is_contiguous() and g.dtype == torch.float32 and g.data_ptr() % 16 == 0:
+                        _ops().ig_accum(acc[j], g, w)      # trapezoid-weighted sum, one launch
+                    else:
+                        g = g.view((kk, B) + tuple(g.shape[1:]))
+                        acc[j] += torch.tensordot(w, g.to(dt), dims=1)
         model.train(was_training)
-        if self.scale_gradients:
-            acc = [g * v.float() for g, v in zip(acc, vals)]       # (x - baseline) * avg grad
-        if self.negative_values == "abs":
-            acc = [g.abs() for g in acc]
-        elif self.negative_values == "clip":
-            acc = [g.clamp(min=0) for g in acc]
+        mode = {"keep": 0, "clip": 1, "abs": 2}[self.negative_values]
+        if hip:
+            e = vf[0].new_zeros(0)
+            acc = [_ops().ig_finalize(g, v if self.scale_gradients else e, mode) for g, v in zip(acc, vf)]
+        else:
+            if self.scale_gradients:
+                acc = [g * v for g, v in zip(acc, vf)]       # (x - baseline) * avg grad
+            if self.negative_values == "abs":
+                acc = [g.abs() for g in acc]
+            elif self.negative_values == "clip":
+                acc = [g.clamp(min=0) for g in acc]
         res = {"pred": pred, "path_pred": path_pred, "target": target}
         if self.ds_type == "cml":
             if self.is_baseline:

@@ -107,9 +107,9 @@ def main():
     h4, g4, c4, logits, loss = ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e)
     hg = [torch.zeros_like(p) for p in head]
     one = torch.ones(1, device=dev)
-    ub = timeit(lambda: ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], head, y, mask, M, *hc, hg))
+    ub = timeit(lambda: ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg))
     print(json.dumps({"bwd": "head+time4", "us": round(ub, 2), "marks": t4marks(ops, x)}), flush=True)
-    dz4, dxt = ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], head, y, mask, M, *hc, hg)
+    dz4, dxt = ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg)
     e8 = torch.zeros(0, dtype=torch.uint8, device=dev)
     xw = [din] + units[:-1]
     Ts = [outs[5 * i].shape[0] for i in range(6)]
@@ -134,7 +134,7 @@ def main():
     sync[16] = 0
     torch.cuda.synchronize()
     both = timeit(lambda: (ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e),
-                           ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], head, y, mask, M, *hc, hg)))
+                           ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg)))
     print(json.dumps({"time4_head_fwd_bwd_us": round(both, 2)}), flush=True)
     st = ops.lstm_chain_status(x).cpu().tolist()
     print(json.dumps({"status": st}), flush=True)

@@ -1,0 +1,69 @@
+"""Integrated gradients on the GPU (alpha folded into the batch, HIP chain / GCN input-gradient
+kernels, ig_interp / ig_accum / ig_finalize) against the same explainer evaluated in float64 with
+plain PyTorch on the CPU."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("negative_values", ["keep", "abs"])
+def test_ig_gpu_matches_fp64_cpu(cuda_device, cml_windows, negative_values):
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.xai.ig import IntegratedGradients, completeness_gap
+    pc, ws = cml_windows
+    torch.manual_seed(0)
+    mc = C.default("model_cml")
+    model = GCNClassifier(mc, pc).to(cuda_device)
+    with torch.no_grad():                      # a non-trivial output range along the path
+        model.dense_out.bias.fill_(0.3)
+        for p in (model.dense.bias, model.dense2.bias):
+            p.normal_(0, 0.2)
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    st_cpu = DeviceStore(ws, "rolling_median", pc.graph, device="cpu")
+    ids = torch.tensor([0, 7, 19, 33])
+    b = st.gather(ids.to(cuda_device))
+    m = 24
+    got = IntegratedGradients(model, "cml", m_steps=m, negative_values=negative_values).attribute(b)
+    torch.cuda.synchronize()
+
+    ref_model = copy.deepcopy(model).cpu().double()
+    bc = st_cpu.gather(ids)
+    for f in ("x", "anom"):
+        setattr(bc, f, getattr(bc, f).double())
+    ref = IntegratedGradients(ref_model, "cml", m_steps=m, negative_values=negative_values).attribute(bc)
+
+    for k in ("grad_x", "grad_anom", "pred", "path_pred"):
+        a, r = got[k].double().cpu(), ref[k]
+        err = (a - r).norm().item()
+        scale = r.norm().item()
+        assert err <= 6e-2 * scale + 1e-6, (k, err, scale)
+    if negative_values == "keep":
+        # completeness (sum of attributions ~ f(x) - f(0)) holds on the GPU as well as in fp64
+        gap_g = completeness_gap(got).abs().cpu().double()
+        gap_r = completeness_gap(ref).abs()
+        span = (ref["path_pred"][-1] - ref["path_pred"][0]).abs()
+        assert bool((gap_g <= gap_r + 0.05 * span + 2e-3).all()), (gap_g, gap_r, span)
+
+
+def test_ig_hip_kernels_match_torch(cuda_device):
+    from gnnqc.utils.native import hip_ops
+    ops = hip_ops()
+    torch.manual_seed(1)
+    v = torch.randn(5, 37, 3, device=cuda_device)            # numel % 4 != 0: scalar tail
+    a = torch.linspace(0, 1, 7, device=cuda_device)
+    out = ops.ig_interp(v, a)
+    torch.testing.assert_close(out.view(7, 5, 37, 3), a.view(7, 1, 1, 1) * v.unsqueeze(0))
+    g = torch.randn(7 * 5, 37, 3, device=cuda_device)
+    w = torch.rand(7, device=cuda_device)
+    acc = torch.randn(5, 37, 3, device=cuda_device)
+    expect = acc + torch.tensordot(w, g.view(7, 5, 37, 3), dims=1)
+    ops.ig_accum(acc, g, w)
+    torch.testing.assert_close(acc, expect, rtol=1e-5, atol=1e-5)
+    for mode, fn in ((0, lambda t: t), (1, lambda t: t.clamp(min=0)), (2, torch.abs)):
+        torch.testing.assert_close(ops.ig_finalize(acc, v, mode), fn(acc * v))
+    torch.testing.assert_close(ops.ig_finalize(acc, v.new_zeros(0), 0), acc)

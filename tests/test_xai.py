@@ -192,3 +192,32 @@ def test_explainer_shards_partition_batches(cml_small, tmp_path):
     assert a | b == full
     with pytest.raises(ValueError):
         run("2/2", "bad")
+
+
+def test_classified_timeseries_plots(cml_small, tmp_path):
+    """plot_classified_timeseries (raw series shaded per classified step) and the neighbours figure
+    (flagged link + every neighbour of its graph, distances in the titles), from a real model's
+    predictions and from given ones."""
+    from gnnqc.viz import (classified_timeseries_figure_with_neighbours, plot_classified_timeseries,
+                           plot_classified_timeseries_with_neighbours)
+    pc, ws, store = cml_small
+    torch.manual_seed(0)
+    mc = C.default("model_cml")
+    mc["plotting"] = {"outdir": str(tmp_path / "plots"), "alpha": 0.2, "plot_time_range": 24}
+    model = create_model(mc, pc)
+    ids = np.arange(min(120, ws.n_windows))
+    paths = plot_classified_timeseries(model, store, ids, mc, max_figures=3)
+    assert paths and all(os.path.getsize(q) > 0 for q in paths)
+    rng = np.random.default_rng(1)
+    paths2 = plot_classified_timeseries(None, store, ids, mc, predictions=rng.random(len(ids)), max_figures=2)
+    assert paths2 and all(os.path.exists(q) for q in paths2)
+    pn = plot_classified_timeseries_with_neighbours(model, store, ids, mc, max_figures=2)
+    assert pn and all(os.path.getsize(q) > 0 for q in pn) and all("_neighbours.png" in q for q in pn)
+    # direct call: 3 sensors x 50 steps x 2 channels, the middle one flagged
+    d = np.arange("2019-07-01T00:00", "2019-07-01T00:50", dtype="datetime64[m]")
+    feats = rng.normal(size=(3, 50, 2))
+    true = np.where(rng.random(50) > 0.5, 1.0, 0.0)
+    pred = np.where(rng.random(50) > 0.5, 1.0, 0.0)
+    q = classified_timeseries_figure_with_neighbours(["a", "b", "c"], feats, d, true, pred, mc, [False, True, False],
+                                                     probabilities=rng.random(50), distances=[1.5, 0.0, 3.2])
+    assert os.path.getsize(q) > 0 and os.path.basename(q).startswith("b_")
