@@ -178,7 +178,9 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(
     float* __restrict__ vm, float* __restrict__ adj, long* __restrict__ ap, float* __restrict__ y,
     float* __restrict__ ym, float* __restrict__ anom, long* __restrict__ wid_out, int B, int Tw, int Ttot, int Tn,
     int N, int C, int tb, int time_norm, int soil) {
+  // grid (B, NY): workgroup (b, y) cuts slice y of sample b's window; y == 0 also writes the meta
   const int b = blockIdx.x, tid = threadIdx.x;
+  const bool meta = blockIdx.y == 0;
   const long* ids = cursor != nullptr ? table + (cursor[0] % nrows) * B : wids;
   const long wraw = ids[b];
   const long w = wraw < 0 ? 0 : wraw;
@@ -192,13 +194,15 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(
   for (int n = tid; n < N; n += 256) {
     const float v = live * (wv[w * N + n] ? 1.f : 0.f);
     svm[n] = v;
-    vm[(long)b * N + n] = v;
-    if (soil) {
-      y[(long)b * N + n] = wlab[w * N + n] * v;
-      ym[(long)b * N + n] = wlabv[w * N + n] * ok;
+    if (meta) {
+      vm[(long)b * N + n] = v;
+      if (soil) {
+        y[(long)b * N + n] = wlab[w * N + n] * v;
+        ym[(long)b * N + n] = wlabv[w * N + n] * ok;
+      }
     }
   }
-  if (tid == 0) {
+  if (meta && tid == 0) {
     ap[b] = a;
     wid_out[b] = wraw;
     if (!soil) {
@@ -207,9 +211,11 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(
     }
   }
   __syncthreads();
-  const float* A = gadj + g * (long)N * N;
-  float* out = adj + (long)b * N * N;
-  for (int e = tid; e < N * N; e += 256) out[e] = A[e] * svm[e / N] * svm[e % N];
+  if (meta) {
+    const float* A = gadj + g * (long)N * N;
+    float* out = adj + (long)b * N * N;
+    for (int e = tid; e < N * N; e += 256) out[e] = A[e] * svm[e / N] * svm[e % N];
+  }
   const long c0 = wc[w];
   const float* src = series + (g * Ttot + (c0 - tb)) * (long)NC;
   const long tn = time_norm ? c0 : 0;
@@ -217,11 +223,13 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(
   const float* sc = scale + (g * Tn + tn) * (long)NC;
   float* xo = x + (long)b * Tw * NC;
   const int total = Tw * NC;
-  for (int e0 = tid; e0 < total; e0 += 4 * 256) {
+  const int per = ((total + gridDim.y - 1) / gridDim.y + 1023) / 1024 * 1024;
+  const int e_end = min(total, ((int)blockIdx.y + 1) * per);
+  for (int e0 = (int)blockIdx.y * per + tid; e0 < e_end; e0 += 4 * 256) {
     float xv[4], sv[4], cv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = min(e0 + u * 256, total - 1);
+      const int e = min(e0 + u * 256, e_end - 1);
       xv[u] = src[e];
       sv[u] = sh[e % NC];
       cv[u] = sc[e % NC];
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = e0 + u * 256;
-      if (e < total) {
+      if (e < e_end) {
         const int nc = e % NC, n = nc / C;
         const float val = (xv[u] - sv[u]) * cv[u] * svm[n];
         xo[e] = val;
@@ -301,7 +309,9 @@ std::vector<at::Tensor> batch_gather(const at::Tensor& series, const at::Tensor&
   at::Tensor ym = soil ? at::empty({B, N}, fo) : at::empty({B}, fo);
   at::Tensor anom = soil ? at::empty({0}, fo) : at::empty({B, seq_len, C}, fo);
   at::Tensor wid = at::empty({B}, win_group.options());
-  hipLaunchKernelGGL(batch_gather_kernel, dim3(B), dim3(256), 0, stream(), series.data_ptr<float>(),
+  // one round of 4 elements per thread per workgroup: the cut is latency-bound per workgroup
+  const int ny = (int)std::max<long>(1, std::min<long>(((long)seq_len * N * C + 1023) / 1024, 32));
+  hipLaunchKernelGGL(batch_gather_kernel, dim3(B, ny), dim3(256), 0, stream(), series.data_ptr<float>(),
                      shift.data_ptr<float>(), scale.data_ptr<float>(), win_group.data_ptr<long>(),
                      win_center.data_ptr<long>(), win_valid.data_ptr<uint8_t>(), wp, tp, cp, nrows,
                      group_adj.data_ptr<float>(), group_anom_pos.data_ptr<long>(), win_label.data_ptr<float>(),

@@ -42,7 +42,7 @@ def cmd_preprocess(args):
     from .common import load_configs, make_raw
     pc, _ = load_configs(args)
     raw = make_raw(args, pc)
-    if pc.ds_type == "cml" and pc.get("create_nc_files", True):
+    if pc.get("per_sensor", pc.ds_type == "cml") and pc.get("create_nc_files", True):
         paths = create_sensors_ncfiles(raw, pc)
         print(f"wrote {len(paths)} neighbourhood files to {pc.ncfiles_dir}")
     ws = create_windows_dataset(pc, raw=raw)

@@ -171,6 +171,9 @@ def normalize_preproc(cfg: Config) -> Config:
     cfg.setdefault("val_fraction", 0.2)
     cfg.setdefault("interpolate", True)
     cfg.setdefault("split_numb", 5)
+    # SoilNet of the XAI generation: per-anomalous-sensor neighbourhoods (one flagged sensor per
+    # box) instead of one network-wide graph (xai/libs/preprocessing_functions.py:951-1025)
+    cfg.setdefault("per_sensor", cfg.ds_type == "cml")
     cfg.dataset.setdefault("split_numb", cfg.split_numb)
     g = cfg.get("graph")
     if not isinstance(g, Mapping):

@@ -100,8 +100,69 @@ def prepare_soilnet_groups(ds: SensorData, cfg) -> List[SensorGroup]:
                         distances=dist, depths=depths, lat=lat, lon=lon, coords=coords)]
 
 
+def select_sensors(ds: SensorData, seed: int = 44) -> np.ndarray:
+    """One sensor per box: the one with the most moisture observations, ties broken at random
+    (``xai/libs/preprocessing_functions.py:1019-1025``; the reference seeds ``random`` with
+    ``random_state`` in ``create_sensors_ncfiles`` ``:952``). Returns sensor positions."""
+    import random
+    rnd = random.Random(seed)
+    box = np.asarray(ds["box_id"].data)
+    n_obs = (~np.isnan(np.asarray(ds["moisture"].data, np.float64))).sum(axis=1)
+    out = []
+    for b in np.unique(box):             # xarray groupby order: sorted box ids
+        pos = np.nonzero(box == b)[0]
+        best = pos[n_obs[pos] == n_obs[pos].max()]
+        out.append(int(rnd.choice(list(best))))
+    return np.asarray(out, np.int64)
+
+
+def prepare_soilnet_sensor_groups(ds: SensorData, cfg) -> List[SensorGroup]:
+    """SoilNet of the XAI generation (``create_sensors_ncfiles`` ``xai/libs/preprocessing_functions.py:
+    951-1016``): for one selected sensor per box, its depth-aware neighbourhood (same-depth sensors
+    within ``max_sample_distance`` and the co-located sensors within ``graph.max_depth`` of depth,
+    ``get_neighbors``), with that sensor's target series and the neighbourhood's distances and depth
+    differences. Group ids are ``<box>_<sensor>`` like the reference's file names."""
+    cfg = normalize_preproc(cfg)
+    lat_all = np.asarray(ds["latitude"].data, np.float64)
+    lon_all = np.asarray(ds["longitude"].data, np.float64)
+    keep = ~(np.isnan(lat_all) | np.isnan(lon_all))
+    ds = ds.isel(sensor_id=np.nonzero(keep)[0])
+    time = ds.time
+    flagged = select_sensors(ds, int(cfg.get("random_state", 44)))
+    feats = []
+    for name in SOIL_FEATURES:
+        v = np.array(ds[name].data, dtype=np.float32)
+        if cfg.interpolate:
+            v = _interp(v, time, np.timedelta64(60, "m"))
+        feats.append(v)
+    X = np.stack(feats, axis=1)
+    target = create_target(ds, ds_type="soilnet", flags_type=cfg.get("flags_type", "manual"))
+    dist = compute_distance_matrix(ds, "soilnet", unit=cfg.get("distance_unit", "m"))
+    depths = compute_depth_matrix(ds)
+    lat, lon = sensor_positions(ds, "soilnet")
+    ids = ds.sensor_ids
+    box = np.asarray(ds["box_id"].data)
+    max_dist = cfg.graph.max_sample_distance
+    max_depth = cfg.graph.get("max_depth", cfg.graph.max_neighbour_depth)
+    groups = []
+    for s in flagged:
+        nb = get_neighbors(dist, s, max_dist, "soilnet", depths=depths, max_depth=max_depth)
+        coords = {k: np.asarray(ds[k].data)[nb] for k in ("box_id", "level_id", "depth") if k in ds}
+        groups.append(SensorGroup(
+            group_id=f"{box[s]}_{ids[s]}", ds_type="soilnet", sensor_ids=ids[nb],
+            anomalous_pos=int(np.nonzero(nb == s)[0][0]), feature_names=list(SOIL_FEATURES),
+            features=np.ascontiguousarray(X[nb]), time=time, target=target[s].astype(np.float32),
+            distances=dist[np.ix_(nb, nb)], depths=depths[np.ix_(nb, nb)], lat=lat[nb], lon=lon[nb],
+            coords=coords))
+    return groups
+
+
 def prepare_groups(ds: SensorData, cfg) -> List[SensorGroup]:
-    return prepare_cml_groups(ds, cfg) if cfg["ds_type"] == "cml" else prepare_soilnet_groups(ds, cfg)
+    if cfg["ds_type"] == "cml":
+        return prepare_cml_groups(ds, cfg)
+    if cfg.get("per_sensor", False):
+        return prepare_soilnet_sensor_groups(ds, cfg)
+    return prepare_soilnet_groups(ds, cfg)
 
 
 def add_statistics(groups: List[SensorGroup], cfg, normalization: Optional[str] = None):
@@ -127,13 +188,14 @@ def group_to_sensordata(g: SensorGroup) -> SensorData:
         ds.set_coord("lon", "sensor_id", g.lon)
     for i, n in enumerate(g.feature_names):
         ds[n] = (("sensor_id", "time"), g.features[:, i, :])
-    if g.ds_type == "cml":
-        ds["target"] = ("time", g.target.astype(bool))
+    if g.per_sensor:
+        ds["target"] = ("time", g.target.astype(bool) if g.ds_type == "cml" else g.target.astype(np.float32))
         flagged = np.zeros(g.n_nodes, bool)
         flagged[g.anomalous_pos] = True
         ds["flagged"] = ("sensor_id", flagged)
     else:
         ds["target"] = (("sensor_id", "time"), g.target.astype(np.float32))
+    if g.depths is not None:
         ds["depths"] = (("sensor_id", "sensor_id1"), g.depths)
     ds["distances"] = (("sensor_id", "sensor_id1"), g.distances)
     return ds
@@ -144,15 +206,14 @@ def sensordata_to_group(ds: SensorData) -> SensorGroup:
     names = CML_FEATURES if ds_type == "cml" else SOIL_FEATURES
     X = np.stack([np.asarray(ds[n].data, np.float32) for n in names], axis=1)
     coords = {k: v.data for k, v in ds.coords.items() if k not in ("sensor_id", "time", "lat", "lon")}
-    if ds_type == "cml":
+    if "flagged" in ds:                  # a flagged-sensor neighbourhood (CML, XAI SoilNet)
         flagged = np.asarray(ds["flagged"].data, bool)
         anom = int(np.nonzero(flagged)[0][0])
-        target = np.asarray(ds["target"].data, bool)
-        depths = None
+        target = np.asarray(ds["target"].data, bool if ds_type == "cml" else np.float32)
     else:
         anom = -1
         target = np.asarray(ds["target"].data, np.float32)
-        depths = np.asarray(ds["depths"].data)
+    depths = np.asarray(ds["depths"].data) if "depths" in ds else None
     return SensorGroup(group_id=str(ds.attrs.get("anomalous_sensor_id", "group")), ds_type=ds_type,
                        sensor_ids=ds.sensor_ids, anomalous_pos=anom, feature_names=list(names), features=X,
                        time=ds.time, target=target, distances=np.asarray(ds["distances"].data), depths=depths,
@@ -161,7 +222,8 @@ def sensordata_to_group(ds: SensorData) -> SensorGroup:
 
 
 def create_sensors_ncfiles(ds: SensorData, preproc_config) -> List[str]:
-    """Write one NetCDF per neighbourhood into ``ncfiles_dir`` (``:79-120``)."""
+    """Write one NetCDF per neighbourhood into ``ncfiles_dir`` (``:79-120``; XAI SoilNet:
+    ``<box>_<sensor>.nc`` per selected sensor, ``xai/libs/preprocessing_functions.py:1005-1016``)."""
     cfg = normalize_preproc(preproc_config)
     out_dir = cfg.ncfiles_dir
     os.makedirs(out_dir, exist_ok=True)
@@ -188,7 +250,7 @@ def create_windows_dataset(preproc_config, groups: Optional[List[SensorGroup]] =
     if groups is None:
         if raw is not None:
             groups = prepare_groups(raw, cfg)
-        elif cfg.ds_type == "cml":
+        elif cfg.get("per_sensor", cfg.ds_type == "cml"):
             groups = load_sensor_groups(cfg)
         else:
             groups = prepare_groups(read_netcdf(cfg.raw_dataset_path), cfg)
@@ -236,7 +298,7 @@ def load_dataset(preproc_config, windows: WindowSet):
     """(train_ids, val_ids, test_ids) window-id arrays (``:485-563``)."""
     cfg = normalize_preproc(preproc_config)
     days = windows.window_days()
-    if windows.ds_type == "cml":
+    if windows.ds_type == "cml":            # (SoilNet of both generations: monthly random split)
         tr, va, te = chronological_split(days, cfg.train_fraction, cfg.val_fraction,
                                          cfg.timestep_before, cfg.timestep_after)
     else:
@@ -284,7 +346,8 @@ def create_batched_dataset(window_ids, preproc_config, store, shuffle: bool = Tr
 
 
 __all__ = [
-    "prepare_cml_groups", "prepare_soilnet_groups", "prepare_groups", "add_statistics",
+    "prepare_cml_groups", "prepare_soilnet_groups", "prepare_soilnet_sensor_groups", "select_sensors",
+    "prepare_groups", "add_statistics",
     "create_sensors_ncfiles", "load_sensor_groups", "create_windows_dataset", "create_tfrecords_dataset",
     "load_dataset", "load_dataset_CV", "create_batched_dataset", "group_to_sensordata", "sensordata_to_group",
 ]

@@ -40,14 +40,17 @@ class Batch:
     y: torch.Tensor                   # [B] (CML) or [B, N] (SoilNet) float labels
     y_mask: torch.Tensor              # [B] or [B, N] float: which labels count
     wid: torch.Tensor                 # [B] window ids (-1 = padding)
+    per_sensor: Optional[bool] = None  # flagged-sensor neighbourhoods (CML, XAI SoilNet); None: CML only
 
     def to(self, device, non_blocking=True):
         return Batch(**{k: (v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v)
                         for k, v in dataclasses.asdict(self).items()})
 
     def model_inputs(self, ds_type: str, baseline: bool = False):
-        """Input tuple in the spirit of the reference's wrapper functions (``:743-768``)."""
-        if ds_type == "cml":
+        """Input tuple in the spirit of the reference's wrapper functions (``:743-768``; XAI
+        SoilNet per-sensor batches: ``xai/libs/preprocessing_functions.py:667-707, 791-802``)."""
+        per_sensor = self.per_sensor if self.per_sensor is not None else ds_type == "cml"
+        if per_sensor:
             if baseline:
                 return (self.anom,)
             return (self.x, self.anom, self.adj, self.node_mask, self.anom_pos)
@@ -116,6 +119,7 @@ class DeviceStore:
                  feature_dtype=torch.float32):
         self.windows = windows
         self.ds_type = windows.ds_type
+        self.per_sensor = windows.per_sensor
         self.normalization = normalization
         self.device = torch.device(device)
         G = len(windows.groups)
@@ -159,7 +163,7 @@ class DeviceStore:
         self.win_center = torch.from_numpy(centers).to(dev)
         self.win_valid = torch.from_numpy(valid).to(dev)
         self.win_valid_u8 = self.win_valid.to(torch.uint8).contiguous()
-        if self.ds_type == "cml":
+        if self.per_sensor:
             lab = np.concatenate([ix.labels for ix in windows.indices]).astype(np.float32)
             self.win_label = torch.from_numpy(lab).to(dev)
             self.win_label_valid = None
@@ -209,8 +213,8 @@ class DeviceStore:
                 self.series, self.shift, self.scale, self.win_group, self.win_center, self.win_valid_u8, *args,
                 self.group_adj, self.group_anom_pos, self.win_label, lv, vs, self.tb, self.seq_len,
                 self.time_varying_norm)
-            return Batch(x=x, adj=adj, node_mask=vm, anom=anom if self.ds_type == "cml" else None, anom_pos=ap,
-                         y=y, y_mask=y_mask, wid=wid)
+            return Batch(x=x, adj=adj, node_mask=vm, anom=anom if self.per_sensor else None, anom_pos=ap,
+                         y=y, y_mask=y_mask, wid=wid, per_sensor=self.per_sensor)
         if cur is not None:
             wids = cur.table[cur.cursor[0] % cur.table.shape[0]]
         wids = wids.to(dev)
@@ -231,7 +235,7 @@ class DeviceStore:
         sample_ok = (~pad).to(x.dtype)
         if valid_sample is not None:
             sample_ok = sample_ok * valid_sample.to(x.dtype)
-        if self.ds_type == "cml":
+        if self.per_sensor:
             idx = ap.clamp(min=0)
             anom = x[torch.arange(x.shape[0], device=dev), :, idx]   # [B, T, C]
             y = self.win_label[w] * sample_ok
@@ -240,7 +244,8 @@ class DeviceStore:
             anom = None
             y = self.win_label[w] * vm
             y_mask = self.win_label_valid[w] * sample_ok[:, None]
-        return Batch(x=x, adj=adj, node_mask=vm, anom=anom, anom_pos=ap, y=y, y_mask=y_mask, wid=wids)
+        return Batch(x=x, adj=adj, node_mask=vm, anom=anom, anom_pos=ap, y=y, y_mask=y_mask, wid=wids,
+                     per_sensor=self.per_sensor)
 
 
 class DeviceLoader:

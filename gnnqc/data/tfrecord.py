@@ -242,7 +242,7 @@ def window_example(ws, gi: int, li: int, graph_cfg=None) -> bytes:
     c = int(ix.center[li])
     t0, t1 = c - tb, c - tb + T
     nodes = np.nonzero(ix.node_valid[li])[0]
-    if g.ds_type == "cml" and g.anomalous_pos not in nodes:
+    if g.per_sensor and g.anomalous_pos not in nodes:
         nodes = np.sort(np.append(nodes, g.anomalous_pos))
     feats = g.features[nodes][:, :, t0:t1]                    # [n, C, T]
     dist = g.distances[np.ix_(nodes, nodes)]
@@ -277,6 +277,25 @@ def window_example(ws, gi: int, li: int, graph_cfg=None) -> bytes:
                         "cml_b_lon": "cml_lon_b"}[name]
                 row = feature_float(np.asarray(g.coords[key], np.float32)[nodes])
                 lists[name] = [row] * T                           # ``coordinates_featurelist``
+    elif g.per_sensor:
+        # XAI-generation SoilNet neighbourhood (xai/libs/preprocessing_functions.py:218-240): the
+        # selected sensor's id, series and window label as context, every node's series as lists
+        ap = int(np.nonzero(nodes == g.anomalous_pos)[0][0])
+        sid = np.asarray(g.sensor_ids)
+        ctx["anomaly_ID"] = feature_int64([int(sid[g.anomalous_pos])])
+        ctx["sensor_ids"] = feature_int64(sid[nodes].astype(np.int64))
+        ctx["anomaly_flag"] = feature_int64([int(ix.labels[li])])
+        for ci, name in enumerate(g.feature_names):
+            ctx[f"{name}_anomalous_sensor"] = feature_float(feats[ap, ci])
+            for s in _STATS:
+                ctx[f"{name}_{s}"] = feature_float(_stat(g, f"{name}_{s}", nodes))
+            for s in _ROLL:
+                ctx[f"{name}_rolling_{s}"] = feature_float(_stat(g, f"{name}_rolling_{s}", nodes, c))
+            lists[name] = _fl_rows(feats[:, ci].T)
+        lists["depths"] = _fl_scalars_f(dep[adj] if dep is not None else np.zeros(len(src)))
+        if g.lat is not None:
+            lists["sensor_lat"] = [feature_float(np.asarray(g.lat, np.float32)[nodes])] * T
+            lists["sensor_lon"] = [feature_float(np.asarray(g.lon, np.float32)[nodes])] * T
     else:
         for ci, name in enumerate(g.feature_names):
             for s in _STATS:
@@ -331,6 +350,14 @@ def parse_window_example(buf: bytes, ds_type: str) -> Dict[str, object]:
         anom_id = ctx["anomaly_ID"][0].decode()
         out.update(features=feats, ids=ids, anom_pos=ids.index(anom_id) if anom_id in ids else 0,
                    label=int(ctx["anomaly_flag"][0]))
+    elif "anomaly_ID" in ctx:          # XAI SoilNet per-sensor record (parse_soilnet_tfrecord_fn :419-509)
+        chans = ["moisture", "temp", "battv"]
+        feats = np.stack([np.stack(lists[c], 1) for c in chans], 1)
+        ids = [int(v) for v in ctx["sensor_ids"]]
+        aid = int(ctx["anomaly_ID"][0])
+        out.update(features=feats, ids=ids, anom_pos=ids.index(aid) if aid in ids else 0,
+                   label=int(ctx["anomaly_flag"][0]),
+                   anom_series=np.stack([np.asarray(ctx[f"{c}_anomalous_sensor"], np.float32) for c in chans], 0))
     else:
         chans = ["moisture", "temp", "battv"]
         feats = np.stack([np.stack(lists[c], 1) for c in chans], 1)
@@ -394,12 +421,15 @@ class TFRecordWindows:
         N = max_nodes or max(r["features"].shape[0] for r in recs)
         C, T = recs[0]["features"].shape[1:]
         W = len(recs)
+        # one label per window (CML, XAI SoilNet) vs one per node (network-wide SoilNet)
+        self.per_sensor = ds_type == "cml" or "label" in recs[0]
+        per = self.per_sensor
         self.x = np.zeros((W, T, N, C), np.float32)
         self.adj = np.zeros((W, N, N), np.float32)
         self.mask = np.zeros((W, N), np.float32)
         self.anom_pos = np.full(W, -1, np.int64)
-        self.y = np.zeros((W,) if ds_type == "cml" else (W, N), np.float32)
-        self.y_mask = np.ones((W,), np.float32) if ds_type == "cml" else np.zeros((W, N), np.float32)
+        self.y = np.zeros((W,) if per else (W, N), np.float32)
+        self.y_mask = np.ones((W,), np.float32) if per else np.zeros((W, N), np.float32)
         for i, r in enumerate(recs):
             f = r["features"]
             n = f.shape[0]
@@ -409,7 +439,7 @@ class TFRecordWindows:
             self.adj[i, r["src"], r["dst"]] = 1.0
             self.mask[i, :n] = 1.0
             self.anom_pos[i] = r["anom_pos"]
-            if ds_type == "cml":
+            if per:
                 self.y[i] = r["label"]
             else:
                 self.y[i, :n] = r["labels"]
@@ -431,7 +461,7 @@ class TFRecordWindows:
             x = self.x[take] * ok[:, None, None, None]
             mask = self.mask[take] * ok[:, None]
             anom = None
-            if self.ds_type == "cml":
+            if self.per_sensor:
                 ap = np.clip(self.anom_pos[take], 0, None)
                 anom = x[np.arange(len(take)), :, ap]
                 y, ym = self.y[take] * ok, ok
@@ -440,7 +470,7 @@ class TFRecordWindows:
             wid = np.concatenate([idx, np.full(pad, -1)]).astype(np.int64)
             yield Batch(x=t(x), adj=t(self.adj[take] * mask[:, :, None] * mask[:, None, :]), node_mask=t(mask),
                         anom=t(anom) if anom is not None else None, anom_pos=t(self.anom_pos[take]), y=t(y),
-                        y_mask=t(ym), wid=t(wid))
+                        y_mask=t(ym), wid=t(wid), per_sensor=self.per_sensor)
 
 
 __all__ = ["TFRecordWriter", "read_tfrecord", "encode_sequence_example", "decode_sequence_example",

@@ -52,6 +52,12 @@ class SensorGroup:
     def n_time(self) -> int:
         return int(self.time.shape[0])
 
+    @property
+    def per_sensor(self) -> bool:
+        """One flagged sensor + its neighbours with that sensor's target series (CML, and the XAI
+        generation's SoilNet neighbourhoods) vs a network-wide graph with per-node targets."""
+        return self.anomalous_pos >= 0 and np.ndim(self.target) == 1
+
 
 @dataclasses.dataclass
 class WindowIndex:
@@ -91,10 +97,13 @@ def build_window_index(group: SensorGroup, group_pos: int, timestep_before: int,
     lo, hi = centers - tb, centers + ta
     nan_any = np.isnan(group.features).any(axis=1)          # [N, Ttot]
     bad = _nan_window_any(nan_any, lo, hi)                   # [W, N]
-    if group.ds_type == "cml":
+    if group.per_sensor:
         keep = ~bad[:, group.anomalous_pos]
+        tgt = np.asarray(group.target)
+        if tgt.dtype.kind == "f":                           # SoilNet (XAI): unlabelled steps are NaN
+            keep &= np.isfinite(tgt[centers])
         centers, bad = centers[keep], bad[keep]
-        labels = group.target[centers].astype(np.int8)
+        labels = (np.nan_to_num(tgt[centers].astype(np.float64)) > 0.5).astype(np.int8)
         return WindowIndex(group_pos, centers.astype(np.int64), ~bad, labels)
     # SoilNet
     tgt = group.target[:, centers].T                         # [W, N]
@@ -120,6 +129,10 @@ class WindowSet:
     timestep_before: int
     timestep_after: int
     freq: int
+
+    @property
+    def per_sensor(self) -> bool:
+        return bool(self.groups) and all(g.per_sensor for g in self.groups)
 
     @property
     def seq_len(self) -> int:
@@ -148,14 +161,14 @@ class WindowSet:
 
     def window_keys(self) -> np.ndarray:
         days = self.window_days().astype(str)
-        if self.ds_type == "cml":
+        if self.per_sensor:
             gid = np.concatenate([np.full(ix.size, self.groups[ix.group].group_id, dtype=object)
                                   for ix in self.indices])
             return np.array([f"{a}_{b}" for a, b in zip(gid, days)])
         return days
 
     def labels_flat(self) -> np.ndarray:
-        if self.ds_type == "cml":
+        if self.per_sensor:
             return np.concatenate([ix.labels for ix in self.indices])
         return np.concatenate([ix.labels for ix in self.indices], axis=0)
 

@@ -29,6 +29,9 @@ class BaselineClassifier(nn.Module):
         mc, pc = model_config, preprocessing_config
         self.model_config = mc
         self.ds_type = pc["ds_type"]
+        # per-sensor data (CML; XAI SoilNet, xai/libs/preprocessing_functions.py:791-802): the model
+        # sees the flagged sensor's series only; network-wide SoilNet: every node's series
+        self.per_sensor = bool(pc.get("per_sensor", self.ds_type == "cml"))
         self.freq = freq_minutes(self.ds_type)
         self.input_feature_numb = 2 if self.ds_type == "cml" else 3
         self.timestep_before, self.timestep_after = int(pc["timestep_before"]), int(pc["timestep_after"])
@@ -54,7 +57,7 @@ class BaselineClassifier(nn.Module):
         self.dense_out = Dense(units, 1)
 
     def temporal_input(self, inputs) -> torch.Tensor:
-        if self.ds_type == "cml":
+        if self.per_sensor:
             return inputs[0]
         x = inputs[0]
         return graph_reshape(x)
@@ -76,7 +79,7 @@ class BaselineClassifier(nn.Module):
 
     def logits(self, inputs) -> torch.Tensor:
         z = self.head(self.time_layer(self.temporal_input(inputs)))
-        if self.ds_type == "soilnet":
+        if not self.per_sensor:
             x = inputs[0]
             z = z.view(x.shape[0], x.shape[2])
         return z

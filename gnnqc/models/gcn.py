@@ -63,6 +63,8 @@ class GCNClassifier(nn.Module):
         mc, pc = model_config, preprocessing_config
         self.model_config = mc
         self.ds_type = pc["ds_type"]
+        # flagged-sensor neighbourhoods (CML; SoilNet of the XAI generation) vs network-wide SoilNet
+        self.per_sensor = bool(pc.get("per_sensor", self.ds_type == "cml"))
         self.freq = freq_minutes(self.ds_type)
         self.timestep_before, self.timestep_after = int(pc["timestep_before"]), int(pc["timestep_after"])
         self.batch_size = int(pc["batch_size"])
@@ -131,8 +133,9 @@ class GCNClassifier(nn.Module):
                 and (self.pooling_type == "selection" or self.aggregation_type in ("mean", "sum")))
 
     def temporal_input(self, inputs) -> torch.Tensor:
-        """Everything before the TimeLayer: CML [B,T,Ca+F]; SoilNet [B*N,T,F+C]."""
-        if self.ds_type == "cml":
+        """Everything before the TimeLayer: per-sensor (CML, XAI SoilNet) [B,T,Ca+F]; network-wide
+        SoilNet [B*N,T,F+C]."""
+        if self.per_sensor:
             x, anom, adj, mask, anom_pos = inputs[:5]
             coords = inputs[5] if len(inputs) > 5 else None
             feats = self._node_features(x, mask, coords)
@@ -152,7 +155,7 @@ class GCNClassifier(nn.Module):
 
     def _soil_fused(self, inputs) -> bool:
         """SoilNet fast path: fused per-node GCN kernel writing the time-major LSTM input."""
-        if self.ds_type != "soilnet" or not self._fused_ok():
+        if self.per_sensor or not self._fused_ok():
             return False
         if self.sensors_time_layer is not None or self.spatial_transformer is not None:
             return False
@@ -170,7 +173,7 @@ class GCNClassifier(nn.Module):
 
     def _cml_time_major(self, inputs) -> bool:
         """CML fast path: the fused GCN + pooling kernel writes the time-major LSTM input."""
-        if self.ds_type != "cml" or not self._fused_ok() or self.sensors_time_layer is not None:
+        if not self.per_sensor or not self._fused_ok() or self.sensors_time_layer is not None:
             return False
         if self.spatial_transformer is not None or len(inputs) > 5:
             return False
@@ -213,7 +216,7 @@ class GCNClassifier(nn.Module):
         weighted BCE and the metric accumulation (``gnnqc.ops.lstm.lstm_chain_head_tm``).
         None when the configuration is not the one those kernels implement."""
         spec = self.head_spec()
-        if spec is None or self.ds_type != "cml" or not self._cml_time_major(inputs):
+        if spec is None or not self.per_sensor or not self._cml_time_major(inputs):
             return None
         if any(d.kernel.shape[1] != 64 for d in spec[:2]) or spec[2].kernel.shape != (64, 1):
             return None
@@ -235,7 +238,7 @@ class GCNClassifier(nn.Module):
 
     def logits(self, inputs) -> torch.Tensor:
         z = self.head(self.features(inputs))
-        if self.ds_type == "soilnet":
+        if not self.per_sensor:
             B, N = inputs[0].shape[0], inputs[0].shape[2]
             z = z.view(B, N)
         return z

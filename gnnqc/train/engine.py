@@ -377,7 +377,7 @@ def predict(model, store, loader, baseline: bool = False, gather_all: bool = Tru
     if gather_all:
         p, y, m, w = (D.all_gather_var(t) for t in (p, y, m, w))
     out = {"p": p.cpu().numpy(), "y": y.cpu().numpy(), "mask": m.cpu().numpy(), "wid": w.cpu().numpy()}
-    if store.ds_type == "soilnet":
+    if not store.per_sensor:
         N = out["p"].shape[1]
         out["node"] = np.broadcast_to(np.arange(N), out["p"].shape).copy()
     return out

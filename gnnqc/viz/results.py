@@ -95,7 +95,7 @@ def extract_target_info(windows, window_ids, timeseries_out: bool = False, store
         g, ix = windows.groups[gi], windows.indices[gi]
         c = int(ix.center[li])
         t = g.time[c - tb:c - tb + T]
-        if windows.ds_type == "cml":
+        if windows.per_sensor:
             sensor_ids.append(str(g.group_id))
             dates.append(g.time[c])
             flags.append(int(ix.labels[li]))
@@ -171,7 +171,7 @@ def plot_classified_samples(model, store, window_ids, model_config, preproc_conf
             preds.append(model(b.model_inputs(store.ds_type, baseline)).reshape(b.y.shape).float().cpu().numpy())
     pred = np.concatenate(preds)
     sids, _, flags, series, sdates = extract_target_info(store.windows, ids, timeseries_out=True)
-    if store.ds_type != "cml":
+    if not store.per_sensor:
         pred = np.concatenate([p[m > 0] for p, m in zip(pred, store.win_valid[torch.as_tensor(ids)].cpu().numpy())])
     cls = (pred.reshape(-1) > threshold).astype(int)
     tb = int(round(store.windows.timestep_before / store.windows.freq))
@@ -323,7 +323,7 @@ def _predict_windows(model, store, ids, baseline, batch_size=256):
     if was:
         model.train()
     pred = np.concatenate(preds)
-    if store.ds_type != "cml":
+    if not store.per_sensor:
         valid = store.win_valid[torch.as_tensor(ids)].cpu().numpy()
         pred = np.concatenate([p[m > 0] for p, m in zip(pred, valid)])
     return pred.reshape(-1)
@@ -332,7 +332,7 @@ def _predict_windows(model, store, ids, baseline, batch_size=256):
 def _node_series(windows, sensor_id):
     """(group, node position) holding ``sensor_id``'s raw series (CML: the group it is flagged in)."""
     for g in windows.groups:
-        if windows.ds_type == "cml":
+        if windows.per_sensor:
             if str(g.group_id) == str(sensor_id):
                 return g, max(g.anomalous_pos, 0)
         else:
@@ -444,8 +444,8 @@ def plot_classified_timeseries_with_neighbours(model, store, window_ids, model_c
     """CML: per flagged sensor and interval, the flagged link and every neighbour of its graph
     (channels of the raw series), shaded by the flagged link's outcomes, with the classifier's
     probability trace and the neighbours' distances to the flagged link."""
-    if store.ds_type != "cml":
-        raise ValueError("neighbour figures follow the CML neighbourhood layout (one flagged link per group)")
+    if not store.per_sensor:
+        raise ValueError("neighbour figures need flagged-sensor neighbourhoods (CML, XAI SoilNet)")
     ids = np.asarray(window_ids, np.int64)
     pred = np.asarray(predictions, np.float64).reshape(-1) if predictions is not None else \
         _predict_windows(model, store, ids, baseline)

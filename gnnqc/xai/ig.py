@@ -95,11 +95,13 @@ class IntegratedGradients:
         self.scale_gradients = scale_gradients
         self.negative_values = negative_values
         self.is_baseline = type(model).__name__ == "BaselineClassifier"
+        # flagged-sensor inputs (CML, XAI SoilNet) vs network-wide SoilNet
+        self.per_sensor = bool(getattr(model, "per_sensor", ds_type == "cml"))
 
     # -- inputs that are interpolated ------------------------------------------------
     def _split(self, batch):
         """(interpolated tensors, static tensors, rebuild fn)."""
-        if self.ds_type == "cml":
+        if self.per_sensor:
             if self.is_baseline:
                 return [batch.anom], [], lambda v, s: (v[0],)
             return ([batch.x, batch.anom], [batch.adj, batch.node_mask, batch.anom_pos],
@@ -178,7 +180,7 @@ class IntegratedGradients:
             elif self.negative_values == "clip":
                 acc = [g.clamp(min=0) for g in acc]
         res = {"pred": pred, "path_pred": path_pred, "target": target}
-        if self.ds_type == "cml":
+        if self.per_sensor:
             if self.is_baseline:
                 res["grad_anom"] = acc[0]
             else:
@@ -373,7 +375,7 @@ class IntegratedGradientsExplainer:
         thr = float(self.ig_cfg.threshold)
         pred = res["pred"].detach().float().cpu().numpy()
         pred_cls = (pred > thr).astype(int)
-        if self.ds_type == "cml":
+        if batch.y.dim() == 1:                   # one label per window (per-sensor data)
             true = batch.y.detach().cpu().numpy().astype(int)
         else:
             t = res.get("target")
