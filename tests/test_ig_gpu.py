@@ -33,7 +33,7 @@ def test_ig_gpu_matches_fp64_cpu(cuda_device, cml_windows, negative_values):
 
     ref_model = copy.deepcopy(model).cpu().double()
     bc = st_cpu.gather(ids)
-    for f in ("x", "anom"):
+    for f in ("x", "anom", "adj", "node_mask"):
         setattr(bc, f, getattr(bc, f).double())
     ref = IntegratedGradients(ref_model, "cml", m_steps=m, negative_values=negative_values).attribute(bc)
 
