@@ -131,6 +131,26 @@ class _Pipe:
     batch = []      # jobs of a chain backward: all gradient passes in one launch at the flush
 
 
+def _grads_side_on() -> bool:
+    """Chain-backward weight-gradient passes on a side stream, concurrent with the rest of the
+    backward (the GCN's), joined before the optimiser (``GNNQC_GRADS_SIDE``, default OFF).
+    Measured 0.3788 vs 0.3812 ms/step (CML, graph replay: the branches mostly serialise), and
+    with the overlap the deterministic-mode bitwise test failed after the kernel tests had run in
+    the same process while it passed with the side stream ordered after the GCN backward
+    (GNNQC_GRADS_SIDE_LATE=1): not worth an unexplained hazard."""
+    import os
+    return os.environ.get("GNNQC_GRADS_SIDE", "0") == "1"
+
+
+def _grads_stream(device: torch.device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _DirectGrad.streams.get(idx)
+    if st is None:
+        st = torch.cuda.Stream(device=idx)
+        _DirectGrad.streams[idx] = st
+    return idx, st
+
+
 # Largest sequence count (rows of 16-sequence tiles) a recurrence may have for its layer to
 # join the pipe: the gradient workgroups only help when the recurrence leaves most CUs idle
 # (CML: 8 tiles). With hundreds of tiles (SoilNet: 418) they compete with the recurrence
@@ -181,11 +201,33 @@ def pipe_flush():
         from ..utils.native import hip_ops
         grads = ([_Pipe.job] if _Pipe.job is not None else []) + _Pipe.batch
         reds = ([_Pipe.red] if _Pipe.red is not None else []) + grads
-        hip_ops().lstm_grads_multi([j["dz"] for j in grads], [j["x"] for j in grads], [j["h"] for j in grads],
-                                   [j["W"] for j in grads], [j["period"] for j in grads],
-                                   [j["hshift"] for j in grads], [j["ws"] for j in grads],
-                                   [r["ws"] for r in reds], [r["W"] for r in reds], [r["g"][0] for r in reds],
-                                   [r["g"][1] for r in reds], [r["g"][2] for r in reds])
+
+        def launch():
+            hip_ops().lstm_grads_multi([j["dz"] for j in grads], [j["x"] for j in grads], [j["h"] for j in grads],
+                                       [j["W"] for j in grads], [j["period"] for j in grads],
+                                       [j["hshift"] for j in grads], [j["ws"] for j in grads],
+                                       [r["ws"] for r in reds], [r["W"] for r in reds], [r["g"][0] for r in reds],
+                                       [r["g"][1] for r in reds], [r["g"][2] for r in reds])
+        # every batched job carries the event recorded after ITS chain backward (never a stale one)
+        ev = grads[0].get("ready")
+        if (ev is not None and all(j.get("ready") is ev for j in grads) and _Pipe.job is None
+                and _Pipe.red is None and _grads_side_on()):
+            # the passes only need the chain backward's dz: they run on a side stream from that
+            # point, concurrent with the GCN backward the current stream has queued since; the
+            # context exit joins the side stream (a graph fork / join under capture)
+            dev = grads[0]["dz"].device
+            idx, st = _grads_stream(dev)
+            import os
+            if os.environ.get("GNNQC_GRADS_SIDE_LATE", "0") == "1":
+                st.wait_stream(torch.cuda.current_stream(dev))      # (diagnostic: no overlap)
+            else:
+                st.wait_event(ev)
+            with torch.cuda.stream(st):
+                launch()
+            _DirectGrad.keep.extend(t for j in reds for t in (j["dz"], j["x"], j["h"], j["W"], j["ws"]))
+            _DirectGrad.pending.add(idx)
+        else:
+            launch()
         _Pipe.job, _Pipe.red, _Pipe.batch = None, None, []
     while _Pipe.job is not None or _Pipe.red is not None:
         _pipe_drain_one()
@@ -402,6 +444,10 @@ class _HipLSTMChain(torch.autograd.Function):
                                      [outs[5 * i + 4] if pools[i] else e8 for i in order],
                                      [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
                                      [outs[5 * i].shape[0] for i in order])
+            ready = None
+            if x.is_cuda and _grads_side_on():
+                ready = torch.cuda.Event()          # the dz of every layer are final from here
+                ready.record()
             for k, i in enumerate(order):
                 nw = need[2 + 3 * i:5 + 3 * i]
                 if not any(nw):
@@ -411,7 +457,9 @@ class _HipLSTMChain(torch.autograd.Function):
                 sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
                 if (_pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
                         and len(_Pipe.batch) < _MULTI_MAX - 2):
-                    _Pipe.batch.append(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
+                    job = _pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1])
+                    job["ready"] = ready
+                    _Pipe.batch.append(job)
                 else:
                     ops.lstm_tm_grads(res[k], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
                 grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]
@@ -522,6 +570,10 @@ class _HipLSTMChainHead(torch.autograd.Function):
             dx = res[ns]
             return (dx if need[0] else None, None, None, None, None, None, None, None, *grads, *hgrads)
         res = ops.lstm_chain_bwd(dxt, *chain_args)
+        ready = None
+        if x.is_cuda and _grads_side_on():
+            ready = torch.cuda.Event()          # the dz of every layer are final from here
+            ready.record()
         dzs = {ns: dz4}
         hs = {ns: h4}
         for k, i in enumerate(order):
@@ -536,7 +588,9 @@ class _HipLSTMChainHead(torch.autograd.Function):
             sk = sinks[i]
             if (_pipe_on(sk, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
                     and len(_Pipe.batch) < _MULTI_MAX - 2):
-                _Pipe.batch.append(_pipe_job(dzs[i], xi, h, Ws[i], sk, h.shape[0] * h.shape[1], h.shape[1]))
+                job = _pipe_job(dzs[i], xi, h, Ws[i], sk, h.shape[0] * h.shape[1], h.shape[1])
+                job["ready"] = ready
+                _Pipe.batch.append(job)
             else:
                 ops.lstm_tm_grads(dzs[i], xi, h, Ws[i], sk[0][0], sk[1][0], sk[2][0], False)
             grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sk, nw)]

@@ -62,6 +62,10 @@ def main():
     sinks = [torch.zeros_like(t) for t in (W, b, gamma, beta, alpha)]
     res["gcn_bwd_finalize"] = timeit(lambda: ops.gcn_bwd_finalize(acc, S, W, b, st, True, *sinks))
     res["acc_rows"] = acc.shape[0]
+    tiny = torch.zeros(16, device=dev)
+    res["floor_tiny_add"] = timeit(lambda: tiny.add_(1.0))                  # a trivial one-workgroup kernel
+    big = torch.zeros(1 << 20, device=dev)
+    res["floor_4MB_add"] = timeit(lambda: big.add_(1.0))
     print(json.dumps(res), flush=True)
 
 
