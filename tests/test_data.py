@@ -237,3 +237,28 @@ def test_tfrecord_crc_detects_corruption(tmp_path):
     open(p, "wb").write(bytes(raw))
     with pytest.raises(ValueError):
         list(read_tfrecord(p))
+
+
+def test_soilnet_spatial_faults_are_locally_plausible():
+    """The neighbour-only fault types of the SoilNet generator (missed / phantom wetting) stay
+    within the sensor's own range and trip none of the automatic range / spike flags: only the
+    neighbours reveal them (the mechanism behind the reference's GCN > baseline)."""
+    import numpy as np
+    from gnnqc.data.synthetic import make_soilnet_raw
+    ds = make_soilnet_raw(n_boxes=8, n_time=60 * 96, seed=4, spatial_fault_frac=1.0)
+    m = np.asarray(ds["moisture"].data, np.float64)
+    man = np.asarray(ds["moisture_flag_Manual"].data, bool)
+    assert man.mean() > 0.02
+    rng_flag = np.asarray(ds["moisture_flag_Auto:Range"].data, bool)
+    spike = np.asarray(ds["moisture_flag_Auto:Spike"].data, bool)
+    assert not (man & rng_flag).any()
+    assert (man & spike).sum() <= 0.01 * man.sum()
+    site = m[~man & np.isfinite(m)]
+    lo, hi = site.min(), site.max()
+    seg = m[man & np.isfinite(m)]
+    assert seg.min() >= lo - 2 and seg.max() <= hi + 5      # inside the site's normal range
+    for i in range(m.shape[0]):                              # and above each sensor's own floor
+        ok = ~man[i] & np.isfinite(m[i])
+        if man[i].any() and ok.any():
+            s_ = m[i, man[i]]
+            assert np.nanmin(s_) >= np.nanmin(m[i, ok]) - 2
