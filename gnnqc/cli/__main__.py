@@ -137,7 +137,8 @@ def cmd_cv(args):
     for baseline in kinds:
         s = run_cv(pc, mc, ws, folds=args.folds, baseline=baseline, store=store, seed=args.seed,
                    gap_days=args.gap_days, log_path=args.log, max_folds=args.max_folds,
-                   fold_ids=[int(v) for v in args.fold_ids.split(",")] if args.fold_ids else None)
+                   fold_ids=[int(v) for v in args.fold_ids.split(",")] if args.fold_ids else None,
+                   fold_per_rank=args.fold_per_gpu)
         out[s["model"]] = s
         if D.is_main():
             print(json.dumps({"model": s["model"], "mean_auc": round(s["mean_auc"], 4), "std_auc": round(s["std_auc"], 4),
@@ -187,6 +188,8 @@ def main(argv=None):
     p.add_argument("--gap-days", type=int, default=None)
     p.add_argument("--max-folds", type=int, default=None, help="only run the first K folds")
     p.add_argument("--fold-ids", default=None, help="comma list: only run these folds (e.g. 0,1)")
+    p.add_argument("--fold-per-gpu", action="store_true",
+                   help="with N processes: each GPU trains its own folds (no DP all-reduce); results merged")
     p.add_argument("--out", default=None)
     p.add_argument("--log", default=None)
     p.set_defaults(fn=cmd_cv)

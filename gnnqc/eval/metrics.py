@@ -154,7 +154,7 @@ def auc_from_hist(hist: np.ndarray) -> float:
         return float("nan")
     tpr = np.r_[0, np.cumsum(pos)] / P
     fpr = np.r_[0, np.cumsum(neg)] / N
-    return float(np.trapz(tpr, fpr))
+    return float(np.trapezoid(tpr, fpr))
 
 
 def keras_metrics_from_counts(tp, tn, fp, fn) -> Dict[str, float]:

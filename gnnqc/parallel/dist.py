@@ -18,6 +18,8 @@ import datetime
 import os
 from typing import List, Optional
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -30,12 +32,45 @@ def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+_LOCAL = [False]
+
+
 def world_size() -> int:
-    return dist.get_world_size() if is_initialized() else 1
+    """Ranks that share the current work (1 inside :func:`local`)."""
+    return 1 if _LOCAL[0] else (dist.get_world_size() if is_initialized() else 1)
 
 
 def rank() -> int:
+    return 0 if _LOCAL[0] else (dist.get_rank() if is_initialized() else 0)
+
+
+def global_world_size() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def global_rank() -> int:
     return dist.get_rank() if is_initialized() else 0
+
+
+@contextlib.contextmanager
+def local():
+    """Run independent per-rank work (e.g. one CV fold per GPU): inside, every collective of this
+    module is a no-op and the rank sees a world of one, so a Trainer built here never all-reduces."""
+    prev = _LOCAL[0]
+    _LOCAL[0] = True
+    try:
+        yield
+    finally:
+        _LOCAL[0] = prev
+
+
+def all_gather_object(obj):
+    """Every rank's ``obj`` (a list in rank order; [obj] without a process group)."""
+    if not is_initialized() or global_world_size() == 1:
+        return [obj]
+    out = [None] * global_world_size()
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def is_main() -> bool:
@@ -68,7 +103,7 @@ def destroy():
 
 
 def barrier():
-    if is_initialized():
+    if is_initialized() and not _LOCAL[0]:
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
@@ -145,4 +180,5 @@ def max_over_ranks(x: float) -> float:
 
 
 __all__ = ["init_distributed", "destroy", "barrier", "all_reduce_", "broadcast_", "broadcast_module", "average_buffers",
-           "all_gather_var", "max_over_ranks", "world_size", "rank", "is_main", "is_initialized", "env_world"]
+           "all_gather_var", "max_over_ranks", "world_size", "rank", "is_main", "is_initialized", "env_world",
+           "local", "all_gather_object", "global_world_size", "global_rank"]

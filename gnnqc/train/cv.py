@@ -29,9 +29,14 @@ from .fit import train_model
 def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, baseline: bool = False,
            device="cpu", seed: int = 0, store: Optional[DeviceStore] = None, gap_days: Optional[int] = None,
            verbose: int = 1, log_path: Optional[str] = None, max_folds: Optional[int] = None,
-           fold_ids: Optional[List[int]] = None) -> Dict:
+           fold_ids: Optional[List[int]] = None, fold_per_rank: bool = False) -> Dict:
     """``fold_ids`` runs only those folds (e.g. to spread a CV over several jobs; merge
-    the per-fold JSONL lines with :func:`summarize_folds`)."""
+    the per-fold JSONL lines with :func:`summarize_folds`).
+
+    ``fold_per_rank`` (one process per GPU): instead of data-parallel training of every fold,
+    rank r trains folds r, r + world, ... on its own GPU with no collective in its steps (the
+    folds are independent - 5 folds on 8 GPUs finish in one fold's time, no all-reduce at all);
+    the per-fold results are gathered on every rank at the end."""
     pc = preproc_config
     mc = model_config
     k = int(folds or pc.get("split_numb", 5))
@@ -39,11 +44,22 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
     pc.dataset["split_numb"] = k
     norm = pc.get("normalization") or ("rolling_median" if windows.ds_type == "cml" else "scale_range")
     store = store or DeviceStore(windows, norm, pc.graph, device=device)
-    rank, world = D.rank(), D.world_size()
     results: List[Dict] = []
     todo = list(range(min(k, int(max_folds)) if max_folds else k))
     if fold_ids is not None:
         todo = [int(f) for f in fold_ids if 0 <= int(f) < k]
+    if fold_per_rank and D.global_world_size() > 1:
+        mine = todo[D.global_rank()::D.global_world_size()]
+        with D.local():
+            part = run_cv(pc, mc, windows, k, baseline, device, seed, store, gap_days, verbose, None, None,
+                          mine if mine else [], False)["per_fold"] if mine else []
+        merged = sorted((r for chunk in D.all_gather_object(part) for r in chunk), key=lambda r: r["fold"])
+        if log_path and D.is_main():
+            with open(log_path, "a") as f:
+                for r in merged:
+                    f.write(json.dumps(r) + "\n")
+        return summarize_folds(merged, "baseline" if baseline else "gcn", windows.ds_type, k)
+    rank, world = D.rank(), D.world_size()
     for fold in todo:
         t0 = time.time()
         tr, te, pcf = load_dataset_CV(pc, windows, fold, gap_days=gap_days)

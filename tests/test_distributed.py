@@ -179,3 +179,38 @@ def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world):
         assert np.array_equal(ps[r], ps[0])
         assert np.allclose(bs[r], bs[0], rtol=0, atol=1e-12)
     assert not np.array_equal(ps[0], p0[0])
+
+
+def _cv_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import json
+    from gnnqc.parallel import dist as D
+    from gnnqc.train.cv import run_cv
+    D.init_distributed(device="cpu")
+    pc, mc, st = _gcn_setup()
+    mc["epochs"] = 1
+    s = run_cv(pc, mc, st.windows, folds=3, store=st, seed=5, verbose=0, fold_per_rank=True)
+    with open(os.path.join(out_dir, f"cv{rank}.json"), "w") as f:
+        json.dump({"folds_run": s["folds_run"], "auc": [r["auc"] for r in s["per_fold"]],
+                   "loss": [r["final_train_loss"] for r in s["per_fold"]]}, f)
+    D.destroy()
+
+
+def test_cv_fold_per_rank(tmp_path):
+    """``cv --fold-per-gpu``: 2 ranks train 3 folds between them (rank 0: folds 0, 2; rank 1: fold 1)
+    without any collective in the steps; every rank ends with all folds, identical to running the
+    folds one by one in a single process."""
+    import json
+    port = _free_port()
+    mp.spawn(_cv_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    a = json.load(open(tmp_path / "cv0.json"))
+    b = json.load(open(tmp_path / "cv1.json"))
+    assert a == b and a["folds_run"] == [0, 1, 2]
+    from gnnqc.train.cv import run_cv
+    pc, mc, st = _gcn_setup()
+    mc["epochs"] = 1
+    ref = run_cv(pc, mc, st.windows, folds=3, store=st, seed=5, verbose=0)
+    assert np.allclose([r["final_train_loss"] for r in ref["per_fold"]], a["loss"], rtol=1e-5)
+    assert np.allclose([r["auc"] for r in ref["per_fold"]], a["auc"], rtol=1e-6, equal_nan=True)
