@@ -1,0 +1,90 @@
+"""Data parallelism on the GPU box (one MI355X): two ranks on cuda:0 over gloo (the RCCL code
+path of gnnqc.parallel.dist / Trainer with a different backend; RCCL itself needs one GPU per rank)
+train the CML GCN through the HIP kernels - per-layer LSTM kernels, as two processes' cross-CU
+chain kernels would share one device - and end with identical parameters; plus an RCCL (nccl)
+process group of one rank doing the Trainer's collectives."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r'''
+import os, sys, json
+sys.path.insert(0, os.environ["GNNQC_ROOT"])
+import numpy as np, torch
+from gnnqc import config as C
+from gnnqc.data.preprocessing import create_windows_dataset
+from gnnqc.data.store import DeviceLoader, DeviceStore
+from gnnqc.data.synthetic import make_cml_raw
+from gnnqc.models import GCNClassifier
+from gnnqc.ops.optim import make_optimizer
+from gnnqc.parallel import dist as D
+from gnnqc.train.engine import Trainer
+backend = os.environ["BACKEND"]
+torch.cuda.set_device(0)
+torch.distributed.init_process_group(backend, init_method="env://")
+rank, world = D.rank(), D.world_size()
+dev = torch.device("cuda", 0)
+pc = C.normalize_preproc(C.default("preprocessing_cml"))
+pc.timestep_before, pc.timestep_after = 60, 30
+ws = create_windows_dataset(pc, raw=make_cml_raw(n_sensors=10, n_minutes=3 * 1440, seed=5))
+st = DeviceStore(ws, "rolling_median", pc.graph, device=dev)
+torch.manual_seed(100 + rank)
+m = GCNClassifier(C.default("model_cml"), pc).to(dev)
+opt = make_optimizer("adam", m.parameters(), 1e-3)
+D.broadcast_module(m)
+t = Trainer(m, st, opt, {0: 1.0, 1: 5.0}, use_graph=True, batch_size=32)
+x = torch.ones(4, device=dev) * (rank + 1)
+D.all_reduce_(x)
+loader = DeviceLoader(st, list(range(min(st.n_windows, 32 * 4 * world))), 32, shuffle=True, seed=2, rank=rank,
+                      world_size=world, drop_last=True)
+logs = t.train_epoch(loader, 0)
+torch.cuda.synchronize()
+bufs = torch.cat([b.reshape(-1).double() for b in m.buffers() if b.is_floating_point()])
+out = {"sum": float(x[0]), "p": opt.flat_p.double().sum().item(), "p2": (opt.flat_p.double() ** 2).sum().item(),
+       "b": bufs.sum().item(), "steps": t.global_step, "loss": logs["loss"], "skipped": logs["skipped_steps"]}
+with open(os.path.join(os.environ["OUT"], f"r{rank}.json"), "w") as f:
+    json.dump(out, f)
+torch.distributed.destroy_process_group()
+'''
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(tmp_path, world, backend):
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world),
+                   LOCAL_RANK=str(r), BACKEND=backend, OUT=str(tmp_path), GNNQC_ROOT=ROOT, GNNQC_CHAIN="0",
+                   GNNQC_HEAD_CHAIN="0", GNNQC_CHAIN_BWD="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, "-c", WORKER], env=env))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    import json
+    return [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+
+
+def test_dp_two_ranks_one_gpu_identical_parameters(tmp_path):
+    a, b = _run(tmp_path, 2, "gloo")
+    assert a["sum"] == b["sum"] == 3.0
+    assert a["steps"] == b["steps"] == 4 and a["skipped"] == b["skipped"] == 0
+    assert a["p"] == b["p"] and a["p2"] == b["p2"], "ranks must apply the same all-reduced update"
+    assert abs(a["b"] - b["b"]) <= 1e-9 * abs(a["b"]), "BN moving statistics averaged at epoch end"
+    assert a["loss"] == b["loss"]
+
+
+def test_rccl_process_group_single_rank(tmp_path):
+    (a,) = _run(tmp_path, 1, "nccl")
+    assert a["sum"] == 1.0 and a["steps"] == 4 and a["skipped"] == 0
