@@ -100,6 +100,7 @@ def main(argv=None):
         # Adam); chunks of trainer.graph_steps of them replay one multi-step HIP graph
         trainer.train_steps(rows, start, k)
 
+    trainer.prepare_graphs(rows)              # graph captures happen here, never inside the timed steps
     run(args.warmup, 0)
     trainer._comm_events = []
     D.barrier()

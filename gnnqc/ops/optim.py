@@ -67,6 +67,12 @@ class FlatOptimizer:
         # multi-step graphs (gnnqc.train.engine): a device batch cursor the update advances
         self.cursor: Optional[torch.Tensor] = None
         self.cursor_mod = 1
+        from . import use_hip
+        if use_hip(self.flat_p):
+            # the chain control words the guard reads are allocated now: a first use inside a
+            # graph capture (a model without the chain kernels) would be refused
+            from .lstm import chain_ctl
+            chain_ctl(dev)
 
     @property
     def skipped_steps(self) -> int:

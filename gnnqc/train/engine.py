@@ -220,6 +220,21 @@ class Trainer:
         self.train_metrics.reset()
         self.opt.zero_grad()
 
+    def prepare_graphs(self, rows: torch.Tensor):
+        """Capture the step graphs for batches drawn from ``rows`` now (outside any timed region):
+        the single-step graph and, when multi-step replay applies, the multi-step graph."""
+        if not self.use_graph:
+            return
+        if self.graph is None:
+            self._capture()
+        if self._multi_ok():
+            if self._table is None or tuple(self._table.shape) != tuple(rows.shape):
+                self._table = torch.empty_like(rows, dtype=torch.long)
+                self.multi_graph = None
+            self._table.copy_(rows)
+            if self.multi_graph is None or self._multi_key != (int(rows.shape[0]), rows.shape[1]):
+                self._capture_multi(int(rows.shape[0]))
+
     def train_steps(self, rows: torch.Tensor, start: int, k: int):
         """``k`` training steps on batches ``rows[(start + i) % len(rows)]`` (rows: [n, B] device
         ids). With graphs, full chunks of ``graph_steps`` steps replay one multi-step graph each;
