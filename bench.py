@@ -115,8 +115,11 @@ def main(argv=None):
     dt = D.max_over_ranks(dt)
     loss = float(trainer.last_loss.item())
     comm_us = None
-    if trainer._comm_events:             # N > 1: HIP events around the first timed all-reduces
+    if trainer._comm_events:             # N > 1, eager layout: HIP events around the timed all-reduces
         comm_us = 1e3 * sum(a.elapsed_time(b) for a, b in trainer._comm_events) / len(trainer._comm_events)
+    elif trainer.collective:             # in-graph all-reduce: the same collective timed on its own, after
+        comm_us = trainer.measure_allreduce()
+    if comm_us is not None:
         comm_us = D.max_over_ranks(comm_us)
     windows = args.steps * args.batch * world
     value = windows / dt
@@ -155,6 +158,8 @@ def main(argv=None):
         }
         if comm_us is not None:
             out["allreduce_us"] = round(comm_us, 2)        # mean RCCL all-reduce of the flat gradients
+            out["allreduce_mode"] = ("in-graph (timed standalone)" if trainer.dp_graph and trainer._multi_ok()
+                                     else "eager")
         print(json.dumps(out), flush=True)
     D.destroy()
 

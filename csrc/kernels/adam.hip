@@ -343,9 +343,28 @@ at::Tensor nonfinite_count(const at::Tensor& x) {
   return out;
 }
 
+// Data parallel: a chain spin timeout on ONE rank must reject the step on EVERY rank. Before the
+// gradient all-reduce, a rank whose chain timed out (ext[2] != 0) writes NaN into g[0]; the SUM
+// spreads it and every rank's guard skips the step (the local guard still counts the timeout).
+__global__ void chain_poison_kernel(float* __restrict__ g, const int* __restrict__ ext) {
+  if (threadIdx.x == 0 && __hip_atomic_load(ext + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    g[0] = __builtin_nanf("");
+}
+
+void chain_poison(at::Tensor g, const at::Tensor& ext) {
+  check_f32_cuda(g, "g");
+  TORCH_CHECK(ext.is_cuda() && ext.scalar_type() == at::kInt && ext.numel() >= 4 && ext.get_device() == g.get_device(),
+              "chain_poison: ext must be int32[4] on the gradient's device");
+  TORCH_CHECK(g.numel() >= 1, "chain_poison: empty gradient buffer");
+  c10::DeviceGuard guard(g.device());
+  hipLaunchKernelGGL(chain_poison_kernel, dim3(1), dim3(64), 0, stream(), g.data_ptr<float>(), ext.data_ptr<int>());
+  GQ_LAUNCH_CHECK();
+}
+
 }  // namespace gq
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("chain_poison", &gq::chain_poison);
   m.impl("adam_step", &gq::adam_step);
   m.impl("nonfinite_count", &gq::nonfinite_count);
   m.impl("grad_guard", &gq::grad_guard);

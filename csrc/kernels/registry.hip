@@ -98,6 +98,7 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("ig_interp(Tensor v, Tensor alpha) -> Tensor");
   m.def("ig_accum(Tensor(a!) acc, Tensor g, Tensor w) -> ()");
   m.def("ig_finalize(Tensor acc, Tensor v, int mode) -> Tensor");
+  m.def("chain_poison(Tensor(a!) g, Tensor ext) -> ()");
   m.def("grad_guard(Tensor g, Tensor(a!) state, Tensor(b!) step, Tensor(c!)? ext=None) -> ()");
   // metrics (metrics.hip)
   m.def("score_histogram(Tensor scores, Tensor labels, Tensor mask, int bins) -> Tensor");

@@ -110,8 +110,16 @@ def barrier():
             dist.barrier()
 
 
-def all_reduce_(t: torch.Tensor, op=None) -> torch.Tensor:
-    if is_initialized() and world_size() > 1:
+def backend() -> Optional[str]:
+    """The default process group's backend ("nccl" = RCCL on ROCm, "gloo"); None without one
+    (or inside :func:`local`)."""
+    return dist.get_backend() if is_initialized() and not _LOCAL[0] else None
+
+
+def all_reduce_(t: torch.Tensor, op=None, force: bool = False) -> torch.Tensor:
+    """In-place all-reduce (SUM by default). ``force``: issue the collective even on a one-rank
+    process group (exercises the RCCL / graph-capture path on a single GPU)."""
+    if is_initialized() and not _LOCAL[0] and (world_size() > 1 or force):
         dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
     return t
 
@@ -181,4 +189,4 @@ def max_over_ranks(x: float) -> float:
 
 __all__ = ["init_distributed", "destroy", "barrier", "all_reduce_", "broadcast_", "broadcast_module", "average_buffers",
            "all_gather_var", "max_over_ranks", "world_size", "rank", "is_main", "is_initialized", "env_world",
-           "local", "all_gather_object", "global_world_size", "global_rank"]
+           "local", "all_gather_object", "global_world_size", "global_rank", "backend"]

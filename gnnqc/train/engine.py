@@ -89,9 +89,18 @@ class Trainer:
         self.batch_size = int(batch_size)
         self.train_metrics = MetricAccumulator(self.device)
         self.graph = None
+        # the step's gradient collective: with more than one rank, or forced on a one-rank process
+        # group (GNNQC_DP_FORCE_COLLECTIVE=1: exercises the captured RCCL path on one GPU)
+        self.collective = self.world > 1 or (os.environ.get("GNNQC_DP_FORCE_COLLECTIVE", "0") == "1"
+                                             and D.is_initialized())
         # DP (or GNNQC_SPLIT_OPT_GRAPH=1): the optimizer runs after the all-reduce, so it
         # is captured as a second small graph instead of being launched eagerly each step
-        self.split_opt = self.world > 1 or os.environ.get("GNNQC_SPLIT_OPT_GRAPH", "0") == "1"
+        self.split_opt = self.collective or os.environ.get("GNNQC_SPLIT_OPT_GRAPH", "0") == "1"
+        # DP over RCCL: the all-reduce is captured INSIDE the multi-step graph (gather -> forward ->
+        # backward -> chain-timeout poison -> all-reduce -> guarded Adam, graph_steps times per
+        # replay): no host round trip per step. gloo (host collectives) stays eager per step.
+        self.dp_graph = (self.collective and self.use_graph and D.backend() == "nccl"
+                         and os.environ.get("GNNQC_DP_GRAPH", "1") == "1")
         self.opt_graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
         self.last_loss = torch.zeros((), device=self.device)
@@ -186,8 +195,38 @@ class Trainer:
         self.opt.zero_grad()
 
     def _multi_ok(self) -> bool:
-        return (self.use_graph and not self.split_opt and self.fault is None and self.graph_steps > 1
-                and getattr(self.opt, "zero_grad_in_step", False) and self.opt.guard)
+        return (self.use_graph and (not self.split_opt or self.dp_graph) and self.fault is None
+                and self.graph_steps > 1 and getattr(self.opt, "zero_grad_in_step", False) and self.opt.guard)
+
+    def _reduce_grads(self):
+        """The DP gradient collective: a rank whose LSTM chain timed out this step poisons its
+        gradient first (so every rank's guard rejects the step), then ONE SUM all-reduce of the
+        flat 753 KB buffer. Not bucketed and not overlapped with the backward on purpose: the
+        cross-CU chain kernels assume no other kernel shares the device while they run, and a
+        single small collective is latency-bound on xGMI, so splitting it only adds latency."""
+        if self.device.type == "cuda":
+            from ..ops.lstm import chain_ctl
+            from ..utils.native import hip_ops
+            hip_ops().chain_poison(self.opt.flat_g, chain_ctl(self.device))
+        D.all_reduce_(self.opt.flat_g, force=True)
+
+    @torch.no_grad()
+    def measure_allreduce(self, n: int = 20) -> Optional[float]:
+        """Mean time (us) of the step's gradient all-reduce run on its own (HIP events around each
+        of ``n`` eager collectives); for the in-graph DP layout, whose collectives cannot be timed
+        one by one. The gradient buffer is zero between steps (Adam clears it), so this changes
+        nothing."""
+        if not self.collective or self.device.type != "cuda":
+            return None
+        D.all_reduce_(self.opt.flat_g, force=True)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for a, b in ev:
+            a.record()
+            D.all_reduce_(self.opt.flat_g, force=True)
+            b.record()
+        torch.cuda.synchronize()
+        self.opt.zero_grad()
+        return 1e3 * sum(a.elapsed_time(b) for a, b in ev) / n
 
     def _capture_multi(self, nrows: int):
         """Capture ``graph_steps`` full training steps (gather -> forward -> backward -> guarded
@@ -200,15 +239,25 @@ class Trainer:
         with torch.cuda.stream(s):
             for _ in range(2):
                 self._body(ids, with_opt=False)
+                if self.dp_graph:
+                    self._reduce_grads()          # (communicator + RCCL state warm before capture)
         torch.cuda.current_stream().wait_stream(s)
         self.opt.zero_grad()
         self.multi_graph = torch.cuda.CUDAGraph()
         it0 = self.opt.iterations
         self.opt.cursor, self.opt.cursor_mod = self._cursor, nrows
+        # (thread-local capture mode: the process group's watchdog thread keeps polling its own
+        # events while this thread captures)
+        kw = {"capture_error_mode": "thread_local"} if self.dp_graph else {}
         try:
-            with torch.cuda.graph(self.multi_graph):
+            with torch.cuda.graph(self.multi_graph, **kw):
                 for _ in range(self.graph_steps):
-                    self._body(ids, with_opt=True)
+                    if self.dp_graph:
+                        self._body(ids, with_opt=False)
+                        self._reduce_grads()
+                        self.opt.step(grad_scale=1.0 / self.world)
+                    else:
+                        self._body(ids, with_opt=True)
         finally:
             self.opt.cursor, self.opt.cursor_mod = None, 1
         self.opt.iterations = it0
@@ -291,17 +340,17 @@ class Trainer:
             self.opt.iterations += int(self.use_graph)
             return
         # data parallel: one all-reduce of the flat gradient buffer, then Adam
-        if self.world > 1:
+        if self.collective:
             with _rf("gnnqc.allreduce"):
                 if self.device.type == "cuda":
                     if len(self._comm_events) < 64:      # sample the first steps of an epoch
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
-                        D.all_reduce_(self.opt.flat_g)
+                        self._reduce_grads()
                         e1.record()
                         self._comm_events.append((e0, e1))
                     else:
-                        D.all_reduce_(self.opt.flat_g)
+                        self._reduce_grads()
                 else:
                     D.all_reduce_(self.opt.flat_g)
         with _rf("gnnqc.optimizer"):

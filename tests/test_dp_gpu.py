@@ -41,13 +41,15 @@ D.broadcast_module(m)
 t = Trainer(m, st, opt, {0: 1.0, 1: 5.0}, use_graph=True, batch_size=32)
 x = torch.ones(4, device=dev) * (rank + 1)
 D.all_reduce_(x)
-loader = DeviceLoader(st, list(range(min(st.n_windows, 32 * 4 * world))), 32, shuffle=True, seed=2, rank=rank,
+nb = int(os.environ.get("NB", "4"))
+loader = DeviceLoader(st, list(range(min(st.n_windows, 32 * nb * world))), 32, shuffle=True, seed=2, rank=rank,
                       world_size=world, drop_last=True)
 logs = t.train_epoch(loader, 0)
 torch.cuda.synchronize()
 bufs = torch.cat([b.reshape(-1).double() for b in m.buffers() if b.is_floating_point()])
 out = {"sum": float(x[0]), "p": opt.flat_p.double().sum().item(), "p2": (opt.flat_p.double() ** 2).sum().item(),
-       "b": bufs.sum().item(), "steps": t.global_step, "loss": logs["loss"], "skipped": logs["skipped_steps"]}
+       "b": bufs.sum().item(), "steps": t.global_step, "loss": logs["loss"], "skipped": logs["skipped_steps"],
+       "dp_graph": bool(t.dp_graph), "multi": bool(t.multi_graph is not None), "ar_us": t.measure_allreduce()}
 with open(os.path.join(os.environ["OUT"], f"r{rank}.json"), "w") as f:
     json.dump(out, f)
 torch.distributed.destroy_process_group()
@@ -62,13 +64,16 @@ def _port():
     return p
 
 
-def _run(tmp_path, world, backend):
+def _run(tmp_path, world, backend, chain=False, **extra):
     port = _port()
+    tmp_path.mkdir(parents=True, exist_ok=True)
     procs = []
     for r in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world),
-                   LOCAL_RANK=str(r), BACKEND=backend, OUT=str(tmp_path), GNNQC_ROOT=ROOT, GNNQC_CHAIN="0",
-                   GNNQC_HEAD_CHAIN="0", GNNQC_CHAIN_BWD="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   LOCAL_RANK=str(r), BACKEND=backend, OUT=str(tmp_path), GNNQC_ROOT=ROOT,
+                   HSA_ENABLE_IPC_MODE_LEGACY="0", **extra)
+        if not chain:          # two processes' co-resident chain grids cannot share one device
+            env.update(GNNQC_CHAIN="0", GNNQC_HEAD_CHAIN="0", GNNQC_CHAIN_BWD="0")
         procs.append(subprocess.Popen([sys.executable, "-c", WORKER], env=env))
     for p in procs:
         assert p.wait(timeout=240) == 0
@@ -88,3 +93,16 @@ def test_dp_two_ranks_one_gpu_identical_parameters(tmp_path):
 def test_rccl_process_group_single_rank(tmp_path):
     (a,) = _run(tmp_path, 1, "nccl")
     assert a["sum"] == 1.0 and a["steps"] == 4 and a["skipped"] == 0
+
+
+def test_rccl_all_reduce_captured_in_multistep_graph(tmp_path):
+    """The DP layout over RCCL with the gradient all-reduce INSIDE the multi-step HIP graph (forced
+    collective on a one-rank nccl group, chain kernels on): it must capture, replay, and train like
+    the same process without a collective (SUM over one rank is the identity)."""
+    (a,) = _run(tmp_path / "a", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="1")
+    assert a["dp_graph"] and a["multi"], "the all-reduce must be captured in the multi-step graph"
+    assert a["steps"] == 16 and a["skipped"] == 0 and a["ar_us"] is not None and a["ar_us"] > 0
+    (b,) = _run(tmp_path / "b", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="0")
+    assert not b["dp_graph"] and b["multi"] and b["steps"] == 16
+    for k in ("p", "p2", "loss"):
+        assert abs(a[k] - b[k]) <= 1e-4 * abs(b[k]) + 1e-6, (k, a[k], b[k])
