@@ -43,35 +43,65 @@ def _interp(values, time, max_gap):
     return interpolate_gaps(values, time, max_gap).astype(np.float32)
 
 
+def _cml_flagged_rows(lat, lon, flagged, unit: str) -> np.ndarray:
+    """Rows ``flagged`` of the CML geodesic distance matrix ([F, S]), each pair evaluated in the
+    (lower index, higher index) orientation :func:`geodesic_distance_matrix` uses, so the values are
+    bit-identical to the full matrix's without computing its S^2 / 2 pairs."""
+    from .geo import vincenty_inverse
+    S = lat.shape[0]
+    j = np.arange(S)
+    rows = np.zeros((len(flagged), S), dtype=np.float64)
+    scale = {"m": 1.0, "km": 1e-3}[unit]
+    for r, s in enumerate(flagged):
+        a, b = np.minimum(s, j), np.maximum(s, j)
+        off = a != b
+        rows[r, off] = vincenty_inverse(lat[a[off]], lon[a[off]], lat[b[off]], lon[b[off]])
+    return rows * scale
+
+
 def prepare_cml_groups(ds: SensorData, cfg) -> List[SensorGroup]:
-    """CML part of ``create_sensors_ncfiles`` (``:79-120``) in memory."""
+    """CML part of ``create_sensors_ncfiles`` (``:79-120``) in memory.
+
+    Only the links that end up in some neighbourhood are touched: distances are computed as the
+    flagged links' rows plus the matrix of the needed links, and gap filling, masking and the
+    expert-vote target run on those rows only. The result is identical to processing every link
+    (the reference writes one NetCDF per flagged link), but the full-size network (3,904 links x
+    133,920 minutes, 20 flagged; ``notebooks/prepare_raw_cml.ipynb``) needs a few hundred MB
+    instead of tens of GB of host temporaries."""
+    from .geo import geodesic_distance_matrix
     cfg = normalize_preproc(cfg)
     time = ds.time
+    unit = cfg.get("distance_unit", "km")
+    lat, lon = sensor_positions(ds, "cml")
+    flagged = np.nonzero(np.asarray(ds["flagged"].data, bool))[0]
+    max_dist = cfg.graph.max_sample_distance
+    rows = _cml_flagged_rows(lat, lon, flagged, unit)
+    nbs = [get_neighbors(rows, r, max_dist, "cml") for r in range(len(flagged))]
+    needed = np.unique(np.concatenate(nbs + [flagged])) if len(flagged) else np.zeros(0, np.int64)
+    pos = {int(s): i for i, s in enumerate(needed)}
+    dist = geodesic_distance_matrix(lat[needed], lon[needed], unit=unit)      # [n_needed, n_needed]
     feats = []
     for name in CML_FEATURES:
-        v = np.array(ds[name].data, dtype=np.float32)
+        v = np.array(np.asarray(ds[name].data)[needed], dtype=np.float32)
         v[v >= 200] = np.nan          # "High (over 200 dB) values replaced with NaN"
         if cfg.interpolate:
             v = _interp(v, time, np.timedelta64(5, "m"))
         feats.append(v)
-    X = np.stack(feats, axis=1)       # [S, C, T]
-    target = create_target(ds, CML_FLAG_VARS, 3, "cml")
-    dist = compute_distance_matrix(ds, "cml", unit=cfg.get("distance_unit", "km"))
-    lat, lon = sensor_positions(ds, "cml")
-    flagged = np.nonzero(np.asarray(ds["flagged"].data, bool))[0]
-    max_dist = cfg.graph.max_sample_distance
+    X = np.stack(feats, axis=1)       # [n_needed, C, T]
+    target = create_target(ds, CML_FLAG_VARS, 3, "cml", sensors=flagged)      # [F, T]
     groups = []
     ids = ds.sensor_ids
-    for s in flagged:
-        nb = get_neighbors(dist, s, max_dist, "cml")
+    for r, s in enumerate(flagged):
+        nb = nbs[r]
+        li = np.array([pos[int(k)] for k in nb], dtype=np.int64)
         coords = {k: np.asarray(ds[k].data)[nb] for k in ("site_a_latitude", "site_a_longitude",
                                                           "site_b_latitude", "site_b_longitude", "length")
                   if k in ds}
         groups.append(SensorGroup(
             group_id=str(ids[s]), ds_type="cml", sensor_ids=ids[nb],
             anomalous_pos=int(np.nonzero(nb == s)[0][0]), feature_names=list(CML_FEATURES),
-            features=np.ascontiguousarray(X[nb]), time=time, target=target[s].astype(bool),
-            distances=dist[np.ix_(nb, nb)], lat=lat[nb], lon=lon[nb], coords=coords))
+            features=np.ascontiguousarray(X[li]), time=time, target=target[r].astype(bool),
+            distances=dist[np.ix_(li, li)], lat=lat[nb], lon=lon[nb], coords=coords))
     return groups
 
 

@@ -63,6 +63,45 @@ def _rain_field(n_sensors, n_time, mx, my, rng, rain_fraction=0.06, minutes_per_
     return rate
 
 
+def _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp):
+    """Anomaly events of flagged link ``s`` added to its TL rows, with the experts' flags."""
+    n_events = rng.poisson(anomaly_rate * days * 1.6)
+    for _ in range(n_events):
+        kind = rng.choice(4, p=[0.3, 0.25, 0.3, 0.15])
+        if kind == 0:    # jump: level shift for a while
+            dur = int(rng.uniform(20, 240))
+            t0 = int(rng.integers(0, T - dur))
+            amp = rng.choice([-1, 1]) * rng.uniform(1.0, 6.0) / difficulty
+            prof = np.ones(dur) * amp
+            ramp = min(3, dur // 4)
+            if ramp > 0:
+                prof[:ramp] *= np.linspace(0.3, 1, ramp)
+        elif kind == 1:  # dew: morning bump
+            dur = int(rng.uniform(60, 240))
+            day0 = int(rng.integers(0, max(1, int(days) - 1)))
+            t0 = min(T - dur - 1, day0 * 1440 + int(rng.uniform(180, 420)))
+            amp = rng.uniform(1.0, 4.0) / difficulty
+            prof = amp * _smooth_bump(dur, 0.5, rng)
+        elif kind == 2:  # fluctuation: high-frequency noise burst
+            dur = int(rng.uniform(30, 240))
+            t0 = int(rng.integers(0, T - dur))
+            sig = rng.uniform(0.6, 2.5) / difficulty
+            prof = rng.normal(0, sig, dur) + np.abs(rng.normal(0, sig / 2, dur))
+        else:            # unknown: deep drops/spikes or drift
+            dur = int(rng.uniform(10, 120))
+            t0 = int(rng.integers(0, T - dur))
+            amp = rng.uniform(3, 12) / difficulty
+            prof = amp * (rng.random(dur) < 0.3) * rng.uniform(0.3, 1.0, dur)
+        tl1[s, t0:t0 + dur] += prof
+        tl2[s, t0:t0 + dur] += prof * rng.uniform(0.7, 1.1)
+        name = flag_names[kind]
+        for e in range(n_exp):
+            if rng.random() < 0.92:
+                j0 = int(np.clip(t0 + rng.integers(-6, 7), 0, T - 1))
+                j1 = int(np.clip(t0 + dur + rng.integers(-6, 7), j0 + 1, T))
+                flags[name][e, s, j0:j1] = True
+
+
 def make_cml_raw(n_sensors: int = 23, n_flagged: int = 1, n_minutes: int = 40320,
                  start: str = "2019-07-02T00:00", seed: int = 0, center=(51.5, 7.45),
                  extent_km: float = 12.0, anomaly_rate: float = 1.0, rain_fraction: float = 0.06,
@@ -117,41 +156,7 @@ def make_cml_raw(n_sensors: int = 23, n_flagged: int = 1, n_minutes: int = 40320
     flags = {k: np.zeros((n_exp, S, T), dtype=bool) for k in flag_names}
     days = T / 1440.0
     for s in np.nonzero(flagged)[0]:
-        n_events = rng.poisson(anomaly_rate * days * 1.6)
-        for _ in range(n_events):
-            kind = rng.choice(4, p=[0.3, 0.25, 0.3, 0.15])
-            if kind == 0:    # jump: level shift for a while
-                dur = int(rng.uniform(20, 240))
-                t0 = int(rng.integers(0, T - dur))
-                amp = rng.choice([-1, 1]) * rng.uniform(1.0, 6.0) / difficulty
-                prof = np.ones(dur) * amp
-                ramp = min(3, dur // 4)
-                if ramp > 0:
-                    prof[:ramp] *= np.linspace(0.3, 1, ramp)
-            elif kind == 1:  # dew: morning bump
-                dur = int(rng.uniform(60, 240))
-                day0 = int(rng.integers(0, max(1, int(days) - 1)))
-                t0 = min(T - dur - 1, day0 * 1440 + int(rng.uniform(180, 420)))
-                amp = rng.uniform(1.0, 4.0) / difficulty
-                prof = amp * _smooth_bump(dur, 0.5, rng)
-            elif kind == 2:  # fluctuation: high-frequency noise burst
-                dur = int(rng.uniform(30, 240))
-                t0 = int(rng.integers(0, T - dur))
-                sig = rng.uniform(0.6, 2.5) / difficulty
-                prof = rng.normal(0, sig, dur) + np.abs(rng.normal(0, sig / 2, dur))
-            else:            # unknown: deep drops/spikes or drift
-                dur = int(rng.uniform(10, 120))
-                t0 = int(rng.integers(0, T - dur))
-                amp = rng.uniform(3, 12) / difficulty
-                prof = amp * (rng.random(dur) < 0.3) * rng.uniform(0.3, 1.0, dur)
-            tl1[s, t0:t0 + dur] += prof
-            tl2[s, t0:t0 + dur] += prof * rng.uniform(0.7, 1.1)
-            name = flag_names[kind]
-            for e in range(n_exp):
-                if rng.random() < 0.92:
-                    j0 = int(np.clip(t0 + rng.integers(-6, 7), 0, T - 1))
-                    j1 = int(np.clip(t0 + dur + rng.integers(-6, 7), j0 + 1, T))
-                    flags[name][e, s, j0:j1] = True
+        _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp)
     # --- quantisation, gaps, out-of-range spikes
     tl1 = np.round(tl1 * 10) / 10
     tl2 = np.round(tl2 * 10) / 10
@@ -184,6 +189,140 @@ def make_cml_raw(n_sensors: int = 23, n_flagged: int = 1, n_minutes: int = 40320
     ds.set_coord("polarization_2", "sensor_id", pol2)
     ds["TL_1"] = (("sensor_id", "time"), tl1.astype(np.float32))
     ds["TL_2"] = (("sensor_id", "time"), tl2.astype(np.float32))
+    for k in flag_names:
+        ds[k] = (("expert", "sensor_id", "time"), flags[k])
+    ds["flagged"] = ("sensor_id", flagged)
+    return ds
+
+
+def make_cml_raw_network(n_sensors: int = 3904, n_flagged: int = 20, n_minutes: int = 133920,
+                         start: str = "2019-07-01T00:00", seed: int = 0, center=(51.16, 10.45),
+                         extent_km: float = 337.0, anomaly_rate: float = 1.0, rain_fraction: float = 0.06,
+                         gap_rate: float = 2e-4, difficulty: float = 1.0, block: int = 128,
+                         min_neighbours: int = 3, max_sample_distance: float = 20.0) -> SensorData:
+    """Country-scale CML raw dataset: the full reference network's SHAPE (3,904 links x 133,920
+    minutes, 20 flagged links; ``notebooks/prepare_raw_cml.ipynb`` cell 9) with the physics of
+    :func:`make_cml_raw`, generated memory-lean: float32 TL rows built in blocks of ``block``
+    links, rain cells spread over the whole disc (count scaled with its area) and evaluated only on
+    the links near each cell's path, expert flags allocated as zero pages that are written only
+    for the flagged links. The default disc (337 km radius ~ Germany's area) gives a 20 km
+    neighbourhood of ~14 links, like the real network's density. Flagged links are drawn among
+    links with at least ``min_neighbours`` others within ``max_sample_distance`` km."""
+    rng = np.random.default_rng(seed)
+    S, T = n_sensors, n_minutes
+    time = np.arange(np.datetime64(start, "m"), np.datetime64(start, "m") + np.timedelta64(T, "m"))
+    r = extent_km * np.sqrt(rng.random(S))
+    th = rng.uniform(0, 2 * np.pi, S)
+    mx, my = r * np.cos(th), r * np.sin(th)
+    length = rng.uniform(0.5, 12.0, S)
+    orient = rng.uniform(0, np.pi, S)
+    ax_, ay_ = mx - np.cos(orient) * length / 2, my - np.sin(orient) * length / 2
+    bx_, by_ = mx + np.cos(orient) * length / 2, my + np.sin(orient) * length / 2
+    lat_a, lon_a = _offset_latlon(center[0], center[1], ax_, ay_)
+    lat_b, lon_b = _offset_latlon(center[0], center[1], bx_, by_)
+    freq1 = rng.choice([15.0, 18.0, 23.0, 26.0, 32.0, 38.0], S)
+    freq2 = freq1 + rng.choice([-1.0, 1.0], S) * rng.uniform(0.5, 1.5, S)
+    pol1 = rng.choice(np.array(["H", "V"]), S)
+    pol2 = np.where(rng.random(S) < 0.8, pol1, np.where(pol1 == "H", "V", "H"))
+    # --- rain rate [S, T] float32 from moving cells, each touching only the links near its path
+    rain = np.zeros((S, T), dtype=np.float32)
+    total_h = T / 60.0
+    n_cells = max(1, int(total_h * rain_fraction / 1.5 * (extent_km / 25.0) ** 2))
+    for _ in range(n_cells):
+        dur = int(rng.uniform(30, 300))
+        t0 = int(rng.integers(0, max(1, T - dur)))
+        ang = rng.uniform(0, 2 * np.pi)
+        speed = rng.uniform(15, 60) / 60.0
+        rr = extent_km * np.sqrt(rng.random())
+        tt_ = rng.uniform(0, 2 * np.pi)
+        start_xy = np.array([rr * np.cos(tt_), rr * np.sin(tt_)])
+        radius = rng.uniform(3, 14)
+        peak = rng.gamma(2.0, 8.0)
+        tt = np.arange(dur)
+        cx = start_xy[0] + np.cos(ang) * speed * (tt - dur / 2)
+        cy = start_xy[1] + np.sin(ang) * speed * (tt - dur / 2)
+        env = _smooth_bump(dur, 1.0, rng)
+        env = env * np.clip(1 + 0.3 * np.convolve(rng.standard_normal(dur), np.ones(9) / 9, "same"), 0.2, 2)
+        reach = 4.0 * radius
+        near = np.nonzero((mx >= cx.min() - reach) & (mx <= cx.max() + reach) &
+                          (my >= cy.min() - reach) & (my <= cy.max() + reach))[0]
+        if near.size == 0:
+            continue
+        d2 = (mx[near, None] - cx[None, :]) ** 2 + (my[near, None] - cy[None, :]) ** 2
+        rain[near, t0:t0 + dur] += (peak * env[None, :] * np.exp(-d2 / (2 * radius ** 2))).astype(np.float32)
+    # --- flagged links: random links with enough neighbours
+    cand = []
+    for s in rng.permutation(S):
+        d = np.hypot(mx - mx[s], my - my[s])
+        if int((d <= max_sample_distance).sum()) - 1 >= min_neighbours:
+            cand.append(int(s))
+            if len(cand) == n_flagged:
+                break
+    flagged = np.zeros(S, bool)
+    flagged[cand] = True
+    n_exp = 4
+    flag_names = ["Jump", "Dew", "Fluctuation", "Unknown anomaly"]
+    flags = {k: np.zeros((n_exp, S, T), dtype=bool) for k in flag_names}     # zero pages until written
+    tl1 = np.empty((S, T), dtype=np.float32)
+    tl2 = np.empty((S, T), dtype=np.float32)
+    minute_of_day = (np.arange(T) % 1440).astype(np.float32)
+    diurnal = np.sin(2 * np.pi * (minute_of_day - 300) / 1440.0).astype(np.float32)
+    ramp = np.linspace(0, 1, T, dtype=np.float32)
+    days = T / 1440.0
+    for b0 in range(0, S, block):
+        b1 = min(S, b0 + block)
+        n = b1 - b0
+        br = np.random.default_rng([seed, b0])
+        base1 = br.uniform(40, 70, n).astype(np.float32)[:, None]
+        base2 = base1 + br.normal(0, 2.0, n).astype(np.float32)[:, None]
+        drift_amp = br.uniform(0.1, 0.5, n).astype(np.float32)[:, None]
+        slow = np.cumsum(br.normal(0, 0.01, (n, T)).astype(np.float32), axis=1)
+        slow -= ramp[None, :] * slow[:, -1:]
+        kc1 = (0.0009 * freq1[b0:b1] ** 1.8).astype(np.float32)[:, None]
+        kc2 = (0.0009 * freq2[b0:b1] ** 1.8).astype(np.float32)[:, None]
+        rb = rain[b0:b1]
+        wet = 1.2 * (1 - np.exp(-rb / 1.5))
+        att = rb ** 1.05 * length[b0:b1, None].astype(np.float32)
+        tl1[b0:b1] = base1 + drift_amp * diurnal[None, :] + slow + br.normal(0, 0.12, (n, T)).astype(np.float32) \
+            + kc1 * att + wet
+        tl2[b0:b1] = base2 + drift_amp * 0.9 * diurnal[None, :] + slow + \
+            br.normal(0, 0.12, (n, T)).astype(np.float32) + kc2 * att + wet
+    del rain
+    for s in np.nonzero(flagged)[0]:
+        _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp)
+    for b0 in range(0, S, block):
+        b1 = min(S, b0 + block)
+        br = np.random.default_rng([seed, b0, 1])
+        for arr in (tl1, tl2):
+            blk = arr[b0:b1]
+            np.round(blk * 10, out=blk)
+            blk /= 10
+            g = br.random(blk.shape, dtype=np.float32) < gap_rate
+            for s_, t_ in zip(*np.nonzero(g)):
+                blk[s_, t_:t_ + int(br.integers(1, 8))] = np.nan
+            blk[br.random(blk.shape, dtype=np.float32) < gap_rate / 4] = 255.0
+    for s in range(S):
+        if not flagged[s] and rng.random() < 0.3:
+            t0 = int(rng.integers(0, T - 600))
+            d = int(rng.uniform(60, 600))
+            tl1[s, t0:t0 + d] = np.nan
+            tl2[s, t0:t0 + d] = np.nan
+    ids = np.array([f"SY{1000 + i:05d}_2_SY{50000 + 7 * i:06d}_{1 + i % 4}" for i in range(S)])
+    ds = SensorData(attrs={"title": "synthetic country-scale CML raw dataset (gnnqc)", "seed": seed})
+    ds.set_coord("sensor_id", "sensor_id", ids)
+    ds.set_coord("time", "time", time)
+    ds.set_coord("expert", "expert", np.arange(n_exp, dtype=np.int32))
+    ds.set_coord("length", "sensor_id", length.astype(np.float64))
+    ds.set_coord("site_a_latitude", "sensor_id", lat_a)
+    ds.set_coord("site_a_longitude", "sensor_id", lon_a)
+    ds.set_coord("site_b_latitude", "sensor_id", lat_b)
+    ds.set_coord("site_b_longitude", "sensor_id", lon_b)
+    ds.set_coord("frequency_1", "sensor_id", freq1)
+    ds.set_coord("frequency_2", "sensor_id", freq2)
+    ds.set_coord("polarization_1", "sensor_id", pol1)
+    ds.set_coord("polarization_2", "sensor_id", pol2)
+    ds["TL_1"] = (("sensor_id", "time"), tl1)
+    ds["TL_2"] = (("sensor_id", "time"), tl2)
     for k in flag_names:
         ds[k] = (("expert", "sensor_id", "time"), flags[k])
     ds["flagged"] = ("sensor_id", flagged)
@@ -360,4 +499,4 @@ def make_soilnet_raw(n_boxes: int = 40, n_time: int = 8545, start: str = "2014-0
     return ds
 
 
-__all__ = ["make_cml_raw", "make_soilnet_raw"]
+__all__ = ["make_cml_raw", "make_cml_raw_network", "make_soilnet_raw"]

@@ -19,13 +19,18 @@ CML_FLAG_VARS = ("Jump", "Dew", "Fluctuation", "Unknown anomaly")
 
 
 def create_target(ds: SensorData, flag_vars: Sequence[str] = CML_FLAG_VARS, min_experts: int = 3,
-                  ds_type: str = "cml", flags_type: str = "manual") -> np.ndarray:
+                  ds_type: str = "cml", flags_type: str = "manual", sensors=None) -> np.ndarray:
+    """``sensors`` (CML): positions along ``sensor_id`` to evaluate (rows of the result, in that
+    order); None = every sensor."""
     if ds_type == "cml":
         per_var = []
         for name in flag_vars:
             v = ds[name]
             ax = v.dims.index("expert")
-            per_var.append(np.asarray(v.data).astype(np.int32).sum(axis=ax) >= min_experts)
+            d = np.asarray(v.data)
+            if sensors is not None:
+                d = np.take(d, np.asarray(sensors, dtype=np.int64), axis=v.dims.index("sensor_id"))
+            per_var.append(d.astype(np.int32).sum(axis=ax) >= min_experts)
         return np.any(np.stack(per_var, axis=0), axis=0)
     if ds_type == "soilnet":
         m = np.asarray(ds["moisture"].data, dtype=np.float64)

@@ -262,3 +262,26 @@ def test_soilnet_spatial_faults_are_locally_plausible():
         if man[i].any() and ok.any():
             s_ = m[i, man[i]]
             assert np.nanmin(s_) >= np.nanmin(m[i, ok]) - 2
+
+
+def test_cml_groups_touch_only_needed_links_and_match_full_processing():
+    """prepare_cml_groups computes distances, gap filling and targets for the neighbourhood links
+    only; the groups equal a straightforward full-network computation (reference semantics)."""
+    from gnnqc.data.graph import compute_distance_matrix, get_neighbors
+    from gnnqc.data.preprocessing import prepare_cml_groups
+    ds = make_cml_raw(n_sensors=40, n_flagged=3, n_minutes=2 * 1440, seed=11, extent_km=30.0)
+    pc = C.normalize_preproc(C.default("preprocessing_cml"))
+    groups = prepare_cml_groups(ds, pc)
+    dist = compute_distance_matrix(ds, "cml")
+    target = create_target(ds)
+    X = np.stack([interpolate_gaps(np.where(ds[n].data >= 200, np.nan, ds[n].data), ds.time,
+                                   np.timedelta64(5, "m")).astype(np.float32) for n in ("TL_1", "TL_2")], 1)
+    flagged = np.nonzero(ds["flagged"].data)[0]
+    assert len(groups) == 3 and len(flagged) == 3
+    for g, s in zip(groups, flagged):
+        nb = get_neighbors(dist, s, pc.graph.max_sample_distance, "cml")
+        assert list(g.sensor_ids) == list(ds.sensor_ids[nb])
+        np.testing.assert_array_equal(g.distances, dist[np.ix_(nb, nb)])
+        np.testing.assert_array_equal(g.features, X[nb])
+        np.testing.assert_array_equal(g.target, target[s])
+        assert g.sensor_ids[g.anomalous_pos] == ds.sensor_ids[s]
