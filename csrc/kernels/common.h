@@ -56,4 +56,22 @@ inline void check_f32_cuda(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), "gnnqc: ", name, " must be contiguous");
 }
 
+// LSTM gate gradients dz: bf16 from the time-major recurrences (they are bf16 values already: the
+// recurrence stages them through bf16 LDS for its MFMAs), fp32 from the sequence-major lstm_bwd
+inline void check_dz_cuda(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda(), "gnnqc: dz must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "gnnqc: dz must be float32 or bfloat16");
+  TORCH_CHECK(t.is_contiguous(), "gnnqc: dz must be contiguous");
+}
+inline int dz_bf16(const at::Tensor& t) { return t.scalar_type() == at::kBFloat16 ? 1 : 0; }
+// saved LSTM gates of the time-major recurrences: bf16 [.., 4] (lstm_tm_common.h gates_pack)
+inline void check_gates_cuda(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(),
+              "gnnqc: saved LSTM gates must be a contiguous bfloat16 GPU tensor");
+}
+inline __bf16* bf16_ptr(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "gnnqc: expected a bfloat16 tensor");
+  return reinterpret_cast<__bf16*>(t.data_ptr<at::BFloat16>());
+}
+
 }  // namespace gq

@@ -59,7 +59,7 @@ struct ChainStage {
   const float* U;
   const float* b;
   float* h;                          // [T+1][Mp][H] (row T: scratch)
-  float* g;                          // train: [T+1][tiles][NW][CPL][64][4]
+  __bf16* g;                         // train: [T+1][tiles][NW][CPL][64][4] packed bf16 gates
   float* c;
   unsigned long long* sout;          // tagged output stream [To][Mp][H] (nullptr: last stage)
   float* pout;                       // last stage only: own pooled output [T/P][Mp][H] (P > 0)
@@ -314,7 +314,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         hf[p][col][u] = hv;
         if constexpr (TRAIN) {
           const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
-          *reinterpret_cast<float4*>(S.g + o * 4) = make_float4(iv, fv, gv, ov);
+          *reinterpret_cast<uint2*>(S.g + o * 4) = gates_pack(iv, fv, gv, ov);
           S.c[o] = c[cc];
         }
       }
@@ -409,11 +409,11 @@ struct ChainBStage {
   const float* dh;                   // stage 0: fp32 gradient of the layer's (pooled) output [Ts][Mp][H]
   const unsigned long long* din;     // stages > 0: tagged dx stream of the stage above [Ts][Mp][H]
   const unsigned char* pidx;         // P > 0: argmax bytes of the pool after this layer [Ts][Mp][H]
-  const float* g;
+  const __bf16* g;
   const float* c;
   const float* W;
   const float* U;
-  float* dz;                         // [T+1][Mp][4H]
+  __bf16* dz;                        // [T+1][Mp][4H] bf16 (the exact MFMA operand values)
   unsigned long long* sout;          // tagged dx stream [T+1][Mp][Din] (nullptr: last stage)
   float* dx;                         // last stage: fp32 dx [T][Mp][Din]
   long long* trace_mid;              // profiling: time the step loop starts
@@ -574,7 +574,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   }
 
   // forward state ring (gates, c_t) and the dh element ring, D reverse steps ahead
-  float4 rg[D];
+  uint2 rg[D];                       // packed bf16 gates
   float rc[D];
   unsigned long long rq[D];
   unsigned ri[D];
@@ -589,7 +589,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   auto load = [&](int J, int SS) {
     const int tt = max(T - 1 - SS, 0);
     const size_t o = sidx(tt);
-    rg[J] = *reinterpret_cast<const float4*>(S.g + o * 4);
+    rg[J] = *reinterpret_cast<const uint2*>(S.g + o * 4);
     rc[J] = S.c[o];
     const int st = max(src_t(tt), 0);
     if constexpr (SRC) rq[J] = ld_granule(S.din + eoff + (size_t)st * hstep);
@@ -611,7 +611,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   };
   // dz storer (one float4 granule of the [16][4H] tile per thread)
   const int gz_seq = tid / (G4 / 4), gz_c = (tid % (G4 / 4)) * 4;
-  float* zbase = S.dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
+  __bf16* zbase = S.dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
   const size_t zstep = (size_t)Mp * G4;
   // dx: element e of the [16][Din] tile per lane, NQ passes (Din <= 64), clamped duplicates
   // instead of a branch; XO: publish granules, else (bottom stage) plain fp32
@@ -662,7 +662,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       {
         const float cp = rc[jn] * (t > 0 ? 1.f : 0.f);
         const float dh = dhn + dhr;
-        const float4 g4 = rg[j];
+        const float4 g4 = gates_unpack(rg[j]);
         const float tc = tanhf_fast(rc[j]);
         const float dct = dc + dh * g4.w * (1.f - tc * tc);
         dc = dct * g4.y;
@@ -674,7 +674,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       {   // state of step s + D and the dh of step s + 1 (time t - 1)
         const int tt = max(T - 1 - (s + D), 0);
         const size_t o = sidx(tt);
-        rg[j] = *reinterpret_cast<const float4*>(S.g + o * 4);
+        rg[j] = *reinterpret_cast<const uint2*>(S.g + o * 4);
         rc[j] = S.c[o];
       }
       dhs[p ^ 1][tid / H][tid % H] = stage_dh(jn, t - 1);
@@ -699,10 +699,9 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         dhr = a0[0] + a1[0];
       }
       {   // dz tile -> HBM (weight-gradient pass)
-        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[p][gz_seq][gz_c]);
+        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][gz_c]);
         const int tz = t >= 0 ? t : T;
-        *reinterpret_cast<float4*>(zbase + (size_t)tz * zstep) =
-            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+        *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
       }
       {   // previous step's dx tile (time t + 1) -> stream / HBM; steps outside write row T
         const int ts = (s >= 1 && s <= T) ? t + 1 : T;
@@ -1012,7 +1011,7 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     S.U = U[s].data_ptr<float>();
     S.b = b[s].data_ptr<float>();
     at::Tensor h = at::empty({T + 1, Mp, H}, opt);
-    at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt) : at::empty({0}, opt);
+    at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
     at::Tensor c = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
     at::Tensor pooled, pidx;
     const TmPool pl = tm_pool_outputs(P, T, Mp, H, opt, pooled, pidx);
@@ -1021,7 +1020,7 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     // the stream carries the UNPOOLED h: a pooling consumer pools it (and writes pooled / pidx)
     at::Tensor so = !last ? at::empty({T, Mp, H}, opt.dtype(at::kLong)) : at::Tensor();
     S.h = h.data_ptr<float>();
-    S.g = train ? g.data_ptr<float>() : nullptr;
+    S.g = train ? bf16_ptr(g) : nullptr;
     S.c = train ? c.data_ptr<float>() : nullptr;
     S.sout = so.defined() ? reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>()) : nullptr;
     S.pout = last ? pl.out : nullptr;
@@ -1115,7 +1114,7 @@ static bool chain_job_x_ok(const at::Tensor& x, int Dw) {
 
 // one weight-gradient job of the chain backward: dz [>= T*Mp rows, 4H] (time-major), x [T, Mp, ldx]
 // (first Dw channels), h [T, Mp, H]; split count for G spare workgroups; ws: its split records
-static void chain_fill_job(ChainGJ& J, const float* dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
+static void chain_fill_job(ChainGJ& J, const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
                            at::Tensor& dW, at::Tensor& dU, at::Tensor& db, int G, int wait, int wait_n,
                            std::vector<at::Tensor>& keep) {
   const int Dw = (int)W.size(0), H = (int)W.size(1) / 4;
@@ -1135,7 +1134,8 @@ static void chain_fill_job(ChainGJ& J, const float* dz, const at::Tensor& x, con
   at::Tensor ws = at::empty({(long)splits * RC}, x.options());
   keep.push_back(ws);
   GradJob& gj = J.g;
-  gj.dz = dz;
+  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == at::kBFloat16, "lstm_chain_bwd_grads: dz must be bf16");
+  gj.dz = dz.data_ptr();
   gj.x = x.data_ptr<float>();
   gj.h = h.data_ptr<float>();
   gj.W = W.data_ptr<float>();
@@ -1197,16 +1197,16 @@ std::vector<at::Tensor> lstm_chain_bwd_grads(const at::Tensor& dh, at::TensorLis
   A.gtrace = A.trace + 3 * 256;
   int nj = 0;
   if (ext.size() == 7) {
-    check_f32_cuda(ext[0], "edz");
+    check_dz_cuda(ext[0]);
     TORCH_CHECK(ext[0].size(-1) == ext[3].size(1) && ext[0].numel() / ext[0].size(-1) >= ext[1].size(0) * ext[1].size(1),
                 "lstm_chain_bwd_grads: edz");
     at::Tensor dWe = ext[4], dUe = ext[5], dbe = ext[6];
-    chain_fill_job(A.gj[nj++], ext[0].data_ptr<float>(), ext[1], ext[2], ext[3], dWe, dUe, dbe, G, -1, 0, keep);
+    chain_fill_job(A.gj[nj++], ext[0], ext[1], ext[2], ext[3], dWe, dUe, dbe, G, -1, 0, keep);
   }
   for (int s = 0; s < ns; ++s) {
     TORCH_CHECK(gx[s].size(0) == T_in[s] && gx[s].size(1) == dh.size(1), "lstm_chain_bwd_grads: stage x shape");
     at::Tensor dWs = gdW[s], dUs = gdU[s], dbs = gdb[s];
-    chain_fill_job(A.gj[nj++], res[s].data_ptr<float>(), gx[s], gh[s], W[s], dWs, dUs, dbs, G, s, A.ntiles, keep);
+    chain_fill_job(A.gj[nj++], res[s], gx[s], gh[s], W[s], dWs, dUs, dbs, G, s, A.ntiles, keep);
   }
   A.njobs = nj;
   int gmax = 0;
@@ -1246,7 +1246,8 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
     const int P = (int)pool[s];
     TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_chain_bwd: hidden size ", H);
     TORCH_CHECK(Dw <= Din && Din <= 64 && Din % 4 == 0 && T >= 1 && T < 4096, "lstm_chain_bwd: stage ", s, " shape");
-    for (const at::Tensor* t : {&g[s], &c[s], &W[s], &U[s]}) check_f32_cuda(*t, "lstm_chain_bwd operand");
+    for (const at::Tensor* t : {&c[s], &W[s], &U[s]}) check_f32_cuda(*t, "lstm_chain_bwd operand");
+    check_gates_cuda(g[s]);
     TORCH_CHECK(g[s].numel() == (long)(T + 1) * Mp * H * 4 && c[s].numel() == (long)(T + 1) * Mp * H,
                 "lstm_chain_bwd: saved state shapes");
     const int Ts = P > 0 ? T / P : T;
@@ -1264,12 +1265,12 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
     S.dh = s == 0 ? dh.data_ptr<float>() : nullptr;
     S.din = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev.data_ptr<int64_t>());
     S.pidx = P > 0 ? pidx[s].data_ptr<uint8_t>() : nullptr;
-    S.g = g[s].data_ptr<float>();
+    S.g = bf16_ptr(g[s]);
     S.c = c[s].data_ptr<float>();
     S.W = W[s].data_ptr<float>();
     S.U = U[s].data_ptr<float>();
-    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, opt);
-    S.dz = dz.data_ptr<float>();
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, opt.dtype(at::kBFloat16));
+    S.dz = bf16_ptr(dz);
     dzs.push_back(dz);
     const bool last = s + 1 == ns && ns > 1;     // (a single stage publishes: profiling)
     if (!last) {

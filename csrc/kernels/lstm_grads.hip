@@ -18,17 +18,18 @@
 #include "lstm_grads_body.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace gq {
 
-template <int H, int DT, int GRX>
+template <int H, int DT, int GRX, typename ZT>
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
-    const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
+    const void* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
     long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems) {
   __shared__ __attribute__((aligned(16))) char smem[GradsLds<H, DT>::BYTES];
-  lstm_grads_body<H, DT, GRX>(dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride, lddx, xg,
-                              x_elems, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, smem);
+  lstm_grads_body<H, DT, GRX, false, ZT>(dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride, lddx,
+                                         xg, x_elems, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, smem);
 }
 
 __global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __restrict__ ws, int splits, int RC,
@@ -49,18 +50,18 @@ __global__ __launch_bounds__(256) void lstm_grads_reduce_final_kernel(const floa
   }
 }
 
-template <int H>
-void launch_grads_h(int DT, int grx, dim3 grid, hipStream_t st, const float* dz, const float* x, const float* h,
+template <int H, typename ZT>
+void launch_grads_h(int DT, int grx, dim3 grid, hipStream_t st, const void* dz, const float* x, const float* h,
                     const float* W, float* dx, float* ws, long rows, long period, long hshift, int Din, int ldx,
                     long dx_cb_stride, int lddx, int xg, long x_elems) {
   switch (DT) {
 #define GQ_DT(D)                                                                                              \
   case D:                                                                                                     \
     if (grx == 4)                                                                                             \
-      hipLaunchKernelGGL((lstm_grads_kernel<H, D, 4>), grid, dim3(256), 0, st, dz, x, h, W, dx, ws, rows,     \
+      hipLaunchKernelGGL((lstm_grads_kernel<H, D, 4, ZT>), grid, dim3(256), 0, st, dz, x, h, W, dx, ws, rows, \
                          period, hshift, Din, ldx, dx_cb_stride, lddx, xg, x_elems);                          \
     else                                                                                                      \
-      hipLaunchKernelGGL((lstm_grads_kernel<H, D, 1>), grid, dim3(256), 0, st, dz, x, h, W, dx, ws, rows,     \
+      hipLaunchKernelGGL((lstm_grads_kernel<H, D, 1, ZT>), grid, dim3(256), 0, st, dz, x, h, W, dx, ws, rows, \
                          period, hshift, Din, ldx, dx_cb_stride, lddx, xg, x_elems);                          \
     break;
     GQ_DT(1) GQ_DT(2) GQ_DT(3) GQ_DT(4) GQ_DT(5) GQ_DT(6) GQ_DT(7) GQ_DT(8) GQ_DT(9)
@@ -74,8 +75,8 @@ void launch_grads_h(int DT, int grx, dim3 grid, hipStream_t st, const float* dz,
 // paths: row r of dz / x / dx has h_{t-1} at row r - hshift when r % period >= hshift.
 // x rows have pitch ldx, dx rows pitch lddx; only the first Din (= rows of W) channels are used.
 //   sequence-major [M,T,C]: period = T, hshift = 1;  time-major [T,Mp,C]: period = T*Mp, hshift = Mp.
-void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
-                     float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
+void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq, const float* W, float* dx,
+                     float* dW, float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
                      long dx_cb_stride, int lddx, long x_elems, hipStream_t st) {
   if (rows == 0) return;
   TORCH_CHECK(ldx >= Din && ldx <= 144, "gnnqc lstm_grads: x row pitch ", ldx, " (Din ", Din, ")");
@@ -98,8 +99,12 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
   dim3 grid(ncb, splits);
 #define GQ_GR_H(HH)                                                                                              \
   case HH:                                                                                                       \
-    launch_grads_h<HH>(DT, grx, grid, st, dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride,  \
-                       lddx, xg, x_elems);                                                                       \
+    if (zbf)                                                                                                     \
+      launch_grads_h<HH, __bf16>(DT, grx, grid, st, dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx,      \
+                                 dx_cb_stride, lddx, xg, x_elems);                                               \
+    else                                                                                                         \
+      launch_grads_h<HH, float>(DT, grx, grid, st, dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx,       \
+                                dx_cb_stride, lddx, xg, x_elems);                                                \
     break;
   switch (H) {
     GQ_GR_H(16) GQ_GR_H(32) GQ_GR_H(64) GQ_GR_H(128)
@@ -125,9 +130,10 @@ void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const f
 // leave as one float4. All 4H gate-units are contracted in one workgroup: no per-column-
 // block slabs and no slab sum. Used when the weight-gradient pass runs on a side stream
 // (off the critical path) while this kernel feeds the next layer's recurrence.
-template <int H, int RW, int NDT>   // RW: waves sharing one 16-row tile; NDT: 16-wide din tiles per wave
-__global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ dz, const float* __restrict__ W,
+template <int H, int RW, int NDT, typename ZT>   // RW: waves sharing one 16-row tile; NDT: din tiles per wave
+__global__ __launch_bounds__(256) void lstm_dx_kernel(const void* __restrict__ dzv, const float* __restrict__ W,
                                                       float* __restrict__ dx, long rows, int Dw, int lddx) {
+  const ZT* __restrict__ dz = reinterpret_cast<const ZT*>(dzv);
   constexpr int G4 = 4 * H, KS = G4 / 32, TPB = 4 / RW;     // row tiles per workgroup pass
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, quad = lane >> 4;
@@ -152,10 +158,14 @@ __global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ 
     bf16x8_t bz[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const float4 a = *reinterpret_cast<const float4*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad);
-      const float4 b = *reinterpret_cast<const float4*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad + 4);
-      bz[ks] = bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
-                        (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+      if constexpr (std::is_same<ZT, __bf16>::value) {
+        bz[ks] = *reinterpret_cast<const bf16x8_t*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad);
+        const float4 b = *reinterpret_cast<const float4*>(dz + (size_t)rc * G4 + 32 * ks + 8 * quad + 4);
+        bz[ks] = bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                          (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+      }
     }
 #pragma unroll
     for (int d = 0; d < NDT; ++d) {
@@ -176,10 +186,11 @@ __global__ __launch_bounds__(256) void lstm_dx_kernel(const float* __restrict__ 
   }
 }
 
-// dz: [>= rows, 4H] fp32 rows; W: [Dw, 4H]; out: [rows, lddx] (lddx >= Dw, multiple of 4).
+// dz: [>= rows, 4H] fp32 (or bf16: zbf) rows; W: [Dw, 4H]; out: [rows, lddx] (lddx >= Dw, multiple of 4).
 // Narrow inputs (1-2 din tiles) give each wave its own row tile instead of a din tile that
 // is then thrown away: no redundant dz loads, 2-4 row tiles per workgroup pass.
-void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, int Dw, int lddx, hipStream_t st) {
+void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows, int H, int Dw, int lddx,
+                  hipStream_t st) {
   if (rows == 0) return;
   const int ndin = (lddx + 15) / 16;
   TORCH_CHECK(ndin <= 8, "lstm_dx: input width ", lddx, " > 128");
@@ -187,8 +198,13 @@ void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, 
   const int ndt = (ndin + rw - 1) / rw;
   const long ngroups = ((rows + 15) / 16 + (4 / rw) - 1) / (4 / rw);
   const int grid = (int)std::max<long>(1, std::min<long>(ngroups, 2048));
-#define GQ_DX(HH, RWV, ND) \
-  hipLaunchKernelGGL((lstm_dx_kernel<HH, RWV, ND>), dim3(grid), dim3(256), 0, st, dz, W, dx, rows, Dw, lddx)
+#define GQ_DX(HH, RWV, ND)                                                                                          \
+  do {                                                                                                              \
+    if (zbf) hipLaunchKernelGGL((lstm_dx_kernel<HH, RWV, ND, __bf16>), dim3(grid), dim3(256), 0, st, dz, W, dx,     \
+                                rows, Dw, lddx);                                                                    \
+    else hipLaunchKernelGGL((lstm_dx_kernel<HH, RWV, ND, float>), dim3(grid), dim3(256), 0, st, dz, W, dx, rows,    \
+                            Dw, lddx);                                                                              \
+  } while (0)
 #define GQ_DX_H(HH)                                                                            \
   case HH:                                                                                     \
     if (rw == 1) GQ_DX(HH, 1, 1); else if (rw == 2) GQ_DX(HH, 2, 1);                           \
@@ -205,7 +221,7 @@ void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, 
 
 // dx = dz[:rows] W^T into a fresh [rows / lead, lead, lddx] tensor (shape taken from `like`).
 at::Tensor lstm_dx(const at::Tensor& dz, const at::Tensor& W, const at::Tensor& like) {
-  check_f32_cuda(dz, "dz");
+  check_dz_cuda(dz);
   check_f32_cuda(W, "W");
   const int G4 = (int)W.size(1), H = G4 / 4, Dw = (int)W.size(0);
   TORCH_CHECK(dz.size(-1) == G4, "lstm_dx: dz / W gate widths differ");
@@ -215,7 +231,7 @@ at::Tensor lstm_dx(const at::Tensor& dz, const at::Tensor& W, const at::Tensor& 
   TORCH_CHECK(dz.numel() / G4 >= rows, "lstm_dx: dz has too few rows");
   c10::DeviceGuard guard(dz.device());
   at::Tensor dx = at::empty(like.sizes(), like.options().dtype(at::kFloat));
-  lstm_dx_rows(dz.data_ptr<float>(), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, lddx, stream());
+  lstm_dx_rows(dz.data_ptr(), dz_bf16(dz), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, lddx, stream());
   return dx;
 }
 
@@ -247,7 +263,8 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   check_f32_cuda(dW, "dW");
   check_f32_cuda(dU, "dU");
   check_f32_cuda(db, "db");
-  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == at::kFloat && dz.stride(2) == 1 && dz.stride(1) == dz.size(2) &&
+  check_dz_cuda(dz);
+  TORCH_CHECK(dz.stride(2) == 1 && dz.stride(1) == dz.size(2) &&
                   dz.stride(0) == dz.size(1) * dz.size(2), "dz must be a contiguous [M,T,4H] row block");
   const int M = x.size(0), T = x.size(1), Din = x.size(2), H = hseq.size(2);
   TORCH_CHECK(dz.size(0) == M && dz.size(1) == T && dz.size(2) == 4 * H, "dz shape");
@@ -264,13 +281,13 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   at::Tensor dx = need_dx ? at::empty({direct ? 1 : ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
   const long rows = (long)M * T;
   if (rows == 0) return need_dx ? dx.sum(0) : dx;
-  lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
+  lstm_grads_rows(dz.data_ptr(), dz_bf16(dz), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
                   (need_dx && !direct) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                   db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, Din,
                   (long)(x.storage().nbytes() / sizeof(float)) - x.storage_offset(), stream());
   if (!need_dx) return dx;
   if (direct) {
-    lstm_dx_rows(dz.data_ptr<float>(), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Din, Din, stream());
+    lstm_dx_rows(dz.data_ptr(), dz_bf16(dz), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Din, Din, stream());
     return dx[0];
   }
   return ncb == 1 ? dx[0] : dx.sum(0);

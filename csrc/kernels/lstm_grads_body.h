@@ -3,6 +3,8 @@
 #pragma once
 #include "common.h"
 
+#include <type_traits>
+
 namespace gq {
 
 constexpr int GR_ROWS = 32;         // rows (sequence, step) per tile = MFMA K
@@ -11,7 +13,7 @@ constexpr int GR_LDR = GR_ROWS + 8; // padded LDS row length (bf16) of transpose
 
 // a weight-gradient pass (lstm_grads_body) and its split reduction as kernel-argument records
 struct GradJob {
-  const float* dz;
+  const void* dz;                   // bf16 (GradJob consumers instantiate the bf16 body only)
   const float* x;
   const float* h;
   const float* W;
@@ -65,12 +67,18 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 
 // CH (chained: extra workgroups of the backward chain kernel): no dx, and the split record is
 // stored write-through (sc1) for a reduction inside the same launch that reads it with sc1 loads
-template <int H, int DT, int GRX, bool CH = false>
+// ZT: dz element type - bf16 (the time-major recurrences: 8 B per 4 gate-units, exact, since the
+// MFMAs consume bf16 either way) or fp32 (the sequence-major lstm_bwd). A compile-time choice: a
+// runtime branch around the prefetch loads made hipcc drain the load ring at the join (measured:
+// the SoilNet weight-gradient passes 20-25 % slower).
+template <int H, int DT, int GRX, bool CH = false, typename ZT = __bf16>
 __device__ __forceinline__ void lstm_grads_body(
-    const float* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
+    const void* __restrict__ dzv, const float* __restrict__ x, const float* __restrict__ hseq,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
     long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems, int cb, int split,
     int ncbv, int splits, char* __restrict__ smem) {
+  constexpr bool ZBF = std::is_same<ZT, __bf16>::value;
+  const ZT* __restrict__ dz = reinterpret_cast<const ZT*>(dzv);
   constexpr int G4 = 4 * H;
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
@@ -134,7 +142,13 @@ __device__ __forceinline__ void lstm_grads_body(
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const long r = min(r0 + zr + 16 * q, rows - 1);
-      rz[q] = *reinterpret_cast<const float4*>(dz + (size_t)r * G4 + gu0 + zc);
+      if constexpr (ZBF) {
+        const uint2 u = *reinterpret_cast<const uint2*>(dz + (size_t)r * G4 + gu0 + zc);
+        rz[q] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                            __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      } else {
+        rz[q] = *reinterpret_cast<const float4*>(dz + (size_t)r * G4 + gu0 + zc);
+      }
     }
     // granule offsets are clamped into the tile's span (idle lanes re-read a line already
     // being fetched instead of the next tile's data) and into the array (rows past the end

@@ -34,12 +34,13 @@
 namespace gq {
 
 // lstm_grads.hip: weight gradients (+ dx) over flat rows, h_{t-1} hshift rows back
-void lstm_grads_rows(const float* dz, const float* x, const float* hseq, const float* W, float* dx, float* dW,
+void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq, const float* W, float* dx, float* dW,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
                      long dx_cb_stride, int lddx, long x_elems, hipStream_t st);
 int lstm_grads_col_blocks(int H);
 bool lstm_dx_direct(int H, int Dw, int lddx);
-void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, int Dw, int lddx, hipStream_t st);
+void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows, int H, int Dw, int lddx,
+                  hipStream_t st);
 
 // =====================================================================================
 // forward
@@ -47,7 +48,7 @@ void lstm_dx_rows(const float* dz, const float* W, float* dx, long rows, int H, 
 template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
-    const float* __restrict__ bias, float* __restrict__ hout, float* __restrict__ gbuf,
+    const float* __restrict__ bias, float* __restrict__ hout, __bf16* __restrict__ gbuf,
     float* __restrict__ cbuf, int Mp, int T, int Din, int Dw, float* __restrict__ pout,
     unsigned* __restrict__ iout, int P) {
   // Din: channels of the x layout (row pitch); Dw <= Din: rows of W (padding channels of x are zero)
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
         hf[p][col][u] = hv;
         if constexpr (TRAIN) {                       // steps past T-1 write the scratch row T
           const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
-          *reinterpret_cast<float4*>(gbuf + o * 4) = make_float4(iv, fv, gv, ov);
+          *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
           cbuf[o] = c[cc];
         }
       }
@@ -196,8 +197,8 @@ template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
 __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
-    const float* __restrict__ bB, float* __restrict__ hA, float* __restrict__ gA, float* __restrict__ cA,
-    float* __restrict__ hB, float* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw,
+    const float* __restrict__ bB, float* __restrict__ hA, __bf16* __restrict__ gA, float* __restrict__ cA,
+    float* __restrict__ hB, __bf16* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw,
     float* __restrict__ pout, unsigned* __restrict__ iout, int P) {
   using C = TMC<H>;
   static_assert(C::CPL == 1, "pair kernel: one cell per lane (H <= 64)");
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
   const int gh = (tl % n_gh) * 4;
   float* hbase = (layerB ? hB : hA) + (size_t)row0 * H + gh;
   const size_t hstep = (size_t)Mp * H;
-  float* gbuf = layerB ? gB : gA;
+  __bf16* gbuf = layerB ? gB : gA;
   float* cbuf = layerB ? cB : cA;
   PoolAcc pool;
 
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
         hf[L][p][col][unit] = hv;
         if constexpr (TRAIN) {                       // invalid steps write the scratch row T
           const size_t o = (((size_t)(tc >= 0 ? min(tc, T) : T) * ntiles + tile) * NW + w) * 64 + lane;
-          *reinterpret_cast<float4*>(gbuf + o * 4) = make_float4(iv, fv, gv, ov);
+          *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
           cbuf[o] = c;
         }
       }
@@ -350,8 +351,8 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
 // dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
 template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
 __device__ __forceinline__ void lstm_tm_bwd_body(
-    const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
-    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
+    const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
+    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P, int tile, int ntiles) {
   // UNPOOL: dhout is the gradient of the fused MaxPooling1D output [T/P][Mp][H] and pidx its
   // argmax bytes; the scatter back to [T][Mp][H] happens as the dh tiles are staged
@@ -409,7 +410,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   }
 
   // ---- streams. internal state (per lane, ring over reverse steps): gates, c_t
-  float4 rg[CPL][D];
+  uint2 rg[CPL][D];                               // packed bf16 gates
   float rc[CPL][D];
   auto idx = [&](int tt, int cc) { return ((((size_t)tt * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane; };
 #define GQ_TMB_LOAD_STATE(J, SS)                                                    \
@@ -417,7 +418,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
     const int tt_ = max(T - 1 - (SS), 0);                                           \
     _Pragma("unroll") for (int cc = 0; cc < CPL; ++cc) {                            \
       const size_t o_ = idx(tt_, cc);                                               \
-      rg[cc][J] = *reinterpret_cast<const float4*>(gbuf + o_ * 4);                  \
+      rg[cc][J] = *reinterpret_cast<const uint2*>(gbuf + o_ * 4);                   \
       rc[cc][J] = cbuf[o_];                                                         \
     }                                                                               \
   }
@@ -438,7 +439,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   };
   // dz storer: one float4 granule of the [16][4H] tile per thread
   const int gz_seq = tid / (G4 / 4), gz_c = (tid % (G4 / 4)) * 4;
-  float* zbase = dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
+  __bf16* zbase = dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
   const size_t zstep = (size_t)Mp * G4;
   // dx storer over [16][Din] granules of GR floats (lanes past the tile rewrite granule 0)
   const int n_gx = 16 * Din / GR;
@@ -495,7 +496,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         const int u = unit[cc];
         const float cp = rc[cc][jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
         const float dh = dhn[cc] + dhr[cc];
-        const float4 g4 = rg[cc][j];
+        const float4 g4 = gates_unpack(rg[cc][j]);
         const float tc = tanhf_fast(rc[cc][j]);
         const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
         dc[cc] = dct * g4.y;
@@ -523,13 +524,12 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         }
         dhr[cc] = a0[0] + a1[0];
       }
-      // (b) dz tile of this step -> HBM (steps past t = 0 pad the unrolled chunk: scratch row)
+      // (b) dz tile of this step -> HBM as bf16 (its exact values: the MFMAs above consumed
+      // these bf16 values; steps past t = 0 pad the unrolled chunk: scratch row)
       if constexpr (DZ) {
-        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[p][gz_seq][gz_c]);
+        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][gz_c]);
         const int tz = t >= 0 ? t : T;
-        *reinterpret_cast<float4*>(zbase + (size_t)tz * zstep) =
-            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+        *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
       }
       // (c) previous step's dx tile -> HBM (written by all waves before this barrier)
       if constexpr (DX) {
@@ -569,8 +569,8 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 
 template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
-    const float* __restrict__ dhout, const float* __restrict__ gbuf, const float* __restrict__ cbuf,
-    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, float* __restrict__ dz,
+    const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
+    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P) {
   lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, UNPOOL>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, pidx, P,
                                                        blockIdx.x, gridDim.x);
@@ -586,9 +586,9 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 // Replaces two lstm_tm_bwd_kernel launches (and B's dx round trip through HBM).
 template <int H, int D>
 __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
-    const float* __restrict__ dhout, const float* __restrict__ gB, const float* __restrict__ cB,
-    const float* __restrict__ gA, const float* __restrict__ cA, const float* __restrict__ WB,
-    const float* __restrict__ UB, const float* __restrict__ UA, float* __restrict__ dzB, float* __restrict__ dzA,
+    const float* __restrict__ dhout, const __bf16* __restrict__ gB, const float* __restrict__ cB,
+    const __bf16* __restrict__ gA, const float* __restrict__ cA, const float* __restrict__ WB,
+    const float* __restrict__ UB, const float* __restrict__ UA, __bf16* __restrict__ dzB, __bf16* __restrict__ dzA,
     int Mp, int T) {
   using C = TMC<H>;
   static_assert(C::CPL == 1, "pair kernel: one cell per lane");
@@ -642,17 +642,17 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
   }
 
   // state rings: B at step s uses t = T-1-s, A uses t = T+1-s (clamped; invalid steps skip compute)
-  const float* gl = layerA ? gA : gB;
+  const __bf16* gl = layerA ? gA : gB;
   const float* cl = layerA ? cA : cB;
   const int Tl = layerA ? T + 2 : T;              // this layer's t = Tl - 1 - s
-  float4 rg[D];
+  uint2 rg[D];                                    // packed bf16 gates
   float rc[D];
   auto idx = [&](int tt) { return (((size_t)tt * ntiles + tile) * NW + w) * 64 + lane; };
 #define GQ_TM2B_STATE(J, SS)                                        \
   {                                                                 \
     const int tt_ = min(max(Tl - 1 - (SS), 0), T - 1);              \
     const size_t o_ = idx(tt_);                                     \
-    rg[J] = *reinterpret_cast<const float4*>(gl + o_ * 4);          \
+    rg[J] = *reinterpret_cast<const uint2*>(gl + o_ * 4);           \
     rc[J] = cl[o_];                                                 \
   }
   constexpr int n_gd = 16 * H / 4;
@@ -663,7 +663,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
 #define GQ_TM2B_D(J, SS)                                                                   \
   rd[J] = *reinterpret_cast<const float4*>(dbase + (size_t)max(T - 1 - (SS), 0) * dstep);
   const int gz_seq = tl / (G4 / 4), gz_c = (tl % (G4 / 4)) * 4;
-  float* zbase = (layerA ? dzA : dzB) + (size_t)(row0 + gz_seq) * G4 + gz_c;
+  __bf16* zbase = (layerA ? dzA : dzB) + (size_t)(row0 + gz_seq) * G4 + gz_c;
   const size_t zstep = (size_t)Mp * G4;
 
 #pragma unroll
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
         const float m = (t >= 0 && t < T) ? 1.f : 0.f;
         const float cp = rc[jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
         const float dh = (dd[L][p][col][unit] + dhr) * m;
-        const float4 g4 = rg[j];
+        const float4 g4 = gates_unpack(rg[j]);
         const float tc = tanhf_fast(rc[j]);
         const float dct = (dc + dh * g4.w * (1.f - tc * tc)) * m;
         dc = dct * g4.y;
@@ -715,10 +715,9 @@ __global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
       }
       // this step's dz tile -> HBM (invalid steps write the scratch row T)
       {
-        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[L][p][gz_seq][gz_c]);
+        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[L][p][gz_seq][gz_c]);
         const int tz = (t >= 0 && t < T) ? t : T;
-        *reinterpret_cast<float4*>(zbase + (size_t)tz * zstep) =
-            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+        *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
       }
       // B: dx_B^T = W_B dz_B^T -> A's dh tile (read two steps later, same parity)
       if (!layerA) {
@@ -756,8 +755,8 @@ static constexpr int PIPE_RED_KB = 8;     // slot blocks per reduce workgroup (l
 
 template <int HR, int HG, int DT>
 __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
-    const float* __restrict__ dh, const float* __restrict__ g, const float* __restrict__ c,
-    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dz, int Mp, int T, int Dw,
+    const float* __restrict__ dh, const __bf16* __restrict__ g, const float* __restrict__ c,
+    const float* __restrict__ W, const float* __restrict__ U, __bf16* __restrict__ dz, int Mp, int T, int Dw,
     int ntiles, GradJob gj, RedJob rj) {
   constexpr int D = HR >= 64 ? 2 : 4;
   const int b = blockIdx.x;
@@ -809,7 +808,7 @@ static bool tm_supported(int H, int Din, int gr) {
 
 // fused MaxPooling1D of the layer output: pooled [T/P, Mp, H] fp32 + argmax uint8 (P = 0: none)
 template <int H, bool TRAIN, int KX, int GR>
-static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, float* g,
+static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, __bf16* g,
                        float* c, int Mp, int T, int Din, int Dw, const TmPool& pl, hipStream_t st) {
   constexpr int D = 6;
   if (pl.P > 0)
@@ -821,8 +820,8 @@ static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* 
 }
 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
-static void tm_bwd_cfg(int ntiles, const float* dh, const float* g, const float* c, const float* W, const float* U,
-                       float* dx, float* dz, int Mp, int T, int Din, int Dw, hipStream_t st,
+static void tm_bwd_cfg(int ntiles, const float* dh, const __bf16* g, const float* c, const float* W, const float* U,
+                       float* dx, __bf16* dz, int Mp, int T, int Din, int Dw, hipStream_t st,
                        const TmPool& pl = TmPool()) {
   constexpr int D = H >= 64 ? 2 : 4;        // H = 64: 16 waves x 128 VGPRs, shorter state rings
   if constexpr (!LAST) {
@@ -897,11 +896,11 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   auto opt = x.options();
   // one extra (scratch) time row: stores of steps that have nothing to store land there
   at::Tensor h = at::empty({T + 1, Mp, H}, opt);
-  at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt) : at::empty({0}, opt);
+  at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   at::Tensor c = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
   const int ntiles = Mp / 16;
   auto st = stream();
-  float* gp = train ? g.data_ptr<float>() : nullptr;
+  __bf16* gp = train ? bf16_ptr(g) : nullptr;
   float* cp = train ? c.data_ptr<float>() : nullptr;
   at::Tensor pooled, pidx;
   const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
@@ -936,20 +935,21 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
     return state ? (train ? at::empty({T + 1, Mp, H, last}, opt) : at::empty({0}, opt)) : at::empty({T + 1, Mp, H}, opt);
   };
   at::Tensor hA = mk(false, 0), hB = mk(false, 0);
-  at::Tensor gA = mk(true, 4), gB = mk(true, 4);
+  at::Tensor gA = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  at::Tensor gB = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   at::Tensor cA = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
   at::Tensor cB = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
   const int ntiles = Mp / 16;
   auto st = stream();
-  float* P[4] = {train ? gA.data_ptr<float>() : nullptr, train ? cA.data_ptr<float>() : nullptr,
-                 train ? gB.data_ptr<float>() : nullptr, train ? cB.data_ptr<float>() : nullptr};
+  __bf16* PG[2] = {train ? bf16_ptr(gA) : nullptr, train ? bf16_ptr(gB) : nullptr};
+  float* P[4] = {nullptr, train ? cA.data_ptr<float>() : nullptr, nullptr, train ? cB.data_ptr<float>() : nullptr};
   at::Tensor pooled, pidx;
   const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
 #define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, PL)                                                                     \
   hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, PL>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,    \
                      x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
-                     WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), P[0], \
-                     P[1], hB.data_ptr<float>(), P[2], P[3], Mp, T, Din, Dw, pl.out, pl.idx, pl.P > 0 ? pl.P : 1)
+                     WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), PG[0], \
+                     P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw, pl.out, pl.idx, pl.P > 0 ? pl.P : 1)
   GQ_TM2_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (pl.P > 0) { if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, true); else GQ_TM2_LAUNCH(HH, false, KXX, GRR, true); }
       else { if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, false); else GQ_TM2_LAUNCH(HH, false, KXX, GRR, false); })));
@@ -959,11 +959,13 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
 }
 
 // Pair backward recurrences (lstm_tm2_bwd_kernel): dh [T, Mp, H] of B's output sequence;
-// returns [dzA, dzB] (fp32 [T+1, Mp, 4H], row T scratch) for the weight-gradient passes.
+// returns [dzA, dzB] (bf16 [T+1, Mp, 4H], row T scratch) for the weight-gradient passes.
 std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB, const at::Tensor& cB,
                                      const at::Tensor& gA, const at::Tensor& cA, const at::Tensor& WB,
                                      const at::Tensor& UB, const at::Tensor& UA) {
-  for (const at::Tensor* t : {&dh, &gB, &cB, &gA, &cA, &WB, &UB, &UA}) check_f32_cuda(*t, "lstm_tm2_bwd operand");
+  for (const at::Tensor* t : {&dh, &cB, &cA, &WB, &UB, &UA}) check_f32_cuda(*t, "lstm_tm2_bwd operand");
+  check_gates_cuda(gA);
+  check_gates_cuda(gB);
   TORCH_CHECK(dh.dim() == 3, "lstm_tm2_bwd: dh must be [T, Mp, H]");
   const int T = (int)dh.size(0), Mp = (int)dh.size(1), H = (int)dh.size(2);
   TORCH_CHECK(Mp % 16 == 0 && (H == 16 || H == 32), "lstm_tm2_bwd: H must be 16 or 32, Mp a multiple of 16");
@@ -972,13 +974,14 @@ std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB,
   TORCH_CHECK(gA.numel() == 4 * st_n && gB.numel() == 4 * st_n && cA.numel() == st_n && cB.numel() == st_n,
               "lstm_tm2_bwd: saved state shapes");
   c10::DeviceGuard guard(dh.device());
-  at::Tensor dzA = at::empty({T + 1, Mp, 4 * H}, dh.options()), dzB = at::empty({T + 1, Mp, 4 * H}, dh.options());
+  const auto zopt = dh.options().dtype(at::kBFloat16);
+  at::Tensor dzA = at::empty({T + 1, Mp, 4 * H}, zopt), dzB = at::empty({T + 1, Mp, 4 * H}, zopt);
   const int ntiles = Mp / 16;
   GQ_TM2_H_DISPATCH(H, hipLaunchKernelGGL((lstm_tm2_bwd_kernel<HH, 4>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,
-                                         stream(), dh.data_ptr<float>(), gB.data_ptr<float>(), cB.data_ptr<float>(),
-                                         gA.data_ptr<float>(), cA.data_ptr<float>(), WB.data_ptr<float>(),
-                                         UB.data_ptr<float>(), UA.data_ptr<float>(), dzB.data_ptr<float>(),
-                                         dzA.data_ptr<float>(), Mp, T));
+                                         stream(), dh.data_ptr<float>(), bf16_ptr(gB), cB.data_ptr<float>(),
+                                         bf16_ptr(gA), cA.data_ptr<float>(), WB.data_ptr<float>(),
+                                         UB.data_ptr<float>(), UA.data_ptr<float>(), bf16_ptr(dzB),
+                                         bf16_ptr(dzA), Mp, T));
   GQ_LAUNCH_CHECK();
   return {dzA, dzB};
 }
@@ -987,7 +990,8 @@ std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB,
 // the weight-gradient pass are then launched separately, the latter on a side stream).
 at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& W,
                           const at::Tensor& U, int64_t T, const c10::optional<at::Tensor>& pool_idx, int64_t pool) {
-  for (const at::Tensor* t : {&dh, &g, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_dz operand");
+  for (const at::Tensor* t : {&dh, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_dz operand");
+  check_gates_cuda(g);
   const int H = (int)U.size(0);
   const bool last = dh.dim() == 2;
   const int Mp = (int)(last ? dh.size(0) : dh.size(1));
@@ -997,15 +1001,15 @@ at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::T
               "lstm_tm_bwd_dz: saved state shapes");
   TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_tm_bwd_dz: hidden size");
   c10::DeviceGuard guard(dh.device());
-  at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, dh.options());
+  at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, dh.options().dtype(at::kBFloat16));
   const int ntiles = Mp / 16;
   auto st = stream();
   GQ_TM_H_DISPATCH(H,
-      if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, (int)T,
+      if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
+            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, (int)T,
             (int)W.size(0), (int)W.size(0), st);
-      else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, (int)T,
+      else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
+            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, (int)T,
             (int)W.size(0), (int)W.size(0), st, pl));
   GQ_LAUNCH_CHECK();
   return dz;
@@ -1054,7 +1058,8 @@ at::Tensor lstm_tm_bwd_pipe(const at::Tensor& dh, const at::Tensor& g, const at:
   int HR = 16, Mp = 0, ntiles = 0, Dw = 1;
   at::Tensor dz = at::empty({0}, ref.options());
   if (rec) {
-    for (const at::Tensor* t : {&dh, &g, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_pipe operand");
+    for (const at::Tensor* t : {&dh, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_pipe operand");
+    check_gates_cuda(g);
     HR = (int)U.size(0);
     Mp = (int)dh.size(1);
     TORCH_CHECK(dh.dim() == 3 && dh.size(0) == T && dh.size(2) == HR && Mp % 16 == 0, "lstm_tm_bwd_pipe: dh shape");
@@ -1063,18 +1068,23 @@ at::Tensor lstm_tm_bwd_pipe(const at::Tensor& dh, const at::Tensor& g, const at:
     TORCH_CHECK(HR == 16 || HR == 32 || HR == 64, "lstm_tm_bwd_pipe: hidden size");
     ntiles = Mp / 16;
     Dw = (int)W.size(0);
-    dz = at::empty({T + 1, Mp, 4 * HR}, dh.options());
+    dz = at::empty({T + 1, Mp, 4 * HR}, dh.options().dtype(at::kBFloat16));
   }
   GradJob gj{};
+  at::Tensor gz_b;
   int HG = 0, DTG = 1;
   if (job) {
-    for (const at::Tensor* t : {&gz, &gh, &gW, &gws}) check_f32_cuda(*t, "lstm_tm_bwd_pipe job operand");
+    check_dz_cuda(gz);
+    for (const at::Tensor* t : {&gh, &gW, &gws}) check_f32_cuda(*t, "lstm_tm_bwd_pipe job operand");
+    // the job bodies read bf16 dz; an fp32 dz (sequence-major lstm_bwd) is rounded here exactly as
+    // the grads body would round it when staging, so the result is the same
+    if (!dz_bf16(gz)) gz_b = gz.to(at::kBFloat16);
     TORCH_CHECK(gx.is_cuda() && gx.scalar_type() == at::kFloat, "lstm_tm_bwd_pipe: job x");
     HG = (int)gW.size(1) / 4;
     const int gDw = (int)gW.size(0);
     TORCH_CHECK(grads_job_ok(gx, gDw), "lstm_tm_bwd_pipe: job x layout");
     DTG = (gDw + 1 + 15) / 16;
-    gj.dz = gz.data_ptr<float>();
+    gj.dz = gz_b.defined() ? gz_b.data_ptr() : gz.data_ptr();
     gj.x = gx.data_ptr<float>();
     gj.h = gh.data_ptr<float>();
     gj.W = gW.data_ptr<float>();
@@ -1119,13 +1129,14 @@ at::Tensor lstm_tm_bwd_pipe(const at::Tensor& dh, const at::Tensor& g, const at:
   const int nblk = ntiles + gj.nblocks + rj.nblocks;
   if (nblk == 0) return dz;
   TORCH_CHECK(!job || HG == HR || HG == 2 * HR || !rec, "lstm_tm_bwd_pipe: job hidden size must be H or 2H of the rec");
-  const float* P[5] = {rec ? dh.data_ptr<float>() : nullptr, rec ? g.data_ptr<float>() : nullptr,
+  const __bf16* PG = rec ? bf16_ptr(g) : nullptr;
+  const float* P[5] = {rec ? dh.data_ptr<float>() : nullptr, nullptr,
                        rec ? c.data_ptr<float>() : nullptr, rec ? W.data_ptr<float>() : nullptr,
                        rec ? U.data_ptr<float>() : nullptr};
-  float* dzp = rec ? dz.data_ptr<float>() : nullptr;
+  __bf16* dzp = rec ? bf16_ptr(dz) : nullptr;
   auto st = stream();
 #define GQ_PIPE_LAUNCH(HRV, HGV, DTV)                                                                          \
-  hipLaunchKernelGGL((lstm_tm_bwd_dual_kernel<HRV, HGV, DTV>), dim3(nblk), dim3(TMC<HRV>::NT), 0, st, P[0], P[1],  \
+  hipLaunchKernelGGL((lstm_tm_bwd_dual_kernel<HRV, HGV, DTV>), dim3(nblk), dim3(TMC<HRV>::NT), 0, st, P[0], PG,    \
                      P[2], P[3], P[4], dzp, Mp, (int)T, Dw, ntiles, gj, rj)
 #define GQ_PIPE_DT(HRV, HGV)                                                                                   \
   switch (DTG) {                                                                                               \
@@ -1226,15 +1237,20 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
     MultiGrad M{};
     M.n = ng;
     int nb = 0;
+    // job bodies read bf16 dz: an fp32 one (sequence-major lstm_bwd) is rounded once here, as the
+    // body would round it when staging (same result); stream-ordered, so the temporaries may go
+    std::vector<at::Tensor> zb(ng);
     for (int k = 0; k < ng; ++k) {
-      for (const at::Tensor* t : {&gz[k], &gh[k], &gW[k], &gws[k]}) check_f32_cuda(*t, "lstm_grads_multi operand");
+      check_dz_cuda(gz[k]);
+      zb[k] = dz_bf16(gz[k]) ? gz[k] : gz[k].to(at::kBFloat16);
+      for (const at::Tensor* t : {&gh[k], &gW[k], &gws[k]}) check_f32_cuda(*t, "lstm_grads_multi operand");
       TORCH_CHECK(gx[k].is_cuda() && gx[k].scalar_type() == at::kFloat, "lstm_grads_multi: x");
       const int HG = (int)gW[k].size(1) / 4, Dw = (int)gW[k].size(0);
       TORCH_CHECK(HG == 16 || HG == 32 || HG == 64 || HG == 128, "lstm_grads_multi: hidden size");
       TORCH_CHECK(grads_job_ok(gx[k], Dw), "lstm_grads_multi: x layout");
       const int DT = (Dw + 1 + 15) / 16;
       GradJob& j = M.j[k];
-      j.dz = gz[k].data_ptr<float>();
+      j.dz = zb[k].data_ptr();
       j.x = gx[k].data_ptr<float>();
       j.h = gh[k].data_ptr<float>();
       j.W = gW[k].data_ptr<float>();
@@ -1296,7 +1312,8 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
 // dW, dU, db; returns dx [T, Mp, Din] if need_dx.
 at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
                          at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx) {
-  for (const at::Tensor* t : {&dz, &x, &h, &W}) check_f32_cuda(*t, "lstm_tm_grads operand");
+  check_dz_cuda(dz);
+  for (const at::Tensor* t : {&x, &h, &W}) check_f32_cuda(*t, "lstm_tm_grads operand");
   for (const at::Tensor* t : {&dW, &dU, &db}) check_f32_cuda(*t, "lstm_tm_grads gradient");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)h.size(2);
   const int Dw = (int)W.size(0);
@@ -1310,12 +1327,12 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
   // padding channels (>= Dw) are written as zeros by the kernel (their W rows are masked)
   const bool direct = need_dx && lstm_dx_direct(H, Dw, Din);   // one dz W^T pass instead of ncb slabs
   at::Tensor dx = need_dx ? at::empty({direct ? 1 : ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
-  lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
+  lstm_grads_rows(dz.data_ptr(), dz_bf16(dz), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                   (need_dx && !direct) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                   db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, stream());
   if (!need_dx) return dx;
   if (direct) {
-    lstm_dx_rows(dz.data_ptr<float>(), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, Din, stream());
+    lstm_dx_rows(dz.data_ptr(), dz_bf16(dz), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, Din, stream());
     return dx[0];
   }
   return ncb == 1 ? dx[0] : dx.sum(0);
@@ -1326,8 +1343,9 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
                        const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, at::Tensor dW, at::Tensor dU,
                        at::Tensor db, bool need_dx, const c10::optional<at::Tensor>& pool_idx, int64_t pool) {
-  const at::Tensor* ops[] = {&dh, &g, &c, &x, &h, &W, &U};
+  const at::Tensor* ops[] = {&dh, &c, &x, &h, &W, &U};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
+  check_gates_cuda(g);
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
   const int Dw = (int)W.size(0);
   TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H, "lstm_tm_bwd: W shape");
@@ -1350,13 +1368,13 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   const int ntiles = Mp / 16;
   auto st = stream();
   if (wg) {
-    // recurrence -> dz (fp32, bf16-exact), then dW/dU/db (+ dx) in one pass over T*Mp rows
-    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options());
+    // recurrence -> dz (bf16), then dW/dU/db (+ dx) in one pass over T*Mp rows
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));
     GQ_TM_H_DISPATCH(H,
-        if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st);
-        else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),
-              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, dz.data_ptr<float>(), Mp, T, Din, Dw, st,
+        if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st);
+        else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st,
               pl));
     GQ_LAUNCH_CHECK();
     const long rows = (long)T * Mp;
@@ -1364,12 +1382,12 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     // dx keeps the x layout (Din channels); padding channels (>= Dw) get zero gradient
     const bool direct = need_dx && lstm_dx_direct(H, Dw, Din);   // one dz W^T pass instead of ncb slabs
     at::Tensor dx = need_dx ? at::empty({direct ? 1 : ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
-    lstm_grads_rows(dz.data_ptr<float>(), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
+    lstm_grads_rows(dz.data_ptr(), 1, x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                     (need_dx && !direct) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                     db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, st);
     if (!need_dx) return dx;
     if (direct) {
-      lstm_dx_rows(dz.data_ptr<float>(), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, Din, st);
+      lstm_dx_rows(dz.data_ptr(), 1, W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, Din, st);
       return dx[0];
     }
     return ncb == 1 ? dx[0] : dx.sum(0);
@@ -1377,7 +1395,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
   TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
 #define GQ_TM_BWD_CALL(LASTV)                                                                               \
-  tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), g.data_ptr<float>(),          \
+  tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),          \
                                                c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
                                                dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st, pl)
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,

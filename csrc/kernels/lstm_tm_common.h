@@ -6,6 +6,19 @@ namespace gq {
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
+// Saved LSTM gates (i, f, g, o of one cell and step) are stored as 4 x bf16 = 8 bytes: the
+// forward's largest stream and the backward's largest read (was 16 bytes of fp32). Gate
+// activations lie in (0, 1) / (-1, 1), so bf16 keeps ~3 significant digits, the precision of
+// the bf16 MFMA operands they are combined with.
+__device__ __forceinline__ uint2 gates_pack(float i, float f, float g, float o) {
+  const bf16x4_t v = bf16x4_t{(__bf16)i, (__bf16)f, (__bf16)g, (__bf16)o};
+  return *reinterpret_cast<const uint2*>(&v);
+}
+__device__ __forceinline__ float4 gates_unpack(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
 // A wave-uniform predicate the compiler can SEE is uniform (an SGPR): branches on it are
 // scalar, so no exec-mask join -> no conservative s_waitcnt vmcnt(0) around the loads
 // inside (measured: with threadIdx-derived predicates every step drained the load ring).

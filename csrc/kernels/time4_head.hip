@@ -41,7 +41,7 @@ struct T4Args {
   float* h;                              // [T][Mp][H]
   float* g;                              // train: [T][tiles][NW][CPL][64][4]
   float* c;                              // train: [T][tiles][NW][CPL][64][2]: c_t, c_{t-1}
-  float* dz;                             // backward: [T + 1][Mp][4H]
+  __bf16* dz;                            // backward: [T + 1][Mp][4H] bf16
   float* dx;                             // backward: [T][Mp][Din]
   int T, Mp, Din, Dw, ntiles;
   ChainHead hd;
@@ -353,8 +353,7 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
       for (int q = 0; q < 16 * T4G / 4 / T4NT; ++q) {   // dz_t -> HBM, the bf16 values the MFMAs use
         const int e = tid + T4NT * q, sq = e / (T4G / 4), c4 = (e % (T4G / 4)) * 4;
         const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[sq][c4]);
-        *reinterpret_cast<float4*>(A.dz + (size_t)t * zstep + (size_t)(row0 + sq) * T4G + c4) =
-            make_float4((float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]);
+        *reinterpret_cast<bf16x4_t*>(A.dz + (size_t)t * zstep + (size_t)(row0 + sq) * T4G + c4) = zv;
       }
       {   // dh_rec^T for unit tile w (full K) and dx^T for din tile dt over gate-column half kh,
           // as 4 + 2 interleaved accumulator chains
@@ -553,9 +552,9 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   A.h = const_cast<float*>(h.data_ptr<float>());
   A.g = const_cast<float*>(g.data_ptr<float>());
   A.c = const_cast<float*>(c.data_ptr<float>());
-  at::Tensor dz = at::empty({T + 1, Mp, T4G}, opt), dx = at::empty({T, Mp, Din}, opt);
+  at::Tensor dz = at::empty({T + 1, Mp, T4G}, opt.dtype(at::kBFloat16)), dx = at::empty({T, Mp, Din}, opt);
   at::Tensor gpart = at::empty({(long)ntiles * ChainHeadRec<T4H>::PITCH}, opt);
-  A.dz = dz.data_ptr<float>();
+  A.dz = bf16_ptr(dz);
   A.dx = dx.data_ptr<float>();
   A.T = T;
   A.Mp = Mp;

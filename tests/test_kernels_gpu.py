@@ -67,18 +67,21 @@ def test_lstm_direct_grad_accumulation_and_padded_rows(cuda_device, Din, H):
 
 @pytest.mark.parametrize("H", [16, 32, 64, 128])
 @pytest.mark.parametrize("Dw,lddx", [(16, 16), (18, 20), (32, 32), (40, 44), (64, 64), (100, 100)])
-def test_lstm_dx_matches_matmul(cuda_device, H, Dw, lddx):
-    """Standalone dx = dz W^T kernel (all row-tile / din-tile layouts) vs an fp32 matmul of the
-    bf16-rounded operands; layout-padding columns come out as zeros."""
+@pytest.mark.parametrize("zdt", [torch.float32, torch.bfloat16])
+def test_lstm_dx_matches_matmul(cuda_device, H, Dw, lddx, zdt):
+    """Standalone dx = dz W^T kernel (all row-tile / din-tile layouts; fp32 dz of the sequence-major
+    recurrence, bf16 dz of the time-major ones) vs an fp32 matmul of the bf16-rounded operands;
+    layout-padding columns come out as zeros."""
     from gnnqc.utils.native import hip_ops
     gen = torch.Generator().manual_seed(H + Dw)
     rows = 16 * 37 + 5
-    dz = torch.randn(rows + 3, 4 * H, generator=gen).to(cuda_device)
+    dz = torch.randn(rows + 3, 4 * H, generator=gen).to(cuda_device).to(zdt)
     W = torch.randn(Dw, 4 * H, generator=gen).to(cuda_device) * 0.2
     like = torch.empty(rows, lddx, device=cuda_device)
     dx = hip_ops().lstm_dx(dz, W, like)
     ref = dz[:rows].bfloat16().float() @ W.bfloat16().float().t()
     torch.testing.assert_close(dx[:, :Dw], ref, atol=1e-3, rtol=1e-3)
+    assert dx.dtype == torch.float32
     assert torch.count_nonzero(dx[:, Dw:]).item() == 0
 
 
