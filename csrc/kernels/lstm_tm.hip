@@ -789,6 +789,16 @@ __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
 
 // =====================================================================================
 // host side
+// GNNQC_TM_RECDX=0: multi-column-block layers take dx from weight-gradient slabs + their sum
+// (the earlier layout) instead of from the recurrence
+static bool tm_rec_dx() {
+  static const bool on = [] {
+    const char* e = std::getenv("GNNQC_TM_RECDX");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 static int tm_granule(int Din, const void* x) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(x);
   if (Din % 4 == 0 && a % 16 == 0) return 4;
@@ -1367,6 +1377,28 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   c10::DeviceGuard guard(x.device());
   const int ntiles = Mp / 16;
   auto st = stream();
+  const int ncb_w = lstm_grads_col_blocks(H);
+  if (wg && need_dx && ncb_w > 1 && tm_rec_dx()) {
+    // several gate-column blocks: the weight-gradient pass could only produce dx as ncb partial
+    // slabs plus a slab sum (ncb + 2 dx-sized passes); the recurrence computes dx^T = W dz^T
+    // itself instead (its MFMA phase has the whole 4H dz tile in LDS) and writes dx once.
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));
+    at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
+    TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
+#define GQ_TM_BWD_CALL2(LASTV)                                                                              \
+  tm_bwd_cfg<HH, KXX, GRR, true, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), \
+                                              W.data_ptr<float>(), U.data_ptr<float>(), dx.data_ptr<float>(),  \
+                                              bf16_ptr(dz), Mp, T, Din, Dw, st, pl)
+    GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
+        if (last) GQ_TM_BWD_CALL2(true); else GQ_TM_BWD_CALL2(false))));
+#undef GQ_TM_BWD_CALL2
+    GQ_LAUNCH_CHECK();
+    const long rows = (long)T * Mp;
+    lstm_grads_rows(dz.data_ptr(), 1, x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(), nullptr,
+                    dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din,
+                    rows * Din, Din, rows * Din, st);
+    return dx.narrow(0, 0, T);
+  }
   if (wg) {
     // recurrence -> dz (bf16), then dW/dU/db (+ dx) in one pass over T*Mp rows
     at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));

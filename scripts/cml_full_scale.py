@@ -95,7 +95,7 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.reset_peak_memory_stats()
         t0 = time.time()
-        res = run_cv(pc, mc, ws, folds=5, device=dev, store=store, fold_ids=[args.fold], verbose=1)
+        res = run_cv(pc, mc, ws, folds=5, device=dev, store=store, fold_ids=[args.fold], verbose=2)
         f = res["per_fold"][0]
         secs = time.time() - t0
         out = {"auc": round(f["auc"], 4), "mcc": round(f["mcc"], 4), "n_train": f["n_train"], "n_test": f["n_test"],
