@@ -237,19 +237,9 @@ at::Tensor lstm_dx(const at::Tensor& dz, const at::Tensor& W, const at::Tensor& 
 
 int lstm_grads_col_blocks(int H) { return (4 * H) / GR_CB; }
 
-// With several column blocks the weight-gradient pass can only produce dx as ncb partial
-// slabs (summed afterwards): ncb writes + ncb reads + 1 write of a dx-sized tensor. One
-// lstm_dx pass re-reads dz instead (4H floats per row) and writes dx once: ~45% less HBM
-// traffic on paper, but measured slower on the SoilNet step (5.016 vs 4.944 ms/step:
-// lstm_dx re-converts dz to bf16 and runs at a fraction of the slab sum's bandwidth), so
-// it is opt-in: GNNQC_DX_DIRECT=1.
-bool lstm_dx_direct(int H, int Dw, int lddx) {
-  static const bool slabs = [] {
-    const char* e = std::getenv("GNNQC_DX_DIRECT");
-    return !(e != nullptr && e[0] == '1');
-  }();
-  return !slabs && lstm_grads_col_blocks(H) > 1 && Dw <= lddx && lddx % 4 == 0 && lddx <= 128;
-}
+// (A one-pass dx = dz W^T over all 4H gate-units instead of ncb slabs + their sum was measured
+// slower on the SoilNet step - 5.016 vs 4.944 ms - and removed; the time-major layers now take dx
+// from their recurrence instead, lstm_tm.hip tm_rec_dx.)
 
 // dz [M(p),T,4H] from lstm_bwd; x [M,T,Din] (unit inner stride, row stride ldx);
 // hseq [M,T,H]; W [Din,4H]. dW/dU/db are ACCUMULATED into (pass zeroed or existing
@@ -274,22 +264,16 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   TORCH_CHECK(Din + 1 <= 9 * 16, "gnnqc lstm_grads: input width ", Din, " too large (max 143)");
   c10::DeviceGuard guard(x.device());
   const int ncb = lstm_grads_col_blocks(H);
-  const bool direct = need_dx && lstm_dx_direct(H, Din, Din);
-  // dx = dz W^T contracts over all 4H gate-units: with several column blocks each
-  // block writes its partial product to its own slab (plain stores), summed below,
-  // unless one lstm_dx pass computes it (direct)
-  at::Tensor dx = need_dx ? at::empty({direct ? 1 : ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
+  // dx = dz W^T contracts over all 4H gate-units: with several column blocks each block writes
+  // its partial product to its own slab (plain stores), summed below
+  at::Tensor dx = need_dx ? at::empty({ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
   const long rows = (long)M * T;
   if (rows == 0) return need_dx ? dx.sum(0) : dx;
   lstm_grads_rows(dz.data_ptr(), dz_bf16(dz), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
-                  (need_dx && !direct) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                  need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                   db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, Din,
                   (long)(x.storage().nbytes() / sizeof(float)) - x.storage_offset(), stream());
   if (!need_dx) return dx;
-  if (direct) {
-    lstm_dx_rows(dz.data_ptr(), dz_bf16(dz), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Din, Din, stream());
-    return dx[0];
-  }
   return ncb == 1 ? dx[0] : dx.sum(0);
 }
 

@@ -38,7 +38,6 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
                      long dx_cb_stride, int lddx, long x_elems, hipStream_t st);
 int lstm_grads_col_blocks(int H);
-bool lstm_dx_direct(int H, int Dw, int lddx);
 void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows, int H, int Dw, int lddx,
                   hipStream_t st);
 
@@ -791,12 +790,9 @@ __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
 // host side
 // GNNQC_TM_RECDX=0: multi-column-block layers take dx from weight-gradient slabs + their sum
 // (the earlier layout) instead of from the recurrence
-static bool tm_rec_dx() {
-  static const bool on = [] {
-    const char* e = std::getenv("GNNQC_TM_RECDX");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  return on;
+static bool tm_rec_dx() {       // read per call (host side of a launch; tests toggle it)
+  const char* e = std::getenv("GNNQC_TM_RECDX");
+  return !(e != nullptr && e[0] == '0');
 }
 
 static int tm_granule(int Din, const void* x) {
@@ -1335,16 +1331,11 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
   const long rows = (long)T * Mp;
   const int ncb = lstm_grads_col_blocks(H);
   // padding channels (>= Dw) are written as zeros by the kernel (their W rows are masked)
-  const bool direct = need_dx && lstm_dx_direct(H, Dw, Din);   // one dz W^T pass instead of ncb slabs
-  at::Tensor dx = need_dx ? at::empty({direct ? 1 : ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
+  at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
   lstm_grads_rows(dz.data_ptr(), dz_bf16(dz), x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
-                  (need_dx && !direct) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                  need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                   db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, stream());
   if (!need_dx) return dx;
-  if (direct) {
-    lstm_dx_rows(dz.data_ptr(), dz_bf16(dz), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, Din, stream());
-    return dx[0];
-  }
   return ncb == 1 ? dx[0] : dx.sum(0);
 }
 
@@ -1412,16 +1403,11 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     const long rows = (long)T * Mp;
     const int ncb = lstm_grads_col_blocks(H);
     // dx keeps the x layout (Din channels); padding channels (>= Dw) get zero gradient
-    const bool direct = need_dx && lstm_dx_direct(H, Dw, Din);   // one dz W^T pass instead of ncb slabs
-    at::Tensor dx = need_dx ? at::empty({direct ? 1 : ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
+    at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
     lstm_grads_rows(dz.data_ptr(), 1, x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
-                    (need_dx && !direct) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                    need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                     db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, st);
     if (!need_dx) return dx;
-    if (direct) {
-      lstm_dx_rows(dz.data_ptr(), 1, W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Dw, Din, st);
-      return dx[0];
-    }
     return ncb == 1 ? dx[0] : dx.sum(0);
   }
   at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
