@@ -158,8 +158,9 @@ def main(argv=None):
         }
         if comm_us is not None:
             out["allreduce_us"] = round(comm_us, 2)        # mean RCCL all-reduce of the flat gradients
-            out["allreduce_mode"] = ("in-graph (timed standalone)" if trainer.dp_graph and trainer._multi_ok()
-                                     else "eager")
+            out["allreduce_mode"] = (("peer one-shot xGMI" if trainer.peer is not None else "RCCL") +
+                                     (" in-graph (timed standalone)" if trainer.dp_graph and trainer._multi_ok()
+                                      else " eager"))
         print(json.dumps(out), flush=True)
     D.destroy()
 

@@ -99,7 +99,13 @@ class Trainer:
         # DP over RCCL: the all-reduce is captured INSIDE the multi-step graph (gather -> forward ->
         # backward -> chain-timeout poison -> all-reduce -> guarded Adam, graph_steps times per
         # replay): no host round trip per step. gloo (host collectives) stays eager per step.
-        self.dp_graph = (self.collective and self.use_graph and D.backend() == "nccl"
+        # opt-in one-shot peer all-reduce over xGMI (GNNQC_PEER_ALLREDUCE=1, gnnqc.parallel.peer):
+        # a plain kernel, so it is captured in the step graph under any process-group backend
+        self.peer = None
+        if self.collective and self.device.type == "cuda":
+            from ..parallel.peer import make_peer_allreduce
+            self.peer = make_peer_allreduce(self.opt.flat_g.numel(), self.device)
+        self.dp_graph = (self.collective and self.use_graph and (D.backend() == "nccl" or self.peer is not None)
                          and os.environ.get("GNNQC_DP_GRAPH", "1") == "1")
         self.opt_graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
@@ -208,7 +214,13 @@ class Trainer:
             from ..ops.lstm import chain_ctl
             from ..utils.native import hip_ops
             hip_ops().chain_poison(self.opt.flat_g, chain_ctl(self.device))
-        D.all_reduce_(self.opt.flat_g, force=True)
+        self._all_reduce_flat()
+
+    def _all_reduce_flat(self):
+        if self.peer is not None:
+            self.peer(self.opt.flat_g)
+        else:
+            D.all_reduce_(self.opt.flat_g, force=True)
 
     @torch.no_grad()
     def measure_allreduce(self, n: int = 20) -> Optional[float]:
@@ -218,11 +230,11 @@ class Trainer:
         nothing."""
         if not self.collective or self.device.type != "cuda":
             return None
-        D.all_reduce_(self.opt.flat_g, force=True)
+        self._all_reduce_flat()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
         for a, b in ev:
             a.record()
-            D.all_reduce_(self.opt.flat_g, force=True)
+            self._all_reduce_flat()
             b.record()
         torch.cuda.synchronize()
         self.opt.zero_grad()
@@ -385,6 +397,8 @@ class Trainer:
             # steps rejected on the device after an LSTM chain spin timeout: fail loudly
             from ..ops.lstm import check_chain
             check_chain(self.device, rejected0)
+        if self.peer is not None and self.peer.timed_out():
+            raise RuntimeError("peer all-reduce: a rank never arrived (spin timeout); those steps were rejected")
         logs["windows_per_sec"] = nsteps * loader.batch_size * self.world / max(dt, 1e-9)
         if self._comm_events:
             logs["allreduce_us"] = 1e3 * sum(a.elapsed_time(b) for a, b in self._comm_events) / len(self._comm_events)

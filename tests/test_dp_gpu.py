@@ -49,7 +49,8 @@ torch.cuda.synchronize()
 bufs = torch.cat([b.reshape(-1).double() for b in m.buffers() if b.is_floating_point()])
 out = {"sum": float(x[0]), "p": opt.flat_p.double().sum().item(), "p2": (opt.flat_p.double() ** 2).sum().item(),
        "b": bufs.sum().item(), "steps": t.global_step, "loss": logs["loss"], "skipped": logs["skipped_steps"],
-       "dp_graph": bool(t.dp_graph), "multi": bool(t.multi_graph is not None), "ar_us": t.measure_allreduce()}
+       "dp_graph": bool(t.dp_graph), "multi": bool(t.multi_graph is not None), "ar_us": t.measure_allreduce(),
+       "peer": t.peer is not None}
 with open(os.path.join(os.environ["OUT"], f"r{rank}.json"), "w") as f:
     json.dump(out, f)
 torch.distributed.destroy_process_group()
@@ -104,5 +105,27 @@ def test_rccl_all_reduce_captured_in_multistep_graph(tmp_path):
     assert a["steps"] == 16 and a["skipped"] == 0 and a["ar_us"] is not None and a["ar_us"] > 0
     (b,) = _run(tmp_path / "b", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="0")
     assert not b["dp_graph"] and b["multi"] and b["steps"] == 16
+    for k in ("p", "p2", "loss"):
+        assert abs(a[k] - b[k]) <= 1e-4 * abs(b[k]) + 1e-6, (k, a[k], b[k])
+
+
+def test_peer_allreduce_two_ranks_one_gpu(tmp_path):
+    """One-shot peer all-reduce (IPC-registered regions, flag signalling, rank-order sum) between two
+    processes sharing the GPU: it verifies against gloo at setup, is captured in the multi-step
+    graph, and both ranks end with identical parameters."""
+    a, b = _run(tmp_path, 2, "gloo", NB="16", GNNQC_PEER_ALLREDUCE="1")
+    assert a["peer"] and b["peer"], "peer all-reduce must pass its verification against gloo"
+    assert a["dp_graph"] and a["multi"]
+    assert a["steps"] == b["steps"] == 16 and a["skipped"] == b["skipped"] == 0
+    assert a["p"] == b["p"] and a["p2"] == b["p2"]
+    assert a["ar_us"] is not None and a["ar_us"] > 0
+
+
+def test_peer_allreduce_matches_rccl_single_rank(tmp_path):
+    """The peer path on a one-rank nccl group with the chain kernels on trains like RCCL."""
+    (a,) = _run(tmp_path / "peer", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="1",
+                GNNQC_PEER_ALLREDUCE="1")
+    (b,) = _run(tmp_path / "rccl", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="1")
+    assert a["peer"] and not b["peer"] and a["dp_graph"] and a["multi"]
     for k in ("p", "p2", "loss"):
         assert abs(a[k] - b[k]) <= 1e-4 * abs(b[k]) + 1e-6, (k, a[k], b[k])
