@@ -25,6 +25,8 @@
 //                    channels with lane shuffles, plus the pass-through of the raw channels.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace gq {
 
 at::Tensor colsum(const at::Tensor& partial);     // gcn.hip
@@ -367,7 +369,11 @@ static NodeGeom node_geom(const at::Tensor& x, const at::Tensor& bits, const at:
   TORCH_CHECK(g.smem <= 150 * 1024, "gcn_node: graph too large for LDS (N=", g.N, ")");
   // enough workgroups to fill 256 CUs several times over
   const long steps = (long)g.B * g.T;
-  g.tchunk = (int)std::max<long>(1, std::min<long>(8, steps / 1024));
+  static const int tmax = [] {                 // steps per workgroup cap (A/B: GNNQC_NODE_TCHUNK)
+    const char* e = std::getenv("GNNQC_NODE_TCHUNK");
+    return e != nullptr ? std::max(1, std::atoi(e)) : 2;   // SoilNet: 2 best of 8 / 4 / 2 / 1 (bwd 238 -> 190 us)
+  }();
+  g.tchunk = (int)std::max<long>(1, std::min<long>(tmax, steps / 1024));
   g.grid = dim3((g.T + g.tchunk - 1) / g.tchunk, g.B);
   return g;
 }

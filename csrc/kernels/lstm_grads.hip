@@ -85,7 +85,11 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
   // ~2 tiles per workgroup for small row counts (latency: everything in flight at once),
   // up to ~8 workgroups per CU for large ones. The split count depends only on the shape
   // and the reduce kernel sums in a fixed order: bitwise reproducible in every mode.
-  const int splits = (int)std::max<long>(1, std::min<long>((ntiles + 1) / 2, std::max(64, 2048 / ncb)));
+  static const int wg_budget = [] {            // workgroups per pass (A/B: GNNQC_GRADS_WG)
+    const char* e = std::getenv("GNNQC_GRADS_WG");
+    return e != nullptr ? std::max(256, std::atoi(e)) : 2048;
+  }();
+  const int splits = (int)std::max<long>(1, std::min<long>((ntiles + 1) / 2, std::max(64, wg_budget / ncb)));
   const int DT = (Din + 1 + 15) / 16;
   const int HT = H / 16;
   const int grx = (ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) ? 4 : 1;
