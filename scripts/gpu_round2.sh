@@ -15,3 +15,5 @@ tail -1 $OUT/ig_bench.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_soil -o run --output-format csv -- python3 $ROOT/bench.py --ds soilnet --steps 10 --warmup 2 --no-graph > $OUT/prof_soil.log 2>&1
 echo "rocprof rc=$?"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_cml -o run --output-format csv -- python3 $ROOT/bench.py --steps 20 --warmup 3 --no-graph > $OUT/prof_cml.log 2>&1
+echo "rocprof cml rc=$?"
