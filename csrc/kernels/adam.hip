@@ -180,13 +180,18 @@ __global__ __launch_bounds__(256) void adam_guarded_kernel(
   // all arrived: no ordering needed. state[4] = 2 * generation + ok of the last decision.
   const int gen0 = __hip_atomic_load(state + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float step0 = __hip_atomic_load(step_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  float4 gg[K];
+  float4 gg[K], pq[K], mq[K], vq[K];
   float gt = 0.f;
   int bad = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const long i = i0 + k * stride;
-    gg[k] = i < n4 ? reinterpret_cast<const float4*>(g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool in = i < n4;
+    gg[k] = in ? reinterpret_cast<const float4*>(g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // p / m / v are loaded now too: their latency overlaps the grid-wide decision below
+    pq[k] = in ? reinterpret_cast<const float4*>(p)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    mq[k] = in ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    vq[k] = in ? reinterpret_cast<const float4*>(v)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     bad += !isfinite(gg[k].x) + !isfinite(gg[k].y) + !isfinite(gg[k].z) + !isfinite(gg[k].w);
   }
   const long it = n4 * 4 + i0;                   // (n % 4 tail: one element per thread at most)
@@ -244,9 +249,7 @@ __global__ __launch_bounds__(256) void adam_guarded_kernel(
       const long i = i0 + k * stride;
       if (i >= n4) break;
       reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      float4 pp = reinterpret_cast<float4*>(p)[i];
-      float4 mm = reinterpret_cast<float4*>(m)[i];
-      float4 vv = reinterpret_cast<float4*>(v)[i];
+      float4 pp = pq[k], mm = mq[k], vv = vq[k];
 #define GQ_ADAM_LANE(c)                                         \
       {                                                         \
         float gc = gg[k].c * gscale + wd * pp.c;                \
