@@ -229,7 +229,9 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_fwd_kernel(
 template <int H, bool BF16, int D>
 __global__ __launch_bounds__(64 * (H / 16)) void lstm_bwd_kernel(
     const float* __restrict__ dh_out, const float* __restrict__ gates, const float* __restrict__ cseq,
-    const float* __restrict__ U, float* __restrict__ dz_out, int M, int T) {
+    const float* __restrict__ U, void* __restrict__ dz_out, int M, int T) {
+  // BF16: dz is stored as bf16 (the weight-gradient / dx passes round it to bf16 for their MFMAs
+  // anyway: same results, half the bytes); fp32 reference mode keeps fp32 dz
   using C = LstmCfg<H, BF16>;
   constexpr int G4 = C::G4;
   constexpr int KB = C::KB;
@@ -323,11 +325,20 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_bwd_kernel(
         }
       }
       if (t >= 0) {   // wave-uniform
-        float* o = dz_out + ((size_t)seq * T + t) * G4 + u0;
-        st4(o + 0 * H, zi[0], zi[1], zi[2], zi[3]);
-        st4(o + 1 * H, zf[0], zf[1], zf[2], zf[3]);
-        st4(o + 2 * H, zg[0], zg[1], zg[2], zg[3]);
-        st4(o + 3 * H, zo[0], zo[1], zo[2], zo[3]);
+        if constexpr (BF16) {
+          typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+          __bf16* o = reinterpret_cast<__bf16*>(dz_out) + ((size_t)seq * T + t) * G4 + u0;
+          *reinterpret_cast<bf16x4_t*>(o + 0 * H) = bf16x4_t{(__bf16)zi[0], (__bf16)zi[1], (__bf16)zi[2], (__bf16)zi[3]};
+          *reinterpret_cast<bf16x4_t*>(o + 1 * H) = bf16x4_t{(__bf16)zf[0], (__bf16)zf[1], (__bf16)zf[2], (__bf16)zf[3]};
+          *reinterpret_cast<bf16x4_t*>(o + 2 * H) = bf16x4_t{(__bf16)zg[0], (__bf16)zg[1], (__bf16)zg[2], (__bf16)zg[3]};
+          *reinterpret_cast<bf16x4_t*>(o + 3 * H) = bf16x4_t{(__bf16)zo[0], (__bf16)zo[1], (__bf16)zo[2], (__bf16)zo[3]};
+        } else {
+          float* o = reinterpret_cast<float*>(dz_out) + ((size_t)seq * T + t) * G4 + u0;
+          st4(o + 0 * H, zi[0], zi[1], zi[2], zi[3]);
+          st4(o + 1 * H, zf[0], zf[1], zf[2], zf[3]);
+          st4(o + 2 * H, zg[0], zg[1], zg[2], zg[3]);
+          st4(o + 3 * H, zo[0], zo[1], zo[2], zo[3]);
+        }
       }
       lds_barrier();
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -395,7 +406,7 @@ template <int H, bool BF16>
 constexpr int bwd_ring() { return (H >= 128 || !BF16) ? 3 : 5; }   // 10 VMEM ops per step
 
 template <bool BF16>
-void launch_bwd(int H, const float* dh, const float* g, const float* c, const float* U, float* dz, int M, int T,
+void launch_bwd(int H, const float* dh, const float* g, const float* c, const float* U, void* dz, int M, int T,
                 hipStream_t st) {
   dim3 grid((M + 15) / 16);
   switch (H) {
@@ -459,11 +470,11 @@ at::Tensor lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Ten
                   cseq.size(0) == M && cseq.size(1) == T && cseq.size(2) == H, "lstm_bwd: shape mismatch");
   c10::DeviceGuard guard(dh.device());
   const int Mp = (M + 15) / 16 * 16;
-  at::Tensor dz = at::empty({Mp, T, 4 * H}, dh.options());
+  at::Tensor dz = at::empty({Mp, T, 4 * H}, dh.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
   if (M == 0 || T == 0) return dz.narrow(0, 0, M);
   auto st = stream();
-  if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
-  else launch_bwd<false>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr<float>(), M, T, st);
+  if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr(), M, T, st);
+  else launch_bwd<false>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr(), M, T, st);
   GQ_LAUNCH_CHECK();
   return Mp == M ? dz : dz.narrow(0, 0, M);
 }

@@ -268,16 +268,22 @@ at::Tensor lstm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Tenso
   TORCH_CHECK(Din + 1 <= 9 * 16, "gnnqc lstm_grads: input width ", Din, " too large (max 143)");
   c10::DeviceGuard guard(x.device());
   const int ncb = lstm_grads_col_blocks(H);
-  // dx = dz W^T contracts over all 4H gate-units: with several column blocks each block writes
-  // its partial product to its own slab (plain stores), summed below
-  at::Tensor dx = need_dx ? at::empty({ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
+  // dx = dz W^T contracts over all 4H gate-units: with a few column blocks each block writes its
+  // partial product to its own slab (plain stores), summed below; with 4+ (H >= 64) the slabs
+  // would cost ncb + 2 dx-sized passes, so one lstm_dx pass over dz produces dx instead
+  const bool onepass = need_dx && ncb >= 4 && Din % 4 == 0 && Din <= 128;
+  at::Tensor dx = need_dx ? at::empty({onepass ? 1 : ncb, M, T, Din}, x.options()) : at::empty({0}, x.options());
   const long rows = (long)M * T;
   if (rows == 0) return need_dx ? dx.sum(0) : dx;
   lstm_grads_rows(dz.data_ptr(), dz_bf16(dz), x.data_ptr<float>(), hseq.data_ptr<float>(), W.data_ptr<float>(),
-                  need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
+                  (need_dx && !onepass) ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                   db.data_ptr<float>(), rows, T, 1, H, Din, x.stride(1), rows * Din, Din,
                   (long)(x.storage().nbytes() / sizeof(float)) - x.storage_offset(), stream());
   if (!need_dx) return dx;
+  if (onepass) {
+    lstm_dx_rows(dz.data_ptr(), dz_bf16(dz), W.data_ptr<float>(), dx.data_ptr<float>(), rows, H, Din, Din, stream());
+    return dx[0];
+  }
   return ncb == 1 ? dx[0] : dx.sum(0);
 }
 

@@ -327,8 +327,13 @@ class _HipLSTM(torch.autograd.Function):
             db = dz2.sum(0) if ctx.needs_input_grad[3] else None
             return dx, dW, dU, db, None, None
         if not any(ctx.needs_input_grad[1:4]):
-            # frozen weights (integrated gradients): only dx = dz W^T, one library GEMM
-            dx = (dz.reshape(M * T, 4 * H) @ W.t()).view(M, T, Din) if ctx.needs_input_grad[0] else None
+            # frozen weights (integrated gradients): only dx = dz W^T (bf16 dz: one HIP pass)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                if Din % 4 == 0 and Din <= 128:
+                    dx = ops.lstm_dx(dz, W.contiguous(), x)
+                else:
+                    dx = (dz.reshape(M * T, 4 * H).float() @ W.t()).view(M, T, Din)
             return dx, None, None, None, None, None
         Wp, Up, bp = ctx.params
         gW, dW_in = _grad_sink(Wp)
