@@ -201,7 +201,7 @@ void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows,
   const int rw = ndin >= 3 ? 4 : ndin;
   const int ndt = (ndin + rw - 1) / rw;
   const long ngroups = ((rows + 15) / 16 + (4 / rw) - 1) / (4 / rw);
-  const int grid = (int)std::max<long>(1, std::min<long>(ngroups, 2048));
+  const int grid = (int)std::max<long>(1, std::min<long>(ngroups, 8192));   // one pass: latency-bound per tile
 #define GQ_DX(HH, RWV, ND)                                                                                          \
   do {                                                                                                              \
     if (zbf) hipLaunchKernelGGL((lstm_dx_kernel<HH, RWV, ND, __bf16>), dim3(grid), dim3(256), 0, st, dz, W, dx,     \
