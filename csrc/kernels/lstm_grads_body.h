@@ -129,7 +129,7 @@ __device__ __forceinline__ void lstm_grads_body(
   }
 
   // ---- per-tile register images (prefetch ring of depth 1)
-  float4 rz[2];                     // dz: rows tid/16 and tid/16 + 16, gate-units 4*(tid%16) ..
+  float4 rz[2];                     // dz: rows 2 (tid/16) and 2 (tid/16) + 1, gate-units 4*(tid%16) ..
   float rx[XGM][GRX];               // x granules of the contiguous [32][ldx] span
   float4 rh[HG];                    // h_{t-1} granules of the contiguous [32][H] span
   const int zr = tid >> 4, zc = (tid & 15) * 4;
@@ -141,7 +141,7 @@ __device__ __forceinline__ void lstm_grads_body(
     const long r0 = tile * GR_ROWS;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const long r = min(r0 + zr + 16 * q, rows - 1);
+      const long r = min(r0 + 2 * zr + q, rows - 1);
       if constexpr (ZBF) {
         const uint2 u = *reinterpret_cast<const uint2*>(dz + (size_t)r * G4 + gu0 + zc);
         rz[q] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
@@ -173,18 +173,24 @@ __device__ __forceinline__ void lstm_grads_body(
   };
   auto stage_tile = [&](long tile) {
     const long r0 = tile * GR_ROWS;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int rr = zr + 16 * q;
-      const float m = (r0 + rr < rows) ? 1.f : 0.f;
-      const __bf16 b0 = (__bf16)(rz[q].x * m), b1 = (__bf16)(rz[q].y * m), b2 = (__bf16)(rz[q].z * m),
-                   b3 = (__bf16)(rz[q].w * m);
+    {
+      // a lane holds rows 2 zr and 2 zr + 1 of its 4 gate-units: the transposed image gets one
+      // packed bf16x2 (4-byte) store per gate-unit instead of two 2-byte stores into a shared
+      // dword (LDS bank conflicts dominated this staging: rocprofv3 SQ_LDS_BANK_CONFLICT)
       typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      if constexpr (!CH) *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = bf16x4_t{b0, b1, b2, b3};
-      dzT[zc + 0][rr] = b0;
-      dzT[zc + 1][rr] = b1;
-      dzT[zc + 2][rr] = b2;
-      dzT[zc + 3][rr] = b3;
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      const int rr = 2 * zr;
+      const float m0 = (r0 + rr < rows) ? 1.f : 0.f, m1 = (r0 + rr + 1 < rows) ? 1.f : 0.f;
+      const bf16x4_t a = bf16x4_t{(__bf16)(rz[0].x * m0), (__bf16)(rz[0].y * m0), (__bf16)(rz[0].z * m0),
+                                  (__bf16)(rz[0].w * m0)};
+      const bf16x4_t b = bf16x4_t{(__bf16)(rz[1].x * m1), (__bf16)(rz[1].y * m1), (__bf16)(rz[1].z * m1),
+                                  (__bf16)(rz[1].w * m1)};
+      if constexpr (!CH) {
+        *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = a;
+        *reinterpret_cast<bf16x4_t*>(&dzR[rr + 1][zc]) = b;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16x2_t*>(&dzT[zc + j][rr]) = bf16x2_t{a[j], b[j]};
     }
 #pragma unroll
     for (int i = 0; i < XGM; ++i) {

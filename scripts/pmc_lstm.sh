@@ -9,6 +9,6 @@ P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_SALU SQ_LDS_
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-include-regex "${KRX:-lstm}" -d $OUT/p$i -o run --output-format csv -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-graph > $OUT/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-include-regex "${KRX:-lstm}" -d $OUT/p$i -o run --output-format csv -- python3 $ROOT/bench.py ${BENCH_ARGS:---steps 3 --warmup 1} --no-graph > $OUT/p$i.log 2>&1
   echo "pass $i rc=$?"
 done
