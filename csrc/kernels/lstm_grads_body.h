@@ -83,7 +83,8 @@ __device__ __forceinline__ void lstm_grads_body(
   constexpr int HT = H / 16;        // k tiles of dU
   constexpr int DP = DT * 16;       // padded din (incl. bias channel)
   constexpr int XGM = (GR_ROWS * 144 / GRX + 255) / 256;   // max x granules per thread
-  constexpr int HG = (GR_ROWS * H / 4 + 255) / 256;        // h float4 granules per thread
+  // h_{t-1} staging items: (row pair, 4-unit quad) -> 16 * H / 4 items, two float4 loads each
+  constexpr int HG = (GR_ROWS / 2 * H / 4 + 255) / 256;    // items per thread
   using L = GradsLds<H, DT>;
   static_assert(L::DZT % 16 == 0 && L::DZR % 16 == 0 && L::XT % 16 == 0, "grads LDS layout");
   auto dzT = reinterpret_cast<__bf16 (*)[GR_LDR]>(smem);                              // [gu][row]
@@ -131,10 +132,9 @@ __device__ __forceinline__ void lstm_grads_body(
   // ---- per-tile register images (prefetch ring of depth 1)
   float4 rz[2];                     // dz: rows 2 (tid/16) and 2 (tid/16) + 1, gate-units 4*(tid%16) ..
   float rx[XGM][GRX];               // x granules of the contiguous [32][ldx] span
-  float4 rh[HG];                    // h_{t-1} granules of the contiguous [32][H] span
+  float4 rh[HG][2];                 // h_{t-1}: rows 2p and 2p + 1 of unit quad c (item = p * H/4 + c)
   const int zr = tid >> 4, zc = (tid & 15) * 4;
   const long xspan = (long)GR_ROWS * ldx;
-  const long hspan = (long)GR_ROWS * H;
   // x_elems: floats readable from x (a strided view may end before rows * ldx)
   const long xlast = (x_elems - GRX) / GRX * GRX, hlast = rows * (long)H - 4;
   auto load_tile = [&](long tile) {
@@ -167,8 +167,10 @@ __device__ __forceinline__ void lstm_grads_body(
     }
 #pragma unroll
     for (int i = 0; i < HG; ++i) {
-      const long o = min(max((r0 - hshift) * H + min((long)(tid + 256 * i) * 4, hspan - 4), 0L), hlast);
-      rh[i] = *reinterpret_cast<const float4*>(hseq + o);
+      const int it = min(tid + 256 * i, GR_ROWS / 2 * H / 4 - 1);     // (idle lanes re-read the last item)
+      const long o = (r0 - hshift + 2 * (it / (H / 4))) * H + 4 * (it % (H / 4));
+      rh[i][0] = *reinterpret_cast<const float4*>(hseq + min(max(o, 0L), hlast));
+      rh[i][1] = *reinterpret_cast<const float4*>(hseq + min(max(o + H, 0L), hlast));
     }
   };
   auto stage_tile = [&](long tile) {
@@ -206,15 +208,18 @@ __device__ __forceinline__ void lstm_grads_body(
     if (tid < GR_ROWS) xT[Din][tid] = (__bf16)((r0 + tid < rows) ? 1.f : 0.f);   // bias channel
 #pragma unroll
     for (int i = 0; i < HG; ++i) {
-      const int g = (tid + 256 * i) * 4;
-      if (g < GR_ROWS * H) {
-        const int rr = g / H, k0 = g % H;
-        const long r = r0 + rr;
-        const float m = (r < rows && r % period >= hshift) ? 1.f : 0.f;
-        hT[k0 + 0][rr] = (__bf16)(rh[i].x * m);
-        hT[k0 + 1][rr] = (__bf16)(rh[i].y * m);
-        hT[k0 + 2][rr] = (__bf16)(rh[i].z * m);
-        hT[k0 + 3][rr] = (__bf16)(rh[i].w * m);
+      // one packed bf16x2 (rows 2p, 2p + 1) per unit: conflict-free across a wave's lanes
+      const int it = tid + 256 * i;
+      if (it < GR_ROWS / 2 * H / 4) {
+        const int rr = 2 * (it / (H / 4)), k0 = 4 * (it % (H / 4));
+        const long ra = r0 + rr, rb = ra + 1;
+        const float ma = (ra < rows && ra % period >= hshift) ? 1.f : 0.f;
+        const float mb = (rb < rows && rb % period >= hshift) ? 1.f : 0.f;
+        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<bf16x2_t*>(&hT[k0 + 0][rr]) = bf16x2_t{(__bf16)(rh[i][0].x * ma), (__bf16)(rh[i][1].x * mb)};
+        *reinterpret_cast<bf16x2_t*>(&hT[k0 + 1][rr]) = bf16x2_t{(__bf16)(rh[i][0].y * ma), (__bf16)(rh[i][1].y * mb)};
+        *reinterpret_cast<bf16x2_t*>(&hT[k0 + 2][rr]) = bf16x2_t{(__bf16)(rh[i][0].z * ma), (__bf16)(rh[i][1].z * mb)};
+        *reinterpret_cast<bf16x2_t*>(&hT[k0 + 3][rr]) = bf16x2_t{(__bf16)(rh[i][0].w * ma), (__bf16)(rh[i][1].w * mb)};
       }
     }
   };
