@@ -131,7 +131,11 @@ __device__ __forceinline__ void lstm_grads_body(
 
   // ---- per-tile register images (prefetch ring of depth 1)
   float4 rz[2];                     // dz: rows 2 (tid/16) and 2 (tid/16) + 1, gate-units 4*(tid%16) ..
-  float rx[XGM][GRX];               // x granules of the contiguous [32][ldx] span
+  // x: GRX == 4 -> items (row pair, 4-channel quad), two float4 each (packed bf16x2 staging);
+  // GRX == 1 (unaligned rows) -> single floats of the contiguous [32][ldx] span
+  constexpr int XGP = (GR_ROWS / 2 * 144 / 4 + 255) / 256;   // max pair items per thread
+  float rx[GRX == 4 ? 1 : XGM][GRX];
+  float4 rxp[GRX == 4 ? XGP : 1][2];
   float4 rh[HG][2];                 // h_{t-1}: rows 2p and 2p + 1 of unit quad c (item = p * H/4 + c)
   const int zr = tid >> 4, zc = (tid & 15) * 4;
   const long xspan = (long)GR_ROWS * ldx;
@@ -153,14 +157,22 @@ __device__ __forceinline__ void lstm_grads_body(
     // granule offsets are clamped into the tile's span (idle lanes re-read a line already
     // being fetched instead of the next tile's data) and into the array (rows past the end
     // and h_{t-1} of a period's first step are masked when staged)
+    if constexpr (GRX == 4) {
+      const int nq = ldx / 4, nit = GR_ROWS / 2 * nq;
 #pragma unroll
-    for (int i = 0; i < XGM; ++i) {
-      if (i < xg) {                               // kernel argument: a scalar (uniform) branch
-        const long o = min(r0 * ldx + min((long)(tid + 256 * i) * GRX, xspan - GRX), xlast);
-        if constexpr (GRX == 4) {
-          const float4 v = *reinterpret_cast<const float4*>(x + o);
-          rx[i][0] = v.x; rx[i][1] = v.y; rx[i][2] = v.z; rx[i][3] = v.w;
-        } else {
+      for (int i = 0; i < XGP; ++i) {
+        if (i < xg) {                             // kernel argument: a scalar (uniform) branch
+          const int it = min(tid + 256 * i, nit - 1);
+          const long o = (r0 + 2 * (it / nq)) * ldx + 4 * (it % nq);
+          rxp[i][0] = *reinterpret_cast<const float4*>(x + min(o, xlast));
+          rxp[i][1] = *reinterpret_cast<const float4*>(x + min(o + ldx, xlast));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XGM; ++i) {
+        if (i < xg) {                             // kernel argument: a scalar (uniform) branch
+          const long o = min(r0 * ldx + min((long)(tid + 256 * i) * GRX, xspan - GRX), xlast);
           rx[i][0] = x[o];
         }
       }
@@ -194,15 +206,32 @@ __device__ __forceinline__ void lstm_grads_body(
 #pragma unroll
       for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16x2_t*>(&dzT[zc + j][rr]) = bf16x2_t{a[j], b[j]};
     }
+    if constexpr (GRX == 4) {
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      const int nq = ldx / 4, nit = GR_ROWS / 2 * nq;
 #pragma unroll
-    for (int i = 0; i < XGM; ++i) {
-      const long g = (long)(tid + 256 * i) * GRX;
-      if (i < xg && g < xspan) {                  // xg: wave-uniform (kernel argument)
-        const int rr = (int)(g / ldx), d0 = (int)(g % ldx);
-        const float m = (r0 + rr < rows) ? 1.f : 0.f;
+      for (int i = 0; i < XGP; ++i) {
+        const int it = tid + 256 * i;
+        if (i < xg && it < nit) {                 // one packed bf16x2 (rows 2p, 2p + 1) per channel
+          const int rr = 2 * (it / nq), d0 = 4 * (it % nq);
+          const float ma = (r0 + rr < rows) ? 1.f : 0.f, mb = (r0 + rr + 1 < rows) ? 1.f : 0.f;
+          const float a[4] = {rxp[i][0].x, rxp[i][0].y, rxp[i][0].z, rxp[i][0].w};
+          const float b[4] = {rxp[i][1].x, rxp[i][1].y, rxp[i][1].z, rxp[i][1].w};
 #pragma unroll
-        for (int q = 0; q < GRX; ++q)
-          if (d0 + q < Din) xT[d0 + q][rr] = (__bf16)(rx[i][q] * m);
+          for (int q = 0; q < 4; ++q)
+            if (d0 + q < Din)
+              *reinterpret_cast<bf16x2_t*>(&xT[d0 + q][rr]) = bf16x2_t{(__bf16)(a[q] * ma), (__bf16)(b[q] * mb)};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XGM; ++i) {
+        const long g = (long)(tid + 256 * i) * GRX;
+        if (i < xg && g < xspan) {                // xg: wave-uniform (kernel argument)
+          const int rr = (int)(g / ldx), d0 = (int)(g % ldx);
+          const float m = (r0 + rr < rows) ? 1.f : 0.f;
+          if (d0 < Din) xT[d0][rr] = (__bf16)(rx[i][0] * m);
+        }
       }
     }
     if (tid < GR_ROWS) xT[Din][tid] = (__bf16)((r0 + tid < rows) ? 1.f : 0.f);   // bias channel
