@@ -106,6 +106,7 @@ __global__ void grad_guard_kernel(const float* __restrict__ g, long n, int* __re
       if (ext != nullptr) {
         stale = atomicExch(&ext[2], 0);
         if (stale) atomicAdd(&ext[3], 1);
+        atomicExch(&ext[7], 0);                  // producer flag (adam_flagged): the scan covers it
       }
       const int ok = cnt == 0 && stale == 0;
       state[2] = ok;
@@ -215,6 +216,7 @@ __global__ __launch_bounds__(256) void adam_guarded_kernel(
       if (ext != nullptr) {
         stale = __hip_atomic_exchange(ext + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (stale) __hip_atomic_fetch_add(ext + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ext + 7, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (the scan covers it)
       }
       ok = nbad == 0 && stale == 0;
       if (ok) step_p[0] = step0 + 1.0f;
@@ -334,6 +336,123 @@ bool adam_guarded(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const 
   return false;
 }
 
+// Adam with the step decision taken from FLAGS instead of a grid-wide scan of g: every kernel that
+// writes this step's gradients (the CML training step: time4 / head, the LSTM weight-gradient
+// reduction, the fused GCN backward) raises ext[7] when a value it adds is not finite; the LSTM
+// chain raises ext[2] on a spin timeout; in data parallel, chain_poison turns either flag into a
+// NaN in g[0] before the all-reduce, so every rank sees it there. Every workgroup reads ext[2],
+// ext[7] and g[0] BEFORE its arrival ticket, and only the last arrival clears them (and g[0], which
+// the update otherwise leaves to it), so all workgroups take the same decision without waiting for
+// each other: no co-residency assumption, no spin (adam_guarded's grid-wide barrier cost ~8 us).
+// A gradient element that is not finite although no producer flagged (fp32 overflow of a sum of
+// finite parts) leaves its parameter and slots untouched and is counted in state[5].
+__global__ __launch_bounds__(256) void adam_flagged_kernel(
+    float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ lr_p, float* __restrict__ step_p, long n, float b1, float b2, float eps, float gscale,
+    float wd, int* __restrict__ state, int* __restrict__ ext, long* __restrict__ cursor, long cursor_mod) {
+  const int tid = threadIdx.x;
+  const float step0 = __hip_atomic_load(step_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int timeout = __hip_atomic_load(ext + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nonfin = __hip_atomic_load(ext + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float g0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool ok = timeout == 0 && nonfin == 0 && isfinite(g0);
+  const long n4 = n / 4;
+  const long i = blockIdx.x * (long)blockDim.x + tid;
+  int skipped = 0;
+  if (i < n4) {
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    if (ok) {
+      float4 pp = reinterpret_cast<const float4*>(p)[i];
+      float4 mm = reinterpret_cast<const float4*>(m)[i];
+      float4 vv = reinterpret_cast<const float4*>(v)[i];
+      const float step = step0 + 1.0f;
+      const float alpha = *lr_p * sqrtf(1.0f - powf(b2, step)) / (1.0f - powf(b1, step));
+#define GQ_ADAMF_LANE(c)                                          \
+      if (isfinite(gg.c)) {                                       \
+        const float gc = gg.c * gscale + wd * pp.c;               \
+        mm.c = b1 * mm.c + (1.f - b1) * gc;                       \
+        vv.c = b2 * vv.c + (1.f - b2) * gc * gc;                  \
+        pp.c -= alpha * mm.c / (sqrtf(vv.c) + eps);               \
+      } else {                                                    \
+        ++skipped;                                                \
+      }
+      GQ_ADAMF_LANE(x) GQ_ADAMF_LANE(y) GQ_ADAMF_LANE(z) GQ_ADAMF_LANE(w)
+#undef GQ_ADAMF_LANE
+      reinterpret_cast<float4*>(p)[i] = pp;
+      reinterpret_cast<float4*>(m)[i] = mm;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    // g[0] stays until the last arrival clears it: every workgroup reads it first
+    reinterpret_cast<float4*>(g)[i] = make_float4(i == 0 ? gg.x : 0.f, 0.f, 0.f, 0.f);
+  }
+  const long it = n4 * 4 + i;                    // (n % 4 tail: one element per thread at most)
+  if (it < n) {
+    const float gt = g[it];
+    g[it] = 0.f;
+    if (ok && isfinite(gt)) {
+      const float step = step0 + 1.0f;
+      const float alpha = *lr_p * sqrtf(1.0f - powf(b2, step)) / (1.0f - powf(b1, step));
+      const float gc = gt * gscale + wd * p[it];
+      m[it] = b1 * m[it] + (1.f - b1) * gc;
+      v[it] = b2 * v[it] + (1.f - b2) * gc * gc;
+      p[it] -= alpha * m[it] / (sqrtf(v[it]) + eps);
+    } else if (ok) {
+      ++skipped;
+    }
+  }
+  if (skipped) atomicAdd(state + 5, skipped);
+  __shared__ int last;
+  // Every thread's reads of the flags / g[0] have returned (their values decided `ok` above), so a
+  // plain s_barrier (no vmcnt drain of this workgroup's stores) and a relaxed ticket suffice: the
+  // last arrival's clears cannot overtake a read that has completed. (An acq_rel ticket or
+  // __syncthreads() here waited for every store of the update: ~6 us.)
+  __builtin_amdgcn_s_barrier();
+  if (tid == 0) last = __hip_atomic_fetch_add(state + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       (int)gridDim.x - 1;
+  lds_barrier();
+  if (!last || tid != 0) return;
+  __hip_atomic_store(state + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  g[0] = 0.f;
+  if (ok) step_p[0] = step0 + 1.0f;
+  else __hip_atomic_fetch_add(state + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(state + 2, ok ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (timeout) {
+    __hip_atomic_store(ext + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(ext + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (nonfin) __hip_atomic_store(ext + 7, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (cursor != nullptr) cursor[0] = (cursor[0] + 1) % cursor_mod;
+}
+
+void adam_flagged(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const at::Tensor& lr, at::Tensor step,
+                  double b1, double b2, double eps, double gscale, double wd, at::Tensor state, at::Tensor ext,
+                  const c10::optional<at::Tensor>& cursor, int64_t cursor_mod) {
+  const at::Tensor* ops[] = {&p, &g, &m, &v, &lr, &step};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "adam operand");
+  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kInt && state.numel() >= 6 && state.is_contiguous(),
+              "adam_flagged: state must be int32[>=6] on the device");
+  TORCH_CHECK(ext.is_cuda() && ext.scalar_type() == at::kInt && ext.numel() >= 8, "adam_flagged: ext int32[8]");
+  const long n = p.numel();
+  TORCH_CHECK(n >= 4 && g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) % 16) == 0 &&
+                  (reinterpret_cast<uintptr_t>(m.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(v.data_ptr()) % 16) == 0,
+              "adam: buffers must be 16-byte aligned");
+  long* cp = nullptr;
+  if (cursor.has_value() && cursor->defined()) {
+    TORCH_CHECK(cursor->is_cuda() && cursor->scalar_type() == at::kLong && cursor->numel() >= 1 && cursor_mod >= 1,
+                "adam_flagged: cursor int64[1], cursor_mod >= 1");
+    cp = cursor->data_ptr<int64_t>();
+  }
+  c10::DeviceGuard guard(p.device());
+  const long work = std::max<long>(n / 4, n % 4);
+  const int grid = (int)((work + 255) / 256);
+  hipLaunchKernelGGL(adam_flagged_kernel, dim3(grid), dim3(256), 0, stream(), p.data_ptr<float>(), g.data_ptr<float>(),
+                     m.data_ptr<float>(), v.data_ptr<float>(), lr.data_ptr<float>(), step.data_ptr<float>(), n,
+                     (float)b1, (float)b2, (float)eps, (float)gscale, (float)wd, state.data_ptr<int>(),
+                     ext.data_ptr<int>(), cp, cursor_mod);
+  GQ_LAUNCH_CHECK();
+}
+
 at::Tensor nonfinite_count(const at::Tensor& x) {
   check_f32_cuda(x, "x");
   c10::DeviceGuard guard(x.device());
@@ -349,15 +468,17 @@ at::Tensor nonfinite_count(const at::Tensor& x) {
 // Data parallel: a chain spin timeout on ONE rank must reject the step on EVERY rank. Before the
 // gradient all-reduce, a rank whose chain timed out (ext[2] != 0) writes NaN into g[0]; the SUM
 // spreads it and every rank's guard skips the step (the local guard still counts the timeout).
+// ext[7] (a gradient producer saw a non-finite value, adam_flagged) poisons the same way.
 __global__ void chain_poison_kernel(float* __restrict__ g, const int* __restrict__ ext) {
-  if (threadIdx.x == 0 && __hip_atomic_load(ext + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+  if (threadIdx.x == 0 && (__hip_atomic_load(ext + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                           __hip_atomic_load(ext + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
     g[0] = __builtin_nanf("");
 }
 
 void chain_poison(at::Tensor g, const at::Tensor& ext) {
   check_f32_cuda(g, "g");
-  TORCH_CHECK(ext.is_cuda() && ext.scalar_type() == at::kInt && ext.numel() >= 4 && ext.get_device() == g.get_device(),
-              "chain_poison: ext must be int32[4] on the gradient's device");
+  TORCH_CHECK(ext.is_cuda() && ext.scalar_type() == at::kInt && ext.numel() >= 8 && ext.get_device() == g.get_device(),
+              "chain_poison: ext must be int32[8] on the gradient's device");
   TORCH_CHECK(g.numel() >= 1, "chain_poison: empty gradient buffer");
   c10::DeviceGuard guard(g.device());
   hipLaunchKernelGGL(chain_poison_kernel, dim3(1), dim3(64), 0, stream(), g.data_ptr<float>(), ext.data_ptr<int>());
@@ -372,4 +493,5 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("nonfinite_count", &gq::nonfinite_count);
   m.impl("grad_guard", &gq::grad_guard);
   m.impl("adam_guarded", &gq::adam_guarded);
+  m.impl("adam_flagged", &gq::adam_flagged);
 }

@@ -419,6 +419,8 @@ __device__ void chain_head_bwd_reduce(const ChainHead& hd, int tile, int ntiles)
       const int e = e0 + q * (int)blockDim.x;
       if (e >= e1) break;
       const float s = acc[q];
+      // (adam_flagged decides the step from such flags instead of scanning the gradient buffer)
+      if (!isfinite(s)) __hip_atomic_store(hd.ctl + 7, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int o = e;
       if (o < F * CH_HU) { hd.dW1[o] += s; continue; }
       o -= F * CH_HU;

@@ -1,0 +1,698 @@
+// Training-step GeneralConv + BatchNorm + PReLU + node pooling, fused with the window gather
+// (SURVEY §2.2 K1 + K2 + K12; reference: spektral GeneralConv at libs/create_model.py:184-189,
+// timeseries_pooling :8-41, Concatenate :223, the window parse libs/preprocessing_functions.py:566-666).
+//
+// The generic path is three launches before the LSTM chain: batch_gather (cut + normalise the
+// windows into x [B,T,N,C]), gcn_prep (per-sample pooling weights + fp64 moments of x, the last
+// workgroup sums them and preps BatchNorm) and gcn_pool_fwd (x -> the time-major LSTM input).
+// Everything gcn_prep computes per sample depends only on the WINDOW (its normalised series, its
+// node mask, its group's adjacency), not on the model, so it is computed once per store
+// (gcn_window_prep: moments [nwin][nstat] fp64 + pooling weights [nwin][N]). A training step then
+// needs ONE launch: every workgroup sums the batch's B moment records in a fixed order (the same
+// order in every workgroup: identical, deterministic statistics, no cross-workgroup hand-off),
+// preps BatchNorm for itself, cuts its rows of ONE window straight from the resident series into
+// LDS and writes the time-major LSTM input [T][Mp][Cp] = [flagged series | pooled | 0 pad].
+// Workgroup (0, 0) also writes S / st for the backward and applies the Keras running-stat update.
+//
+// Backward (gcn_fused_bwd): the closed-form BatchNorm/PReLU/pooling parameter gradient is LINEAR
+// in the per-row partial sums (A = sum dy, Z = sum dy z, P = sum da y[y<=0], Q_k = sum x_k dy), so
+// every workgroup maps its own partial sums to dW, dgamma, dbeta, dalpha contributions and adds them
+// with float atomics: no partial-record workspace and no finalize launch (not bitwise
+// reproducible: the deterministic mode keeps the generic path).
+#include "common.h"
+
+namespace gq {
+
+int* chain_ctl(int dev);   // lstm_chain.hip: word 7 = a gradient producer saw a non-finite value
+
+constexpr int GF_MAX_CIN = 4;
+constexpr int GF_ROW_MAX = 128;        // N * Cin floats per staged row
+constexpr int GF_RPP = 64;             // rows per pass (4 threads per row, 256 threads)
+
+struct GfData {                        // the resident window store (gnnqc.data.store.DeviceStore)
+  const float* series;                 // [G][Ttot][N][C]
+  const float* shift;                  // [G][Tn][N][C]
+  const float* scale;
+  const long* wg;                      // window -> group
+  const long* wc;                      // window -> centre time index
+  const uint8_t* wv;                   // [nwin][N] node valid
+  const float* wlab;                   // [nwin] label
+  const long* gap;                     // [G] flagged node position
+  const double* mom;                   // [nwin][nstat] (gcn_window_prep)
+  const float* pw;                     // [nwin][N]
+  const long* wids;                    // [B] ids, or
+  const long* table;                   // [nrows][B] + cursor
+  const long* cursor;
+  long nrows;
+  int Ttot, Tn, N, tb, T, time_norm;
+};
+
+__device__ __forceinline__ const long* gf_ids(const GfData& D, int B) {
+  return D.cursor != nullptr ? D.table + (D.cursor[0] % D.nrows) * B : D.wids;
+}
+
+// ---- per-window precompute: one workgroup per window
+template <int Cin>
+__global__ __launch_bounds__(256) void gcn_window_prep_kernel(GfData D, const float* __restrict__ gadj,
+                                                              int agg_mean, int pool, int nwin,
+                                                              double* __restrict__ mom, float* __restrict__ pw) {
+  constexpr int nstat = Cin + Cin * Cin + 1;
+  const int w = blockIdx.x, tid = threadIdx.x, N = D.N;
+  extern __shared__ float sh_[];      // vm [N], coef [N]
+  float* svm = sh_;
+  float* coef = sh_ + N;
+  __shared__ float red[4];
+  __shared__ double dred[4][nstat];
+  const long g = D.wg[w];
+  for (int n = tid; n < N; n += 256) svm[n] = D.wv[(long)w * N + n] ? 1.f : 0.f;
+  __syncthreads();
+  // pooling weights (gcn_glue.hip gcn_prep_kernel, on the masked group adjacency)
+  const float* A = gadj + g * (long)N * N;
+  float ms = 0.f;
+  for (int i = tid; i < N; i += 256) ms += svm[i];
+  ms = wave_sum(ms);
+  if ((tid & 63) == 0) red[tid >> 6] = ms;
+  __syncthreads();
+  ms = red[0] + red[1] + red[2] + red[3];
+  const long ap = D.gap[g];
+  for (int i = tid; i < N; i += 256) {
+    float p;
+    if (pool == 0) p = svm[i] / fmaxf(ms, 1.f);
+    else if (pool == 1) p = svm[i];
+    else p = (i == (ap < 0 ? 0 : ap)) ? 1.f : 0.f;
+    float c = p;
+    if (agg_mean && p != 0.f) {
+      float deg = 0.f;
+      for (int j = 0; j < N; ++j) deg += A[(long)i * N + j] * svm[i] * svm[j];
+      c = p / fmaxf(deg, 1.f);
+    }
+    coef[i] = c;
+  }
+  __syncthreads();
+  for (int j = tid; j < N; j += 256) {
+    float s = 0.f;
+    for (int i = 0; i < N; ++i) s += coef[i] * (A[(long)i * N + j] * svm[i] * svm[j]);
+    pw[(long)w * N + j] = s;
+  }
+  // fp64 moments of the window's normalised values over its T x N rows (masked rows: zeros)
+  const int NC = N * Cin;
+  const long c0 = D.wc[w];
+  const float* src = D.series + (g * D.Ttot + (c0 - D.tb)) * (long)NC;
+  const long tn = D.time_norm ? c0 : 0;
+  const float* shp = D.shift + (g * D.Tn + tn) * (long)NC;
+  const float* scp = D.scale + (g * D.Tn + tn) * (long)NC;
+  double acc[nstat];
+#pragma unroll
+  for (int i = 0; i < nstat; ++i) acc[i] = 0.0;
+  const int R = D.T * N;
+  for (int r = tid; r < R; r += 256) {
+    const int n = r % N;
+    const float m = svm[n];
+    float xv[Cin];
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) {
+      const int e = n * Cin + k;
+      xv[k] = (src[(long)r * Cin + k] - shp[e]) * scp[e] * m;
+    }
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) {
+      const float mx = m * xv[k];
+      acc[k] += mx;
+#pragma unroll
+      for (int l = 0; l < Cin; ++l) acc[Cin + k * Cin + l] += (double)mx * xv[l];
+    }
+    acc[nstat - 1] += m;
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < nstat; ++i) {
+    double v = acc[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) dred[wv][i] = v;
+  }
+  __syncthreads();
+  if (tid < nstat) mom[(long)w * nstat + tid] = (dred[0][tid] + dred[1][tid]) + (dred[2][tid] + dred[3][tid]);
+}
+
+// ---- step kernels. A workgroup owns `rows` consecutive steps of ONE sample's window. Every load
+// of a pass is issued before the first wait (the slab of series values, the node tables, the
+// parameters, the batch's moment records, the upstream gradient): one memory round trip after the
+// id -> window chain, instead of one per dependent stage.
+constexpr int GF_SLAB = 4096;          // floats of series staged per pass (16 per thread)
+constexpr int GF_SPT = GF_SLAB / 256;
+
+__device__ __forceinline__ int gf_rows_per_pass(int NC) { return min(GF_RPP, GF_SLAB / NC); }
+
+// issue the loads of rows [t0, t0 + nr) of a window (contiguous NC floats per row) into registers
+__device__ __forceinline__ void gf_slab_load(const float* __restrict__ src, int n, float (&v)[GF_SPT]) {
+#pragma unroll
+  for (int u = 0; u < GF_SPT; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    v[u] = i < n ? src[i] : 0.f;
+  }
+}
+
+// normalise the loaded values into sx[n] (element i: node (i % NC) / Cin, channel i % Cin)
+template <int Cin>
+__device__ __forceinline__ void gf_slab_park(const float (&v)[GF_SPT], int n, int NC, const float* svm,
+                                             const float* ssh, const float* ssc, float* sx) {
+  int e = threadIdx.x % NC;
+  const int step = 256 % NC;
+#pragma unroll
+  for (int u = 0; u < GF_SPT; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i < n) sx[i] = (v[u] - ssh[e]) * ssc[e] * svm[e / Cin];
+    e += step;
+    if (e >= NC) e -= NC;
+  }
+}
+
+// ---- forward: grid (Mp, NY), 256 threads
+template <int Cin, int F>
+__global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
+    GfData D, int B, int Mp, int Cp, int rows, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ alpha,
+    float* __restrict__ rmean, float* __restrict__ rvar, int training, float momentum, float eps,
+    float* __restrict__ out, double* __restrict__ Sout, float* __restrict__ st, float* __restrict__ y,
+    float* __restrict__ ym, long* __restrict__ wid_out) {
+  constexpr int nstat = Cin + Cin * Cin + 1;
+  constexpr int FQ = F / 4;
+  constexpr int Ca = Cin;
+  const int b = blockIdx.x, tid = threadIdx.x, N = D.N, T = D.T;
+  const int t0 = blockIdx.y * rows, t1 = min(T, t0 + rows);
+  if (b >= B) {                                   // padding sequences of the time-major input: zeros
+    for (int t = t0; t < t1; ++t)
+      for (int c = tid; c < Cp; c += 256) out[((long)t * Mp + b) * Cp + c] = 0.f;
+    return;
+  }
+  __shared__ double dred[4][nstat];
+  __shared__ double S[nstat];
+  __shared__ float prm[Cin + 2][F];             // W' = W * scale, b' = b * scale + shift, alpha
+  __shared__ float svm[GF_ROW_MAX], spw[GF_ROW_MAX], ssh[GF_ROW_MAX], ssc[GF_ROW_MAX];
+  __shared__ __attribute__((aligned(16))) float sx[GF_SLAB];
+  const int NC = N * Cin;
+  const int RP = gf_rows_per_pass(NC);
+  // ---- phase A: all loads
+  const long* ids = gf_ids(D, B);
+  const long wraw = ids[b];
+  const long w = wraw < 0 ? 0 : wraw;
+  const float live = wraw >= 0 ? 1.f : 0.f;
+  const long g = D.wg[w], c0 = D.wc[w];
+  const long tn = D.time_norm ? c0 : 0;
+  float pv[Cin + 6];                              // this thread's parameter column (tid < F)
+  if (tid < F) {
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) pv[k] = W[k * F + tid];
+    pv[Cin] = bias[tid];
+    pv[Cin + 1] = gamma[tid];
+    pv[Cin + 2] = beta[tid];
+    pv[Cin + 3] = alpha[tid];
+    pv[Cin + 4] = rmean[tid];
+    pv[Cin + 5] = rvar[tid];
+  }
+  float nv = 0.f, npw = 0.f, nsh = 0.f, nsc = 0.f;
+  if (tid < N) {
+    nv = D.wv[w * N + tid] ? live : 0.f;
+    npw = D.pw[w * N + tid] * live;
+  }
+  if (tid < NC) {
+    nsh = D.shift[(g * D.Tn + tn) * (long)NC + tid];
+    nsc = D.scale[(g * D.Tn + tn) * (long)NC + tid];
+  }
+  double mv[nstat];
+#pragma unroll
+  for (int i = 0; i < nstat; ++i) mv[i] = 0.0;
+  if (training) {                                 // the batch's moments: B window records
+    for (int k = tid; k < B; k += 256) {
+      const long wk = ids[k];
+      if (wk >= 0) {
+#pragma unroll
+        for (int i = 0; i < nstat; ++i) mv[i] += D.mom[wk * nstat + i];
+      }
+    }
+  }
+  float v[GF_SPT];
+  const float* src = D.series + (g * D.Ttot + (c0 - D.tb)) * (long)NC;
+  int nr = min(RP, t1 - t0);
+  gf_slab_load(src + (long)t0 * NC, nr * NC, v);
+  // ---- phase B
+  if (tid < N) {
+    svm[tid] = nv;
+    spw[tid] = npw;
+  }
+  if (tid < NC) {
+    ssh[tid] = nsh;
+    ssc[tid] = nsc;
+  }
+  if (training) {                                 // fixed-order reduction: identical in every workgroup
+    const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < nstat; ++i) {
+      double sv = mv[i];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+      if (lane == 0) dred[wv][i] = sv;
+    }
+  }
+  __syncthreads();
+  if (training && tid < nstat) S[tid] = (dred[0][tid] + dred[1][tid]) + (dred[2][tid] + dred[3][tid]);
+  gf_slab_park<Cin>(v, nr * NC, NC, svm, ssh, ssc, sx);
+  __syncthreads();
+  if (tid < F) {
+    float mu, var;
+    if (training) {
+      const double cnt = fmax(S[Cin + Cin * Cin], 1.0);
+      double ex[Cin];
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) ex[k] = S[k] / cnt;
+      double m = pv[Cin], vv = 0.0;
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) {
+        m += ex[k] * (double)pv[k];
+#pragma unroll
+        for (int l = 0; l < Cin; ++l) vv += (double)pv[k] * (S[Cin + k * Cin + l] / cnt - ex[k] * ex[l]) * (double)pv[l];
+      }
+      mu = (float)m;
+      var = (float)fmax(vv, 0.0);
+    } else {
+      mu = pv[Cin + 4];
+      var = pv[Cin + 5];
+    }
+    const float inv = rsqrtf(var + eps);
+    const float sc = pv[Cin + 1] * inv;
+    const float sh = pv[Cin + 2] - mu * sc;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) prm[k][tid] = pv[k] * sc;
+    prm[Cin][tid] = pv[Cin] * sc + sh;
+    prm[Cin + 1][tid] = pv[Cin + 3];
+    if (b == 0 && blockIdx.y == 0) {
+      st[tid] = mu;
+      st[F + tid] = inv;
+      st[2 * F + tid] = sc;
+      st[3 * F + tid] = sh;
+      if (training) {
+        rmean[tid] = pv[Cin + 4] * momentum + mu * (1.f - momentum);
+        rvar[tid] = pv[Cin + 5] * momentum + var * (1.f - momentum);
+      }
+    }
+  }
+  if (b == 0 && blockIdx.y == 0 && training && tid < nstat) Sout[tid] = S[tid];
+  if (blockIdx.y == 0 && tid == 0) {
+    y[b] = D.wlab[w] * live;
+    ym[b] = live;
+    wid_out[b] = wraw;
+  }
+  __syncthreads();
+  const long apl = D.gap[g];
+  const int ap = apl < 0 ? 0 : (int)apl;
+  const int r = tid >> 2, q = tid & 3, f0 = q * FQ;
+  float pwk[Cin][FQ], pb[FQ], pal[FQ];
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) pwk[k][j] = prm[k][f0 + j];
+    pb[j] = prm[Cin][f0 + j];
+    pal[j] = prm[Cin + 1][f0 + j];
+  }
+  for (int p0 = t0; p0 < t1; p0 += RP) {
+    if (p0 != t0) {                               // (more rows than one pass: stage the next slab)
+      nr = min(RP, t1 - p0);
+      gf_slab_load(src + (long)p0 * NC, nr * NC, v);
+      __syncthreads();
+      gf_slab_park<Cin>(v, nr * NC, NC, svm, ssh, ssc, sx);
+      __syncthreads();
+    }
+    for (int rr = r; rr < nr; rr += 64) {
+      const int t = p0 + rr;
+      float acc[FQ];
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) acc[j] = 0.f;
+      const float* xr = sx + rr * NC;
+      for (int n = 0; n < N; ++n) {
+        const float wn = spw[n];
+        float xv[Cin];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
+#pragma unroll
+        for (int j = 0; j < FQ; ++j) {
+          float yv = pb[j];
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) yv += xv[k] * pwk[k][j];
+          acc[j] += wn * (yv > 0.f ? yv : pal[j] * yv);
+        }
+      }
+      float* o = out + ((long)t * Mp + b) * Cp;
+      if (q < Ca) o[q] = xr[ap * Cin + q];
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) o[Ca + f0 + j] = acc[j];
+      for (int c = Ca + F + q; c < Cp; c += 4) o[c] = 0.f;
+    }
+  }
+}
+
+// ---- backward (training): grid (B, NY), 256 threads; parameter gradients added with float atomics
+template <int Cin, int F>
+__global__ __launch_bounds__(256) void gcn_fused_bwd_kernel(
+    GfData D, int B, int Mp, int Dh, int c_off, int rows, const float* __restrict__ dh,
+    const double* __restrict__ Sg, const float* __restrict__ st, const float* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ alpha, float* __restrict__ dW,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dalpha, int* __restrict__ nf) {
+  constexpr int FQ = F / 4;
+  constexpr int NA = 3 + Cin;
+  const int b = blockIdx.x, tid = threadIdx.x, N = D.N, T = D.T;
+  const int t0 = blockIdx.y * rows, t1 = min(T, t0 + rows);
+  __shared__ float svm[GF_ROW_MAX], spw[GF_ROW_MAX], ssh[GF_ROW_MAX], ssc[GF_ROW_MAX];
+  __shared__ __attribute__((aligned(16))) float sx[GF_SLAB];
+  __shared__ float red[4][NA][F];
+  const int NC = N * Cin;
+  const int RP = gf_rows_per_pass(NC);
+  const int r = tid >> 2, q = tid & 3, f0 = q * FQ;
+  // ---- phase A: all loads (the upstream gradient and the parameters do not depend on the ids)
+  float gv[FQ];
+  {
+    const int t = t0 + r;
+    const float* dr = dh + ((long)min(t, T - 1) * Mp + b) * Dh + c_off + f0;
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) gv[j] = (r < min(RP, t1 - t0)) ? dr[j] : 0.f;
+  }
+  float wk[Cin][FQ], bb[FQ], sc[FQ], sh[FQ], al[FQ];
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+    const int f = f0 + j;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) wk[k][j] = W[k * F + f];
+    bb[j] = bias[f];
+    sc[j] = st[2 * F + f];
+    sh[j] = st[3 * F + f];
+    al[j] = alpha[f];
+  }
+  const long* ids = gf_ids(D, B);
+  const long wraw = ids[b];
+  if (wraw < 0) return;                           // padding sample: no contribution (uniform exit)
+  const long w = wraw;
+  const long g = D.wg[w], c0 = D.wc[w];
+  const long tn = D.time_norm ? c0 : 0;
+  float nv = 0.f, npw = 0.f, nsh = 0.f, nsc = 0.f;
+  if (tid < N) {
+    nv = D.wv[w * N + tid] ? 1.f : 0.f;
+    npw = D.pw[w * N + tid];
+  }
+  if (tid < NC) {
+    nsh = D.shift[(g * D.Tn + tn) * (long)NC + tid];
+    nsc = D.scale[(g * D.Tn + tn) * (long)NC + tid];
+  }
+  float v[GF_SPT];
+  const float* src = D.series + (g * D.Ttot + (c0 - D.tb)) * (long)NC;
+  int nr = min(RP, t1 - t0);
+  gf_slab_load(src + (long)t0 * NC, nr * NC, v);
+  // ---- phase B
+  if (tid < N) {
+    svm[tid] = nv;
+    spw[tid] = npw;
+  }
+  if (tid < NC) {
+    ssh[tid] = nsh;
+    ssc[tid] = nsc;
+  }
+  __syncthreads();
+  gf_slab_park<Cin>(v, nr * NC, NC, svm, ssh, ssc, sx);
+  __syncthreads();
+  float acc[NA][FQ];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) acc[a][j] = 0.f;
+  for (int p0 = t0; p0 < t1; p0 += RP) {
+    if (p0 != t0) {
+      nr = min(RP, t1 - p0);
+      gf_slab_load(src + (long)p0 * NC, nr * NC, v);
+      __syncthreads();
+      gf_slab_park<Cin>(v, nr * NC, NC, svm, ssh, ssc, sx);
+      __syncthreads();
+      if (r < nr) {
+        const float* dr = dh + ((long)(p0 + r) * Mp + b) * Dh + c_off + f0;
+#pragma unroll
+        for (int j = 0; j < FQ; ++j) gv[j] = dr[j];
+      }
+    }
+    if (r < nr) {
+      const float* xr = sx + r * NC;
+      for (int n = 0; n < N; ++n) {
+        const float wn = spw[n];                  // 0 for masked / unpooled nodes: no contribution
+        float xv[Cin];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
+#pragma unroll
+        for (int j = 0; j < FQ; ++j) {
+          float z = bb[j];
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) z += xv[k] * wk[k][j];
+          const float yv = z * sc[j] + sh[j];
+          const float da = wn * gv[j];
+          const bool pos = yv > 0.f;
+          const float dy = pos ? da : al[j] * da;
+          acc[0][j] += dy;
+          acc[1][j] += dy * z;
+          acc[2][j] += pos ? 0.f : da * yv;
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) acc[3 + k][j] += xv[k] * dy;
+        }
+      }
+    }
+  }
+  // reduce over the workgroup's rows: lanes with equal q (stride 4) inside the wave, then 4 waves
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) {
+      float x = acc[a][j];
+#pragma unroll
+      for (int o = 32; o >= 4; o >>= 1) x += __shfl_xor(x, o, 64);
+      if (lane < 4) red[wv][a][lane * FQ + j] = x;
+    }
+  __syncthreads();
+  if (tid >= F) return;
+  const int f = tid;
+  float tot[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) tot[a] = (red[0][a][f] + red[1][a][f]) + (red[2][a][f] + red[3][a][f]);
+  // the closed form of gcn_glue.hip gcn_bwd_finalize_kernel (training), applied to this partial
+  const float mu = st[f], inv = st[F + f], scf = st[2 * F + f];
+  const float A = tot[0], Z = tot[1], P = tot[2];
+  const float dg = inv * (Z - mu * A);
+  bool fin = isfinite(A) && isfinite(dg) && isfinite(P);
+  atomicAdd(dbeta + f, A);
+  atomicAdd(dgamma + f, dg);
+  atomicAdd(dalpha + f, P);
+  const double n = fmax(Sg[Cin + Cin * Cin], 1.0);
+  const double bf = bias[f];
+#pragma unroll
+  for (int k = 0; k < Cin; ++k) {
+    double s2w = 0.0;
+#pragma unroll
+    for (int l = 0; l < Cin; ++l) s2w += Sg[Cin + k * Cin + l] * (double)W[l * F + f];
+    const double s1 = Sg[k];
+    const double sxx = inv * (s2w + s1 * (bf - mu));
+    const float d = (float)(scf * (tot[3 + k] - s1 * A / n - sxx * dg / n));
+    fin = fin && isfinite(d);
+    atomicAdd(dW + k * F + f, d);
+  }
+  if (!fin) __hip_atomic_store(nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ host
+static GfData gf_data(const at::Tensor& series, const at::Tensor& shift, const at::Tensor& scale,
+                      const at::Tensor& win_group, const at::Tensor& win_center, const at::Tensor& win_valid,
+                      const at::Tensor& win_label, const at::Tensor& group_anom_pos, const at::Tensor& mom,
+                      const at::Tensor& pw, const at::Tensor& wids, const at::Tensor& table,
+                      const c10::optional<at::Tensor>& cursor, int64_t tb, int64_t seq_len, bool time_norm, int& B) {
+  check_f32_cuda(series, "series");
+  check_f32_cuda(shift, "shift");
+  check_f32_cuda(scale, "scale");
+  TORCH_CHECK(series.dim() == 4 && shift.dim() == 4 && scale.sizes() == shift.sizes(), "gcn_fused: store shapes");
+  TORCH_CHECK(win_group.scalar_type() == at::kLong && win_center.scalar_type() == at::kLong &&
+                  group_anom_pos.scalar_type() == at::kLong && win_valid.scalar_type() == at::kByte &&
+                  win_valid.is_contiguous(), "gcn_fused: index tables");
+  GfData D{};
+  D.series = series.data_ptr<float>();
+  D.shift = shift.data_ptr<float>();
+  D.scale = scale.data_ptr<float>();
+  D.wg = win_group.data_ptr<long>();
+  D.wc = win_center.data_ptr<long>();
+  D.wv = win_valid.data_ptr<uint8_t>();
+  D.gap = group_anom_pos.data_ptr<long>();
+  D.Ttot = (int)series.size(1);
+  D.Tn = (int)shift.size(1);
+  D.N = (int)series.size(2);
+  D.tb = (int)tb;
+  D.T = (int)seq_len;
+  D.time_norm = time_norm ? 1 : 0;
+  TORCH_CHECK(win_valid.size(1) == D.N, "gcn_fused: win_valid must be [nwin, N]");
+  const int C = (int)series.size(3);
+  TORCH_CHECK(C >= 1 && C <= GF_MAX_CIN && D.N * C <= GF_ROW_MAX, "gcn_fused: N * C must be <= 128, C <= 4");
+  if (win_label.numel() > 0) {
+    check_f32_cuda(win_label, "win_label");
+    TORCH_CHECK(win_label.dim() == 1, "gcn_fused: per-window labels (flagged-sensor windows)");
+    D.wlab = win_label.data_ptr<float>();
+  }
+  if (mom.numel() > 0) {
+    TORCH_CHECK(mom.is_cuda() && mom.scalar_type() == at::kDouble && mom.is_contiguous() &&
+                    mom.size(1) == C + C * C + 1, "gcn_fused: moments [nwin, nstat] fp64");
+    D.mom = mom.data_ptr<double>();
+  }
+  if (pw.numel() > 0) {
+    check_f32_cuda(pw, "pool weights");
+    TORCH_CHECK(pw.size(1) == D.N, "gcn_fused: pool weights [nwin, N]");
+    D.pw = pw.data_ptr<float>();
+  }
+  if (cursor.has_value() && cursor->defined()) {
+    TORCH_CHECK(table.dim() == 2 && table.scalar_type() == at::kLong && table.is_contiguous() && table.is_cuda(),
+                "gcn_fused: table must be a contiguous int64 [rows, B] device tensor");
+    TORCH_CHECK(cursor->scalar_type() == at::kLong && cursor->numel() >= 1 && cursor->is_cuda(),
+                "gcn_fused: cursor must be int64[1] on the device");
+    B = (int)table.size(1);
+    D.table = table.data_ptr<long>();
+    D.cursor = cursor->data_ptr<long>();
+    D.nrows = table.size(0);
+  } else if (wids.numel() > 0 || wids.dim() == 1) {
+    TORCH_CHECK(wids.scalar_type() == at::kLong && wids.is_contiguous() && wids.is_cuda(), "gcn_fused: wids int64");
+    B = (int)wids.size(0);
+    D.wids = wids.data_ptr<long>();
+    D.nrows = 1;
+  }
+  TORCH_CHECK(B >= 0 && B <= 4096, "gcn_fused: batch size");
+  return D;
+}
+
+// workgroups per sample (ny) and steps per workgroup (rows): one staging pass per workgroup
+static void gf_grid(int T, int NC, int& ny, int& rows) {
+  const int rp = std::min(GF_RPP, GF_SLAB / NC);
+  ny = std::max(1, std::min(16, (T + rp - 1) / rp));
+  rows = (T + ny - 1) / ny;
+}
+
+#define GQ_GF_CIN(CIN_RT, ...)                                 \
+  switch (CIN_RT) {                                            \
+    case 1: { constexpr int CIN = 1; __VA_ARGS__; } break;     \
+    case 2: { constexpr int CIN = 2; __VA_ARGS__; } break;     \
+    case 3: { constexpr int CIN = 3; __VA_ARGS__; } break;     \
+    case 4: { constexpr int CIN = 4; __VA_ARGS__; } break;     \
+    default: TORCH_CHECK(false, "gcn_fused: 1..4 input channels"); \
+  }
+#define GQ_GF_F(F_RT, ...)                                     \
+  switch (F_RT) {                                              \
+    case 8: { constexpr int FF = 8; __VA_ARGS__; } break;      \
+    case 16: { constexpr int FF = 16; __VA_ARGS__; } break;    \
+    case 32: { constexpr int FF = 32; __VA_ARGS__; } break;    \
+    default: TORCH_CHECK(false, "gcn_fused: 8, 16 or 32 output channels"); \
+  }
+
+// [moments [nwin, nstat] fp64, pool weights [nwin, N]] of every window of the store
+std::vector<at::Tensor> gcn_window_prep(const at::Tensor& series, const at::Tensor& shift, const at::Tensor& scale,
+                                        const at::Tensor& win_group, const at::Tensor& win_center,
+                                        const at::Tensor& win_valid, const at::Tensor& group_adj,
+                                        const at::Tensor& group_anom_pos, int64_t tb, int64_t seq_len,
+                                        bool time_norm, bool agg_mean, int64_t pool) {
+  int B = 0;
+  const at::Tensor e = series.new_zeros(0);
+  GfData D = gf_data(series, shift, scale, win_group, win_center, win_valid, e, group_anom_pos, e, e,
+                     e.to(at::kLong), e.to(at::kLong), c10::nullopt, tb, seq_len, time_norm, B);
+  check_f32_cuda(group_adj, "group_adj");
+  TORCH_CHECK(pool >= 0 && pool <= 2, "gcn_window_prep: pool 0 mean, 1 sum, 2 selection");
+  const int C = (int)series.size(3);
+  const long nwin = win_group.size(0);
+  c10::DeviceGuard guard(series.device());
+  at::Tensor mom = at::empty({nwin, C + C * C + 1}, series.options().dtype(at::kDouble));
+  at::Tensor pw = at::empty({nwin, D.N}, series.options());
+  if (nwin > 0)
+    GQ_GF_CIN(C, hipLaunchKernelGGL(gcn_window_prep_kernel<CIN>, dim3(nwin), dim3(256), 2 * D.N * sizeof(float),
+                                    stream(), D, group_adj.data_ptr<float>(), agg_mean ? 1 : 0, (int)pool, (int)nwin,
+                                    mom.data_ptr<double>(), pw.data_ptr<float>()));
+  GQ_LAUNCH_CHECK();
+  return {mom, pw};
+}
+
+// returns [h [T, Mp, Cp], S [nstat] fp64 (training), st [4, F], y [B], y_mask [B], wid [B]]
+std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor& shift, const at::Tensor& scale,
+                                      const at::Tensor& win_group, const at::Tensor& win_center,
+                                      const at::Tensor& win_valid, const at::Tensor& win_label,
+                                      const at::Tensor& group_anom_pos, const at::Tensor& mom, const at::Tensor& pw,
+                                      const at::Tensor& wids, const at::Tensor& table,
+                                      const c10::optional<at::Tensor>& cursor, int64_t tb, int64_t seq_len,
+                                      bool time_norm, const at::Tensor& W, const at::Tensor& bias,
+                                      const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& alpha,
+                                      at::Tensor rmean, at::Tensor rvar, bool training, double momentum, double eps,
+                                      int64_t Mp, int64_t Cp) {
+  int B = 0;
+  GfData D = gf_data(series, shift, scale, win_group, win_center, win_valid, win_label, group_anom_pos, mom, pw,
+                     wids, table, cursor, tb, seq_len, time_norm, B);
+  TORCH_CHECK(D.wlab != nullptr && D.pw != nullptr && (!training || D.mom != nullptr), "gcn_fused_fwd: tables");
+  for (const at::Tensor* t : {&W, &bias, &gamma, &beta, &alpha, (const at::Tensor*)&rmean, (const at::Tensor*)&rvar})
+    check_f32_cuda(*t, "gcn_fused_fwd parameter");
+  const int C = (int)series.size(3), F = (int)W.size(1);
+  TORCH_CHECK(W.size(0) == C && bias.numel() == F && gamma.numel() == F && beta.numel() == F && alpha.numel() == F &&
+                  rmean.numel() == F && rvar.numel() == F, "gcn_fused_fwd: parameter shapes");
+  TORCH_CHECK(Mp >= B && Mp % 16 == 0 && Cp >= C + F && Cp % 4 == 0, "gcn_fused_fwd: Mp / Cp");
+  c10::DeviceGuard guard(series.device());
+  auto fo = series.options();
+  const int T = (int)seq_len;
+  at::Tensor out = at::empty({T, Mp, Cp}, fo);
+  at::Tensor S = at::empty({training ? C + C * C + 1 : 0}, fo.dtype(at::kDouble));
+  at::Tensor st = at::empty({4, F}, fo);
+  at::Tensor y = at::empty({B}, fo), ym = at::empty({B}, fo);
+  at::Tensor wid = at::empty({B}, win_group.options());
+  int ny, rows;
+  gf_grid(T, D.N * C, ny, rows);
+  GQ_GF_CIN(C, GQ_GF_F(F, hipLaunchKernelGGL((gcn_fused_fwd_kernel<CIN, FF>), dim3(Mp, ny), dim3(256), 0, stream(),
+      D, B, (int)Mp, (int)Cp, rows, W.data_ptr<float>(), bias.data_ptr<float>(), gamma.data_ptr<float>(),
+      beta.data_ptr<float>(), alpha.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+      training ? 1 : 0, (float)momentum, (float)eps, out.data_ptr<float>(), training ? S.data_ptr<double>() : nullptr,
+      st.data_ptr<float>(), y.data_ptr<float>(), ym.data_ptr<float>(), wid.data_ptr<long>())));
+  GQ_LAUNCH_CHECK();
+  return {out, S, st, y, ym, wid};
+}
+
+// Training backward: adds dW, dgamma, dbeta, dalpha (float atomics) from dh [T, Mp, Dh] channels
+// [c_off, c_off + F). (db is zero in training: BatchNorm removes the bias.)
+void gcn_fused_bwd(const at::Tensor& dh, int64_t c_off, const at::Tensor& series, const at::Tensor& shift,
+                   const at::Tensor& scale, const at::Tensor& win_group, const at::Tensor& win_center,
+                   const at::Tensor& win_valid, const at::Tensor& group_anom_pos, const at::Tensor& pw,
+                   const at::Tensor& wids, const at::Tensor& table, const c10::optional<at::Tensor>& cursor, int64_t tb,
+                   int64_t seq_len, bool time_norm, const at::Tensor& S, const at::Tensor& st, const at::Tensor& W,
+                   const at::Tensor& bias, const at::Tensor& alpha, at::Tensor dW, at::Tensor dgamma, at::Tensor dbeta,
+                   at::Tensor dalpha) {
+  int B = 0;
+  const at::Tensor e = series.new_zeros(0);
+  GfData D = gf_data(series, shift, scale, win_group, win_center, win_valid, e, group_anom_pos, e, pw, wids, table,
+                     cursor, tb, seq_len, time_norm, B);
+  check_f32_cuda(dh, "dh");
+  for (const at::Tensor* t : {&st, &W, &bias, &alpha, (const at::Tensor*)&dW, (const at::Tensor*)&dgamma,
+                              (const at::Tensor*)&dbeta, (const at::Tensor*)&dalpha})
+    check_f32_cuda(*t, "gcn_fused_bwd operand");
+  const int C = (int)series.size(3), F = (int)W.size(1);
+  TORCH_CHECK(S.is_cuda() && S.scalar_type() == at::kDouble && S.numel() == C + C * C + 1, "gcn_fused_bwd: S");
+  TORCH_CHECK(dh.dim() == 3 && dh.size(0) == seq_len && dh.size(1) >= B && dh.size(2) >= c_off + F,
+              "gcn_fused_bwd: dh [T, Mp, Dh]");
+  TORCH_CHECK(dW.numel() == (long)C * F && dgamma.numel() == F && dbeta.numel() == F && dalpha.numel() == F &&
+                  st.numel() == 4 * F, "gcn_fused_bwd: gradient shapes");
+  c10::DeviceGuard guard(series.device());
+  int ny, rows;
+  gf_grid((int)seq_len, D.N * C, ny, rows);
+  if (B > 0)
+    GQ_GF_CIN(C, GQ_GF_F(F, hipLaunchKernelGGL((gcn_fused_bwd_kernel<CIN, FF>), dim3(B, ny), dim3(256), 0, stream(),
+        D, B, (int)dh.size(1), (int)dh.size(2), (int)c_off, rows, dh.data_ptr<float>(), S.data_ptr<double>(),
+        st.data_ptr<float>(), W.data_ptr<float>(), bias.data_ptr<float>(), alpha.data_ptr<float>(),
+        dW.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dalpha.data_ptr<float>(),
+        chain_ctl(series.get_device()) + 7)));
+  GQ_LAUNCH_CHECK();
+}
+
+}  // namespace gq
+
+TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("gcn_window_prep", &gq::gcn_window_prep);
+  m.impl("gcn_fused_fwd", &gq::gcn_fused_fwd);
+  m.impl("gcn_fused_bwd", &gq::gcn_fused_bwd);
+}

@@ -72,6 +72,7 @@ struct ChainStage {
 struct ChainArgs {
   ChainStage st[CHAIN_MAX];
   int ns, ntiles, nt8, Mp;
+  int roles;                         // H <= 32 stages: role-split bodies (chain_stage_roles)
   int* ctl;                          // [0] epoch, [1] finished workgroups, [2] spin timeout seen
   long long* trace;                  // [blocks][2] start / end s_memrealtime (100 MHz) of the last launch
   // extra workgroups past the stages (the chain leaves most CUs idle): build the time4 kernel's
@@ -132,7 +133,9 @@ struct ChainLds {
   static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
   static constexpr int BYTES = HS + XS + HF;
 };
-static constexpr int CHAIN_LDS = ChainLds<64, 2>::BYTES;
+static constexpr int CHAIN_LDS_A = ChainLds<64, 2>::BYTES;
+static constexpr int CHAIN_LDS_B = 2 * 16 * 40 * 2 + 2 * 16 * 72 * 2 + 2 * 16 * 36 * 4 + 2 * 8 * 64 * 12;  // ChainRLds<32, 2>
+static constexpr int CHAIN_LDS = CHAIN_LDS_A > CHAIN_LDS_B ? CHAIN_LDS_A : CHAIN_LDS_B;
 
 template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN>
 __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
@@ -323,6 +326,321 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   }
 }
 
+// ---- role-split stage (H <= 32). chain_stage keeps every wave on the serial path: the same waves
+// that run the recurrence also wait for the input ring's loads, issue the h / gate / cell-state
+// stores and publish the granules, so every step pays their issue slots and waits (the v3 recurrence
+// microbenchmark: 249 ns per H = 16 step without stores, 435 with them, r1_lstm_microbench.md).
+// Here the workgroup's waves take fixed roles, one LDS barrier per step for all of them:
+//   compute (NW = H / 4 waves, one cell per lane): MFMA on the x / h tiles in LDS, cell update,
+//            h_t (bf16 for the next MFMA, fp32) and the packed gates / c_t into LDS; never touches
+//            global memory inside the loop;
+//   loader  (NL waves): the input ring (fp32 x or the producer's tagged granules, D steps ahead,
+//            tag checks and bounded re-polls, consumer-side MaxPooling1D + argmax bytes), stages
+//            x_{t+1} into LDS during step t;
+//   storer  (NS waves): during step t copies step t-1's h / gates / c from LDS to HBM, publishes
+//            h_{t-1} as granules (or pools it: last stage); only stores, so it never waits on vmcnt.
+// Compute waves run at s_setprio 3, loaders 2, storers 0 (they share SIMDs with compute waves).
+// Global layouts are those of chain_stage (the backward is unchanged).
+template <int H, int KX>
+struct ChainRLds {
+  static constexpr int NW = H / 4;
+  static constexpr int HS = 2 * 16 * (TMC<H>::KPH + 8) * 2;
+  static constexpr int XS = 2 * 16 * (32 * KX + 8) * 2;
+  static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
+  static constexpr int GS = 2 * NW * 64 * 8;
+  static constexpr int CS = 2 * NW * 64 * 4;
+  static constexpr int BYTES = HS + XS + HF + GS + CS;
+};
+
+// loader waves of a role-split stage: its input ring (D steps of the tile's granules) in <= ~48 VGPRs
+constexpr int chain_loaders(int H, bool SRC, int PIN, int DX) {
+  return SRC ? (PIN == 3 ? (H == 16 ? 2 : 4) : (DX > 16 ? 2 : 1)) : (DX > 32 ? 2 : 1);
+}
+
+template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN, int NL, int NS, int DX>
+__device__ __forceinline__ void chain_stage_roles(const ChainStage S, int tile, int ntiles, int Mp, unsigned tagb,
+                                                  int* ctl, char* smem, long long* rt) {
+  // rt (profiling, else nullptr): per role [loop cycles, cycles waiting at the step barriers]
+  // (s_memtime) of its first wave -> rt[2 * role ..]
+  long long wt = 0, lt0 = 0;
+  auto rbar = [&]() {
+    if (rt != nullptr) {
+      const long long a = __builtin_amdgcn_s_memtime();
+      lds_barrier();
+      wt += __builtin_amdgcn_s_memtime() - a;
+    } else {
+      lds_barrier();
+    }
+  };
+  auto rmark = [&](int role) {
+    if (rt != nullptr && (threadIdx.x & 63) == 0) {
+      rt[2 * role] = __builtin_amdgcn_s_memtime() - lt0;
+      rt[2 * role + 1] = wt;
+    }
+  };
+  using C = TMC<H>;
+  static_assert(C::CPL == 1 && H <= 32, "role-split stage: one cell per lane");
+  constexpr int NW = C::NW, G4 = C::G4;
+  constexpr int KPX = 32 * KX;
+  using L = ChainRLds<H, KX>;
+  static_assert(L::BYTES <= CHAIN_LDS && L::HS % 16 == 0 && L::XS % 16 == 0 && L::HF % 16 == 0 &&
+                L::GS % 16 == 0, "chain role LDS layout");
+  static_assert(NW + NL + NS <= 16, "roles fit one 1024-thread workgroup");
+  auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
+  auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
+  auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
+  auto gsl = reinterpret_cast<uint2 (*)[NW * 64]>(smem + L::HS + L::XS + L::HF);
+  auto csl = reinterpret_cast<float (*)[NW * 64]>(smem + L::HS + L::XS + L::HF + L::GS);
+
+  const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row0 = tile * 16;
+  const int To = P > 0 ? T / P : T;
+  const size_t hstep = (size_t)Mp * H;
+
+  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += 1024) (&hs[0][0][0])[i] = (__bf16)0.f;
+  for (int i = tid; i < 2 * 16 * (KPX + 8); i += 1024) (&xs[0][0][0])[i] = (__bf16)0.f;
+  __syncthreads();
+
+  if (w < NW) {
+    // ------------------------------------------------------------------ compute
+    __builtin_amdgcn_s_setprio(3);
+    const int col = lane & 15, quad = lane >> 4;
+    bf16x8_t ufr[C::KSH], wfr[KX];
+    const int au = 4 * w + (col >> 2), ag = col & 3;
+    const int u = 4 * w + quad;
+#pragma unroll
+    for (int s = 0; s < C::KSH; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(S.U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+      }
+      ufr[s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
+      }
+      wfr[s] = v;
+    }
+    const f32x4_t bias4 = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
+    float c = 0.f;
+    __syncthreads();                              // x_0 staged
+    if (rt != nullptr) lt0 = __builtin_amdgcn_s_memtime();
+    for (int t = 0; t < T; ++t) {
+      const int p = t & 1;
+      f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KSH; ++s) {
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
+        acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[s], bh, acch, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < KX; ++s) {
+        const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
+        accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[s], bx, accx, 0, 0, 0);
+      }
+      const f32x4_t acc = accx + acch;
+      const float iv = sigmoidf_fast(acc[0]);
+      const float fv = sigmoidf_fast(acc[1]);
+      const float gv = tanhf_fast(acc[2]);
+      const float ov = sigmoidf_fast(acc[3]);
+      c = fv * c + iv * gv;
+      const float hv = ov * tanhf_fast(c);
+      hs[p ^ 1][col][u] = (__bf16)hv;
+      hf[p][col][u] = hv;
+      if constexpr (TRAIN) {
+        gsl[p][w * 64 + lane] = gates_pack(iv, fv, gv, ov);
+        csl[p][w * 64 + lane] = c;
+      }
+      rbar();
+    }
+    if (w == 0) rmark(0);
+    __builtin_amdgcn_s_setprio(0);
+    return;
+  }
+
+  if (w < NW + NL) {
+    // ------------------------------------------------------------------ loader
+    __builtin_amdgcn_s_setprio(2);
+    const int li = (w - NW) * 64 + lane;          // loader lane 0 .. NL*64-1
+    constexpr int GR = SRC ? 1 : 4;               // floats per granule
+    static_assert(DX <= KPX, "input width bound");
+    constexpr int NGMAX = 16 * DX / GR;           // granules of a [16][Din] tile, Din <= DX
+    constexpr int GPL = (NGMAX + NL * 64 - 1) / (NL * 64);
+    const int ng = 16 * Din / GR;
+    const size_t xstep = (size_t)Mp * Din;
+    int goff[GPL], grow[GPL], gk[GPL];
+    bool gon[GPL];
+#pragma unroll
+    for (int q = 0; q < GPL; ++q) {
+      const int gi = min(li + q * NL * 64, ng - 1);
+      gon[q] = li + q * NL * 64 < ng;
+      goff[q] = row0 * Din + gi * GR;
+      grow[q] = gi * GR / Din;
+      gk[q] = gi * GR % Din;
+    }
+    float4 xr[D][SRC ? 1 : GPL];
+    unsigned long long xq[D][SRC ? GPL : 1][PIN];
+    auto load_x = [&](int j, int tx) {
+#pragma unroll
+      for (int q = 0; q < GPL; ++q) {
+        if (q * NL * 64 >= ng) break;             // (uniform: lanes past the tile)
+        if constexpr (SRC) {
+#pragma unroll
+          for (int r = 0; r < PIN; ++r)
+            xq[j][q][r] = ld_granule(S.xin + goff[q] + (size_t)(PIN * tx + r) * xstep);
+        } else {
+          xr[j][q] = *reinterpret_cast<const float4*>(S.x + goff[q] + (size_t)tx * xstep);
+        }
+      }
+    };
+    auto stage_x = [&](int buf, int j, int tx) {
+      if constexpr (SRC) {
+        bool bad = false;
+#pragma unroll
+        for (int q = 0; q < GPL; ++q)
+#pragma unroll
+          for (int r = 0; r < PIN; ++r) bad |= (unsigned)(xq[j][q][r] >> 32) != (tagb | (unsigned)(PIN * tx + r));
+        if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+#pragma unroll
+          for (int q = 0; q < GPL; ++q)
+#pragma unroll
+            for (int r = 0; r < PIN; ++r)
+              xq[j][q][r] = chain_wait(S.xin + goff[q] + (size_t)(PIN * tx + r) * xstep,
+                                       tagb | (unsigned)(PIN * tx + r), ctl);
+        }
+#pragma unroll
+        for (int q = 0; q < GPL; ++q) {
+          float m = __uint_as_float((unsigned)xq[j][q][0]);
+          if constexpr (PIN > 1) {
+            unsigned arg = 0;
+#pragma unroll
+            for (int r = 1; r < PIN; ++r) {
+              const float v = __uint_as_float((unsigned)xq[j][q][r]);
+              if (v > m) { m = v; arg = r; }
+            }
+            if (gon[q]) {
+              S.pin_out[goff[q] + (size_t)tx * xstep] = m;
+              S.pin_idx[goff[q] + (size_t)tx * xstep] = (unsigned char)arg;
+            }
+          }
+          if (gon[q]) xs[buf][grow[q]][gk[q]] = (__bf16)m;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < GPL; ++q) {
+          if (gon[q]) {
+            const float4 v = xr[j][q];
+            xs[buf][grow[q]][gk[q]] = (__bf16)v.x;
+            xs[buf][grow[q]][gk[q] + 1] = (__bf16)v.y;
+            xs[buf][grow[q]][gk[q] + 2] = (__bf16)v.z;
+            xs[buf][grow[q]][gk[q] + 3] = (__bf16)v.w;
+          }
+        }
+      }
+    };
+    if constexpr (SRC) {
+      // start once the producer is D + LEAD (input) steps ahead (see chain_stage)
+      constexpr int LEAD = PIN > 1 ? CHAIN_LEAD3 : CHAIN_LEAD1;
+      const int tw = min(D + LEAD, T - 1);
+      (void)chain_wait(S.xin + goff[0] + (size_t)(PIN * tw + PIN - 1) * xstep, tagb | (unsigned)(PIN * tw + PIN - 1),
+                       ctl);
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_x(j, min(j, T - 1));
+    stage_x(0, 0, 0);
+    load_x(0, min(D, T - 1));
+    __syncthreads();                              // x_0 staged
+    if (rt != nullptr) lt0 = __builtin_amdgcn_s_memtime();
+    for (int t0 = 0; t0 < T; t0 += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const int t = t0 + j;
+        if (t >= T) break;                        // (uniform)
+        const int jn = (j + 1 == D) ? 0 : j + 1;
+        if (t + 1 < T) {
+          stage_x((t + 1) & 1, jn, t + 1);
+          load_x(jn, min(t + 1 + D, T - 1));
+        }
+        rbar();
+      }
+    }
+    if (w == NW) rmark(1);
+    __builtin_amdgcn_s_setprio(0);
+    return;
+  }
+
+  if (w < NW + NL + NS) {
+    // ------------------------------------------------------------------ storer
+    const int si = (w - NW - NL) * 64 + lane;     // storer lane 0 .. NS*64-1
+    constexpr int NH4 = 16 * H / 4;               // float4 granules of the h tile
+    constexpr int HPL = (NH4 + NS * 64 - 1) / (NS * 64);
+    constexpr int EPL = (16 * H + NS * 64 - 1) / (NS * 64);        // published elements per lane
+    constexpr int NB4 = NW * 64 * 8 / 16;         // float4 of the packed gates block
+    constexpr int BPL = (NB4 + NS * 64 - 1) / (NS * 64);
+    constexpr int NC4 = NW * 64 / 4;              // float4 of the c block
+    constexpr int CPLS = (NC4 + NS * 64 - 1) / (NS * 64);
+    const bool publish = S.sout != nullptr;
+    PoolAcc pool[HPL];
+    auto store_step = [&](int q, int t) {         // step t's data from LDS buffer q
+#pragma unroll
+      for (int k = 0; k < HPL; ++k) {
+        const int i = si + k * NS * 64;
+        if (i < NH4) {
+          const int r = (4 * i) / H, cc = (4 * i) % H;
+          const float4 v = *reinterpret_cast<const float4*>(&hf[q][r][cc]);
+          *reinterpret_cast<float4*>(S.h + ((size_t)t * Mp + row0) * H + 4 * i) = v;
+          if (P > 0) pool[k].step(v, t, P, To, S.pout, S.iout, (size_t)row0 * H + 4 * i, hstep);
+        }
+      }
+      if (publish) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+          const int e = si + k * NS * 64;
+          if (e < 16 * H)
+            st_granule(S.sout + ((size_t)t * Mp + row0) * H + e, hf[q][e / H][e % H], tagb | (unsigned)t);
+        }
+      }
+      if constexpr (TRAIN) {
+        const size_t blk = ((size_t)t * ntiles + tile) * NW * 64;
+#pragma unroll
+        for (int k = 0; k < BPL; ++k) {
+          const int i = si + k * NS * 64;
+          if (i < NB4)
+            *reinterpret_cast<float4*>(reinterpret_cast<char*>(S.g + blk * 4) + 16 * i) =
+                *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(&gsl[q][0]) + 16 * i);
+        }
+#pragma unroll
+        for (int k = 0; k < CPLS; ++k) {
+          const int i = si + k * NS * 64;
+          if (i < NC4)
+            *reinterpret_cast<float4*>(S.c + blk + 4 * i) = *reinterpret_cast<const float4*>(&csl[q][4 * i]);
+        }
+      }
+    };
+    __syncthreads();                              // x_0 staged
+    if (rt != nullptr) lt0 = __builtin_amdgcn_s_memtime();
+    for (int t = 0; t < T; ++t) {
+      if (t >= 1) store_step((t - 1) & 1, t - 1);
+      rbar();
+    }
+    store_step((T - 1) & 1, T - 1);
+    if (w == NW + NL) rmark(2);
+    return;
+  }
+  // spare waves: the same barriers, nothing else
+  __syncthreads();
+  for (int t = 0; t < T; ++t) lds_barrier();
+}
+
 __device__ __forceinline__ void chain_finish(int* ctl, int nblk, int* sync = nullptr) {
   if (threadIdx.x == 0) {
     const int old = __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -375,7 +693,9 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned tagb = chain_tag_base(E);
   __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS];
-  const ChainStage& S = A.st[s];
+  // (a local copy: field-wise scalar loads of the kernel arguments; a reference into the by-value
+  // argument array made the compiler copy the whole array to scratch)
+  const ChainStage S = A.st[s];
   const int H = S.H, KX = S.KX;
   const bool src = s > 0;
 #define GQ_CHAIN_BODY(HH, KXX, DD, SRCV, PINV)                                          \
@@ -388,9 +708,23 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
 #define GQ_CHAIN_KX(HH)                                                                 \
   if (src) { if (S.PIN == 3) { GQ_CHAIN_SRC(HH, 3, CHAIN_D3) } else { GQ_CHAIN_SRC(HH, 1, CHAIN_D) } } \
   else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false, 1) else GQ_CHAIN_BODY(HH, 2, 6, false, 1) }
-  if (H == 16) GQ_CHAIN_KX(16)
-  else if (H == 32) GQ_CHAIN_KX(32)
-  else GQ_CHAIN_KX(64)
+#define GQ_CHAIN_ROLES(HH, KXX, DD, SRCV, PINV, DXV)                                    \
+  chain_stage_roles<HH, TRAIN, KXX, DD, SRCV, PINV, chain_loaders(HH, SRCV, PINV, DXV), (HH == 16 ? 2 : 3), DXV>( \
+      S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem, A.roles > 1 ? A.trace + 6912 + 6 * blockIdx.x : nullptr);
+  if (H == 64 || !A.roles) {
+    if (H == 16) GQ_CHAIN_KX(16)
+    else if (H == 32) GQ_CHAIN_KX(32)
+    else GQ_CHAIN_KX(64)
+  } else if (H == 16) {
+    if (src) { if (S.PIN == 3) { GQ_CHAIN_ROLES(16, 1, CHAIN_D3, true, 3, 16) } else { GQ_CHAIN_ROLES(16, 1, CHAIN_D, true, 1, 16) } }
+    else if (KX == 1) { GQ_CHAIN_ROLES(16, 1, 6, false, 1, 32) } else { GQ_CHAIN_ROLES(16, 2, 6, false, 1, 64) }
+  } else {
+    if (src) {
+      if (S.PIN == 3) { if (S.Din <= 16) { GQ_CHAIN_ROLES(32, 1, CHAIN_D3, true, 3, 16) } else { GQ_CHAIN_ROLES(32, 1, CHAIN_D3, true, 3, 32) } }
+      else { if (S.Din <= 16) { GQ_CHAIN_ROLES(32, 1, CHAIN_D, true, 1, 16) } else { GQ_CHAIN_ROLES(32, 1, CHAIN_D, true, 1, 32) } }
+    } else if (KX == 1) { GQ_CHAIN_ROLES(32, 1, 6, false, 1, 32) } else { GQ_CHAIN_ROLES(32, 2, 6, false, 1, 64) }
+  }
+#undef GQ_CHAIN_ROLES
 #undef GQ_CHAIN_KX
 #undef GQ_CHAIN_SRC
 #undef GQ_CHAIN_BODY
@@ -886,7 +1220,8 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
 static long long* chain_trace_buf(int dev) {
   static long long* tr[64] = {nullptr};
   // [0, 768): per-workgroup start / end and stage-loop start; then the grads role's [8][256][3]
-  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], (3 * 256 + 8 * 256 * 3) * sizeof(long long)) == hipSuccess,
+  // then (profiling) the role-split stages' [256][3 roles][loop, barrier-wait cycles]
+  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], (3 * 256 + 8 * 256 * 3 + 256 * 6) * sizeof(long long)) == hipSuccess,
                             "lstm_chain: trace");
   return tr[dev];
 }
@@ -991,6 +1326,11 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   A.Mp = Mp;
   A.ctl = chain_ctl(x.get_device());
   A.trace = chain_trace_buf(x.get_device());
+  static const int roles = [] {
+    const char* e = std::getenv("GNNQC_CHAIN_ROLES");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  A.roles = roles;
   std::vector<at::Tensor> out;
   at::Tensor prev_stream;
   int T = (int)x.size(0), Din = (int)x.size(2);
@@ -1318,7 +1658,7 @@ at::Tensor lstm_chain_status(const at::Tensor& like) {
 at::Tensor lstm_chain_trace(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
   long long* p = chain_trace_buf(like.get_device());
-  at::Tensor o = at::empty({3 * 256 + 8 * 256 * 3}, like.options().dtype(at::kLong));
+  at::Tensor o = at::empty({3 * 256 + 8 * 256 * 3 + 256 * 6}, like.options().dtype(at::kLong));
   TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, o.numel() * sizeof(long long), hipMemcpyDeviceToDevice,
                              stream()) == hipSuccess, "lstm_chain_trace");
   return o;

@@ -322,8 +322,11 @@ __device__ __forceinline__ void lstm_grads_body(
 //           added to the gradient buffers directly, else it goes to ws2[g][slot] and
 //   final:  thread = record slot sums its NG group sums and adds them.
 // Adding: one writer per element, plain read-modify-write into dW [Din,4H] / db / dU [H,4H].
+// nf (optional): raised when a sum is not finite (adam_flagged reads it instead of scanning g)
 __device__ __forceinline__ void grads_add(float s, int e, int ncb, int DT, int HT, int Din, int H,
-                                          float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dU) {
+                                          float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dU,
+                                          int* nf = nullptr) {
+  if (nf != nullptr && !isfinite(s)) __hip_atomic_store(nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int R = (DT + HT) * 1024;
   const int G4 = 4 * H;
   // record layout: [split][cb][DT + HT fragments][4 waves][64 lanes][4]
@@ -344,7 +347,8 @@ __device__ __forceinline__ void grads_add(float s, int e, int ncb, int DT, int H
 __device__ __forceinline__ void lstm_grads_reduce_body(const float* __restrict__ ws, int splits, int RC,
                                                        float* __restrict__ ws2, int ncb, int DT, int HT, int Din,
                                                        int H, float* __restrict__ dW, float* __restrict__ db,
-                                                       float* __restrict__ dU, int bx, int g, int NG) {
+                                                       float* __restrict__ dU, int bx, int g, int NG,
+                                                       int* nf = nullptr) {
   // 16 consecutive slots (64 B per split row) x 16 split lanes (measured faster than 8 x 32)
   __shared__ float red[16][17];
   const int sl = threadIdx.x & 15, l = threadIdx.x >> 4;
@@ -365,7 +369,7 @@ __device__ __forceinline__ void lstm_grads_reduce_body(const float* __restrict__
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += red[k][sl];
-    if (NG == 1) grads_add(s, slot, ncb, DT, HT, Din, H, dW, db, dU);
+    if (NG == 1) grads_add(s, slot, ncb, DT, HT, Din, H, dW, db, dU, nf);
     else ws2[(size_t)g * RC + slot] = s;
   }
 }
@@ -378,7 +382,8 @@ __device__ __forceinline__ void lstm_grads_reduce_body(const float* __restrict__
 template <int KB>
 __device__ __forceinline__ void lstm_grads_reduce_multi(const float* __restrict__ ws, int splits, int RC, int ncb,
                                                         int DT, int HT, int Din, int H, float* __restrict__ dW,
-                                                        float* __restrict__ db, float* __restrict__ dU, int bx) {
+                                                        float* __restrict__ db, float* __restrict__ dU, int bx,
+                                                        int* nf = nullptr) {
   __shared__ float red[KB][16][17];
   const int sl = threadIdx.x & 15, l = threadIdx.x >> 4;
   int slot[KB];
@@ -403,7 +408,7 @@ __device__ __forceinline__ void lstm_grads_reduce_multi(const float* __restrict_
       float s = 0.f;
 #pragma unroll
       for (int j = 0; j < 16; ++j) s += red[k][j][sl];
-      grads_add(s, e, ncb, DT, HT, Din, H, dW, db, dU);
+      grads_add(s, e, ncb, DT, HT, Din, H, dW, db, dU, nf);
     }
   }
 }

@@ -38,6 +38,7 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
                      long dx_cb_stride, int lddx, long x_elems, hipStream_t st);
 int lstm_grads_col_blocks(int H);
+int* chain_ctl(int dev);   // lstm_chain.hip: the device's chain control words
 void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows, int H, int Dw, int lddx,
                   hipStream_t st);
 
@@ -1189,6 +1190,7 @@ struct MultiRed {
   RedJob j[MULTI_MAX];
   int start[MULTI_MAX + 1];
   int n;
+  int* nf;                         // non-finite gradient flag (chain control word 7)
 };
 
 __global__ __launch_bounds__(256) void lstm_grads_multi_kernel(MultiGrad M) {
@@ -1220,10 +1222,10 @@ __global__ __launch_bounds__(256) void lstm_grads_reduce_multi_kernel(MultiRed M
   const RedJob rj = M.j[k];
   if (rj.kb > 1)
     lstm_grads_reduce_multi<PIPE_RED_KB>(rj.ws, rj.splits, rj.RC, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
-                                         rj.dU, b - M.start[k]);
+                                         rj.dU, b - M.start[k], M.nf);
   else
     lstm_grads_reduce_body(rj.ws, rj.splits, rj.RC, nullptr, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
-                           rj.dU, b - M.start[k], 0, 1);
+                           rj.dU, b - M.start[k], 0, 1, M.nf);
 }
 
 // grads of jobs (dz, x, h, W, period, hshift, ws) then reductions of rjobs (ws, W, dW, dU, db):
@@ -1285,6 +1287,7 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
   if (nr) {
     MultiRed R{};
     R.n = nr;
+    R.nf = chain_ctl(rws[0].get_device()) + 7;
     int nb = 0;
     for (int k = 0; k < nr; ++k) {
       RedJob& r = R.j[k];

@@ -68,6 +68,19 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor alpha, int c_off, bool time_major=False) -> Tensor");
   m.def("gcn_pool_bwd_input(Tensor x, Tensor w, Tensor mask, Tensor dout, Tensor W, Tensor b, Tensor scale, "
         "Tensor shift, Tensor alpha, Tensor dzcoef, int c_off, bool time_major=False) -> Tensor");
+  // window gather + GeneralConv + pooling from the resident store (gcn_fused.hip)
+  m.def("gcn_window_prep(Tensor series, Tensor shift, Tensor scale, Tensor win_group, Tensor win_center, "
+        "Tensor win_valid, Tensor group_adj, Tensor group_anom_pos, int tb, int seq_len, bool time_norm, "
+        "bool agg_mean, int pool) -> Tensor[]");
+  m.def("gcn_fused_fwd(Tensor series, Tensor shift, Tensor scale, Tensor win_group, Tensor win_center, "
+        "Tensor win_valid, Tensor win_label, Tensor group_anom_pos, Tensor mom, Tensor pw, Tensor wids, "
+        "Tensor table, Tensor? cursor, int tb, int seq_len, bool time_norm, Tensor W, Tensor b, Tensor gamma, "
+        "Tensor beta, Tensor alpha, Tensor(a!) rmean, Tensor(b!) rvar, bool training, float momentum, float eps, "
+        "int Mp, int Cp) -> Tensor[]");
+  m.def("gcn_fused_bwd(Tensor dh, int c_off, Tensor series, Tensor shift, Tensor scale, Tensor win_group, "
+        "Tensor win_center, Tensor win_valid, Tensor group_anom_pos, Tensor pw, Tensor wids, Tensor table, "
+        "Tensor? cursor, int tb, int seq_len, bool time_norm, Tensor S, Tensor st, Tensor W, Tensor b, "
+        "Tensor alpha, Tensor(a!) dW, Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) dalpha) -> ()");
   // per-node GeneralConv writing the time-major LSTM input (gcn_node.hip)
   m.def("gcn_adj_bits(Tensor adj, bool agg_mean) -> Tensor[]");
   m.def("gcn_node_fwd(Tensor x, Tensor bits, Tensor rs, Tensor mask, Tensor W, Tensor b, Tensor scale, "
@@ -94,6 +107,9 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("adam_guarded(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor(e!) step, float beta1, "
         "float beta2, float eps, float grad_scale, float weight_decay, Tensor(f!) state, Tensor(g!)? ext=None, "
         "Tensor(h!)? cursor=None, int cursor_mod=1) -> bool");
+  m.def("adam_flagged(Tensor(a!) p, Tensor(d!) g, Tensor(b!) m, Tensor(c!) v, Tensor lr, Tensor(e!) step, float beta1, "
+        "float beta2, float eps, float grad_scale, float weight_decay, Tensor(f!) state, Tensor(g!) ext, "
+        "Tensor(h!)? cursor=None, int cursor_mod=1) -> ()");
   m.def("nonfinite_count(Tensor x) -> Tensor");
   m.def("ig_interp(Tensor v, Tensor alpha) -> Tensor");
   m.def("ig_accum(Tensor(a!) acc, Tensor g, Tensor w) -> ()");

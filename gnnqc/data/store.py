@@ -180,6 +180,31 @@ class DeviceStore:
             self.win_label_valid = torch.from_numpy(lv).to(dev)
         self.t_offsets = torch.arange(-self.tb, self.seq_len - self.tb, device=dev)
 
+    def gcn_fused_data(self, agg_mean: bool, pool: int) -> dict:
+        """Operands of the fused gather + GCN kernels (``gcn_fused.hip``): the store tensors plus
+        the per-window tables that depend only on the data (fp64 moments of each window's
+        normalised values, the node pooling weights of each window for this aggregation / pooling),
+        computed once per (aggregation, pooling) on first use - never inside a graph capture."""
+        key = (bool(agg_mean), int(pool))
+        cache = self.__dict__.setdefault("_gcn_fused", {})
+        d = cache.get(key)
+        if d is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("DeviceStore.gcn_fused_data: first use inside a HIP graph capture; call it "
+                                   "(or run one eager step) before capturing")
+            from ..utils.native import hip_ops
+            mom, pw = hip_ops().gcn_window_prep(self.series, self.shift, self.scale, self.win_group, self.win_center,
+                                                self.win_valid_u8, self.group_adj, self.group_anom_pos, self.tb,
+                                                self.seq_len, self.time_varying_norm, bool(agg_mean), int(pool))
+            d = {"fwd": (self.series, self.shift, self.scale, self.win_group, self.win_center, self.win_valid_u8,
+                         self.win_label, self.group_anom_pos, mom, pw),
+                 "bwd": (self.series, self.shift, self.scale, self.win_group, self.win_center, self.win_valid_u8,
+                         self.group_anom_pos, pw),
+                 "dims": (self.tb, self.seq_len, self.time_varying_norm),
+                 "ca": self.n_feat, "mom": mom, "pw": pw}
+            cache[key] = d
+        return d
+
     @property
     def n_windows(self) -> int:
         return int(self.win_center.shape[0])

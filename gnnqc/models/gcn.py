@@ -25,7 +25,8 @@ import torch
 import torch.nn as nn
 
 from ..config import freq_minutes
-from ..ops.gcn import gcn_node_tm, gcn_node_tm_ok, gcn_pool, gcn_pool_hip_ok, pool_nodes
+from ..ops.gcn import (gcn_node_tm, gcn_node_tm_ok, gcn_pool, gcn_pool_from_store, gcn_pool_hip_ok, pool_nodes,
+                       store_gcn_ok)
 from .graphconv import GeneralConv, make_graph_layer
 from .layers import Dense, Dropout, LeakyReLU
 from .spatial import SensorsTimeLayer, SpatialTransformer
@@ -235,6 +236,35 @@ class GCNClassifier(nn.Module):
         yf = y.reshape(-1).float().contiguous()
         mf = mask.reshape(-1).float().contiguous()
         return self.time_layer.forward_time_major_head(h, M, spec[:3], spec[3:], yf, mf, w0, w1, sums, hist)
+
+    def store_fused_ok(self, store) -> bool:
+        """Whether :meth:`fused_store_loss` applies: the CML headed-chain configuration, on the GPU,
+        with the window store as the input (gather, GCN and pooling fused into one launch)."""
+        spec = self.head_spec()
+        if spec is None or not self.per_sensor or not self._fused_ok() or self.sensors_time_layer is not None:
+            return False
+        if self.spatial_transformer is not None:
+            return False
+        if any(d.kernel.shape[1] != 64 for d in spec[:2]) or spec[2].kernel.shape != (64, 1):
+            return False
+        if spec[0].kernel.shape[0] != 128 or (self.training and (self.dropout1.rate or self.dropout2.rate)):
+            return False
+        pooling = "selection" if self.pooling_type == "selection" else self.aggregation_type
+        return store_gcn_ok(store, self.gcn_layer, self.training, pooling)
+
+    def fused_store_loss(self, store, ids, w0: float, w1: float, sums=None, hist=None):
+        """(loss, logits) of a batch given by window ids (or a device cursor into an id table)
+        straight from the resident store: ONE launch for the window gather + GeneralConv +
+        BatchNorm + PReLU + node pooling + concat (``gcn_fused.hip``), then the headed LSTM chain
+        of :meth:`fused_loss`. Check :meth:`store_fused_ok` first."""
+        spec = self.head_spec()
+        g = self.gcn_layer
+        pooling = "selection" if self.pooling_type == "selection" else self.aggregation_type
+        h, M, y, ym, _ = gcn_pool_from_store(store, ids, g, self.training, pooling)
+        if not self.time_layer.head_chain_ok(h):
+            from ..ops.head import fused_head_loss
+            return fused_head_loss(self.time_layer.forward_time_major(h, M), *spec, y, ym, w0, w1, sums, hist)
+        return self.time_layer.forward_time_major_head(h, M, spec[:3], spec[3:], y, ym, w0, w1, sums, hist)
 
     def logits(self, inputs) -> torch.Tensor:
         z = self.head(self.features(inputs))

@@ -276,6 +276,89 @@ def gcn_node_tm_eager(x, adj, mask, W, b, gamma, beta, alpha, running_mean, runn
     return F.pad(seq, (0, (-C) % cpad_to, 0, Mp - M)), M
 
 
+class _HipStoreGCN(torch.autograd.Function):
+    """Window gather + GeneralConv + BatchNorm + PReLU + node pooling + concat in ONE launch,
+    straight from the resident window store (``gcn_fused.hip``): ``(h [T, Mp, Cp], y, y_mask,
+    wid)``. Backward: ONE launch adding the parameter gradients with float atomics (training mode
+    only; not bitwise reproducible, so the deterministic mode keeps :class:`_HipGCNPool`)."""
+
+    @staticmethod
+    def forward(ctx, data, ids, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
+                momentum: float, eps: float, Mp: int, Cp: int):
+        from ..utils.native import hip_ops
+        wids, table, cursor = ids
+        h, S, st, y, ym, wid = hip_ops().gcn_fused_fwd(
+            *data["fwd"], wids, table, cursor, *data["dims"], W.contiguous(), b.contiguous(), gamma.contiguous(),
+            beta.contiguous(), alpha.contiguous(), running_mean, running_var, bool(training), float(momentum),
+            float(eps), int(Mp), int(Cp))
+        ctx.data, ctx.ids, ctx.training = data, ids, bool(training)
+        ctx.params = (W, b, gamma, beta, alpha)
+        ctx.save_for_backward(W, b, alpha, S, st)
+        ctx.mark_non_differentiable(y, ym, wid)
+        ctx.set_materialize_grads(False)
+        return h, y, ym, wid
+
+    @staticmethod
+    def backward(ctx, dh, _dy, _dym, _dwid):
+        from ..utils.native import hip_ops
+        from .lstm import _grad_sink
+        W, b, alpha, S, st = ctx.saved_tensors
+        need = ctx.needs_input_grad[2:7]
+        if dh is None or not any(need):
+            return (None,) * 14
+        if not ctx.training:
+            raise RuntimeError("gcn_fused backward: parameter gradients in eval mode take the generic path")
+        sinks = [(_grad_sink(p) if n else (torch.zeros_like(p), False)) for p, n in zip(ctx.params, need)]
+        wids, table, cursor = ctx.ids
+        hip_ops().gcn_fused_bwd(dh.contiguous(), int(ctx.data["ca"]), *ctx.data["bwd"], wids, table, cursor,
+                                *ctx.data["dims"], S, st, W.contiguous(), b.contiguous(), alpha.contiguous(),
+                                sinks[0][0], sinks[2][0], sinks[3][0], sinks[4][0])
+        grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need)]
+        return (None, None, *grads, None, None, None, None, None, None, None)
+
+
+def store_gcn_ok(store, layer, training: bool, pooling: str) -> bool:
+    """Whether :func:`gcn_pool_from_store` runs for this store / GeneralConv configuration."""
+    from . import deterministic, use_hip
+    if not (use_hip(store.series) and getattr(store, "per_sensor", False) and store.series.dtype == torch.float32
+            and store.win_label.dim() == 1):
+        return False
+    if training and deterministic():
+        return False
+    W = layer.kernel
+    C, N = store.n_feat, store.n_nodes
+    return (layer.aggregate in ("mean", "sum") and pooling in ("mean", "sum", "selection")
+            and not (layer.dropout and training) and W.shape[0] == C and 1 <= C <= 4 and N * C <= 128
+            and W.shape[1] in (8, 16, 32) and store.seq_len >= 1)
+
+
+def gcn_pool_from_store(store, ids, layer, training: bool, pooling: str = "mean"):
+    """The CML GCN front end of a training / evaluation step straight from ``store``:
+    ``(h [T, Mp, Cp], B, y [B], y_mask [B], wid [B])`` with ``h`` the time-major LSTM input
+    (``[flagged series | pooled GCN | 0 pad]``) of :meth:`gnnqc.models.timelayer.TimeLayer.forward_time_major`.
+    ``ids``: window ids [B] (-1 = padding) or a :class:`gnnqc.data.store.CursorIds`."""
+    from ..data.store import CursorIds
+    agg_mean = layer.aggregate == "mean"
+    pool = {"mean": 0, "sum": 1, "selection": 2}[pooling]
+    data = store.gcn_fused_data(agg_mean, pool)
+    e = store.series.new_zeros(0, dtype=torch.long)
+    if isinstance(ids, CursorIds):
+        idt = (e, ids.table, ids.cursor)
+        B = int(ids.table.shape[1])
+    else:
+        idt = (ids.to(store.device).long().contiguous(), e, None)
+        B = int(idt[0].shape[0])
+    F_ = layer.kernel.shape[1]
+    C = store.n_feat
+    Mp = (B + 15) // 16 * 16
+    Cp = C + F_
+    Cp += (-Cp) % 4
+    h, y, ym, wid = _HipStoreGCN.apply(data, idt, layer.kernel, layer.bias, layer.bn_gamma, layer.bn_beta,
+                                       layer.prelu_alpha, layer.bn_moving_mean, layer.bn_moving_variance,
+                                       bool(training), float(layer.momentum), float(layer.eps), Mp, Cp)
+    return h, B, y, ym, wid
+
+
 def pool_nodes(h: torch.Tensor, mask: torch.Tensor, anom_pos, pooling: str = "mean") -> torch.Tensor:
     """``timeseries_pooling`` over valid nodes: [B,T,N,F] -> [B,T,F]."""
     m = mask[:, None, :, None].to(h.dtype)

@@ -60,8 +60,8 @@ class FlatOptimizer:
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)   # applied steps (bias correction)
         self.iterations = 0                                              # attempted steps (host)
         self.guard = bool(guard)
-        # [nonfinite count, ticket, ok flag, skipped steps, decision generation, -, -, -]
-        # (adam.hip grad_guard / adam_guarded)
+        # [nonfinite count, ticket, ok flag, skipped steps, decision generation, overflowed elements
+        # (adam_flagged), -, -] (adam.hip grad_guard / adam_guarded / adam_flagged)
         self.guard_state = torch.zeros(8, device=dev, dtype=torch.int32)
         self.guard_state[2] = 1
         # multi-step graphs (gnnqc.train.engine): a device batch cursor the update advances
@@ -153,6 +153,10 @@ class FlatAdam(FlatOptimizer):
         # the HIP update clears the gradient buffer once it has read it (no separate zero-fill
         # launch per training step); the trainer then skips zero_grad (grad_zeroed_by_step)
         self.zero_grad_in_step = self.flat_p.is_cuda
+        # set by the trainer when EVERY kernel writing this model's gradients flags non-finite
+        # values (chain control word 7): the update then decides from the flags (adam_flagged, no
+        # grid-wide scan of the gradient buffer)
+        self.flagged_producers = False
 
     @property
     def grad_zeroed_by_step(self) -> bool:
@@ -166,6 +170,12 @@ class FlatAdam(FlatOptimizer):
             # guard + update (+ batch cursor) as ONE launch when the buffer fits a co-resident grid
             from ..utils.native import hip_ops
             from .lstm import chain_ctl
+            if self.flagged_producers:
+                hip_ops().adam_flagged(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
+                                       self.beta2, self.eps, float(grad_scale), self.wd, self.guard_state,
+                                       chain_ctl(self.flat_g.device), self.cursor, int(self.cursor_mod))
+                self.iterations += 1
+                return
             if hip_ops().adam_guarded(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
                                       self.beta2, self.eps, float(grad_scale), self.wd, self.guard_state,
                                       chain_ctl(self.flat_g.device), self.cursor, int(self.cursor_mod)):

@@ -127,11 +127,26 @@ class Trainer:
         self._cursor = torch.zeros(1, dtype=torch.long, device=self.device)
         self._graph_loss = None
         self._multi_loss = None
+        # the store-fused CML step's gradient kernels all flag non-finite values: the update can
+        # decide from those flags (one pass, no grid-wide barrier; gnnqc.ops.optim.FlatAdam)
+        if hasattr(self.opt, "flagged_producers"):
+            was = self.model.training
+            self.model.train()
+            self.opt.flagged_producers = bool(
+                self.device.type == "cuda" and self._store_fused() and self.model.regularization_loss() is None
+                and os.environ.get("GNNQC_FLAGGED_ADAM", "1") == "1")
+            self.model.train(was)
 
     # ---------------------------------------------------------------- body
     def _loss(self, wids, metrics: Optional["MetricAccumulator"] = None):
         """(total, loss, logits, batch). With a fused-head model the loss, logits and
         the metric update come out of one HIP kernel (``gnnqc.ops.head``)."""
+        if self._store_fused():
+            # the gather is fused into the GCN kernel: no Batch is materialised
+            loss, z = self.model.fused_store_loss(self.store, wids, self.w0, self.w1,
+                                                  metrics.sums if metrics else None, metrics.hist if metrics else None)
+            reg = self.model.regularization_loss()
+            return (loss + reg if reg is not None else loss), loss, z, None
         with _rf("gnnqc.gather"):
             b = self.store.gather(wids)
             inputs = b.model_inputs(self.ds_type, self.baseline)
@@ -155,6 +170,17 @@ class Trainer:
         reg = self.model.regularization_loss() if hasattr(self.model, "regularization_loss") else None
         total = loss + reg if reg is not None else loss
         return total, loss, z, b
+
+    def _store_fused(self) -> bool:
+        """The CML headed-chain model reads its batches straight from the store (one launch for
+        gather + GCN + pooling, ``gnnqc.ops.gcn.gcn_pool_from_store``). Decided once per mode;
+        ``GNNQC_STORE_GCN=0`` keeps the gather + generic GCN kernels (A/B measurements)."""
+        key = bool(self.model.training)
+        cache = self.__dict__.setdefault("_store_fused_cache", {})
+        if key not in cache:
+            cache[key] = (not self.baseline and os.environ.get("GNNQC_STORE_GCN", "1") == "1"
+                          and hasattr(self.model, "store_fused_ok") and self.model.store_fused_ok(self.store))
+        return cache[key]
 
     def _body(self, wids, with_opt: bool):
         # every training step ends with the optimizer update (here, or after the DP all-reduce);
