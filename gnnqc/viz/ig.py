@@ -5,10 +5,10 @@ and ``xai/libs/visualize.py``).
   a time heatmap underneath, then one row per neighbour node (attributions scaled by
   ``plot.heatmap.scale_feature_gradients``), diverging colormap with the configured
   limits (``_plot_ig_heatmap``, ``:1612-1891``);
-* :func:`plot_ig_heatmap_from_directory` - redo every sample directory written by the
-  explainer (``:1893-2044``);
+* :func:`plot_ig_heatmap_from_directory` - heatmaps of the sample directories written by the
+  explainer, filtered by sensor / centre-time range and split over workers (``:1893-2044``);
 * :func:`plot_gradient_saturation` - model output along the alpha path (``:1516-1610``);
-* :func:`plot_interpolated_series` - a few interpolated inputs (``:1415-1466``).
+* :func:`plot_interpolated_series` - every 10th interpolated input along the path (``:1415-1466``).
 """
 from __future__ import annotations
 
@@ -134,21 +134,68 @@ def parse_sample_dir(name: str) -> dict:
     return {"sensor": sensor, "date": f"{day}_{tod}", "true": int(true), "pred": int(pred)}
 
 
-def plot_ig_heatmap_from_directory(directory: str, xai_config=None, overwrite: bool = True):
-    out = []
-    for d in sorted(glob.glob(os.path.join(directory, "*", "*"))):
+def list_sample_dirs(directory: str, sensors=None, time_from=None, time_to=None) -> list:
+    """Sample directories ``<directory>/<sensor>/<sample>`` of an explainer run, as
+    ``(sensor, sample)`` pairs sorted by sample name (``integrated_gradients.py:1903-1936``): the
+    sensor directories (all but ``log`` and dot files, or the given ``sensors``), then, with both
+    ``time_from`` and ``time_to``, only samples whose centre time (parsed from the name) lies in
+    [time_from, time_to]."""
+    import pandas as pd
+    if sensors is None:
+        sensors = sorted(os.listdir(directory)) if os.path.isdir(directory) else []
+    sensors = [str(s) for s in sensors if s != "log" and not str(s).startswith(".")]
+    pairs = []
+    for sensor in sensors:
+        d = os.path.join(directory, sensor)
         if not os.path.isdir(d):
             continue
+        for dn in os.listdir(d):
+            if os.path.isdir(os.path.join(d, dn)):
+                pairs.append((sensor, dn))
+    pairs.sort(key=lambda p: p[1])
+    if time_from is not None and time_to is not None:
+        lo, hi = pd.to_datetime(time_from), pd.to_datetime(time_to)
+        keep = []
+        for sensor, dn in pairs:
+            try:
+                t = pd.to_datetime(parse_sample_dir(dn)["date"], format="%Y%m%d_%H%M%S")
+            except ValueError:
+                continue
+            if lo <= t <= hi:
+                keep.append((sensor, dn))
+        pairs = keep
+    return pairs
+
+
+def plot_ig_heatmap_from_directory(directory: str, xai_config=None, overwrite: bool = False, sensors=None,
+                                   time_from=None, time_to=None, workerid: Optional[int] = None,
+                                   n_worker: Optional[int] = None, stem: Optional[str] = None):
+    """Heatmaps of every saved sample (``integrated_gradients.py:1893-2044``): selected by sensor and
+    centre-time range (:func:`list_sample_dirs`), split round-robin over ``n_worker`` workers
+    (SLURM array / ``--shard``), written as ``ig_heatmap_<stem>_<sample>.png`` next to the sample's
+    arrays (``stem`` = ``<project>_<ds_type>_<dataset>``; default: taken from the array names).
+    Existing heatmaps are kept unless ``overwrite``. Returns the written paths."""
+    samples = list_sample_dirs(directory, sensors, time_from, time_to)
+    if workerid is not None and n_worker:
+        samples = [s for i, s in enumerate(samples) if i % n_worker == workerid]
+    out = []
+    for sensor, dn in samples:
+        d = os.path.join(directory, sensor, dn)
         try:
-            rec = parse_sample_dir(os.path.basename(d))
+            rec = parse_sample_dir(dn)
         except ValueError:
             continue
         files = _load_sample_dir(d)
-        if not files:
+        if "features_unwrapped" not in files:      # (the reference skips samples without features)
             continue
         if "predictions_unwrapped" in files:
             rec["score"] = float(np.asarray(files["predictions_unwrapped"]).reshape(-1)[0])
-        p = os.path.join(d, f"ig_heatmap_{os.path.basename(d)}.png")
+        st = stem
+        if st is None:
+            hit = [f for f in os.listdir(d) if f.startswith("features_unwrapped_") and f.endswith(f"_{dn}.npy")]
+            st = hit[0][len("features_unwrapped_"):-len(f"_{dn}.npy")] if hit else None
+        name = f"ig_heatmap_{st}_{dn}.png" if st else f"ig_heatmap_{dn}.png"
+        p = os.path.join(d, name)
         if os.path.exists(p) and not overwrite:
             continue
         out.append(plot_ig_heatmap(files, rec, xai_config, p))
@@ -173,18 +220,27 @@ def plot_gradient_saturation(path_pred: np.ndarray, out_path: str, normalize: bo
     return out_path
 
 
-def plot_interpolated_series(series: np.ndarray, alphas: np.ndarray, out_path: str, n_show: int = 5):
-    """``series`` [m+1, T, C] interpolated inputs of one sample."""
-    idx = np.linspace(0, len(alphas) - 1, n_show).round().astype(int)
-    fig, axes = plt.subplots(1, n_show, figsize=(3 * n_show, 2.5), sharey=True)
-    for ax, i in zip(np.atleast_1d(axes), idx):
-        ax.plot(series[i])
-        ax.set_title(f"alpha {alphas[i]:.2f}")
+def plot_interpolated_series(series: np.ndarray, alphas: np.ndarray, out_path: str, every: int = 10,
+                             max_steps: int = 500):
+    """Every ``every``-th interpolated input of one sample along the alpha path, one row each
+    (``_plot_interpolated_data_element_series``, ``integrated_gradients.py:1415-1466``):
+    ``series`` [m+1, T, C] (flagged series) or [m+1, N, T, C] (node features: node 0 drawn)."""
+    series = np.asarray(series)
+    if series.ndim == 4:
+        series = series[:, 0]
+    sel = list(range(0, len(alphas), every))
+    ymin, ymax = float(np.min(series)), float(np.max(series))
+    fig = plt.figure(figsize=(20, 10))
+    for k, i in enumerate(sel):
+        ax = fig.add_subplot(len(sel), 1, k + 1)
+        ax.set_title(f"alpha: {alphas[i]:.1f}")
+        ax.plot(series[i][:max_steps])
+        ax.set_ylim(ymin, ymax if ymax > ymin else ymin + 1)
     fig.tight_layout()
-    fig.savefig(out_path, bbox_inches="tight")
+    fig.savefig(out_path, dpi=50)
     plt.close(fig)
     return out_path
 
 
 __all__ = ["plot_ig_heatmap", "plot_ig_heatmap_from_directory", "plot_gradient_saturation",
-           "plot_interpolated_series", "parse_sample_dir"]
+           "plot_interpolated_series", "parse_sample_dir", "list_sample_dirs"]

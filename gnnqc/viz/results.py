@@ -119,8 +119,11 @@ def extract_target_info(windows, window_ids, timeseries_out: bool = False, store
 
 def timeseries_figure(predicted, true, sensor_timeseries, sensor_id, dates, outdir, anomaly_time_ind,
                       model_config=None, ds_type="cml", alpha: Optional[float] = None):
-    """One window: the flagged sensor's channels, the centre step shaded by outcome."""
+    """One window: the flagged sensor's channels, the centre step shaded by outcome. ``outdir``
+    with a file extension is the output path itself (``libs/visualize.py:201-206``)."""
     alpha = alpha if alpha is not None else float(((model_config or {}).get("plotting") or {}).get("alpha", 0.2))
+    target = outdir if os.path.splitext(str(outdir))[1] else None
+    outdir = (os.path.dirname(target) or ".") if target else outdir
     os.makedirs(outdir, exist_ok=True)
     dates = np.asarray(dates).astype("datetime64[m]").astype(object)
     sensor_timeseries = np.asarray(sensor_timeseries, np.float64)
@@ -149,7 +152,8 @@ def timeseries_figure(predicted, true, sensor_timeseries, sensor_id, dates, outd
     curr = dates[anomaly_time_ind]
     ax.set_title(f"{sensor_id} on {curr}", pad=12)
     ax.legend(handles=legend)
-    outpath = os.path.join(outdir, f"{sensor_id}_{curr}_true_{int(true)}_pred_{int(predicted)}.png".replace(":", "-"))
+    outpath = target or os.path.join(outdir,
+                                     f"{sensor_id}_{curr}_true_{int(true)}_pred_{int(predicted)}.png".replace(":", "-"))
     fig.savefig(outpath, bbox_inches="tight")
     plt.close(fig)
     return outpath

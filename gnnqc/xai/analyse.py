@@ -41,6 +41,7 @@ from ..viz.ig import parse_sample_dir  # noqa: E402
 from .ig import CONFUSION  # noqa: E402
 
 COLOR_MAP = {(0, 0): "white", (0, 1): "orange", (1, 0): "red", (1, 1): "green"}
+TL_COLORS = [(1 / 255, 183 / 255, 1.0), (0.0, 117 / 255, 177 / 255), (0.2, 0.6, 0.2), (0.5, 0.5, 0.5)]
 COLOR_NAMES = {(0, 0): "True Negative", (0, 1): "False Positive", (1, 0): "False Negative", (1, 1): "True Positive"}
 STEM_GF, STEM_GA = "gradients_features_unwrapped", "gradients_anom_ts_unwrapped"
 STEM_F, STEM_A = "features_unwrapped", "anom_ts_unwrapped"
@@ -222,88 +223,152 @@ class IntegrateGradientsAnalyser:
 
     def plot_agg_samples_over_time(self, sensor: str, time_from=None, time_to=None, agg_type: Optional[str] = None,
                                    norm_by_prediction: Optional[bool] = None, cbar_limits=None) -> Optional[str]:
-        """Consecutive samples of one sensor: centre value of the flagged series, score,
-        outcome, and the per-sample aggregated attribution (over time) of every channel
-        and neighbour - a spatio-temporal attribution map (``:1169-1710``)."""
+        """Spatio-temporal attribution map of one sensor (``integrated_gradients_analyser.py:1169-1710``).
+
+        Frames sit on a regular grid of ``aggregate_sample_along_time.interval`` seconds from
+        ``time_from`` to ``time_to`` (default: the sensor's first / last sample); a grid time with
+        no saved sample is a NaN frame (a gap stays a gap). Per frame: the flagged channels and
+        every neighbour's channels at the window centre, the prediction, the outcome, and each
+        series' attribution aggregated over the window's time steps (``agg_type``), optionally
+        divided by the prediction (``norm_by_prediction``) - drawn as coloured bands under the
+        series. A frame whose neighbour count differs from the first frame's is NaN, as in the
+        reference. Written as ``agg_samples_over_time_<sensor>_<from>-<to>_<agg>[_norm].png`` in
+        the analysis directory (the paper's script draws each range with and without the
+        normalisation, ``run_integrated_gradients_analyser_20240318.py:25-36``)."""
         cfg = self.an.aggregate_sample_along_time
         agg_type = agg_type or cfg.agg_type
-        norm_by_prediction = cfg.norm_by_prediction if norm_by_prediction is None else norm_by_prediction
+        norm_by_prediction = bool(cfg.norm_by_prediction if norm_by_prediction is None else norm_by_prediction)
         cbar_limits = cbar_limits if cbar_limits is not None else cfg.cbar_limits
         if self.df_unfiltered is None:
             self.get_overview(plots=False)
         sub = self.df_unfiltered[self.df_unfiltered["sensor_id"] == str(sensor)].sort_values("date_time")
-        if time_from is not None:
-            sub = sub[sub["date_time"] >= pd.to_datetime(time_from)]
-        if time_to is not None:
-            sub = sub[sub["date_time"] <= pd.to_datetime(time_to)]
+        if time_from is not None and time_to is not None:
+            time_from, time_to = pd.to_datetime(time_from), pd.to_datetime(time_to)
+            sub = sub[(sub["date_time"] >= time_from) & (sub["date_time"] <= time_to)]
         if not len(sub):
+            return None
+        if time_from is None or time_to is None:
+            time_from, time_to = sub["date_time"].min(), sub["date_time"].max()
+        grid = pd.date_range(start=time_from, end=time_to, freq=pd.Timedelta(int(cfg.interval), unit="s"))
+        if not len(grid):
             return None
         agg = {"mean": np.nanmean, "sum": np.nansum, "max": np.nanmax, "min": np.nanmin}[agg_type]
         tb = int(round(self.preproc_config.timestep_before / max(1, int(self.preproc_config.get("freq", 1) or 1))))
-        times, centre, scores, flags, ga_rows, gf_rows = [], [], [], [], [], []
-        n_nb = None
         scale = cfg.scale_feature_gradients
-        for _, row in sub.iterrows():
-            a, ga, gf = self._load(row, STEM_A), self._load(row, STEM_GA), self._load(row, STEM_GF)
-            p = self._load(row, STEM_P)
+        by_time = {pd.Timestamp(r["date_time"]): r for _, r in sub.iterrows()}
+        frames = []
+        shape_nb = None
+        for t in grid:
+            row = by_time.get(pd.Timestamp(t))
+            if row is None:
+                frames.append(None)
+                continue
+            a, ga, gf, f = (self._load(row, k) for k in (STEM_A, STEM_GA, STEM_GF, STEM_F))
+            p, y = self._load(row, STEM_P), self._load(row, STEM_Y)
+            if a is None or ga is None or gf is None or f is None:
+                frames.append(None)
+                continue
             score = float(np.asarray(p).reshape(-1)[0]) if p is not None else np.nan
-            if norm_by_prediction and score > 0:
-                ga = ga / score if ga is not None else None
-                gf = gf / score if gf is not None else None
-            if gf is not None:
-                gf = gf / gf.shape[0] * 2 if scale == "auto" else gf * float(scale)
-                if n_nb is None:
-                    n_nb = gf.shape[0]
-                if gf.shape[0] != n_nb:      # neighbour set changed: mark missing (reference does the same)
-                    gf = np.full((n_nb,) + gf.shape[1:], np.nan)
-            times.append(row["date_time"])
-            centre.append(a[min(tb, a.shape[0] - 1)] if a is not None else np.nan)
-            scores.append(score)
-            flags.append(row["true"])
-            ga_rows.append(agg(ga, axis=0) if ga is not None else None)
-            gf_rows.append(agg(gf, axis=1) if gf is not None else None)
+            if norm_by_prediction:
+                ga, gf = ga / score, gf / score
+            gf = gf / gf.shape[0] * 2 if scale == "auto" else gf * float(scale)
+            if shape_nb is None:
+                shape_nb = gf.shape
+            if gf.shape != shape_nb:                   # the neighbour set changed: a missing frame
+                frames.append(("nb", a, score, y))
+                continue
+            frames.append((a[min(tb, a.shape[0] - 1)], score, float(np.asarray(y).reshape(-1)[0]) if y is not None
+                           else float(row["true"]), agg(ga, axis=0), agg(gf, axis=1), f[:, min(tb, f.shape[1] - 1)]))
+        if shape_nb is None:
+            return None
+        n_nb, C = shape_nb[0], shape_nb[2]
+        S = len(grid)
+        anom_c = np.full((S, C), np.nan)
+        pred = np.full(S, np.nan)
+        flag = np.full(S, np.nan)
+        ga_agg = np.full((S, C), np.nan)
+        gf_agg = np.full((S, n_nb, C), np.nan)
+        feat_c = np.full((S, n_nb, C), np.nan)
+        for i, fr in enumerate(frames):
+            if fr is None:
+                continue
+            if isinstance(fr[0], str):                 # neighbour set changed: series / score, no attribution
+                _, a, score, y = fr
+                anom_c[i] = a[min(tb, a.shape[0] - 1)]
+                pred[i] = score
+                continue
+            anom_c[i], pred[i], flag[i], ga_agg[i], gf_agg[i], feat_c[i] = fr
+        if isinstance(cbar_limits, (list, tuple)):
+            vmin, vmax = float(cbar_limits[0]), float(cbar_limits[1])
+        else:
+            vmin, vmax = float(np.nanmin(gf_agg)), float(np.nanmax(gf_agg))
+            if not np.isfinite(vmin) or vmin == vmax:
+                vmin, vmax = -1.0, 1.0
+        norm = mcolors.Normalize(vmin=vmin, vmax=vmax)
+        group = bool(cfg.get("group_tl_channels", True))
+        if group:
+            import warnings
+            with warnings.catch_warnings():           # (NaN frames: all-NaN rows are expected)
+                warnings.simplefilter("ignore", RuntimeWarning)
+                gf_rows = [(f"N{j} TL", feat_c[:, j, :], np.nanmean(gf_agg[:, j, :], axis=1)) for j in range(n_nb)]
+        else:
+            gf_rows = [(f"N{j} TL{c + 1}", feat_c[:, j, c:c + 1], gf_agg[:, j, c]) for j in range(n_nb) for c in range(C)]
         thr = float(self.ig.threshold)
-        pred_cls = (np.asarray(scores) > thr).astype(int)
-        rows_maps = []
-        if any(g is not None for g in ga_rows):
-            rows_maps.append(("flagged", np.stack([g for g in ga_rows if g is not None]).T))
-        if any(g is not None for g in gf_rows):
-            G = np.stack([g for g in gf_rows if g is not None])               # [S, n_nb, C]
-            if cfg.get("group_tl_channels", True):
-                G = G.mean(-1, keepdims=True)
-            for j in range(G.shape[1]):
-                rows_maps.append((f"node {j}", G[:, j].T))
-        nrows = 2 + len(rows_maps)
-        fig, axes = plt.subplots(nrows, 1, figsize=tuple(cfg.figsize), sharex=True,
-                                 height_ratios=[2, 0.5] + [1] * len(rows_maps))
-        x = np.arange(len(times))
-        cen = np.asarray([c if np.ndim(c) else [c] for c in centre], dtype=np.float64)
-        axes[0].plot(x, cen)
-        axes[0].plot(x, scores, color="k", linewidth=0.8, label="score")
-        if isinstance(cfg.ylims, (list, tuple)):
-            axes[0].set_ylim(*cfg.ylims)
-        axes[0].legend(loc="upper right")
-        cols = [COLOR_MAP[(int(t), int(p))] for t, p in zip(flags, pred_cls)]
-        axes[1].bar(x, 1, width=1.0, color=cols, edgecolor="none")
-        axes[1].set_yticks([])
-        vmin, vmax = (cbar_limits if isinstance(cbar_limits, (list, tuple)) else
-                      (-np.nanmax(np.abs(np.concatenate([m.reshape(-1) for _, m in rows_maps]))),
-                       np.nanmax(np.abs(np.concatenate([m.reshape(-1) for _, m in rows_maps])))))
+        pred_cls = np.where(pred > thr, 1.0, np.where(np.isnan(pred), np.nan, 0.0))
+        cval = {(0, 0): 0.0, (0, 1): 0.33, (1, 0): 0.66, (1, 1): 1.0}
+        cvals = np.array([0.0 if (np.isnan(t) or np.isnan(q)) else cval[(int(t), int(q))]
+                          for t, q in zip(flag, pred_cls)])
+        cmap_cm = mcolors.LinearSegmentedColormap.from_list(
+            "confusion", list(zip([0.0, 0.33, 0.66, 1.0], ["white", "orange", "red", "green"])))
+        rows = 1 + C + len(gf_rows)
+        fig, axes = plt.subplots(rows, 1, figsize=(max(8.0, S / 300), 2 + 0.5 + 0.9 * rows), sharex=True,
+                                 squeeze=False)
+        axes = axes[:, 0]
+        X = np.linspace(-0.5, S - 0.5, S + 1)
+        x = X[:-1] + 0.5
+        ylims = cfg.ylims
+        fixed = isinstance(ylims, (list, tuple))
+
+        def band(ax, series, z):
+            lo, hi = (float(ylims[0]), float(ylims[1])) if fixed else (np.nanmin(anom_c), np.nanmax(anom_c))
+            if not np.isfinite(lo) or lo == hi:
+                lo, hi = 0.0, 1.0
+            m = ax.pcolormesh(X, [lo, hi], np.reshape(z, (1, S)), norm=norm, alpha=0.8, cmap="RdBu_r")
+            for c in range(series.shape[1]):
+                ax.plot(x, series[:, c], color=TL_COLORS[c % len(TL_COLORS)], linewidth=0.8)
+            ax.set_ylim(lo, hi)
+            return m
+
+        top = axes[0]
+        top.pcolormesh(X, [0, 1], cvals.reshape(1, S), alpha=0.2, cmap=cmap_cm, vmin=0, vmax=1)
+        top.plot(x, pred, color="k", linewidth=0.8)
+        top.set_ylim(0, 1)
+        top.set_ylabel("Prediction")
+        top.legend(handles=[plt.Rectangle((0, 0), 1, 1, facecolor=c, edgecolor="grey", alpha=0.2, label=l)
+                            for c, l in zip(["white", "orange", "red", "green"], ["TN", "FP", "FN", "TP"])],
+                   loc="upper center", bbox_to_anchor=(0.5, -0.05), ncol=4, frameon=False, fontsize=7)
         mesh = None
-        for ax, (name, m) in zip(axes[2:], rows_maps):
-            mesh = ax.pcolormesh(np.arange(len(x) + 1) - 0.5, np.arange(m.shape[0] + 1), m, cmap="RdBu_r",
-                                 vmin=vmin, vmax=vmax, shading="flat")
-            ax.set_ylabel(name, rotation=0, ha="right", fontsize=7)
-            ax.set_yticks([])
-        if mesh is not None:
-            fig.colorbar(mesh, ax=list(axes[2:]), shrink=0.8)
-        tick = max(1, len(x) // 8)
+        for c in range(C):
+            mesh = band(axes[1 + c], anom_c[:, c:c + 1], ga_agg[:, c])
+            axes[1 + c].set_ylabel(f"TL {c + 1}", rotation=0, labelpad=30)
+        axes[1].set_title("Flagged Sensor", fontsize=9)
+        for k, (name, series, z) in enumerate(gf_rows):
+            mesh = band(axes[1 + C + k], series, z)
+            axes[1 + C + k].set_ylabel(name, rotation=0, labelpad=30, fontsize=7)
+        if gf_rows:
+            axes[1 + C].set_title("Self Reference Cycle and Neighbouring Sensors", fontsize=9)
+        tick = max(1, S // 8)
+        axes[-1].set_xlim(x[0], x[-1] if S > 1 else x[0] + 1)
         axes[-1].set_xticks(x[::tick])
-        axes[-1].set_xticklabels([pd.Timestamp(t).strftime("%m-%d %H:%M") for t in times][::tick], rotation=30)
-        fig.suptitle(f"{sensor}: {agg_type} attribution per sample")
-        d = os.path.join(self.output_dir_analysis, str(sensor))
-        os.makedirs(d, exist_ok=True)
-        p = os.path.join(d, f"agg_samples_over_time_{agg_type}.png")
+        axes[-1].set_xticklabels([t.strftime("%m-%d %H:%M") for t in grid][::tick], rotation=30)
+        if mesh is not None:
+            fig.colorbar(mesh, ax=list(axes[1:]), shrink=0.6, orientation="vertical", label="Attribution")
+        self.last_agg = {"times": grid, "prediction": pred, "flag_true": flag, "anom": anom_c,
+                         "gradients_anom": ga_agg, "gradients_features": gf_agg, "features": feat_c}
+        os.makedirs(self.output_dir_analysis, exist_ok=True)
+        name = (f"agg_samples_over_time_{sensor}_{pd.Timestamp(time_from).strftime('%Y%m%d-%H%M%S')}-"
+                f"{pd.Timestamp(time_to).strftime('%Y%m%d-%H%M%S')}_{agg_type}{'_norm' if norm_by_prediction else ''}.png")
+        p = os.path.join(self.output_dir_analysis, name)
         fig.savefig(p, bbox_inches="tight")
         plt.close(fig)
         return p

@@ -354,12 +354,42 @@ class IntegratedGradientsExplainer:
             res = None
             if not self.ig_cfg.get("load_gradients_from_sample_file", False):
                 res = engine.attribute(batch)
+                if self.ig_cfg.get("plot_interpolated_data_element_series", False):
+                    self._plot_interpolated(batch, bid, int(self.ig_cfg.m_steps))
             else:
                 with torch.no_grad():
                     res = {"pred": self.model(batch.model_inputs(self.ds_type, self.is_baseline)).reshape(
                         len(batch.wid), -1)[:, 0].float()}
             self._unwrap_and_save(bid, batch, ids, res)
         return self.results
+
+    def _plot_interpolated(self, batch, bid: int, m: int):
+        """The batch's first sample along the zero-baseline path x_a = a x (``_interpolate`` +
+        ``_plot_interpolated_data_element_series``, ``integrated_gradients.py:919-942,1415-1466``):
+        ``interpolated_data_element_1_batch_<id>.png`` (flagged series) and ``..._2_..`` (node
+        features) in the output directory."""
+        from ..viz.ig import plot_interpolated_series
+        alphas = np.linspace(0.0, 1.0, m + 1)
+        out = []
+        if batch.anom is not None:
+            a0 = batch.anom[0].detach().float().cpu().numpy()
+            out.append(plot_interpolated_series(alphas[:, None, None] * a0[None], alphas,
+                                                os.path.join(self.output_dir,
+                                                             f"interpolated_data_element_1_batch_{bid}.png")))
+        x0 = batch.x[0].detach().float().cpu().numpy().transpose(1, 0, 2)          # [N, T, C]
+        out.append(plot_interpolated_series(alphas[:, None, None, None] * x0[None], alphas,
+                                            os.path.join(self.output_dir, f"interpolated_data_element_2_batch_{bid}.png")))
+        return out
+
+    def _sample_dates(self, wid: int) -> np.ndarray:
+        """Time stamps of window ``wid`` (``timestep_before`` steps before its centre ... after)."""
+        ws = self.windows
+        g_of, l_of = self._flat if hasattr(self, "_flat") else ws.flat()
+        self._flat = (g_of, l_of)
+        g = ws.groups[int(g_of[wid])]
+        c = int(ws.indices[int(g_of[wid])].center[int(l_of[wid])])
+        tb = int(round(ws.timestep_before / ws.freq))
+        return np.asarray(g.time[c - tb: c - tb + ws.seq_len])
 
     def _sample_info(self, wid: int):
         ws = self.windows
@@ -418,6 +448,13 @@ class IntegratedGradientsExplainer:
                    "score": float(pred[i]), "dir": out, "file_stem": fn,
                    "timestep_before_steps": int(round(self.windows.timestep_before / self.windows.freq))}
             self.results.append(rec)
+            if self.ig_cfg.get("plot_classified_timeseries_sample", False) and anom is not None:
+                # the flagged series of the window, the centre step shaded by outcome
+                # (``plot_classified_timeseries_sample``, ``integrated_gradients.py:1468-1514``)
+                from ..viz.results import timeseries_figure
+                timeseries_figure(pr, tr, anom[i], sensor, self._sample_dates(int(ids[i])),
+                                  os.path.join(out, f"anomalous_ts_{fn}.png"), rec["timestep_before_steps"],
+                                  self.model_config, ds_type=self.ds_type)
             if self.ig_cfg.get("plot_heatmap", False):
                 from ..viz.ig import plot_ig_heatmap
                 plot_ig_heatmap(files, rec, self.xai_config, out_path=os.path.join(out, f"ig_heatmap_{fn}.png"),
@@ -427,9 +464,17 @@ class IntegratedGradientsExplainer:
                 plot_gradient_saturation(files["path_predictions_unwrapped"],
                                          os.path.join(out, f"gradient_saturation_{fn}.png"))
 
-    def plot_ig_heatmap_from_directory(self, directory: Optional[str] = None):
+    def plot_ig_heatmap_from_directory(self, overwrite: bool = False, sensors=None, time_from=None, time_to=None,
+                                       directory: Optional[str] = None):
+        """Heatmaps of the saved samples of ``sensors`` whose centre time lies in
+        [time_from, time_to], this worker's round-robin share (``integrated_gradients.py:1893-2044``;
+        the paper's script calls it once per sensor and range,
+        ``xai/notebooks/run_integrated_gradients_20240318.py:22-31``)."""
         from ..viz.ig import plot_ig_heatmap_from_directory
-        return plot_ig_heatmap_from_directory(directory or self.output_dir, self.xai_config)
+        return plot_ig_heatmap_from_directory(directory or self.output_dir, self.xai_config, overwrite=overwrite,
+                                              sensors=sensors, time_from=time_from, time_to=time_to,
+                                              workerid=self.workerid, n_worker=self.n_worker,
+                                              stem=self._file_name())
 
 
 def run_explainer(args):

@@ -221,3 +221,100 @@ def test_classified_timeseries_plots(cml_small, tmp_path):
     q = classified_timeseries_figure_with_neighbours(["a", "b", "c"], feats, d, true, pred, mc, [False, True, False],
                                                      probabilities=rng.random(50), distances=[1.5, 0.0, 3.2])
     assert os.path.getsize(q) > 0 and os.path.basename(q).startswith("b_")
+
+
+def test_reference_run_scripts_golden(cml_small, tmp_path):
+    """The call sequences of xai/notebooks/run_integrated_gradients_20240318.py and
+    run_integrated_gradients_analyser_20240318.py on a synthetic explainer run: per-sensor,
+    per-time-range heatmaps (no overwrite, round-robin worker split), the optional per-sample plots,
+    and the analyser's aggregated-over-time figures for both normalisation modes on an
+    ``interval`` grid with a missing sample (NaN frame), each under its own file name."""
+    import pandas as pd
+    from gnnqc.ckpt import save_model
+    from gnnqc.viz.ig import list_sample_dirs
+    from gnnqc.xai.analyse import IntegrateGradientsAnalyser
+    pc, ws, _ = cml_small
+    torch.manual_seed(4)
+    mc = C.default("model_cml")
+    mc["plotting"] = {"outdir": str(tmp_path / "plots"), "alpha": 0.2}
+    model = _sharp(create_model(mc, pc))
+    mdir = str(tmp_path / "model")
+    save_model(model, mdir, preproc_config=pc)
+    mc["model_path"] = mdir
+    pc2 = C.Config(dict(pc))
+    pc2["batch_size"] = 16
+
+    def xcfg():
+        xc = C.default("xai_ig")
+        xc["output_dir"] = str(tmp_path / "xplain")
+        ig = xc.integrated_gradients
+        ig["m_steps"], ig["dataset"], ig["threshold"] = 4, "all", 0.5
+        ig["plot_interpolated_data_element_series"] = True
+        ig["plot_classified_timeseries_sample"] = True
+        return xc
+
+    ex = IntegratedGradientsExplainer(pc2, mc, xcfg(), windows=ws, device="cpu")
+    ex.prepare_data()
+    ex.sample_ids = ex.sample_ids[:48]
+    res = ex.get_gradients()
+    assert len(res) == 48
+    for bid in range(3):
+        for k in (1, 2):
+            assert os.path.exists(os.path.join(ex.output_dir, f"interpolated_data_element_{k}_batch_{bid}.png"))
+    for r in res:
+        assert os.path.exists(os.path.join(r["dir"], f"anomalous_ts_{r['file_stem']}.png"))
+    # the script: two sensors, each with its own time range
+    sensors = sorted({r["sensor"] for r in res})
+    s1 = sensors[0]
+    t1 = sorted(pd.to_datetime(r["date"], format="%Y%m%d_%H%M%S") for r in res if r["sensor"] == s1)
+    lo, hi = t1[len(t1) // 4], t1[3 * len(t1) // 4]
+    want = {os.path.basename(r["dir"]) for r in res if r["sensor"] == s1
+            and lo <= pd.to_datetime(r["date"], format="%Y%m%d_%H%M%S") <= hi}
+    out = ex.plot_ig_heatmap_from_directory(sensors=[s1], time_from=str(lo), time_to=str(hi))
+    assert {os.path.basename(os.path.dirname(p)) for p in out} == want and len(out) == len(want)
+    stem = ex._file_name()
+    for p in out:
+        d = os.path.basename(os.path.dirname(p))
+        assert os.path.basename(p) == f"ig_heatmap_{stem}_{d}.png"
+    assert ex.plot_ig_heatmap_from_directory(sensors=[s1], time_from=str(lo), time_to=str(hi)) == []  # no overwrite
+    assert len(ex.plot_ig_heatmap_from_directory(sensors=[s1], time_from=str(lo), time_to=str(hi),
+                                                 overwrite=True)) == len(want)
+    # SLURM-style split of the same selection: disjoint, together the whole set
+    parts = []
+    for i in range(2):
+        exi = IntegratedGradientsExplainer(pc2, mc, xcfg(), windows=ws, device="cpu", shard=f"{i}/2")
+        parts.append({os.path.dirname(p) for p in exi.plot_ig_heatmap_from_directory(overwrite=True)})
+    allp = {os.path.join(ex.output_dir, s, d) for s, d in list_sample_dirs(ex.output_dir)}
+    assert parts[0] and parts[1] and not (parts[0] & parts[1]) and parts[0] | parts[1] == allp
+
+    # analyser script: overview, spatial aggregation, videos, both normalisation modes
+    xc = xcfg()
+    xc.integrated_gradients.analyser["which_sensors"] = [s1]
+    xc.integrated_gradients.analyser.spatial_aggregation["which_samples"] = ["TP", "FP", "TN", "FN"]
+    an = IntegrateGradientsAnalyser(pc2, mc, xc)
+    an.get_overview()
+    an.spatial_aggregate_gradients()
+    assert an.plot_spatial_aggregated_gradients()
+    assert an.create_videos(sensor=s1, time_from=str(lo), time_to=str(hi))
+    # a gap: one sample of the range removed -> its grid frame is NaN
+    gap = sorted(want)[1]
+    import shutil
+    shutil.rmtree(os.path.join(ex.output_dir, s1, gap))
+    an.get_overview(plots=False)
+    p0 = an.plot_agg_samples_over_time(sensor=s1, time_from=str(lo), time_to=str(hi), agg_type="mean",
+                                       norm_by_prediction=False, cbar_limits=(-0.015, 0.015))
+    agg0 = an.last_agg
+    p1 = an.plot_agg_samples_over_time(sensor=s1, time_from=str(lo), time_to=str(hi), agg_type="mean",
+                                       norm_by_prediction=True, cbar_limits=(-0.015, 0.015))
+    fmt = "%Y%m%d-%H%M%S"
+    rng_s = f"{pd.Timestamp(lo).strftime(fmt)}-{pd.Timestamp(hi).strftime(fmt)}"
+    assert os.path.basename(p0) == f"agg_samples_over_time_{s1}_{rng_s}_mean.png"
+    assert os.path.basename(p1) == f"agg_samples_over_time_{s1}_{rng_s}_mean_norm.png"
+    assert os.path.exists(p0) and os.path.exists(p1)
+    grid = agg0["times"]
+    assert len(grid) == int((hi - lo) / pd.Timedelta(60, unit="s")) + 1
+    gt = pd.to_datetime(parse_gap := gap.rsplit("_", 4)[1] + "_" + gap.rsplit("_", 4)[2], format="%Y%m%d_%H%M%S")
+    k = list(grid).index(gt)
+    assert np.isnan(agg0["prediction"][k]) and np.isnan(agg0["gradients_features"][k]).all()
+    assert np.isfinite(agg0["prediction"]).sum() == len(want) - 1
+    assert parse_gap
