@@ -186,22 +186,60 @@ def plot_classified_samples(model, store, window_ids, model_config, preproc_conf
     return paths
 
 
-def _strip(ax, dates, pred, true, lo, hi, alpha, tn_color="white", empty="grey", label=True):
+def _strip(ax, dates, pred, true, lo, hi, alpha, tn_color="white", empty="grey", label=True, no_data=True):
     for (p, t), col, name in (((1, 1), "green", "True Positive"), ((0, 0), tn_color, "True Negative"),
                               ((0, 1), "red", "False Negative"), ((1, 0), "orange", "False Positive")):
         ax.fill_between(dates, lo, hi, where=(pred == p) & (true == t), alpha=alpha, color=col,
                         label=name if label else None, step="mid")
-    ax.fill_between(dates, lo, hi, where=np.isnan(true), alpha=alpha, color=empty, label="No data" if label else None,
-                    step="mid")
+    if no_data:
+        ax.fill_between(dates, lo, hi, where=np.isnan(true), alpha=alpha, color=empty,
+                        label="No data" if label else None, step="mid")
+
+
+def soilnet_plot_series(raw, interpolation_max: str = "60min"):
+    """What ``plot_results`` draws for SoilNet from the raw dataset (``libs/visualize.py:200-215``):
+    gap-interpolated moisture and battery voltage [sensor, time] and the automatic-flag state:
+    1 where ``moisture_flag_Auto:{BattV,Range,Spike}`` is set, NaN where the step is unlabelled
+    (``moisture_flag_no_label``) and no automatic flag is set, 0 otherwise."""
+    from ..data.interp import interpolate_gaps
+    t = np.asarray(raw.time)
+    moist = interpolate_gaps(np.asarray(raw["moisture"].values, np.float64), t, interpolation_max)
+    battv = interpolate_gaps(np.asarray(raw["battv"].values, np.float64), t, interpolation_max)
+    auto = np.where(np.asarray(raw["moisture_flag_no_label"].values, bool), np.nan, 0.0)
+    hit = np.zeros(auto.shape, bool)
+    for k in ("moisture_flag_Auto:BattV", "moisture_flag_Auto:Range", "moisture_flag_Auto:Spike"):
+        if k in raw:
+            hit |= np.asarray(raw[k].values, bool)
+    auto[hit] = 1.0
+    return {"sensor_ids": np.asarray(raw.sensor_ids).astype(str), "time": t.astype("datetime64[m]"),
+            "moisture": moist, "battv": battv, "automatic_flags": auto}
+
+
+def _soil_strip(ax, dates, pred, true, auto, lo, hi, alpha, label=True):
+    """Outcome bands plus the reference's two SoilNet bands (``libs/visualize.py:351-359``):
+    'Automatic flag' where the automatic-flag state is not 0 - which, as in the reference (its
+    ``where=`` casts the NaN of unlabelled steps to True), includes unlabelled steps - and
+    'No data' where a labelled step has no prediction."""
+    _strip(ax, dates, pred, true, lo, hi, alpha, label=label, no_data=False)
+    ax.fill_between(dates, lo, hi, where=(auto != 0), alpha=alpha, color="blue",
+                    label="Automatic flag" if label else None, step="mid")
+    ax.fill_between(dates, lo, hi, where=np.isnan(true) & (auto == 0), alpha=alpha, color="grey",
+                    label="No data" if label else None, step="mid")
 
 
 def plot_results(sensor_ids, anomaly_dates, anomaly_flags_pred, anomaly_flags_true, predictions, preproc_config,
                  model_config, windows=None, comparison: bool = False, sensor_ids_baseline=None,
                  anomaly_dates_baseline=None, anomaly_flags_pred_baseline=None, anomaly_flags_true_baseline=None,
                  predictions_baseline=None, labels=("GCN", "baseline"), interval: Optional[float] = None,
-                 plot_example: bool = False, max_figures: int = 5) -> List[str]:
+                 plot_example: bool = False, max_figures: int = 5, raw=None) -> List[str]:
     """Per-sensor panels: flagged-sensor series on top, outcome strip(s) below, one
-    figure per ``interval`` hours (``plotting.plot_time_range``)."""
+    figure per ``interval`` hours (``plotting.plot_time_range``; at most ``max_figures``,
+    the reference stops after 5, ``libs/visualize.py:219,235``).
+
+    SoilNet with the ``raw`` dataset (``libs/visualize.py:200-215,285-291,316-322,351-389``):
+    the raw time axis of the range, moisture on the left axis (limits floor(min) .. ceil(min(60,
+    max))), battery voltage [V] on a twin axis, the outcomes placed at their window centres, and
+    the 'Automatic flag' / 'No data' bands of :func:`_soil_strip`."""
     pl = (model_config.get("plotting") or {}) if model_config is not None else {}
     alpha = float(pl.get("alpha", 0.2))
     interval = float(interval if interval is not None else pl.get("plot_time_range", 144))
@@ -210,6 +248,7 @@ def plot_results(sensor_ids, anomaly_dates, anomaly_flags_pred, anomaly_flags_tr
     sensor_ids = np.asarray(sensor_ids)
     anomaly_dates = np.asarray(anomaly_dates).astype("datetime64[m]")
     groups = {str(g.group_id): g for g in windows.groups} if windows is not None else {}
+    soil = soilnet_plot_series(raw) if (raw is not None and preproc_config.ds_type == "soilnet") else None
     paths: List[str] = []
     for sid in np.unique(sensor_ids):
         sel = np.nonzero(sensor_ids == sid)[0]
@@ -225,6 +264,15 @@ def plot_results(sensor_ids, anomaly_dates, anomaly_flags_pred, anomaly_flags_tr
                 continue
             order = inwin[np.argsort(anomaly_dates[inwin])]
             dts = anomaly_dates[order].astype(object)
+            if soil is not None and str(sid) in set(soil["sensor_ids"]):
+                paths.append(_plot_soil_range(soil, str(sid), t0, t1, order, anomaly_dates, anomaly_flags_pred,
+                                              anomaly_flags_true, alpha, out_dir, labels, comparison,
+                                              sensor_ids_baseline, anomaly_dates_baseline,
+                                              anomaly_flags_pred_baseline, anomaly_flags_true_baseline))
+                t0 = t1
+                if plot_example:
+                    break
+                continue
             nrows = 2
             fig, ax = plt.subplots(nrows, 1, sharex="all", height_ratios=[2, 1], figsize=(18, 4.5))
             g = groups.get(str(sid))
@@ -261,6 +309,56 @@ def plot_results(sensor_ids, anomaly_dates, anomaly_flags_pred, anomaly_flags_tr
             if plot_example:
                 break
     return paths
+
+
+def _place(plot_dates, dates, values):
+    """values at ``dates`` spread onto ``plot_dates`` (NaN elsewhere), as the reference's intersect1d."""
+    out = np.full(len(plot_dates), np.nan)
+    _, pi, ai = np.intersect1d(plot_dates, dates, return_indices=True)
+    out[pi] = np.asarray(values, np.float64)[ai]
+    return out
+
+
+def _plot_soil_range(soil, sid, t0, t1, order, anomaly_dates, pred, true, alpha, out_dir, labels, comparison,
+                     sids_b, dates_b, pred_b, true_b):
+    k = int(np.nonzero(soil["sensor_ids"] == sid)[0][0])
+    tt = soil["time"]
+    m = (tt >= t0) & (tt <= t1)
+    plot_dates = tt[m]
+    moist, batt, auto = soil["moisture"][k, m], soil["battv"][k, m] / 1000.0, soil["automatic_flags"][k, m]
+    p_ts = _place(plot_dates, anomaly_dates[order], np.asarray(pred)[order])
+    t_ts = _place(plot_dates, anomaly_dates[order], np.asarray(true)[order])
+    fig, ax = plt.subplots(2, 1, sharex="all", height_ratios=[1.2, 1] if comparison else [2, 1],
+                           figsize=(18, 6 if comparison else 4.5))
+    pd_obj = plot_dates.astype(object)
+    ax[0].plot(pd_obj, moist, linewidth=2, color=LINE_COLORS[0])
+    fin = moist[np.isfinite(moist)]
+    if fin.size:
+        ax[0].set_ylim([int(np.floor(fin.min())), int(np.ceil(min(60.0, fin.max())))])
+    ax[0].set_ylabel("Soil moisture [%]", color=LINE_COLORS[0], fontsize=14)
+    ax2 = ax[0].twinx()
+    ax2.plot(pd_obj, batt, linewidth=2, color=LINE_COLORS[1], zorder=1)
+    ax2.set_ylabel("Battery voltage [V]", color=LINE_COLORS[1], fontsize=14)
+    ax2.locator_params(axis="y", nbins=4)
+    ax[0].xaxis.set_major_formatter(mdates.DateFormatter("%Y-%m-%d %H:%M"))
+    base = 0.5 if comparison else 0.0
+    _soil_strip(ax[1], pd_obj, p_ts, t_ts, auto, base, 1, alpha)
+    if comparison and sids_b is not None:
+        sb = np.nonzero(np.asarray(sids_b) == sid)[0]
+        db = np.asarray(dates_b).astype("datetime64[m]")
+        sb = sb[(db[sb] >= t0) & (db[sb] <= t1)]
+        _soil_strip(ax[1], pd_obj, _place(plot_dates, db[sb], np.asarray(pred_b)[sb]),
+                    _place(plot_dates, db[sb], np.asarray(true_b)[sb]), auto, 0, 0.5, alpha, label=False)
+        ax[1].axhline(0.5, color="black", alpha=alpha)
+        ax[1].text(-0.05, 0.25, labels[1], transform=ax[1].transAxes, fontsize=12)
+    ax[1].text(-0.05, 0.5 + base / 2, labels[0], transform=ax[1].transAxes, fontsize=12)
+    ax[1].set_axis_off()
+    ax[1].legend(loc=10, bbox_to_anchor=(0.5, -0.1), ncols=6)
+    fig.suptitle(sid, y=0.99)
+    p = os.path.join(out_dir, f"{sid}_{t0}_{t1}.png".replace(":", "-"))
+    fig.savefig(p, bbox_inches="tight")
+    plt.close(fig)
+    return p
 
 
 _OUTCOMES = (((1, 1), "green", "True Positive"), ((0, 0), "blue", "True Negative"),

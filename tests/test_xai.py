@@ -318,3 +318,43 @@ def test_reference_run_scripts_golden(cml_small, tmp_path):
     assert np.isnan(agg0["prediction"][k]) and np.isnan(agg0["gradients_features"][k]).all()
     assert np.isfinite(agg0["prediction"]).sum() == len(want) - 1
     assert parse_gap
+
+
+def test_soilnet_result_plots_automatic_flags(tmp_path):
+    """SoilNet plot_results with the raw dataset: the automatic-flag state (Auto flags -> 1,
+    unlabelled -> NaN, else 0), the 'Automatic flag' / 'No data' bands with the reference's NaN
+    semantics, and the battery-voltage twin axis (libs/visualize.py:200-215,285-291,351-359)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    from gnnqc.viz import extract_target_info, plot_results
+    from gnnqc.viz.results import _soil_strip, soilnet_plot_series
+    raw = make_soilnet_raw(n_boxes=3, n_time=20 * 96, seed=4)
+    pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
+    pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
+    ws = create_windows_dataset(pc, raw=raw)
+    sp = soilnet_plot_series(raw)
+    nl = np.asarray(raw["moisture_flag_no_label"].values, bool)
+    au = np.zeros_like(nl)
+    for k in ("moisture_flag_Auto:BattV", "moisture_flag_Auto:Range", "moisture_flag_Auto:Spike"):
+        au |= np.asarray(raw[k].values, bool)
+    a = sp["automatic_flags"]
+    assert au.any() and (a[au] == 1).all()
+    assert np.isnan(a[nl & ~au]).all() and (a[~nl & ~au] == 0).all()
+    # the strip: automatic band covers auto-flagged AND unlabelled steps; 'No data' only labelled ones
+    fig, ax = plt.subplots()
+    d = np.arange("2014-08-01T00:00", "2014-08-01T02:00", 15, dtype="datetime64[m]").astype(object)
+    auto = np.array([1.0, np.nan, 0.0, 0.0, 0.0, 0.0, 1.0, np.nan])
+    true = np.array([np.nan, np.nan, np.nan, 0.0, 1.0, 1.0, 0.0, np.nan])
+    pred = np.array([np.nan, np.nan, np.nan, 0.0, 1.0, 0.0, 1.0, np.nan])
+    _soil_strip(ax, d, pred, true, auto, 0, 1, 0.2)
+    labels = [c.get_label() for c in ax.collections]
+    assert "Automatic flag" in labels and "No data" in labels and "True Positive" in labels
+    plt.close(fig)
+    ids = np.arange(0, ws.n_windows, max(1, ws.n_windows // 30))
+    sids, dates, flags = extract_target_info(ws, ids)
+    rng = np.random.default_rng(0)
+    mc = C.Config({"plotting": {"outdir": str(tmp_path / "plots"), "alpha": 0.2, "plot_time_range": 72}})
+    paths = plot_results(sids, dates, (rng.random(len(sids)) > 0.5).astype(int), flags, rng.random(len(sids)), pc, mc,
+                         windows=ws, raw=raw, max_figures=3)
+    assert paths and all(os.path.getsize(q) > 0 for q in paths)
