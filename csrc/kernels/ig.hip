@@ -8,7 +8,7 @@
 //   ig_accum    acc[b, e]  += sum_i w[i] * g[i, b, e]                 (trapezoid weights, fixed
 //                                                                     step order: deterministic)
 //   ig_finalize out[b, e]   = policy(acc[b, e] * (scale ? v[b, e] : 1))  (keep / clip / abs)
-// All three stream float4 granules (E % 4 == 0 on the fast path, scalar tail otherwise).
+// All three stream float4 granules when n % 4 == 0 (every step slice aligned), scalars otherwise.
 #include "common.h"
 
 namespace gq {
@@ -16,7 +16,8 @@ namespace gq {
 __global__ __launch_bounds__(256) void ig_interp_kernel(const float* __restrict__ v, const float* __restrict__ alpha,
                                                         float* __restrict__ out, int kk, long n) {
   const long stride = (long)gridDim.x * blockDim.x;
-  const long n4 = n / 4;
+  // float4 slices only when every step's slice out + s n stays 16-byte aligned (n % 4 == 0)
+  const long n4 = n % 4 == 0 ? n / 4 : 0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float4 x = reinterpret_cast<const float4*>(v)[i];
     for (int s = 0; s < kk; ++s) {
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(256) void ig_interp_kernel(const float* __restrict_
 __global__ __launch_bounds__(256) void ig_accum_kernel(float* __restrict__ acc, const float* __restrict__ g,
                                                        const float* __restrict__ w, int kk, long n) {
   const long stride = (long)gridDim.x * blockDim.x;
-  const long n4 = n / 4;
+  const long n4 = n % 4 == 0 ? n / 4 : 0;          // (as ig_interp: aligned step slices only)
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = reinterpret_cast<float4*>(acc)[i];
     for (int s = 0; s < kk; ++s) {

@@ -98,6 +98,8 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> torch.device
 
 
 def destroy():
+    from .peer import close_all
+    close_all()                    # (peer all-reduce mappings of this process, if any)
     if is_initialized():
         dist.destroy_process_group()
 

@@ -10,7 +10,8 @@ multi-step training graph like the RCCL collective it replaces.
 Opt-in (``GNNQC_PEER_ALLREDUCE=1``) and validated against RCCL / gloo when it is set up
 (:meth:`PeerAllReduce.verify`); one process per GPU of one node, at most 8 ranks. The handles
 are exchanged with the default process group, so it works over gloo as well (tests: two ranks
-sharing one GPU).
+sharing one GPU). Between different GPUs over xGMI it has NOT been run (no multi-GPU box was
+available): treat it as unverified there until a multi-GPU run checks it against RCCL.
 """
 from __future__ import annotations
 
@@ -83,11 +84,33 @@ class PeerAllReduce:
         self._opened = []
 
 
+_CACHE = {}
+
+
 def make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
     """A verified peer all-reduce when ``GNNQC_PEER_ALLREDUCE=1`` (None otherwise or if it fails
-    verification, which falls back to the process group's collective)."""
+    verification, which falls back to the process group's collective). One registered region per
+    (device, size, group size) for the whole process: every Trainer (one per CV fold) reuses it
+    instead of exporting and opening a new set of IPC regions."""
     if not peer_enabled() or torch.device(device).type != "cuda" or not D.is_initialized():
         return None
+    key = (str(torch.device(device)), (int(numel) + 3) // 4 * 4, D.world_size(), D.rank())
+    if key in _CACHE:
+        return _CACHE[key]
+    pa = _make_peer_allreduce(numel, device)
+    if pa is not None:
+        _CACHE[key] = pa
+    return pa
+
+
+def close_all():
+    """Close every cached peer region's peer mappings (process teardown)."""
+    for pa in _CACHE.values():
+        pa.close()
+    _CACHE.clear()
+
+
+def _make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
     pa, err = None, None
     try:                           # (IPC export / open can fail: every rank must learn it)
         pa = PeerAllReduce(numel, device)
@@ -110,4 +133,4 @@ def make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
     return pa
 
 
-__all__ = ["PeerAllReduce", "make_peer_allreduce", "peer_enabled"]
+__all__ = ["PeerAllReduce", "make_peer_allreduce", "peer_enabled", "close_all"]

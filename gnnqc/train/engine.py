@@ -414,6 +414,15 @@ class Trainer:
         else:
             for row in rows:
                 self.train_step(row)
+        if self.peer is not None:
+            # a peer all-reduce timeout on ANY rank is fatal on EVERY rank (its steps were rejected
+            # there only, so the ranks' parameters may differ): agree before any other collective
+            flag = torch.tensor([1.0 if self.peer.timed_out() else 0.0],
+                                device=self.device if D.backend() == "nccl" else "cpu")
+            D.all_reduce_(flag, force=True)
+            if float(flag.item()) != 0.0:
+                raise RuntimeError("peer all-reduce: a rank never arrived (spin timeout); training stopped on "
+                                   "every rank")
         D.average_buffers(self.model)                 # DP: BN moving statistics agree on every rank
         logs = self.train_metrics.result()            # device -> host: synchronises the epoch
         dt = time.perf_counter() - t0
@@ -423,8 +432,6 @@ class Trainer:
             # steps rejected on the device after an LSTM chain spin timeout: fail loudly
             from ..ops.lstm import check_chain
             check_chain(self.device, rejected0)
-        if self.peer is not None and self.peer.timed_out():
-            raise RuntimeError("peer all-reduce: a rank never arrived (spin timeout); those steps were rejected")
         logs["windows_per_sec"] = nsteps * loader.batch_size * self.world / max(dt, 1e-9)
         if self._comm_events:
             logs["allreduce_us"] = 1e3 * sum(a.elapsed_time(b) for a, b in self._comm_events) / len(self._comm_events)

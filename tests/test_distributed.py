@@ -95,11 +95,21 @@ def test_bench_runs_with_two_gloo_ranks():
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 256 and out["value"] > 0
 
 
-def _gcn_setup():
+def _gcn_setup(ds="cml"):
     from gnnqc import config as C
     from gnnqc.data.preprocessing import create_windows_dataset
     from gnnqc.data.store import DeviceStore
-    from gnnqc.data.synthetic import make_cml_raw
+    from gnnqc.data.synthetic import make_cml_raw, make_soilnet_raw
+    if ds == "soilnet":          # network-wide SoilNet: one prediction per node (BASELINE config iii)
+        pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
+        pc.timestep_before, pc.timestep_after = 24 * 60, 6 * 60
+        raw = make_soilnet_raw(n_boxes=3, n_time=8 * 96, seed=6)
+        pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
+        ws = create_windows_dataset(pc, raw=raw)
+        st = DeviceStore(ws, "scale_range", pc.graph)
+        mc = C.default("model_soilnet")
+        mc.sequence_layer.filter_1_size = 4
+        return pc, mc, st
     pc = C.normalize_preproc(C.default("preprocessing_cml"))
     pc.timestep_before, pc.timestep_after = 30, 15
     ws = create_windows_dataset(pc, raw=make_cml_raw(n_sensors=8, n_minutes=4 * 1440, seed=5))
@@ -110,7 +120,7 @@ def _gcn_setup():
     return pc, mc, st
 
 
-def _gcn_worker(rank, world, port, out_dir, ids, n_epoch_batches):
+def _gcn_worker(rank, world, port, out_dir, ids, n_epoch_batches, ds="cml"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
@@ -120,7 +130,7 @@ def _gcn_worker(rank, world, port, out_dir, ids, n_epoch_batches):
     from gnnqc.parallel import dist as D
     from gnnqc.train.engine import Trainer
     D.init_distributed(device="cpu")
-    pc, mc, st = _gcn_setup()
+    pc, mc, st = _gcn_setup(ds)
     torch.manual_seed(rank + 200)             # different init per rank: broadcast must fix it
     m = GCNClassifier(mc, pc)
     opt = make_optimizer("adam", m.parameters(), 1e-3)
@@ -143,8 +153,8 @@ def _gcn_worker(rank, world, port, out_dir, ids, n_epoch_batches):
     D.destroy()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world):
+@pytest.mark.parametrize("world,ds", [(2, "cml"), (4, "cml"), (2, "soilnet")])
+def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world, ds):
     """GCNClassifier under data parallelism (gloo, the RCCL path by construction): the all-reduced
     gradient equals the mean of single-process per-shard gradients (BatchNorm batch statistics are
     per replica, as in Keras MirroredStrategy), and after an epoch parameters and BN moving
@@ -152,7 +162,7 @@ def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world):
     per = 6
     ids = [list(range(r * per, (r + 1) * per)) for r in range(world)]
     port = _free_port()
-    mp.spawn(_gcn_worker, args=(world, port, str(tmp_path), ids, 2), nprocs=world, join=True)
+    mp.spawn(_gcn_worker, args=(world, port, str(tmp_path), ids, 2, ds), nprocs=world, join=True)
     p0 = [np.load(tmp_path / f"p0_{r}.npy") for r in range(world)]
     for r in range(1, world):
         assert np.array_equal(p0[r], p0[0])
@@ -163,7 +173,7 @@ def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world):
     from gnnqc.models import GCNClassifier
     from gnnqc.ops.optim import make_optimizer
     from gnnqc.train.engine import Trainer
-    pc, mc, st = _gcn_setup()
+    pc, mc, st = _gcn_setup(ds)
     m = GCNClassifier(mc, pc)
     opt = make_optimizer("adam", m.parameters(), 1e-3)
     opt.flat_p.copy_(torch.from_numpy(p0[0]))
