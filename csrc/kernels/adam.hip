@@ -177,10 +177,15 @@ __global__ __launch_bounds__(256) void adam_guarded_kernel(
   const int tid = threadIdx.x;
   const long n4 = n / 4, stride = (long)gridDim.x * blockDim.x;
   const long i0 = blockIdx.x * (long)blockDim.x + tid;
-  // every workgroup reads these before it arrives and the last arrival changes them only after
-  // all arrived: no ordering needed. state[4] = 2 * generation + ok of the last decision.
-  const int gen0 = __hip_atomic_load(state + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const float step0 = __hip_atomic_load(step_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ int gen_s;
+  __shared__ float step_s;
+  // state[4] = 2 * generation + ok of the last decision. Thread 0 reads it and the step counter
+  // with ACQUIRE loads before its arrival ticket: they complete before the ticket is issued, so
+  // the last arrival (which changes both only after every ticket) cannot overtake them.
+  if (tid == 0) {
+    gen_s = __hip_atomic_load(state + 4, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    step_s = __hip_atomic_load(step_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   float4 gg[K], pq[K], mq[K], vq[K];
   float gt = 0.f;
   int bad = 0;
@@ -205,6 +210,8 @@ __global__ __launch_bounds__(256) void adam_guarded_kernel(
   if ((tid & 63) == 0) wsum[tid >> 6] = bad;
   __syncthreads();
   if (tid == 0) {
+    const int gen0 = gen_s;
+    const float step0 = step_s;
     const int tot = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
     // ONE atomic carries both the arrival (low 16 bits) and "this workgroup saw a non-finite
     // value" (high bits): the last arrival learns everything from the value it gets back
@@ -228,13 +235,22 @@ __global__ __launch_bounds__(256) void adam_guarded_kernel(
       int spins = 0, gv;
       while ((gv = __hip_atomic_load(state + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == gen0) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 22)) break;          // never expected (co-resident grid): skip below
+        if (++spins > (1 << 22)) break;          // never expected (co-resident grid)
       }
-      ok = gv != gen0 ? (gv & 1) : 0;
+      if (gv != gen0) {
+        ok = gv & 1;
+      } else {
+        // the decision never arrived (the grid was not co-resident): this workgroup's slice is
+        // left unchanged while others may update theirs - a partial step. Count it in state[6];
+        // the trainer raises on it at epoch end (FlatOptimizer.check_update).
+        ok = 0;
+        __hip_atomic_fetch_add(state + 6, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     okf = ok;
   }
   __syncthreads();
+  const float step0 = step_s;
   if (!okf) {                                    // rejected step: parameters untouched, g cleared
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -298,8 +314,8 @@ bool adam_guarded(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, const 
                   const c10::optional<at::Tensor>& ext, const c10::optional<at::Tensor>& cursor, int64_t cursor_mod) {
   const at::Tensor* ops[] = {&p, &g, &m, &v, &lr, &step};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "adam operand");
-  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kInt && state.numel() >= 5 && state.is_contiguous(),
-              "adam_guarded: state must be int32[>=5] on the device");
+  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kInt && state.numel() >= 7 && state.is_contiguous(),
+              "adam_guarded: state must be int32[>=7] on the device");
   const long n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) % 16) == 0 &&

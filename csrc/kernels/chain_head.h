@@ -182,8 +182,10 @@ struct ChainHeadFwdLds {
 };
 
 // Forward of the 16 rows of `tile` from hl [16][F + 4] (LDS).
+// (hd by value: a reference into a kernel's by-value argument struct makes the compiler copy the
+// whole struct to scratch)
 template <int F>
-__device__ void chain_head_fwd(const ChainHead& hd, int tile, int ntiles, const float* hl, char* scratch) {
+__device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int ntiles, const float* hl, char* scratch) {
   float* part = reinterpret_cast<float*>(scratch);    // [2][16][CH_AP]
   float* sa1 = part + 2 * 16 * CH_AP;                 // [16][CH_AP]
   float* rowv = sa1 + 16 * CH_AP;                     // [16][8]

@@ -29,6 +29,7 @@
 // CML layer), while the consumer, running at a third of the producer's step rate, has slack.
 // Each stage also writes everything the per-layer kernels write (h, gate / cell state for
 // the backward, pooled output + argmax bytes), so the backward is unchanged.
+#include "chain_head.h"
 #include "common.h"
 #include "lstm_grads_body.h"
 #include "lstm_tm_common.h"
@@ -69,10 +70,23 @@ struct ChainStage {
   int H, T, Din, Dw, KX, P, PIN;
 };
 
+struct ChainT4 {
+  const unsigned long long* xin;     // the last chain stage's granule stream [>= 3 T][Mp][Din]
+  const float* W;                    // [Dw][512]
+  const float* U;                    // [128][512]
+  const float* b;                    // [512]
+  float* h;                          // [T][Mp][128]
+  float* g;                          // train: [T][tiles][8][4][64][4] fp32 gates (time4_head.hip t4_sidx)
+  float* c;                          // train: [T][tiles][8][4][64][2] (c_t, c_{t-1})
+  float* pin_out;                    // pooled input [T][Mp][Din]: the chain stage's pooled output
+  unsigned char* pin_idx;            //   and its argmax bytes
+  int T, Din, Dw, on;
+  ChainHead hd;
+};
+
 struct ChainArgs {
   ChainStage st[CHAIN_MAX];
   int ns, ntiles, nt8, Mp;
-  int roles;                         // H <= 32 stages: role-split bodies (chain_stage_roles)
   int* ctl;                          // [0] epoch, [1] finished workgroups, [2] spin timeout seen
   long long* trace;                  // [blocks][2] start / end s_memrealtime (100 MHz) of the last launch
   // extra workgroups past the stages (the chain leaves most CUs idle): build the time4 kernel's
@@ -81,6 +95,7 @@ struct ChainArgs {
   const float* pkW;
   bf16x8_t* pk;
   int pkDw;
+  ChainT4 t4;                        // t4.on: time4 + head as one more stage (blocks [ns nt8, (ns + 1) nt8))
 };
 
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
@@ -133,9 +148,7 @@ struct ChainLds {
   static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
   static constexpr int BYTES = HS + XS + HF;
 };
-static constexpr int CHAIN_LDS_A = ChainLds<64, 2>::BYTES;
-static constexpr int CHAIN_LDS_B = 2 * 16 * 40 * 2 + 2 * 16 * 72 * 2 + 2 * 16 * 36 * 4 + 2 * 8 * 64 * 12;  // ChainRLds<32, 2>
-static constexpr int CHAIN_LDS = CHAIN_LDS_A > CHAIN_LDS_B ? CHAIN_LDS_A : CHAIN_LDS_B;
+static constexpr int CHAIN_LDS_STAGE = ChainLds<64, 2>::BYTES;
 
 template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN>
 __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
@@ -145,7 +158,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   constexpr int KPX = 32 * KX;
   constexpr int GR = SRC ? 1 : 4;
   using L = ChainLds<H, KX>;
-  static_assert(L::BYTES <= CHAIN_LDS && L::HS % 16 == 0 && L::XS % 16 == 0, "chain LDS layout");
+  static_assert(L::BYTES <= CHAIN_LDS_STAGE && L::HS % 16 == 0 && L::XS % 16 == 0, "chain LDS layout");
   auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
   auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
   auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
@@ -326,99 +339,69 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   }
 }
 
-// ---- role-split stage (H <= 32). chain_stage keeps every wave on the serial path: the same waves
-// that run the recurrence also wait for the input ring's loads, issue the h / gate / cell-state
-// stores and publish the granules, so every step pays their issue slots and waits (the v3 recurrence
-// microbenchmark: 249 ns per H = 16 step without stores, 435 with them, r1_lstm_microbench.md).
-// Here the workgroup's waves take fixed roles, one LDS barrier per step for all of them:
-//   compute (NW = H / 4 waves, one cell per lane): MFMA on the x / h tiles in LDS, cell update,
-//            h_t (bf16 for the next MFMA, fp32) and the packed gates / c_t into LDS; never touches
-//            global memory inside the loop;
-//   loader  (NL waves): the input ring (fp32 x or the producer's tagged granules, D steps ahead,
-//            tag checks and bounded re-polls, consumer-side MaxPooling1D + argmax bytes), stages
-//            x_{t+1} into LDS during step t;
-//   storer  (NS waves): during step t copies step t-1's h / gates / c from LDS to HBM, publishes
-//            h_{t-1} as granules (or pools it: last stage); only stores, so it never waits on vmcnt.
-// Compute waves run at s_setprio 3, loaders 2, storers 0 (they share SIMDs with compute waves).
-// Global layouts are those of chain_stage (the backward is unchanged).
-template <int H, int KX>
-struct ChainRLds {
-  static constexpr int NW = H / 4;
-  static constexpr int HS = 2 * 16 * (TMC<H>::KPH + 8) * 2;
-  static constexpr int XS = 2 * 16 * (32 * KX + 8) * 2;
-  static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
-  static constexpr int GS = 2 * NW * 64 * 8;
-  static constexpr int CS = 2 * NW * 64 * 4;
-  static constexpr int BYTES = HS + XS + HF + GS + CS;
+// ---- time4 (H = 128, the CML TimeLayer's last layer, last state only) + head + weighted BCE as one
+// more consumer stage of the forward chain (lstm_chain_head_fwd). As its own launch
+// (time4_head.hip) it could only start once the whole chain had drained, and its six steps plus
+// the head (~22 us) ran serially behind it. Here one workgroup per tile consumes the last chain
+// stage's UNPOOLED granules, max-pools them (MaxPooling1D(3); the pooled input and the argmax
+// bytes are written for the backward) and runs each step as soon as its three input steps are
+// published; the head and the loss follow the last step. 1024 threads with two cells per lane
+// (the chain kernel's launch bounds give a lane 128 VGPRs; the standalone kernel's four cells per
+// lane need 256). time4_head.hip's saved-state layouts (h; fp32 gates and (c_t, c_{t-1}) in its
+// t4_sidx order) are kept, so its backward is unchanged.
+struct ChainT4Lds {
+  static constexpr int HS = 2 * 16 * (128 + 8) * 2;       // bf16 h_{t-1} (double buffer)
+  static constexpr int XS = 2 * 16 * (64 + 8) * 2;        // bf16 x_t (double buffer)
+  static constexpr int HL = 16 * (128 + 4) * 4;           // fp32 h_{T-1} for the head
+  static constexpr int BYTES = HS + XS + HL + ChainHeadFwdLds<128>::BYTES;
 };
 
-// loader waves of a role-split stage: its input ring (D steps of the tile's granules) in <= ~48 VGPRs
-constexpr int chain_loaders(int H, bool SRC, int PIN, int DX) {
-  return SRC ? (PIN == 3 ? (H == 16 ? 2 : 4) : (DX > 16 ? 2 : 1)) : (DX > 32 ? 2 : 1);
-}
-
-template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN, int NL, int NS, int DX>
-__device__ __forceinline__ void chain_stage_roles(const ChainStage S, int tile, int ntiles, int Mp, unsigned tagb,
-                                                  int* ctl, char* smem, long long* rt) {
-  // rt (profiling, else nullptr): per role [loop cycles, cycles waiting at the step barriers]
-  // (s_memtime) of its first wave -> rt[2 * role ..]
-  long long wt = 0, lt0 = 0;
-  auto rbar = [&]() {
-    if (rt != nullptr) {
-      const long long a = __builtin_amdgcn_s_memtime();
-      lds_barrier();
-      wt += __builtin_amdgcn_s_memtime() - a;
-    } else {
-      lds_barrier();
-    }
-  };
-  auto rmark = [&](int role) {
-    if (rt != nullptr && (threadIdx.x & 63) == 0) {
-      rt[2 * role] = __builtin_amdgcn_s_memtime() - lt0;
-      rt[2 * role + 1] = wt;
-    }
-  };
-  using C = TMC<H>;
-  static_assert(C::CPL == 1 && H <= 32, "role-split stage: one cell per lane");
-  constexpr int NW = C::NW, G4 = C::G4;
-  constexpr int KPX = 32 * KX;
-  using L = ChainRLds<H, KX>;
-  static_assert(L::BYTES <= CHAIN_LDS && L::HS % 16 == 0 && L::XS % 16 == 0 && L::HF % 16 == 0 &&
-                L::GS % 16 == 0, "chain role LDS layout");
-  static_assert(NW + NL + NS <= 16, "roles fit one 1024-thread workgroup");
-  auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
-  auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
-  auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
-  auto gsl = reinterpret_cast<uint2 (*)[NW * 64]>(smem + L::HS + L::XS + L::HF);
-  auto csl = reinterpret_cast<float (*)[NW * 64]>(smem + L::HS + L::XS + L::HF + L::GS);
-
-  const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
+template <bool TRAIN>
+__device__ __forceinline__ void chain_t4_stage(const ChainT4 Q, int tile, int ntiles, int Mp, unsigned tagb, int* ctl,
+                                               char* smem) {
+  constexpr int H = 128, G4 = 4 * H, NW = 16, CPL = 2, KX = 2, KSH = H / 32, HPB = H + 8, XP = 64 + 8;
+  static_assert(ChainT4Lds::HS % 16 == 0 && ChainT4Lds::XS % 16 == 0 && ChainT4Lds::HL % 16 == 0, "t4 LDS layout");
+  auto hs = reinterpret_cast<__bf16 (*)[16][HPB]>(smem);
+  auto xs = reinterpret_cast<__bf16 (*)[16][XP]>(smem + ChainT4Lds::HS);
+  float* hl = reinterpret_cast<float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS);
+  const int T = Q.T, Din = Q.Din, Dw = Q.Dw;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, quad = lane >> 4;
   const int row0 = tile * 16;
-  const int To = P > 0 ? T / P : T;
-  const size_t hstep = (size_t)Mp * H;
 
-  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += 1024) (&hs[0][0][0])[i] = (__bf16)0.f;
-  for (int i = tid; i < 2 * 16 * (KPX + 8); i += 1024) (&xs[0][0][0])[i] = (__bf16)0.f;
-  __syncthreads();
-
-  if (w < NW) {
-    // ------------------------------------------------------------------ compute
-    __builtin_amdgcn_s_setprio(3);
-    const int col = lane & 15, quad = lane >> 4;
-    bf16x8_t ufr[C::KSH], wfr[KX];
-    const int au = 4 * w + (col >> 2), ag = col & 3;
-    const int u = 4 * w + quad;
+  for (int i = tid; i < 2 * 16 * HPB; i += 1024) (&hs[0][0][0])[i] = (__bf16)0.0f;
+  for (int i = tid; i < 2 * 16 * XP; i += 1024) (&xs[0][0][0])[i] = (__bf16)0.0f;
+  // input element of this thread: (sequence er, channel ek) of the [16][Din] tile; threads past
+  // the tile re-load the last element (every lane of a waiting wave must hold a real granule)
+  const int n_el = 16 * Din;
+  const bool own = tid < n_el;
+  const int el = min(tid, n_el - 1), er = el / Din, ek = el % Din;
+  const size_t xstep = (size_t)Mp * Din, xoff = (size_t)(row0 + er) * Din + ek;
+  unsigned long long xq[3];
+  auto load_x = [&](int tx) {
 #pragma unroll
-    for (int s = 0; s < C::KSH; ++s) {
+    for (int r = 0; r < 3; ++r) xq[r] = ld_granule(Q.xin + xoff + (size_t)(3 * tx + r) * xstep);
+  };
+  // the first input's granules are requested before the weight gathers (their latency overlaps)
+  load_x(0);
+
+  // weights -> permuted A fragments (as chain_stage) straight from global memory: the gathers'
+  // latency is hidden behind the wait for the first input
+  bf16x8_t ufr[CPL][KSH], wfr[CPL][KX];
+  f32x4_t bias4[CPL];
+  int unit[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) {
+    const int gi = w + NW * cc;
+    const int au = 4 * gi + (col >> 2), ag = col & 3;
+    unit[cc] = 4 * gi + quad;
+#pragma unroll
+    for (int s = 0; s < KSH; ++s) {
       bf16x8_t v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 32 * s + 8 * quad + j;
-        v[j] = (__bf16)(S.U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
-      }
-      ufr[s] = v;
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)Q.U[(32 * s + 8 * quad + j) * G4 + ag * H + au];
+      ufr[cc][s] = v;
     }
 #pragma unroll
     for (int s = 0; s < KX; ++s) {
@@ -426,260 +409,129 @@ __device__ __forceinline__ void chain_stage_roles(const ChainStage S, int tile, 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 32 * s + 8 * quad + j;
-        v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
+        v[j] = (__bf16)(Q.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
       }
-      wfr[s] = v;
+      wfr[cc][s] = v;
     }
-    const f32x4_t bias4 = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
-    float c = 0.f;
-    __syncthreads();                              // x_0 staged
-    if (rt != nullptr) lt0 = __builtin_amdgcn_s_memtime();
-    for (int t = 0; t < T; ++t) {
-      const int p = t & 1;
-      f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};
+    const int u = unit[cc];
+    bias4[cc] = f32x4_t{Q.b[u], Q.b[H + u], Q.b[2 * H + u], Q.b[3 * H + u]};
+  }
+
+  // x_tx = MaxPool(3) of the producer's h at 3 tx .. 3 tx + 2 (first maximum wins, its byte kept)
+  auto stage_x = [&](int buf, int tx) {
+    bool bad = false;
 #pragma unroll
-      for (int s = 0; s < C::KSH; ++s) {
-        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
-        acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[s], bh, acch, 0, 0, 0);
-      }
+    for (int r = 0; r < 3; ++r) bad |= (unsigned)(xq[r] >> 32) != (tagb | (unsigned)(3 * tx + r));
+    if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        xq[r] = chain_wait(Q.xin + xoff + (size_t)(3 * tx + r) * xstep, tagb | (unsigned)(3 * tx + r), ctl);
+    }
+    float m = __uint_as_float((unsigned)xq[0]);
+    unsigned arg = 0;
+#pragma unroll
+    for (int r = 1; r < 3; ++r) {
+      const float v = __uint_as_float((unsigned)xq[r]);
+      if (v > m) { m = v; arg = r; }
+    }
+    if (own) {
+      Q.pin_out[xoff + (size_t)tx * xstep] = m;
+      Q.pin_idx[xoff + (size_t)tx * xstep] = (unsigned char)arg;
+      xs[buf][er][ek] = (__bf16)m;
+    }
+  };
+
+  __syncthreads();                                // LDS zeroed
+  stage_x(0, 0);
+  if (T > 1) load_x(1);
+  float c[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) c[cc] = 0.f;
+  __syncthreads();
+
+  for (int t = 0; t < T; ++t) {
+    const int p = t & 1;
+    f32x4_t acc[CPL];
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) {
+      f32x4_t accx = bias4[cc], acch = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KX; ++s) {
         const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
-        accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[s], bx, accx, 0, 0, 0);
+        accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, accx, 0, 0, 0);
       }
-      const f32x4_t acc = accx + acch;
-      const float iv = sigmoidf_fast(acc[0]);
-      const float fv = sigmoidf_fast(acc[1]);
-      const float gv = tanhf_fast(acc[2]);
-      const float ov = sigmoidf_fast(acc[3]);
-      c = fv * c + iv * gv;
-      const float hv = ov * tanhf_fast(c);
+#pragma unroll
+      for (int s = 0; s < KSH; ++s) {
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
+        acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acch, 0, 0, 0);
+      }
+      acc[cc] = accx + acch;
+    }
+    if (wave_uniform(t + 1 < T)) {
+      stage_x(p ^ 1, t + 1);
+      if (wave_uniform(t + 2 < T)) load_x(t + 2);
+    }
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) {
+      const float iv = sigmoidf_fast(acc[cc][0]);
+      const float fv = sigmoidf_fast(acc[cc][1]);
+      const float gv = tanhf_fast(acc[cc][2]);
+      const float ov = sigmoidf_fast(acc[cc][3]);
+      const float cold = c[cc];
+      c[cc] = fv * cold + iv * gv;
+      const float hv = ov * tanhf_fast(c[cc]);
+      const int u = unit[cc];
       hs[p ^ 1][col][u] = (__bf16)hv;
-      hf[p][col][u] = hv;
+      Q.h[((size_t)t * Mp + row0 + col) * H + u] = hv;
+      if (t == T - 1) hl[col * (H + 4) + u] = hv;
       if constexpr (TRAIN) {
-        gsl[p][w * 64 + lane] = gates_pack(iv, fv, gv, ov);
-        csl[p][w * 64 + lane] = c;
+        const int gi = w + NW * cc;                 // time4_head.hip's (wave, cell) of this cell
+        const size_t o = ((((size_t)t * ntiles + tile) * 8 + (gi & 7)) * 4 + (gi >> 3)) * 64 + lane;
+        *reinterpret_cast<float4*>(Q.g + o * 4) = make_float4(iv, fv, gv, ov);
+        *reinterpret_cast<float2*>(Q.c + o * 2) = make_float2(c[cc], cold);
       }
-      rbar();
     }
-    if (w == 0) rmark(0);
-    __builtin_amdgcn_s_setprio(0);
-    return;
+    lds_barrier();
   }
-
-  if (w < NW + NL) {
-    // ------------------------------------------------------------------ loader
-    __builtin_amdgcn_s_setprio(2);
-    const int li = (w - NW) * 64 + lane;          // loader lane 0 .. NL*64-1
-    constexpr int GR = SRC ? 1 : 4;               // floats per granule
-    static_assert(DX <= KPX, "input width bound");
-    constexpr int NGMAX = 16 * DX / GR;           // granules of a [16][Din] tile, Din <= DX
-    constexpr int GPL = (NGMAX + NL * 64 - 1) / (NL * 64);
-    const int ng = 16 * Din / GR;
-    const size_t xstep = (size_t)Mp * Din;
-    int goff[GPL], grow[GPL], gk[GPL];
-    bool gon[GPL];
-#pragma unroll
-    for (int q = 0; q < GPL; ++q) {
-      const int gi = min(li + q * NL * 64, ng - 1);
-      gon[q] = li + q * NL * 64 < ng;
-      goff[q] = row0 * Din + gi * GR;
-      grow[q] = gi * GR / Din;
-      gk[q] = gi * GR % Din;
-    }
-    float4 xr[D][SRC ? 1 : GPL];
-    unsigned long long xq[D][SRC ? GPL : 1][PIN];
-    auto load_x = [&](int j, int tx) {
-#pragma unroll
-      for (int q = 0; q < GPL; ++q) {
-        if (q * NL * 64 >= ng) break;             // (uniform: lanes past the tile)
-        if constexpr (SRC) {
-#pragma unroll
-          for (int r = 0; r < PIN; ++r)
-            xq[j][q][r] = ld_granule(S.xin + goff[q] + (size_t)(PIN * tx + r) * xstep);
-        } else {
-          xr[j][q] = *reinterpret_cast<const float4*>(S.x + goff[q] + (size_t)tx * xstep);
-        }
-      }
-    };
-    auto stage_x = [&](int buf, int j, int tx) {
-      if constexpr (SRC) {
-        bool bad = false;
-#pragma unroll
-        for (int q = 0; q < GPL; ++q)
-#pragma unroll
-          for (int r = 0; r < PIN; ++r) bad |= (unsigned)(xq[j][q][r] >> 32) != (tagb | (unsigned)(PIN * tx + r));
-        if (__builtin_amdgcn_ballot_w64(bad) != 0) {
-#pragma unroll
-          for (int q = 0; q < GPL; ++q)
-#pragma unroll
-            for (int r = 0; r < PIN; ++r)
-              xq[j][q][r] = chain_wait(S.xin + goff[q] + (size_t)(PIN * tx + r) * xstep,
-                                       tagb | (unsigned)(PIN * tx + r), ctl);
-        }
-#pragma unroll
-        for (int q = 0; q < GPL; ++q) {
-          float m = __uint_as_float((unsigned)xq[j][q][0]);
-          if constexpr (PIN > 1) {
-            unsigned arg = 0;
-#pragma unroll
-            for (int r = 1; r < PIN; ++r) {
-              const float v = __uint_as_float((unsigned)xq[j][q][r]);
-              if (v > m) { m = v; arg = r; }
-            }
-            if (gon[q]) {
-              S.pin_out[goff[q] + (size_t)tx * xstep] = m;
-              S.pin_idx[goff[q] + (size_t)tx * xstep] = (unsigned char)arg;
-            }
-          }
-          if (gon[q]) xs[buf][grow[q]][gk[q]] = (__bf16)m;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < GPL; ++q) {
-          if (gon[q]) {
-            const float4 v = xr[j][q];
-            xs[buf][grow[q]][gk[q]] = (__bf16)v.x;
-            xs[buf][grow[q]][gk[q] + 1] = (__bf16)v.y;
-            xs[buf][grow[q]][gk[q] + 2] = (__bf16)v.z;
-            xs[buf][grow[q]][gk[q] + 3] = (__bf16)v.w;
-          }
-        }
-      }
-    };
-    if constexpr (SRC) {
-      // start once the producer is D + LEAD (input) steps ahead (see chain_stage)
-      constexpr int LEAD = PIN > 1 ? CHAIN_LEAD3 : CHAIN_LEAD1;
-      const int tw = min(D + LEAD, T - 1);
-      (void)chain_wait(S.xin + goff[0] + (size_t)(PIN * tw + PIN - 1) * xstep, tagb | (unsigned)(PIN * tw + PIN - 1),
-                       ctl);
-    }
-#pragma unroll
-    for (int j = 0; j < D; ++j) load_x(j, min(j, T - 1));
-    stage_x(0, 0, 0);
-    load_x(0, min(D, T - 1));
-    __syncthreads();                              // x_0 staged
-    if (rt != nullptr) lt0 = __builtin_amdgcn_s_memtime();
-    for (int t0 = 0; t0 < T; t0 += D) {
-#pragma unroll
-      for (int j = 0; j < D; ++j) {
-        const int t = t0 + j;
-        if (t >= T) break;                        // (uniform)
-        const int jn = (j + 1 == D) ? 0 : j + 1;
-        if (t + 1 < T) {
-          stage_x((t + 1) & 1, jn, t + 1);
-          load_x(jn, min(t + 1 + D, T - 1));
-        }
-        rbar();
-      }
-    }
-    if (w == NW) rmark(1);
-    __builtin_amdgcn_s_setprio(0);
-    return;
-  }
-
-  if (w < NW + NL + NS) {
-    // ------------------------------------------------------------------ storer
-    const int si = (w - NW - NL) * 64 + lane;     // storer lane 0 .. NS*64-1
-    constexpr int NH4 = 16 * H / 4;               // float4 granules of the h tile
-    constexpr int HPL = (NH4 + NS * 64 - 1) / (NS * 64);
-    constexpr int EPL = (16 * H + NS * 64 - 1) / (NS * 64);        // published elements per lane
-    constexpr int NB4 = NW * 64 * 8 / 16;         // float4 of the packed gates block
-    constexpr int BPL = (NB4 + NS * 64 - 1) / (NS * 64);
-    constexpr int NC4 = NW * 64 / 4;              // float4 of the c block
-    constexpr int CPLS = (NC4 + NS * 64 - 1) / (NS * 64);
-    const bool publish = S.sout != nullptr;
-    PoolAcc pool[HPL];
-    auto store_step = [&](int q, int t) {         // step t's data from LDS buffer q
-#pragma unroll
-      for (int k = 0; k < HPL; ++k) {
-        const int i = si + k * NS * 64;
-        if (i < NH4) {
-          const int r = (4 * i) / H, cc = (4 * i) % H;
-          const float4 v = *reinterpret_cast<const float4*>(&hf[q][r][cc]);
-          *reinterpret_cast<float4*>(S.h + ((size_t)t * Mp + row0) * H + 4 * i) = v;
-          if (P > 0) pool[k].step(v, t, P, To, S.pout, S.iout, (size_t)row0 * H + 4 * i, hstep);
-        }
-      }
-      if (publish) {
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) {
-          const int e = si + k * NS * 64;
-          if (e < 16 * H)
-            st_granule(S.sout + ((size_t)t * Mp + row0) * H + e, hf[q][e / H][e % H], tagb | (unsigned)t);
-        }
-      }
-      if constexpr (TRAIN) {
-        const size_t blk = ((size_t)t * ntiles + tile) * NW * 64;
-#pragma unroll
-        for (int k = 0; k < BPL; ++k) {
-          const int i = si + k * NS * 64;
-          if (i < NB4)
-            *reinterpret_cast<float4*>(reinterpret_cast<char*>(S.g + blk * 4) + 16 * i) =
-                *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(&gsl[q][0]) + 16 * i);
-        }
-#pragma unroll
-        for (int k = 0; k < CPLS; ++k) {
-          const int i = si + k * NS * 64;
-          if (i < NC4)
-            *reinterpret_cast<float4*>(S.c + blk + 4 * i) = *reinterpret_cast<const float4*>(&csl[q][4 * i]);
-        }
-      }
-    };
-    __syncthreads();                              // x_0 staged
-    if (rt != nullptr) lt0 = __builtin_amdgcn_s_memtime();
-    for (int t = 0; t < T; ++t) {
-      if (t >= 1) store_step((t - 1) & 1, t - 1);
-      rbar();
-    }
-    store_step((T - 1) & 1, T - 1);
-    if (w == NW + NL) rmark(2);
-    return;
-  }
-  // spare waves: the same barriers, nothing else
   __syncthreads();
-  for (int t = 0; t < T; ++t) lds_barrier();
 }
 
-__device__ __forceinline__ void chain_finish(int* ctl, int nblk, int* sync = nullptr) {
+__device__ __forceinline__ void chain_finish(int* ctl, int nblk) {
   if (threadIdx.x == 0) {
     const int old = __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == nblk - 1) {            // last workgroup: next launch gets a new epoch
-      if (sync != nullptr)            // (every waiter of this launch is past its wait)
-        for (int i = 0; i < 16; ++i) __hip_atomic_store(sync + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-// Lane 0 polls an arrival counter (sc1 loads, short naps) until it reaches `want`, then the
-// workgroup barrier releases the other waves. Bounded like chain_wait: a timeout (or one seen
-// elsewhere in the launch) sets / honours ctl[2] and the step is rejected by the guard.
-template <bool LONG = false>
-__device__ __forceinline__ void chain_wait_count(const int* p, int want, int* ctl) {
-  if (threadIdx.x == 0) {
-    const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int lim = lim0 > 0 ? lim0 : CHAIN_SPIN;
-    for (int it = 0;; ++it) {
-      if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-      if (it >= lim || ((it & 63) == 63 && __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      if (LONG) __builtin_amdgcn_s_sleep(40);
-      else if (it < 64) __builtin_amdgcn_s_sleep(2);
-      else __builtin_amdgcn_s_sleep(8);
-    }
-  }
-  __syncthreads();
-}
+static constexpr int CHAIN_LDS = ChainT4Lds::BYTES > CHAIN_LDS_STAGE ? ChainT4Lds::BYTES : CHAIN_LDS_STAGE;
 
 template <bool TRAIN>
 __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const int nblk = gridDim.x;
-  if ((int)blockIdx.x >= A.ns * A.nt8) {          // packing workgroups
-    const int f = ((int)blockIdx.x - A.ns * A.nt8) * 1024 + (int)threadIdx.x;
+  __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS];
+  if ((int)blockIdx.x >= A.ns * A.nt8) {
+    int r = (int)blockIdx.x - A.ns * A.nt8;
+    if (A.t4.on) {
+      if (r < A.nt8) {                            // time4 + head stage of tile r
+        if (r < A.ntiles) {
+          if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
+          const unsigned tagb = chain_tag_base((unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          chain_t4_stage<TRAIN>(A.t4, r, A.ntiles, A.Mp, tagb, A.ctl, smem);
+          if (threadIdx.x >= 64 * CH_NW) return;    // the head runs on 8 waves (the rest exit)
+          chain_head_fwd<128>(A.t4.hd, r, A.ntiles, reinterpret_cast<const float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS),
+                              smem + ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL);
+          __syncthreads();
+          if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+        }
+        chain_finish(A.ctl, nblk);
+        return;
+      }
+      r -= A.nt8;
+    }
+    const int f = r * 1024 + (int)threadIdx.x;    // packing workgroups
     if (A.pk != nullptr && f < T4PK_ALL) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
     chain_finish(A.ctl, nblk);
     return;
@@ -692,7 +544,6 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned tagb = chain_tag_base(E);
-  __shared__ __attribute__((aligned(16))) char smem[CHAIN_LDS];
   // (a local copy: field-wise scalar loads of the kernel arguments; a reference into the by-value
   // argument array made the compiler copy the whole array to scratch)
   const ChainStage S = A.st[s];
@@ -708,23 +559,9 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
 #define GQ_CHAIN_KX(HH)                                                                 \
   if (src) { if (S.PIN == 3) { GQ_CHAIN_SRC(HH, 3, CHAIN_D3) } else { GQ_CHAIN_SRC(HH, 1, CHAIN_D) } } \
   else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false, 1) else GQ_CHAIN_BODY(HH, 2, 6, false, 1) }
-#define GQ_CHAIN_ROLES(HH, KXX, DD, SRCV, PINV, DXV)                                    \
-  chain_stage_roles<HH, TRAIN, KXX, DD, SRCV, PINV, chain_loaders(HH, SRCV, PINV, DXV), (HH == 16 ? 2 : 3), DXV>( \
-      S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem, A.roles > 1 ? A.trace + 6912 + 6 * blockIdx.x : nullptr);
-  if (H == 64 || !A.roles) {
-    if (H == 16) GQ_CHAIN_KX(16)
-    else if (H == 32) GQ_CHAIN_KX(32)
-    else GQ_CHAIN_KX(64)
-  } else if (H == 16) {
-    if (src) { if (S.PIN == 3) { GQ_CHAIN_ROLES(16, 1, CHAIN_D3, true, 3, 16) } else { GQ_CHAIN_ROLES(16, 1, CHAIN_D, true, 1, 16) } }
-    else if (KX == 1) { GQ_CHAIN_ROLES(16, 1, 6, false, 1, 32) } else { GQ_CHAIN_ROLES(16, 2, 6, false, 1, 64) }
-  } else {
-    if (src) {
-      if (S.PIN == 3) { if (S.Din <= 16) { GQ_CHAIN_ROLES(32, 1, CHAIN_D3, true, 3, 16) } else { GQ_CHAIN_ROLES(32, 1, CHAIN_D3, true, 3, 32) } }
-      else { if (S.Din <= 16) { GQ_CHAIN_ROLES(32, 1, CHAIN_D, true, 1, 16) } else { GQ_CHAIN_ROLES(32, 1, CHAIN_D, true, 1, 32) } }
-    } else if (KX == 1) { GQ_CHAIN_ROLES(32, 1, 6, false, 1, 32) } else { GQ_CHAIN_ROLES(32, 2, 6, false, 1, 64) }
-  }
-#undef GQ_CHAIN_ROLES
+  if (H == 16) GQ_CHAIN_KX(16)
+  else if (H == 32) GQ_CHAIN_KX(32)
+  else GQ_CHAIN_KX(64)
 #undef GQ_CHAIN_KX
 #undef GQ_CHAIN_SRC
 #undef GQ_CHAIN_BODY
@@ -754,26 +591,11 @@ struct ChainBStage {
   int H, T, Din, Dw, KX, P, Ts;
 };
 
-// A weight-gradient pass run by the backward chain's spare workgroups (lstm_chain_bwd_grads):
-// it starts when the stage whose dz it reads has finished (or at once: wait < 0), and its split
-// records are reduced into the gradient buffers by the same workgroups.
-struct ChainGJ {
-  GradJob g;
-  RedJob r;          // r.kb: slot lanes of the in-launch reduction (16 .. 256)
-  int key;           // HG * 8 + DT
-  int wait;          // chain stage producing dz (-1: ready at launch)
-  int wait_n;        // that stage's workgroups
-};
-
 struct ChainBArgs {
   ChainBStage st[CHAIN_MAX];
   int ns, ntiles, nt8, Mp;
   int* ctl;
   long long* trace;
-  ChainGJ gj[CHAIN_MAX];
-  int njobs;
-  int* sync;         // [0, 8): stage-done counters, [8, 16): job arrival tickets (reset by the last workgroup)
-  long long* gtrace; // profiling: [job][256 workgroups][3] = pass start, arrival, reduction end (s_memrealtime)
 };
 
 template <int H, int KX>
@@ -1066,104 +888,12 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   if constexpr (!PUBW) store_dx((T - 1) & 1, 0, tagb);     // dx tile of t = 0
 }
 
-// In-launch split reduction of job r by workgroup `part` of `nparts`: slots [s0, s1) of the
-// record, SL slot lanes x (256 / SL) split lanes, every split summed in a fixed order, records
-// read with sc1 loads (they were stored sc1). One writer per gradient element: deterministic.
-__device__ __forceinline__ void chain_grads_reduce(const RedJob& r, int part, int nparts, float* red) {
-  const int SL = r.kb, NL = 256 / SL;
-  const int tid = threadIdx.x, sl = tid % SL, l = tid / SL;
-  const int per = (r.RC + nparts - 1) / nparts;
-  const int s0 = part * per, s1 = min(r.RC, s0 + per);
-  for (int base = s0; base < s1; base += SL) {
-    const int slot = min(base + sl, s1 - 1);
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int sp = l;
-    for (; sp + 3 * NL < r.splits; sp += 4 * NL) {
-      a0 += ld_sc1(r.ws + (size_t)sp * r.RC + slot);
-      a1 += ld_sc1(r.ws + (size_t)(sp + NL) * r.RC + slot);
-      a2 += ld_sc1(r.ws + (size_t)(sp + 2 * NL) * r.RC + slot);
-      a3 += ld_sc1(r.ws + (size_t)(sp + 3 * NL) * r.RC + slot);
-    }
-    for (; sp < r.splits; sp += NL) a0 += ld_sc1(r.ws + (size_t)sp * r.RC + slot);
-    red[tid] = (a0 + a1) + (a2 + a3);
-    __syncthreads();
-    if (tid < SL && base + tid < s1) {
-      float v = 0.f;
-      for (int k = 0; k < NL; ++k) v += red[k * SL + tid];
-      grads_add(v, base + tid, r.ncb, r.DT, r.HT, r.Din, r.H, r.dW, r.db, r.dU);
-    }
-    __syncthreads();
-  }
-}
-
-// One job's gradient-pass share, one instance per (HG, DT) so each gets its own register
-// allocation (one function holding all twenty spilled in every one of them).
-template <int HG, int DT>
-__device__ __noinline__ void chain_grads_job(const ChainBArgs* A, __attribute__((address_space(3))) char* lds, int gb,
-                                             int k) {
-  const GradJob& g = A->gj[k].g;
-  lstm_grads_body<HG, DT, 4, true>(g.dz, g.x, g.h, g.W, nullptr, g.ws, g.rows, g.period, g.hshift, g.Din, g.ldx, 0,
-                                   g.Din, g.xg, g.x_elems, gb % g.ncb, gb / g.ncb, g.ncb, g.splits, (char*)lds);
-}
-
-// The spare workgroups' role (256 of their threads): every job in order - wait for its dz,
-// this workgroup's (column block, split) share of the gradient pass, arrival, then (once all
-// of the job's workgroups arrived) this workgroup's slice of the reduction. A points at the
-// kernel's own argument segment (the kernel passes it: in a called function the kernarg
-// builtin is null), so nothing is copied by value.
-__device__ __noinline__ void chain_grads_role(const ChainBArgs* A, __attribute__((address_space(3))) char* lds, int gb) {
-  int* ctl = A->ctl;
-  // sync[16]: profiling knobs (bit 0: waits and arrivals only; bit 1: long naps in stage waits)
-  const int dbg = __hip_atomic_load(A->sync + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int k = 0; k < A->njobs; ++k) {
-    const ChainGJ* J = &A->gj[k];
-    const int nb = J->g.nblocks;
-    if (gb >= nb) continue;                       // (workgroup-uniform)
-    if (J->wait >= 0) {
-      if (dbg & 2) chain_wait_count<true>(A->sync + J->wait, J->wait_n, ctl);
-      else chain_wait_count(A->sync + J->wait, J->wait_n, ctl);
-      // the stage published dz with plain stores + release: acquire before reading them
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    long long* gt = A->gtrace + ((size_t)k * 256 + min(gb, 255)) * 3;
-    if (threadIdx.x == 0) gt[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (!(dbg & 1)) switch (J->key) {
-#define GQ_CG(HG, DT) case HG * 8 + DT: chain_grads_job<HG, DT>(A, lds, gb, k); break;
-#define GQ_CG_H(HG) GQ_CG(HG, 1) GQ_CG(HG, 2) GQ_CG(HG, 3) GQ_CG(HG, 4) GQ_CG(HG, 5)
-      GQ_CG_H(16) GQ_CG_H(32) GQ_CG_H(64) GQ_CG_H(128)
-#undef GQ_CG_H
-#undef GQ_CG
-      default: break;
-    }
-    // records stored sc1: every wave's stores acknowledged, then one arrival per workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(A->sync + 8 + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      gt[1] = (long long)__builtin_amdgcn_s_memrealtime();
-    }
-    chain_wait_count(A->sync + 8 + k, nb, ctl);
-    if (!(dbg & 1)) chain_grads_reduce(J->r, gb, nb, reinterpret_cast<float*>((char*)lds));
-    if (threadIdx.x == 0) gt[2] = (long long)__builtin_amdgcn_s_memrealtime();
-  }
-}
-
 __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   const int nblk = gridDim.x;
   __shared__ __attribute__((aligned(16))) char smem[CHAINB_LDS];
-  if ((int)blockIdx.x >= A.ns * A.nt8) {          // spare workgroups: weight-gradient passes
-    if (threadIdx.x >= 256) return;
-    chain_grads_role((const ChainBArgs*)__builtin_amdgcn_kernarg_segment_ptr(),
-                     (__attribute__((address_space(3))) char*)smem, (int)blockIdx.x - A.ns * A.nt8);
-    __syncthreads();
-    chain_finish(A.ctl, nblk, A.sync);
-    return;
-  }
   const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
   if (s >= A.ns || tile >= A.ntiles) {
-    chain_finish(A.ctl, nblk, A.sync);
+    chain_finish(A.ctl, nblk);
     return;
   }
   if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1200,28 +930,17 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
 #undef GQ_CHAINB_BODY
 #undef GQ_CHAINB_BODY2
 #undef GQ_CHAINB_BODY3
-  // stage done: every storing wave's dz / dx stores retired, then one lane releases them
-  // (agent fence: written back from this XCD's L2) and counts this tile as finished
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (A.njobs > 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(A.sync + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  chain_finish(A.ctl, nblk, A.sync);
+  if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+  chain_finish(A.ctl, nblk);
 }
 
 // ---------------------------------------------------------------------------------------
 // host
 static long long* chain_trace_buf(int dev) {
   static long long* tr[64] = {nullptr};
-  // [0, 768): per-workgroup start / end and stage-loop start; then the grads role's [8][256][3]
-  // then (profiling) the role-split stages' [256][3 roles][loop, barrier-wait cycles]
-  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], (3 * 256 + 8 * 256 * 3 + 256 * 6) * sizeof(long long)) == hipSuccess,
+  // [0, 512): per-workgroup start / end; [512, 768): stage-loop start (backward)
+  if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], 3 * 256 * sizeof(long long)) == hipSuccess,
                             "lstm_chain: trace");
   return tr[dev];
 }
@@ -1234,8 +953,8 @@ int* chain_ctl(int dev) {
     TORCH_CHECK(hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
                 "lstm_chain: first use must not be inside a graph capture");
     int* p = nullptr;
-    TORCH_CHECK(hipMalloc(&p, 8 * sizeof(int)) == hipSuccess, "lstm_chain: control word allocation");
-    const int init[8] = {1, 0, 0, 0, 0, 0, 0, 0};     // epoch 1; [4], [5]: head tickets
+    TORCH_CHECK(hipMalloc(&p, 16 * sizeof(int)) == hipSuccess, "lstm_chain: control word allocation");
+    const int init[16] = {1, 0};     // epoch 1; [4], [5]: head tickets; [8]: head backward reduce arrivals
     TORCH_CHECK(hipMemcpy(p, init, sizeof(init), hipMemcpyHostToDevice) == hipSuccess, "lstm_chain: init");
     ctl[dev] = p;
   }
@@ -1272,22 +991,39 @@ int64_t lstm_chain_capacity(const at::Tensor& like) {
   return chain_capacity(like.get_device());
 }
 
-// The device's chain control words as an int32[8] view (no copy): [epoch, finished workgroups,
+// The device's chain control words as an int32[16] view (no copy): [epoch, finished workgroups,
 // spin-timeout flag, timeouts consumed by the gradient guard, time4/head kernel tickets (2),
-// debug spin limit (0: default), 0]. The optimiser's grad_guard reads
-// and clears the flag inside the captured step (a timed-out step is skipped, never applied).
+// debug spin limit (0: default), a gradient producer saw a non-finite value, head backward
+// reduce arrivals, 0...]. The optimiser's update reads and clears the flags inside the captured
+// step (a timed-out or non-finite step is skipped, never applied).
 at::Tensor lstm_chain_ctl(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "lstm_chain_ctl: a GPU tensor names the device");
   c10::DeviceGuard guard(like.device());
   int* p = chain_ctl(like.get_device());
-  return at::from_blob(p, {8}, like.options().dtype(at::kInt));
+  return at::from_blob(p, {16}, like.options().dtype(at::kInt));
 }
 
 // x [T, Mp, Din] (Din % 4 == 0, 16-B aligned); per stage W [Dw, 4H], U [H, 4H], b [4H];
 // pool[s] > 0: MaxPooling1D(pool[s]) after stage s. Returns per stage [h, g, c, pooled, idx].
+// time4 + head as a chain stage (lstm_chain_head_fwd): its weights, the head and the loss inputs
+struct T4Host {
+  const at::Tensor* b;
+  at::TensorList head;
+  const at::Tensor* y;
+  const at::Tensor* mask;
+  int64_t M;
+  double alpha1, alpha2, w0, w1;
+  at::Tensor sums, hist;
+};
+
+// time4_head.hip: the forward head arguments (weights, labels, metric accumulators, ticket)
+void t4_head_fwd_args(ChainHead& hd, at::TensorList head, const at::Tensor& y, const at::Tensor& mask, int64_t M,
+                      int Mp, double alpha1, double alpha2, double w0, double w1, const at::Tensor& sums,
+                      const at::Tensor& hist, at::Tensor& logits, at::Tensor& loss, at::Tensor& part);
+
 static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorList W, at::TensorList U,
                                               at::TensorList b, at::IntArrayRef pool, bool train, const at::Tensor* pkW,
-                                              const at::Tensor* pkU);
+                                              const at::Tensor* pkU, const T4Host* t4 = nullptr);
 
 std::vector<at::Tensor> lstm_chain_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U, at::TensorList b,
                                        at::IntArrayRef pool, bool train) {
@@ -1302,9 +1038,23 @@ std::vector<at::Tensor> lstm_chain_fwd_pack(const at::Tensor& x, at::TensorList 
   return chain_fwd_impl(x, W, U, b, pool, train, &Wt4, &Ut4);
 }
 
+// The chain forward with time4 (Wt4 [Din, 512], Ut4 [128, 512], bt4 [512], last state only) and the
+// classifier head + weighted BCE (head = [W1, b1, W2, b2, W3, b3], y / mask [M]) as one more stage
+// consuming the last chain stage's output, which must be max-pooled by 3 (chain_t4_stage). Returns
+// lstm_chain_fwd_pack's result followed by [h4 [T4, Mp, 128], g4, c4, logits [M], loss [1]] (the
+// outputs of time4_head_fwd); with sums / hist non-empty the metric accumulators are updated.
+std::vector<at::Tensor> lstm_chain_head_fwd(const at::Tensor& x, at::TensorList W, at::TensorList U, at::TensorList b,
+                                            at::IntArrayRef pool, bool train, const at::Tensor& Wt4,
+                                            const at::Tensor& Ut4, const at::Tensor& bt4, at::TensorList head,
+                                            const at::Tensor& y, const at::Tensor& mask, int64_t M, double alpha1,
+                                            double alpha2, double w0, double w1, at::Tensor sums, at::Tensor hist) {
+  T4Host h4{&bt4, head, &y, &mask, M, alpha1, alpha2, w0, w1, sums, hist};
+  return chain_fwd_impl(x, W, U, b, pool, train, &Wt4, &Ut4, &h4);
+}
+
 static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorList W, at::TensorList U,
                                               at::TensorList b, at::IntArrayRef pool, bool train, const at::Tensor* pkW,
-                                              const at::Tensor* pkU) {
+                                              const at::Tensor* pkU, const T4Host* t4) {
   check_f32_cuda(x, "x");
   const int ns = (int)W.size();
   TORCH_CHECK(ns >= 1 && ns <= CHAIN_MAX && (int)U.size() == ns && (int)b.size() == ns && (int)pool.size() == ns,
@@ -1326,11 +1076,6 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   A.Mp = Mp;
   A.ctl = chain_ctl(x.get_device());
   A.trace = chain_trace_buf(x.get_device());
-  static const int roles = [] {
-    const char* e = std::getenv("GNNQC_CHAIN_ROLES");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
-  A.roles = roles;
   std::vector<at::Tensor> out;
   at::Tensor prev_stream;
   int T = (int)x.size(0), Din = (int)x.size(2);
@@ -1342,8 +1087,9 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     TORCH_CHECK(Dw <= Din && Din <= 64 && (s == 0 || Din <= H), "lstm_chain: stage ", s, " input width ", Din);
     TORCH_CHECK(T >= 1 && T < 4096, "lstm_chain: sequence length");
     const int P = (int)pool[s];
-    const bool last = s + 1 == ns;
+    const bool last = s + 1 == ns && t4 == nullptr;   // (time4 consumes the last chain stage)
     TORCH_CHECK(last || P == 0 || P == 3, "lstm_chain: pools between stages must be 3 (got ", P, ")");
+    TORCH_CHECK(t4 == nullptr || s + 1 < ns || P == 3, "lstm_chain_head_fwd: the last chain stage must pool by 3");
     ChainStage& S = A.st[s];
     S.x = s == 0 ? x.data_ptr<float>() : nullptr;
     S.xin = s == 0 ? nullptr : reinterpret_cast<const unsigned long long*>(prev_stream.data_ptr<int64_t>());
@@ -1366,9 +1112,12 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     S.pout = last ? pl.out : nullptr;
     S.iout = last ? pl.idx : nullptr;
     S.P = last ? P : 0;
-    if (!last && P > 0) {          // the next stage pools this stage's output
+    if (!last && P > 0 && s + 1 < ns) {          // the next stage pools this stage's output
       A.st[s + 1].pin_out = pooled.data_ptr<float>();
       A.st[s + 1].pin_idx = pidx.data_ptr<uint8_t>();
+    } else if (!last && P > 0) {                 // ... or time4 does
+      A.t4.pin_out = pooled.data_ptr<float>();
+      A.t4.pin_idx = pidx.data_ptr<uint8_t>();
     }
     S.H = H;
     S.T = T;
@@ -1383,6 +1132,34 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     Din = H;
   }
   int nblk = ns * nt8;
+  std::vector<at::Tensor> t4out;
+  if (t4 != nullptr) {
+    TORCH_CHECK(pkW != nullptr && pkU != nullptr, "lstm_chain_head_fwd: time4 weights");
+    check_f32_cuda(*t4->b, "bt4");
+    const int Dw4 = (int)pkW->size(0);
+    TORCH_CHECK(T >= 1 && T <= 16, "lstm_chain_head_fwd: time4 sequence length 1..16 (got ", T, ")");
+    TORCH_CHECK(Din <= 64 && Dw4 >= 1 && Dw4 <= Din && t4->b->numel() == 512, "lstm_chain_head_fwd: time4 input width");
+    ChainT4& Q = A.t4;
+    Q.on = 1;
+    Q.xin = reinterpret_cast<const unsigned long long*>(prev_stream.data_ptr<int64_t>());
+    Q.W = pkW->data_ptr<float>();
+    Q.U = pkU->data_ptr<float>();
+    Q.b = t4->b->data_ptr<float>();
+    at::Tensor h4 = at::empty({T, Mp, 128}, opt);
+    at::Tensor g4 = train ? at::empty({(long)T * Mp * 128 * 4}, opt) : at::empty({0}, opt);
+    at::Tensor c4 = train ? at::empty({(long)T * Mp * 128 * 2}, opt) : at::empty({0}, opt);
+    Q.h = h4.data_ptr<float>();
+    Q.g = train ? g4.data_ptr<float>() : nullptr;
+    Q.c = train ? c4.data_ptr<float>() : nullptr;
+    Q.T = T;
+    Q.Din = Din;
+    Q.Dw = Dw4;
+    at::Tensor logits, loss, part;
+    t4_head_fwd_args(Q.hd, t4->head, *t4->y, *t4->mask, t4->M, Mp, t4->alpha1, t4->alpha2, t4->w0, t4->w1, t4->sums,
+                     t4->hist, logits, loss, part);
+    t4out = {h4, g4, c4, logits, loss, part};
+    nblk += nt8;
+  }
   at::Tensor pk;
   if (pkW != nullptr) {
     check_f32_cuda(*pkW, "Wt4");
@@ -1408,6 +1185,7 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   for (auto& t : out)
     if (t.scalar_type() != at::kLong) res.push_back(t);
   if (pk.defined()) res.push_back(pk);
+  for (int i = 0; i < 5 && i < (int)t4out.size(); ++i) res.push_back(t4out[i]);
   return res;
 }
 
@@ -1427,131 +1205,6 @@ std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, a
   std::vector<at::Tensor> keep;
   auto res = chain_bwd_setup(A, keep, dh, g, c, W, U, pidx, pool, x_width, T_in, 0);
   hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(A.ns * A.nt8), dim3(1024), 0, stream(), A);
-  GQ_LAUNCH_CHECK();
-  return res;
-}
-
-static int* chain_sync(int dev) {
-  static int* p[64] = {nullptr};
-  TORCH_CHECK(dev >= 0 && dev < 64, "lstm_chain: device index");
-  if (!p[dev]) {
-    hipStreamCaptureStatus cs;
-    TORCH_CHECK(hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
-                "lstm_chain: first use must not be inside a graph capture");
-    TORCH_CHECK(hipMalloc(&p[dev], 32 * sizeof(int)) == hipSuccess, "lstm_chain: sync counters");
-    TORCH_CHECK(hipMemset(p[dev], 0, 32 * sizeof(int)) == hipSuccess, "lstm_chain: sync init");
-  }
-  return p[dev];
-}
-
-int lstm_grads_col_blocks(int H);
-
-static bool chain_job_x_ok(const at::Tensor& x, int Dw) {
-  const int ldx = (int)x.stride(-2);
-  return ldx % 4 == 0 && ldx >= Dw && ldx <= 144 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
-         (Dw + 1 + 15) / 16 <= 5 && x.stride(-1) == 1;
-}
-
-// one weight-gradient job of the chain backward: dz [>= T*Mp rows, 4H] (time-major), x [T, Mp, ldx]
-// (first Dw channels), h [T, Mp, H]; split count for G spare workgroups; ws: its split records
-static void chain_fill_job(ChainGJ& J, const at::Tensor& dz, const at::Tensor& x, const at::Tensor& h, const at::Tensor& W,
-                           at::Tensor& dW, at::Tensor& dU, at::Tensor& db, int G, int wait, int wait_n,
-                           std::vector<at::Tensor>& keep) {
-  const int Dw = (int)W.size(0), H = (int)W.size(1) / 4;
-  TORCH_CHECK(H == 16 || H == 32 || H == 64 || H == 128, "lstm_chain_bwd_grads: hidden size");
-  TORCH_CHECK(x.dim() == 3 && h.dim() == 3 && h.size(0) == x.size(0) && h.size(1) == x.size(1) && h.size(2) == H &&
-                  h.stride(2) == 1 && h.stride(1) == H && h.stride(0) == (long)H * h.size(1),
-              "lstm_chain_bwd_grads: x [T, Mp, C] / h [T, Mp, H]");
-  TORCH_CHECK(chain_job_x_ok(x, Dw) && x.stride(0) == x.stride(1) * x.size(1), "lstm_chain_bwd_grads: x layout");
-  TORCH_CHECK(dW.numel() == W.numel() && dU.numel() == (long)H * 4 * H && db.numel() == 4 * H,
-              "lstm_chain_bwd_grads: gradient buffers");
-  for (const at::Tensor* t : {&dW, &dU, &db}) check_f32_cuda(*t, "lstm_chain_bwd_grads gradient");
-  const int DT = (Dw + 1 + 15) / 16, HT = H / 16, ncb = lstm_grads_col_blocks(H);
-  const long rows = x.size(0) * x.size(1);
-  const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
-  const int splits = (int)std::max<long>(1, std::min<long>((ntiles + 1) / 2, std::max(1, G / ncb)));
-  const int RC = (DT + HT) * 1024 * ncb;
-  at::Tensor ws = at::empty({(long)splits * RC}, x.options());
-  keep.push_back(ws);
-  GradJob& gj = J.g;
-  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == at::kBFloat16, "lstm_chain_bwd_grads: dz must be bf16");
-  gj.dz = dz.data_ptr();
-  gj.x = x.data_ptr<float>();
-  gj.h = h.data_ptr<float>();
-  gj.W = W.data_ptr<float>();
-  gj.ws = ws.data_ptr<float>();
-  gj.rows = rows;
-  gj.period = rows;                 // time-major [T, Mp]: h_{t-1} one Mp block back, none at t = 0
-  gj.hshift = x.size(1);
-  gj.ldx = (int)x.stride(1);
-  gj.x_elems = (long)(x.storage().nbytes() / sizeof(float)) - x.storage_offset();
-  gj.Din = Dw;
-  gj.xg = (int)((32L * gj.ldx / 4 + 255) / 256);
-  gj.ncb = ncb;
-  gj.splits = splits;
-  gj.nblocks = ncb * splits;
-  RedJob& r = J.r;
-  r.ws = gj.ws;
-  r.dW = dW.data_ptr<float>();
-  r.dU = dU.data_ptr<float>();
-  r.db = db.data_ptr<float>();
-  r.splits = splits;
-  r.RC = RC;
-  r.ncb = ncb;
-  r.DT = DT;
-  r.HT = HT;
-  r.Din = Dw;
-  r.H = H;
-  r.nblocks = gj.nblocks;
-  const int per = (RC + gj.nblocks - 1) / gj.nblocks;
-  int sl = 16;
-  while (sl < 256 && sl < per) sl *= 2;
-  r.kb = sl;
-  J.key = H * 8 + DT;
-  J.wait = wait;
-  J.wait_n = wait_n;
-}
-
-// lstm_chain_bwd with the weight-gradient passes of its stages (x_s, h_s, sinks dW_s / dU_s / db_s
-// per stage, top first like W) - and optionally of one more layer whose dz is already known
-// (edz, ex, eh, eW, edW, edU, edb: time4 of the CML stack) - run by the launch's spare workgroups,
-// reduced into the sinks inside the same launch. Returns what lstm_chain_bwd returns.
-std::vector<at::Tensor> lstm_chain_bwd_grads(const at::Tensor& dh, at::TensorList g, at::TensorList c,
-                                             at::TensorList W, at::TensorList U, at::TensorList pidx,
-                                             at::IntArrayRef pool, at::IntArrayRef x_width, at::IntArrayRef T_in,
-                                             at::TensorList gx, at::TensorList gh, at::TensorList gdW,
-                                             at::TensorList gdU, at::TensorList gdb, at::TensorList ext) {
-  const int ns = (int)W.size();
-  TORCH_CHECK((int)gx.size() == ns && (int)gh.size() == ns && (int)gdW.size() == ns && (int)gdU.size() == ns &&
-                  (int)gdb.size() == ns && (ext.size() == 0 || ext.size() == 7),
-              "lstm_chain_bwd_grads: job lists");
-  const int cap = chain_capacity(dh.get_device());
-  const int nt8 = (int)((dh.size(1) / 16 + 7) / 8 * 8);
-  const int G = std::min(cap - ns * nt8, 256);
-  TORCH_CHECK(G >= 8, "lstm_chain_bwd_grads: too few spare workgroups (", G, ")");
-  ChainBArgs A{};
-  std::vector<at::Tensor> keep;
-  auto res = chain_bwd_setup(A, keep, dh, g, c, W, U, pidx, pool, x_width, T_in, G);
-  c10::DeviceGuard guard(dh.device());
-  A.sync = chain_sync(dh.get_device());
-  A.gtrace = A.trace + 3 * 256;
-  int nj = 0;
-  if (ext.size() == 7) {
-    check_dz_cuda(ext[0]);
-    TORCH_CHECK(ext[0].size(-1) == ext[3].size(1) && ext[0].numel() / ext[0].size(-1) >= ext[1].size(0) * ext[1].size(1),
-                "lstm_chain_bwd_grads: edz");
-    at::Tensor dWe = ext[4], dUe = ext[5], dbe = ext[6];
-    chain_fill_job(A.gj[nj++], ext[0], ext[1], ext[2], ext[3], dWe, dUe, dbe, G, -1, 0, keep);
-  }
-  for (int s = 0; s < ns; ++s) {
-    TORCH_CHECK(gx[s].size(0) == T_in[s] && gx[s].size(1) == dh.size(1), "lstm_chain_bwd_grads: stage x shape");
-    at::Tensor dWs = gdW[s], dUs = gdU[s], dbs = gdb[s];
-    chain_fill_job(A.gj[nj++], res[s], gx[s], gh[s], W[s], dWs, dUs, dbs, G, s, A.ntiles, keep);
-  }
-  A.njobs = nj;
-  int gmax = 0;
-  for (int k = 0; k < nj; ++k) gmax = std::max(gmax, A.gj[k].g.nblocks);
-  hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3(A.ns * A.nt8 + gmax), dim3(1024), 0, stream(), A);
   GQ_LAUNCH_CHECK();
   return res;
 }
@@ -1637,13 +1290,6 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
   return dzs;
 }
 
-// the backward chain's grads-role counters as an int32[32] view ([16]: profiling knobs)
-at::Tensor lstm_chain_sync(const at::Tensor& like) {
-  TORCH_CHECK(like.is_cuda(), "lstm_chain_sync: a GPU tensor names the device");
-  c10::DeviceGuard guard(like.device());
-  return at::from_blob(chain_sync(like.get_device()), {32}, like.options().dtype(at::kInt));
-}
-
 // [epoch, finished, timeout flag, 0] of this device's chain control words (tests)
 at::Tensor lstm_chain_status(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
@@ -1658,7 +1304,7 @@ at::Tensor lstm_chain_status(const at::Tensor& like) {
 at::Tensor lstm_chain_trace(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
   long long* p = chain_trace_buf(like.get_device());
-  at::Tensor o = at::empty({3 * 256 + 8 * 256 * 3 + 256 * 6}, like.options().dtype(at::kLong));
+  at::Tensor o = at::empty({3 * 256}, like.options().dtype(at::kLong));
   TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, o.numel() * sizeof(long long), hipMemcpyDeviceToDevice,
                              stream()) == hipSuccess, "lstm_chain_trace");
   return o;
@@ -1669,11 +1315,10 @@ at::Tensor lstm_chain_trace(const at::Tensor& like) {
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_fwd", &gq::lstm_chain_fwd);
   m.impl("lstm_chain_fwd_pack", &gq::lstm_chain_fwd_pack);
+  m.impl("lstm_chain_head_fwd", &gq::lstm_chain_head_fwd);
   m.impl("lstm_chain_status", &gq::lstm_chain_status);
   m.impl("lstm_chain_capacity", &gq::lstm_chain_capacity);
   m.impl("lstm_chain_ctl", &gq::lstm_chain_ctl);
   m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
   m.impl("lstm_chain_bwd", &gq::lstm_chain_bwd);
-  m.impl("lstm_chain_bwd_grads", &gq::lstm_chain_bwd_grads);
-  m.impl("lstm_chain_sync", &gq::lstm_chain_sync);
 }

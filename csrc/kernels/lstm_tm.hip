@@ -577,172 +577,6 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
 }
 
 // =====================================================================================
-// backward of a layer PAIR (A: Din -> H, B: H -> H), wavefront-pipelined like the pair
-// forward: waves [0, NW) run B's reverse recurrence at time t = T-1-s, waves [NW, 2 NW) run
-// A's at t + 2, taking dh_A = W_B dz_B from LDS (written in B's MFMA phase two steps back:
-// the one barrier per step orders it before A's cell phase). Per step:
-// cell phase (dz of both layers -> LDS), one LDS barrier, MFMA phase (U dz for both chains,
-// W_B dz_B -> A's dh tile; both dz tiles -> HBM for the weight-gradient passes).
-// Replaces two lstm_tm_bwd_kernel launches (and B's dx round trip through HBM).
-template <int H, int D>
-__global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_bwd_kernel(
-    const float* __restrict__ dhout, const __bf16* __restrict__ gB, const float* __restrict__ cB,
-    const __bf16* __restrict__ gA, const float* __restrict__ cA, const float* __restrict__ WB,
-    const float* __restrict__ UB, const float* __restrict__ UA, __bf16* __restrict__ dzB, __bf16* __restrict__ dzA,
-    int Mp, int T) {
-  using C = TMC<H>;
-  static_assert(C::CPL == 1, "pair kernel: one cell per lane");
-  constexpr int NW = C::NW, NTL = C::NT, G4 = C::G4, KB = C::KB;
-  constexpr int NXB = H / 16;                     // 16-row blocks of dx_B^T (din = H)
-  constexpr int TX = (NXB + NW - 1) / NW;
-  static_assert(16 * G4 / 4 == NTL, "one dz float4 granule per layer thread");
-  // [layer L (0 = B, 1 = A)][parity]; dd[0] = B's dh_out tile, dd[1] = W_B dz_B = A's dh tile.
-  // Indexed by the (uniform) layer, never pointer-selected: all accesses stay DS instructions.
-  __shared__ __attribute__((aligned(16))) __bf16 zs[2][2][16][G4 + 8];
-  __shared__ __attribute__((aligned(16))) float dd[2][2][16][C::HP];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool layerA = wv >= NW;                   // SGPR
-  const int L = layerA ? 1 : 0;
-  const int w = layerA ? wv - NW : wv;
-  const int tl = tid - (layerA ? NTL : 0);
-  const int col = lane & 15, quad = lane >> 4;
-  const int tile = blockIdx.x, ntiles = gridDim.x, row0 = tile * 16;
-
-  for (int i = tid; i < 2 * 2 * 16 * C::HP; i += 2 * NTL) (&dd[0][0][0][0])[i] = 0.f;
-  for (int i = tid; i < 2 * 2 * 16 * (G4 + 8); i += 2 * NTL) (&zs[0][0][0][0])[i] = (__bf16)0.f;
-  const int unit = 4 * w + quad;
-  const int au = 4 * w + (col >> 2);
-  const float* Ul = layerA ? UA : UB;
-  bf16x8_t ufr[KB];
-#pragma unroll
-  for (int s = 0; s < KB; ++s) {
-    bf16x8_t v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float val = Ul[(size_t)au * G4 + 32 * s + 8 * quad + j];
-      v[j] = (__bf16)(val * ((col & 3) == 0 ? 1.0f : 0.0f));
-    }
-    ufr[s] = v;
-  }
-  bf16x8_t wfr[TX][KB];                           // B waves: W_B rows (din) for dx_B^T
-#pragma unroll
-  for (int q = 0; q < TX; ++q) {
-    const int xb = w + NW * q;
-    const int din = 16 * xb + col;
-#pragma unroll
-    for (int s = 0; s < KB; ++s) {
-      bf16x8_t v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = (__bf16)(WB[(size_t)min(din, H - 1) * G4 + 32 * s + 8 * quad + j] * ((xb < NXB && din < H) ? 1.0f : 0.0f));
-      wfr[q][s] = v;
-    }
-  }
-
-  // state rings: B at step s uses t = T-1-s, A uses t = T+1-s (clamped; invalid steps skip compute)
-  const __bf16* gl = layerA ? gA : gB;
-  const float* cl = layerA ? cA : cB;
-  const int Tl = layerA ? T + 2 : T;              // this layer's t = Tl - 1 - s
-  uint2 rg[D];                                    // packed bf16 gates
-  float rc[D];
-  auto idx = [&](int tt) { return (((size_t)tt * ntiles + tile) * NW + w) * 64 + lane; };
-#define GQ_TM2B_STATE(J, SS)                                        \
-  {                                                                 \
-    const int tt_ = min(max(Tl - 1 - (SS), 0), T - 1);              \
-    const size_t o_ = idx(tt_);                                     \
-    rg[J] = *reinterpret_cast<const uint2*>(gl + o_ * 4);           \
-    rc[J] = cl[o_];                                                 \
-  }
-  constexpr int n_gd = 16 * H / 4;
-  const int gd = (tid % n_gd) * 4;
-  const float* dbase = dhout + (size_t)row0 * H + gd;
-  const size_t dstep = (size_t)Mp * H;
-  float4 rd[D];
-#define GQ_TM2B_D(J, SS)                                                                   \
-  rd[J] = *reinterpret_cast<const float4*>(dbase + (size_t)max(T - 1 - (SS), 0) * dstep);
-  const int gz_seq = tl / (G4 / 4), gz_c = (tl % (G4 / 4)) * 4;
-  __bf16* zbase = (layerA ? dzA : dzB) + (size_t)(row0 + gz_seq) * G4 + gz_c;
-  const size_t zstep = (size_t)Mp * G4;
-
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    GQ_TM2B_STATE(j, j)
-    GQ_TM2B_D(j, j)
-  }
-  __syncthreads();
-  *reinterpret_cast<float4*>(&dd[0][0][gd / H][gd % H]) = rd[0];
-  GQ_TM2B_D(0, D)
-  float dc = 0.f, dhr = 0.f;
-  __syncthreads();
-
-  for (int s0 = 0; s0 <= T + 1; s0 += D) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-      const int s = s0 + j;
-      const int t = Tl - 1 - s;                    // this layer's time step
-      const int p = s & 1;
-      const int jn = (j + 1 == D) ? 0 : j + 1;
-      // ---------------- cell phase
-      {   // branch-free: invalid steps (B past t = 0, A before its first step) are masked to 0
-        const float m = (t >= 0 && t < T) ? 1.f : 0.f;
-        const float cp = rc[jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
-        const float dh = (dd[L][p][col][unit] + dhr) * m;
-        const float4 g4 = gates_unpack(rg[j]);
-        const float tc = tanhf_fast(rc[j]);
-        const float dct = (dc + dh * g4.w * (1.f - tc * tc)) * m;
-        dc = dct * g4.y;
-        zs[L][p][col][0 * H + unit] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
-        zs[L][p][col][1 * H + unit] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
-        zs[L][p][col][2 * H + unit] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
-        zs[L][p][col][3 * H + unit] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
-      }
-      GQ_TM2B_STATE(j, s + D)
-      *reinterpret_cast<float4*>(&dd[0][p ^ 1][gd / H][gd % H]) = rd[jn];   // B's dh tile of step s+1
-      GQ_TM2B_D(jn, s + 1 + D)
-      lds_barrier();
-      // ---------------- MFMA phase: dh_{t-1} = U dz_t (both chains)
-      {
-        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[L][p][col][32 * k + 8 * quad]);
-          if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a1, 0, 0, 0);
-          else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a0, 0, 0, 0);
-        }
-        dhr = a0[0] + a1[0];
-      }
-      // this step's dz tile -> HBM (invalid steps write the scratch row T)
-      {
-        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[L][p][gz_seq][gz_c]);
-        const int tz = (t >= 0 && t < T) ? t : T;
-        *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
-      }
-      // B: dx_B^T = W_B dz_B^T -> A's dh tile (read two steps later, same parity)
-      if (!layerA) {
-#pragma unroll
-        for (int q = 0; q < TX; ++q) {
-          const int xb = w + NW * q;
-          if (xb < NXB) {                          // wave-uniform
-            f32x4_t a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < KB; ++k) {
-              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[0][p][col][32 * k + 8 * quad]);
-              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q][k], bz, a, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dd[1][p][col][16 * xb + 4 * quad + r] = a[r];
-          }
-        }
-      }
-    }
-  }
-#undef GQ_TM2B_STATE
-#undef GQ_TM2B_D
-}
-
-// =====================================================================================
 // Horizontal fusion of the backward: one launch = the reverse recurrence of layer L (the
 // serial critical path, workgroups [0, ntiles)) + the weight-gradient pass of the layer
 // processed just before it (extra 256-thread workgroups) + the split reduction of the layer
@@ -963,63 +797,6 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
 #undef GQ_TM2_LAUNCH
   GQ_LAUNCH_CHECK();
   return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB, pooled, pidx};
-}
-
-// Pair backward recurrences (lstm_tm2_bwd_kernel): dh [T, Mp, H] of B's output sequence;
-// returns [dzA, dzB] (bf16 [T+1, Mp, 4H], row T scratch) for the weight-gradient passes.
-std::vector<at::Tensor> lstm_tm2_bwd(const at::Tensor& dh, const at::Tensor& gB, const at::Tensor& cB,
-                                     const at::Tensor& gA, const at::Tensor& cA, const at::Tensor& WB,
-                                     const at::Tensor& UB, const at::Tensor& UA) {
-  for (const at::Tensor* t : {&dh, &cB, &cA, &WB, &UB, &UA}) check_f32_cuda(*t, "lstm_tm2_bwd operand");
-  check_gates_cuda(gA);
-  check_gates_cuda(gB);
-  TORCH_CHECK(dh.dim() == 3, "lstm_tm2_bwd: dh must be [T, Mp, H]");
-  const int T = (int)dh.size(0), Mp = (int)dh.size(1), H = (int)dh.size(2);
-  TORCH_CHECK(Mp % 16 == 0 && (H == 16 || H == 32), "lstm_tm2_bwd: H must be 16 or 32, Mp a multiple of 16");
-  TORCH_CHECK(UA.size(0) == H && UB.size(0) == H && WB.size(0) == H && WB.size(1) == 4 * H, "lstm_tm2_bwd: weights");
-  const long st_n = (long)(T + 1) * Mp * H;
-  TORCH_CHECK(gA.numel() == 4 * st_n && gB.numel() == 4 * st_n && cA.numel() == st_n && cB.numel() == st_n,
-              "lstm_tm2_bwd: saved state shapes");
-  c10::DeviceGuard guard(dh.device());
-  const auto zopt = dh.options().dtype(at::kBFloat16);
-  at::Tensor dzA = at::empty({T + 1, Mp, 4 * H}, zopt), dzB = at::empty({T + 1, Mp, 4 * H}, zopt);
-  const int ntiles = Mp / 16;
-  GQ_TM2_H_DISPATCH(H, hipLaunchKernelGGL((lstm_tm2_bwd_kernel<HH, 4>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,
-                                         stream(), dh.data_ptr<float>(), bf16_ptr(gB), cB.data_ptr<float>(),
-                                         bf16_ptr(gA), cA.data_ptr<float>(), WB.data_ptr<float>(),
-                                         UB.data_ptr<float>(), UA.data_ptr<float>(), bf16_ptr(dzB),
-                                         bf16_ptr(dzA), Mp, T));
-  GQ_LAUNCH_CHECK();
-  return {dzA, dzB};
-}
-
-// Backward recurrence only: dz [T+1, Mp, 4H] (row T scratch) for the split backward (dx and
-// the weight-gradient pass are then launched separately, the latter on a side stream).
-at::Tensor lstm_tm_bwd_dz(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& W,
-                          const at::Tensor& U, int64_t T, const c10::optional<at::Tensor>& pool_idx, int64_t pool) {
-  for (const at::Tensor* t : {&dh, &c, &W, &U}) check_f32_cuda(*t, "lstm_tm_bwd_dz operand");
-  check_gates_cuda(g);
-  const int H = (int)U.size(0);
-  const bool last = dh.dim() == 2;
-  const int Mp = (int)(last ? dh.size(0) : dh.size(1));
-  TORCH_CHECK(last ? dh.size(1) == H : ((pool > 0 || dh.size(0) == T) && dh.size(2) == H), "lstm_tm_bwd_dz: dh shape");
-  const TmPool pl = tm_pool_input(pool_idx, last ? 0 : pool, dh, (int)T, Mp, H);
-  TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H,
-              "lstm_tm_bwd_dz: saved state shapes");
-  TORCH_CHECK(H == 16 || H == 32 || H == 64, "lstm_tm_bwd_dz: hidden size");
-  c10::DeviceGuard guard(dh.device());
-  at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, dh.options().dtype(at::kBFloat16));
-  const int ntiles = Mp / 16;
-  auto st = stream();
-  GQ_TM_H_DISPATCH(H,
-      if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
-            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, (int)T,
-            (int)W.size(0), (int)W.size(0), st);
-      else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
-            c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, (int)T,
-            (int)W.size(0), (int)W.size(0), st, pl));
-  GQ_LAUNCH_CHECK();
-  return dz;
 }
 
 // ---- pipelined backward (see lstm_tm_bwd_dual_kernel)
@@ -1431,9 +1208,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_tm_fwd", &gq::lstm_tm_fwd);
   m.impl("lstm_tm2_fwd", &gq::lstm_tm2_fwd);
-  m.impl("lstm_tm2_bwd", &gq::lstm_tm2_bwd);
   m.impl("lstm_tm_grads", &gq::lstm_tm_grads);
-  m.impl("lstm_tm_bwd_dz", &gq::lstm_tm_bwd_dz);
   m.impl("lstm_tm_bwd_pipe", &gq::lstm_tm_bwd_pipe);
   m.impl("lstm_grads_job_ws", &gq::lstm_grads_job_ws);
   m.impl("lstm_grads_multi", &gq::lstm_grads_multi);

@@ -27,28 +27,23 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train, int pool=0) -> Tensor[]");
   m.def("lstm_tm2_fwd(Tensor x, Tensor WA, Tensor UA, Tensor bA, Tensor WB, Tensor UB, Tensor bB, bool train, "
         "int pool=0) -> Tensor[]");
-  m.def("lstm_tm2_bwd(Tensor dh, Tensor gB, Tensor cB, Tensor gA, Tensor cA, Tensor WB, Tensor UB, Tensor UA) "
-        "-> Tensor[]");
   m.def("lstm_tm_grads(Tensor dz, Tensor x, Tensor h, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
         "bool need_dx) -> Tensor");
-  m.def("lstm_tm_bwd_dz(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T, Tensor? pool_idx=None, "
-        "int pool=0) -> Tensor");
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
   m.def("lstm_chain_fwd(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train) -> Tensor[]");
   m.def("lstm_chain_fwd_pack(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train, Tensor Wt4, "
         "Tensor Ut4) -> Tensor[]");
+  m.def("lstm_chain_head_fwd(Tensor x, Tensor[] W, Tensor[] U, Tensor[] b, int[] pool, bool train, Tensor Wt4, "
+        "Tensor Ut4, Tensor bt4, Tensor[] head, Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, "
+        "float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");
   m.def("lstm_chain_status(Tensor like) -> Tensor");
   m.def("lstm_chain_capacity(Tensor like) -> int");
   m.def("lstm_chain_ctl(Tensor like) -> Tensor");
-  m.def("lstm_chain_sync(Tensor like) -> Tensor");
   m.def("lstm_grads_multi(Tensor[] gz, Tensor[] gx, Tensor[] gh, Tensor[] gW, int[] period, int[] hshift, "
         "Tensor[] gws, Tensor[] rws, Tensor[] rW, Tensor(a!)[] rdW, Tensor(b!)[] rdU, Tensor(c!)[] rdb) -> ()");
   m.def("lstm_chain_trace(Tensor like) -> Tensor");
   m.def("lstm_chain_bwd(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");
-  m.def("lstm_chain_bwd_grads(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
-        "int[] x_width, int[] T_in, Tensor[] gx, Tensor[] gh, Tensor(a!)[] gdW, Tensor(b!)[] gdU, Tensor(c!)[] gdb, "
-        "Tensor(d!)[] ext) -> Tensor[]");
   m.def("time4_head_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor pk, bool train, Tensor[] head, Tensor y, Tensor mask, "
         "int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");
   m.def("time4_head_bwd(Tensor dloss, Tensor x, Tensor h, Tensor g, Tensor c, Tensor W, Tensor U, Tensor pk, Tensor[] head, "

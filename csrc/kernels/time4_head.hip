@@ -461,6 +461,33 @@ static void t4_check(const at::Tensor& x, const at::Tensor& W, const at::Tensor&
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "time4_head: x must be 16-byte aligned");
 }
 
+// The forward head's arguments: weights, labels, outputs (logits [M], loss [1], per-tile partials
+// allocated here), the metric accumulators (sums [6] fp64 / hist [2, bins], empty: none) and the
+// arrival ticket (chain control word 4). Also used by lstm_chain_head_fwd (lstm_chain.hip).
+void t4_head_fwd_args(ChainHead& hd, at::TensorList head, const at::Tensor& y, const at::Tensor& mask, int64_t M,
+                      int Mp, double alpha1, double alpha2, double w0, double w1, const at::Tensor& sums,
+                      const at::Tensor& hist, at::Tensor& logits, at::Tensor& loss, at::Tensor& part) {
+  t4_head_args(hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1);
+  auto opt = y.options();
+  logits = at::empty({M}, opt);
+  loss = at::empty({1}, opt);
+  part = at::empty({Mp / 16 * 8}, opt);
+  hd.logits = logits.data_ptr<float>();
+  hd.loss = loss.data_ptr<float>();
+  hd.part = part.data_ptr<float>();
+  hd.ticket = chain_ctl(y.get_device()) + 4;
+  if (sums.numel() > 0) {
+    TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.numel() == 6, "sums: 6 float64");
+    hd.sums = sums.data_ptr<double>();
+  }
+  if (hist.numel() > 0) {
+    check_f32_cuda(hist, "hist");
+    TORCH_CHECK(hist.dim() == 2 && hist.size(0) == 2, "hist must be [2, bins]");
+    hd.hist = hist.data_ptr<float>();
+    hd.bins = (int)hist.size(1);
+  }
+}
+
 // time4 + head + weighted BCE forward. x: [T, Mp, Din] (the pooled output of the chain); pk: the
 // A-fragment image of (W, U) built by lstm_chain_fwd_pack (empty: built here through LDS);
 // head = [W1, b1, W2, b2, W3, b3], y / mask [M]. Returns [h [T, Mp, 128], g, c, logits [M], loss [1]];
@@ -488,7 +515,7 @@ std::vector<at::Tensor> time4_head_fwd(const at::Tensor& x, const at::Tensor& W,
   at::Tensor h = at::empty({T, Mp, T4H}, opt);
   at::Tensor g = train ? at::empty({(long)T * Mp * T4H * 4}, opt) : at::empty({0}, opt);
   at::Tensor c = train ? at::empty({(long)T * Mp * T4H * 2}, opt) : at::empty({0}, opt);
-  at::Tensor logits = at::empty({M}, opt), loss = at::empty({1}, opt), part = at::empty({ntiles * 8}, opt);
+  at::Tensor logits, loss, part;
   A.h = h.data_ptr<float>();
   A.g = train ? g.data_ptr<float>() : nullptr;
   A.c = train ? c.data_ptr<float>() : nullptr;
@@ -497,21 +524,7 @@ std::vector<at::Tensor> time4_head_fwd(const at::Tensor& x, const at::Tensor& W,
   A.Din = Din;
   A.Dw = Dw;
   A.ntiles = ntiles;
-  t4_head_args(A.hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1);
-  A.hd.logits = logits.data_ptr<float>();
-  A.hd.loss = loss.data_ptr<float>();
-  A.hd.part = part.data_ptr<float>();
-  A.hd.ticket = chain_ctl(x.get_device()) + 4;
-  if (sums.numel() > 0) {
-    TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.numel() == 6, "sums: 6 float64");
-    A.hd.sums = sums.data_ptr<double>();
-  }
-  if (hist.numel() > 0) {
-    check_f32_cuda(hist, "hist");
-    TORCH_CHECK(hist.dim() == 2 && hist.size(0) == 2, "hist must be [2, bins]");
-    A.hd.hist = hist.data_ptr<float>();
-    A.hd.bins = (int)hist.size(1);
-  }
+  t4_head_fwd_args(A.hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1, sums, hist, logits, loss, part);
   A.head = 1;
   A.trace = t4_trace_buf(x.get_device());
   TORCH_CHECK(ntiles <= 256, "time4_head: at most 256 tiles");
@@ -571,7 +584,7 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   A.hd.dW3 = hgrads[4].data_ptr<float>();
   A.hd.db3 = hgrads[5].data_ptr<float>();
   A.hd.ticket = chain_ctl(x.get_device()) + 5;
-  A.hd.done = chain_ctl(x.get_device()) + 7;
+  A.hd.done = chain_ctl(x.get_device()) + 8;     // ([7] is the non-finite gradient flag)
   A.hd.ctl = chain_ctl(x.get_device());
   A.head = 1;
   A.trace = t4_trace_buf(x.get_device());

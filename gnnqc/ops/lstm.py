@@ -51,72 +51,21 @@ class _DirectGrad:
     ``lstm_grads`` kernels straight into ``param.grad`` (the optimiser's flat gradient
     buffer views) instead of being returned to autograd - no separate AccumulateGrad add
     per parameter. Off by default so that ``torch.autograd.grad`` (e.g. integrated
-    gradients) never touches ``.grad``.
+    gradients) never touches ``.grad``. In this mode the weight-gradient passes are deferred
+    and batched (:class:`_Pipe`).
 
-    In this mode the weight-gradient passes can also leave the critical path: each layer's
-    backward recurrence is followed by a small dx kernel on the current stream (what the
-    next layer's recurrence waits for), while dW/dU/db run on a side stream that the
-    current stream re-joins when the context exits (HIP-graph capture turns this into
-    parallel graph branches). Opt-in, see :func:`_split_mode`."""
+    (Measured on MI355X and removed: dW/dU/db on a side stream behind a dx-only kernel -
+    0.885 vs 0.757 ms/step, cross-stream event waits cost more than the overlap won - and the
+    chain's weight-gradient batch on a side stream concurrent with the GCN backward, 0.3812 vs
+    0.3788 ms/step.)"""
 
     enabled = False
-    streams = {}          # device index -> side stream
-    pending = set()       # devices with side-stream work not yet joined
-    keep = []             # tensors the side stream reads: held until the join (allocator safety)
-
-
-def _split_mode() -> str:
-    """Backward of a direct-accumulation LSTM layer: ``pipe`` (default: weight gradients of
-    each layer fused behind the next layer's recurrence, see :class:`_Pipe`; layers with
-    large recurrence grids keep ``fused``), ``fused`` (recurrence, then one weight-gradient
-    kernel also producing dx, then the split reduction), ``split`` (dx kernel +
-    weight-gradient kernel, one stream) or ``side`` (weight gradients on a side stream).
-    Env ``GNNQC_LSTM_BWD``.
-
-    Measured on MI355X (CML bench, ms/step, HIP graph / eager): pipe 0.667 / 0.985,
-    fused 0.709 / 0.986; earlier: fused 0.757 / 1.238 vs side 0.885 / 2.037 - cross-stream
-    event waits cost more than the overlap wins here."""
-    import os
-    return os.environ.get("GNNQC_LSTM_BWD", "pipe")
-
-
-def _side_stream(device: torch.device):
-    if _split_mode() != "side" or device.type != "cuda":
-        return None
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _DirectGrad.streams.get(idx)
-    if st is None:
-        st = torch.cuda.Stream(device=idx)
-        _DirectGrad.streams[idx] = st
-    return st
-
-
-def join_side_streams():
-    """Make the current stream wait for all pending weight-gradient side-stream work."""
-    for idx in list(_DirectGrad.pending):
-        torch.cuda.current_stream(idx).wait_stream(_DirectGrad.streams[idx])
-    _DirectGrad.pending.clear()
-    # freed only now: later reuse of their memory on the current stream is ordered after the
-    # side-stream kernels (no record_stream, which does not mix with graph capture)
-    _DirectGrad.keep.clear()
-
-
-def _off_critical_path(device: torch.device, tensors, fn):
-    """Run ``fn()`` (weight-gradient kernels) on the side stream after the current stream's
-    work so far; ``tensors`` stay referenced until :func:`join_side_streams`."""
-    st = _side_stream(device) if _DirectGrad.enabled else None
-    if st is None:
-        fn()
-        return
-    st.wait_stream(torch.cuda.current_stream(device))
-    with torch.cuda.stream(st):
-        fn()
-    _DirectGrad.keep.extend(tensors)
-    _DirectGrad.pending.add(device.index if device.index is not None else torch.cuda.current_device())
 
 
 class _Pipe:
-    """Pipelined backward (``GNNQC_LSTM_BWD=pipe``, direct-accumulation mode only).
+    """Pipelined backward (direct-accumulation mode only; measured 0.667 vs 0.709 ms/step for
+    one weight-gradient kernel per layer behind its recurrence, the fallback for layers the pipe
+    does not take).
 
     A layer's weight-gradient pass does not feed any later recurrence, so it is deferred:
     each time-major backward recurrence launches ONE kernel (``lstm_tm_bwd_pipe``) whose
@@ -126,29 +75,10 @@ class _Pipe:
     (the next recurrence's input). Leftover work is flushed when the direct-accumulation
     context exits. Single stream: ordering is plain stream order, no events."""
 
+    enabled = True  # (tests switch it off to compare with the per-layer fused backward)
     job = None      # layer whose weight-gradient pass has not run yet
     red = None      # layer whose gradient pass ran; its split reduction has not
     batch = []      # jobs of a chain backward: all gradient passes in one launch at the flush
-
-
-def _grads_side_on() -> bool:
-    """Chain-backward weight-gradient passes on a side stream, concurrent with the rest of the
-    backward (the GCN's), joined before the optimiser (``GNNQC_GRADS_SIDE``, default OFF).
-    Measured 0.3788 vs 0.3812 ms/step (CML, graph replay: the branches mostly serialise), and
-    with the overlap the deterministic-mode bitwise test failed after the kernel tests had run in
-    the same process while it passed with the side stream ordered after the GCN backward
-    (GNNQC_GRADS_SIDE_LATE=1): not worth an unexplained hazard."""
-    import os
-    return os.environ.get("GNNQC_GRADS_SIDE", "0") == "1"
-
-
-def _grads_stream(device: torch.device):
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _DirectGrad.streams.get(idx)
-    if st is None:
-        st = torch.cuda.Stream(device=idx)
-        _DirectGrad.streams[idx] = st
-    return idx, st
 
 
 # Largest sequence count (rows of 16-sequence tiles) a recurrence may have for its layer to
@@ -162,8 +92,7 @@ _MULTI_MAX = 12        # jobs per lstm_grads_multi launch (lstm_tm.hip MULTI_MAX
 
 
 def _pipe_on(sinks, n_seq: int) -> bool:
-    return (_DirectGrad.enabled and _split_mode() == "pipe" and all(d for _, d in sinks)
-            and n_seq <= PIPE_MAX_SEQ)
+    return _Pipe.enabled and _DirectGrad.enabled and all(d for _, d in sinks) and n_seq <= PIPE_MAX_SEQ
 
 
 def _pipe_job(dz, x, h, W, sinks, period: int, hshift: int):
@@ -201,33 +130,11 @@ def pipe_flush():
         from ..utils.native import hip_ops
         grads = ([_Pipe.job] if _Pipe.job is not None else []) + _Pipe.batch
         reds = ([_Pipe.red] if _Pipe.red is not None else []) + grads
-
-        def launch():
-            hip_ops().lstm_grads_multi([j["dz"] for j in grads], [j["x"] for j in grads], [j["h"] for j in grads],
-                                       [j["W"] for j in grads], [j["period"] for j in grads],
-                                       [j["hshift"] for j in grads], [j["ws"] for j in grads],
-                                       [r["ws"] for r in reds], [r["W"] for r in reds], [r["g"][0] for r in reds],
-                                       [r["g"][1] for r in reds], [r["g"][2] for r in reds])
-        # every batched job carries the event recorded after ITS chain backward (never a stale one)
-        ev = grads[0].get("ready")
-        if (ev is not None and all(j.get("ready") is ev for j in grads) and _Pipe.job is None
-                and _Pipe.red is None and _grads_side_on()):
-            # the passes only need the chain backward's dz: they run on a side stream from that
-            # point, concurrent with the GCN backward the current stream has queued since; the
-            # context exit joins the side stream (a graph fork / join under capture)
-            dev = grads[0]["dz"].device
-            idx, st = _grads_stream(dev)
-            import os
-            if os.environ.get("GNNQC_GRADS_SIDE_LATE", "0") == "1":
-                st.wait_stream(torch.cuda.current_stream(dev))      # (diagnostic: no overlap)
-            else:
-                st.wait_event(ev)
-            with torch.cuda.stream(st):
-                launch()
-            _DirectGrad.keep.extend(t for j in reds for t in (j["dz"], j["x"], j["h"], j["W"], j["ws"]))
-            _DirectGrad.pending.add(idx)
-        else:
-            launch()
+        hip_ops().lstm_grads_multi([j["dz"] for j in grads], [j["x"] for j in grads], [j["h"] for j in grads],
+                                   [j["W"] for j in grads], [j["period"] for j in grads],
+                                   [j["hshift"] for j in grads], [j["ws"] for j in grads],
+                                   [r["ws"] for r in reds], [r["W"] for r in reds], [r["g"][0] for r in reds],
+                                   [r["g"][1] for r in reds], [r["g"][2] for r in reds])
         _Pipe.job, _Pipe.red, _Pipe.batch = None, None, []
     while _Pipe.job is not None or _Pipe.red is not None:
         _pipe_drain_one()
@@ -274,8 +181,6 @@ def direct_grad_accumulation(flag: bool = True):
         _DirectGrad.enabled = prev
         if _Pipe.job is not None or _Pipe.red is not None or _Pipe.batch:
             pipe_flush()
-        if _DirectGrad.pending and torch.cuda.is_available():
-            join_side_streams()
 
 
 def _grad_sink(p: torch.Tensor):
@@ -346,12 +251,6 @@ class _HipLSTM(torch.autograd.Function):
             dx = ops.lstm_dx(dz, Wc, x) if need_dx else None
             _pipe_push(_pipe_job(dz, x, h, Wc, ((gW, True), (gU, True), (gb, True)), T, 1))
             return dx, None, None, None, None, None
-        if dW_in and dU_in and db_in and _split_mode() not in ("fused", "pipe") and x.shape[-1] % 4 == 0:
-            # critical path: dx only; dW/dU/db on the side stream
-            dx = ops.lstm_dx(dz, Wc, x) if need_dx else None
-            _off_critical_path(dz.device, (dz, x, h, Wc),
-                               lambda: ops.lstm_grads(dz, x, h, Wc, gW, gU, gb, False))
-            return dx, None, None, None, None, None
         dx = ops.lstm_grads(dz, x, h, Wc, gW, gU, gb, need_dx)
         return (dx if need_dx else None,
                 None if dW_in or not ctx.needs_input_grad[1] else gW,
@@ -360,21 +259,8 @@ class _HipLSTM(torch.autograd.Function):
                 None, None)
 
 
-def _tm_split_backward(dh, g, c, x, h, W, U, sinks, need_dx, pool_idx=None, pool: int = 0):
-    """Time-major layer backward in direct-accumulation mode: recurrence -> dz, dx = dz W^T
-    on the current stream; the weight-gradient pass on the side stream."""
-    from ..utils.native import hip_ops
-    ops = hip_ops()
-    T = x.shape[0]
-    dz = ops.lstm_tm_bwd_dz(dh, g, c, W, U, T, pool_idx, int(pool))
-    dx = ops.lstm_dx(dz, W, x) if need_dx else None
-    _off_critical_path(x.device, (dz, x, h, W),
-                       lambda: ops.lstm_tm_grads(dz, x, h, W, sinks[0][0], sinks[1][0], sinks[2][0], False))
-    return dx
-
-
 def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx, pidx=None, pool: int = 0):
-    """Backward of one time-major layer (pipe / split / fused, see :func:`_split_mode`).
+    """Backward of one time-major layer (the pipe when it takes the layer, else one fused kernel).
     Returns dx (or None) and the three weight gradients to hand to autograd (None where they
     were accumulated directly into ``.grad``)."""
     from ..utils.native import hip_ops
@@ -390,8 +276,6 @@ def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx, pidx=Non
     Wc, Uc = W.contiguous(), U.contiguous()
     if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
         dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx)
-    elif wgrad and all(d for _, d in sinks) and _split_mode() not in ("fused", "pipe"):
-        dx = _tm_split_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx, pi, pool)
     else:
         dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, sinks[0][0], sinks[1][0], sinks[2][0],
                                    need_dx, pi, pool)
@@ -449,10 +333,6 @@ class _HipLSTMChain(torch.autograd.Function):
                                      [outs[5 * i + 4] if pools[i] else e8 for i in order],
                                      [pools[i] for i in order], [layer_x(i).shape[-1] for i in order],
                                      [outs[5 * i].shape[0] for i in order])
-            ready = None
-            if x.is_cuda and _grads_side_on():
-                ready = torch.cuda.Event()          # the dz of every layer are final from here
-                ready.record()
             for k, i in enumerate(order):
                 nw = need[2 + 3 * i:5 + 3 * i]
                 if not any(nw):
@@ -462,9 +342,7 @@ class _HipLSTMChain(torch.autograd.Function):
                 sinks = [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]]
                 if (_pipe_on(sinks, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
                         and len(_Pipe.batch) < _MULTI_MAX - 2):
-                    job = _pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1])
-                    job["ready"] = ready
-                    _Pipe.batch.append(job)
+                    _Pipe.batch.append(_pipe_job(res[k], xi, h, Ws[i], sinks, h.shape[0] * h.shape[1], h.shape[1]))
                 else:
                     ops.lstm_tm_grads(res[k], xi, h, Ws[i], sinks[0][0], sinks[1][0], sinks[2][0], False)
                 grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, nw)]
@@ -509,14 +387,25 @@ class _HipLSTMChainHead(torch.autograd.Function):
         head = [p.contiguous() for p in params[3 * (ns + 1):]]
         need = any(ctx.needs_input_grad)
         e = x.new_zeros(0)
-        # (the chain's spare workgroups build time4's weight-fragment image on the way)
-        outs = ops.lstm_chain_fwd_pack(x, Ws[:ns], Us[:ns], bs[:ns], [int(p) for p in pools], need, Ws[ns], Us[ns])
-        pk = outs.pop()
-        xt = outs[5 * (ns - 1) + 3] if pools[-1] else outs[5 * (ns - 1)]      # time4's input [T4, Mp, C]
-        h4, g4, c4, logits, loss = ops.time4_head_fwd(xt, Ws[ns], Us[ns], bs[ns], pk, need, head, y, mask, int(M),
-                                                      *[float(c) for c in consts],
-                                                      sums if sums is not None else e.double(),
-                                                      hist if hist is not None else e)
+        sums_ = sums if sums is not None else e.double()
+        hist_ = hist if hist is not None else e
+        if _t4_chain_on() and pools[-1] == 3:
+            # time4 + head + loss as one more stage of the chain launch (it consumes the last
+            # stage's output as it is produced); spare workgroups build time4's backward fragments
+            outs = ops.lstm_chain_head_fwd(x, Ws[:ns], Us[:ns], bs[:ns], [int(p) for p in pools], need, Ws[ns],
+                                           Us[ns], bs[ns], head, y, mask, int(M), *[float(c) for c in consts],
+                                           sums_, hist_)
+            h4, g4, c4, logits, loss = outs[-5:]
+            del outs[-5:]
+            pk = outs.pop()
+        else:
+            # (the chain's spare workgroups build time4's weight-fragment image on the way)
+            outs = ops.lstm_chain_fwd_pack(x, Ws[:ns], Us[:ns], bs[:ns], [int(p) for p in pools], need, Ws[ns],
+                                           Us[ns])
+            pk = outs.pop()
+            xt = outs[5 * (ns - 1) + 3] if pools[-1] else outs[5 * (ns - 1)]      # time4's input [T4, Mp, C]
+            h4, g4, c4, logits, loss = ops.time4_head_fwd(xt, Ws[ns], Us[ns], bs[ns], pk, need, head, y, mask, int(M),
+                                                          *[float(c) for c in consts], sums_, hist_)
         ctx.pools, ctx.consts, ctx.M = tuple(int(p) for p in pools), tuple(float(c) for c in consts), int(M)
         ctx.params = params
         ctx.set_materialize_grads(False)     # (no zeros tensor for the non-differentiable logits)
@@ -561,24 +450,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
                       [outs[5 * i].shape[0] for i in order])
         grads = [None] * npar
         sinks = {i: [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]] for i in range(ns + 1)}
-        if (_chain_grads_on() and all(all(need[8 + 3 * i:11 + 3 * i]) for i in range(ns + 1))
-                and all(d for i in range(ns + 1) for _, d in sinks[i])
-                and all(_pipe_x_ok(layer_x(i), Ws[i].shape[0]) for i in range(ns + 1))
-                and chain_fits(x.shape[1], ns, x.device, spare=8)):
-            # the seven weight-gradient passes and their reductions inside the chain backward
-            # launch (its spare workgroups start each pass as soon as its layer's dz is final)
-            res = ops.lstm_chain_bwd_grads(
-                dxt, *chain_args, [layer_x(i) for i in order], [outs[5 * i] for i in order],
-                [sinks[i][0][0] for i in order], [sinks[i][1][0] for i in order], [sinks[i][2][0] for i in order],
-                [dz4, xt, h4, Ws[ns], sinks[ns][0][0], sinks[ns][1][0], sinks[ns][2][0]])
-            hgrads = [None if (direct or not n) else buf for (buf, direct), n in zip(hsinks, need[8 + npar:])]
-            dx = res[ns]
-            return (dx if need[0] else None, None, None, None, None, None, None, None, *grads, *hgrads)
         res = ops.lstm_chain_bwd(dxt, *chain_args)
-        ready = None
-        if x.is_cuda and _grads_side_on():
-            ready = torch.cuda.Event()          # the dz of every layer are final from here
-            ready.record()
         dzs = {ns: dz4}
         hs = {ns: h4}
         for k, i in enumerate(order):
@@ -593,9 +465,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
             sk = sinks[i]
             if (_pipe_on(sk, h.shape[1]) and _pipe_x_ok(xi, Ws[i].shape[0])
                     and len(_Pipe.batch) < _MULTI_MAX - 2):
-                job = _pipe_job(dzs[i], xi, h, Ws[i], sk, h.shape[0] * h.shape[1], h.shape[1])
-                job["ready"] = ready
-                _Pipe.batch.append(job)
+                _Pipe.batch.append(_pipe_job(dzs[i], xi, h, Ws[i], sk, h.shape[0] * h.shape[1], h.shape[1]))
             else:
                 ops.lstm_tm_grads(dzs[i], xi, h, Ws[i], sk[0][0], sk[1][0], sk[2][0], False)
             grads[3 * i:3 * i + 3] = [None if (direct or not n) else buf for (buf, direct), n in zip(sk, nw)]
@@ -622,6 +492,13 @@ def _chain_bwd_on() -> bool:
     """Cross-CU pipelined backward of the chain (``GNNQC_CHAIN_BWD``, default on)."""
     import os
     return os.environ.get("GNNQC_CHAIN_BWD", "1") == "1"
+
+
+def _t4_chain_on() -> bool:
+    """time4 + head as a stage of the forward chain launch (``lstm_chain_head_fwd``;
+    ``GNNQC_T4_CHAIN``, default on) instead of its own launch after the chain."""
+    import os
+    return os.environ.get("GNNQC_T4_CHAIN", "1") == "1"
 
 
 def _chain_on() -> bool:
@@ -665,20 +542,14 @@ def chain_fits(Mp: int, n_stages: int, device=None, spare: int = 0) -> bool:
     return (2 <= n_stages <= 8 and n_stages * ((Mp // 16 + 7) // 8 * 8) + spare <= chain_capacity(device))
 
 
-def _chain_grads_on() -> bool:
-    """Weight-gradient passes inside the chain backward launch (``GNNQC_CHAIN_GRADS``, default off:
-    measured slower - the waiting workgroups slowed the chain itself by ~25%, profiles/r2_chain_grads_trace.jsonl)."""
-    import os
-    return os.environ.get("GNNQC_CHAIN_GRADS", "0") == "1"
-
-
 _CHAIN_CTL = {}
 
 
 def chain_ctl(device) -> Optional[torch.Tensor]:
     """The device's chain control words ``[epoch, finished, timeout flag, rejected steps, fwd / bwd
-    head tickets, debug spin limit, 0]`` as an int32[8] view (``lstm_chain.hip``); None off the GPU. The optimiser's non-finite guard reads
-    and clears the timeout flag inside the captured step."""
+    head tickets, debug spin limit, non-finite gradient flag, head backward arrivals, 0 ...]`` as an
+    int32[16] view (``lstm_chain.hip``); None off the GPU. The optimiser's update reads and clears
+    the timeout / non-finite flags inside the captured step."""
     device = torch.device(device)
     if device.type != "cuda":
         return None
@@ -753,9 +624,6 @@ class _HipLSTMTM(torch.autograd.Function):
         pi = pidx if pool else None
         if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
             dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
-        elif wgrad and all(d for _, d in sinks) and _split_mode() not in ("fused", "pipe"):
-            dx = _tm_split_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx,
-                                    pi, pool)
         else:
             dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
                                        sinks[0][0], sinks[1][0], sinks[2][0], need_dx, pi, pool)
@@ -766,7 +634,9 @@ class _HipLSTMTM(torch.autograd.Function):
 class _HipLSTMTMPair(torch.autograd.Function):
     """Two stacked time-major layers A (Din -> H) and B (H -> H), both returning sequences:
     ONE wavefront-pipelined forward kernel (``lstm_tm2_fwd``); the backward runs the
-    per-layer fused kernels (B first, its dx is A's dh)."""
+    per-layer kernels (B first, its dx is A's dh). (A pipelined pair backward was measured
+    slower - 148 vs 118 us for the CML H=16 pair: B's in-loop dx MFMAs and A's waves share each
+    SIMD's MFMA pipe - and removed.)"""
 
     @staticmethod
     def forward(ctx, x, WA, UA, bA, WB, UB, bB, pool: int = 0):
@@ -802,24 +672,10 @@ class _HipLSTMTMPair(torch.autograd.Function):
         sA = sinks(ctx.params[:3], need[1:4])
         need_dx = bool(need[0])
         dx = None
-        if any(need[1:7]) and _pair_bwd():
-            # training: both reverse recurrences in one pipelined kernel (B's dx stays in LDS),
-            # then one weight-gradient pass per layer (+ dx of A)
-            if pool:      # (this kernel takes the unpooled gradient)
-                T, Mp, H = hB.shape
-                dout = ops.maxpool1d_bwd(dout.view(1, -1, Mp * H), pidx.view(1, -1, Mp * H), T, pool).view(T, Mp, H)
-            dzA, dzB = ops.lstm_tm2_bwd(dout, gB, cB, gA, cA, WB.contiguous(), UB.contiguous(),
-                                        UA.contiguous())
-            ops.lstm_tm_grads(dzB, hA, hB, WB.contiguous(), sB[0][0], sB[1][0], sB[2][0], False)
-            dx = ops.lstm_tm_grads(dzA, x, hA, WA.contiguous(), sA[0][0], sA[1][0], sA[2][0], need_dx)
-        elif (any(need[4:7]) and any(need[1:4]) and not pool and _pipe_on(sB, x.shape[1]) and _pipe_on(sA, x.shape[1])
-              and _pipe_x_ok(x, WA.shape[0]) and _pipe_x_ok(hA, WB.shape[0])):
+        if (any(need[4:7]) and any(need[1:4]) and not pool and _pipe_on(sB, x.shape[1]) and _pipe_on(sA, x.shape[1])
+                and _pipe_x_ok(x, WA.shape[0]) and _pipe_x_ok(hA, WB.shape[0])):
             dhA = _pipe_tm_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
             dx = _pipe_tm_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
-        elif (any(need[4:7]) and all(d for _, d in sB) and any(need[1:4]) and all(d for _, d in sA)
-              and _split_mode() not in ("fused", "pipe")):
-            dhA = _tm_split_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True, pi, pool)
-            dx = _tm_split_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
             dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
                                   sB[0][0], sB[1][0], sB[2][0], True, pi, pool)
@@ -829,17 +685,6 @@ class _HipLSTMTMPair(torch.autograd.Function):
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
         return (dx if need_dx else None, *gA_, *gB_, None)
-
-
-def _pair_bwd() -> bool:
-    """Pipelined pair backward (``lstm_tm2_bwd``), opt-in with ``GNNQC_PAIR_BWD=1``.
-
-    Measured slower than two per-layer kernels on MI355X (CML 148 vs 118 us for the H=16
-    pair, 103 vs 62 us for H=32; SoilNet likewise): B's in-loop dx MFMAs and the second
-    layer's waves sharing each SIMD's MFMA pipe lengthen every step more than the fusion
-    saves, unlike the forward pair where both layers' per-step work is symmetric."""
-    import os
-    return os.environ.get("GNNQC_PAIR_BWD", "0") == "1"
 
 
 def lstm_pair_tm(x_tm, A, B, pool: int = 0) -> torch.Tensor:
@@ -874,5 +719,4 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
 
 __all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
            "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError", "lstm_chain_head_tm",
-           "direct_grad_accumulation",
-           "join_side_streams"]
+           "direct_grad_accumulation"]

@@ -61,7 +61,8 @@ class FlatOptimizer:
         self.iterations = 0                                              # attempted steps (host)
         self.guard = bool(guard)
         # [nonfinite count, ticket, ok flag, skipped steps, decision generation, overflowed elements
-        # (adam_flagged), -, -] (adam.hip grad_guard / adam_guarded / adam_flagged)
+        # (adam_flagged), decision-wait timeouts (adam_guarded), -] (adam.hip grad_guard /
+        # adam_guarded / adam_flagged)
         self.guard_state = torch.zeros(8, device=dev, dtype=torch.int32)
         self.guard_state[2] = 1
         # multi-step graphs (gnnqc.train.engine): a device batch cursor the update advances
@@ -77,6 +78,16 @@ class FlatOptimizer:
     @property
     def skipped_steps(self) -> int:
         return int(self.guard_state[3].item())
+
+    def check_update(self):
+        """Raise if a workgroup of the one-launch guarded update gave up waiting for the step
+        decision (adam.hip adam_guarded_kernel counts it in guard_state[6]): that step may have
+        updated only part of the parameters. Synchronises."""
+        n = int(self.guard_state[6].item())
+        if n:
+            self.guard_state[6:7].zero_()
+            raise RuntimeError(f"guarded Adam: {n} workgroup(s) never saw the step decision (grid not co-resident: "
+                               "another kernel held the CUs?); the parameters may be partially updated")
 
     def _begin_step(self, need_flag: bool = True):
         """Advance the step counter; with the guard, only if the gradients are finite.

@@ -414,20 +414,27 @@ class Trainer:
         else:
             for row in rows:
                 self.train_step(row)
-        if self.peer is not None:
-            # a peer all-reduce timeout on ANY rank is fatal on EVERY rank (its steps were rejected
-            # there only, so the ranks' parameters may differ): agree before any other collective
-            flag = torch.tensor([1.0 if self.peer.timed_out() else 0.0],
+        if self.world > 1:
+            # a peer all-reduce timeout or a partial guarded update on ANY rank is fatal on EVERY
+            # rank (the ranks' parameters may differ): agree before any other collective
+            upd = getattr(self.opt, "guard_state", None)
+            flag = torch.tensor([1.0 if self.peer is not None and self.peer.timed_out() else 0.0,
+                                 float(upd[6].item()) if upd is not None else 0.0],
                                 device=self.device if D.backend() == "nccl" else "cpu")
             D.all_reduce_(flag, force=True)
-            if float(flag.item()) != 0.0:
+            if float(flag[0].item()) != 0.0:
                 raise RuntimeError("peer all-reduce: a rank never arrived (spin timeout); training stopped on "
                                    "every rank")
+            if float(flag[1].item()) != 0.0:
+                raise RuntimeError("guarded Adam: a workgroup never saw the step decision on some rank (partial "
+                                   "update); training stopped on every rank")
         D.average_buffers(self.model)                 # DP: BN moving statistics agree on every rank
         logs = self.train_metrics.result()            # device -> host: synchronises the epoch
         dt = time.perf_counter() - t0
         nsteps = self.global_step - steps0
         logs["skipped_steps"] = float(self.opt.skipped_steps - skipped0)
+        if hasattr(self.opt, "check_update"):
+            self.opt.check_update()
         if rejected0 is not None:
             # steps rejected on the device after an LSTM chain spin timeout: fail loudly
             from ..ops.lstm import check_chain

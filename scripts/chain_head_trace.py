@@ -47,27 +47,6 @@ def t4marks(ops, x, ntiles=8):
     return [[round((int(v) - t0) / 100, 1) for v in row if int(v) >= t0] for row in tr]
 
 
-def grads_trace(ops, x, a6g, nt8, dbg):
-    """lstm_chain_bwd_grads: stage timeline and per job [workgroups, first / last pass start,
-    last arrival, last reduction end] (us after the first stage started)."""
-    ubg = timeit(lambda: ops.lstm_chain_bwd_grads(*a6g))
-    tr = ops.lstm_chain_trace(x).cpu()
-    st = tr[:512].view(256, 2)
-    t0 = int(st[:6 * nt8:nt8, 0].min())
-    g = tr[768:].view(8, 256, 3)
-    jobs = []
-    for k in range(7):
-        v = g[k]
-        ok = v[:, 0] >= t0
-        if int(ok.sum()) == 0:
-            continue
-        v = v[ok]
-        jobs.append([int(ok.sum())] + [round((int(u) - t0) / 100, 1) for u in
-                                       (v[:, 0].min(), v[:, 0].max(), v[:, 1].max(), v[:, 2].max())])
-    print(json.dumps({"bwd": "chain6+grads", "dbg": dbg, "us": round(ubg, 2), "stages": stages(ops, x, 6, nt8, True),
-                      "jobs": jobs}), flush=True)
-
-
 def main():
     from gnnqc.utils.native import hip_ops
     ops = hip_ops()
@@ -119,20 +98,6 @@ def main():
           [pools[i] for i in order6], [xw[i] for i in order6], [Ts[i] for i in order6])
     ub6 = timeit(lambda: ops.lstm_chain_bwd(*a6))
     print(json.dumps({"bwd": "chain6", "us": round(ub6, 2), "stages": stages(ops, x, 6, nt8, True)}), flush=True)
-    # the same backward with the seven weight-gradient passes in the launch's spare workgroups
-    def lx(i):
-        return x if i == 0 else (outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)])
-    sinks = [[torch.zeros_like(Ws[i]), torch.zeros_like(Us[i]), torch.zeros_like(bs[i])] for i in range(7)]
-    ext = [dz4, xt, h4, Ws[6], *sinks[6]]
-    a6g = a6 + ([lx(i) for i in order6], [outs[5 * i] for i in order6], [sinks[i][0] for i in order6],
-                [sinks[i][1] for i in order6], [sinks[i][2] for i in order6], ext)
-    sync = ops.lstm_chain_sync(x)
-    for dbg in [int(v) for v in os.environ.get("GRADS_DBG", "0").split(",")]:
-        sync[16] = dbg
-        torch.cuda.synchronize()
-        grads_trace(ops, x, a6g, nt8, dbg)
-    sync[16] = 0
-    torch.cuda.synchronize()
     both = timeit(lambda: (ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e),
                            ops.time4_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg)))
     print(json.dumps({"time4_head_fwd_bwd_us": round(both, 2)}), flush=True)

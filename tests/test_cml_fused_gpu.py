@@ -148,22 +148,33 @@ def test_headed_chain_eval_metrics_match(cuda_device, cml_windows, monkeypatch):
         assert abs(a[k] - r[k]) <= 2e-3 * abs(r[k]) + 2e-3, (k, a[k], r[k])
 
 
-def test_chain_grads_role_matches_separate_passes(cuda_device, cml_windows, monkeypatch):
-    """Weight gradients computed by the chain backward's spare workgroups (in-launch passes and
-    reductions, GNNQC_CHAIN_GRADS=1) == the separate lstm_grads_multi launches; and run-to-run
-    bitwise identical (fixed-order reductions)."""
-    _, _, _, model, b = _setup(cuda_device, cml_windows)
+@pytest.mark.parametrize("B", [128, 40])
+def test_t4_chain_stage_matches_separate_launch(cuda_device, cml_windows, monkeypatch, B):
+    """time4 + head + loss as a stage of the forward chain launch (lstm_chain_head_fwd: the stage
+    pools the last chain stage's granules itself, two cells per lane) == the separate time4_head_fwd
+    launch after the chain: loss, logits, every gradient (same bf16 operands and accumulation order
+    per cell: equal up to fp contraction), no consumer spin timed out."""
+    from gnnqc.utils.native import hip_ops
+    _, _, _, model, b = _setup(cuda_device, cml_windows, B=B)
     inputs = b.model_inputs("cml")
 
-    def run(flag):
-        monkeypatch.setenv("GNNQC_CHAIN_GRADS", flag)
+    def run(on):
+        monkeypatch.setenv("GNNQC_T4_CHAIN", "1" if on else "0")
         return _grads(model, lambda: model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0))
 
-    l1, _, g1 = run("1")
-    _, _, g1b = run("1")
-    l0, _, g0 = run("0")
-    torch.testing.assert_close(l1, l0)
+    l0, z0, g0 = run(False)
+    l1, z1, g1 = run(True)
+    st = hip_ops().lstm_chain_status(z1).cpu()
+    assert int(st[2]) == 0, "a consumer spin timed out"
+    torch.testing.assert_close(z1, z0, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(l1, l0, atol=1e-6, rtol=1e-5)
     for n in g0:
-        assert torch.equal(g1[n], g1b[n]), n
         err = (g1[n] - g0[n]).norm().item()
-        assert err <= 1e-4 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())
+        assert err <= 1e-5 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())
+    with torch.no_grad():                      # evaluation (TRAIN = false kernels)
+        monkeypatch.setenv("GNNQC_T4_CHAIN", "1")
+        le1, ze1 = model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0)
+        monkeypatch.setenv("GNNQC_T4_CHAIN", "0")
+        le0, ze0 = model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0)
+    torch.testing.assert_close(ze1, ze0, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(le1, le0, atol=1e-6, rtol=1e-5)

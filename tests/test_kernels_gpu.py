@@ -591,11 +591,9 @@ def test_soilnet_gcn_fused_path_matches_eager(cuda_device, monkeypatch):
 
 @pytest.mark.parametrize("H,Din", [(16, 20), (16, 16), (32, 16), (32, 32)])
 @pytest.mark.parametrize("wgrad", [True, False])
-@pytest.mark.parametrize("pair_bwd", [True, False])
-def test_lstm_pair_fused_forward_matches_two_layers(cuda_device, monkeypatch, H, Din, wgrad, pair_bwd):
-    """lstm_tm2_fwd / lstm_tm2_bwd (layer pair, pipelined kernels) == two single layers, incl. gradients."""
+def test_lstm_pair_fused_forward_matches_two_layers(cuda_device, H, Din, wgrad):
+    """lstm_tm2_fwd (layer pair, pipelined kernel) + per-layer backward == two single layers, incl. gradients."""
     from gnnqc.ops.lstm import _HipLSTMTMPair, lstm_layer_tm
-    monkeypatch.setenv("GNNQC_PAIR_BWD", "1" if pair_bwd else "0")
     dev = cuda_device
     gen = torch.Generator().manual_seed(H * 7 + Din)
     T, M = 23, 40
@@ -722,13 +720,13 @@ def test_batch_meta_matches_torch_gather(cuda_device, cml_windows, ds):
 
 
 @pytest.mark.parametrize("use_graph", [True, False])
-@pytest.mark.parametrize("mode", ["side", "split", "pipe"])
-def test_split_lstm_backward_matches_fused(cuda_device, cml_windows, monkeypatch, use_graph, mode):
-    """Training steps with the weight-gradient passes on a side stream (graph branches when
-    captured) == the same steps with everything on one stream."""
+def test_pipe_training_steps_match_fused(cuda_device, cml_windows, monkeypatch, use_graph):
+    """Training steps with the deferred, batched weight-gradient passes (the pipe) == the same
+    steps with one fused backward kernel per layer."""
     from gnnqc import config as C
     from gnnqc.data.store import DeviceLoader, DeviceStore
     from gnnqc.models import GCNClassifier
+    from gnnqc.ops.lstm import _Pipe
     from gnnqc.ops.optim import make_optimizer
     from gnnqc.train.engine import Trainer
     pc, ws = cml_windows
@@ -736,7 +734,7 @@ def test_split_lstm_backward_matches_fused(cuda_device, cml_windows, monkeypatch
     st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
 
     def run(side):
-        monkeypatch.setenv("GNNQC_LSTM_BWD", mode if side else "fused")
+        monkeypatch.setattr(_Pipe, "enabled", bool(side))
         torch.manual_seed(0)
         model = GCNClassifier(mc, pc).to(cuda_device)
         opt = make_optimizer("adam", model.parameters(), 1e-3)
@@ -770,7 +768,7 @@ def test_pipe_lstm_backward_gradients(cuda_device, cml_windows, monkeypatch, ds)
     inputs = b.model_inputs(ds, False)
 
     def run(mode):
-        monkeypatch.setenv("GNNQC_LSTM_BWD", mode)
+        monkeypatch.setattr(_Pipe, "enabled", mode == "pipe")
         for p in model.parameters():
             p.grad = torch.zeros_like(p)
         with direct_grad_accumulation(True):

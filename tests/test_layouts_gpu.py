@@ -9,11 +9,7 @@ pytestmark = pytest.mark.gpu
 LAYOUTS = [
     # (switches of the variant, switches of both runs)
     ({"GNNQC_TM_RECDX": "0"}, {"GNNQC_CHAIN": "0"}),          # dx from weight-gradient slabs + sum
-    ({"GNNQC_LSTM_BWD": "fused"}, {"GNNQC_CHAIN": "0"}),      # recurrence, then one grads kernel per layer
-    ({"GNNQC_LSTM_BWD": "split"}, {"GNNQC_CHAIN": "0"}),      # dx kernel + weight grads on a side stream
     ({"GNNQC_POOL_FUSION": "1"}, {"GNNQC_CHAIN": "0"}),       # MaxPooling1D inside the recurrences
-    ({"GNNQC_PAIR_BWD": "1"}, {"GNNQC_CHAIN": "0"}),          # layer-pair backward kernel
-    ({"GNNQC_GRADS_SIDE": "1"}, {"GNNQC_CHAIN": "1"}),        # chain weight-gradient passes on a side stream
 ]
 
 
