@@ -46,6 +46,8 @@ def main(argv=None):
                     help="radius = the reference's rule (max_sample_distance, SURVEY 5.11.4); knn = symmetrised "
                          "k-nearest-neighbour graph (BASELINE.json's 'k=5')")
     ap.add_argument("--k", type=int, default=5, help="neighbours per node for --adjacency knn")
+    ap.add_argument("--no-knn-line", dest="knn_line", action="store_false",
+                    help="skip the second measurement on the k=5 graph (reported as 'knn5' in the JSON line)")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -81,39 +83,44 @@ def main(argv=None):
     if soil:
         pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
     ws = create_windows_dataset(pc, raw=raw)
-    store = DeviceStore(ws, "scale_range" if soil else "rolling_median", pc.graph, device=dev)
     tr = list(range(ws.n_windows))          # throughput: every window is a training window
-    loader = DeviceLoader(store, tr, args.batch, shuffle=True, seed=44, rank=rank, world_size=world,
-                          drop_last=True)
     baseline = args.model == "baseline"
-    model = (BaselineClassifier if baseline else GCNClassifier)(mc, pc).to(dev)
-    n_params = sum(p.numel() for p in model.parameters() if p.requires_grad)
-    opt = make_optimizer("adam", model.parameters(), mc.learning_rate)
-    D.broadcast_module(model)
-    trainer = Trainer(model, store, opt, calculate_weights(mc), baseline,
-                      use_graph=not args.no_graph, batch_size=args.batch)
-    rows = loader.batch_ids()                 # [n_batches, B] device tensor, no host sync while stepping
-    nb = rows.shape[0]
 
-    def run(k, start):
-        # every one of the k steps is a full training step (gather, forward, backward, guarded
-        # Adam); chunks of trainer.graph_steps of them replay one multi-step HIP graph
-        trainer.train_steps(rows, start, k)
+    def measure(graph_cfg):
+        """Build store / model / trainer for one adjacency rule, warm up, time args.steps full
+        training steps (max over ranks). Returns (seconds, trainer, loss, trainable params)."""
+        store = DeviceStore(ws, "scale_range" if soil else "rolling_median", graph_cfg, device=dev)
+        loader = DeviceLoader(store, tr, args.batch, shuffle=True, seed=44, rank=rank, world_size=world,
+                              drop_last=True)
+        torch.manual_seed(1234)
+        model = (BaselineClassifier if baseline else GCNClassifier)(mc, pc).to(dev)
+        n_params = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        opt = make_optimizer("adam", model.parameters(), mc.learning_rate)
+        D.broadcast_module(model)
+        trainer = Trainer(model, store, opt, calculate_weights(mc), baseline,
+                          use_graph=not args.no_graph, batch_size=args.batch)
+        rows = loader.batch_ids()                 # [n_batches, B] device tensor, no host sync while stepping
 
-    trainer.prepare_graphs(rows)              # graph captures happen here, never inside the timed steps
-    run(args.warmup, 0)
-    trainer._comm_events = []
-    D.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps, args.warmup)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    D.barrier()
-    dt = time.perf_counter() - t0
-    dt = D.max_over_ranks(dt)
-    loss = float(trainer.last_loss.item())
+        def run(k, start):
+            # every one of the k steps is a full training step (gather, forward, backward, guarded
+            # Adam); chunks of trainer.graph_steps of them replay one multi-step HIP graph
+            trainer.train_steps(rows, start, k)
+
+        trainer.prepare_graphs(rows)              # graph captures happen here, never inside the timed steps
+        run(args.warmup, 0)
+        trainer._comm_events = []
+        D.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(args.steps, args.warmup)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        D.barrier()
+        dt = D.max_over_ranks(time.perf_counter() - t0)
+        return dt, trainer, float(trainer.last_loss.item()), n_params
+
+    dt, trainer, loss, n_params = measure(pc.graph)
     comm_us = None
     if trainer._comm_events:             # N > 1, eager layout: HIP events around the timed all-reduces
         comm_us = 1e3 * sum(a.elapsed_time(b) for a, b in trainer._comm_events) / len(trainer._comm_events)
@@ -123,6 +130,15 @@ def main(argv=None):
         comm_us = D.max_over_ranks(comm_us)
     windows = args.steps * args.batch * world
     value = windows / dt
+    knn = None
+    if args.knn_line and args.adjacency == "radius" and not soil:
+        # BASELINE.json names the CML graph "k=5": the same measurement on the symmetrised
+        # 5-nearest-neighbour graph, reported inside the one JSON line
+        g5 = dict(pc.graph)
+        g5["adjacency"], g5["k"] = "knn", 5
+        dt5, _, loss5, _ = measure(g5)
+        knn = {"adjacency": "knn(k=5)", "value": round(windows / dt5, 2),
+               "ms_per_step": round(1000.0 * dt5 / args.steps, 4), "final_loss": round(loss5, 5)}
     if rank == 0:
         out = {
             "metric": ("train windows/sec, SoilNet GCN (diagnostic; not the headline metric)" if soil else
@@ -159,6 +175,8 @@ def main(argv=None):
                 "final_loss": round(loss, 5),
             },
         }
+        if knn is not None:
+            out["knn5"] = knn
         if comm_us is not None:
             out["allreduce_us"] = round(comm_us, 2)        # mean RCCL all-reduce of the flat gradients
             out["allreduce_mode"] = (("peer one-shot xGMI" if trainer.peer is not None else "RCCL") +

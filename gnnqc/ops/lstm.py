@@ -27,7 +27,11 @@ _ACT = {
 
 def lstm_eager(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
                return_sequences: bool = True, activation: str = "tanh") -> torch.Tensor:
-    """Reference implementation: x [M,T,Din], W [Din,4H], U [H,4H], b [4H]."""
+    """Reference implementation: x [M,T,Din], W [Din,4H], U [H,4H], b [4H]. Inside
+    :func:`gnnqc.ops.lstm_ref.kernel_rounding` it rounds where the HIP kernels do (numerics tests)."""
+    from .lstm_ref import KernelLSTM, kernel_rounding_on
+    if kernel_rounding_on() and activation == "tanh":
+        return KernelLSTM.apply(x, W, U, b, bool(return_sequences), True)
     act = _ACT[activation]
     M, T, _ = x.shape
     H = U.shape[0]

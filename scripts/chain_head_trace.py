@@ -74,6 +74,10 @@ def main():
     hc = (0.3, 0.3, 1.0, 5.0)
     us6 = timeit(lambda: ops.lstm_chain_fwd(x, Ws[:6], Us[:6], bs[:6], pools[:6], True))
     print(json.dumps({"fwd": "chain6", "us": round(us6, 2), "stages": stages(ops, x, 6, nt8)}), flush=True)
+    # time4 + head + loss as the seventh stage of the forward launch (lstm_chain_head_fwd)
+    uh = timeit(lambda: ops.lstm_chain_head_fwd(x, Ws[:6], Us[:6], bs[:6], pools[:6], True, Ws[6], Us[6], bs[6], head,
+                                                y, mask, M, *hc, e.double(), e))
+    print(json.dumps({"fwd": "chain6+time4head", "us": round(uh, 2), "stages": stages(ops, x, 7, nt8)}), flush=True)
     outs = ops.lstm_chain_fwd_pack(x, Ws[:6], Us[:6], bs[:6], pools[:6], True, Ws[6], Us[6])
     pk = outs.pop()
     up = timeit(lambda: ops.lstm_chain_fwd_pack(x, Ws[:6], Us[:6], bs[:6], pools[:6], True, Ws[6], Us[6]))

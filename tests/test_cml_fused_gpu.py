@@ -67,10 +67,13 @@ def test_headed_chain_matches_separate_kernels(cuda_device, cml_windows, monkeyp
         assert err <= 5e-3 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())
 
 
-def test_cml_default_path_matches_fp64_eager(cuda_device, cml_windows):
+def test_cml_default_path_matches_kernel_rounding_reference(cuda_device, cml_windows):
     """The benched CML step (fused GCN, headed chain, bf16 MFMA recurrences) against the same
-    model evaluated in float64 with plain PyTorch on the CPU: logits, loss, every gradient."""
+    model in float64 on the CPU with the LSTM rounded where the kernels round (bf16 MFMA operands,
+    bf16 saved gates and dz: gnnqc/ops/lstm_ref.py): logits, loss and every parameter gradient
+    within 5e-3 - rounding explains the rest, so a logic error at the percent level fails."""
     from gnnqc.data.store import DeviceStore
+    from gnnqc.ops.lstm_ref import kernel_rounding
     from gnnqc.train.loss import weighted_bce_with_logits
     pc, _, _, model, b = _setup(cuda_device, cml_windows, B=96)
     inputs = b.model_inputs("cml")
@@ -84,17 +87,22 @@ def test_cml_default_path_matches_fp64_eager(cuda_device, cml_windows):
     st = DeviceStore(ws, "rolling_median", pc.graph, device="cpu")
     bc = st.gather(torch.arange(b.y.shape[0]))
     ri = [t.double() if torch.is_tensor(t) and t.is_floating_point() else t for t in bc.model_inputs("cml")]
-    zr = ref.logits(ri)
-    lr = weighted_bce_with_logits(zr, bc.y.double(), bc.y_mask.double(), 1.0, 5.0)
-    lr.backward()
-    assert abs(loss.item() - lr.item()) <= 2e-2 * abs(lr.item()) + 1e-4, (loss.item(), lr.item())
-    assert (z.cpu().double() - zr.detach()).abs().max().item() < 5e-2
+    with kernel_rounding():
+        zr = ref.logits(ri)
+        lr = weighted_bce_with_logits(zr, bc.y.double(), bc.y_mask.double(), 1.0, 5.0)
+        lr.backward()
+    assert abs(loss.item() - lr.item()) <= 2e-3 * abs(lr.item()) + 1e-5, (loss.item(), lr.item())
+    zerr = (z.cpu().double() - zr.detach()).abs().max().item()
+    assert zerr <= 5e-3 * zr.detach().abs().max().item() + 1e-6, (zerr, zr.abs().max().item())
+    worst = {}
     for n, p in ref.named_parameters():
         if p.grad is None:
             continue
         err = (g[n].cpu().double() - p.grad).norm().item()
         scale = p.grad.norm().item()
-        assert err <= 8e-2 * scale + 1e-5, (n, err, scale)
+        worst[n] = err / (scale + 1e-12)
+        assert err <= 5e-3 * scale + 1e-6, (n, err, scale)
+    print("max relative gradient error", max(worst.values()), max(worst, key=worst.get))
 
 
 def test_chain_timeout_rejects_the_step(cuda_device, cml_windows):

@@ -1,6 +1,6 @@
 """Integrated gradients on the GPU (alpha folded into the batch, HIP chain / GCN input-gradient
-kernels, ig_interp / ig_accum / ig_finalize) against the same explainer evaluated in float64 with
-plain PyTorch on the CPU."""
+kernels, ig_interp / ig_accum / ig_finalize) against the same explainer evaluated in float64 on the
+CPU with the LSTM rounded where the kernels round (gnnqc/ops/lstm_ref.py)."""
 import copy
 
 import pytest
@@ -35,13 +35,15 @@ def test_ig_gpu_matches_fp64_cpu(cuda_device, cml_windows, negative_values):
     bc = st_cpu.gather(ids)
     for f in ("x", "anom", "adj", "node_mask"):
         setattr(bc, f, getattr(bc, f).double())
-    ref = IntegratedGradients(ref_model, "cml", m_steps=m, negative_values=negative_values).attribute(bc)
+    from gnnqc.ops.lstm_ref import kernel_rounding
+    with kernel_rounding():
+        ref = IntegratedGradients(ref_model, "cml", m_steps=m, negative_values=negative_values).attribute(bc)
 
     for k in ("grad_x", "grad_anom", "pred", "path_pred"):
         a, r = got[k].double().cpu(), ref[k]
         err = (a - r).norm().item()
         scale = r.norm().item()
-        assert err <= 6e-2 * scale + 1e-6, (k, err, scale)
+        assert err <= 6e-3 * scale + 1e-6, (k, err, scale)
     if negative_values == "keep":
         # completeness (sum of attributions ~ f(x) - f(0)) holds on the GPU as well as in fp64
         gap_g = completeness_gap(got).abs().cpu().double()

@@ -558,9 +558,14 @@ def test_gcn_node_tm_matches_eager(cuda_device, training, aggregate, F):
 
 
 def test_soilnet_gcn_fused_path_matches_eager(cuda_device, monkeypatch):
-    """SoilNet GCNClassifier: fused GCN + time-major LSTM vs the all-eager path (same weights)."""
+    """SoilNet GCNClassifier: fused GCN + time-major LSTM kernels vs the same model in float64 on
+    the CPU with the LSTM rounded where the kernels round (gnnqc/ops/lstm_ref.py): logits and
+    every gradient within 8e-3 (rounding explains the rest)."""
+    import copy
+
     from gnnqc import config as C
     from gnnqc.models import GCNClassifier
+    from gnnqc.ops.lstm_ref import kernel_rounding
     torch.manual_seed(0)
     pc = C.normalize_preproc(C.default("preprocessing_soilnet"))
     mc = C.default("model_soilnet")
@@ -571,22 +576,24 @@ def test_soilnet_gcn_fused_path_matches_eager(cuda_device, monkeypatch):
     x = torch.rand(B, T, N, 3, generator=gen).to(cuda_device) * mask[:, None, :, None]
     inputs = (x, adj, mask)
     assert model._soil_fused(inputs)
-
-    def run(eager):
-        monkeypatch.setenv("GNNQC_FORCE_EAGER", "1" if eager else "0")
-        for p in model.parameters():
-            p.grad = None
-        z = model.logits(inputs)
-        (z * mask).pow(2).sum().backward()
-        return z.detach(), {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
-
-    z1, g1 = run(False)
-    z0, g0 = run(True)
+    ref = copy.deepcopy(model).cpu().double()
+    for p in model.parameters():
+        p.grad = None
+    z1 = model.logits(inputs)
+    (z1 * mask).pow(2).sum().backward()
+    g1 = {k: p.grad.detach().double().cpu() for k, p in model.named_parameters() if p.grad is not None}
+    ri = [t.double().cpu() for t in inputs]
+    with kernel_rounding():
+        z0 = ref.logits(ri)
+        (z0 * ri[2]).pow(2).sum().backward()
+    g0 = {k: p.grad.detach() for k, p in ref.named_parameters() if p.grad is not None}
+    z1 = z1.detach().double().cpu()
     assert z1.shape == z0.shape == (B, N)
-    assert (z1 - z0).norm().item() < 3e-2 * z0.norm().item()
+    assert (z1 - z0.detach()).norm().item() < 3e-3 * z0.norm().item()
     assert set(g1) == set(g0)
     for k in g0:
-        assert (g1[k] - g0[k]).norm().item() < 8e-2 * (g0[k].norm().item() + 1e-6), k
+        err = (g1[k] - g0[k]).norm().item()
+        assert err < 8e-3 * (g0[k].norm().item() + 1e-6), (k, err, g0[k].norm().item())
 
 
 @pytest.mark.parametrize("H,Din", [(16, 20), (16, 16), (32, 16), (32, 32)])
