@@ -14,7 +14,10 @@
 //             dh_{T-1} of time4 in LDS and writes the tile's weight-gradient record; the
 //             workgroup holding the last ticket sums the records in tile order and adds them to
 //             the gradients.
-// 512 threads (8 waves); a thread owns unit j = tid & 63 of rows w = tid >> 6 and w + 8.
+// 512 threads (8 waves); a thread owns unit j = tid & 63 of rows w = tid >> 6 and w + 8. The
+// backward also runs in 1024-thread workgroups (the chain backward launch): there tid is taken
+// modulo 512, so waves 8..15 repeat waves 0..7's work - the same values to the same LDS / global
+// addresses - and join every barrier; counter atomics stay with thread 0 alone.
 // The products run on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32: lane l holds A[l&15][k=l>>4]
 // and B[k=l>>4][l&15], D[4(l>>4)+j][l&15]): one output per thread on the FMA pipes needed two
 // LDS reads per multiply-add (13 us forward / 23 us backward per tile, measured). Weights come
@@ -72,11 +75,13 @@ __device__ __forceinline__ float ch_leaky(float z, float a) { return z > 0.f ? z
 __device__ __forceinline__ float ch_dleaky(float z, float a) { return z > 0.f ? 1.f : a; }
 
 // Sum of mask[0..M) over the workgroup (red: CH_NW floats of LDS). Contains a barrier.
+__device__ __forceinline__ int ch_tid() { return threadIdx.x & (64 * CH_NW - 1); }
+
 __device__ __forceinline__ float ch_mask_sum(const float* __restrict__ mask, int M, float* red) {
   float s = 0.f;
-  for (int i = threadIdx.x; i < M; i += 64 * CH_NW) s += mask[i];
+  for (int i = ch_tid(); i < M; i += 64 * CH_NW) s += mask[i];
   s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  if ((threadIdx.x & 63) == 0) red[ch_tid() >> 6] = s;
   __syncthreads();
   float t = 0.f;
 #pragma unroll
@@ -128,19 +133,20 @@ __device__ __forceinline__ void ch_put(float* part, int lp, int ot, const ch_f4&
 template <int F>
 __device__ __forceinline__ void ch_stage_weights(const ChainHead& hd, float* sW1, float* sW2) {
   constexpr int N1 = F * CH_HU / 4, N2 = CH_HU * CH_HU / 4, NT = 64 * CH_NW;
+  const int tid = ch_tid();
   float4 v1[(N1 + NT - 1) / NT], v2[(N2 + NT - 1) / NT];
 #pragma unroll
-  for (int i = 0; i < (N1 + NT - 1) / NT; ++i) v1[i] = reinterpret_cast<const float4*>(hd.W1)[min((int)threadIdx.x + NT * i, N1 - 1)];
+  for (int i = 0; i < (N1 + NT - 1) / NT; ++i) v1[i] = reinterpret_cast<const float4*>(hd.W1)[min(tid + NT * i, N1 - 1)];
 #pragma unroll
-  for (int i = 0; i < (N2 + NT - 1) / NT; ++i) v2[i] = reinterpret_cast<const float4*>(hd.W2)[min((int)threadIdx.x + NT * i, N2 - 1)];
+  for (int i = 0; i < (N2 + NT - 1) / NT; ++i) v2[i] = reinterpret_cast<const float4*>(hd.W2)[min(tid + NT * i, N2 - 1)];
 #pragma unroll
   for (int i = 0; i < (N1 + NT - 1) / NT; ++i) {
-    const int e = 4 * ((int)threadIdx.x + NT * i);
+    const int e = 4 * (tid + NT * i);
     *reinterpret_cast<float4*>(sW1 + (e / CH_HU) * CH_WP + e % CH_HU) = v1[i];
   }
 #pragma unroll
   for (int i = 0; i < (N2 + NT - 1) / NT; ++i) {
-    const int e = 4 * ((int)threadIdx.x + NT * i);
+    const int e = 4 * (tid + NT * i);
     *reinterpret_cast<float4*>(sW2 + (e / CH_HU) * CH_WP + e % CH_HU) = v2[i];
   }
   __syncthreads();
@@ -153,7 +159,7 @@ template <int F>
 __device__ __forceinline__ void ch_head_z2(const ChainHead& hd, const float* sW1, const float* sW2, const float* hl,
                                            float* part, float* sz1, float* sa1, float z2[2]) {
   constexpr int HLP = F + 4, PT = 16 * CH_AP;
-  const int tid = threadIdx.x, w = tid >> 6, j = tid & 63;
+  const int tid = ch_tid(), w = tid >> 6, j = tid & 63;
   const int ot = w & 3, kh = w >> 2;                // output tile, K half
   const float b1j = hd.b1[j], b2j = hd.b2[j];
   ch_put(part + kh * PT, CH_AP, ot, ch_mm_wk<F / 8>(sW1, CH_WP, ot, kh * (F / 2), hl, HLP));
@@ -265,8 +271,8 @@ struct ChainHeadBwdLds {
 // hd.gpart[tile], then the tile's arrival is counted in hd.ticket (chain_head_bwd_reduce waits
 // for all of them).
 template <int F>
-__device__ void chain_head_bwd(const ChainHead& hd, const float* __restrict__ hT, int tile, int ntiles, float* dh,
-                               char* scratch) {
+__device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* __restrict__ hT, int tile, int ntiles,
+                                               float* dh, char* scratch) {
   constexpr int HLP = F + 4, PT = 16 * CH_AP;
   using Rec = ChainHeadRec<F>;
   float* sh = reinterpret_cast<float*>(scratch);     // [16][HLP]
@@ -280,7 +286,7 @@ __device__ void chain_head_bwd(const ChainHead& hd, const float* __restrict__ hT
   float* sW1 = misc + 32;                            // [F][CH_WP]
   float* sW2 = sW1 + F * CH_WP;                      // [64][CH_WP]
   ch_stage_weights<F>(hd, sW1, sW2);
-  const int tid = threadIdx.x, w = tid >> 6, j = tid & 63;
+  const int tid = ch_tid(), w = tid >> 6, j = tid & 63;
   const int l = tid & 63, lm = l & 15, lq = l >> 4;
   const int row0 = tile * 16;
   for (int e = tid; e < 16 * F / 4; e += 64 * CH_NW) {
@@ -341,21 +347,21 @@ __device__ void chain_head_bwd(const ChainHead& hd, const float* __restrict__ hT
   };
   float* rec = hd.gpart + (size_t)tile * Rec::PITCH;
   float* rec2 = rec + F * CH_HU + CH_HU;
-#pragma unroll
-  for (int q = 0; q < F / 16 * 4 / CH_NW; ++q) {      // dW1 [F][64]: (F/16) x 4 tiles
-    const int t = w + CH_NW * q, it = t >> 2, jt = t & 3;
+  // the record tiles are spread over ALL waves of the workgroup (8 or 16), each stored once
+  const int wa = threadIdx.x >> 6, nwa = blockDim.x >> 6;
+  for (int t = wa; t < F / 16 * 4; t += nwa) {        // dW1 [F][64]: (F/16) x 4 tiles
+    const int it = t >> 2, jt = t & 3;
     const ch_f4 acc = wgrad(sh, HLP, it, sdz1, jt);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ch_st(rec + (16 * it + 4 * lq + k) * CH_HU + 16 * jt + lm, acc[k]);
   }
-#pragma unroll
-  for (int q = 0; q < 16 / CH_NW; ++q) {              // dW2 [64][64]: 16 tiles
-    const int t = w + CH_NW * q, it = t >> 2, jt = t & 3;
+  for (int t = wa; t < 16; t += nwa) {                // dW2 [64][64]: 16 tiles
+    const int it = t >> 2, jt = t & 3;
     const ch_f4 acc = wgrad(sa1, CH_AP, it, sz2, jt);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ch_st(rec2 + (16 * it + 4 * lq + k) * CH_HU + 16 * jt + lm, acc[k]);
   }
-  if (tid < CH_HU) {
+  if (threadIdx.x < CH_HU) {
     float s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) {
@@ -366,7 +372,7 @@ __device__ void chain_head_bwd(const ChainHead& hd, const float* __restrict__ hT
     ch_st(rec + F * CH_HU + j, s1);                             // db1
     ch_st(rec2 + CH_HU * CH_HU + j, s2);                        // db2
     ch_st(rec2 + CH_HU * CH_HU + CH_HU + j, s3);                // dW3
-  } else if (tid == CH_HU) {
+  } else if (threadIdx.x == CH_HU) {
     float s = 0.f;
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) s += misc[rr];
@@ -375,7 +381,7 @@ __device__ void chain_head_bwd(const ChainHead& hd, const float* __restrict__ hT
   // (sc1 stores, every wave's vmcnt(0), barrier, one lane's counter add: no fence)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add(hd.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(hd.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // After chain_head_bwd: once every tile's record is in (ticket == ntiles; the workgroups of the
@@ -384,7 +390,7 @@ __device__ void chain_head_bwd(const ChainHead& hd, const float* __restrict__ hT
 // it to the gradients; the last one to finish re-arms both counters. One workgroup reducing all
 // of it took ~60 us (25 rounds of 8 dependent-latency loads per thread).
 template <int F>
-__device__ void chain_head_bwd_reduce(const ChainHead& hd, int tile, int ntiles) {
+__device__ __forceinline__ void chain_head_bwd_reduce(const ChainHead hd, int tile, int ntiles) {
   using Rec = ChainHeadRec<F>;
   __shared__ int bad;
   if (threadIdx.x == 0) {

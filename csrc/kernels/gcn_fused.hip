@@ -19,37 +19,9 @@
 // every workgroup maps its own partial sums to dW, dgamma, dbeta, dalpha contributions and adds them
 // with float atomics: no partial-record workspace and no finalize launch (not bitwise
 // reproducible: the deterministic mode keeps the generic path).
-#include "common.h"
+#include "gcn_fused.h"
 
 namespace gq {
-
-int* chain_ctl(int dev);   // lstm_chain.hip: word 7 = a gradient producer saw a non-finite value
-
-constexpr int GF_MAX_CIN = 4;
-constexpr int GF_ROW_MAX = 128;        // N * Cin floats per staged row
-constexpr int GF_RPP = 64;             // rows per pass (4 threads per row, 256 threads)
-
-struct GfData {                        // the resident window store (gnnqc.data.store.DeviceStore)
-  const float* series;                 // [G][Ttot][N][C]
-  const float* shift;                  // [G][Tn][N][C]
-  const float* scale;
-  const long* wg;                      // window -> group
-  const long* wc;                      // window -> centre time index
-  const uint8_t* wv;                   // [nwin][N] node valid
-  const float* wlab;                   // [nwin] label
-  const long* gap;                     // [G] flagged node position
-  const double* mom;                   // [nwin][nstat] (gcn_window_prep)
-  const float* pw;                     // [nwin][N]
-  const long* wids;                    // [B] ids, or
-  const long* table;                   // [nrows][B] + cursor
-  const long* cursor;
-  long nrows;
-  int Ttot, Tn, N, tb, T, time_norm;
-};
-
-__device__ __forceinline__ const long* gf_ids(const GfData& D, int B) {
-  return D.cursor != nullptr ? D.table + (D.cursor[0] % D.nrows) * B : D.wids;
-}
 
 // ---- per-window precompute: one workgroup per window
 template <int Cin>
@@ -133,39 +105,6 @@ __global__ __launch_bounds__(256) void gcn_window_prep_kernel(GfData D, const fl
   }
   __syncthreads();
   if (tid < nstat) mom[(long)w * nstat + tid] = (dred[0][tid] + dred[1][tid]) + (dred[2][tid] + dred[3][tid]);
-}
-
-// ---- step kernels. A workgroup owns `rows` consecutive steps of ONE sample's window. Every load
-// of a pass is issued before the first wait (the slab of series values, the node tables, the
-// parameters, the batch's moment records, the upstream gradient): one memory round trip after the
-// id -> window chain, instead of one per dependent stage.
-constexpr int GF_SLAB = 4096;          // floats of series staged per pass (16 per thread)
-constexpr int GF_SPT = GF_SLAB / 256;
-
-__device__ __forceinline__ int gf_rows_per_pass(int NC) { return min(GF_RPP, GF_SLAB / NC); }
-
-// issue the loads of rows [t0, t0 + nr) of a window (contiguous NC floats per row) into registers
-__device__ __forceinline__ void gf_slab_load(const float* __restrict__ src, int n, float (&v)[GF_SPT]) {
-#pragma unroll
-  for (int u = 0; u < GF_SPT; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    v[u] = i < n ? src[i] : 0.f;
-  }
-}
-
-// normalise the loaded values into sx[n] (element i: node (i % NC) / Cin, channel i % Cin)
-template <int Cin>
-__device__ __forceinline__ void gf_slab_park(const float (&v)[GF_SPT], int n, int NC, const float* svm,
-                                             const float* ssh, const float* ssc, float* sx) {
-  int e = threadIdx.x % NC;
-  const int step = 256 % NC;
-#pragma unroll
-  for (int u = 0; u < GF_SPT; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    if (i < n) sx[i] = (v[u] - ssh[e]) * ssc[e] * svm[e / Cin];
-    e += step;
-    if (e >= NC) e -= NC;
-  }
 }
 
 // ---- forward: grid (Mp, NY), 256 threads
@@ -351,155 +290,12 @@ __global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
   }
 }
 
-// ---- backward (training): grid (B, NY), 256 threads; parameter gradients added with float atomics
+// ---- backward (training): grid (B, NY), 256 threads (body in gcn_fused.h: it also runs as extra
+// workgroups of the LSTM weight-gradient launch, lstm_tm.hip lstm_grads_multi)
 template <int Cin, int F>
-__global__ __launch_bounds__(256) void gcn_fused_bwd_kernel(
-    GfData D, int B, int Mp, int Dh, int c_off, int rows, const float* __restrict__ dh,
-    const double* __restrict__ Sg, const float* __restrict__ st, const float* __restrict__ W,
-    const float* __restrict__ bias, const float* __restrict__ alpha, float* __restrict__ dW,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dalpha, int* __restrict__ nf) {
-  constexpr int FQ = F / 4;
-  constexpr int NA = 3 + Cin;
-  const int b = blockIdx.x, tid = threadIdx.x, N = D.N, T = D.T;
-  const int t0 = blockIdx.y * rows, t1 = min(T, t0 + rows);
-  __shared__ float svm[GF_ROW_MAX], spw[GF_ROW_MAX], ssh[GF_ROW_MAX], ssc[GF_ROW_MAX];
-  __shared__ __attribute__((aligned(16))) float sx[GF_SLAB];
-  __shared__ float red[4][NA][F];
-  const int NC = N * Cin;
-  const int RP = gf_rows_per_pass(NC);
-  const int r = tid >> 2, q = tid & 3, f0 = q * FQ;
-  // ---- phase A: all loads (the upstream gradient and the parameters do not depend on the ids)
-  float gv[FQ];
-  {
-    const int t = t0 + r;
-    const float* dr = dh + ((long)min(t, T - 1) * Mp + b) * Dh + c_off + f0;
-#pragma unroll
-    for (int j = 0; j < FQ; ++j) gv[j] = (r < min(RP, t1 - t0)) ? dr[j] : 0.f;
-  }
-  float wk[Cin][FQ], bb[FQ], sc[FQ], sh[FQ], al[FQ];
-#pragma unroll
-  for (int j = 0; j < FQ; ++j) {
-    const int f = f0 + j;
-#pragma unroll
-    for (int k = 0; k < Cin; ++k) wk[k][j] = W[k * F + f];
-    bb[j] = bias[f];
-    sc[j] = st[2 * F + f];
-    sh[j] = st[3 * F + f];
-    al[j] = alpha[f];
-  }
-  const long* ids = gf_ids(D, B);
-  const long wraw = ids[b];
-  if (wraw < 0) return;                           // padding sample: no contribution (uniform exit)
-  const long w = wraw;
-  const long g = D.wg[w], c0 = D.wc[w];
-  const long tn = D.time_norm ? c0 : 0;
-  float nv = 0.f, npw = 0.f, nsh = 0.f, nsc = 0.f;
-  if (tid < N) {
-    nv = D.wv[w * N + tid] ? 1.f : 0.f;
-    npw = D.pw[w * N + tid];
-  }
-  if (tid < NC) {
-    nsh = D.shift[(g * D.Tn + tn) * (long)NC + tid];
-    nsc = D.scale[(g * D.Tn + tn) * (long)NC + tid];
-  }
-  float v[GF_SPT];
-  const float* src = D.series + (g * D.Ttot + (c0 - D.tb)) * (long)NC;
-  int nr = min(RP, t1 - t0);
-  gf_slab_load(src + (long)t0 * NC, nr * NC, v);
-  // ---- phase B
-  if (tid < N) {
-    svm[tid] = nv;
-    spw[tid] = npw;
-  }
-  if (tid < NC) {
-    ssh[tid] = nsh;
-    ssc[tid] = nsc;
-  }
-  __syncthreads();
-  gf_slab_park<Cin>(v, nr * NC, NC, svm, ssh, ssc, sx);
-  __syncthreads();
-  float acc[NA][FQ];
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-#pragma unroll
-    for (int j = 0; j < FQ; ++j) acc[a][j] = 0.f;
-  for (int p0 = t0; p0 < t1; p0 += RP) {
-    if (p0 != t0) {
-      nr = min(RP, t1 - p0);
-      gf_slab_load(src + (long)p0 * NC, nr * NC, v);
-      __syncthreads();
-      gf_slab_park<Cin>(v, nr * NC, NC, svm, ssh, ssc, sx);
-      __syncthreads();
-      if (r < nr) {
-        const float* dr = dh + ((long)(p0 + r) * Mp + b) * Dh + c_off + f0;
-#pragma unroll
-        for (int j = 0; j < FQ; ++j) gv[j] = dr[j];
-      }
-    }
-    if (r < nr) {
-      const float* xr = sx + r * NC;
-      for (int n = 0; n < N; ++n) {
-        const float wn = spw[n];                  // 0 for masked / unpooled nodes: no contribution
-        float xv[Cin];
-#pragma unroll
-        for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
-#pragma unroll
-        for (int j = 0; j < FQ; ++j) {
-          float z = bb[j];
-#pragma unroll
-          for (int k = 0; k < Cin; ++k) z += xv[k] * wk[k][j];
-          const float yv = z * sc[j] + sh[j];
-          const float da = wn * gv[j];
-          const bool pos = yv > 0.f;
-          const float dy = pos ? da : al[j] * da;
-          acc[0][j] += dy;
-          acc[1][j] += dy * z;
-          acc[2][j] += pos ? 0.f : da * yv;
-#pragma unroll
-          for (int k = 0; k < Cin; ++k) acc[3 + k][j] += xv[k] * dy;
-        }
-      }
-    }
-  }
-  // reduce over the workgroup's rows: lanes with equal q (stride 4) inside the wave, then 4 waves
-  const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-#pragma unroll
-    for (int j = 0; j < FQ; ++j) {
-      float x = acc[a][j];
-#pragma unroll
-      for (int o = 32; o >= 4; o >>= 1) x += __shfl_xor(x, o, 64);
-      if (lane < 4) red[wv][a][lane * FQ + j] = x;
-    }
-  __syncthreads();
-  if (tid >= F) return;
-  const int f = tid;
-  float tot[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) tot[a] = (red[0][a][f] + red[1][a][f]) + (red[2][a][f] + red[3][a][f]);
-  // the closed form of gcn_glue.hip gcn_bwd_finalize_kernel (training), applied to this partial
-  const float mu = st[f], inv = st[F + f], scf = st[2 * F + f];
-  const float A = tot[0], Z = tot[1], P = tot[2];
-  const float dg = inv * (Z - mu * A);
-  bool fin = isfinite(A) && isfinite(dg) && isfinite(P);
-  atomicAdd(dbeta + f, A);
-  atomicAdd(dgamma + f, dg);
-  atomicAdd(dalpha + f, P);
-  const double n = fmax(Sg[Cin + Cin * Cin], 1.0);
-  const double bf = bias[f];
-#pragma unroll
-  for (int k = 0; k < Cin; ++k) {
-    double s2w = 0.0;
-#pragma unroll
-    for (int l = 0; l < Cin; ++l) s2w += Sg[Cin + k * Cin + l] * (double)W[l * F + f];
-    const double s1 = Sg[k];
-    const double sxx = inv * (s2w + s1 * (bf - mu));
-    const float d = (float)(scf * (tot[3 + k] - s1 * A / n - sxx * dg / n));
-    fin = fin && isfinite(d);
-    atomicAdd(dW + k * F + f, d);
-  }
-  if (!fin) __hip_atomic_store(nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__global__ __launch_bounds__(256) void gcn_fused_bwd_kernel(GcnBwdJob J) {
+  __shared__ __attribute__((aligned(16))) char smem[GcnBwdLds<Cin, F>::BYTES];
+  gcn_fused_bwd_body<Cin, F>(J, blockIdx.x, blockIdx.y, smem);
 }
 
 // ------------------------------------------------------------------ host
@@ -654,8 +450,55 @@ std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor
   return {out, S, st, y, ym, wid};
 }
 
-// Training backward: adds dW, dgamma, dbeta, dalpha (float atomics) from dh [T, Mp, Dh] channels
-// [c_off, c_off + F). (db is zero in training: BatchNorm removes the bias.)
+// The training backward's job (gcn_fused_bwd_body): adds dW, dgamma, dbeta, dalpha (float atomics)
+// from dh [T, Mp, Dh] channels [c_off, c_off + F). (db is zero in training: BatchNorm removes the
+// bias.) nblocks = B * ny workgroups (0: nothing to do). Shared with lstm_grads_multi (lstm_tm.hip).
+GcnBwdJob gcn_bwd_job(const at::Tensor& dh, int64_t c_off, const at::Tensor& series, const at::Tensor& shift,
+                      const at::Tensor& scale, const at::Tensor& win_group, const at::Tensor& win_center,
+                      const at::Tensor& win_valid, const at::Tensor& group_anom_pos, const at::Tensor& pw,
+                      const at::Tensor& wids, const at::Tensor& table, const c10::optional<at::Tensor>& cursor,
+                      int64_t tb, int64_t seq_len, bool time_norm, const at::Tensor& S, const at::Tensor& st,
+                      const at::Tensor& W, const at::Tensor& bias, const at::Tensor& alpha, const at::Tensor& dW,
+                      const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dalpha, int& nblocks) {
+  int B = 0;
+  const at::Tensor e = series.new_zeros(0);
+  GcnBwdJob J{};
+  J.D = gf_data(series, shift, scale, win_group, win_center, win_valid, e, group_anom_pos, e, pw, wids, table, cursor,
+                tb, seq_len, time_norm, B);
+  check_f32_cuda(dh, "dh");
+  for (const at::Tensor* t : {&st, &W, &bias, &alpha, &dW, &dgamma, &dbeta, &dalpha})
+    check_f32_cuda(*t, "gcn_fused_bwd operand");
+  const int C = (int)series.size(3), F = (int)W.size(1);
+  TORCH_CHECK(C >= 1 && C <= GF_MAX_CIN && (F == 8 || F == 16 || F == 32), "gcn_fused_bwd: 1..4 input, 8/16/32 output channels");
+  TORCH_CHECK(S.is_cuda() && S.scalar_type() == at::kDouble && S.numel() == C + C * C + 1, "gcn_fused_bwd: S");
+  TORCH_CHECK(dh.dim() == 3 && dh.size(0) == seq_len && dh.size(1) >= B && dh.size(2) >= c_off + F,
+              "gcn_fused_bwd: dh [T, Mp, Dh]");
+  TORCH_CHECK(dW.numel() == (long)C * F && dgamma.numel() == F && dbeta.numel() == F && dalpha.numel() == F &&
+                  st.numel() == 4 * F, "gcn_fused_bwd: gradient shapes");
+  int ny, rows;
+  gf_grid((int)seq_len, J.D.N * C, ny, rows);
+  J.B = B;
+  J.Mp = (int)dh.size(1);
+  J.Dh = (int)dh.size(2);
+  J.c_off = (int)c_off;
+  J.rows = rows;
+  J.ny = ny;
+  J.key = C * 64 + F;
+  J.dh = dh.data_ptr<float>();
+  J.Sg = S.data_ptr<double>();
+  J.st = st.data_ptr<float>();
+  J.W = W.data_ptr<float>();
+  J.bias = bias.data_ptr<float>();
+  J.alpha = alpha.data_ptr<float>();
+  J.dW = dW.data_ptr<float>();
+  J.dgamma = dgamma.data_ptr<float>();
+  J.dbeta = dbeta.data_ptr<float>();
+  J.dalpha = dalpha.data_ptr<float>();
+  J.nf = chain_ctl(series.get_device()) + 7;
+  nblocks = B * ny;
+  return J;
+}
+
 void gcn_fused_bwd(const at::Tensor& dh, int64_t c_off, const at::Tensor& series, const at::Tensor& shift,
                    const at::Tensor& scale, const at::Tensor& win_group, const at::Tensor& win_center,
                    const at::Tensor& win_valid, const at::Tensor& group_anom_pos, const at::Tensor& pw,
@@ -663,29 +506,15 @@ void gcn_fused_bwd(const at::Tensor& dh, int64_t c_off, const at::Tensor& series
                    int64_t seq_len, bool time_norm, const at::Tensor& S, const at::Tensor& st, const at::Tensor& W,
                    const at::Tensor& bias, const at::Tensor& alpha, at::Tensor dW, at::Tensor dgamma, at::Tensor dbeta,
                    at::Tensor dalpha) {
-  int B = 0;
-  const at::Tensor e = series.new_zeros(0);
-  GfData D = gf_data(series, shift, scale, win_group, win_center, win_valid, e, group_anom_pos, e, pw, wids, table,
-                     cursor, tb, seq_len, time_norm, B);
-  check_f32_cuda(dh, "dh");
-  for (const at::Tensor* t : {&st, &W, &bias, &alpha, (const at::Tensor*)&dW, (const at::Tensor*)&dgamma,
-                              (const at::Tensor*)&dbeta, (const at::Tensor*)&dalpha})
-    check_f32_cuda(*t, "gcn_fused_bwd operand");
-  const int C = (int)series.size(3), F = (int)W.size(1);
-  TORCH_CHECK(S.is_cuda() && S.scalar_type() == at::kDouble && S.numel() == C + C * C + 1, "gcn_fused_bwd: S");
-  TORCH_CHECK(dh.dim() == 3 && dh.size(0) == seq_len && dh.size(1) >= B && dh.size(2) >= c_off + F,
-              "gcn_fused_bwd: dh [T, Mp, Dh]");
-  TORCH_CHECK(dW.numel() == (long)C * F && dgamma.numel() == F && dbeta.numel() == F && dalpha.numel() == F &&
-                  st.numel() == 4 * F, "gcn_fused_bwd: gradient shapes");
   c10::DeviceGuard guard(series.device());
-  int ny, rows;
-  gf_grid((int)seq_len, D.N * C, ny, rows);
-  if (B > 0)
-    GQ_GF_CIN(C, GQ_GF_F(F, hipLaunchKernelGGL((gcn_fused_bwd_kernel<CIN, FF>), dim3(B, ny), dim3(256), 0, stream(),
-        D, B, (int)dh.size(1), (int)dh.size(2), (int)c_off, rows, dh.data_ptr<float>(), S.data_ptr<double>(),
-        st.data_ptr<float>(), W.data_ptr<float>(), bias.data_ptr<float>(), alpha.data_ptr<float>(),
-        dW.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dalpha.data_ptr<float>(),
-        chain_ctl(series.get_device()) + 7)));
+  int nb = 0;
+  const GcnBwdJob J = gcn_bwd_job(dh, c_off, series, shift, scale, win_group, win_center, win_valid, group_anom_pos,
+                                  pw, wids, table, cursor, tb, seq_len, time_norm, S, st, W, bias, alpha, dW, dgamma,
+                                  dbeta, dalpha, nb);
+  const int C = (int)series.size(3), F = (int)W.size(1);
+  if (nb > 0)
+    GQ_GF_CIN(C, GQ_GF_F(F, hipLaunchKernelGGL((gcn_fused_bwd_kernel<CIN, FF>), dim3(J.B, J.ny), dim3(256), 0,
+                                               stream(), J)));
   GQ_LAUNCH_CHECK();
 }
 

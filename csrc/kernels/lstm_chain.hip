@@ -34,6 +34,8 @@
 #include "lstm_grads_body.h"
 #include "lstm_tm_common.h"
 
+#include <cstdlib>
+
 namespace gq {
 
 static constexpr int CHAIN_MAX = 8;
@@ -67,6 +69,7 @@ struct ChainStage {
   unsigned* iout;
   float* pin_out;                    // PIN > 1: the pooled input [T][Mp][Din] + argmax bytes,
   unsigned char* pin_idx;            //   written here (the producer publishes unpooled h)
+  long long* prof;                   // profiling (GNNQC_CHAIN_PROF=1): tile 0's per-step phase clocks
   int H, T, Din, Dw, KX, P, PIN;
 };
 
@@ -130,6 +133,21 @@ __device__ __noinline__ unsigned long long chain_wait(const unsigned long long* 
   __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return v;
 }
+
+// Per-step phase clocks of tile 0 (s_memtime: shader clock ticks) into pr[step][8] for the first
+// CHAIN_PROF_STEPS steps; pr is workgroup-uniform (nullptr: off). Compiled in only with
+// -DGQ_CHAIN_PROF (GNNQC_CHAIN_PROF_BUILD=1 at build time): even when off, the marks' clock reads
+// and conditional stores kept the compiler from overlapping the step phases (chain forward 107 ->
+// 131 us, backward 124 -> 155 us, measured).
+static constexpr int CHAIN_PROF_STEPS = 64;
+#ifdef GQ_CHAIN_PROF
+__device__ __forceinline__ void chain_mark(long long* pr, int step, int k) {
+  if (pr != nullptr && threadIdx.x == 0 && step < CHAIN_PROF_STEPS)
+    pr[step * 8 + k] = (long long)__builtin_amdgcn_s_memtime();
+}
+#else
+__device__ __forceinline__ void chain_mark(long long*, int, int) {}
+#endif
 
 // Tag base of a launch: (epoch mod (2^20 - 1)) + 1 in the high 20 bits of the 32-bit tag, the
 // time index (< 4096) in the low 12. Never 0, so a zeroed granule (fresh or reused memory)
@@ -280,12 +298,14 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   for (int cc = 0; cc < CPL; ++cc) c[cc] = 0.f;
   __syncthreads();
 
+  long long* pr = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
   for (int t0 = 0; t0 <= T; t0 += D) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       const int t = t0 + j;
       const int p = t & 1;
       const int jn = (j + 1 == D) ? 0 : j + 1;
+      chain_mark(pr, t, 0);
       {
         const int ts = (t >= 1 && t <= T) ? t - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
@@ -315,8 +335,10 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         }
         acc[cc] = accx + acch;
       }
+      chain_mark(pr, t, 1);
       stage_x(p ^ 1, jn, min(t + 1, T - 1));
       load_x(jn, min(t + 1 + D, T - 1));
+      chain_mark(pr, t, 2);
 #pragma unroll
       for (int cc = 0; cc < CPL; ++cc) {
         const float iv = sigmoidf_fast(acc[cc][0]);
@@ -334,7 +356,9 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
           S.c[o] = c[cc];
         }
       }
+      chain_mark(pr, t, 3);
       lds_barrier();
+      chain_mark(pr, t, 4);
     }
   }
 }
@@ -588,7 +612,23 @@ struct ChainBStage {
   unsigned long long* sout;          // tagged dx stream [T+1][Mp][Din] (nullptr: last stage)
   float* dx;                         // last stage: fp32 dx [T][Mp][Din]
   long long* trace_mid;              // profiling: time the step loop starts
+  long long* prof;                   // profiling (GNNQC_CHAIN_PROF=1): tile 0's per-step phase clocks
   int H, T, Din, Dw, KX, P, Ts;
+};
+
+// time4's backward (with the head backward and the loss gradient as its prologue) as the first
+// stage of the backward launch (lstm_chain_head_bwd): it publishes dx - the gradient of the
+// chain's pooled top output - as granules, so the top chain stage starts after time4's first
+// reverse step instead of after the whole time4_head_bwd launch (~26 us).
+struct ChainT4B {
+  const float* h;                    // time4's h [T][Mp][128] (h_{T-1} feeds the head)
+  const float* g;                    // saved gates, fp32 (time4_head.hip t4_sidx layout)
+  const float* c;                    // saved (c_t, c_{t-1})
+  const bf16x8_t* pk;                // the forward's fragment image of (W, U) (lstm_chain_head_fwd)
+  __bf16* dz;                        // [T+1][Mp][512] bf16 (the weight-gradient pass's input)
+  unsigned long long* sout;          // dx granule stream [T][Mp][Din]
+  int T, Din, Dw, on;
+  ChainHead hd;
 };
 
 struct ChainBArgs {
@@ -596,6 +636,7 @@ struct ChainBArgs {
   int ns, ntiles, nt8, Mp;
   int* ctl;
   long long* trace;
+  ChainT4B t4;                       // t4.on: blocks [ns nt8, (ns + 1) nt8) run time4's backward
 };
 
 template <int H, int KX>
@@ -607,7 +648,36 @@ struct ChainBLds {
   static constexpr int WB = WL ? 2 * KX * 16 * (4 * H + 8) * 2 : 0;
   static constexpr int BYTES = ZS + DH + DX + WB;
 };
-static constexpr int CHAINB_LDS = ChainBLds<64, 2>::BYTES;
+// H >= 32 stages split the two per-step products over K (chain_bwd_stage, SK): every wave runs a
+// full 16-row MFMA tile of dh_rec^T = U dz^T / dx^T = W dz^T over a K slice and the partial tiles
+// meet in LDS (dpart / xpart, a second barrier per step). The one-tile-per-wave layout (each wave
+// owning its own four units: 12 of every 16 A rows zero) issued 4x the MFMAs and made those stages
+// MFMA-pipe bound (H = 64: ~0.4 us of a 1.3 us step in the products alone, measured).
+template <int H, int KX>
+struct ChainBLdsSK {
+  static constexpr int NW = TMC<H>::NW, UT = H / 16, KG = NW / UT, NXB = 2 * KX, KXG = NW / NXB;
+  static constexpr int ZS = 2 * 16 * (4 * H + 8) * 2;
+  static constexpr int DH = 2 * 16 * TMC<H>::HP * 4;
+  static constexpr int DP = KG * 16 * TMC<H>::HP * 4;
+  static constexpr int XPP = 32 * KX + 4;              // xpart row pitch
+  static constexpr int XP = 2 * KXG * 16 * XPP * 4;
+  static constexpr int BYTES = ZS + DH + DP + XP;
+};
+constexpr int chainb_max(int a, int b) { return a > b ? a : b; }
+static constexpr int CHAINB_LDS_STAGE =
+    chainb_max(chainb_max(ChainBLds<64, 2>::BYTES, ChainBLdsSK<64, 1>::BYTES),
+               chainb_max(ChainBLdsSK<64, 2>::BYTES, chainb_max(ChainBLdsSK<32, 1>::BYTES, ChainBLdsSK<32, 2>::BYTES)));
+
+struct ChainT4BLds {
+  static constexpr int DHT = 16 * 132 * 4;                 // dh_{T-1} from the head
+  static constexpr int ZS = 16 * (512 + 8) * 2;            // bf16 dz tile
+  static constexpr int DN = 2 * 16 * 132 * 4;              // dh_rec partials of the two K halves
+  static constexpr int DXP = 4 * 16 * 68 * 4;              // dx partials of the four K quarters
+  static constexpr int STEP = ZS + DN + DXP;
+  static constexpr int HEAD = ChainHeadBwdLds<128>::BYTES; // the head prologue's scratch (same bytes)
+  static constexpr int BYTES = DHT + (STEP > HEAD ? STEP : HEAD);
+};
+static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT4BLds::BYTES : CHAINB_LDS_STAGE;
 
 #ifndef CHAINB_LEAD
 #define CHAINB_LEAD 2
@@ -632,13 +702,20 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
   constexpr int NXB = KX * 2;
   constexpr int TX = (NXB + NW - 1) / NW;
+  constexpr bool SK = H >= 32;                     // split-K products (ChainBLdsSK)
   static_assert(CPL == 1 && 16 * H == NT, "one dh element per lane");
   using L = ChainBLds<H, KX>;
-  static_assert(L::BYTES <= CHAINB_LDS && L::ZS % 16 == 0 && L::DH % 16 == 0, "chain bwd LDS layout");
+  using LK = ChainBLdsSK<H, KX>;
+  constexpr int UT = LK::UT, KG = LK::KG, KXG = LK::KXG, KPG = SK ? KB / KG : 1, KPX = SK ? KB / KXG : 1;
+  static_assert(!SK || (NW % UT == 0 && KB % KG == 0 && NW % NXB == 0 && KB % KXG == 0), "split-K tiling");
+  static_assert(L::BYTES <= CHAINB_LDS_STAGE && LK::BYTES <= CHAINB_LDS_STAGE && L::ZS % 16 == 0 && L::DH % 16 == 0,
+                "chain bwd LDS layout");
   auto zs = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem);
   auto dhs = reinterpret_cast<float (*)[16][C::HP]>(smem + L::ZS);
   auto dxs = reinterpret_cast<float (*)[16][32 * KX]>(smem + L::ZS + L::DH);
   auto wl = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem + L::ZS + L::DH + L::DX);
+  auto dpart = reinterpret_cast<float (*)[16][C::HP]>(smem + LK::ZS + LK::DH);                      // [KG]
+  auto xpart = reinterpret_cast<float (*)[KXG][16][LK::XPP]>(smem + LK::ZS + LK::DH + LK::DP);      // [2][KXG]
 
   const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P, Ts = S.Ts;
   // source kind and un-pooling are template parameters: with run-time branches around the
@@ -661,7 +738,14 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         const unsigned tag = tagb | (unsigned)ts;
         int row = lane / Din, k = lane % Din;
         for (int e = lane; e < nx; e += 64) {        // (the publisher's own divergence only)
-          const float v = dxs[buf][row][k];
+          float v;
+          if constexpr (SK) {
+            v = 0.f;
+#pragma unroll
+            for (int g = 0; g < KXG; ++g) v += xpart[buf][g][row][k];
+          } else {
+            v = dxs[buf][row][k];
+          }
           const size_t o = (size_t)row0 * Din + e + (size_t)ts * xstep;
           if constexpr (XO) st_granule(S.sout + o, v, tag);
           else S.dx[o] = v;
@@ -672,13 +756,22 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       };
       __syncthreads();
       __syncthreads();
-      for (int s = 0; s < nsteps; ++s) {
-        lds_barrier();
-        const int t = T - 1 - s;
-        if (s >= 1 && s <= T) publish((s - 1) & 1, t + 1);
+      if constexpr (SK) {            // two barriers per step; step s's dx tile is complete after the second
+        for (int s = 0; s < nsteps; ++s) {
+          lds_barrier();
+          lds_barrier();
+          if (s < T) publish(s & 1, T - 1 - s);
+        }
+        __syncthreads();
+      } else {
+        for (int s = 0; s < nsteps; ++s) {
+          lds_barrier();
+          const int t = T - 1 - s;
+          if (s >= 1 && s <= T) publish((s - 1) & 1, t + 1);
+        }
+        __syncthreads();
+        publish((T - 1) & 1, 0);
       }
-      __syncthreads();
-      publish((T - 1) & 1, 0);
       return;
     }
   }
@@ -687,9 +780,29 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
 
   for (int i = tid; i < 2 * 16 * C::HP; i += NT) (&dhs[0][0][0])[i] = 0.f;
 
-  bf16x8_t ufr[KB];
   const int unit = 4 * w + quad;
-  {
+  // SK: wave w owns unit tile ut over K slice kg of dh_rec^T, din tile xt over K slice kx of dx^T
+  const int ut = w % UT, kg = w / UT, xt = w % NXB, kx = w / NXB;
+  bf16x8_t ufr[SK ? KPG : KB];
+  bf16x8_t ufk[SK ? KPX : 1];                      // (SK: the W fragments of this wave's dx slice)
+  if constexpr (SK) {
+#pragma unroll
+    for (int q = 0; q < KPG; ++q) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)S.U[(size_t)(16 * ut + col) * G4 + 32 * (kg * KPG + q) + 8 * quad + j];
+      ufr[q] = v;
+    }
+    const int din = 16 * xt + col;
+#pragma unroll
+    for (int q = 0; q < KPX; ++q) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (__bf16)(S.W[(size_t)min(din, Dw - 1) * G4 + 32 * (kx * KPX + q) + 8 * quad + j] * (din < Dw ? 1.f : 0.f));
+      ufk[q] = v;
+    }
+  } else {
     const int au = 4 * w + (col >> 2);
 #pragma unroll
     for (int s = 0; s < KB; ++s) {
@@ -702,8 +815,9 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       ufr[s] = v;
     }
   }
-  bf16x8_t wfr[L::WL ? 1 : TX][L::WL ? 1 : KB];
-  if constexpr (L::WL) {     // W^T blocks [NXB][16 din][4H] in LDS (unrolled: all loads in flight)
+  bf16x8_t wfr[(L::WL || SK) ? 1 : TX][(L::WL || SK) ? 1 : KB];
+  if constexpr (SK) {
+  } else if constexpr (L::WL) {     // W^T blocks [NXB][16 din][4H] in LDS (unrolled: all loads in flight)
     static_assert((NXB * 16 * G4) % NT == 0, "W staging trip count");
 #pragma unroll
     for (int it = 0; it < NXB * 16 * G4 / NT; ++it) {
@@ -785,7 +899,14 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   auto store_dx = [&](int buf, int ts, unsigned tag) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const float v = dxs[buf][xrow[q]][xk[q]];
+      float v;
+      if constexpr (SK) {
+        v = 0.f;
+#pragma unroll
+        for (int g = 0; g < KXG; ++g) v += xpart[buf][g][xrow[q]][xk[q]];
+      } else {
+        v = dxs[buf][xrow[q]][xk[q]];
+      }
       const size_t o = (size_t)xo[q] + (size_t)ts * xstep;
       if constexpr (XO) st_granule(S.sout + o, v, tag);
       else S.dx[o] = v;
@@ -808,6 +929,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   dhn = dhs[0][col][unit];
   if (tid == 0 && S.trace_mid) S.trace_mid[blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
 
+  long long* pr = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
   for (int s0 = 0; s0 < T; s0 += D) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -815,6 +937,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       const int t = T - 1 - s;
       const int p = s & 1;
       const int jn = (j + 1 == D) ? 0 : j + 1;
+      chain_mark(pr, s, 0);
       {
         const float cp = rc[jn] * (t > 0 ? 1.f : 0.f);
         const float dh = dhn + dhr;
@@ -833,7 +956,9 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         rg[j] = *reinterpret_cast<const uint2*>(S.g + o * 4);
         rc[j] = S.c[o];
       }
+      chain_mark(pr, s, 1);
       dhs[p ^ 1][tid / H][tid % H] = stage_dh(jn, t - 1);
+      chain_mark(pr, s, 2);
       {
         const int tt = max(T - 1 - (s + 1 + D), 0);
         const int st = max(src_t(tt), 0);
@@ -843,8 +968,27 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         else ri[jn] = 0u;
       }
       lds_barrier();
+      chain_mark(pr, s, 3);
       dhn = dhs[p ^ 1][col][unit];
-      {   // serial chain: dh_{t-1} = U dz_t
+      if constexpr (SK) {   // partial products of this wave's K slices -> LDS
+        f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < KPG; ++q) {
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * (kg * KPG + q) + 8 * quad]);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[q], bz, a, 0, 0, 0);
+        }
+        f32x4_t b = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < KPX; ++q) {
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * (kx * KPX + q) + 8 * quad]);
+          b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufk[q], bz, b, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dpart[kg][col][16 * ut + 4 * quad + r] = a[r];
+          xpart[p][kx][col][16 * xt + 4 * quad + r] = b[r];
+        }
+      } else {   // serial chain: dh_{t-1} = U dz_t
         f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
@@ -853,7 +997,11 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
           else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a0, 0, 0, 0);
         }
         dhr = a0[0] + a1[0];
+#ifdef GQ_CHAIN_PROF
+        if (pr != nullptr) asm volatile("" ::"v"(dhr));
+#endif
       }
+      chain_mark(pr, s, 4);
       {   // dz tile -> HBM (weight-gradient pass)
         const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][gz_c]);
         const int tz = t >= 0 ? t : T;
@@ -863,7 +1011,13 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         const int ts = (s >= 1 && s <= T) ? t + 1 : T;
         if constexpr (!PUBW) store_dx(p ^ 1, ts, tagb | (unsigned)ts);
       }
-      if (t >= 0) {   // dx^T = W dz^T of this step
+      if constexpr (SK) {   // the partial tiles meet: dh_{t-1} of this lane's cell
+        lds_barrier();
+        float sdh = 0.f;
+#pragma unroll
+        for (int g = 0; g < KG; ++g) sdh += dpart[g][col][unit];
+        dhr = sdh;
+      } else if (t >= 0) {   // dx^T = W dz^T of this step
 #pragma unroll
         for (int q = 0; q < TX; ++q) {
           const int xb = w + NW * q;
@@ -882,16 +1036,148 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
           }
         }
       }
+      chain_mark(pr, s, 5);
     }
   }
   __syncthreads();
   if constexpr (!PUBW) store_dx((T - 1) & 1, 0, tagb);     // dx tile of t = 0
 }
 
+// time4's backward on one 16-sequence tile with 1024 threads: the head backward (chain_head.h,
+// waves 8..15 repeating waves 0..7), then the reverse recurrence with two cells per lane:
+// dh_rec^T = U dz^T with wave w on unit tile w % 8 over K half w / 8, dx^T = W dz^T with din tile
+// w % 4 over K quarter w / 4 (partials summed through LDS), dz -> HBM, dx -> granules (tag =
+// pooled time of the chain's top layer). Then this tile's share of the head-gradient reduction.
+__device__ __forceinline__ void chain_t4_bwd_stage(const ChainT4B Q, int tile, int ntiles, int Mp, unsigned tagb,
+                                                   char* smem) {
+  constexpr int H = 128, G4 = 4 * H, NW = 16, CPL = 2, HP = H + 4, ZP = G4 + 8, XP = 68;
+  using L = ChainT4BLds;
+  static_assert(L::DHT % 16 == 0 && L::ZS % 16 == 0 && L::DN % 16 == 0, "t4 backward LDS layout");
+  float* dhT = reinterpret_cast<float*>(smem);
+  char* rs = smem + L::DHT;
+  auto zs = reinterpret_cast<__bf16 (*)[ZP]>(rs);
+  auto dhn = reinterpret_cast<float (*)[16][HP]>(rs + L::ZS);
+  auto dxp = reinterpret_cast<float (*)[16][XP]>(rs + L::ZS + L::DN);
+  const int T = Q.T, Din = Q.Din, Dw = Q.Dw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, quad = lane >> 4;
+  const int row0 = tile * 16;
+
+  int unit[CPL];
+  size_t so[CPL];                                  // this cell's index in time4's state layout (t = 0)
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) {
+    const int gi = w + NW * cc;
+    unit[cc] = 4 * gi + quad;
+    so[cc] = (((size_t)tile * 8 + (gi & 7)) * 4 + (gi >> 3)) * 64 + lane;
+  }
+  const size_t sstep = (size_t)ntiles * 8 * 4 * 64;
+  // forward state ring (2 reverse steps), refilled right after the cell phase that used a slot
+  float4 rg[2][CPL];
+  float2 rcs[2][CPL];
+  auto load_slot = [&](int j, int t) {
+    const size_t tc = (size_t)max(t, 0);
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) {
+      const size_t o = tc * sstep + so[cc];
+      rg[j][cc] = *reinterpret_cast<const float4*>(Q.g + o * 4);
+      rcs[j][cc] = *reinterpret_cast<const float2*>(Q.c + o * 2);
+    }
+  };
+  load_slot(0, T - 1);
+  load_slot(1, T - 2);
+  chain_head_bwd<H>(Q.hd, Q.h + (size_t)(T - 1) * Mp * H, tile, ntiles, dhT, rs);
+  // weight fragments (after the head prologue: live through it they would crowd its registers),
+  // from the forward's lane-contiguous fragment image (time4_head.hip's backward layout: wave
+  // w' < 8 holds unit tile w' over the full K, and din tile w' % 4 over gate-column half w' / 4)
+  const int ut = w & 7, kh = w >> 3, dt = w & 3, kq = w >> 2;
+  bf16x8_t ufr[8], wfr[4];
+  {
+    const bf16x8_t* pu = Q.pk + T4PK_N + (size_t)ut * 16 * 64 + lane;
+    const bf16x8_t* pw = Q.pk + T4PK_N + T4PK_BU + (size_t)(dt + 4 * (kq >> 1)) * 8 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ufr[s] = pu[(8 * kh + s) * 64];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) wfr[s] = pw[(4 * (kq & 1) + s) * 64];
+  }
+  __syncthreads();                                 // the head scratch becomes the step tiles
+  // dx element of this thread (threads past the [16][Din] tile re-read the last one, no store)
+  const int nx = 16 * Din;
+  const bool ownx = tid < nx;
+  const int ex = min(tid, nx - 1), er = ex / Din, ek = ex % Din;
+  const size_t xstep = (size_t)Mp * Din, xoff = (size_t)(row0 + er) * Din + ek;
+  const int zq = tid >> 6, zc = (tid & 63) * 8;    // dz store: 8 bf16 of the [16][512] tile
+  float dc[CPL], dhr[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
+  for (int s0 = 0; s0 < T; s0 += 2) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {                   // (static ring slot: a dynamic index spilled the ring)
+    const int s = s0 + j;
+    if (s >= T) break;
+    const int t = T - 1 - s;
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) {
+      const int u = unit[cc];
+      const float dh = dhr[cc] + (s == 0 ? dhT[col * HP + u] : 0.f);
+      const float4 g = rg[j][cc];
+      const float cprev = rcs[j][cc].y;            // (0 at t = 0: the forward's initial state)
+      const float tc = tanhf_fast(rcs[j][cc].x);
+      const float dct = dc[cc] + dh * g.w * (1.f - tc * tc);
+      dc[cc] = dct * g.y;
+      zs[col][0 * H + u] = (__bf16)(dct * g.z * g.x * (1.f - g.x));
+      zs[col][1 * H + u] = (__bf16)(dct * cprev * g.y * (1.f - g.y));
+      zs[col][2 * H + u] = (__bf16)(dct * g.x * (1.f - g.z * g.z));
+      zs[col][3 * H + u] = (__bf16)(dh * tc * g.w * (1.f - g.w));
+    }
+    load_slot(j, t - 2);
+    lds_barrier();
+    *reinterpret_cast<uint4*>(Q.dz + ((size_t)t * Mp + row0 + zq) * G4 + zc) = *reinterpret_cast<const uint4*>(&zs[zq][zc]);
+    {
+      f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, b0 = a0, b1 = a0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[col][32 * (8 * kh + q) + 8 * quad]);
+        if (q & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[q], bz, a1, 0, 0, 0);
+        else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[q], bz, a0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[col][32 * (4 * kq + q) + 8 * quad]);
+        if (q & 1) b1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q], bz, b1, 0, 0, 0);
+        else b0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q], bz, b0, 0, 0, 0);
+      }
+      const f32x4_t a = a0 + a1, b = b0 + b1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dhn[kh][col][16 * ut + 4 * quad + r] = a[r];
+        dxp[kq][col][16 * dt + 4 * quad + r] = b[r];
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) dhr[cc] = dhn[0][col][unit[cc]] + dhn[1][col][unit[cc]];
+    const float v = (dxp[0][er][ek] + dxp[1][er][ek]) + (dxp[2][er][ek] + dxp[3][er][ek]);
+    if (ownx) st_granule(Q.sout + xoff + (size_t)t * xstep, v, tagb | (unsigned)t);
+  }
+  }
+  chain_head_bwd_reduce<H>(Q.hd, tile, ntiles);
+}
+
 __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   const int nblk = gridDim.x;
   __shared__ __attribute__((aligned(16))) char smem[CHAINB_LDS];
   const int s = blockIdx.x / A.nt8, tile = blockIdx.x % A.nt8;
+  if (s == A.ns && A.t4.on && tile < A.ntiles) {  // time4 + head backward of this tile
+    if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
+    const unsigned tagb = chain_tag_base((unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    chain_t4_bwd_stage(A.t4, tile, A.ntiles, A.Mp, tagb, smem);
+    __syncthreads();
+    if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+    chain_finish(A.ctl, nblk);
+    return;
+  }
   if (s >= A.ns || tile >= A.ntiles) {
     chain_finish(A.ctl, nblk);
     return;
@@ -904,7 +1190,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   // scratch and read every field from there inside the step loop
   const ChainBStage S = A.st[s];
   const int H = S.H, KX = S.KX;
-  const bool src = s > 0;
+  const bool src = s > 0 || A.t4.on;              // (stage 0 then reads time4's dx granules)
 #define GQ_CHAINB_BODY3(HH, KXX, DD, SRCV, UPV, XOV)                                    \
   {                                                                                     \
     if (threadIdx.x >= TMC<HH>::NT + (TMC<HH>::NT + 64 <= 1024 ? 64 : 0)) return;       \
@@ -943,6 +1229,37 @@ static long long* chain_trace_buf(int dev) {
   if (!tr[dev]) TORCH_CHECK(hipMalloc(&tr[dev], 3 * 256 * sizeof(long long)) == hipSuccess,
                             "lstm_chain: trace");
   return tr[dev];
+}
+
+// tile 0's per-step phase clocks [CHAIN_MAX stages][CHAIN_PROF_STEPS][8] of the last launch with
+// GNNQC_CHAIN_PROF=1 (forward and backward use the same buffer)
+static long long* chain_prof_buf(int dev) {
+#ifdef GQ_CHAIN_PROF
+  static const bool on = [] {
+    const char* e = std::getenv("GNNQC_CHAIN_PROF");
+    return e != nullptr && e[0] == '1';
+  }();
+#else
+  const bool on = false;
+#endif
+  if (!on) return nullptr;
+  static long long* pb[64] = {nullptr};
+  if (!pb[dev]) {
+    TORCH_CHECK(hipMalloc(&pb[dev], CHAIN_MAX * CHAIN_PROF_STEPS * 8 * sizeof(long long)) == hipSuccess, "chain prof");
+    TORCH_CHECK(hipMemset(pb[dev], 0, CHAIN_MAX * CHAIN_PROF_STEPS * 8 * sizeof(long long)) == hipSuccess, "chain prof");
+  }
+  return pb[dev];
+}
+
+at::Tensor lstm_chain_prof(const at::Tensor& like) {
+  c10::DeviceGuard guard(like.device());
+  long long* p = chain_prof_buf(like.get_device());
+  TORCH_CHECK(p != nullptr, "lstm_chain_prof: build with GNNQC_CHAIN_PROF_BUILD=1 and set GNNQC_CHAIN_PROF=1 "
+                            "before the first chain launch");
+  at::Tensor o = at::empty({CHAIN_MAX, CHAIN_PROF_STEPS, 8}, like.options().dtype(at::kLong));
+  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int64_t>(), p, o.numel() * sizeof(long long), hipMemcpyDeviceToDevice,
+                             stream()) == hipSuccess, "lstm_chain_prof");
+  return o;
 }
 
 int* chain_ctl(int dev) {
@@ -1125,6 +1442,10 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     S.Dw = Dw;
     S.KX = (Din + 31) / 32;
     S.PIN = s > 0 ? std::max(1, (int)pool[s - 1]) : 1;
+    {
+      long long* pb = chain_prof_buf(x.get_device());
+      S.prof = pb != nullptr ? pb + (size_t)s * CHAIN_PROF_STEPS * 8 : nullptr;
+    }
     out.insert(out.end(), {h.narrow(0, 0, T), g, c, pooled, pidx});
     if (so.defined()) out.push_back(so);        // kept alive until the launch is enqueued
     prev_stream = so;
@@ -1209,6 +1530,64 @@ std::vector<at::Tensor> lstm_chain_bwd(const at::Tensor& dh, at::TensorList g, a
   return res;
 }
 
+// time4_head.hip: the backward head arguments (weights, labels, dloss, gradient sinks, tickets)
+void t4_head_bwd_args(ChainHead& hd, at::TensorList head, const at::Tensor& y, const at::Tensor& mask, int64_t M,
+                      int Mp, double alpha1, double alpha2, double w0, double w1, const at::Tensor& dloss,
+                      at::TensorList hgrads, at::Tensor& gpart);
+
+// lstm_chain_bwd with time4 + the head as its first stage (chain_t4_bwd_stage): dloss [1]; x4 the
+// pooled top chain output (time4's input, [T4, Mp, Din]); h4 / g4 / c4 time4's saved forward state
+// (lstm_chain_head_fwd / time4_head_fwd); Wt4 / Ut4 its weights and pk their fragment image (the
+// forward's last result); head = [W1, b1, W2, b2, W3, b3]
+// with their gradients hgrads (accumulated); then the chain stages, TOP layer first, as for
+// lstm_chain_bwd (the top one must pool by 3). Returns [dz4 [T4 + 1, Mp, 512], dz_0 .. dz_{n-1}, dx].
+std::vector<at::Tensor> lstm_chain_head_bwd(const at::Tensor& dloss, const at::Tensor& x4, const at::Tensor& h4,
+                                            const at::Tensor& g4, const at::Tensor& c4, const at::Tensor& Wt4,
+                                            const at::Tensor& Ut4, const at::Tensor& pk, at::TensorList head, const at::Tensor& y,
+                                            const at::Tensor& mask, int64_t M, double alpha1, double alpha2, double w0,
+                                            double w1, at::TensorList hgrads, at::TensorList g, at::TensorList c,
+                                            at::TensorList W, at::TensorList U, at::TensorList pidx,
+                                            at::IntArrayRef pool, at::IntArrayRef x_width, at::IntArrayRef T_in) {
+  check_f32_cuda(x4, "x4");
+  for (const at::Tensor* t : {&dloss, &h4, &g4, &c4, &Wt4, &Ut4}) check_f32_cuda(*t, "lstm_chain_head_bwd operand");
+  TORCH_CHECK(x4.dim() == 3 && x4.is_contiguous(), "lstm_chain_head_bwd: x4 must be a contiguous [T4, Mp, Din]");
+  const int T4 = (int)x4.size(0), Mp = (int)x4.size(1), Din = (int)x4.size(2), Dw = (int)Wt4.size(0);
+  TORCH_CHECK(T4 >= 1 && T4 <= 16 && Din <= 64 && Dw >= 1 && Dw <= Din && Wt4.size(1) == 512 && Ut4.size(0) == 128 &&
+                  Ut4.size(1) == 512, "lstm_chain_head_bwd: time4 shapes");
+  TORCH_CHECK(dloss.numel() == 1, "lstm_chain_head_bwd: dloss must be a scalar");
+  TORCH_CHECK(h4.numel() == (long)T4 * Mp * 128 && g4.numel() == (long)T4 * Mp * 128 * 4 && c4.numel() == (long)T4 * Mp * 128 * 2,
+              "lstm_chain_head_bwd: time4 saved state shapes");
+  TORCH_CHECK(pool.size() >= 1 && pool[0] == 3, "lstm_chain_head_bwd: the top chain stage must pool by 3");
+  ChainBArgs A{};
+  std::vector<at::Tensor> keep;
+  c10::DeviceGuard guard(x4.device());
+  auto opt = x4.options();
+  at::Tensor so = at::empty({T4, Mp, Din}, opt.dtype(at::kLong));      // time4's dx granules
+  auto res = chain_bwd_setup(A, keep, x4, g, c, W, U, pidx, pool, x_width, T_in, (Mp / 16 + 7) / 8 * 8);
+  A.st[0].dh = nullptr;
+  A.st[0].din = reinterpret_cast<const unsigned long long*>(so.data_ptr<int64_t>());
+  ChainT4B& Q = A.t4;
+  Q.on = 1;
+  Q.h = h4.data_ptr<float>();
+  Q.g = g4.data_ptr<float>();
+  Q.c = c4.data_ptr<float>();
+  TORCH_CHECK(pk.is_cuda() && pk.is_contiguous() && pk.nbytes() == (size_t)T4PK_ALL * 16,
+              "lstm_chain_head_bwd: pk must be the forward's full fragment image");
+  Q.pk = reinterpret_cast<const bf16x8_t*>(pk.data_ptr());
+  at::Tensor dz4 = at::empty({T4 + 1, Mp, 512}, opt.dtype(at::kBFloat16));
+  Q.dz = bf16_ptr(dz4);
+  Q.sout = reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>());
+  Q.T = T4;
+  Q.Din = Din;
+  Q.Dw = Dw;
+  at::Tensor gpart;
+  t4_head_bwd_args(Q.hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1, dloss, hgrads, gpart);
+  hipLaunchKernelGGL(lstm_chain_bwd_kernel, dim3((A.ns + 1) * A.nt8), dim3(1024), 0, stream(), A);
+  GQ_LAUNCH_CHECK();
+  res.insert(res.begin(), dz4);
+  return res;
+}
+
 static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Tensor>& keep, const at::Tensor& dh,
                                                at::TensorList g, at::TensorList c, at::TensorList W, at::TensorList U,
                                                at::TensorList pidx, at::IntArrayRef pool, at::IntArrayRef x_width,
@@ -1285,6 +1664,10 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
     S.P = P;
     S.Ts = Ts;
     S.trace_mid = A.trace + 512;
+    {
+      long long* pb = chain_prof_buf(dh.get_device());
+      S.prof = pb != nullptr ? pb + (size_t)s * CHAIN_PROF_STEPS * 8 : nullptr;
+    }
   }
   dzs.push_back(dx.defined() ? dx.narrow(0, 0, (int)T_in[ns - 1]) : at::empty({0}, opt));
   return dzs;
@@ -1320,5 +1703,7 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("lstm_chain_capacity", &gq::lstm_chain_capacity);
   m.impl("lstm_chain_ctl", &gq::lstm_chain_ctl);
   m.impl("lstm_chain_trace", &gq::lstm_chain_trace);
+  m.impl("lstm_chain_prof", &gq::lstm_chain_prof);
   m.impl("lstm_chain_bwd", &gq::lstm_chain_bwd);
+  m.impl("lstm_chain_head_bwd", &gq::lstm_chain_head_bwd);
 }

@@ -29,6 +29,7 @@
 
 #include <cstdlib>
 #include "lstm_grads_body.h"
+#include "gcn_fused.h"
 #include "lstm_tm_common.h"
 
 namespace gq {
@@ -962,6 +963,8 @@ struct MultiGrad {
   int start[MULTI_MAX + 1];
   int key[MULTI_MAX];              // HG * 8 + DT
   int n;
+  int gcn_nb;                      // > 0: blocks [0, gcn_nb) run the fused GCN backward (gcn_fused.h)
+  GcnBwdJob gcn;
 };
 struct MultiRed {
   RedJob j[MULTI_MAX];
@@ -971,12 +974,19 @@ struct MultiRed {
 };
 
 __global__ __launch_bounds__(256) void lstm_grads_multi_kernel(MultiGrad M) {
-  const int b = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) char smem[GradsLds<128, 5>::BYTES];   // the largest instance
+  static_assert(GcnBwdLds<2, 16>::BYTES <= GradsLds<128, 5>::BYTES, "GCN job LDS");
+  if ((int)blockIdx.x < M.gcn_nb) {                      // the GCN backward's workgroups
+    const int gb = blockIdx.x;
+    if (M.gcn.key == 2 * 64 + 16)                          // (the CML configuration)
+      gcn_fused_bwd_body<2, 16>(M.gcn, gb % M.gcn.B, gb / M.gcn.B, smem);
+    return;
+  }
+  const int b = blockIdx.x - M.gcn_nb;
   int k = 0;
   while (k + 1 < M.n && b >= M.start[k + 1]) ++k;        // uniform
   const GradJob gj = M.j[k];                              // by value: scalar loads, no scratch copy
   const int gb = b - M.start[k];
-  __shared__ __attribute__((aligned(16))) char smem[GradsLds<128, 5>::BYTES];   // the largest instance
 #define GQ_MG(HG, DT)                                                                                    \
   case HG * 8 + DT:                                                                                      \
     lstm_grads_body<HG, DT, 4>(gj.dz, gj.x, gj.h, gj.W, nullptr, gj.ws, gj.rows, gj.period, gj.hshift, gj.Din, \
@@ -1005,22 +1015,47 @@ __global__ __launch_bounds__(256) void lstm_grads_reduce_multi_kernel(MultiRed M
                            rj.dU, b - M.start[k], 0, 1, M.nf);
 }
 
+// gcn_fused.hip: the fused GCN backward's job (run here as extra workgroups)
+GcnBwdJob gcn_bwd_job(const at::Tensor& dh, int64_t c_off, const at::Tensor& series, const at::Tensor& shift,
+                      const at::Tensor& scale, const at::Tensor& win_group, const at::Tensor& win_center,
+                      const at::Tensor& win_valid, const at::Tensor& group_anom_pos, const at::Tensor& pw,
+                      const at::Tensor& wids, const at::Tensor& table, const c10::optional<at::Tensor>& cursor,
+                      int64_t tb, int64_t seq_len, bool time_norm, const at::Tensor& S, const at::Tensor& st,
+                      const at::Tensor& W, const at::Tensor& bias, const at::Tensor& alpha, const at::Tensor& dW,
+                      const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dalpha, int& nblocks);
+
 // grads of jobs (dz, x, h, W, period, hshift, ws) then reductions of rjobs (ws, W, dW, dU, db):
-// a reduce job may be one of this call's grads jobs (stream order runs the grads first)
+// a reduce job may be one of this call's grads jobs (stream order runs the grads first).
+// gcn_t / gcn_i (optional): the arguments of gcn_fused_bwd - [dh, series, shift, scale, win_group,
+// win_center, win_valid, group_anom_pos, pw, wids, table, cursor (empty: none), S, st, W, bias,
+// alpha, dW, dgamma, dbeta, dalpha] / [c_off, tb, seq_len, time_norm] - run as extra workgroups of
+// the gradient launch (both only need the chain backward's results; the CML configuration,
+// Cin = 2, F = 16, only: every instantiation would raise the launch's register allocation).
 void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, at::TensorList gW,
                       at::IntArrayRef period, at::IntArrayRef hshift, at::TensorList gws, at::TensorList rws,
-                      at::TensorList rW, at::TensorList rdW, at::TensorList rdU, at::TensorList rdb) {
+                      at::TensorList rW, at::TensorList rdW, at::TensorList rdU, at::TensorList rdb,
+                      at::TensorList gcn_t, at::IntArrayRef gcn_i) {
   const int ng = (int)gz.size(), nr = (int)rws.size();
   TORCH_CHECK(ng <= MULTI_MAX && nr <= MULTI_MAX && (int)gx.size() == ng && (int)gh.size() == ng &&
                   (int)gW.size() == ng && (int)period.size() == ng && (int)hshift.size() == ng &&
                   (int)gws.size() == ng && (int)rW.size() == nr && (int)rdW.size() == nr && (int)rdU.size() == nr &&
                   (int)rdb.size() == nr, "lstm_grads_multi: job lists");
+  TORCH_CHECK((gcn_t.size() == 0 && gcn_i.size() == 0) || (gcn_t.size() == 21 && gcn_i.size() == 4),
+              "lstm_grads_multi: gcn job lists");
+  TORCH_CHECK(gcn_t.size() == 0 || ng > 0, "lstm_grads_multi: a GCN job rides on a gradient launch");
   if (ng + nr == 0) return;
   c10::DeviceGuard guard(ng ? gz[0].device() : rws[0].device());
   auto st = stream();
   if (ng) {
     MultiGrad M{};
     M.n = ng;
+    if (gcn_t.size() > 0) {
+      const c10::optional<at::Tensor> cur = gcn_t[11].numel() > 0 ? c10::optional<at::Tensor>(gcn_t[11]) : c10::nullopt;
+      M.gcn = gcn_bwd_job(gcn_t[0], gcn_i[0], gcn_t[1], gcn_t[2], gcn_t[3], gcn_t[4], gcn_t[5], gcn_t[6], gcn_t[7],
+                          gcn_t[8], gcn_t[9], gcn_t[10], cur, gcn_i[1], gcn_i[2], gcn_i[3] != 0, gcn_t[12], gcn_t[13],
+                          gcn_t[14], gcn_t[15], gcn_t[16], gcn_t[17], gcn_t[18], gcn_t[19], gcn_t[20], M.gcn_nb);
+      TORCH_CHECK(M.gcn.key == 2 * 64 + 16, "lstm_grads_multi: the GCN job takes 2 input / 16 output channels");
+    }
     int nb = 0;
     // job bodies read bf16 dz: an fp32 one (sequence-major lstm_bwd) is rounded once here, as the
     // body would round it when staging (same result); stream-ordered, so the temporaries may go
@@ -1058,7 +1093,7 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
       nb += j.nblocks;
     }
     M.start[ng] = nb;
-    hipLaunchKernelGGL(lstm_grads_multi_kernel, dim3(nb), dim3(256), 0, st, M);
+    hipLaunchKernelGGL(lstm_grads_multi_kernel, dim3(M.gcn_nb + nb), dim3(256), 0, st, M);
     GQ_LAUNCH_CHECK();
   }
   if (nr) {

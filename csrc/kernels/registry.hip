@@ -40,9 +40,15 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_chain_capacity(Tensor like) -> int");
   m.def("lstm_chain_ctl(Tensor like) -> Tensor");
   m.def("lstm_grads_multi(Tensor[] gz, Tensor[] gx, Tensor[] gh, Tensor[] gW, int[] period, int[] hshift, "
-        "Tensor[] gws, Tensor[] rws, Tensor[] rW, Tensor(a!)[] rdW, Tensor(b!)[] rdU, Tensor(c!)[] rdb) -> ()");
+        "Tensor[] gws, Tensor[] rws, Tensor[] rW, Tensor(a!)[] rdW, Tensor(b!)[] rdU, Tensor(c!)[] rdb, "
+        "Tensor[] gcn_t, int[] gcn_i) -> ()");
   m.def("lstm_chain_trace(Tensor like) -> Tensor");
+  m.def("lstm_chain_prof(Tensor like) -> Tensor");
   m.def("lstm_chain_bwd(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
+        "int[] x_width, int[] T_in) -> Tensor[]");
+  m.def("lstm_chain_head_bwd(Tensor dloss, Tensor x4, Tensor h4, Tensor g4, Tensor c4, Tensor Wt4, Tensor Ut4, "
+        "Tensor pk, Tensor[] head, Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, "
+        "Tensor(a!)[] hgrads, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");
   m.def("time4_head_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor pk, bool train, Tensor[] head, Tensor y, Tensor mask, "
         "int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!) sums, Tensor(b!) hist) -> Tensor[]");

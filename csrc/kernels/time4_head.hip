@@ -537,6 +537,35 @@ std::vector<at::Tensor> time4_head_fwd(const at::Tensor& x, const at::Tensor& W,
   return {h, g, c, logits, loss};
 }
 
+// The backward head's arguments: dloss [1], the head gradient sinks (accumulated), the per-tile
+// record buffer (allocated here) and the chain control words' tickets ([5] arrivals, [8] reduce
+// done; [7] is the non-finite gradient flag). Also used by lstm_chain_head_bwd (lstm_chain.hip).
+void t4_head_bwd_args(ChainHead& hd, at::TensorList head, const at::Tensor& y, const at::Tensor& mask, int64_t M,
+                      int Mp, double alpha1, double alpha2, double w0, double w1, const at::Tensor& dloss,
+                      at::TensorList hgrads, at::Tensor& gpart) {
+  check_f32_cuda(dloss, "dloss");
+  TORCH_CHECK(dloss.numel() == 1, "time4_head_bwd: dloss must be a scalar");
+  TORCH_CHECK(hgrads.size() == 6, "time4_head_bwd: head gradient list");
+  t4_head_args(hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1);
+  for (size_t i = 0; i < 6; ++i) {
+    check_f32_cuda(hgrads[i], "head gradient");
+    TORCH_CHECK(hgrads[i].numel() == head[i].numel(), "time4_head_bwd: head gradient ", i, " size");
+  }
+  gpart = at::empty({(long)(Mp / 16) * ChainHeadRec<T4H>::PITCH}, y.options());
+  hd.dloss = dloss.data_ptr<float>();
+  hd.gpart = gpart.data_ptr<float>();
+  hd.dW1 = hgrads[0].data_ptr<float>();
+  hd.db1 = hgrads[1].data_ptr<float>();
+  hd.dW2 = hgrads[2].data_ptr<float>();
+  hd.db2 = hgrads[3].data_ptr<float>();
+  hd.dW3 = hgrads[4].data_ptr<float>();
+  hd.db3 = hgrads[5].data_ptr<float>();
+  const int dev = y.get_device();
+  hd.ticket = chain_ctl(dev) + 5;
+  hd.done = chain_ctl(dev) + 8;
+  hd.ctl = chain_ctl(dev);
+}
+
 // Backward: dloss [1]; x / h / g / c from the forward. Adds the head's weight gradients to
 // hgrads = [dW1, db1, dW2, db2, dW3, db3]; returns [dz [T + 1, Mp, 512], dx [T, Mp, Din]].
 std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor& x, const at::Tensor& h,
@@ -550,11 +579,6 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   TORCH_CHECK(dloss.numel() == 1, "time4_head_bwd: dloss must be a scalar");
   TORCH_CHECK(h.numel() == (long)T * Mp * T4H && g.numel() == (long)T * Mp * T4H * 4 && c.numel() == (long)T * Mp * T4H * 2,
               "time4_head_bwd: saved state shapes");
-  TORCH_CHECK(hgrads.size() == 6, "time4_head_bwd: head gradient list");
-  for (size_t i = 0; i < 6; ++i) {
-    check_f32_cuda(hgrads[i], "head gradient");
-    TORCH_CHECK(hgrads[i].numel() == head[i].numel(), "time4_head_bwd: head gradient ", i, " size");
-  }
   c10::DeviceGuard guard(x.device());
   auto opt = x.options();
   const int ntiles = Mp / 16;
@@ -566,7 +590,6 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   A.g = const_cast<float*>(g.data_ptr<float>());
   A.c = const_cast<float*>(c.data_ptr<float>());
   at::Tensor dz = at::empty({T + 1, Mp, T4G}, opt.dtype(at::kBFloat16)), dx = at::empty({T, Mp, Din}, opt);
-  at::Tensor gpart = at::empty({(long)ntiles * ChainHeadRec<T4H>::PITCH}, opt);
   A.dz = bf16_ptr(dz);
   A.dx = dx.data_ptr<float>();
   A.T = T;
@@ -574,18 +597,8 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   A.Din = Din;
   A.Dw = Dw;
   A.ntiles = ntiles;
-  t4_head_args(A.hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1);
-  A.hd.dloss = dloss.data_ptr<float>();
-  A.hd.gpart = gpart.data_ptr<float>();
-  A.hd.dW1 = hgrads[0].data_ptr<float>();
-  A.hd.db1 = hgrads[1].data_ptr<float>();
-  A.hd.dW2 = hgrads[2].data_ptr<float>();
-  A.hd.db2 = hgrads[3].data_ptr<float>();
-  A.hd.dW3 = hgrads[4].data_ptr<float>();
-  A.hd.db3 = hgrads[5].data_ptr<float>();
-  A.hd.ticket = chain_ctl(x.get_device()) + 5;
-  A.hd.done = chain_ctl(x.get_device()) + 8;     // ([7] is the non-finite gradient flag)
-  A.hd.ctl = chain_ctl(x.get_device());
+  at::Tensor gpart;
+  t4_head_bwd_args(A.hd, head, y, mask, M, Mp, alpha1, alpha2, w0, w1, dloss, hgrads, gpart);
   A.head = 1;
   A.trace = t4_trace_buf(x.get_device());
   if (pk.numel() > 0) {         // the chain forward's image including the backward fragments

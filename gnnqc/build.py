@@ -81,9 +81,12 @@ def build_hip(verbose=False, jobs=None) -> str:
     if not srcs:
         raise RuntimeError("no HIP sources found")
     cflags, ldflags = _torch_flags()
-    hdr_digest = _hash_files(headers + [__file__])
+    # GNNQC_CHAIN_PROF_BUILD=1: compile the chain kernels' per-step phase clocks in (diagnostics
+    # only: scripts/chain_phase_prof.py; they slow the chain launches when compiled in)
+    prof = ["-DGQ_CHAIN_PROF"] if os.environ.get("GNNQC_CHAIN_PROF_BUILD", "0") == "1" else []
+    hdr_digest = _hash_files(headers + [__file__]) + ("prof" if prof else "")
     common = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-              "-munsafe-fp-atomics", f"-I{os.path.join(CSRC, 'kernels')}", *cflags]
+              "-munsafe-fp-atomics", f"-I{os.path.join(CSRC, 'kernels')}", *prof, *cflags]
 
     def compile_one(src):
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")

@@ -310,11 +310,25 @@ class _HipStoreGCN(torch.autograd.Function):
             raise RuntimeError("gcn_fused backward: parameter gradients in eval mode take the generic path")
         sinks = [(_grad_sink(p) if n else (torch.zeros_like(p), False)) for p, n in zip(ctx.params, need)]
         wids, table, cursor = ctx.ids
-        hip_ops().gcn_fused_bwd(dh.contiguous(), int(ctx.data["ca"]), *ctx.data["bwd"], wids, table, cursor,
-                                *ctx.data["dims"], S, st, W.contiguous(), b.contiguous(), alpha.contiguous(),
-                                sinks[0][0], sinks[2][0], sinks[3][0], sinks[4][0])
+        args = (dh.contiguous(), int(ctx.data["ca"]), *ctx.data["bwd"], wids, table, cursor, *ctx.data["dims"], S, st,
+                W.contiguous(), b.contiguous(), alpha.contiguous(), sinks[0][0], sinks[2][0], sinks[3][0], sinks[4][0])
+        from .lstm import defer_to_grads_launch
+        # (deferred onto the batched LSTM weight-gradient launch when every gradient goes straight
+        # into .grad and the configuration is the one that launch instantiates)
+        if not (all(direct for (_, direct), n in zip(sinks, need) if n) and tuple(W.shape) == (2, 16)
+                and defer_to_grads_launch(_gcn_job_lists(args))):
+            hip_ops().gcn_fused_bwd(*args)
         grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need)]
         return (None, None, *grads, None, None, None, None, None, None, None)
+
+
+def _gcn_job_lists(args):
+    """gcn_fused_bwd's arguments as lstm_grads_multi's (gcn_t, gcn_i) job lists."""
+    (dh, c_off, series, shift, scale, wg, wc, wv, gap, pw, wids, table, cursor, tb, seq_len, time_norm, S, st, W, b,
+     alpha, dW, dgamma, dbeta, dalpha) = args
+    cur = cursor if cursor is not None else series.new_zeros(0, dtype=torch.long)
+    return ([dh, series, shift, scale, wg, wc, wv, gap, pw, wids, table, cur, S, st, W, b, alpha, dW, dgamma, dbeta,
+             dalpha], [int(c_off), int(tb), int(seq_len), int(bool(time_norm))])
 
 
 def store_gcn_ok(store, layer, training: bool, pooling: str) -> bool:

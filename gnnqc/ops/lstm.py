@@ -83,6 +83,7 @@ class _Pipe:
     job = None      # layer whose weight-gradient pass has not run yet
     red = None      # layer whose gradient pass ran; its split reduction has not
     batch = []      # jobs of a chain backward: all gradient passes in one launch at the flush
+    gcn = None      # (gcn_t, gcn_i): the fused GCN backward, run as extra workgroups of that launch
 
 
 # Largest sequence count (rows of 16-sequence tiles) a recurrence may have for its layer to
@@ -127,6 +128,18 @@ def _pipe_drain_one():
     _Pipe.job, _Pipe.red = None, job
 
 
+def defer_to_grads_launch(gcn_lists) -> bool:
+    """Queue the fused GCN backward (``lstm_grads_multi``'s gcn_t / gcn_i lists) onto the pending
+    batched weight-gradient launch of this backward: the two are independent, and one launch
+    overlaps them on the CUs the recurrences left idle. False (the caller launches it itself) when
+    no batch is pending or ``GNNQC_GCN_DEFER=0``."""
+    import os
+    if not (_DirectGrad.enabled and _Pipe.batch and _Pipe.gcn is None and os.environ.get("GNNQC_GCN_DEFER", "1") == "1"):
+        return False
+    _Pipe.gcn = gcn_lists
+    return True
+
+
 def pipe_flush():
     """Run all pending weight-gradient / reduction work (end of the backward). With a chain
     backward's batch: every pending gradient pass in ONE launch, every reduction in one more."""
@@ -134,12 +147,13 @@ def pipe_flush():
         from ..utils.native import hip_ops
         grads = ([_Pipe.job] if _Pipe.job is not None else []) + _Pipe.batch
         reds = ([_Pipe.red] if _Pipe.red is not None else []) + grads
+        gt, gi = _Pipe.gcn if _Pipe.gcn is not None else ([], [])
         hip_ops().lstm_grads_multi([j["dz"] for j in grads], [j["x"] for j in grads], [j["h"] for j in grads],
                                    [j["W"] for j in grads], [j["period"] for j in grads],
                                    [j["hshift"] for j in grads], [j["ws"] for j in grads],
                                    [r["ws"] for r in reds], [r["W"] for r in reds], [r["g"][0] for r in reds],
-                                   [r["g"][1] for r in reds], [r["g"][2] for r in reds])
-        _Pipe.job, _Pipe.red, _Pipe.batch = None, None, []
+                                   [r["g"][1] for r in reds], [r["g"][2] for r in reds], gt, gi)
+        _Pipe.job, _Pipe.red, _Pipe.batch, _Pipe.gcn = None, None, [], None
     while _Pipe.job is not None or _Pipe.red is not None:
         _pipe_drain_one()
 
@@ -185,6 +199,7 @@ def direct_grad_accumulation(flag: bool = True):
         _DirectGrad.enabled = prev
         if _Pipe.job is not None or _Pipe.red is not None or _Pipe.batch:
             pipe_flush()
+        _Pipe.gcn = None
 
 
 def _grad_sink(p: torch.Tensor):
@@ -443,8 +458,6 @@ class _HipLSTMChainHead(torch.autograd.Function):
             g = g.contiguous()
         hsinks = [_grad_sink(p) for p in ctx.params[npar:]]
         xt = layer_x(ns)
-        dz4, dxt = ops.time4_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], pk, list(head), y, mask, ctx.M, *ctx.consts,
-                                      [s for s, _ in hsinks])
         order = list(reversed(range(ns)))
         e8 = x.new_zeros(0, dtype=torch.uint8)
         chain_args = ([outs[5 * i + 1] for i in order], [outs[5 * i + 2] for i in order],
@@ -454,7 +467,16 @@ class _HipLSTMChainHead(torch.autograd.Function):
                       [outs[5 * i].shape[0] for i in order])
         grads = [None] * npar
         sinks = {i: [_grad_sink(p) for p in ctx.params[3 * i:3 * i + 3]] for i in range(ns + 1)}
-        res = ops.lstm_chain_bwd(dxt, *chain_args)
+        if _t4_chain_on() and pools[-1] == 3 and xt.is_contiguous():
+            # time4 + head backward as the first stage of the chain backward launch: the top
+            # chain stage consumes time4's dx as it is produced
+            res = ops.lstm_chain_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], pk, list(head), y, mask, ctx.M, *ctx.consts,
+                                          [s for s, _ in hsinks], *chain_args)
+            dz4 = res.pop(0)
+        else:
+            dz4, dxt = ops.time4_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], pk, list(head), y, mask, ctx.M,
+                                          *ctx.consts, [s for s, _ in hsinks])
+            res = ops.lstm_chain_bwd(dxt, *chain_args)
         dzs = {ns: dz4}
         hs = {ns: h4}
         for k, i in enumerate(order):
@@ -499,8 +521,8 @@ def _chain_bwd_on() -> bool:
 
 
 def _t4_chain_on() -> bool:
-    """time4 + head as a stage of the forward chain launch (``lstm_chain_head_fwd``;
-    ``GNNQC_T4_CHAIN``, default on) instead of its own launch after the chain."""
+    """time4 + head as a stage of the chain launches (``lstm_chain_head_fwd`` / ``_bwd``;
+    ``GNNQC_T4_CHAIN``, default on) instead of their own launches after / before the chain."""
     import os
     return os.environ.get("GNNQC_T4_CHAIN", "1") == "1"
 

@@ -32,7 +32,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
   python3 $ROOT/bench.py --steps 48 --warmup 8 $BENCH_ARGS > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
-f=$(ls $OUT/prof/*/run_kernel_stats.csv 2>/dev/null | head -1)
+f=$(ls $OUT/prof/run_kernel_stats.csv $OUT/prof/*/run_kernel_stats.csv 2>/dev/null | head -1)
 [ -n "$f" ] && python3 $ROOT/scripts/prof_summary.py $f 56 30
 if [ "${SOIL:-0}" = "1" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/profs -o run --output-format csv -- \

@@ -158,10 +158,11 @@ def test_headed_chain_eval_metrics_match(cuda_device, cml_windows, monkeypatch):
 
 @pytest.mark.parametrize("B", [128, 40])
 def test_t4_chain_stage_matches_separate_launch(cuda_device, cml_windows, monkeypatch, B):
-    """time4 + head + loss as a stage of the forward chain launch (lstm_chain_head_fwd: the stage
-    pools the last chain stage's granules itself, two cells per lane) == the separate time4_head_fwd
-    launch after the chain: loss, logits, every gradient (same bf16 operands and accumulation order
-    per cell: equal up to fp contraction), no consumer spin timed out."""
+    """time4 + head + loss as stages of the chain launches (lstm_chain_head_fwd: the stage pools the
+    last chain stage's granules itself; lstm_chain_head_bwd: the head backward + time4's reverse
+    recurrence publish dx granules to the top chain stage; two cells per lane) == the separate
+    time4_head_fwd / _bwd launches: loss and logits (same bf16 operands and accumulation order per
+    cell), every gradient (the backward's partial sums are split differently), no spin timed out."""
     from gnnqc.utils.native import hip_ops
     _, _, _, model, b = _setup(cuda_device, cml_windows, B=B)
     inputs = b.model_inputs("cml")
@@ -178,7 +179,7 @@ def test_t4_chain_stage_matches_separate_launch(cuda_device, cml_windows, monkey
     torch.testing.assert_close(l1, l0, atol=1e-6, rtol=1e-5)
     for n in g0:
         err = (g1[n] - g0[n]).norm().item()
-        assert err <= 1e-5 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())
+        assert err <= 1e-3 * (g0[n].norm().item() + 1e-6), (n, err, g0[n].norm().item())
     with torch.no_grad():                      # evaluation (TRAIN = false kernels)
         monkeypatch.setenv("GNNQC_T4_CHAIN", "1")
         le1, ze1 = model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0)

@@ -131,6 +131,43 @@ def test_training_step_store_path_matches_gather_path(cuda_device, cml_windows, 
                                                                            d0.norm().item())
 
 
+def test_gcn_backward_inside_grads_launch_matches_own_launch(cuda_device, cml_windows, monkeypatch):
+    """The fused GCN backward run as extra workgroups of the batched LSTM weight-gradient launch
+    (GNNQC_GCN_DEFER=1, the training default) == its own launch: every parameter gradient of a full
+    CML loss backward (float atomics: equal up to summation order)."""
+    from gnnqc.data.store import CursorIds
+    from gnnqc.ops import lstm as L
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    _, st, model = _setup(cuda_device, cml_windows)
+    ids = _ids(st, 128, cuda_device)
+    assert model.store_fused_ok(st)
+    deferred = []
+    real = L.defer_to_grads_launch
+
+    def spy(lists):
+        ok = real(lists)
+        deferred.append(ok)
+        return ok
+
+    monkeypatch.setattr(L, "defer_to_grads_launch", spy)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GNNQC_GCN_DEFER", flag)
+        for p in model.parameters():
+            p.grad = torch.zeros_like(p)
+        with direct_grad_accumulation(True):
+            loss = model.fused_store_loss(st, ids, 1.0, 5.0, None, None)[0]
+            loss.backward()
+        torch.cuda.synchronize()
+        out[flag] = {n: p.grad.clone() for n, p in model.named_parameters()}
+    assert deferred == [True, False], deferred
+    for n in out["0"]:
+        a, r = out["1"][n], out["0"][n]
+        # (float atomics: the GCN kernel gradient is a sum with strong cancellation, so its
+        # run-to-run ordering noise reaches ~1e-4 of its norm)
+        assert (a - r).norm().item() <= 2e-3 * (r.norm().item() + 1e-6), (n, (a - r).norm().item())
+
+
 def test_adam_flagged_matches_guarded_and_honours_flags(cuda_device):
     """adam_flagged (decision from producer flags, no grid-wide scan) == adam_guarded on finite
     gradients; a raised producer flag, a chain timeout or a NaN in g[0] skips the whole step (g
