@@ -886,7 +886,15 @@ def test_split_optimizer_graph_matches_fused(cuda_device, cml_windows, monkeypat
         assert opt.iterations == 6 and float(opt.step_t.item()) == 6.0
         return torch.cat([p.detach().reshape(-1) for p in model.parameters()]), float(tr.last_loss.item())
 
-    p1, l1 = run(True)
-    p0, l0 = run(False)
-    assert abs(l1 - l0) < 1e-3 * abs(l0) + 1e-5, (l1, l0)
-    assert (p1 - p0).norm().item() < 1e-4 * p0.norm().item()
+    # bitwise-reproducible kernels: the default store-fused GCN backward sums with atomics, and
+    # Adam amplifies that run-to-run noise on near-zero gradients (two runs of the SAME layout
+    # differ by ~1e-3 of the parameter norm after 6 steps), which would hide a layout difference
+    from gnnqc.ops import set_deterministic
+    prev = set_deterministic(True)
+    try:
+        p1, l1 = run(True)
+        p0, l0 = run(False)
+    finally:
+        set_deterministic(prev)
+    assert abs(l1 - l0) < 1e-5 * abs(l0) + 1e-6, (l1, l0)
+    assert (p1 - p0).norm().item() < 1e-6 * p0.norm().item()
