@@ -6,6 +6,8 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <vector>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
@@ -46,6 +48,24 @@ inline bool& deterministic_mode() {
   static bool v = false;
   return v;
 }
+
+// Deferred weight-gradient reductions (direct-accumulation training steps whose layers run the
+// per-layer backward, e.g. SoilNet's 418-tile recurrences): while set, lstm_grads_rows queues its
+// split reduction (workspace + destination buffers) instead of launching it, and
+// lstm_reduce_flush (lstm_tm.hip) runs every queued one in ONE launch at the end of the backward.
+// Set per call by gnnqc.ops.lstm, only when the gradient buffers are the optimiser's own.
+inline bool& defer_reduce_mode() {
+  static bool v = false;
+  return v;
+}
+struct DeferredRed {
+  at::Tensor ws;                 // [splits][RC] split records (kept alive until the flush)
+  int H, Din, splits;
+  float* dW;
+  float* dU;
+  float* db;
+};
+std::vector<DeferredRed>& deferred_reds();      // lstm_grads.hip
 
 #define GQ_CHECK(cond, msg) TORCH_CHECK(cond, "gnnqc: ", msg)
 #define GQ_LAUNCH_CHECK() do { hipError_t e__ = hipGetLastError(); TORCH_CHECK(e__ == hipSuccess, "gnnqc kernel launch failed: ", hipGetErrorString(e__)); } while (0)

@@ -104,6 +104,43 @@ __global__ __launch_bounds__(256) void gcn_bn_prep_kernel(const double* __restri
 // already reduced); st: [4, F] from the BN prep. Workgroup f sums column (j, f) over the R rows
 // (fixed order: deterministic) and adds dW[:, f], db, dgamma, dbeta, dalpha (nullptr = not
 // needed) into the gradient buffers; coef: [3, F]. (Replaces a separate column-sum launch.)
+// First stage of the finalize for many partial rows (SoilNet's node backward: one row per
+// (window, 2-step chunk) workgroup, 5,408 rows): workgroup p sums rows [p*chunk, (p+1)*chunk) of
+// acc [R][ncol] for every column in a fixed order (coalesced rows; 256/ncol row lanes per column,
+// combined in order), out [P][ncol]. The finalize then sums P rows instead of R (a workgroup per
+// column striding 384 B between its R loads took 49 us).
+__global__ __launch_bounds__(256) void gcn_acc_colsum_kernel(const float* __restrict__ acc, int R, int ncol,
+                                                             int chunk, float* __restrict__ out) {
+  __shared__ float part[256];
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int r0 = p * chunk, r1 = min(R, r0 + chunk);
+  if (ncol <= 128) {
+    const int nsub = 256 / ncol, c = tid % ncol, rs = tid / ncol;
+    float a0 = 0.f, a1 = 0.f;
+    if (rs < nsub) {
+      int r = r0 + rs;
+      for (; r + nsub < r1; r += 2 * nsub) {          // two independent loads in flight
+        a0 += acc[(long)r * ncol + c];
+        a1 += acc[(long)(r + nsub) * ncol + c];
+      }
+      if (r < r1) a0 += acc[(long)r * ncol + c];
+    }
+    part[tid] = a0 + a1;
+    __syncthreads();
+    if (tid < ncol) {
+      float t = 0.f;
+      for (int q = 0; q < nsub; ++q) t += part[q * ncol + tid];
+      out[(long)p * ncol + tid] = t;
+    }
+  } else {
+    for (int c = tid; c < ncol; c += 256) {
+      float t = 0.f;
+      for (int r = r0; r < r1; ++r) t += acc[(long)r * ncol + c];
+      out[(long)p * ncol + c] = t;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void gcn_bwd_finalize_kernel(
     const float* __restrict__ acc, int R, const double* __restrict__ S, int Cin, int F, const float* __restrict__ W,
     const float* __restrict__ b, const float* __restrict__ st, int training, float* __restrict__ dW,
@@ -495,6 +532,19 @@ at::Tensor gcn_bwd_finalize(const at::Tensor& acc, const at::Tensor& S, const at
     TORCH_CHECK(acc.numel() % ((long)(3 + Cin) * F) == 0, "gcn_bwd_finalize: acc must be [R,3+Cin,F]");
     R = (int)(acc.numel() / ((long)(3 + Cin) * F));
     ap = acc.data_ptr<float>();
+  }
+  at::Tensor pre;
+  if (R > 256) {        // two-stage fixed-order sum (still deterministic)
+    const int ncol = (3 + Cin) * F;
+    const int P = std::min(256, (R + 15) / 16), chunk = (R + P - 1) / P;
+    const int Pn = (R + chunk - 1) / chunk;
+    pre = at::empty({(long)Pn, ncol}, W.options());
+    c10::DeviceGuard g0(W.device());
+    hipLaunchKernelGGL(gcn_acc_colsum_kernel, dim3(Pn), dim3(256), 0, stream(), ap, R, ncol, chunk,
+                       pre.data_ptr<float>());
+    GQ_LAUNCH_CHECK();
+    ap = pre.data_ptr<float>();
+    R = Pn;
   }
   const double* sp = nullptr;
   if (training) {

@@ -54,8 +54,18 @@ __device__ __forceinline__ void stage_lds(float* __restrict__ dst, const float* 
 
 // mask sum over all rows (every block recomputes it: no cross-block dependency)
 __device__ float block_mask_sum(const float* __restrict__ mask, int R, float* red) {
+  // 8 independent loads in flight per thread (large R, e.g. SoilNet's 6,688 node rows: a
+  // one-load-per-iteration loop paid one memory latency per 256 rows)
   float s = 0.f;
-  for (int i = threadIdx.x; i < R; i += blockDim.x) s += mask[i];
+  int i = threadIdx.x;
+  for (; i + 7 * 256 < R; i += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = mask[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; i < R; i += 256) s += mask[i];
   s = wave_sum(s);
   const int w = threadIdx.x >> 6;
   __syncthreads();
@@ -331,9 +341,12 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   }
 }
 
-static int head_grid(int R) {
+// backward: persistent over at most 256 tiles (each workgroup flushes its weight-gradient
+// partials once with atomics); forward: one tile per workgroup up to 512 (two 66 KB-LDS
+// workgroups per CU: SoilNet's 418 node-row tiles run in one round instead of two)
+static int head_grid(int R, bool fwd = false) {
   const int nt = (R + HT - 1) / HT;
-  return deterministic_mode() ? 1 : std::max(1, std::min(nt, 256));
+  return deterministic_mode() ? 1 : std::max(1, std::min(nt, fwd ? 512 : 256));
 }
 
 #define GQ_HEAD_F_DISPATCH(F_, ...)                                 \
@@ -377,7 +390,7 @@ std::vector<at::Tensor> head_fwd(const at::Tensor& feat, const at::Tensor& W1, c
   auto opt = feat.options();
   at::Tensor z1 = at::empty({R, HU}, opt), z2 = at::empty({R, HU}, opt), lo = at::empty({R}, opt);
   at::Tensor aux = at::zeros({2}, opt);
-  const int grid = head_grid(R);
+  const int grid = head_grid(R, true);
   GQ_HEAD_F_DISPATCH(F, hipLaunchKernelGGL(head_fwd_kernel<FF>, dim3(grid), dim3(256), 0, stream(),
                                            feat.data_ptr<float>(), (int)feat.stride(0), W1.data_ptr<float>(),
                                            b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),

@@ -22,6 +22,11 @@
 
 namespace gq {
 
+std::vector<DeferredRed>& deferred_reds() {
+  static std::vector<DeferredRed> v;
+  return v;
+}
+
 template <int H, int DT, int GRX, typename ZT>
 __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const void* __restrict__ dz, const float* __restrict__ x, const float* __restrict__ hseq,
@@ -116,6 +121,10 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
   }
 #undef GQ_GR_H
   GQ_LAUNCH_CHECK();
+  if (defer_reduce_mode()) {                      // summed by lstm_reduce_flush with the other layers'
+    deferred_reds().push_back(DeferredRed{ws_t, H, Din, splits, dW, dU, db});
+    return;
+  }
   hipLaunchKernelGGL(lstm_grads_reduce_kernel, dim3((RC + 15) / 16, NG), dim3(256), 0, st, ws, splits, RC, ws2, ncb,
                      DT, HT, Din, H, dW, db, dU);
   GQ_LAUNCH_CHECK();

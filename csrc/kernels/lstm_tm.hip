@@ -46,8 +46,16 @@ void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows,
 // =====================================================================================
 // forward
 // x: [T][Mp][Din]  hout: [T][Mp][H]  gbuf: [T][tiles][NW][CPL][64][4]  cbuf: [..][64]
+// 1024-thread workgroups (H = 64) ask for 8 waves per SIMD, i.e. two workgroups per CU: at the
+// default allocation (~80 VGPRs) only one fits, and a 418-tile grid (SoilNet, 6,688 sequences)
+// then runs in two rounds on 256 CUs.
+template <int NT>
+struct TmOcc {
+  static constexpr int W = NT >= 1024 ? 8 : 1;
+};
+
 template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
-__global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
+__global__ __launch_bounds__(TMC<H>::NT, TmOcc<TMC<H>::NT>::W) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hout, __bf16* __restrict__ gbuf,
     float* __restrict__ cbuf, int Mp, int T, int Din, int Dw, float* __restrict__ pout,
@@ -195,7 +203,7 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_fwd_kernel(
 // of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
 // (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
 template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
-__global__ __launch_bounds__(2 * TMC<H>::NT) void lstm_tm2_fwd_kernel(
+__global__ __launch_bounds__(2 * TMC<H>::NT, TmOcc<2 * TMC<H>::NT>::W) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
     const float* __restrict__ bB, float* __restrict__ hA, __bf16* __restrict__ gA, float* __restrict__ cA,
@@ -1127,6 +1135,56 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
     hipLaunchKernelGGL(lstm_grads_reduce_multi_kernel, dim3(nb), dim3(256), 0, st, R);
     GQ_LAUNCH_CHECK();
   }
+}
+
+// Switch for the deferred split reductions (common.h defer_reduce_mode); returns the previous value.
+bool lstm_defer_reduce(bool flag) {
+  const bool old = defer_reduce_mode();
+  defer_reduce_mode() = flag;
+  return old;
+}
+
+// Every queued split reduction (lstm_grads_rows under defer_reduce_mode) in one launch per
+// MULTI_MAX jobs: each job's slot blocks are workgroups of lstm_grads_reduce_multi_kernel, so the
+// layers' reductions (7 launches of 9-36 us on the SoilNet step, all of them a tail of idle CUs)
+// run side by side. Same fixed summation order per slot as the per-layer reduce: deterministic.
+// Returns the number of reductions run.
+int64_t lstm_reduce_flush() {
+  auto& q = deferred_reds();
+  const int n = (int)q.size();
+  for (int k0 = 0; k0 < n; k0 += MULTI_MAX) {
+    const int kn = std::min(MULTI_MAX, n - k0);
+    MultiRed R{};
+    R.n = kn;
+    R.nf = nullptr;
+    int nb = 0;
+    for (int k = 0; k < kn; ++k) {
+      const DeferredRed& d = q[k0 + k];
+      RedJob& r = R.j[k];
+      r.H = d.H;
+      r.Din = d.Din;
+      r.DT = (r.Din + 1 + 15) / 16;
+      r.HT = r.H / 16;
+      r.ncb = lstm_grads_col_blocks(r.H);
+      r.RC = (r.DT + r.HT) * 1024 * r.ncb;
+      r.splits = d.splits;
+      TORCH_CHECK(d.ws.numel() >= (long)r.splits * r.RC, "lstm_reduce_flush: workspace size");
+      r.ws = d.ws.data_ptr<float>();
+      r.dW = d.dW;
+      r.dU = d.dU;
+      r.db = d.db;
+      r.kb = (r.RC + 15) / 16 > 1024 ? PIPE_RED_KB : 1;
+      r.nblocks = (r.RC + 16 * r.kb - 1) / (16 * r.kb);
+      R.start[k] = nb;
+      nb += r.nblocks;
+    }
+    R.start[kn] = nb;
+    c10::DeviceGuard guard(q[k0].ws.device());
+    hipLaunchKernelGGL(lstm_grads_reduce_multi_kernel, dim3(nb), dim3(256), 0, stream(), R);
+    GQ_LAUNCH_CHECK();
+  }
+  q.clear();       // workspaces return to the caching allocator in stream order
+  return n;
 }
 
 // Weight gradients (+ dx) of one time-major layer from its dz (lstm_grads_rows): accumulates

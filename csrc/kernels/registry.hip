@@ -7,6 +7,8 @@
 #include "common.h"
 
 namespace gq {
+bool lstm_defer_reduce(bool flag);      // lstm_tm.hip
+int64_t lstm_reduce_flush();
 // returns the previous value (see deterministic_mode in common.h)
 static bool set_deterministic(bool flag) {
   const bool old = deterministic_mode();
@@ -18,6 +20,8 @@ static bool set_deterministic(bool flag) {
 TORCH_LIBRARY(gnnqc, m) {
   // process-wide switches (catch-all kernels: no tensor arguments)
   m.def("set_deterministic(bool flag) -> bool", &gq::set_deterministic);
+  m.def("lstm_defer_reduce(bool flag) -> bool", &gq::lstm_defer_reduce);
+  m.def("lstm_reduce_flush() -> int", &gq::lstm_reduce_flush);
   // persistent LSTM recurrence (lstm.hip)
   m.def("lstm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train, bool bf16) -> Tensor[]");
   m.def("lstm_bwd(Tensor dh, Tensor gates, Tensor cseq, Tensor U, bool bf16) -> Tensor");

@@ -190,6 +190,30 @@ def _pipe_x_ok(x: torch.Tensor, Dw: int) -> bool:
 
 
 @contextlib.contextmanager
+def _deferred_reduce(on: bool):
+    """Queue the split reductions of the weight-gradient launches issued inside (direct
+    accumulation into the optimiser's gradient buffers only: nothing reads those before the
+    step's optimizer update) for :func:`direct_grad_accumulation`'s exit, which runs all of them
+    in one launch (``lstm_reduce_flush``) instead of one reduce launch per layer."""
+    import os
+    if not (on and _DirectGrad.enabled and os.environ.get("GNNQC_DEFER_REDUCE", "1") == "1"):
+        yield
+        return
+    from ..utils.native import hip_ops
+    ops = hip_ops()
+    prev = ops.lstm_defer_reduce(True)
+    _Deferred.pending = True
+    try:
+        yield
+    finally:
+        ops.lstm_defer_reduce(prev)
+
+
+class _Deferred:
+    pending = False     # split reductions queued in the native library (lstm_reduce_flush)
+
+
+@contextlib.contextmanager
 def direct_grad_accumulation(flag: bool = True):
     prev = _DirectGrad.enabled
     _DirectGrad.enabled = flag
@@ -200,6 +224,10 @@ def direct_grad_accumulation(flag: bool = True):
         if _Pipe.job is not None or _Pipe.red is not None or _Pipe.batch:
             pipe_flush()
         _Pipe.gcn = None
+        if _Deferred.pending:
+            from ..utils.native import hip_ops
+            _Deferred.pending = False
+            hip_ops().lstm_reduce_flush()
 
 
 def _grad_sink(p: torch.Tensor):
@@ -270,7 +298,8 @@ class _HipLSTM(torch.autograd.Function):
             dx = ops.lstm_dx(dz, Wc, x) if need_dx else None
             _pipe_push(_pipe_job(dz, x, h, Wc, ((gW, True), (gU, True), (gb, True)), T, 1))
             return dx, None, None, None, None, None
-        dx = ops.lstm_grads(dz, x, h, Wc, gW, gU, gb, need_dx)
+        with _deferred_reduce(dW_in and dU_in and db_in):
+            dx = ops.lstm_grads(dz, x, h, Wc, gW, gU, gb, need_dx)
         return (dx if need_dx else None,
                 None if dW_in or not ctx.needs_input_grad[1] else gW,
                 None if dU_in or not ctx.needs_input_grad[2] else gU,
@@ -296,8 +325,9 @@ def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx, pidx=Non
     if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
         dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx)
     else:
-        dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, sinks[0][0], sinks[1][0], sinks[2][0],
-                                   need_dx, pi, pool)
+        with _deferred_reduce(wgrad and all(d for _, d in sinks)):
+            dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, sinks[0][0], sinks[1][0],
+                                       sinks[2][0], need_dx, pi, pool)
     grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need_w)]
     return (dx if need_dx else None), grads
 

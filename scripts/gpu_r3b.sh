@@ -45,12 +45,22 @@ if [ "${SKIP_AR:-0}" != "1" ]; then
 fi
 [ "${NOPROF:-0}" = "1" ] && exit 0
 cd /tmp && export TMPDIR=/tmp
+if [ "${IGPROF:-0}" = "1" ]; then
+  step "rocprofv3 ig"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/profig -o run --output-format csv -- \
+    python3 $ROOT/scripts/bench_ig.py --batches 2 --max-rows 16384 > $OUT/profig.log 2>&1
+  rc=$?; echo "rocprof ig rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  f=$(ls $OUT/profig/run_kernel_stats.csv $OUT/profig/*/run_kernel_stats.csv 2>/dev/null | head -1)
+  [ -n "$f" ] && python3 $ROOT/scripts/prof_summary.py $f 3 30 > $OUT/ig_stats.txt && cat $OUT/ig_stats.txt
+fi
+[ "${SKIP_CML_PROF:-0}" = "1" ] || {
 step "rocprofv3 cml"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
   python3 $ROOT/bench.py --steps 48 --warmup 8 > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
 f=$(ls $OUT/prof/run_kernel_stats.csv $OUT/prof/*/run_kernel_stats.csv 2>/dev/null | head -1)
 [ -n "$f" ] && python3 $ROOT/scripts/prof_summary.py $f 56 30 > $OUT/cml_stats.txt && cat $OUT/cml_stats.txt
+}
 step "rocprofv3 soilnet"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/profs -o run --output-format csv -- \
   python3 $ROOT/bench.py --ds soilnet --steps 16 --warmup 8 > $OUT/profs.log 2>&1
