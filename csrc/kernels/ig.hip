@@ -123,9 +123,238 @@ at::Tensor ig_finalize(const at::Tensor& acc, const at::Tensor& v, int64_t mode)
   return out;
 }
 
+// =====================================================================================
+// Path-folded GeneralConv + BatchNorm (eval) + PReLU + node pooling for the CML GCN (K10: the
+// alpha scaling folded into the input load). The zero-baseline path point s of window b is
+// x_s = alpha_s x_b, so its GCN pre-activation is z = alpha_s (x_b W) + bias: x W is computed
+// ONCE per (window, step, node) and no kk x B copy of x (ig_interp: 430 MB per CML batch) or of
+// the static adjacency / mask tensors exists. Rows of the time-major LSTM input are step-major
+// (row = s * B + b), as the explainer's path batch.
+//
+// forward: out [T][Mp][Cp] = [alpha_s anom_b | sum_n w_bn prelu((alpha_s xW_bn + bias) sc + sh) | 0]
+// backward: the input gradients of every path point, trapezoid-weighted and summed over the
+// chunk's steps in ONE pass (ig_accum folded in, fixed step order: deterministic):
+//   acc_x[b,t,n,k]  += sum_s wt_s sum_f W[k,f] m_n w_bn sc_f prelu'(y) g_f(s)
+//   acc_a[b,t,c]    += sum_s wt_s g_c(s)           (g = dL/d out, rows s * B + b)
+// The workgroup of (t, 256 / F windows) first stages every step's output-gradient rows of its
+// windows (contiguous per step) in LDS, so all those loads are in flight at once.
+constexpr int IGG_NMAX = 32;      // nodes per window (lanes of the backward's node axis)
+constexpr int IGG_SCH = 32;       // path points staged per LDS pass of the backward
+
+template <int Cin, int F>
+__global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ anom,
+    const float* __restrict__ W, const float* __restrict__ bias, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ prelu_a, const float* __restrict__ alphas,
+    float* __restrict__ out, int B, int T, int N, int Ca, int kk, int Mp, int Cp) {
+  constexpr int BB = 256 / F;                       // windows per workgroup
+  const int f = threadIdx.x % F, bl = threadIdx.x / F;
+  const int t = blockIdx.y, b = blockIdx.x * BB + bl;
+  if (blockIdx.x == 0) {                            // zero the padding rows kk*B .. Mp-1 of step t
+    const long z0 = ((long)t * Mp + (long)kk * B) * Cp, z1 = ((long)t + 1) * Mp * Cp;
+    for (long e = z0 + threadIdx.x; e < z1; e += 256) out[e] = 0.f;
+  }
+  if (b >= B) return;
+  float wk[Cin];
+#pragma unroll
+  for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + f];
+  const float sc = scale[f], A0 = bias[f] * sc + shift[f], al = prelu_a[f];
+  // y_n(s) = alpha_s * xs_n + A0 with xs_n = (x_bn . W_f) sc
+  float xs[IGG_NMAX], wn[IGG_NMAX];
+  const float* xb = x + ((long)b * T + t) * (long)N * Cin;
+#pragma unroll
+  for (int n = 0; n < IGG_NMAX; ++n) {
+    float z = 0.f;
+    if (n < N) {
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) z += xb[n * Cin + k] * wk[k];
+    }
+    xs[n] = z * sc;
+    wn[n] = n < N ? w[(long)b * N + n] : 0.f;
+  }
+  const int ca = f < Ca ? f : 0;
+  const float a_in = Ca > 0 ? anom[((long)b * T + t) * Ca + ca] : 0.f;
+  for (int s = 0; s < kk; ++s) {
+    const float a = alphas[s];
+    float acc = 0.f;
+#pragma unroll
+    for (int n = 0; n < IGG_NMAX; ++n) {
+      const float y = a * xs[n] + A0;
+      acc += wn[n] * (y > 0.f ? y : al * y);
+    }
+    float* o = out + ((long)t * Mp + (long)s * B + b) * Cp;
+    o[Ca + f] = acc;
+    if (f < Ca) o[f] = a * a_in;
+    for (int c = Ca + F + f; c < Cp; c += F) o[c] = 0.f;
+  }
+}
+
+template <int Cin, int F>
+__global__ __launch_bounds__(256) void ig_gcn_pool_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ mask,
+    const float* __restrict__ g, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ prelu_a,
+    const float* __restrict__ alphas, const float* __restrict__ wts, float* __restrict__ acc_x,
+    float* __restrict__ acc_a, int B, int T, int N, int Ca, int kk, int Mp, int Cp) {
+  constexpr int BB = 256 / IGG_NMAX;                // windows per workgroup (lanes: node n)
+  extern __shared__ __attribute__((aligned(16))) float sg[];   // [IGG_SCH][BB][Cp]
+  __shared__ float sW[Cin][F], sA0[F], sSc[F], sAl[F];
+  const int n = threadIdx.x % IGG_NMAX, bl = threadIdx.x / IGG_NMAX;
+  const int t = blockIdx.y, b0 = blockIdx.x * BB, b = b0 + bl;
+  const int nb = min(BB, B - b0);
+  for (int e = threadIdx.x; e < Cin * F; e += 256) sW[e / F][e % F] = W[e];
+  for (int e = threadIdx.x; e < F; e += 256) {
+    sSc[e] = scale[e];
+    sA0[e] = bias[e] * scale[e] + shift[e];
+    sAl[e] = prelu_a[e];
+  }
+  __syncthreads();
+  const bool live = b < B && n < N;
+  float xv[Cin], xw[F];
+  float dxa[Cin];
+#pragma unroll
+  for (int k = 0; k < Cin; ++k) {
+    xv[k] = live ? x[(((long)b * T + t) * N + n) * Cin + k] : 0.f;
+    dxa[k] = 0.f;
+  }
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    float z = 0.f;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) z += xv[k] * sW[k][f];
+    xw[f] = z * sSc[f];                             // y_f(s) = alpha_s xw_f + A0_f
+  }
+  // m_n w_bn: the node's share of the pooled output (0 for masked / unpooled nodes)
+  const float mw = live ? (mask[(long)b * N + n] != 0.f ? 1.f : 0.f) * w[(long)b * N + n] : 0.f;
+  float da = 0.f;                                   // anomaly channel n (< Ca) of window b
+  const int row_elems = nb * Cp;                    // the workgroup's rows of one step: contiguous
+  for (int s0 = 0; s0 < kk; s0 += IGG_SCH) {
+    const int ns = min(IGG_SCH, kk - s0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * row_elems; e += 256) {
+      const int si = e / row_elems, r = e - si * row_elems;
+      sg[si * BB * Cp + r] = g[((long)t * Mp + (long)(s0 + si) * B + b0) * Cp + r];
+    }
+    __syncthreads();
+    if (b < B) {
+      for (int si = 0; si < ns; ++si) {
+        const float a = alphas[s0 + si], wt = wts[s0 + si];
+        const float* gr = sg + (si * BB + bl) * Cp;
+        if (n < Ca) da += wt * gr[n];
+        float d[Cin];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) d[k] = 0.f;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          const float y = a * xw[f] + sA0[f];
+          const float dz = sSc[f] * (y > 0.f ? 1.f : sAl[f]) * gr[Ca + f];
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) d[k] += sW[k][f] * dz;
+        }
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) dxa[k] += wt * d[k];
+      }
+    }
+  }
+  if (live) {
+    float* o = acc_x + (((long)b * T + t) * N + n) * Cin;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) o[k] += mw * dxa[k];
+  }
+  if (b < B && n < Ca) acc_a[((long)b * T + t) * Ca + n] += da;
+}
+
+#define GQ_IGG_DISPATCH(CIN_RT, F_RT, ...)                                                         \
+  do {                                                                                             \
+    if (CIN_RT == 2 && F_RT == 16) { constexpr int CIN = 2, FF = 16; __VA_ARGS__; }                \
+    else if (CIN_RT == 1 && F_RT == 16) { constexpr int CIN = 1, FF = 16; __VA_ARGS__; }           \
+    else if (CIN_RT == 3 && F_RT == 16) { constexpr int CIN = 3, FF = 16; __VA_ARGS__; }           \
+    else if (CIN_RT == 2 && F_RT == 32) { constexpr int CIN = 2, FF = 32; __VA_ARGS__; }           \
+    else if (CIN_RT == 2 && F_RT == 8) { constexpr int CIN = 2, FF = 8; __VA_ARGS__; }             \
+    else TORCH_CHECK(false, "ig_gcn_pool: unsupported Cin ", CIN_RT, " / F ", F_RT);               \
+  } while (0)
+
+bool ig_gcn_shape_ok(int64_t Cin, int64_t F, int64_t N) {
+  return N >= 1 && N <= IGG_NMAX &&
+         ((Cin == 2 && (F == 8 || F == 16 || F == 32)) || ((Cin == 1 || Cin == 3) && F == 16));
+}
+
+// x [B,T,N,Cin], w [B,N] pool weights (gcn_prep), anom [B,T,Ca] (or empty), st rows 2/3 = BN scale /
+// shift (eval), alphas [kk]. Returns [T, Mp, Cp] with Mp = kk*B rounded up to 16.
+at::Tensor ig_gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& anom, const at::Tensor& W,
+                           const at::Tensor& b, const at::Tensor& scale, const at::Tensor& shift,
+                           const at::Tensor& alpha, const at::Tensor& alphas, int64_t Cp) {
+  for (auto* p : {&x, &w, &W, &b, &scale, &shift, &alpha, &alphas}) check_f32_cuda(*p, "ig_gcn_pool_fwd input");
+  TORCH_CHECK(x.dim() == 4, "ig_gcn_pool_fwd: x must be [B,T,N,Cin]");
+  const int B = x.size(0), T = x.size(1), N = x.size(2), Cin = x.size(3), F = W.size(1);
+  TORCH_CHECK(ig_gcn_shape_ok(Cin, F, N) && W.size(0) == Cin, "ig_gcn_pool_fwd: unsupported shape");
+  TORCH_CHECK(w.size(0) == B && w.size(1) == N && b.numel() == F && scale.numel() == F && shift.numel() == F &&
+                  alpha.numel() == F, "ig_gcn_pool_fwd: parameter shapes");
+  int Ca = 0;
+  if (anom.numel() > 0) {
+    check_f32_cuda(anom, "anom");
+    TORCH_CHECK(anom.dim() == 3 && anom.size(0) == B && anom.size(1) == T, "ig_gcn_pool_fwd: anom must be [B,T,Ca]");
+    Ca = anom.size(2);
+  }
+  TORCH_CHECK(Ca <= F && Cp >= Ca + F, "ig_gcn_pool_fwd: Cp / Ca");
+  const int kk = (int)alphas.numel();
+  TORCH_CHECK(kk >= 1, "ig_gcn_pool_fwd: no path points");
+  const long Mp = ((long)kk * B + 15) / 16 * 16;
+  c10::DeviceGuard guard(x.device());
+  at::Tensor out = at::empty({T, Mp, Cp}, x.options());
+  GQ_IGG_DISPATCH(Cin, F,
+      hipLaunchKernelGGL((ig_gcn_pool_fwd_kernel<CIN, FF>), dim3((B + 256 / FF - 1) / (256 / FF), T), dim3(256), 0,
+                         stream(), x.data_ptr<float>(), w.data_ptr<float>(), Ca ? anom.data_ptr<float>() : nullptr,
+                         W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                         alpha.data_ptr<float>(), alphas.data_ptr<float>(), out.data_ptr<float>(), B, T, N, Ca, kk,
+                         (int)Mp, (int)Cp));
+  GQ_LAUNCH_CHECK();
+  return out;
+}
+
+// g = dL/d out [T, Mp, Cp] of ig_gcn_pool_fwd; accumulates into acc_x [B,T,N,Cin] and acc_a [B,T,Ca].
+void ig_gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& mask, const at::Tensor& g,
+                     const at::Tensor& W, const at::Tensor& b, const at::Tensor& scale, const at::Tensor& shift,
+                     const at::Tensor& alpha, const at::Tensor& alphas, const at::Tensor& wts, at::Tensor acc_x,
+                     at::Tensor acc_a) {
+  for (auto* p : {&x, &w, &mask, &g, &W, &b, &scale, &shift, &alpha, &alphas, &wts})
+    check_f32_cuda(*p, "ig_gcn_pool_bwd input");
+  check_f32_cuda(acc_x, "ig_gcn_pool_bwd acc_x");
+  const int B = x.size(0), T = x.size(1), N = x.size(2), Cin = x.size(3), F = W.size(1);
+  TORCH_CHECK(ig_gcn_shape_ok(Cin, F, N), "ig_gcn_pool_bwd: unsupported shape");
+  const int kk = (int)alphas.numel();
+  TORCH_CHECK(wts.numel() == kk && kk >= 1, "ig_gcn_pool_bwd: weights per path point");
+  TORCH_CHECK(acc_x.sizes() == x.sizes() && mask.numel() == (long)B * N && w.numel() == (long)B * N,
+              "ig_gcn_pool_bwd: accumulator / mask shapes");
+  TORCH_CHECK(g.dim() == 3 && g.size(0) == T && g.size(1) >= (long)kk * B, "ig_gcn_pool_bwd: g must be [T, Mp, Cp]");
+  const int Cp = g.size(2);
+  int Ca = 0;
+  if (acc_a.numel() > 0) {
+    check_f32_cuda(acc_a, "acc_a");
+    TORCH_CHECK(acc_a.dim() == 3 && acc_a.size(0) == B && acc_a.size(1) == T, "ig_gcn_pool_bwd: acc_a [B,T,Ca]");
+    Ca = acc_a.size(2);
+  }
+  TORCH_CHECK(Cp >= Ca + F && Ca <= IGG_NMAX, "ig_gcn_pool_bwd: Cp / Ca");
+  constexpr int BB = 256 / IGG_NMAX;
+  const size_t smem = (size_t)IGG_SCH * BB * Cp * sizeof(float);
+  TORCH_CHECK(smem <= 96 * 1024, "ig_gcn_pool_bwd: output rows too wide");
+  c10::DeviceGuard guard(x.device());
+  GQ_IGG_DISPATCH(Cin, F,
+      hipLaunchKernelGGL((ig_gcn_pool_bwd_kernel<CIN, FF>), dim3((B + BB - 1) / BB, T), dim3(256), smem, stream(),
+                         x.data_ptr<float>(), w.data_ptr<float>(), mask.data_ptr<float>(), g.data_ptr<float>(),
+                         W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                         alpha.data_ptr<float>(), alphas.data_ptr<float>(), wts.data_ptr<float>(),
+                         acc_x.data_ptr<float>(), Ca ? acc_a.data_ptr<float>() : nullptr, B, T, N, Ca, kk,
+                         (int)g.size(1), Cp));
+  GQ_LAUNCH_CHECK();
+}
+#undef GQ_IGG_DISPATCH
+
 }  // namespace gq
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
+  m.impl("ig_gcn_pool_fwd", &gq::ig_gcn_pool_fwd);
+  m.impl("ig_gcn_pool_bwd", &gq::ig_gcn_pool_bwd);
   m.impl("ig_interp", &gq::ig_interp);
   m.impl("ig_accum", &gq::ig_accum);
   m.impl("ig_finalize", &gq::ig_finalize);

@@ -46,16 +46,18 @@ void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows,
 // =====================================================================================
 // forward
 // x: [T][Mp][Din]  hout: [T][Mp][H]  gbuf: [T][tiles][NW][CPL][64][4]  cbuf: [..][64]
-// 1024-thread workgroups (H = 64) ask for 8 waves per SIMD, i.e. two workgroups per CU: at the
-// default allocation (~80 VGPRs) only one fits, and a 418-tile grid (SoilNet, 6,688 sequences)
-// then runs in two rounds on 256 CUs.
-template <int NT>
+// 1024-thread workgroups ask for 8 waves per SIMD, i.e. two workgroups per CU (at the default
+// allocation, ~70-80 VGPRs, only one fits and a 418-tile grid - SoilNet, 6,688 sequences - runs in
+// two rounds on 256 CUs) where that costs no spills: the H = 64 layer with a 32-channel input
+// (70.6 vs 76.7 us on the SoilNet step) and the H = 32 pair (214.5 vs 221.5 us). The 64-channel
+// input variant spills at 64 VGPRs (169 vs 105 us) and keeps the default.
+template <int NT, int KX = 1>
 struct TmOcc {
-  static constexpr int W = NT >= 1024 ? 8 : 1;
+  static constexpr int W = (NT >= 1024 && KX == 1) ? 8 : 1;
 };
 
 template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
-__global__ __launch_bounds__(TMC<H>::NT, TmOcc<TMC<H>::NT>::W) void lstm_tm_fwd_kernel(
+__global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hout, __bf16* __restrict__ gbuf,
     float* __restrict__ cbuf, int Mp, int T, int Din, int Dw, float* __restrict__ pout,
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(TMC<H>::NT, TmOcc<TMC<H>::NT>::W) void lstm_tm_fwd_
 // of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
 // (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
 template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
-__global__ __launch_bounds__(2 * TMC<H>::NT, TmOcc<2 * TMC<H>::NT>::W) void lstm_tm2_fwd_kernel(
+__global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
     const float* __restrict__ bB, float* __restrict__ hA, __bf16* __restrict__ gA, float* __restrict__ cA,

@@ -117,6 +117,10 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor(h!)? cursor=None, int cursor_mod=1) -> ()");
   m.def("nonfinite_count(Tensor x) -> Tensor");
   m.def("ig_interp(Tensor v, Tensor alpha) -> Tensor");
+  m.def("ig_gcn_pool_fwd(Tensor x, Tensor w, Tensor anom, Tensor W, Tensor b, Tensor scale, Tensor shift, "
+        "Tensor alpha, Tensor alphas, int Cp) -> Tensor");
+  m.def("ig_gcn_pool_bwd(Tensor x, Tensor w, Tensor mask, Tensor g, Tensor W, Tensor b, Tensor scale, Tensor shift, "
+        "Tensor alpha, Tensor alphas, Tensor wts, Tensor(a!) acc_x, Tensor(b!) acc_a) -> ()");
   m.def("ig_accum(Tensor(a!) acc, Tensor g, Tensor w) -> ()");
   m.def("ig_finalize(Tensor acc, Tensor v, int mode) -> Tensor");
   m.def("chain_poison(Tensor(a!) g, Tensor ext) -> ()");

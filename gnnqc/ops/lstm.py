@@ -681,8 +681,9 @@ class _HipLSTMTM(torch.autograd.Function):
         if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
             dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
         else:
-            dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
-                                       sinks[0][0], sinks[1][0], sinks[2][0], need_dx, pi, pool)
+            with _deferred_reduce(wgrad and all(d for _, d in sinks)):
+                dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
+                                           sinks[0][0], sinks[1][0], sinks[2][0], need_dx, pi, pool)
         grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
         return (dx if need_dx else None, *grads, None, None)
 
@@ -733,11 +734,12 @@ class _HipLSTMTMPair(torch.autograd.Function):
             dhA = _pipe_tm_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
             dx = _pipe_tm_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
-            dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
-                                  sB[0][0], sB[1][0], sB[2][0], True, pi, pool)
-            if need_dx or any(need[1:4]):
-                dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0],
-                                     sA[2][0], need_dx)
+            with _deferred_reduce(all(d for _, d in sB) and all(d for _, d in sA)):
+                dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
+                                      sB[0][0], sB[1][0], sB[2][0], True, pi, pool)
+                if need_dx or any(need[1:4]):
+                    dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0],
+                                         sA[2][0], need_dx)
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
         return (dx if need_dx else None, *gA_, *gB_, None)

@@ -141,8 +141,12 @@ class IntegratedGradients:
         k = max(1, min(self.m_steps + 1, self.max_rows // max(B, 1)))
         hip = _ig_hip(vals[0])
         vf = [v.to(dt).contiguous() for v in vals]
+        fused = hip and self._cml_path_folded_ok(batch)
         with _frozen(model), torch.enable_grad():
-            for s in range(0, self.m_steps + 1, k):
+            for s in (range(0, self.m_steps + 1, k) if fused else ()):
+                self._cml_path_folded_chunk(batch, alphas[s:s + k].contiguous(), wts[s:s + k].contiguous(),
+                                            acc, path_pred[s:s + k], target)
+            for s in (range(0, self.m_steps + 1, k) if not fused else ()):
                 a = alphas[s:s + k]
                 kk = a.numel()
                 # zero baseline: x_alpha = alpha * x, folded into the batch dimension (HIP: one
@@ -188,6 +192,62 @@ class IntegratedGradients:
         else:
             res["grad_x"] = acc[0]
         return res
+
+
+    # -- CML GCN on the GPU: the alpha scaling folded into the GCN kernels ---------------
+    def _cml_path_folded_ok(self, batch) -> bool:
+        """The CML GCN's path-folded IG (``ig_gcn_pool_fwd`` / ``ig_gcn_pool_bwd``): the path
+        points' GCN + pooling computed from the un-replicated batch, their input gradients
+        trapezoid-summed in the same backward launch (no kk x B copies of x, anom, adj, mask)."""
+        m = self.model
+        if self.is_baseline or not self.per_sensor or type(m).__name__ != "GCNClassifier" or m.training:
+            return False
+        if getattr(m, "sensors_time_layer", None) is not None or getattr(m, "spatial_transformer", None) is not None:
+            return False
+        x, anom = batch.x, batch.anom
+        if x.dtype != torch.float32 or anom is None or not m._fused_ok():
+            return False
+        inputs = (x, anom, batch.adj, batch.node_mask, batch.anom_pos)
+        if not m._cml_time_major(inputs):
+            return False
+        g = m.gcn_layer
+        cin, F, N = x.shape[-1], g.kernel.shape[1], x.shape[2]
+        shape_ok = N <= 32 and ((cin == 2 and F in (8, 16, 32)) or (cin in (1, 3) and F == 16))
+        return bool(shape_ok and anom.shape[-1] <= F and not (g.dropout and m.training))
+
+    def _cml_path_folded_chunk(self, batch, a: torch.Tensor, wt: torch.Tensor, acc, path_pred_rows,
+                               target: Optional[torch.Tensor]):
+        """One chunk of path points: GCN forward of all of them (one launch), the TimeLayer + head
+        on the path batch, one backward to the LSTM input, then one launch that turns that gradient
+        into the trapezoid-weighted input gradients of x and anom (accumulated into ``acc``)."""
+        m = self.model
+        ops = _ops()
+        g = m.gcn_layer
+        x = batch.x.contiguous()
+        anom = batch.anom.float().contiguous()
+        mask = batch.node_mask.float().contiguous()
+        B = x.shape[0]
+        kk = a.numel()
+        pooling = "selection" if m.pooling_type == "selection" else m.aggregation_type
+        ap = (batch.anom_pos.long().contiguous() if (pooling == "selection" and batch.anom_pos is not None)
+              else x.new_zeros(0))
+        with torch.no_grad():
+            w, _S, st = ops.gcn_prep(x, batch.adj.float().contiguous(), mask, ap, g.aggregate == "mean",
+                                     {"mean": 0, "sum": 1, "selection": 2}[pooling], g.kernel.contiguous(),
+                                     g.bias.contiguous(), g.bn_gamma.contiguous(), g.bn_beta.contiguous(),
+                                     g.bn_moving_mean, g.bn_moving_variance, False, float(g.momentum), float(g.eps))
+            Cp = g.kernel.shape[1] + anom.shape[-1]
+            Cp += (-Cp) % 4
+            h0 = ops.ig_gcn_pool_fwd(x, w, anom, g.kernel.contiguous(), g.bias.contiguous(), st[2].contiguous(),
+                                     st[3].contiguous(), g.prelu_alpha.contiguous(), a, int(Cp))
+        h0.requires_grad_(True)
+        out = torch.sigmoid(m.head(m.time_layer.forward_time_major(h0, kk * B)))
+        y = self._select(out, B, kk, target)
+        (gh,) = torch.autograd.grad(y.sum(), h0)
+        path_pred_rows.copy_(y.detach().view(kk, B).to(path_pred_rows.dtype))
+        ops.ig_gcn_pool_bwd(x, w, mask, gh.contiguous(), g.kernel.contiguous(), g.bias.contiguous(),
+                            st[2].contiguous(), st[3].contiguous(), g.prelu_alpha.contiguous(), a, wt.float(),
+                            acc[0], acc[1])
 
 
 def completeness_gap(ig_res: Dict[str, torch.Tensor]) -> torch.Tensor:

@@ -69,3 +69,34 @@ def test_ig_hip_kernels_match_torch(cuda_device):
     for mode, fn in ((0, lambda t: t), (1, lambda t: t.clamp(min=0)), (2, torch.abs)):
         torch.testing.assert_close(ops.ig_finalize(acc, v, mode), fn(acc * v))
     torch.testing.assert_close(ops.ig_finalize(acc, v.new_zeros(0), 0), acc)
+
+
+def test_ig_path_folded_gcn_matches_replicated_path(cuda_device, cml_windows, monkeypatch):
+    """The CML GCN's path-folded IG (alpha applied inside ig_gcn_pool_fwd, input gradients
+    trapezoid-summed inside ig_gcn_pool_bwd) == the generic path over kk x B interpolated copies
+    (ig_interp -> GCN kernels -> ig_accum), with several path chunks (max_rows < (m+1) B)."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.xai.ig import IntegratedGradients
+    pc, ws = cml_windows
+    torch.manual_seed(3)
+    model = GCNClassifier(C.default("model_cml"), pc).to(cuda_device)
+    with torch.no_grad():
+        model.dense_out.bias.fill_(0.2)
+        model.gcn_layer.bn_moving_mean.normal_(0, 0.3)
+        model.gcn_layer.bn_moving_variance.uniform_(0.5, 2.0)
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    b = st.gather(torch.tensor([1, 5, 11, 23, 40], device=cuda_device))
+    ig = IntegratedGradients(model, "cml", m_steps=30, max_rows=5 * 8)
+    model.eval()                               # (attribute() switches to eval itself)
+    assert ig._cml_path_folded_ok(b)
+    model.train()
+    got = ig.attribute(b)
+    monkeypatch.setattr(IntegratedGradients, "_cml_path_folded_ok", lambda self, batch: False)
+    ref = IntegratedGradients(model, "cml", m_steps=30, max_rows=5 * 8).attribute(b)
+    torch.cuda.synchronize()
+    for k in ("grad_x", "grad_anom", "pred", "path_pred"):
+        err = (got[k] - ref[k]).abs().max().item()
+        scale = ref[k].abs().max().item()
+        assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
