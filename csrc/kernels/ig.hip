@@ -141,6 +141,8 @@ at::Tensor ig_finalize(const at::Tensor& acc, const at::Tensor& v, int64_t mode)
 constexpr int IGG_NMAX = 32;      // nodes per window (lanes of the backward's node axis)
 constexpr int IGG_SCH = 32;       // path points staged per LDS pass of the backward
 
+constexpr int IGG_FSG = 8;        // path points per coalesced store pass of the forward
+
 template <int Cin, int F>
 __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ anom,
@@ -148,20 +150,22 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
     const float* __restrict__ shift, const float* __restrict__ prelu_a, const float* __restrict__ alphas,
     float* __restrict__ out, int B, int T, int N, int Ca, int kk, int Mp, int Cp) {
   constexpr int BB = 256 / F;                       // windows per workgroup
+  extern __shared__ __attribute__((aligned(16))) float so[];   // [IGG_FSG][BB][Cp] output rows
   const int f = threadIdx.x % F, bl = threadIdx.x / F;
-  const int t = blockIdx.y, b = blockIdx.x * BB + bl;
+  const int t = blockIdx.y, b0 = blockIdx.x * BB, b = b0 + bl;
+  const int nb = min(BB, B - b0);
   if (blockIdx.x == 0) {                            // zero the padding rows kk*B .. Mp-1 of step t
     const long z0 = ((long)t * Mp + (long)kk * B) * Cp, z1 = ((long)t + 1) * Mp * Cp;
     for (long e = z0 + threadIdx.x; e < z1; e += 256) out[e] = 0.f;
   }
-  if (b >= B) return;
+  const bool live = b < B;
   float wk[Cin];
 #pragma unroll
   for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + f];
   const float sc = scale[f], A0 = bias[f] * sc + shift[f], al = prelu_a[f];
   // y_n(s) = alpha_s * xs_n + A0 with xs_n = (x_bn . W_f) sc
   float xs[IGG_NMAX], wn[IGG_NMAX];
-  const float* xb = x + ((long)b * T + t) * (long)N * Cin;
+  const float* xb = x + ((long)(live ? b : 0) * T + t) * (long)N * Cin;
 #pragma unroll
   for (int n = 0; n < IGG_NMAX; ++n) {
     float z = 0.f;
@@ -170,22 +174,34 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
       for (int k = 0; k < Cin; ++k) z += xb[n * Cin + k] * wk[k];
     }
     xs[n] = z * sc;
-    wn[n] = n < N ? w[(long)b * N + n] : 0.f;
+    wn[n] = (live && n < N) ? w[(long)b * N + n] : 0.f;
   }
-  const int ca = f < Ca ? f : 0;
-  const float a_in = Ca > 0 ? anom[((long)b * T + t) * Ca + ca] : 0.f;
-  for (int s = 0; s < kk; ++s) {
-    const float a = alphas[s];
-    float acc = 0.f;
+  const float a_in = (live && f < Ca) ? anom[((long)b * T + t) * Ca + f] : 0.f;
+  const int rowf = nb * Cp;                         // floats of one step's rows (contiguous)
+  for (int s0 = 0; s0 < kk; s0 += IGG_FSG) {
+    const int ns = min(IGG_FSG, kk - s0);
+    for (int si = 0; si < ns; ++si) {
+      const float a = alphas[s0 + si];
+      float acc = 0.f;
 #pragma unroll
-    for (int n = 0; n < IGG_NMAX; ++n) {
-      const float y = a * xs[n] + A0;
-      acc += wn[n] * (y > 0.f ? y : al * y);
+      for (int n = 0; n < IGG_NMAX; ++n) {
+        const float y = a * xs[n] + A0;
+        acc += wn[n] * (y > 0.f ? y : al * y);
+      }
+      float* o = so + (si * BB + bl) * Cp;
+      o[Ca + f] = acc;
+      if (f < Ca) o[f] = a * a_in;
+      for (int c = Ca + F + f; c < Cp; c += F) o[c] = 0.f;
     }
-    float* o = out + ((long)t * Mp + (long)s * B + b) * Cp;
-    o[Ca + f] = acc;
-    if (f < Ca) o[f] = a * a_in;
-    for (int c = Ca + F + f; c < Cp; c += F) o[c] = 0.f;
+    __syncthreads();
+    // coalesced float4 stores of the ns x nb rows (Cp % 4 == 0: every row starts 16-byte aligned)
+    const int r4 = rowf / 4;
+    for (int e = threadIdx.x; e < ns * r4; e += 256) {
+      const int si = e / r4, q = e - si * r4;
+      const float4 v = reinterpret_cast<const float4*>(so + si * BB * Cp)[q];
+      reinterpret_cast<float4*>(out + ((long)t * Mp + (long)(s0 + si) * B + b0) * Cp)[q] = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -197,33 +213,38 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_bwd_kernel(
     const float* __restrict__ alphas, const float* __restrict__ wts, float* __restrict__ acc_x,
     float* __restrict__ acc_a, int B, int T, int N, int Ca, int kk, int Mp, int Cp) {
   constexpr int BB = 256 / IGG_NMAX;                // windows per workgroup (lanes: node n)
-  extern __shared__ __attribute__((aligned(16))) float sg[];   // [IGG_SCH][BB][Cp]
-  __shared__ float sW[Cin][F], sA0[F], sSc[F], sAl[F];
+  // staged output gradients of IGG_SCH path points: GCN channels [s][b][F] (16-byte rows: four
+  // broadcast ds_read_b128 per step) and anomaly channels [s][b][4]
+  extern __shared__ __attribute__((aligned(16))) float sg[];
+  float* sga = sg + IGG_SCH * BB * F;
   const int n = threadIdx.x % IGG_NMAX, bl = threadIdx.x / IGG_NMAX;
   const int t = blockIdx.y, b0 = blockIdx.x * BB, b = b0 + bl;
   const int nb = min(BB, B - b0);
-  for (int e = threadIdx.x; e < Cin * F; e += 256) sW[e / F][e % F] = W[e];
-  for (int e = threadIdx.x; e < F; e += 256) {
-    sSc[e] = scale[e];
-    sA0[e] = bias[e] * scale[e] + shift[e];
-    sAl[e] = prelu_a[e];
-  }
-  __syncthreads();
   const bool live = b < B && n < N;
-  float xv[Cin], xw[F];
+  // per node: y_f(s) = alpha_s xw_f + A0_f; dz_f = sc_f prelu'(y_f) g_f; dx_k = sum_f W_kf dz_f
+  float xw[F], A0[F], al[F], Wp[Cin][F];
+  {
+    float xv[Cin];
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) xv[k] = live ? x[(((long)b * T + t) * N + n) * Cin + k] : 0.f;
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const float sc = scale[f];
+      float z = 0.f;
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) {
+        const float wkf = W[k * F + f];
+        z += xv[k] * wkf;
+        Wp[k][f] = wkf * sc;
+      }
+      xw[f] = z * sc;
+      A0[f] = bias[f] * sc + shift[f];
+      al[f] = prelu_a[f];
+    }
+  }
   float dxa[Cin];
 #pragma unroll
-  for (int k = 0; k < Cin; ++k) {
-    xv[k] = live ? x[(((long)b * T + t) * N + n) * Cin + k] : 0.f;
-    dxa[k] = 0.f;
-  }
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    float z = 0.f;
-#pragma unroll
-    for (int k = 0; k < Cin; ++k) z += xv[k] * sW[k][f];
-    xw[f] = z * sSc[f];                             // y_f(s) = alpha_s xw_f + A0_f
-  }
+  for (int k = 0; k < Cin; ++k) dxa[k] = 0.f;
   // m_n w_bn: the node's share of the pooled output (0 for masked / unpooled nodes)
   const float mw = live ? (mask[(long)b * N + n] != 0.f ? 1.f : 0.f) * w[(long)b * N + n] : 0.f;
   float da = 0.f;                                   // anomaly channel n (< Ca) of window b
@@ -233,23 +254,32 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_bwd_kernel(
     __syncthreads();
     for (int e = threadIdx.x; e < ns * row_elems; e += 256) {
       const int si = e / row_elems, r = e - si * row_elems;
-      sg[si * BB * Cp + r] = g[((long)t * Mp + (long)(s0 + si) * B + b0) * Cp + r];
+      const int rb = r / Cp, c = r - rb * Cp;
+      const float v = g[((long)t * Mp + (long)(s0 + si) * B + b0) * Cp + r];
+      if (c >= Ca && c < Ca + F) sg[(si * BB + rb) * F + (c - Ca)] = v;
+      else if (c < Ca) sga[(si * BB + rb) * 4 + c] = v;
     }
     __syncthreads();
     if (b < B) {
       for (int si = 0; si < ns; ++si) {
         const float a = alphas[s0 + si], wt = wts[s0 + si];
-        const float* gr = sg + (si * BB + bl) * Cp;
-        if (n < Ca) da += wt * gr[n];
+        const float4* gr = reinterpret_cast<const float4*>(sg + (si * BB + bl) * F);
+        if (n < Ca) da += wt * sga[(si * BB + bl) * 4 + n];
         float d[Cin];
 #pragma unroll
         for (int k = 0; k < Cin; ++k) d[k] = 0.f;
 #pragma unroll
-        for (int f = 0; f < F; ++f) {
-          const float y = a * xw[f] + sA0[f];
-          const float dz = sSc[f] * (y > 0.f ? 1.f : sAl[f]) * gr[Ca + f];
+        for (int f4 = 0; f4 < F / 4; ++f4) {
+          const float4 g4 = gr[f4];
+          const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
-          for (int k = 0; k < Cin; ++k) d[k] += sW[k][f] * dz;
+          for (int u = 0; u < 4; ++u) {
+            const int f = 4 * f4 + u;
+            const float y = a * xw[f] + A0[f];
+            const float tz = (y > 0.f ? 1.f : al[f]) * gv[u];
+#pragma unroll
+            for (int k = 0; k < Cin; ++k) d[k] += Wp[k][f] * tz;
+          }
         }
 #pragma unroll
         for (int k = 0; k < Cin; ++k) dxa[k] += wt * d[k];
@@ -296,15 +326,15 @@ at::Tensor ig_gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::T
     TORCH_CHECK(anom.dim() == 3 && anom.size(0) == B && anom.size(1) == T, "ig_gcn_pool_fwd: anom must be [B,T,Ca]");
     Ca = anom.size(2);
   }
-  TORCH_CHECK(Ca <= F && Cp >= Ca + F, "ig_gcn_pool_fwd: Cp / Ca");
+  TORCH_CHECK(Ca <= F && Cp >= Ca + F && Cp % 4 == 0, "ig_gcn_pool_fwd: Cp / Ca");
   const int kk = (int)alphas.numel();
   TORCH_CHECK(kk >= 1, "ig_gcn_pool_fwd: no path points");
   const long Mp = ((long)kk * B + 15) / 16 * 16;
   c10::DeviceGuard guard(x.device());
   at::Tensor out = at::empty({T, Mp, Cp}, x.options());
   GQ_IGG_DISPATCH(Cin, F,
-      hipLaunchKernelGGL((ig_gcn_pool_fwd_kernel<CIN, FF>), dim3((B + 256 / FF - 1) / (256 / FF), T), dim3(256), 0,
-                         stream(), x.data_ptr<float>(), w.data_ptr<float>(), Ca ? anom.data_ptr<float>() : nullptr,
+      hipLaunchKernelGGL((ig_gcn_pool_fwd_kernel<CIN, FF>), dim3((B + 256 / FF - 1) / (256 / FF), T), dim3(256),
+                         (size_t)IGG_FSG * (256 / FF) * Cp * sizeof(float), stream(), x.data_ptr<float>(), w.data_ptr<float>(), Ca ? anom.data_ptr<float>() : nullptr,
                          W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
                          alpha.data_ptr<float>(), alphas.data_ptr<float>(), out.data_ptr<float>(), B, T, N, Ca, kk,
                          (int)Mp, (int)Cp));
@@ -334,10 +364,9 @@ void ig_gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor&
     TORCH_CHECK(acc_a.dim() == 3 && acc_a.size(0) == B && acc_a.size(1) == T, "ig_gcn_pool_bwd: acc_a [B,T,Ca]");
     Ca = acc_a.size(2);
   }
-  TORCH_CHECK(Cp >= Ca + F && Ca <= IGG_NMAX, "ig_gcn_pool_bwd: Cp / Ca");
+  TORCH_CHECK(Cp >= Ca + F && Ca <= 4 && F % 4 == 0, "ig_gcn_pool_bwd: Cp / Ca");
   constexpr int BB = 256 / IGG_NMAX;
-  const size_t smem = (size_t)IGG_SCH * BB * Cp * sizeof(float);
-  TORCH_CHECK(smem <= 96 * 1024, "ig_gcn_pool_bwd: output rows too wide");
+  const size_t smem = (size_t)IGG_SCH * BB * (F + 4) * sizeof(float);
   c10::DeviceGuard guard(x.device());
   GQ_IGG_DISPATCH(Cin, F,
       hipLaunchKernelGGL((ig_gcn_pool_bwd_kernel<CIN, FF>), dim3((B + BB - 1) / BB, T), dim3(256), smem, stream(),

@@ -100,3 +100,27 @@ def test_ig_path_folded_gcn_matches_replicated_path(cuda_device, cml_windows, mo
         err = (got[k] - ref[k]).abs().max().item()
         scale = ref[k].abs().max().item()
         assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
+
+
+def test_ig_graph_replay_matches_eager(cuda_device, cml_windows):
+    """The path-folded IG replays one HIP graph per input shape: a second batch of the same shape
+    (inputs copied into the captured buffers) gives what the eager attribution gives."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.xai.ig import IntegratedGradients
+    pc, ws = cml_windows
+    torch.manual_seed(5)
+    model = GCNClassifier(C.default("model_cml"), pc).to(cuda_device)
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    b1 = st.gather(torch.tensor([2, 9, 17], device=cuda_device))
+    b2 = st.gather(torch.tensor([4, 12, 30], device=cuda_device))
+    ig = IntegratedGradients(model, "cml", m_steps=20)
+    ig.attribute(b1)
+    assert ig._graph is not None
+    got = ig.attribute(b2)
+    ref = IntegratedGradients(model, "cml", m_steps=20, use_graph=False).attribute(b2)
+    torch.cuda.synchronize()
+    for k in ("grad_x", "grad_anom", "pred", "path_pred"):
+        err = (got[k] - ref[k]).abs().max().item()
+        assert err <= 1e-5 * ref[k].abs().max().item() + 1e-7, (k, err)
