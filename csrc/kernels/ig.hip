@@ -143,7 +143,7 @@ constexpr int IGG_SCH = 32;       // path points staged per LDS pass of the back
 
 constexpr int IGG_FSG = 8;        // path points per coalesced store pass of the forward
 
-template <int Cin, int F>
+template <int Cin, int F, int NM>                  // NM >= N: node slots (unrolled)
 __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ anom,
     const float* __restrict__ W, const float* __restrict__ bias, const float* __restrict__ scale,
@@ -164,10 +164,10 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
   for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + f];
   const float sc = scale[f], A0 = bias[f] * sc + shift[f], al = prelu_a[f];
   // y_n(s) = alpha_s * xs_n + A0 with xs_n = (x_bn . W_f) sc
-  float xs[IGG_NMAX], wn[IGG_NMAX];
+  float xs[NM], wn[NM];
   const float* xb = x + ((long)(live ? b : 0) * T + t) * (long)N * Cin;
 #pragma unroll
-  for (int n = 0; n < IGG_NMAX; ++n) {
+  for (int n = 0; n < NM; ++n) {
     float z = 0.f;
     if (n < N) {
 #pragma unroll
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
       const float a = alphas[s0 + si];
       float acc = 0.f;
 #pragma unroll
-      for (int n = 0; n < IGG_NMAX; ++n) {
+      for (int n = 0; n < NM; ++n) {
         const float y = a * xs[n] + A0;
         acc += wn[n] * (y > 0.f ? y : al * y);
       }
@@ -205,93 +205,93 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
   }
 }
 
+// Backward in closed form over the path. For a node n and channel f, y(s) = alpha_s xw + A0 is
+// monotone in s (alphas ascending), so prelu'(y(s)) takes one value c0 before a single flip index j
+// and another, c1, after it. With the prefix sums P(j) = sum_{s<j} wt_s g_f(s) (Q = P(kk)):
+//   sum_s wt_s prelu'(y(s)) g_f(s) = c0 P(j) + c1 (Q - P(j)),
+// j found by a binary search on the same predicate (y > 0, same fma) the forward evaluated. Per
+// (window, step) that is kk F prefix adds + N F log2(kk) compares instead of N F kk terms.
+constexpr int IGG_KMAX = 128;     // path points per launch (the host splits longer chunks)
+constexpr int IGG_BWB = 4;        // windows per backward workgroup (128 threads: lanes = nodes)
+
 template <int Cin, int F>
-__global__ __launch_bounds__(256) void ig_gcn_pool_bwd_kernel(
+__global__ __launch_bounds__(IGG_BWB * IGG_NMAX) void ig_gcn_pool_bwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ mask,
     const float* __restrict__ g, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ prelu_a,
     const float* __restrict__ alphas, const float* __restrict__ wts, float* __restrict__ acc_x,
-    float* __restrict__ acc_a, int B, int T, int N, int Ca, int kk, int Mp, int Cp) {
-  constexpr int BB = 256 / IGG_NMAX;                // windows per workgroup (lanes: node n)
-  // staged output gradients of IGG_SCH path points: GCN channels [s][b][F] (16-byte rows: four
-  // broadcast ds_read_b128 per step) and anomaly channels [s][b][4]
-  extern __shared__ __attribute__((aligned(16))) float sg[];
-  float* sga = sg + IGG_SCH * BB * F;
-  const int n = threadIdx.x % IGG_NMAX, bl = threadIdx.x / IGG_NMAX;
-  const int t = blockIdx.y, b0 = blockIdx.x * BB, b = b0 + bl;
-  const int nb = min(BB, B - b0);
-  const bool live = b < B && n < N;
-  // per node: y_f(s) = alpha_s xw_f + A0_f; dz_f = sc_f prelu'(y_f) g_f; dx_k = sum_f W_kf dz_f
-  float xw[F], A0[F], al[F], Wp[Cin][F];
-  {
-    float xv[Cin];
-#pragma unroll
-    for (int k = 0; k < Cin; ++k) xv[k] = live ? x[(((long)b * T + t) * N + n) * Cin + k] : 0.f;
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      const float sc = scale[f];
-      float z = 0.f;
-#pragma unroll
-      for (int k = 0; k < Cin; ++k) {
-        const float wkf = W[k * F + f];
-        z += xv[k] * wkf;
-        Wp[k][f] = wkf * sc;
+    float* __restrict__ acc_a, int B, int T, int N, int Ca, int kk, int s_off, int Mp, int Cp) {
+  constexpr int PC = F + 4;                         // prefix channels: F GCN + 4 anomaly slots
+  extern __shared__ __attribute__((aligned(16))) float sP[];   // [IGG_BWB][kk + 1][PC]
+  __shared__ float sA[IGG_KMAX];
+  const int tid = threadIdx.x;
+  const int n = tid % IGG_NMAX, bl = tid / IGG_NMAX;
+  const int t = blockIdx.y, b0 = blockIdx.x * IGG_BWB, b = b0 + bl;
+  const int rowp = (kk + 1) * PC;
+  for (int e = tid; e < kk; e += IGG_BWB * IGG_NMAX) sA[e] = alphas[e];
+  // prefix sums over the path points of wt_s g_c(s): thread (window, channel)
+  for (int e = tid; e < IGG_BWB * PC; e += IGG_BWB * IGG_NMAX) {
+    const int wb = e / PC, c = e - wb * PC, bb = b0 + wb;
+    const int ch = c < F ? Ca + c : (c - F < Ca ? c - F : -1);
+    float* P = sP + wb * rowp + c;
+    float acc = 0.f;
+    P[0] = 0.f;
+    if (bb < B && ch >= 0) {
+      const float* gp = g + ((long)t * Mp + (long)s_off * B + bb) * Cp + ch;
+      const long stride = (long)B * Cp;
+#pragma unroll 8
+      for (int s = 0; s < kk; ++s) {
+        acc += wts[s] * gp[s * stride];
+        P[(s + 1) * PC] = acc;
       }
-      xw[f] = z * sc;
-      A0[f] = bias[f] * sc + shift[f];
-      al[f] = prelu_a[f];
+    } else {
+      for (int s = 0; s < kk; ++s) P[(s + 1) * PC] = 0.f;
     }
   }
-  float dxa[Cin];
+  __syncthreads();
+  if (b >= B) return;
+  const float* P = sP + bl * rowp;
+  if (n < Ca) acc_a[((long)b * T + t) * Ca + n] += P[kk * PC + F + n];
+  if (n >= N) return;
+  float xv[Cin];
 #pragma unroll
-  for (int k = 0; k < Cin; ++k) dxa[k] = 0.f;
-  // m_n w_bn: the node's share of the pooled output (0 for masked / unpooled nodes)
-  const float mw = live ? (mask[(long)b * N + n] != 0.f ? 1.f : 0.f) * w[(long)b * N + n] : 0.f;
-  float da = 0.f;                                   // anomaly channel n (< Ca) of window b
-  const int row_elems = nb * Cp;                    // the workgroup's rows of one step: contiguous
-  for (int s0 = 0; s0 < kk; s0 += IGG_SCH) {
-    const int ns = min(IGG_SCH, kk - s0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < ns * row_elems; e += 256) {
-      const int si = e / row_elems, r = e - si * row_elems;
-      const int rb = r / Cp, c = r - rb * Cp;
-      const float v = g[((long)t * Mp + (long)(s0 + si) * B + b0) * Cp + r];
-      if (c >= Ca && c < Ca + F) sg[(si * BB + rb) * F + (c - Ca)] = v;
-      else if (c < Ca) sga[(si * BB + rb) * 4 + c] = v;
+  for (int k = 0; k < Cin; ++k) xv[k] = x[(((long)b * T + t) * N + n) * Cin + k];
+  const float mw = (mask[(long)b * N + n] != 0.f ? 1.f : 0.f) * w[(long)b * N + n];
+  const float a_first = sA[0], a_last = sA[kk - 1];
+  float d[Cin];
+#pragma unroll
+  for (int k = 0; k < Cin; ++k) d[k] = 0.f;
+#pragma unroll 4
+  for (int f = 0; f < F; ++f) {
+    const float sc = scale[f];
+    float z = 0.f;
+    float wp[Cin];
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) {
+      const float wkf = W[k * F + f];
+      z += xv[k] * wkf;
+      wp[k] = wkf * sc;
     }
-    __syncthreads();
-    if (b < B) {
-      for (int si = 0; si < ns; ++si) {
-        const float a = alphas[s0 + si], wt = wts[s0 + si];
-        const float4* gr = reinterpret_cast<const float4*>(sg + (si * BB + bl) * F);
-        if (n < Ca) da += wt * sga[(si * BB + bl) * 4 + n];
-        float d[Cin];
-#pragma unroll
-        for (int k = 0; k < Cin; ++k) d[k] = 0.f;
-#pragma unroll
-        for (int f4 = 0; f4 < F / 4; ++f4) {
-          const float4 g4 = gr[f4];
-          const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int f = 4 * f4 + u;
-            const float y = a * xw[f] + A0[f];
-            const float tz = (y > 0.f ? 1.f : al[f]) * gv[u];
-#pragma unroll
-            for (int k = 0; k < Cin; ++k) d[k] += Wp[k][f] * tz;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < Cin; ++k) dxa[k] += wt * d[k];
+    const float xw = z * sc, A0 = bias[f] * sc + shift[f], al = prelu_a[f];
+    const bool p0 = a_first * xw + A0 > 0.f;
+    const bool p1 = a_last * xw + A0 > 0.f;
+    int lo = 0, hi = kk;                            // p(lo) == p0; first flip in (lo, hi]
+    if (p1 != p0) {
+      hi = kk - 1;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((sA[mid] * xw + A0 > 0.f) == p0) lo = mid;
+        else hi = mid;
       }
     }
-  }
-  if (live) {
-    float* o = acc_x + (((long)b * T + t) * N + n) * Cin;
+    const float Pj = P[hi * PC + f], Q = P[kk * PC + f];
+    const float H = (p0 ? 1.f : al) * Pj + (p1 ? 1.f : al) * (Q - Pj);
 #pragma unroll
-    for (int k = 0; k < Cin; ++k) o[k] += mw * dxa[k];
+    for (int k = 0; k < Cin; ++k) d[k] += wp[k] * H;
   }
-  if (b < B && n < Ca) acc_a[((long)b * T + t) * Ca + n] += da;
+  float* o = acc_x + (((long)b * T + t) * N + n) * Cin;
+#pragma unroll
+  for (int k = 0; k < Cin; ++k) o[k] += mw * d[k];
 }
 
 #define GQ_IGG_DISPATCH(CIN_RT, F_RT, ...)                                                         \
@@ -332,12 +332,16 @@ at::Tensor ig_gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::T
   const long Mp = ((long)kk * B + 15) / 16 * 16;
   c10::DeviceGuard guard(x.device());
   at::Tensor out = at::empty({T, Mp, Cp}, x.options());
+#define GQ_IGG_FWD(NMV)                                                                                     \
+  hipLaunchKernelGGL((ig_gcn_pool_fwd_kernel<CIN, FF, NMV>), dim3((B + 256 / FF - 1) / (256 / FF), T), dim3(256), \
+                     (size_t)IGG_FSG * (256 / FF) * Cp * sizeof(float), stream(), x.data_ptr<float>(),              \
+                     w.data_ptr<float>(), Ca ? anom.data_ptr<float>() : nullptr, W.data_ptr<float>(),               \
+                     b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(), \
+                     alphas.data_ptr<float>(), out.data_ptr<float>(), B, T, N, Ca, kk, (int)Mp, (int)Cp)
   GQ_IGG_DISPATCH(Cin, F,
-      hipLaunchKernelGGL((ig_gcn_pool_fwd_kernel<CIN, FF>), dim3((B + 256 / FF - 1) / (256 / FF), T), dim3(256),
-                         (size_t)IGG_FSG * (256 / FF) * Cp * sizeof(float), stream(), x.data_ptr<float>(), w.data_ptr<float>(), Ca ? anom.data_ptr<float>() : nullptr,
-                         W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                         alpha.data_ptr<float>(), alphas.data_ptr<float>(), out.data_ptr<float>(), B, T, N, Ca, kk,
-                         (int)Mp, (int)Cp));
+      if (N <= 8) GQ_IGG_FWD(8); else if (N <= 16) GQ_IGG_FWD(16); else if (N <= 24) GQ_IGG_FWD(24);
+      else GQ_IGG_FWD(32));
+#undef GQ_IGG_FWD
   GQ_LAUNCH_CHECK();
   return out;
 }
@@ -364,18 +368,21 @@ void ig_gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor&
     TORCH_CHECK(acc_a.dim() == 3 && acc_a.size(0) == B && acc_a.size(1) == T, "ig_gcn_pool_bwd: acc_a [B,T,Ca]");
     Ca = acc_a.size(2);
   }
-  TORCH_CHECK(Cp >= Ca + F && Ca <= 4 && F % 4 == 0, "ig_gcn_pool_bwd: Cp / Ca");
-  constexpr int BB = 256 / IGG_NMAX;
-  const size_t smem = (size_t)IGG_SCH * BB * (F + 4) * sizeof(float);
+  TORCH_CHECK(Cp >= Ca + F && Ca <= 4, "ig_gcn_pool_bwd: Cp / Ca");
   c10::DeviceGuard guard(x.device());
-  GQ_IGG_DISPATCH(Cin, F,
-      hipLaunchKernelGGL((ig_gcn_pool_bwd_kernel<CIN, FF>), dim3((B + BB - 1) / BB, T), dim3(256), smem, stream(),
-                         x.data_ptr<float>(), w.data_ptr<float>(), mask.data_ptr<float>(), g.data_ptr<float>(),
-                         W.data_ptr<float>(), b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                         alpha.data_ptr<float>(), alphas.data_ptr<float>(), wts.data_ptr<float>(),
-                         acc_x.data_ptr<float>(), Ca ? acc_a.data_ptr<float>() : nullptr, B, T, N, Ca, kk,
-                         (int)g.size(1), Cp));
-  GQ_LAUNCH_CHECK();
+  // path points in slices of at most IGG_KMAX (the prefix table of a workgroup lives in LDS)
+  for (int s0 = 0; s0 < kk; s0 += IGG_KMAX) {
+    const int ks = std::min(IGG_KMAX, kk - s0);
+    const size_t smem = (size_t)IGG_BWB * (ks + 1) * (F + 4) * sizeof(float);
+    GQ_IGG_DISPATCH(Cin, F,
+        hipLaunchKernelGGL((ig_gcn_pool_bwd_kernel<CIN, FF>), dim3((B + IGG_BWB - 1) / IGG_BWB, T),
+                           dim3(IGG_BWB * IGG_NMAX), smem, stream(), x.data_ptr<float>(), w.data_ptr<float>(),
+                           mask.data_ptr<float>(), g.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(),
+                           scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
+                           alphas.data_ptr<float>() + s0, wts.data_ptr<float>() + s0, acc_x.data_ptr<float>(),
+                           Ca ? acc_a.data_ptr<float>() : nullptr, B, T, N, Ca, ks, s0, (int)g.size(1), Cp));
+    GQ_LAUNCH_CHECK();
+  }
 }
 #undef GQ_IGG_DISPATCH
 

@@ -169,9 +169,18 @@ class IntegratedGradients:
         model = self.model
         vals, static, build = self._split(batch)
         B = vals[0].shape[0]
-        with torch.no_grad():
-            pred_full = model(build(vals, static)).reshape(B, -1).float()
-        if pred_full.shape[1] > 1:
+        hip = _ig_hip(vals[0])
+        fused = hip and self._cml_path_folded_ok(batch)
+        if fused:
+            # the prediction is the path's last point (alpha = 1: the unscaled inputs), read off
+            # path_pred below instead of a separate forward pass
+            pred_full = None
+        else:
+            with torch.no_grad():
+                pred_full = model(build(vals, static)).reshape(B, -1).float()
+        if pred_full is None:
+            pred = None
+        elif pred_full.shape[1] > 1:
             if target is None:
                 masked = pred_full.masked_fill(batch.node_mask <= 0, -1.0)
                 target = masked.argmax(1)
@@ -189,9 +198,7 @@ class IntegratedGradients:
         acc = [torch.zeros_like(v, dtype=dt) for v in vals]
         path_pred = torch.empty(self.m_steps + 1, B, device=dev, dtype=dt)
         k = max(1, min(self.m_steps + 1, self.max_rows // max(B, 1)))
-        hip = _ig_hip(vals[0])
         vf = [v.to(dt).contiguous() for v in vals]
-        fused = hip and self._cml_path_folded_ok(batch)
         with _frozen(model), torch.enable_grad():
             for s in (range(0, self.m_steps + 1, k) if fused else ()):
                 self._cml_path_folded_chunk(batch, alphas[s:s + k].contiguous(), wts[s:s + k].contiguous(),
@@ -232,6 +239,8 @@ class IntegratedGradients:
                 acc = [g.abs() for g in acc]
             elif self.negative_values == "clip":
                 acc = [g.clamp(min=0) for g in acc]
+        if pred is None:
+            pred = path_pred[-1].float()
         res = {"pred": pred, "path_pred": path_pred, "target": target}
         if self.per_sensor:
             if self.is_baseline:

@@ -27,9 +27,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=4, help="timed batches per rank")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=256, help="windows explained per attribute() call")
     ap.add_argument("--m-steps", type=int, default=100)
-    ap.add_argument("--max-rows", type=int, default=16384)
+    ap.add_argument("--max-rows", type=int, default=32768, help="path rows (windows x path points) per pass")
     args = ap.parse_args(argv)
 
     from gnnqc import config as C
