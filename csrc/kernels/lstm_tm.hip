@@ -56,12 +56,11 @@ struct TmOcc {
   static constexpr int W = (NT >= 1024 && KX == 1) ? 8 : 1;
 };
 
-template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
+template <int H, bool TRAIN, int KX, int GR, int D>
 __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hout, __bf16* __restrict__ gbuf,
-    float* __restrict__ cbuf, int Mp, int T, int Din, int Dw, float* __restrict__ pout,
-    unsigned* __restrict__ iout, int P) {
+    float* __restrict__ cbuf, int Mp, int T, int Din, int Dw) {
   // Din: channels of the x layout (row pitch); Dw <= Din: rows of W (padding channels of x are zero)
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
@@ -126,7 +125,6 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
   const int gh = (tid % n_gh) * 4;
   float* hbase = hout + (size_t)row0 * H + gh;
   const size_t hstep = (size_t)Mp * H;
-  PoolAcc pool;
 
 #pragma unroll
   for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
@@ -150,7 +148,6 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
         const int ts = (t >= 1 && t <= T) ? t - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
-        if (POOL && t >= 1 && t <= T) pool.step(v, t - 1, P, T / P, pout, iout, (size_t)row0 * H + gh, hstep);
       }
       f32x4_t acc[CPL];
 #pragma unroll
@@ -204,13 +201,12 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
 // recurrence of T + 1 steps instead of two of T. Outputs and saved state are exactly those
 // of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
 // (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
-template <int H, bool TRAIN, int KX, int GR, int D, bool POOL>
+template <int H, bool TRAIN, int KX, int GR, int D>
 __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
     const float* __restrict__ bB, float* __restrict__ hA, __bf16* __restrict__ gA, float* __restrict__ cA,
-    float* __restrict__ hB, __bf16* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw,
-    float* __restrict__ pout, unsigned* __restrict__ iout, int P) {
+    float* __restrict__ hB, __bf16* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw) {
   using C = TMC<H>;
   static_assert(C::CPL == 1, "pair kernel: one cell per lane (H <= 64)");
   constexpr int NW = C::NW, NTL = C::NT, G4 = C::G4;
@@ -277,8 +273,6 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
   const size_t hstep = (size_t)Mp * H;
   __bf16* gbuf = layerB ? gB : gA;
   float* cbuf = layerB ? cB : cA;
-  PoolAcc pool;
-
 #pragma unroll
   for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
   __syncthreads();
@@ -301,9 +295,6 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
         const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
-        // layer B's output feeds the MaxPooling1D that follows the pair
-        if (POOL && layerB && tc >= 1 && tc <= T)
-          pool.step(v, tc - 1, P, T / P, pout, iout, (size_t)row0 * H + gh, hstep);
       }
       f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};   // independent MFMA chains
       if (layerB) {
@@ -360,13 +351,11 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 //       lengthens every step of the serial chain and pushes H = 32 past the VGPR budget.
 //   DX: dx^T = W dz_t^T tile -> HBM (frozen-weight input gradients, e.g. integrated gradients).
 // dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
 __device__ __forceinline__ void lstm_tm_bwd_body(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
-    int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P, int tile, int ntiles) {
-  // UNPOOL: dhout is the gradient of the fused MaxPooling1D output [T/P][Mp][H] and pidx its
-  // argmax bytes; the scatter back to [T][Mp][H] happens as the dh tiles are staged
+    int Mp, int T, int Din, int Dw, int tile, int ntiles) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
   constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
@@ -440,14 +429,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   const float* dbase = dhout + (size_t)row0 * H + gd;
   const size_t dstep = LAST ? 0 : (size_t)Mp * H;
   float4 rd[D];
-  unsigned ri[UNPOOL ? D : 1];
-  const int To = UNPOOL ? T / P : 0;
-  const unsigned* pbase = UNPOOL ? pidx + ((size_t)row0 * H + gd) / 4 : nullptr;
-  // stage the dh tile of time t (UNPOOL: scatter the pooled gradient by its argmax)
-  auto dh_tile = [&](int j, int t) -> float4 {
-    if constexpr (UNPOOL) return unpool4(rd[j], ri[j], t, P, To);
-    else return rd[j];
-  };
+  auto dh_tile = [&](int j, int t) -> float4 { (void)t; return rd[j]; };
   // dz storer: one float4 granule of the [16][4H] tile per thread
   const int gz_seq = tid / (G4 / 4), gz_c = (tid % (G4 / 4)) * 4;
   __bf16* zbase = dz + (size_t)(row0 + gz_seq) * G4 + gz_c;
@@ -463,18 +445,12 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #define GQ_TMB_LOAD_D(J, SS)                                                                \
   {                                                                                         \
     const int tt_ = max(T - 1 - (SS), 0);                                                   \
-    if (UNPOOL) {                                                                           \
-      const size_t k_ = (size_t)min(tt_ / P, To - 1) * dstep;                               \
-      rd[J] = *reinterpret_cast<const float4*>(dbase + k_);                                 \
-      ri[J] = pbase[k_ / 4];                                                                \
-    } else {                                                                                \
-      float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)tt_ * dstep);            \
-      if (LAST) {                                                                           \
-        const float m_ = (SS) == 0 ? 1.f : 0.f;                                             \
-        v_.x *= m_; v_.y *= m_; v_.z *= m_; v_.w *= m_;                                     \
-      }                                                                                     \
-      rd[J] = v_;                                                                           \
+    float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)tt_ * dstep);              \
+    if (LAST) {                                                                             \
+      const float m_ = (SS) == 0 ? 1.f : 0.f;                                               \
+      v_.x *= m_; v_.y *= m_; v_.z *= m_; v_.w *= m_;                                       \
     }                                                                                       \
+    rd[J] = v_;                                                                             \
   }
 #pragma unroll
   for (int j = 0; j < D; ++j) {
@@ -578,13 +554,12 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #undef GQ_TMB_LOAD_D
 }
 
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool UNPOOL>
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
-    int Mp, int T, int Din, int Dw, const unsigned* __restrict__ pidx, int P) {
-  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, UNPOOL>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, pidx, P,
-                                                       blockIdx.x, gridDim.x);
+    int Mp, int T, int Din, int Dw) {
+  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, blockIdx.x, gridDim.x);
 }
 
 // =====================================================================================
@@ -606,8 +581,7 @@ __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
   constexpr int D = HR >= 64 ? 2 : 4;
   const int b = blockIdx.x;
   if (b < ntiles) {
-    lstm_tm_bwd_body<HR, 1, 1, D, true, false, false, false>(dh, g, c, W, U, nullptr, dz, Mp, T, Dw, Dw, nullptr, 1,
-                                                             b, ntiles);
+    lstm_tm_bwd_body<HR, 1, 1, D, true, false, false>(dh, g, c, W, U, nullptr, dz, Mp, T, Dw, Dw, b, ntiles);
     return;
   }
   if (threadIdx.x >= 256) return;
@@ -658,46 +632,23 @@ static bool tm_supported(int H, int Din, int gr) {
   return 16 * Din / gr <= 16 * H;
 }
 
-// fused MaxPooling1D of the layer output: pooled [T/P, Mp, H] fp32 + argmax uint8 (P = 0: none)
+// (MaxPooling1D fused into the recurrences - running max + argmax in the forward, un-pooling on
+// load in the backward - was measured slower on both shapes: CML 0.766 vs 0.713 ms, SoilNet 3.920 vs
+// 3.894 ms; profiles/r3_bench_soilnet_poolfusion.json. Pooling runs as pool.hip kernels.)
 template <int H, bool TRAIN, int KX, int GR>
 static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, __bf16* g,
-                       float* c, int Mp, int T, int Din, int Dw, const TmPool& pl, hipStream_t st) {
+                       float* c, int Mp, int T, int Din, int Dw, hipStream_t st) {
   constexpr int D = 6;
-  if (pl.P > 0)
-    hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D, true>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W,
-                       U, b, h, g, c, Mp, T, Din, Dw, pl.out, pl.idx, pl.P);
-  else
-    hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D, false>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W,
-                       U, b, h, g, c, Mp, T, Din, Dw, nullptr, nullptr, 1);
+  hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W, U, b, h,
+                     g, c, Mp, T, Din, Dw);
 }
 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
 static void tm_bwd_cfg(int ntiles, const float* dh, const __bf16* g, const float* c, const float* W, const float* U,
-                       float* dx, __bf16* dz, int Mp, int T, int Din, int Dw, hipStream_t st,
-                       const TmPool& pl = TmPool()) {
+                       float* dx, __bf16* dz, int Mp, int T, int Din, int Dw, hipStream_t st) {
   constexpr int D = H >= 64 ? 2 : 4;        // H = 64: 16 waves x 128 VGPRs, shorter state rings
-  if constexpr (!LAST) {
-    if (pl.P > 0) {
-      hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST, true>), dim3(ntiles), dim3(TMC<H>::NT), 0,
-                         st, dh, g, c, W, U, dx, dz, Mp, T, Din, Dw, pl.cidx, pl.P);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST, false>), dim3(ntiles), dim3(TMC<H>::NT), 0, st,
-                     dh, g, c, W, U, dx, dz, Mp, T, Din, Dw, nullptr, 1);
-}
-
-static TmPool tm_pool_input(const c10::optional<at::Tensor>& pidx, int64_t P, const at::Tensor& dh, int T, int Mp,
-                            int H) {
-  TmPool pl;
-  if (P <= 0) return pl;
-  TORCH_CHECK(pidx.has_value() && pidx->scalar_type() == at::kByte && pidx->is_contiguous() && pidx->is_cuda(),
-              "lstm_tm_bwd: pool_idx must be the uint8 argmax of the fused pooling");
-  TORCH_CHECK(dh.dim() == 3 && dh.size(0) == T / P && dh.size(1) == Mp && dh.size(2) == H &&
-                  pidx->sizes() == dh.sizes(), "lstm_tm_bwd: pooled gradient shape");
-  pl.P = (int)P;
-  pl.cidx = reinterpret_cast<const unsigned*>(pidx->data_ptr<uint8_t>());
-  return pl;
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh, g,
+                     c, W, U, dx, dz, Mp, T, Din, Dw);
 }
 
 #define GQ_TM_H_DISPATCH(HV, ...)                                  \
@@ -731,7 +682,7 @@ static TmPool tm_pool_input(const c10::optional<at::Tensor>& pidx, int64_t P, co
 // x: [T, Mp, Din] time-major; W: [Dw, 4H] with Dw <= Din (x channels >= Dw must be zero, e.g. the
 // alignment padding of a 19-channel input to 20). Returns [h (T,Mp,H), gates (state), c (state)].
 std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
-                                    const at::Tensor& b, bool train, int64_t pool) {
+                                    const at::Tensor& b, bool train) {
   check_f32_cuda(x, "x");
   check_f32_cuda(W, "W");
   check_f32_cuda(U, "U");
@@ -754,22 +705,20 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   auto st = stream();
   __bf16* gp = train ? bf16_ptr(g) : nullptr;
   float* cp = train ? c.data_ptr<float>() : nullptr;
-  at::Tensor pooled, pidx;
-  const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (train) tm_fwd_cfg<HH, true, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, pl, st);
+                                                b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st);
       else tm_fwd_cfg<HH, false, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, pl, st))));
+                                           b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st))));
   GQ_LAUNCH_CHECK();
-  return {h.narrow(0, 0, T), g, c, pooled, pidx};
+  return {h.narrow(0, 0, T), g, c};
 }
 
 // Pair forward (lstm_tm2_fwd_kernel): x [T, Mp, Din]; A: W [Dw <= Din, 4H], B: W [H, 4H].
 // Returns [hA, gA, cA, hB, gB, cB] with the layouts of lstm_tm_fwd.
 std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, const at::Tensor& UA,
                                      const at::Tensor& bA, const at::Tensor& WB, const at::Tensor& UB,
-                                     const at::Tensor& bB, bool train, int64_t pool) {
+                                     const at::Tensor& bB, bool train) {
   for (const at::Tensor* t : {&x, &WA, &UA, &bA, &WB, &UB, &bB}) check_f32_cuda(*t, "lstm_tm2_fwd operand");
   TORCH_CHECK(x.dim() == 3, "lstm_tm2_fwd: x must be [T, Mp, Din]");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)UA.size(0);
@@ -795,19 +744,16 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   auto st = stream();
   __bf16* PG[2] = {train ? bf16_ptr(gA) : nullptr, train ? bf16_ptr(gB) : nullptr};
   float* P[4] = {nullptr, train ? cA.data_ptr<float>() : nullptr, nullptr, train ? cB.data_ptr<float>() : nullptr};
-  at::Tensor pooled, pidx;
-  const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
-#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, PL)                                                                     \
-  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, PL>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,    \
+#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR)                                                                         \
+  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,        \
                      x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
                      WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), PG[0], \
-                     P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw, pl.out, pl.idx, pl.P > 0 ? pl.P : 1)
+                     P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw)
   GQ_TM2_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
-      if (pl.P > 0) { if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, true); else GQ_TM2_LAUNCH(HH, false, KXX, GRR, true); }
-      else { if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, false); else GQ_TM2_LAUNCH(HH, false, KXX, GRR, false); })));
+      if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR); else GQ_TM2_LAUNCH(HH, false, KXX, GRR))));
 #undef GQ_TM2_LAUNCH
   GQ_LAUNCH_CHECK();
-  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB, pooled, pidx};
+  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB};
 }
 
 // ---- pipelined backward (see lstm_tm_bwd_dual_kernel)
@@ -1218,7 +1164,7 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
 // (empty if !need_dx) and accumulates dW, dU, db when they are non-empty.
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
                        const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, at::Tensor dW, at::Tensor dU,
-                       at::Tensor db, bool need_dx, const c10::optional<at::Tensor>& pool_idx, int64_t pool) {
+                       at::Tensor db, bool need_dx) {
   const at::Tensor* ops[] = {&dh, &c, &x, &h, &W, &U};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
   check_gates_cuda(g);
@@ -1227,8 +1173,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H, "lstm_tm_bwd: W shape");
   const bool last = dh.dim() == 2;
   TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H)
-                   : ((pool > 0 || dh.size(0) == T) && dh.size(1) == Mp && dh.size(2) == H), "lstm_tm_bwd: dh shape");
-  const TmPool pl = tm_pool_input(pool_idx, last ? 0 : pool, dh, T, Mp, H);
+                   : (dh.size(0) == T && dh.size(1) == Mp && dh.size(2) == H), "lstm_tm_bwd: dh shape");
   TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H &&
                   h.numel() == (long)T * Mp * H, "lstm_tm_bwd: saved state shapes");
   const bool wg = dW.numel() > 0;
@@ -1254,7 +1199,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #define GQ_TM_BWD_CALL2(LASTV)                                                                              \
   tm_bwd_cfg<HH, KXX, GRR, true, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), \
                                               W.data_ptr<float>(), U.data_ptr<float>(), dx.data_ptr<float>(),  \
-                                              bf16_ptr(dz), Mp, T, Din, Dw, st, pl)
+                                              bf16_ptr(dz), Mp, T, Din, Dw, st)
     GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
         if (last) GQ_TM_BWD_CALL2(true); else GQ_TM_BWD_CALL2(false))));
 #undef GQ_TM_BWD_CALL2
@@ -1272,8 +1217,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
         if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
               c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st);
         else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
-              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st,
-              pl));
+              c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st));
     GQ_LAUNCH_CHECK();
     const long rows = (long)T * Mp;
     const int ncb = lstm_grads_col_blocks(H);
@@ -1290,7 +1234,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #define GQ_TM_BWD_CALL(LASTV)                                                                               \
   tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),          \
                                                c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
-                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st, pl)
+                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st)
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (last) GQ_TM_BWD_CALL(true); else GQ_TM_BWD_CALL(false))));
 #undef GQ_TM_BWD_CALL

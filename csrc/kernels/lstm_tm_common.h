@@ -56,7 +56,8 @@ struct Granule {
   __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
 };
 
-// ---- fused MaxPooling1D(P) (valid, stride P) of a stored h sequence. Each storer lane owns
+// ---- fused MaxPooling1D(P) (valid, stride P) of a stored h sequence (the chain forward's last
+// stage, lstm_chain.hip, whose pooled output leaves the chain). Each storer lane owns
 // one float4 granule of the [16][H] tile for the whole sequence, so the running max and the
 // byte argmax (first maximum wins, like TF's MaxPoolGrad) stay in its registers; the pooled
 // granule and its 4 argmax bytes are written when a window closes. Layout = maxpool1d_fwd's
@@ -85,24 +86,11 @@ struct PoolAcc {
   }
 };
 
-// inverse for the backward: dh_t = dpool[t / P] where the argmax byte == t % P, else 0
-__device__ __forceinline__ float4 unpool4(const float4& v, unsigned idx, int t, int P, int To) {
-  const bool ok = t >= 0 && t < To * P;
-  const unsigned r = ok ? (unsigned)(t % P) : 0xffu;
-  float4 o;
-  o.x = ((idx & 0xffu) == r) ? v.x : 0.f;
-  o.y = (((idx >> 8) & 0xffu) == r) ? v.y : 0.f;
-  o.z = (((idx >> 16) & 0xffu) == r) ? v.z : 0.f;
-  o.w = ((idx >> 24) == r) ? v.w : 0.f;
-  return o;
-}
-
-// fused-pool outputs of a forward (host)
+// fused-pool outputs of the chain forward (host)
 struct TmPool {
   int P = 0;
   float* out = nullptr;
   unsigned* idx = nullptr;
-  const unsigned* cidx = nullptr;   // backward: argmax of the pooled gradient given as dh
 };
 
 inline TmPool tm_pool_outputs(int P, int T, int Mp, int H, const at::TensorOptions& opt, at::Tensor& pooled,

@@ -121,14 +121,10 @@ class TimeLayer(nn.Module):
                     and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16)
                     and nxt.activation == mod.activation and nxt.compute_bf16 == mod.compute_bf16):
                 i += 1
-                pool = self._fusable_pool(seq, i, h.shape[0])
-                h = lstm_pair_tm(h, mod, nxt, pool)      # two layers, one pipelined forward kernel
-                i += 1 if pool else 0
+                h = lstm_pair_tm(h, mod, nxt)      # two layers, one pipelined forward kernel
                 continue
             if tm and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16):
-                pool = self._fusable_pool(seq, i, h.shape[0]) if mod.return_sequences else 0
-                h = lstm_layer_tm(h, mod.kernel, mod.recurrent_kernel, mod.bias, mod.return_sequences, pool)
-                i += 1 if pool else 0
+                h = lstm_layer_tm(h, mod.kernel, mod.recurrent_kernel, mod.bias, mod.return_sequences)
                 if not mod.return_sequences:
                     return h[:M]
                 continue
@@ -209,20 +205,6 @@ class TimeLayer(nn.Module):
         if not chain_fits(Mp, len(mods), h.device):
             return None
         return mods, pools, i
-
-    @staticmethod
-    def _fusable_pool(seq, i: int, T: int) -> int:
-        """Pool size if ``seq[i]`` is a MaxPooling1D the preceding time-major kernel can fuse
-        (its epilogue writes the pooled sequence + argmax; the backward un-pools on load).
-
-        Opt-in (``GNNQC_POOL_FUSION=1``): measured slower on MI355X (CML step 0.766 vs 0.713
-        ms): the per-step running max / argmax and the un-pool select lengthen the serial
-        recurrence by more than the three separate pool launches cost (~23 us)."""
-        mod = seq[i] if i < len(seq) else None
-        if (isinstance(mod, MaxPooling1D) and 1 <= mod.pool_size <= 255 and T // mod.pool_size >= 1
-                and os.environ.get("GNNQC_POOL_FUSION", "0") == "1"):
-            return int(mod.pool_size)
-        return 0
 
     def _forward_cnn(self, x: torch.Tensor) -> torch.Tensor:
         """CNN branch (``create_model.py:80-101``): every Conv1D + LeakyReLU pair is one fused

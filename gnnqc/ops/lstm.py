@@ -307,7 +307,7 @@ class _HipLSTM(torch.autograd.Function):
                 None, None)
 
 
-def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx, pidx=None, pool: int = 0):
+def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx):
     """Backward of one time-major layer (the pipe when it takes the layer, else one fused kernel).
     Returns dx (or None) and the three weight gradients to hand to autograd (None where they
     were accumulated directly into ``.grad``)."""
@@ -320,14 +320,13 @@ def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx, pidx=Non
     else:
         e = x.new_zeros(0)
         sinks = [(e, True)] * 3
-    pi = pidx if pool else None
     Wc, Uc = W.contiguous(), U.contiguous()
-    if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+    if wgrad and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
         dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx)
     else:
         with _deferred_reduce(wgrad and all(d for _, d in sinks)):
             dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, sinks[0][0], sinks[1][0],
-                                       sinks[2][0], need_dx, pi, pool)
+                                       sinks[2][0], need_dx)
     grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need_w)]
     return (dx if need_dx else None), grads
 
@@ -647,45 +646,39 @@ class _HipLSTMTM(torch.autograd.Function):
     accumulated straight into the gradient buffers (direct mode) or returned."""
 
     @staticmethod
-    def forward(ctx, x, W, U, b, return_sequences: bool, pool: int = 0):
+    def forward(ctx, x, W, U, b, return_sequences: bool):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:4])
-        h, g, c, pooled, pidx = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need,
-                                                      int(pool))
+        h, g, c = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need)
         ctx.params = (W, U, b)
         ctx.return_sequences = return_sequences
-        ctx.pool = int(pool)
         if need:
-            ctx.save_for_backward(x, W, U, h, g, c, pidx)
-        if pool:
-            return pooled
+            ctx.save_for_backward(x, W, U, h, g, c)
         return h if return_sequences else h[-1]
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
-        x, W, U, h, g, c, pidx = ctx.saved_tensors
+        x, W, U, h, g, c = ctx.saved_tensors
         need = ctx.needs_input_grad
         wgrad = any(need[1:4])
         need_dx = bool(need[0])
-        pool = ctx.pool
         if not wgrad and not need_dx:
-            return None, None, None, None, None, None
+            return None, None, None, None, None
         if wgrad:
             sinks = [_grad_sink(p) for p in ctx.params]
         else:
             e = x.new_zeros(0)
             sinks = [(e, True)] * 3
-        pi = pidx if pool else None
-        if wgrad and not pool and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+        if wgrad and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
             dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
         else:
             with _deferred_reduce(wgrad and all(d for _, d in sinks)):
                 dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
-                                           sinks[0][0], sinks[1][0], sinks[2][0], need_dx, pi, pool)
+                                           sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
         grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
-        return (dx if need_dx else None, *grads, None, None)
+        return (dx if need_dx else None, *grads, None)
 
 
 class _HipLSTMTMPair(torch.autograd.Function):
@@ -696,28 +689,25 @@ class _HipLSTMTMPair(torch.autograd.Function):
     SIMD's MFMA pipe - and removed.)"""
 
     @staticmethod
-    def forward(ctx, x, WA, UA, bA, WB, UB, bB, pool: int = 0):
+    def forward(ctx, x, WA, UA, bA, WB, UB, bB):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:7])
-        hA, gA, cA, hB, gB, cB, pooled, pidx = hip_ops().lstm_tm2_fwd(
+        hA, gA, cA, hB, gB, cB = hip_ops().lstm_tm2_fwd(
             x, WA.contiguous(), UA.contiguous(), bA.contiguous(), WB.contiguous(), UB.contiguous(), bB.contiguous(),
-            need, int(pool))
+            need)
         ctx.params = (WA, UA, bA, WB, UB, bB)
-        ctx.pool = int(pool)
         if need:
-            ctx.save_for_backward(x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB, pidx)
-        return pooled if pool else hB
+            ctx.save_for_backward(x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB)
+        return hB
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB, pidx = ctx.saved_tensors
+        x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB = ctx.saved_tensors
         need = ctx.needs_input_grad
         e = x.new_zeros(0)
-        pool = ctx.pool
-        pi = pidx if pool else None
         dout = dout.contiguous()
 
         def sinks(params, flags):
@@ -729,27 +719,25 @@ class _HipLSTMTMPair(torch.autograd.Function):
         sA = sinks(ctx.params[:3], need[1:4])
         need_dx = bool(need[0])
         dx = None
-        if (any(need[4:7]) and any(need[1:4]) and not pool and _pipe_on(sB, x.shape[1]) and _pipe_on(sA, x.shape[1])
+        if (any(need[4:7]) and any(need[1:4]) and _pipe_on(sB, x.shape[1]) and _pipe_on(sA, x.shape[1])
                 and _pipe_x_ok(x, WA.shape[0]) and _pipe_x_ok(hA, WB.shape[0])):
             dhA = _pipe_tm_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
             dx = _pipe_tm_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
             with _deferred_reduce(all(d for _, d in sB) and all(d for _, d in sA)):
                 dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
-                                      sB[0][0], sB[1][0], sB[2][0], True, pi, pool)
+                                      sB[0][0], sB[1][0], sB[2][0], True)
                 if need_dx or any(need[1:4]):
                     dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0],
                                          sA[2][0], need_dx)
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
-        return (dx if need_dx else None, *gA_, *gB_, None)
+        return (dx if need_dx else None, *gA_, *gB_)
 
 
-def lstm_pair_tm(x_tm, A, B, pool: int = 0) -> torch.Tensor:
-    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``); ``pool`` > 0
-    also fuses the following MaxPooling1D (returns the pooled sequence)."""
-    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias,
-                                int(pool))
+def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:
+    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``)."""
+    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias)
 
 
 def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf16: bool = True) -> bool:
@@ -760,9 +748,9 @@ def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf1
 
 
 def lstm_layer_tm(x_tm: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
-                  return_sequences: bool = True, pool: int = 0) -> torch.Tensor:
-    """Time-major layer; ``pool`` > 0 fuses a following MaxPooling1D(pool) into the kernels."""
-    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences), int(pool))
+                  return_sequences: bool = True) -> torch.Tensor:
+    """Time-major layer ``[T, Mp, Din] -> [T, Mp, H]`` (or the last step)."""
+    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences))
 
 
 def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,

@@ -9,7 +9,6 @@ pytestmark = pytest.mark.gpu
 LAYOUTS = [
     # (switches of the variant, switches of both runs)
     ({"GNNQC_TM_RECDX": "0"}, {"GNNQC_CHAIN": "0"}),          # dx from weight-gradient slabs + sum
-    ({"GNNQC_POOL_FUSION": "1"}, {"GNNQC_CHAIN": "0"}),       # MaxPooling1D inside the recurrences
 ]
 
 
