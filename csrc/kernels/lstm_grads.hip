@@ -210,7 +210,11 @@ void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows,
   const int rw = ndin >= 3 ? 4 : ndin;
   const int ndt = (ndin + rw - 1) / rw;
   const long ngroups = ((rows + 15) / 16 + (4 / rw) - 1) / (4 / rw);
-  const int grid = (int)std::max<long>(1, std::min<long>(ngroups, 8192));   // one pass: latency-bound per tile
+  // every wave converts its W fragments (KS x 2 float4 rows per din tile: 32 KB per wave at H = 128)
+  // once and then walks row tiles: wide layers cap the grid so that setup is amortised over several
+  // tiles (at one tile per wave, H = 128 re-read ~640 MB of W through L2 on the SoilNet step)
+  const long cap = H >= 128 ? 1024 : (H >= 64 ? 2048 : 8192);
+  const int grid = (int)std::max<long>(1, std::min<long>(ngroups, cap));
 #define GQ_DX(HH, RWV, ND)                                                                                          \
   do {                                                                                                              \
     if (zbf) hipLaunchKernelGGL((lstm_dx_kernel<HH, RWV, ND, __bf16>), dim3(grid), dim3(256), 0, st, dz, W, dx,     \
