@@ -27,6 +27,7 @@ constexpr int HT = 16;     // rows per tile: 8 workgroups for a CML batch of 128
 constexpr int HU = 64;     // dense units (model_config dense.units)
 constexpr int RPG = HT / 4;  // rows per wave group
 constexpr int UPG = HU / 4;  // dense units per wave group (dW2 rows per thread)
+constexpr int HEAD_HIST_LDS = 1024;   // score-histogram bins aggregated in LDS (engine: 1001)
 
 __device__ __forceinline__ float leaky(float z, float a) { return z > 0.f ? z : a * z; }
 __device__ __forceinline__ float dleaky(float z, float a) { return z > 0.f ? 1.f : a; }
@@ -91,7 +92,14 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
   __shared__ float sa2[HT][HU + 4];
   __shared__ float red[4];
   __shared__ float mred[4][8];
+  // the workgroup's score histogram, flushed with one global atomic per non-empty bin: per-row
+  // global atomics all landed on the same few bins (an untrained model scores every node ~0.5)
+  // and serialised - SoilNet's 6,688 node rows per step made this kernel ~50 us
+  __shared__ float shist[2 * HEAD_HIST_LDS];
+  const bool lds_hist = hist != nullptr && bins <= HEAD_HIST_LDS;
   const int tid = threadIdx.x, j = tid & 63, g = tid >> 6;
+  if (lds_hist)
+    for (int e = tid; e < 2 * bins; e += 256) shist[e] = 0.f;
   stage_lds<F * HU, HU, HU>(&sW1[0][0], W1);
   stage_lds<HU * HU, HU, HU>(&sW2[0][0], W2);
   const float bj1 = b1[j], bj2 = b2[j], w3 = W3[j], b3v = b3[0];
@@ -174,12 +182,16 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
         if (hist != nullptr && m != 0.f) {
           int b = (int)rintf(fminf(fmaxf(p, 0.f), 1.f) * (float)(bins - 1));
           b = b < 0 ? 0 : (b >= bins ? bins - 1 : b);
-          atomicAdd(&hist[(pos ? bins : 0) + b], m);
+          if (lds_hist) atomicAdd(&shist[(pos ? bins : 0) + b], m);
+          else atomicAdd(&hist[(pos ? bins : 0) + b], m);
         }
       }
     }
     __syncthreads();
   }
+  if (lds_hist)
+    for (int e = tid; e < 2 * bins; e += 256)
+      if (shist[e] != 0.f) atomicAdd(&hist[e], shist[e]);
   // block reduction of the loss / metric partials (lanes >= RPG hold zeros)
   float v[6] = {m_loss, m_n, m_tp, m_tn, m_fp, m_fn};
 #pragma unroll
