@@ -13,6 +13,7 @@ available), random-init weights. Reports, as ONE JSON line:
   with ``--fp32``, again in fp32: ROC-AUC / MCC of the held-out fold and training windows/s.
 
     python scripts/cml_full_scale.py [--epochs E] [--fp32] [--sensors S --minutes M --flagged F]
+    python scripts/cml_full_scale.py --all-folds      (5-fold CV at full size, bf16)
 """
 from __future__ import annotations
 
@@ -41,6 +42,8 @@ def main(argv=None):
     ap.add_argument("--fold", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-train", action="store_true", help="stop after the DeviceStore")
+    ap.add_argument("--all-folds", action="store_true",
+                    help="bf16: all 5 folds of the reference's splitter (the headline 5-fold CV protocol at full size)")
     args = ap.parse_args(argv)
 
     import numpy as np
@@ -86,7 +89,20 @@ def main(argv=None):
     rec["host_peak_rss_gb"] = round(_rss_gb(), 2)
     print(json.dumps({"stage": "store", **rec}), flush=True)
 
-    runs = [] if args.no_train else ["bf16"] + (["fp32"] if args.fp32 else [])
+    if args.all_folds and not args.no_train:
+        mc = C.default("model_cml")
+        mc.runtime.compute_dtype = "bf16"
+        if args.epochs:
+            mc["epochs"] = int(args.epochs)
+        t0 = time.time()
+        res = run_cv(pc, mc, ws, folds=5, device=dev, store=store, verbose=2)
+        folds = [{"auc": round(f["auc"], 4), "mcc": round(f["mcc"], 4), "n_train": f["n_train"],
+                  "n_test": f["n_test"], "epochs": len(f["loss_curve"])} for f in res["per_fold"]]
+        aucs = [f["auc"] for f in folds]
+        rec["cv5_bf16"] = {"mean_auc": round(float(np.mean(aucs)), 4), "std_auc": round(float(np.std(aucs)), 4),
+                           "folds": folds, "seconds": round(time.time() - t0, 1)}
+        print(json.dumps({"stage": "cv5_bf16", **rec["cv5_bf16"]}), flush=True)
+    runs = [] if (args.no_train or args.all_folds) else ["bf16"] + (["fp32"] if args.fp32 else [])
     for dt in runs:
         mc = C.default("model_cml")
         mc.runtime.compute_dtype = dt

@@ -33,7 +33,7 @@ done
 if [ "${SKIP_IG:-0}" != "1" ]; then
   for r in ${IG_ROWS:-640 16384}; do
     step "ig rows=$r"
-    timeout -k 10 300 python scripts/bench_ig.py --batches 3 --max-rows $r > $OUT/ig_$r.log 2>&1 \
+    timeout -k 10 300 python scripts/bench_ig.py --batches 6 --max-rows $r > $OUT/ig_$r.log 2>&1 \
       || { tail -20 $OUT/ig_$r.log; exit 3; }
     tail -1 $OUT/ig_$r.log
   done
