@@ -229,31 +229,23 @@ __global__ __launch_bounds__(IGG_BWB * IGG_NMAX) void ig_gcn_pool_bwd_kernel(
   const int t = blockIdx.y, b0 = blockIdx.x * IGG_BWB, b = b0 + bl;
   const int rowp = (kk + 1) * PC;
   for (int e = tid; e < kk; e += IGG_BWB * IGG_NMAX) sA[e] = alphas[e];
-  // prefix sums over the path points of wt_s g_c(s). First every weighted value goes to LDS (the
-  // workgroup's rows of one step are contiguous: all loads independent, one memory latency), then
-  // each (window, channel) scans its column in LDS.
-  const int nb = min(IGG_BWB, B - b0);
-  {
-    const int per_s = nb * Cp;
-    const long stride = (long)B * Cp;
-    const float* gbase = g + ((long)t * Mp + (long)s_off * B + b0) * Cp;
-    for (int e = tid; e < kk * per_s; e += IGG_BWB * IGG_NMAX) {
-      const int si = e / per_s, r = e - si * per_s;
-      const int wb = r / Cp, ch = r - wb * Cp;
-      const int c = (ch >= Ca && ch < Ca + F) ? ch - Ca : (ch < Ca ? F + ch : -1);
-      if (c >= 0) sP[wb * rowp + (si + 1) * PC + c] = wts[si] * gbase[si * stride + r];
-    }
-  }
-  __syncthreads();
-  for (int e = tid; e < nb * PC; e += IGG_BWB * IGG_NMAX) {
-    const int wb = e / PC, c = e - wb * PC;
-    if (c >= F && c - F >= Ca) continue;            // unused anomaly slot
+  // prefix sums over the path points of wt_s g_c(s): thread (window, channel)
+  for (int e = tid; e < IGG_BWB * PC; e += IGG_BWB * IGG_NMAX) {
+    const int wb = e / PC, c = e - wb * PC, bb = b0 + wb;
+    const int ch = c < F ? Ca + c : (c - F < Ca ? c - F : -1);
     float* P = sP + wb * rowp + c;
     float acc = 0.f;
     P[0] = 0.f;
-    for (int si = 1; si <= kk; ++si) {
-      acc += P[si * PC];
-      P[si * PC] = acc;
+    if (bb < B && ch >= 0) {
+      const float* gp = g + ((long)t * Mp + (long)s_off * B + bb) * Cp + ch;
+      const long stride = (long)B * Cp;
+#pragma unroll 8
+      for (int s = 0; s < kk; ++s) {
+        acc += wts[s] * gp[s * stride];
+        P[(s + 1) * PC] = acc;
+      }
+    } else {
+      for (int s = 0; s < kk; ++s) P[(s + 1) * PC] = 0.f;
     }
   }
   __syncthreads();
