@@ -227,29 +227,14 @@ __device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int
       rowv[r * 8 + 3] = (!pp && !pos) ? m : 0.f;
       rowv[r * 8 + 4] = (pp && !pos) ? m : 0.f;
       rowv[r * 8 + 5] = (!pp && pos) ? m : 0.f;
-      int key = -1;
       if (hd.hist != nullptr && m != 0.f) {
         int b = (int)rintf(fminf(fmaxf(p, 0.f), 1.f) * (float)(hd.bins - 1));
         b = b < 0 ? 0 : (b >= hd.bins ? hd.bins - 1 : b);
-        key = (pos ? hd.bins : 0) + b;
+        atomicAdd(&hd.hist[(pos ? hd.bins : 0) + b], m);
       }
-      rowv[r * 8 + 6] = __int_as_float(key);      // (slots 6 / 7 of the row record are free)
-      rowv[r * 8 + 7] = m;
     }
   }
   __syncthreads();
-  // score histogram: one global atomic per distinct bin of the tile (the rows of a batch mostly
-  // share a bin, and 16 atomics per tile on one address serialised before the hand-off's vmcnt wait)
-  if (tid < 16 && __float_as_int(rowv[tid * 8 + 6]) >= 0) {
-    const int key = __float_as_int(rowv[tid * 8 + 6]);
-    bool first = true;
-    for (int k = 0; k < tid; ++k) first = first && __float_as_int(rowv[k * 8 + 6]) != key;
-    if (first) {
-      float sm = 0.f;
-      for (int k = tid; k < 16; ++k) sm += __float_as_int(rowv[k * 8 + 6]) == key ? rowv[k * 8 + 7] : 0.f;
-      atomicAdd(&hd.hist[key], sm);
-    }
-  }
   // hand-off without fences (MI355X_MICROARCH.md: an agent fence costs 1.7-3.5 us): sc1 stores,
   // the storing wave's vmcnt(0), a workgroup barrier, ONE lane's agent-scope counter add; the
   // workgroup whose add came last reads the partials with sc1 loads
