@@ -239,7 +239,7 @@ __global__ __launch_bounds__(IGG_BWB * IGG_NMAX) void ig_gcn_pool_bwd_kernel(
     if (bb < B && ch >= 0) {
       const float* gp = g + ((long)t * Mp + (long)s_off * B + bb) * Cp + ch;
       const long stride = (long)B * Cp;
-#pragma unroll 32
+#pragma unroll 8
       for (int s = 0; s < kk; ++s) {
         acc += wts[s] * gp[s * stride];
         P[(s + 1) * PC] = acc;

@@ -17,6 +17,11 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   rc=$?; tail -3 $OUT/pytest.log; grep -E "^(FAILED|ERROR)" $OUT/pytest.log | head -20
   [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 fi
+if [ "${SMOKE:-1}" = "1" ]; then
+  step "smoke"
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 3; }
+  grep -v amdgpu.ids $OUT/smoke.log | tail -2
+fi
 step "bench cml"
 timeout -k 10 300 python bench.py --steps 400 --warmup 24 > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 3; }
 tail -1 $OUT/bench.log
