@@ -144,6 +144,10 @@ class IntegratedGradients:
         import dataclasses
         ts = [getattr(batch, f) for f in self._GRAPH_FIELDS]
         key = tuple((None if t is None else (tuple(t.shape), t.dtype, str(t.device))) for t in ts)
+        # the graph reads the weights and buffers by address: a model whose tensors were replaced
+        # (moved, re-created) must be captured again (in-place updates such as load_state_dict or
+        # an optimizer step keep the addresses and are seen by the replay)
+        key += tuple(t.data_ptr() for t in list(self.model.parameters()) + list(self.model.buffers()))
         if self._graph is None or self._graph[0] != key:
             self._graph = None
             static = dataclasses.replace(batch, **{f: (None if t is None else t.clone())
