@@ -48,6 +48,9 @@ def main(argv=None):
     ap.add_argument("--k", type=int, default=5, help="neighbours per node for --adjacency knn")
     ap.add_argument("--no-knn-line", dest="knn_line", action="store_false",
                     help="skip the second measurement on the k=5 graph (reported as 'knn5' in the JSON line)")
+    ap.add_argument("--no-ig-line", dest="ig_line", action="store_false",
+                    help="skip the integrated-gradients throughput (BASELINE.json config v; reported as 'ig' in "
+                         "the JSON line, one GPU only)")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -139,6 +142,30 @@ def main(argv=None):
         dt5, _, loss5, _ = measure(g5)
         knn = {"adjacency": "knn(k=5)", "value": round(windows / dt5, 2),
                "ms_per_step": round(1000.0 * dt5 / args.steps, 4), "final_loss": round(loss5, 5)}
+    ig = None
+    if args.ig_line and world == 1 and not soil and not baseline and dev.type == "cuda":
+        # BASELINE.json config (v): integrated-gradients attribution of the CML GCN (m_steps = 100: 101
+        # forward + backward passes per explained window), on the trained-for-a-few-steps model
+        from gnnqc.xai.ig import IntegratedGradients
+        store, model = trainer.store, trainer.model
+        expl = IntegratedGradients(model, "cml", m_steps=100, max_rows=32768)
+        B, nb = 256, 6
+        span = max(1, store.n_windows - B)
+
+        def ig_batch(i):
+            s0 = (i * B) % span
+            return store.gather(torch.arange(s0, s0 + B, device=dev))
+
+        for i in range(2):                        # graph capture + one replay outside the timed region
+            expl.attribute(ig_batch(i))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nb):
+            expl.attribute(ig_batch(2 + i))
+        torch.cuda.synchronize()
+        dti = time.perf_counter() - t0
+        ig = {"metric": "integrated-gradients explained windows/s (CML GCN, m_steps=100, 101 passes per window)",
+              "value": round(nb * B / dti, 2), "windows_per_call": B, "ms_per_call": round(1e3 * dti / nb, 3)}
     if rank == 0:
         out = {
             "metric": ("train windows/sec, SoilNet GCN (diagnostic; not the headline metric)" if soil else
@@ -177,6 +204,8 @@ def main(argv=None):
         }
         if knn is not None:
             out["knn5"] = knn
+        if ig is not None:
+            out["ig"] = ig
         if comm_us is not None:
             out["allreduce_us"] = round(comm_us, 2)        # mean RCCL all-reduce of the flat gradients
             out["allreduce_mode"] = (("peer one-shot xGMI" if trainer.peer is not None else "RCCL") +
