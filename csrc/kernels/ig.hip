@@ -177,19 +177,58 @@ __global__ __launch_bounds__(256) void ig_gcn_pool_fwd_kernel(
     wn[n] = (live && n < N) ? w[(long)b * N + n] : 0.f;
   }
   const float a_in = (live && f < Ca) ? anom[((long)b * T + t) * Ca + f] : 0.f;
+  // Piecewise-linear form over the path (see the backward): prelu(y_n(s)) = c_n(s) y_n(s) with
+  // c_n in {1, al} flipping at most once, at j_n, so out(s) = alpha_s S1(s) + A0 S0(s) where
+  // S1 = sum_n w_n c_n(s) xs_n and S0 = sum_n w_n c_n(s) change only at the flips: per node one
+  // binary search, then a running sum over the steps (O(N log kk + kk) per thread, not O(N kk)).
+  const float a_first = alphas[0], a_last = alphas[kk - 1];
+  float S1 = 0.f, S0 = 0.f;
+  int jn[NM];
+  float d1[NM], d0[NM];
+#pragma unroll
+  for (int n = 0; n < NM; ++n) {
+    const bool p0 = a_first * xs[n] + A0 > 0.f, p1 = a_last * xs[n] + A0 > 0.f;
+    const float c0 = p0 ? 1.f : al, c1 = p1 ? 1.f : al;
+    S1 += wn[n] * c0 * xs[n];
+    S0 += wn[n] * c0;
+    int j = kk;                                     // no flip along the path
+    if (p0 != p1) {
+      int lo = 0, hi = kk - 1;                      // p(lo) == p0, p(hi) != p0
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((alphas[mid] * xs[n] + A0 > 0.f) == p0) lo = mid;
+        else hi = mid;
+      }
+      j = hi;
+    }
+    jn[n] = j;
+    d1[n] = wn[n] * (c1 - c0) * xs[n];
+    d0[n] = wn[n] * (c1 - c0);
+  }
+  float* D1 = so + IGG_FSG * BB * Cp + threadIdx.x;  // this thread's flip deltas [IGG_FSG][256]
+  float* D0 = D1 + IGG_FSG * 256;
   const int rowf = nb * Cp;                         // floats of one step's rows (contiguous)
   for (int s0 = 0; s0 < kk; s0 += IGG_FSG) {
     const int ns = min(IGG_FSG, kk - s0);
+#pragma unroll
+    for (int q = 0; q < IGG_FSG; ++q) {
+      D1[q * 256] = 0.f;
+      D0[q * 256] = 0.f;
+    }
+#pragma unroll
+    for (int n = 0; n < NM; ++n) {
+      const int r = jn[n] - s0;
+      if (r >= 0 && r < IGG_FSG) {
+        D1[r * 256] += d1[n];
+        D0[r * 256] += d0[n];
+      }
+    }
     for (int si = 0; si < ns; ++si) {
       const float a = alphas[s0 + si];
-      float acc = 0.f;
-#pragma unroll
-      for (int n = 0; n < NM; ++n) {
-        const float y = a * xs[n] + A0;
-        acc += wn[n] * (y > 0.f ? y : al * y);
-      }
+      S1 += D1[si * 256];
+      S0 += D0[si * 256];
       float* o = so + (si * BB + bl) * Cp;
-      o[Ca + f] = acc;
+      o[Ca + f] = a * S1 + A0 * S0;
       if (f < Ca) o[f] = a * a_in;
       for (int c = Ca + F + f; c < Cp; c += F) o[c] = 0.f;
     }
@@ -334,7 +373,8 @@ at::Tensor ig_gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::T
   at::Tensor out = at::empty({T, Mp, Cp}, x.options());
 #define GQ_IGG_FWD(NMV)                                                                                     \
   hipLaunchKernelGGL((ig_gcn_pool_fwd_kernel<CIN, FF, NMV>), dim3((B + 256 / FF - 1) / (256 / FF), T), dim3(256), \
-                     (size_t)IGG_FSG * (256 / FF) * Cp * sizeof(float), stream(), x.data_ptr<float>(),              \
+                     ((size_t)IGG_FSG * (256 / FF) * Cp + 2 * IGG_FSG * 256) * sizeof(float), stream(),           \
+                     x.data_ptr<float>(),                                                                           \
                      w.data_ptr<float>(), Ca ? anom.data_ptr<float>() : nullptr, W.data_ptr<float>(),               \
                      b.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(), \
                      alphas.data_ptr<float>(), out.data_ptr<float>(), B, T, N, Ca, kk, (int)Mp, (int)Cp)
