@@ -61,7 +61,7 @@ fi
 [ "${SKIP_CML_PROF:-0}" = "1" ] || {
 step "rocprofv3 cml"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-  python3 $ROOT/bench.py --steps 48 --warmup 8 > $OUT/prof.log 2>&1
+  python3 $ROOT/bench.py --steps 48 --warmup 8 --no-ig-line --no-knn-line > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
 f=$(ls $OUT/prof/run_kernel_stats.csv $OUT/prof/*/run_kernel_stats.csv 2>/dev/null | head -1)
 [ -n "$f" ] && python3 $ROOT/scripts/prof_summary.py $f 56 30 > $OUT/cml_stats.txt && cat $OUT/cml_stats.txt
