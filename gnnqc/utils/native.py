@@ -17,7 +17,9 @@ import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(__file__)), "_lib")
 HOST_LIB = os.path.join(LIB_DIR, "libgnnqc_host.so")
-HIP_LIB = os.path.join(LIB_DIR, "libgnnqc_hip.so")
+# GNNQC_HIP_LIB: an alternative build of the HIP library (A/B measurements of compile-time variants,
+# scripts/build_chain_variants.py); unset in every normal run
+HIP_LIB = os.environ.get("GNNQC_HIP_LIB") or os.path.join(LIB_DIR, "libgnnqc_hip.so")
 
 _lock = threading.Lock()
 _host = None
