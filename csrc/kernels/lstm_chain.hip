@@ -41,15 +41,20 @@ namespace gq {
 static constexpr int CHAIN_MAX = 8;
 static constexpr int CHAIN_SPIN = 1 << 20;
 // granule ring depth of a non-pooling consumer: an sc1 load of a line another CU wrote
-// through to memory takes microseconds under load, D steps of ~0.33 us each must cover it
+// through to memory takes microseconds under load, D steps of ~0.33 us each must cover it.
+// D, LEAD1 and CHAINB_LEAD (below) from a same-box sweep of compile-time variants
+// (scripts/build_chain_variants.py, scripts/gpu_ab_chain.sh; CML step, ms): D = 6 / LEAD 2 / 2:
+// 0.3099 0.3092; D = 5: 0.3105; D = 4: 0.3072 0.3070; D = 3: 0.3055; D = 8: 0.3121; D = 4 with
+// CHAINB_LEAD 1: 0.3025; D = 4 with both leads 1: 0.3021 0.3022 0.3006 (kept); D = 3 with both
+// leads 1: 0.3044 0.2999. A shorter ring lets each consumer start sooner behind its producer.
 #ifndef CHAIN_D
-#define CHAIN_D 6
+#define CHAIN_D 4
 #endif
 #ifndef CHAIN_D3
 #define CHAIN_D3 3           // ring of a pooling (PIN = 3) consumer: it runs at a third of the rate
 #endif
 #ifndef CHAIN_LEAD1
-#define CHAIN_LEAD1 2
+#define CHAIN_LEAD1 1
 #endif
 #ifndef CHAIN_LEAD3
 #define CHAIN_LEAD3 1
@@ -680,7 +685,7 @@ struct ChainT4BLds {
 static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT4BLds::BYTES : CHAINB_LDS_STAGE;
 
 #ifndef CHAINB_LEAD
-#define CHAINB_LEAD 2
+#define CHAINB_LEAD 1
 #endif
 // ring depths (reverse steps of prefetch) per hidden size
 #ifndef CHAINB_D16
