@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """Flagship benchmark: CML GCN training throughput (windows/s) on N MI355X.
 
-    python bench.py --gpus N --steps K --warmup W
-    torchrun --nproc-per-node N bench.py --gpus N ...      (driver launches N > 1 like this)
+    python bench.py --gpus N --steps K --warmup W          (N > 1: spawns the N rank processes itself)
+    torchrun --nproc-per-node N bench.py --gpus N ...      (or one rank per GPU from a launcher)
 
-One process per GPU, data parallel over RCCL (backend "nccl"). Per-GPU batch is the
+One process per GPU, data parallel over RCCL (backend "nccl"). Without a launcher (no WORLD_SIZE in the
+environment) ``--gpus N > 1`` starts N child processes of this script with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set; the parent never touches HIP, forwards rank 0's
+JSON line (the children inherit stdout) and exits non-zero if any child fails. Under a launcher,
+WORLD_SIZE must equal ``--gpus``. Per-GPU batch is the
 reference's ``batch_size`` 128 windows (weak scaling: global batch = 128 * N).
 Model = the reference CML GCN architecture (GeneralConv 2->16 + mean pooling +
 7-layer LSTM TimeLayer 16/16/32/32/64/64/128 + dense head, 188,193 trainables),
@@ -20,6 +24,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,7 +34,91 @@ import torch
 REF_GCN_WINDOWS_PER_S = 350.0   # reference GCN predict() on V100 (training not published)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Run this script as ``n`` rank processes (one per GPU) and wait for all of them. The parent
+    only counts devices (``torch.cuda.device_count`` does not initialise HIP) and never calls into
+    the GPU; a child that fails takes the others down (exact Popen handles, no pattern kills) and
+    its exit code becomes this process's."""
+    ndev = torch.cuda.device_count()
+    if ndev and n > ndev:
+        print(f"bench.py: --gpus {n} but only {ndev} GPUs are visible", file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if not ndev:                  # CPU (gloo) rehearsal: do not oversubscribe the cores
+            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // n)))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def measure_ig(args, trainer, dev, world, rank, D):
+    """BASELINE.json config (v): integrated-gradients attribution of the CML GCN (m_steps = 100: 101
+    forward + backward passes per explained window) on the trained-for-a-few-steps model. Batches are
+    dealt round-robin over the ranks (batch i on rank i % world, as the reference deals them over
+    workers, ``xai/libs/integrated_gradients.py:180-187,432-448``); every rank explains ``calls`` of
+    them. Aggregate explained windows/s over the max-over-ranks time."""
+    from gnnqc.xai.ig import IntegratedGradients
+    gpu = dev.type == "cuda"
+    B = args.ig_windows or (256 if gpu else 4)
+    nb = args.ig_calls or (6 if gpu else 1)
+    store, model = trainer.store, trainer.model
+    expl = IntegratedGradients(model, "cml", m_steps=100, max_rows=32768)
+    span = max(1, store.n_windows - B)
+
+    def ig_batch(j):                  # this rank's j-th batch = global batch rank + world * j
+        s0 = ((rank + world * j) * B) % span
+        return store.gather(torch.arange(s0, s0 + B, device=dev))
+
+    warm = 2 if gpu else 0            # graph capture + one replay outside the timed region
+    for j in range(warm):
+        expl.attribute(ig_batch(j))
+    D.barrier()
+    if gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(nb):
+        expl.attribute(ig_batch(warm + j))
+    if gpu:
+        torch.cuda.synchronize()
+    D.barrier()
+    dti = D.max_over_ranks(time.perf_counter() - t0)
+    return {"metric": "integrated-gradients explained windows/s (CML GCN, m_steps=100, 101 passes per window)",
+            "value": round(world * nb * B / dti, 2), "windows_per_call": B, "calls_per_rank": nb,
+            "n_ranks": world, "ms_per_call": round(1e3 * dti / nb, 3),
+            "sharding": "round-robin batches over ranks" if world > 1 else "one rank"}
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -50,8 +140,19 @@ def main(argv=None):
                     help="skip the second measurement on the k=5 graph (reported as 'knn5' in the JSON line)")
     ap.add_argument("--no-ig-line", dest="ig_line", action="store_false",
                     help="skip the integrated-gradients throughput (BASELINE.json config v; reported as 'ig' in "
-                         "the JSON line, one GPU only)")
+                         "the JSON line; under DP every rank explains its own shard of the batches)")
+    ap.add_argument("--ig-windows", type=int, default=None,
+                    help="windows per attribute() call (default 256 on a GPU, 4 on the CPU)")
+    ap.add_argument("--ig-calls", type=int, default=None,
+                    help="timed attribute() calls per rank (default 6 on a GPU, 1 on the CPU)")
     args = ap.parse_args(argv)
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus, argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from gnnqc import config as C
@@ -66,6 +167,9 @@ def main(argv=None):
 
     dev = D.init_distributed()
     world, rank = D.world_size(), D.rank()
+    if os.environ.get("GNNQC_BENCH_FAIL_RANK") == str(rank):    # fault injection (tests/test_bench_launch.py)
+        print(f"bench.py: rank {rank} failing on request", file=sys.stderr)
+        return 3
     torch.manual_seed(1234)
     soil = args.ds == "soilnet"
     args.sensors = args.sensors or (40 if soil else 23)
@@ -143,29 +247,8 @@ def main(argv=None):
         knn = {"adjacency": "knn(k=5)", "value": round(windows / dt5, 2),
                "ms_per_step": round(1000.0 * dt5 / args.steps, 4), "final_loss": round(loss5, 5)}
     ig = None
-    if args.ig_line and world == 1 and not soil and not baseline and dev.type == "cuda":
-        # BASELINE.json config (v): integrated-gradients attribution of the CML GCN (m_steps = 100: 101
-        # forward + backward passes per explained window), on the trained-for-a-few-steps model
-        from gnnqc.xai.ig import IntegratedGradients
-        store, model = trainer.store, trainer.model
-        expl = IntegratedGradients(model, "cml", m_steps=100, max_rows=32768)
-        B, nb = 256, 6
-        span = max(1, store.n_windows - B)
-
-        def ig_batch(i):
-            s0 = (i * B) % span
-            return store.gather(torch.arange(s0, s0 + B, device=dev))
-
-        for i in range(2):                        # graph capture + one replay outside the timed region
-            expl.attribute(ig_batch(i))
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(nb):
-            expl.attribute(ig_batch(2 + i))
-        torch.cuda.synchronize()
-        dti = time.perf_counter() - t0
-        ig = {"metric": "integrated-gradients explained windows/s (CML GCN, m_steps=100, 101 passes per window)",
-              "value": round(nb * B / dti, 2), "windows_per_call": B, "ms_per_call": round(1e3 * dti / nb, 3)}
+    if args.ig_line and not soil and not baseline:
+        ig = measure_ig(args, trainer, dev, world, rank, D)
     if rank == 0:
         out = {
             "metric": ("train windows/sec, SoilNet GCN (diagnostic; not the headline metric)" if soil else
@@ -216,4 +299,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

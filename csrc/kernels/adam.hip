@@ -398,8 +398,16 @@ __global__ __launch_bounds__(256) void adam_flagged_kernel(
       reinterpret_cast<float4*>(m)[i] = mm;
       reinterpret_cast<float4*>(v)[i] = vv;
     }
-    // g[0] stays until the last arrival clears it: every workgroup reads it first
-    reinterpret_cast<float4*>(g)[i] = make_float4(i == 0 ? gg.x : 0.f, 0.f, 0.f, 0.f);
+    // g[0] stays until the last arrival clears it (every workgroup reads it first): the first
+    // float4's owner never stores lane x, so the last arrival's clear is the only write of g[0]
+    // (a store of the old value here could land after that clear)
+    if (i == 0) {
+      g[1] = 0.f;
+      g[2] = 0.f;
+      g[3] = 0.f;
+    } else {
+      reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
   const long it = n4 * 4 + i;                    // (n % 4 tail: one element per thread at most)
   if (it < n) {

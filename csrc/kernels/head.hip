@@ -22,6 +22,8 @@
 
 namespace gq {
 
+int* chain_ctl(int dev);   // lstm_chain.hip: the device's chain control words
+
 constexpr int HT = 16;     // rows per tile: 8 workgroups for a CML batch of 128 (LDS-bound loops
                            // spread over 8 CUs; 64-row tiles left 2 CUs doing 4x the work each)
 constexpr int HU = 64;     // dense units (model_config dense.units)
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const float* __restrict__ logits, const float* __restrict__ y, const float* __restrict__ mask, int R,
     float alpha1, float alpha2, float w0, float w1, const float* __restrict__ gout, const float* __restrict__ aux,
     float* __restrict__ dfeat, int ldd, float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ dW2,
-    float* __restrict__ db2, float* __restrict__ dW3, float* __restrict__ db3) {
+    float* __restrict__ db2, float* __restrict__ dW3, float* __restrict__ db3, int* __restrict__ nf) {
   constexpr int KPT = F / 4;            // dW1 rows per thread
   constexpr int RPT = HT * F / 256;     // dfeat rows per thread
   __shared__ float sf[HT][F + 4];
@@ -337,11 +339,20 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     }
     __syncthreads();
   }
-  // flush: coalesced atomics (lanes = consecutive j)
+  // flush: coalesced atomics (lanes = consecutive j); a non-finite partial raises the flag the
+  // flag-driven Adam decides from (chain control word 7)
+  bool fin = isfinite(aW3) && isfinite(ab1) && isfinite(ab2) && isfinite(ab3);
 #pragma unroll
-  for (int q = 0; q < KPT; ++q) atomicAdd(&dW1[(g * KPT + q) * HU + j], aW1[q]);
+  for (int q = 0; q < KPT; ++q) {
+    fin = fin && isfinite(aW1[q]);
+    atomicAdd(&dW1[(g * KPT + q) * HU + j], aW1[q]);
+  }
 #pragma unroll
-  for (int q = 0; q < UPG; ++q) atomicAdd(&dW2[(g * UPG + q) * HU + j], aW2[q]);
+  for (int q = 0; q < UPG; ++q) {
+    fin = fin && isfinite(aW2[q]);
+    atomicAdd(&dW2[(g * UPG + q) * HU + j], aW2[q]);
+  }
+  if (!fin && nf != nullptr) __hip_atomic_store(nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   red[g][j] = aW3;
   __syncthreads();
   if (g == 0) {
@@ -439,7 +450,8 @@ at::Tensor head_bwd(const at::Tensor& feat, const at::Tensor& W1, const at::Tens
                                            (float)w1, gout.data_ptr<float>(), aux.data_ptr<float>(),
                                            need_dfeat ? dfeat.data_ptr<float>() : nullptr, F,
                                            dW1.data_ptr<float>(), db1.data_ptr<float>(), dW2.data_ptr<float>(),
-                                           db2.data_ptr<float>(), dW3.data_ptr<float>(), db3.data_ptr<float>()));
+                                           db2.data_ptr<float>(), dW3.data_ptr<float>(), db3.data_ptr<float>(),
+                                           chain_ctl(feat.get_device()) + 7));
   GQ_LAUNCH_CHECK();
   return dfeat;
 }

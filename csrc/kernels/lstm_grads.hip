@@ -22,6 +22,8 @@
 
 namespace gq {
 
+int* chain_ctl(int dev);   // lstm_chain.hip: the device's chain control words
+
 std::vector<DeferredRed>& deferred_reds() {
   static std::vector<DeferredRed> v;
   return v;
@@ -40,18 +42,19 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
 __global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __restrict__ ws, int splits, int RC,
                                                                 float* __restrict__ ws2, int ncb, int DT, int HT,
                                                                 int Din, int H, float* __restrict__ dW,
-                                                                float* __restrict__ db, float* __restrict__ dU) {
-  lstm_grads_reduce_body(ws, splits, RC, ws2, ncb, DT, HT, Din, H, dW, db, dU, blockIdx.x, blockIdx.y, gridDim.y);
+                                                                float* __restrict__ db, float* __restrict__ dU,
+                                                                int* nf) {
+  lstm_grads_reduce_body(ws, splits, RC, ws2, ncb, DT, HT, Din, H, dW, db, dU, blockIdx.x, blockIdx.y, gridDim.y, nf);
 }
 
 __global__ __launch_bounds__(256) void lstm_grads_reduce_final_kernel(const float* __restrict__ ws2, int NG, int RC,
                                                                       int ncb, int DT, int HT, int Din, int H,
                                                                       float* __restrict__ dW, float* __restrict__ db,
-                                                                      float* __restrict__ dU) {
+                                                                      float* __restrict__ dU, int* nf) {
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < RC; e += gridDim.x * blockDim.x) {
     float s = 0.f;
     for (int g = 0; g < NG; ++g) s += ws2[(size_t)g * RC + e];
-    grads_add(s, e, ncb, DT, HT, Din, H, dW, db, dU);
+    grads_add(s, e, ncb, DT, HT, Din, H, dW, db, dU, nf);
   }
 }
 
@@ -125,12 +128,15 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
     deferred_reds().push_back(DeferredRed{ws_t, H, Din, splits, dW, dU, db});
     return;
   }
+  // every weight-gradient reduction raises the non-finite flag (chain control word 7) that the
+  // flag-driven Adam (adam_flagged) decides from
+  int* nf = chain_ctl(c10::hip::current_device()) + 7;
   hipLaunchKernelGGL(lstm_grads_reduce_kernel, dim3((RC + 15) / 16, NG), dim3(256), 0, st, ws, splits, RC, ws2, ncb,
-                     DT, HT, Din, H, dW, db, dU);
+                     DT, HT, Din, H, dW, db, dU, nf);
   GQ_LAUNCH_CHECK();
   if (NG > 1) {
     hipLaunchKernelGGL(lstm_grads_reduce_final_kernel, dim3(std::min((RC + 255) / 256, 1024)), dim3(256), 0, st, ws2,
-                       NG, RC, ncb, DT, HT, Din, H, dW, db, dU);
+                       NG, RC, ncb, DT, HT, Din, H, dW, db, dU, nf);
     GQ_LAUNCH_CHECK();
   }
 }

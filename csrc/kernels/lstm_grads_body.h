@@ -27,6 +27,7 @@ struct RedJob {
   float* dW;
   float* db;
   float* dU;
+  int* nf;                // non-finite gradient flag (chain control word 7, read by adam_flagged)
   int splits, RC, ncb, DT, HT, Din, H, nblocks, kb;
 };
 

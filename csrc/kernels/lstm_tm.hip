@@ -599,10 +599,10 @@ __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
   if (rb < rj.nblocks) {
     if (rj.kb > 1)     // many slots: KB slot blocks per workgroup
       lstm_grads_reduce_multi<PIPE_RED_KB>(rj.ws, rj.splits, rj.RC, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
-                                           rj.dU, rb);
+                                           rj.dU, rb, rj.nf);
     else               // few slots, many splits: one slot block per workgroup, 4 add chains per lane
       lstm_grads_reduce_body(rj.ws, rj.splits, rj.RC, nullptr, rj.ncb, rj.DT, rj.HT, rj.Din, rj.H, rj.dW, rj.db,
-                             rj.dU, rb, 0, 1);
+                             rj.dU, rb, 0, 1, rj.nf);
   }
 }
 
@@ -863,6 +863,7 @@ at::Tensor lstm_tm_bwd_pipe(const at::Tensor& dh, const at::Tensor& g, const at:
     rj.dW = rdW.data_ptr<float>();
     rj.dU = rdU.data_ptr<float>();
     rj.db = rdb.data_ptr<float>();
+    rj.nf = chain_ctl(rws.get_device()) + 7;
     // the wide form once the one-block-per-16-slots grid would exceed a few waves of workgroups
     rj.kb = (rj.RC + 15) / 16 > 1024 ? PIPE_RED_KB : 1;
     rj.nblocks = (rj.RC + 16 * rj.kb - 1) / (16 * rj.kb);
@@ -1104,7 +1105,7 @@ int64_t lstm_reduce_flush() {
     const int kn = std::min(MULTI_MAX, n - k0);
     MultiRed R{};
     R.n = kn;
-    R.nf = nullptr;
+    R.nf = chain_ctl(c10::hip::current_device()) + 7;
     int nb = 0;
     for (int k = 0; k < kn; ++k) {
       const DeferredRed& d = q[k0 + k];

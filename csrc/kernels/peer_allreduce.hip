@@ -17,7 +17,7 @@
 // peer's region; the reader acquires each flag at system scope and reads peer data with 16-byte
 // loads that bypass L1 and L2 (sc0 sc1; no stale lines from two launches ago). The region is
 // uncached device memory where the driver allows it. Every spin is bounded: a workgroup that
-// gives up rejects the step (chain word 2, read by the optimiser's guard), sets ctl[2] and exits;
+// gives up rejects the step (non-finite flag word 7 + a NaN in its slice), sets ctl[2] and exits;
 // the host all-reduces ctl[2] at the epoch end and raises on every rank. It never hangs the device.
 // Verified bitwise against RCCL / gloo with two ranks on ONE GPU only (tests/test_dp_gpu.py):
 // between different GPUs over xGMI it is unverified (no multi-GPU box was available).
@@ -95,12 +95,16 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(PeerArgs A) {
       }
     }
     if (!ok) {
-      // ANY workgroup that gave up rejects the whole step on this rank through the optimiser's
-      // guard (ext[2], read by adam_guarded / adam_flagged; counted in ext[3]) and records the
-      // timeout for the host (ctl[2]), which all-reduces it at the epoch end and raises on every
-      // rank: a peer timeout is fatal for the job, since the ranks' parameters may now differ.
+      // ANY workgroup that gave up rejects the whole step on this rank: it raises the non-finite
+      // gradient flag (ext[7], read by adam_flagged; adam_guarded scans g) and leaves a NaN in the
+      // first element of its own, never-reduced slice (so an unguarded update shows it too). The
+      // timeout is recorded in this region's own control word (ctl[2], not the chain-timeout word),
+      // which the host all-reduces at the epoch end and raises on every rank: a peer timeout is
+      // fatal for the job, since the ranks' parameters may now differ.
       __hip_atomic_store(A.ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (A.ext != nullptr) __hip_atomic_store(A.ext + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (A.ext != nullptr) __hip_atomic_store(A.ext + 7, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const long i0 = blockIdx.x * 256L * 4;
+      if (i0 < A.n) A.g[i0] = __builtin_nanf("");
     }
     go = ok;
   }

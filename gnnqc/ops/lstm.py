@@ -230,10 +230,22 @@ def direct_grad_accumulation(flag: bool = True):
             hip_ops().lstm_reduce_flush()
 
 
+class _Unflagged:
+    count = 0     # gradients handed back to autograd (summed into .grad by PyTorch: no non-finite flag)
+
+
+def unflagged_grad_writes() -> int:
+    """How many weight gradients so far went through autograd's own accumulation instead of a HIP
+    kernel that raises the non-finite flag (chain control word 7). The trainer takes the flag-driven
+    Adam only for steps whose backward added none (``gnnqc.train.engine.Trainer._body``)."""
+    return _Unflagged.count
+
+
 def _grad_sink(p: torch.Tensor):
     g = p.grad if _DirectGrad.enabled and isinstance(p, torch.nn.Parameter) else None
     if g is not None and g.is_contiguous() and g.dtype == torch.float32 and g.device == p.device:
         return g, True
+    _Unflagged.count += 1
     return torch.zeros_like(p), False
 
 
@@ -763,6 +775,6 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
     return lstm_eager(x, W, U, b, return_sequences, activation)
 
 
-__all__ = ["lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
+__all__ = ["unflagged_grad_writes", "lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
            "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError", "lstm_chain_head_tm",
            "direct_grad_accumulation"]

@@ -128,13 +128,17 @@ class Trainer:
         self._graph_loss = None
         self._multi_loss = None
         # the store-fused CML step's gradient kernels all flag non-finite values: the update can
-        # decide from those flags (one pass, no grid-wide barrier; gnnqc.ops.optim.FlatAdam)
+        # decide from those flags (one pass, no grid-wide barrier; gnnqc.ops.optim.FlatAdam). This is
+        # the mode's eligibility; every step (and so every captured graph) re-checks that its backward
+        # really wrote all gradients through flagging kernels (_body)
+        self._flag_base = False
         if hasattr(self.opt, "flagged_producers"):
             was = self.model.training
             self.model.train()
-            self.opt.flagged_producers = bool(
+            self._flag_base = bool(
                 self.device.type == "cuda" and self._store_fused() and self.model.regularization_loss() is None
                 and os.environ.get("GNNQC_FLAGGED_ADAM", "1") == "1")
+            self.opt.flagged_producers = self._flag_base
             self.model.train(was)
 
     # ---------------------------------------------------------------- body
@@ -190,8 +194,13 @@ class Trainer:
             self.opt.zero_grad()
         with _rf("gnnqc.forward"):
             total, loss, z, b = self._loss(wids, self.train_metrics)
+        from ..ops.lstm import unflagged_grad_writes
+        n_unflagged = unflagged_grad_writes()
         with _rf("gnnqc.backward"), direct_grad_accumulation(True):
             total.backward(self._one)          # (a kept seed: no ones_like fill launch per step)
+        if self._flag_base:
+            # a gradient summed by autograd itself raised no flag: this step takes the scanning update
+            self.opt.flagged_producers = unflagged_grad_writes() == n_unflagged
         if self.poison is not None:
             self.opt.flat_g[:1].add_(self.poison)
         self.last_loss = loss.detach()       # (a reference, not a copy launch: graph replays refresh it)
@@ -405,6 +414,8 @@ class Trainer:
         self.train_metrics.reset()
         self._comm_events = []
         skipped0 = self.opt.skipped_steps
+        upd_state = getattr(self.opt, "guard_state", None)
+        partial0 = int(upd_state[5].item()) if upd_state is not None else 0
         rejected0 = self._chain_rejected()
         steps0 = self.global_step
         t0 = time.perf_counter()
@@ -433,6 +444,14 @@ class Trainer:
         dt = time.perf_counter() - t0
         nsteps = self.global_step - steps0
         logs["skipped_steps"] = float(self.opt.skipped_steps - skipped0)
+        if upd_state is not None:
+            # gradient elements the flag-driven Adam left untouched because they were not finite
+            # although no producer flagged them (an fp32 overflow of a sum of finite parts)
+            logs["nonfinite_grad_elements"] = float(int(upd_state[5].item()) - partial0)
+            if logs["nonfinite_grad_elements"]:
+                import warnings
+                warnings.warn(f"{int(logs['nonfinite_grad_elements'])} non-finite gradient element(s) were "
+                              "skipped by the update this epoch (their parameters were not changed)")
         if hasattr(self.opt, "check_update"):
             self.opt.check_update()
         if rejected0 is not None:

@@ -242,13 +242,19 @@ class IntegrateGradientsAnalyser:
         if self.df_unfiltered is None:
             self.get_overview(plots=False)
         sub = self.df_unfiltered[self.df_unfiltered["sensor_id"] == str(sensor)].sort_values("date_time")
-        if time_from is not None and time_to is not None:
-            time_from, time_to = pd.to_datetime(time_from), pd.to_datetime(time_to)
-            sub = sub[(sub["date_time"] >= time_from) & (sub["date_time"] <= time_to)]
+        # each bound applies on its own; a missing one is the sensor's first / last sample
+        if time_from is not None:
+            time_from = pd.to_datetime(time_from)
+            sub = sub[sub["date_time"] >= time_from]
+        if time_to is not None:
+            time_to = pd.to_datetime(time_to)
+            sub = sub[sub["date_time"] <= time_to]
         if not len(sub):
             return None
-        if time_from is None or time_to is None:
-            time_from, time_to = sub["date_time"].min(), sub["date_time"].max()
+        if time_from is None:
+            time_from = sub["date_time"].min()
+        if time_to is None:
+            time_to = sub["date_time"].max()
         grid = pd.date_range(start=time_from, end=time_to, freq=pd.Timedelta(int(cfg.interval), unit="s"))
         if not len(grid):
             return None
