@@ -155,68 +155,123 @@ class IntegrateGradientsAnalyser:
         plt.close(ax.figure)
 
     # ----------------------------------------------------------------- aggregation
+    def _spatial_mean(self, sid, classes, normalize: bool):
+        """(node-mean feature gradients [T, C], anomalous-series gradients [T, C], n) averaged over
+        the samples of sensor ``sid`` whose confusion class is in ``classes``; each sample optionally
+        normalised by its max |gradient| first."""
+        sub = self.df[(self.df["sensor_id"] == sid) & self.df["confusion_matrix_abbr"].isin(classes)]
+        sf = sa = None
+        n = 0
+        for _, row in sub.iterrows():
+            gf, ga = self._load(row, STEM_GF), self._load(row, STEM_GA)
+            if gf is None and ga is None:
+                continue
+            if normalize:
+                parts = [np.abs(a).reshape(-1) for a in (gf, ga) if a is not None]
+                m = float(np.max(np.concatenate(parts))) if parts else 0.0
+                if m > 0:
+                    gf = gf / m if gf is not None else None
+                    ga = ga / m if ga is not None else None
+            f = gf.sum(0) / gf.shape[0] if gf is not None else None      # neighbour count varies: node mean
+            sf = f if sf is None else sf + f
+            sa = ga if sa is None else (sa + ga if ga is not None else sa)
+            n += 1
+        if n == 0:
+            return None, None, 0
+        return (sf / n if sf is not None else None), (sa / n if sa is not None else None), n
+
     def spatial_aggregate_gradients(self) -> dict:
-        """Per sensor: mean over selected samples of (node-mean feature gradients, anomalous-series
-        gradients), optionally normalised per sample by the max |gradient|."""
+        """Per sensor: mean over the selected samples (``spatial_aggregation.which_samples``) of the
+        node-mean feature gradients and the anomalous-series gradients, optionally normalised per
+        sample by the max |gradient| (``integrated_gradients_analyser.py`` spatial aggregation), saved
+        as ``spatial_aggregated_gradients_{features,anom_ts}_<classes>.npy``; the per-class means the
+        figure draws are kept too."""
         if self.df is None:
             self.get_overview(plots=False)
         which = list(self.an.spatial_aggregation.which_samples)
         normalize = bool(self.an.spatial_aggregation.normalize)
         out = {}
         for sid in self.selected_sensors:
-            sub = self.df[(self.df["sensor_id"] == sid) & self.df["confusion_matrix_abbr"].isin(which)]
-            sf = sa = None
-            n = 0
-            for _, row in sub.iterrows():
-                gf, ga = self._load(row, STEM_GF), self._load(row, STEM_GA)
-                if gf is None and ga is None:
-                    continue
-                if normalize:
-                    parts = [np.abs(a).reshape(-1) for a in (gf, ga) if a is not None]
-                    m = float(np.max(np.concatenate(parts))) if parts else 0.0
-                    if m > 0:
-                        gf = gf / m if gf is not None else None
-                        ga = ga / m if ga is not None else None
-                f = gf.sum(0) / gf.shape[0] if gf is not None else None      # neighbour count varies: node mean
-                sf = f if sf is None else sf + f
-                sa = ga if sa is None else (sa + ga if ga is not None else sa)
-                n += 1
+            sf, sa, n = self._spatial_mean(sid, which, normalize)
             if n == 0:
                 print("No samples found for", sid)
                 continue
             d = os.path.join(self.output_dir_analysis, str(sid))
             os.makedirs(d, exist_ok=True)
-            res = {}
+            res = {"n_samples": n, "per_class": {}}
             if sf is not None:
-                res["features"] = sf / n
-                np.save(os.path.join(d, f"spatial_aggregated_gradients_features_{self.conf_matrix_string}.npy"),
-                        res["features"])
+                res["features"] = sf
+                np.save(os.path.join(d, f"spatial_aggregated_gradients_features_{self.conf_matrix_string}.npy"), sf)
             if sa is not None:
-                res["anom_ts"] = sa / n
-                np.save(os.path.join(d, f"spatial_aggregated_gradients_anom_ts_{self.conf_matrix_string}.npy"),
-                        res["anom_ts"])
-            res["n_samples"] = n
+                res["anom_ts"] = sa
+                np.save(os.path.join(d, f"spatial_aggregated_gradients_anom_ts_{self.conf_matrix_string}.npy"), sa)
+            for cls in which:
+                cf, ca, cn = self._spatial_mean(sid, [cls], normalize)
+                if cn:
+                    res["per_class"][cls] = {"features": cf, "anom_ts": ca, "n_samples": cn}
             out[sid] = res
         self.spatial = out
         return out
 
     def plot_spatial_aggregated_gradients(self) -> List[str]:
+        """The reference's figure (``integrated_gradients_analyser.py:811-964``): per confusion class of
+        ``which_samples`` four banded rows - TL1 and TL2 of the flagged sensor's own series, then TL1
+        and TL2 of the neighbours ("N", feature gradients scaled by ``scale_feature_gradients``) - on
+        one fixed symmetric ``coolwarm`` scale (``spatial_aggregation.cbar_limit``, default the
+        reference's 0.1), rows stacked without spacing, colour bar on the left. Saved as
+        ``<sensor>/spatial_aggregated_gradients_<sensor>[_norm].png`` by the ``normalize`` flag, so the
+        two normalisation runs keep both figures. Difference: every class's rows show that class's
+        own mean (the reference draws the all-classes mean in each class's rows)."""
         if not hasattr(self, "spatial"):
             self.spatial_aggregate_gradients()
-        scale = float(self.an.spatial_aggregation.scale_feature_gradients)
+        sp = self.an.spatial_aggregation
+        scale = float(sp.scale_feature_gradients)
+        lim = float(sp.get("cbar_limit", 0.1) or 0.1)
+        norm = mcolors.Normalize(vmin=-lim, vmax=lim)
+        which = list(sp.which_samples)
+        suffix = "_norm" if bool(sp.normalize) else ""
+        n_rows = 4
         paths = []
         for sid, res in self.spatial.items():
-            panels = [(k, v * (scale if k == "features" else 1.0)) for k, v in res.items() if k != "n_samples"]
-            fig, axes = plt.subplots(len(panels), 1, figsize=(12, 1.8 * len(panels)), squeeze=False, sharex=True)
-            vmax = max(float(np.abs(v).max()) for _, v in panels) or 1.0
-            norm = mcolors.Normalize(-vmax, vmax)
-            for ax, (k, v) in zip(axes[:, 0], panels):
-                m = ax.pcolormesh(v.T, cmap="RdBu_r", norm=norm)
-                ax.set_ylabel(k + (f" x{scale:g}" if k == "features" else ""))
-            fig.colorbar(m, ax=list(axes[:, 0]))
-            axes[0, 0].set_title(f"{sid}: mean attribution over {res['n_samples']} samples ({self.conf_matrix_string})")
-            p = os.path.join(self.output_dir_analysis, str(sid), f"spatial_aggregated_{self.conf_matrix_string}.png")
-            fig.savefig(p, bbox_inches="tight")
+            fig, ax = plt.subplots(len(which) * n_rows, 1, figsize=(16, 8), sharex=True, squeeze=False)
+            ax = ax[:, 0]
+            for a in ax:
+                a.set_yticklabels([])
+                a.tick_params(axis="y", labelrotation=90)
+            pcol = None
+
+            def band(v, a):
+                v = np.asarray(v, dtype=np.float64)
+                xs = np.arange(v.shape[0] + 1) - 0.5
+                return a.pcolormesh(xs, np.array([0.0, 1.0]), v[None, :], norm=norm, alpha=0.8, cmap="coolwarm")
+
+            for i, cls in enumerate(which):
+                d = res["per_class"].get(cls)
+                if d is None:
+                    continue
+                rows = []
+                if d["anom_ts"] is not None:
+                    rows += [(d["anom_ts"][:, k], lbl) for k, lbl in ((0, "TL1"), (1, "TL2")) if k < d["anom_ts"].shape[1]]
+                if d["features"] is not None:
+                    rows += [(d["features"][:, k] * scale, lbl) for k, lbl in ((0, "TL1\nN"), (1, "TL2\nN"))
+                             if k < d["features"].shape[1]]
+                for j, (v, lbl) in enumerate(rows[:n_rows]):
+                    a = ax[i * n_rows + j]
+                    pcol = band(v, a)
+                    a.set_ylabel(lbl)
+                    a.text(0.03, 0.5, cls, ha="center", va="center", transform=a.transAxes, fontsize=16)
+            if pcol is None:
+                plt.close(fig)
+                print("No data for plotting found.")
+                continue
+            cbar_ax = fig.add_axes([0.07, 0.2, 0.01, 0.6])
+            cbar = fig.colorbar(pcol, cax=cbar_ax, orientation="vertical", location="left")
+            cbar.set_label("Attention")
+            fig.text(0.5, 0.95, "Spatially Averaged Attention for sensor " + str(sid), fontsize=16, ha="center",
+                     va="center")
+            fig.subplots_adjust(hspace=0)
+            p = os.path.join(self.output_dir_analysis, str(sid), f"spatial_aggregated_gradients_{sid}{suffix}.png")
+            fig.savefig(p)
             plt.close(fig)
             paths.append(p)
         return paths

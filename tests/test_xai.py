@@ -294,7 +294,19 @@ def test_reference_run_scripts_golden(cml_small, tmp_path):
     an = IntegrateGradientsAnalyser(pc2, mc, xc)
     an.get_overview()
     an.spatial_aggregate_gradients()
-    assert an.plot_spatial_aggregated_gradients()
+    (pn,) = an.plot_spatial_aggregated_gradients()
+    assert os.path.basename(pn) == f"spatial_aggregated_gradients_{s1}_norm.png"
+    # the script's second pass with normalize off writes its own figure (both are kept)
+    xc.integrated_gradients.analyser.spatial_aggregation["normalize"] = False
+    an = IntegrateGradientsAnalyser(pc2, mc, xc)
+    an.get_overview(plots=False)
+    an.spatial_aggregate_gradients()
+    (pr,) = an.plot_spatial_aggregated_gradients()
+    assert os.path.basename(pr) == f"spatial_aggregated_gradients_{s1}.png"
+    assert os.path.exists(pn) and os.path.exists(pr) and os.path.dirname(pn) == os.path.dirname(pr)
+    res = an.spatial[s1]
+    assert set(res["per_class"]) <= {"TP", "FP", "TN", "FN"} and res["per_class"]
+    assert sum(d["n_samples"] for d in res["per_class"].values()) == res["n_samples"]
     assert an.create_videos(sensor=s1, time_from=str(lo), time_to=str(hi))
     # a gap: one sample of the range removed -> its grid frame is NaN
     gap = sorted(want)[1]
