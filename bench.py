@@ -290,10 +290,17 @@ def main(argv=None):
         if ig is not None:
             out["ig"] = ig
         if comm_us is not None:
-            out["allreduce_us"] = round(comm_us, 2)        # mean RCCL all-reduce of the flat gradients
+            # the collective of the timed steps, run on its own (in-graph collectives cannot be timed one
+            # by one), plus the setup-time comparison of both modes when the peer kernel was considered
+            from gnnqc.parallel.peer import LAST_SELECTION
+            out["allreduce_us"] = round(comm_us, 2)
             out["allreduce_mode"] = (("peer one-shot xGMI" if trainer.peer is not None else "RCCL") +
+                                     (" fused into the Adam launch" if trainer.peer_fused() else "") +
                                      (" in-graph (timed standalone)" if trainer.dp_graph and trainer._multi_ok()
                                       else " eager"))
+            if LAST_SELECTION:
+                out["allreduce_selection"] = {k: (round(v, 2) if isinstance(v, float) else v)
+                                              for k, v in LAST_SELECTION.items()}
         print(json.dumps(out), flush=True)
     D.destroy()
 

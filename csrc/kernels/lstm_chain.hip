@@ -35,8 +35,13 @@
 #include "lstm_tm_common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace gq {
+
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 static constexpr int CHAIN_MAX = 8;
 static constexpr int CHAIN_SPIN = 1 << 20;
@@ -56,6 +61,15 @@ static constexpr int CHAIN_SPIN = 1 << 20;
                              // instead of 4 and LEAD3 = 0 were slower: 0.3054 0.3057, 0.3043)
 #ifndef CHAIN_LEAD1
 #define CHAIN_LEAD1 1
+#endif
+#ifndef CHAIN_D0
+#define CHAIN_D0 6           // x prefetch depth of stage 0 (its input is complete before the launch)
+#endif
+#ifndef CHAIN_LD16
+#define CHAIN_LD16 0         // 1: one 16-byte buffer load per granule pair (measured: stale reads, ~4.5k re-polls per launch)
+#endif
+#ifndef CHAIN_PRIO
+#define CHAIN_PRIO 2         // s_setprio of the compute waves of a stage with I/O waves
 #endif
 #ifndef CHAIN_LEAD3
 #define CHAIN_LEAD3 1
@@ -119,9 +133,23 @@ __device__ __forceinline__ void st_granule(unsigned long long* p, float v, unsig
 // slow path: lane 0 alone polls (its granule) with a growing back-off, then the wave checks
 // every lane's granule. (All 64 lanes of every waiting wave polling back-to-back loaded the
 // memory system enough to slow the running stages' own streams severalfold.)
+template <bool INL>
+__device__ __forceinline__ unsigned long long chain_wait_body(const unsigned long long* p, unsigned want, int* ctl);
 __device__ __noinline__ unsigned long long chain_wait(const unsigned long long* p, unsigned want, int* ctl) {
+  return chain_wait_body<false>(p, want, ctl);
+}
+// inlined form for the forward I/O waves: a call in their step loop made the compiler drain vmcnt
+// at the tag checks (the whole x ring waited for each step)
+__device__ __forceinline__ unsigned long long chain_wait_inl(const unsigned long long* p, unsigned want, int* ctl) {
+  return chain_wait_body<true>(p, want, ctl);
+}
+template <bool INL>
+__device__ __forceinline__ unsigned long long chain_wait_body(const unsigned long long* p, unsigned want, int* ctl) {
   unsigned long long v = 0;
   const bool l0 = (threadIdx.x & 63) == 0;
+#ifdef GQ_CHAIN_PROF
+  if (l0) __hip_atomic_fetch_add(ctl + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-polls (diagnostics)
+#endif
   int nap = 1;
   // ctl[6] != 0: a debug spin limit (tests force a timeout with it)
   const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -151,8 +179,14 @@ __device__ __forceinline__ void chain_mark(long long* pr, int step, int k) {
   if (pr != nullptr && threadIdx.x == 0 && step < CHAIN_PROF_STEPS)
     pr[step * 8 + k] = (long long)__builtin_amdgcn_s_memtime();
 }
+// (the same from lane 0 of the calling wave: the forward's I/O waves)
+__device__ __forceinline__ void chain_mark_wave(long long* pr, int step, int k) {
+  if (pr != nullptr && (threadIdx.x & 63) == 0 && step < CHAIN_PROF_STEPS)
+    pr[step * 8 + k] = (long long)__builtin_amdgcn_s_memtime();
+}
 #else
 __device__ __forceinline__ void chain_mark(long long*, int, int) {}
+__device__ __forceinline__ void chain_mark_wave(long long*, int, int) {}
 #endif
 
 // Tag base of a launch: (epoch mod (2^20 - 1)) + 1 in the high 20 bits of the 32-bit tag, the
@@ -160,9 +194,8 @@ __device__ __forceinline__ void chain_mark(long long*, int, int) {}
 // can never pass as a valid one, whatever the epoch counter has wrapped to.
 __device__ __forceinline__ unsigned chain_tag_base(unsigned E) { return ((E % 0xFFFFFu) + 1u) << 12; }
 
-// One layer of one tile: lstm_tm_fwd_kernel's step loop with the x ring fed either from
-// global memory (stage 0) or from the previous stage's granule stream (SRC), and the
-// output (optionally max-pooled) also published as granules.
+// One layer of one tile: lstm_tm_fwd_kernel's step with the x ring fed either from global memory
+// (stage 0) or from the previous stage's granule stream (SRC), the output also published as granules.
 // LDS of one stage (carved from the kernel's one buffer: the stage bodies must not each
 // reserve their own static arrays)
 template <int H, int KX>
@@ -170,40 +203,214 @@ struct ChainLds {
   static constexpr int HS = 2 * 16 * (TMC<H>::KPH + 8) * 2;
   static constexpr int XS = 2 * 16 * (32 * KX + 8) * 2;
   static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
-  static constexpr int BYTES = HS + XS + HF;
+  // (stages with a publisher wave, H <= 32) the cells' packed gates and c of two steps
+  static constexpr int GS = H <= 32 ? 2 * TMC<H>::NT * 8 : 0;
+  static constexpr int CS = H <= 32 ? 2 * TMC<H>::NT * 4 : 0;
+  static constexpr int BYTES = HS + XS + HF + GS + CS;
 };
-static constexpr int CHAIN_LDS_STAGE = ChainLds<64, 2>::BYTES;
+constexpr int chain_max2(int a, int b) { return a > b ? a : b; }
+static constexpr int CHAIN_LDS_STAGE = chain_max2(chain_max2(ChainLds<64, 2>::BYTES, ChainLds<32, 2>::BYTES),
+                                                  ChainLds<16, 2>::BYTES);
+
+// Gate scaling: sigmoid(z) = 1 / (1 + 2^(-z log2 e)), tanh(z) = 2 / (1 + 2^(-2 z log2 e)) - 1, one
+// v_exp_f32 each after one multiply. (Folding the scale into the bf16 weight fragments saved the
+// multiplies but rounded W log2(e) instead of W: the kernels' rounding no longer matched the other
+// LSTM kernels' and the numerics oracle, so the weights stay unscaled.)
+__device__ __forceinline__ float chain_gate_scale(int ag) { return ag == 2 ? -2.8853900817779268f : -1.4426950408889634f; }
+
+// Roles of a stage workgroup. H = 16 / 32: waves [0, NW) compute the cells and store their own
+// outputs straight from registers (h, the granule that publishes it, the packed gates and c for the
+// backward); they issue no global load, so no s_waitcnt vmcnt ever waits on their write-through
+// stores. D more waves (the I/O waves) take turns streaming x: I/O wave k loads the whole [16][Din]
+// tile of every step s = k (mod D) D steps ahead and, in step s - 1, waits for it (its own loads
+// only: a plain vmcnt(0)), checks the tags (re-polls a stale granule), max-pools PIN consecutive
+// steps (writing the pooled input and the argmax bytes for the backward) and writes x_s into the
+// LDS tile of the next step. (A register ring of D slots in one wave was the first form: the
+// compiler's wait insertion drained the whole ring at the top of every unrolled round.) For a last
+// stage that pools its own output, I/O wave 0 pools h from the fp32 LDS tile. One LDS barrier per
+// step. H = 64 fills a 1024-thread workgroup with compute waves: there every thread also streams x
+// through a D-slot register ring, as one role.
+// (only when they fit the 1024-thread workgroup and a lane's share of one step's tile - ngl granules
+// of pin steps each - stays within 24 registers pairs; else every thread streams, as for H = 64)
+__host__ __device__ constexpr int chain_io_waves(int nt, int d, int ngl = 1, int pin = 1) {
+  return nt + 64 * d + 64 <= 1024 && ngl * pin <= 12 ? d : 0;   // (+ the publisher wave)
+}
+// a pooling consumer (pin = 3 granules per element) splits each step's tile over two I/O waves
+__host__ __device__ constexpr int chain_io_group(int pin) { return pin > 1 ? 2 : 1; }
+// threads of a stage workgroup that run the stage (compute + I/O waves + the publisher)
+__host__ __device__ constexpr int chain_live_threads(int nt, int d, int kx, bool src, int pin) {
+  return nt + 64 * chain_io_waves(nt, d * chain_io_group(pin),
+                                  (16 * 32 * kx / (src ? 2 : 4) + 64 * chain_io_group(pin) - 1) / (64 * chain_io_group(pin)),
+                                  pin) +
+         (chain_io_waves(nt, d * chain_io_group(pin),
+                         (16 * 32 * kx / (src ? 2 : 4) + 64 * chain_io_group(pin) - 1) / (64 * chain_io_group(pin)),
+                         pin) > 0 ? 64 : 0);
+}
 
 template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN>
 __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
                                             int* ctl, char* smem) {
   using C = TMC<H>;
-  constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4;
+  constexpr int NW = C::NW, NT = C::NT, G4 = C::G4;
+  static_assert(C::CPL == 1, "chain stages run one cell per lane");
   constexpr int KPX = 32 * KX;
-  constexpr int GR = SRC ? 1 : 4;
+  // elements per streamed granule: stage 0 reads float4 of x; a stream consumer reads two adjacent
+  // 8-byte {value, tag} granules with one 16-byte load (each half is one whole granule)
+  constexpr int GR = SRC ? 2 : 4;
+  constexpr int G = chain_io_group(PIN);         // I/O waves sharing one step's tile
+  constexpr int NIOW = chain_io_waves(NT, D * G, (16 * KPX / GR + 64 * G - 1) / (64 * G), PIN);   // (0: none)
+  constexpr bool IOW = NIOW > 0;
+  constexpr int NIO = IOW ? 64 * G : NT;         // threads streaming one step's tile
+  constexpr int NSLOT = IOW ? 1 : D;             // x slots per streaming thread
+  // granules per streaming lane: I/O waves cover the largest tile the template allows; without
+  // them every thread streams one granule (the host requires 16 Din / GR <= NT then)
+  constexpr int NGL = IOW ? (16 * KPX / GR + NIO - 1) / NIO : 1;
   using L = ChainLds<H, KX>;
   static_assert(L::BYTES <= CHAIN_LDS_STAGE && L::HS % 16 == 0 && L::XS % 16 == 0, "chain LDS layout");
   auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
   auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
   auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
+  auto gst = reinterpret_cast<uint2 (*)[NT]>(smem + L::HS + L::XS + L::HF);               // [2][NT] (IOW)
+  auto cst = reinterpret_cast<float (*)[NT]>(smem + L::HS + L::XS + L::HF + L::GS);      // [2][NT] (IOW)
 
   const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, quad = lane >> 4;
   const int row0 = tile * 16;
+  const size_t hstep = (size_t)Mp * H;
+  const int To = P > 0 ? T / P : T;      // (P > 0 only without a consumer stage)
 
-  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += NT) (&hs[0][0][0])[i] = (__bf16)0.0f;
-  for (int i = tid; i < 2 * 16 * (KPX + 8); i += NT) (&xs[0][0][0])[i] = (__bf16)0.0f;
+  constexpr int NTL = NT + 64 * NIOW + (IOW ? 64 : 0);   // live threads (the rest exited)
+  for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += NTL) (&hs[0][0][0])[i] = (__bf16)0.0f;
+  for (int i = tid; i < 2 * 16 * (KPX + 8); i += NTL) (&xs[0][0][0])[i] = (__bf16)0.0f;
 
-  bf16x8_t ufr[CPL][C::KSH], wfr[CPL][KX];
-  f32x4_t bias4[CPL];
-  int unit[CPL];
+  // ---- x streaming: lane iot of a streaming wave / thread block owns granules iot + NIO j of the
+  // contiguous [16][Din] tile (mod n_gx: duplicate lanes load and write the same values; no branch
+  // around a load - the compiler drains vmcnt at the join of one)
+  const bool compute = w < NW;
+  const int iow = IOW ? (w - NW) / G : 0;        // I/O wave group (IOW): steps s = iow (mod D)
+  const int iot = IOW ? ((w - NW) % G) * 64 + lane : tid;
+  const int n_gx = 16 * Din / GR;
+  const size_t xstep = (size_t)Mp * Din;
+  // per granule: its element offset in the tile (32 bits; the tile of step tx starts at element
+  // (tx Mp + row0) Din) and its LDS byte offset in the bf16 x tile
+  int goff[NGL], loff[NGL];
 #pragma unroll
-  for (int cc = 0; cc < CPL; ++cc) {
-    const int gi = w + NW * cc;
-    const int au = 4 * gi + (col >> 2), ag = col & 3;
-    unit[cc] = 4 * gi + quad;
+  for (int j = 0; j < NGL; ++j) {
+    const int gx = min(iot + NIO * j, n_gx - 1) * GR;
+    goff[j] = gx;
+    loff[j] = ((gx / Din) * (KPX + 8) + gx % Din) * 2;
+  }
+  const size_t xbase = (size_t)row0 * Din;
+  char* xsb = reinterpret_cast<char*>(&xs[0][0][0]);
+  constexpr int XBUF = 16 * (KPX + 8) * 2;       // bytes of one x tile buffer
+  // (x granules as whole vectors: a float[4] ring was split into scalars and the compiler copied
+  // lanes of a just-issued load into the loop-carried registers - an immediate vmcnt wait for the
+  // full memory latency in every staging step)
+  f32x4_t xr[NSLOT][NGL];
+  u64x2_t xq[NSLOT][NGL][PIN];
+  // (SRC: L1-bypassing 16-byte buffer loads of the granule stream; byte offsets < 2^32, host-checked)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned long long*>(SRC ? S.xin : nullptr), (short)0, 0x7fffffff, 0x00020000);
+  auto load_x = [&](int r, int tx) {
+#pragma unroll
+    for (int q = 0; q < (SRC ? PIN : 1); ++q) {
+      const size_t tb = xbase + (size_t)(SRC ? PIN * tx + q : tx) * xstep;
+#pragma unroll
+      for (int j = 0; j < NGL; ++j) {
+        if constexpr (SRC) {
+#if CHAIN_LD16
+          const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)((tb + goff[j]) * 8), 0, 16);
+          xq[r][j][q] = u64x2_t{((unsigned long long)v.y << 32) | v.x, ((unsigned long long)v.w << 32) | v.z};
+#else
+          xq[r][j][q] = u64x2_t{ld_granule(S.xin + tb + goff[j]), ld_granule(S.xin + tb + goff[j] + 1)};
+#endif
+        } else {
+          xr[r][j] = *reinterpret_cast<const f32x4_t*>(S.x + tb + goff[j]);
+        }
+      }
+    }
+  };
+  auto stage_x = [&](int buf, int r, int tx) {
+    if constexpr (SRC) {
+      // every granule's tag first (one ballot), the re-poll only on a miss
+      bool bad = false;
+#pragma unroll
+      for (int j = 0; j < NGL; ++j)
+#pragma unroll
+        for (int q = 0; q < PIN; ++q) {
+          const unsigned want = tagb | (unsigned)(PIN * tx + q);
+          bad |= (unsigned)(xq[r][j][q].x >> 32) != want || (unsigned)(xq[r][j][q].y >> 32) != want;
+        }
+      if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+        // re-poll: every granule of the tile re-loaded AT ONCE per round (one memory round trip a
+        // round, not one per granule), short back-off, bounded (a timeout flags the step)
+#ifdef GQ_CHAIN_PROF
+        if (lane == 0) __hip_atomic_fetch_add(ctl + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int lim = lim0 > 0 ? lim0 : CHAIN_SPIN;
+        int nap = 1;
+        for (int it = 0;; ++it) {
+#pragma unroll
+          for (int q = 0; q < PIN; ++q) {
+            const size_t tb = xbase + (size_t)(PIN * tx + q) * xstep;
+#pragma unroll
+            for (int j = 0; j < NGL; ++j)
+              xq[r][j][q] = u64x2_t{ld_granule(S.xin + tb + goff[j]), ld_granule(S.xin + tb + goff[j] + 1)};
+          }
+          bad = false;
+#pragma unroll
+          for (int j = 0; j < NGL; ++j)
+#pragma unroll
+            for (int q = 0; q < PIN; ++q) {
+              const unsigned want = tagb | (unsigned)(PIN * tx + q);
+              bad |= (unsigned)(xq[r][j][q].x >> 32) != want || (unsigned)(xq[r][j][q].y >> 32) != want;
+            }
+          if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
+          if (it >= lim) {
+            __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(2);
+          nap = min(nap * 2, 16);
+        }
+      }
+      const size_t po = xbase + (size_t)tx * xstep;
+#pragma unroll
+      for (int j = 0; j < NGL; ++j) {
+        float m0 = __uint_as_float((unsigned)xq[r][j][0].x), m1 = __uint_as_float((unsigned)xq[r][j][0].y);
+        if constexpr (PIN > 1) {
+          unsigned a0 = 0, a1 = 0;
+#pragma unroll
+          for (int q = 1; q < PIN; ++q) {
+            const float v0 = __uint_as_float((unsigned)xq[r][j][q].x), v1 = __uint_as_float((unsigned)xq[r][j][q].y);
+            if (v0 > m0) { m0 = v0; a0 = q; }
+            if (v1 > m1) { m1 = v1; a1 = q; }
+          }
+          *reinterpret_cast<float2*>(S.pin_out + po + goff[j]) = make_float2(m0, m1);
+          *reinterpret_cast<unsigned short*>(S.pin_idx + po + goff[j]) = (unsigned short)(a0 | (a1 << 8));
+        }
+        *reinterpret_cast<bf16x2_t*>(xsb + buf * XBUF + loff[j]) = bf16x2_t{(__bf16)m0, (__bf16)m1};
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NGL; ++j) {
+        // GR = 4 consecutive channels of one sequence (Din % 4 == 0): one 8-byte LDS write
+        const bf16x4_t v = __builtin_convertvector(xr[r][j], bf16x4_t);
+        *reinterpret_cast<bf16x4_t*>(xsb + buf * XBUF + loff[j]) = v;
+      }
+    }
+  };
+
+  // ---- compute role: fragments of the pre-scaled gate weights, one cell (unit, sequence) per lane
+  const int wc = compute ? w : 0;
+  const int au = 4 * wc + (col >> 2), ag = col & 3;
+  const int unit = 4 * wc + quad;
+  bf16x8_t ufr[C::KSH], wfr[KX];
+  f32x4_t bias4 = {0.f, 0.f, 0.f, 0.f};
+  if (compute) {
 #pragma unroll
     for (int s = 0; s < C::KSH; ++s) {
       bf16x8_t v;
@@ -212,7 +419,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         const int k = 32 * s + 8 * quad + j;
         v[j] = (__bf16)(S.U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
       }
-      ufr[cc][s] = v;
+      ufr[s] = v;
     }
 #pragma unroll
     for (int s = 0; s < KX; ++s) {
@@ -222,150 +429,184 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
         const int k = 32 * s + 8 * quad + j;
         v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
       }
-      wfr[cc][s] = v;
+      wfr[s] = v;
     }
-    const int u = unit[cc];
-    bias4[cc] = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
+    bias4 = f32x4_t{S.b[unit], S.b[H + unit], S.b[2 * H + unit], S.b[3 * H + unit]};
   }
-
-  // x ring: granule (tid mod n_gx) of the contiguous [16][Din] tile (duplicates across lanes)
-  const int n_gx = 16 * Din / GR;
-  const int gx = (tid % n_gx) * GR;
-  const int gx_seq = gx / Din, gx_k = gx % Din;
-  const size_t xstep = (size_t)Mp * Din;
-  const size_t xoff = (size_t)row0 * Din + gx;
-  // SRC: x_t = MaxPool(PIN) of the producer's h at PIN t .. PIN t + PIN - 1 (PIN == 1: h_t),
-  // pooled here from PIN granules (value + first-max argmax byte also stored for the backward)
-  Granule<GR> xr[D];
-  unsigned long long xq[D][PIN];
-  auto load_x = [&](int j, int tx) {
-    if constexpr (SRC) {
-#pragma unroll
-      for (int r = 0; r < PIN; ++r) xq[j][r] = ld_granule(S.xin + xoff + (size_t)(PIN * tx + r) * xstep);
-    } else {
-      xr[j].load(S.x + xoff + (size_t)tx * xstep);
-    }
-  };
-  auto stage_x = [&](int buf, int j, int tx) {
-    if constexpr (SRC) {
-      bool bad = false;
-#pragma unroll
-      for (int r = 0; r < PIN; ++r) bad |= (unsigned)(xq[j][r] >> 32) != (tagb | (unsigned)(PIN * tx + r));
-      if (__builtin_amdgcn_ballot_w64(bad) != 0) {
-#pragma unroll
-        for (int r = 0; r < PIN; ++r)
-          xq[j][r] = chain_wait(S.xin + xoff + (size_t)(PIN * tx + r) * xstep, tagb | (unsigned)(PIN * tx + r), ctl);
-      }
-      float m = __uint_as_float((unsigned)xq[j][0]);
-      if constexpr (PIN > 1) {
-        unsigned arg = 0;
-#pragma unroll
-        for (int r = 1; r < PIN; ++r) {
-          const float v = __uint_as_float((unsigned)xq[j][r]);
-          if (v > m) { m = v; arg = r; }
-        }
-        S.pin_out[xoff + (size_t)tx * xstep] = m;
-        S.pin_idx[xoff + (size_t)tx * xstep] = (unsigned char)arg;
-      }
-      xs[buf][gx_seq][gx_k] = (__bf16)m;
-    } else {
-#pragma unroll
-      for (int q = 0; q < GR; ++q) xs[buf][gx_seq][gx_k + q] = (__bf16)xr[j].v[q];
-    }
-  };
-
-  // h storer: granule (tid mod n_gh) of the [16][H] tile; lane group tid / n_gh (0..3)
-  // publishes element `el` of that float4 to the stream (no duplicate granule stores)
-  constexpr int n_gh = 16 * H / 4;
-  const int gh = (tid % n_gh) * 4;
-  const int el = tid / n_gh;
-  float* hbase = S.h + (size_t)row0 * H + gh;
-  const size_t hstep = (size_t)Mp * H;
-  unsigned long long* sbase = S.sout ? S.sout + (size_t)row0 * H + gh + el : nullptr;
+  // this lane's output element (sequence row0 + col, unit) in the [T][Mp][H] streams
+  const size_t hoff = (size_t)(row0 + col) * H + unit;
+  float* hp = S.h + hoff;
+  unsigned long long* sp = S.sout != nullptr ? S.sout + hoff : nullptr;
   const bool publish = S.sout != nullptr;
-  const int To = P > 0 ? T / P : T;      // (P > 0 only without a consumer stage)
-  PoolAcc pool;
+  const bool own_pool = P > 0;
+  const size_t gstride = (size_t)ntiles * NW * 64;
+  __bf16* gp = S.g + (((size_t)tile * NW + wc) * 64 + lane) * 4;
+  float* cp = S.c + ((size_t)tile * NW + wc) * 64 + lane;
 
-  if constexpr (SRC) {
-    // start once the producer is D + LEAD (input) steps ahead: the ring's loads then find
-    // their granules. (Starting at once left every ring slot stale: each of the first D
-    // steps then paid a full re-poll round trip, ~12 us of lag per stage.)
-    constexpr int LEAD = PIN > 1 ? CHAIN_LEAD3 : CHAIN_LEAD1;
-    const int tw = min(D + LEAD, T - 1);
-    (void)chain_wait(S.xin + xoff + (size_t)(PIN * tw + PIN - 1) * xstep, tagb | (unsigned)(PIN * tw + PIN - 1), ctl);
+  // ---- a last stage that pools its own output: the pooling lanes (I/O wave 0, or the first 16 H / 4
+  // threads) own float4 granules of the [16][H] tile
+  constexpr int n_gh = 16 * H / 4;
+  constexpr int NPT = IOW ? 64 : NT;             // pooling threads (the publisher wave, or every thread)
+  constexpr int NPL = (n_gh + NPT - 1) / NPT;
+  PoolAcc pool[NPL];
+  const bool publisher = IOW && w == NW + NIOW;
+  const bool pooler = IOW ? publisher : wave_uniform(tid < n_gh);
+  auto pool_step = [&](int tp) {           // h_tp from hf[tp & 1]
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      const int gh = (((IOW ? lane : tid) + NPT * q) % n_gh) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(&hf[tp & 1][gh / H][gh % H]);
+      pool[q].step(v, tp, P, To, S.pout, S.iout, (size_t)row0 * H + gh, hstep);
+    }
+  };
+
+  // ---- prologue: x_0 in LDS buffer 0, the first D steps' loads in flight
+  const bool streamer = IOW ? (!compute && !publisher) : true;
+  if (streamer) {
+    if constexpr (SRC) {
+      // start once the producer is D + LEAD (input) steps ahead: the loads then find their
+      // granules. (Starting at once left every load stale: each of the first D steps then paid a
+      // full re-poll round trip, ~12 us of lag per stage.)
+      constexpr int LEAD = PIN > 1 ? CHAIN_LEAD3 : CHAIN_LEAD1;
+      const int tw = min(D + LEAD, T - 1);
+      (void)chain_wait(S.xin + xbase + goff[0] + 1 + (size_t)(PIN * tw + PIN - 1) * xstep,
+                       tagb | (unsigned)(PIN * tw + PIN - 1), ctl);
+    }
+    if constexpr (IOW) {
+      load_x(0, min(iow, T - 1));            // I/O wave k: x_k
+    } else {
+#pragma unroll
+      for (int r = 0; r < D; ++r) load_x(r, min(r, T - 1));
+    }
   }
-#pragma unroll
-  for (int j = 0; j < D; ++j) load_x(j, min(j, T - 1));
   __syncthreads();
-  stage_x(0, 0, 0);
-  load_x(0, min(D, T - 1));
-  float c[CPL];
-#pragma unroll
-  for (int cc = 0; cc < CPL; ++cc) c[cc] = 0.f;
+  if (IOW ? (streamer && iow == 0) : streamer) {
+    stage_x(0, 0, 0);
+    load_x(0, min(D, T - 1));
+  }
+  float c = 0.f;
   __syncthreads();
 
   long long* pr = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
-  for (int t0 = 0; t0 <= T; t0 += D) {
+  // the compute step of time t (reads xs[p], hs[p]; writes hs[p ^ 1], the outputs)
+  auto compute_step = [&](int t, auto IO, int rn) {
+    constexpr bool DOI = decltype(IO)::value;
+    const int p = t & 1;
+    chain_mark(pr, t, 0);
+    f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-      const int t = t0 + j;
-      const int p = t & 1;
-      const int jn = (j + 1 == D) ? 0 : j + 1;
-      chain_mark(pr, t, 0);
-      {
-        const int ts = (t >= 1 && t <= T) ? t - 1 : T;
-        const float4 v = *reinterpret_cast<const float4*>(&hf[p ^ 1][gh / H][gh % H]);
-        *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
-        if (t >= 1 && t <= T) {
-          if (P > 0) {              // last stage: pools its own output (the consumer pools otherwise)
-            pool.step(v, t - 1, P, To, S.pout, S.iout, (size_t)row0 * H + gh, hstep);
-          } else if (publish) {
-            const float m = el == 0 ? v.x : el == 1 ? v.y : el == 2 ? v.z : v.w;
-            st_granule(sbase + (size_t)(t - 1) * hstep, m, tagb | (unsigned)(t - 1));
-          }
-        }
-      }
-      f32x4_t acc[CPL];
-#pragma unroll
-      for (int cc = 0; cc < CPL; ++cc) {
-        f32x4_t accx = bias4[cc], acch = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KX; ++s) {
-          const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
-          accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, accx, 0, 0, 0);
-        }
-#pragma unroll
-        for (int s = 0; s < C::KSH; ++s) {
-          const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
-          acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acch, 0, 0, 0);
-        }
-        acc[cc] = accx + acch;
-      }
-      chain_mark(pr, t, 1);
-      stage_x(p ^ 1, jn, min(t + 1, T - 1));
-      load_x(jn, min(t + 1 + D, T - 1));
-      chain_mark(pr, t, 2);
-#pragma unroll
-      for (int cc = 0; cc < CPL; ++cc) {
-        const float iv = sigmoidf_fast(acc[cc][0]);
-        const float fv = sigmoidf_fast(acc[cc][1]);
-        const float gv = tanhf_fast(acc[cc][2]);
-        const float ov = sigmoidf_fast(acc[cc][3]);
-        c[cc] = fv * c[cc] + iv * gv;
-        const float hv = ov * tanhf_fast(c[cc]);
-        const int u = unit[cc];
-        hs[p ^ 1][col][u] = (__bf16)hv;
-        hf[p][col][u] = hv;
-        if constexpr (TRAIN) {
-          const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
-          *reinterpret_cast<uint2*>(S.g + o * 4) = gates_pack(iv, fv, gv, ov);
-          S.c[o] = c[cc];
-        }
-      }
-      chain_mark(pr, t, 3);
-      lds_barrier();
-      chain_mark(pr, t, 4);
+    for (int s = 0; s < KX; ++s) {
+      const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
+      accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[s], bx, accx, 0, 0, 0);
     }
+#pragma unroll
+    for (int s = 0; s < C::KSH; ++s) {
+      const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
+      acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[s], bh, acch, 0, 0, 0);
+    }
+    const f32x4_t a = accx + acch;
+    chain_mark(pr, t, 1);
+    if constexpr (DOI) {                 // (H = 64: every thread also streams x through its ring)
+      stage_x(p ^ 1, rn, min(t + 1, T - 1));
+      load_x(rn, min(t + 1 + D, T - 1));
+    }
+    const float iv = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(0) * a[0]));
+    const float fv = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(1) * a[1]));
+    const float gv = 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(2) * a[2])) - 1.0f;
+    const float ov = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(3) * a[3]));
+    c = fv * c + iv * gv;
+    const float rc = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.8853900817779268f * c));
+    const float hv = (2.0f * ov) * rc - ov;            // o tanh(c)
+    hs[p ^ 1][col][unit] = (__bf16)hv;
+    // the granule that publishes h_t goes out at once, from registers (write-through: the consumer
+    // polls it); the bulk outputs (h, packed gates, c) are staged in LDS for the publisher wave, whose
+    // wide contiguous stores keep the CU's vector-memory path free for the consumer-side loads
+    if (publish) st_granule(sp + (size_t)t * hstep, hv, tagb | (unsigned)t);
+    if constexpr (IOW) {
+      hf[p][col][unit] = hv;
+      if constexpr (TRAIN) {
+        gst[p][wc * 64 + lane] = gates_pack(iv, fv, gv, ov);
+        cst[p][wc * 64 + lane] = c;
+      }
+    } else {
+      if (own_pool) hf[p][col][unit] = hv;
+      hp[(size_t)t * hstep] = hv;
+      if constexpr (TRAIN) {
+        *reinterpret_cast<uint2*>(gp + (size_t)t * gstride * 4) = gates_pack(iv, fv, gv, ov);
+        cp[(size_t)t * gstride] = c;
+      }
+    }
+    chain_mark(pr, t, 2);
+  };
+  // publisher wave: step tp's h tile, gates and c from LDS buffer tp & 1 with 16-byte stores; a whole
+  // [16][H] row block of the time-major streams is contiguous. (Publishing the granules from here as
+  // well, a step later with 16-byte write-through buffer stores, timed out: consumers never saw them.)
+  auto publish_step = [&](int tp) {
+    const int pb = tp & 1;
+    const size_t tile_off = ((size_t)tp * Mp + row0) * H;
+#pragma unroll
+    for (int q = lane; q < 16 * H / 4; q += 64) {
+      const int e = 4 * q;
+      *reinterpret_cast<float4*>(S.h + tile_off + e) = *reinterpret_cast<const float4*>(&hf[pb][e / H][e % H]);
+    }
+    if constexpr (TRAIN) {
+      const size_t cell0 = ((size_t)tp * ntiles + tile) * NW * 64;     // this tile's cells of step tp
+#pragma unroll
+      for (int q = lane; q < NT / 2; q += 64)
+        *reinterpret_cast<uint4*>(S.g + (cell0 + 2 * q) * 4) = *reinterpret_cast<const uint4*>(&gst[pb][2 * q]);
+#pragma unroll
+      for (int q = lane; q < NT / 4; q += 64)
+        *reinterpret_cast<float4*>(S.c + cell0 + 4 * q) = *reinterpret_cast<const float4*>(&cst[pb][4 * q]);
+    }
+    if (own_pool) pool_step(tp);
+  };
+  using yes = std::true_type;
+  using no = std::false_type;
+  if constexpr (IOW) {
+    if (compute) {
+      if (CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(CHAIN_PRIO);   // the serial cell math issues first on a shared SIMD
+      for (int t = 0; t < T; ++t) {
+        compute_step(t, no{}, 0);
+        lds_barrier();
+        chain_mark(pr, t, 3);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    } else if (publisher) {
+      for (int t = 0; t < T; ++t) {
+        if (t >= 1) publish_step(t - 1);
+        lds_barrier();
+      }
+      publish_step(T - 1);
+    } else {
+      // I/O wave k stages the steps s = k (mod D): x_{t+1} in step t, then loads x_{t+1+D}
+      int kt = (iow + D - 1) % D;        // steps until this wave's turn: t = kt, kt + D, ...
+      for (int t = 0; t < T; ++t) {
+        if (kt == 0 && t + 1 < T) {
+          if (iot == 0) chain_mark_wave(pr, t, 4);
+          stage_x((t + 1) & 1, 0, t + 1);
+          if (iot == 0) chain_mark_wave(pr, t, 5);
+          load_x(0, min(t + 1 + D, T - 1));
+          if (iot == 0) chain_mark_wave(pr, t, 6);
+        }
+        kt = kt == 0 ? D - 1 : kt - 1;
+        lds_barrier();
+      }
+    }
+  } else {
+    for (int t0 = 0; t0 < T; t0 += D) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) {
+        const int t = t0 + r;
+        if (t >= T) break;               // (uniform: the last round of the ring may be partial)
+        compute_step(t, yes{}, (r + 1 == D) ? 0 : r + 1);
+        if (own_pool && pooler && t >= 1) pool_step(t - 1);
+        lds_barrier();
+        chain_mark(pr, t, 3);
+      }
+    }
+  }
+  if constexpr (!IOW) {
+    if (own_pool && pooler) pool_step(T - 1);
   }
 }
 
@@ -581,14 +822,14 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const bool src = s > 0;
 #define GQ_CHAIN_BODY(HH, KXX, DD, SRCV, PINV)                                          \
   {                                                                                     \
-    if (threadIdx.x >= TMC<HH>::NT) return;                                             \
+    if (threadIdx.x >= chain_live_threads(TMC<HH>::NT, DD, KXX, SRCV, PINV)) return;   \
     chain_stage<HH, TRAIN, KXX, DD, SRCV, PINV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
   }
 #define GQ_CHAIN_SRC(HH, PINV, DD)                                                      \
   if (KX == 1) GQ_CHAIN_BODY(HH, 1, DD, true, PINV) else GQ_CHAIN_BODY(HH, 2, DD, true, PINV)
 #define GQ_CHAIN_KX(HH)                                                                 \
   if (src) { if (S.PIN == 3) { GQ_CHAIN_SRC(HH, 3, CHAIN_D3) } else { GQ_CHAIN_SRC(HH, 1, CHAIN_D) } } \
-  else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, 6, false, 1) else GQ_CHAIN_BODY(HH, 2, 6, false, 1) }
+  else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, CHAIN_D0, false, 1) else GQ_CHAIN_BODY(HH, 2, CHAIN_D0, false, 1) }
   if (H == 16) GQ_CHAIN_KX(16)
   else if (H == 32) GQ_CHAIN_KX(32)
   else GQ_CHAIN_KX(64)
@@ -1448,6 +1689,11 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     S.Dw = Dw;
     S.KX = (Din + 31) / 32;
     S.PIN = s > 0 ? std::max(1, (int)pool[s - 1]) : 1;
+    // a stage without I/O waves (H = 64) streams one granule per thread (chain_stage NGL)
+    TORCH_CHECK(H < 64 || 16 * Din / (s == 0 ? 4 : 2) <= 64 * TMC<64>::NW, "lstm_chain: stage ", s, " input tile");
+    TORCH_CHECK(s == 0 || (long)T * Mp * Din * 8 < (1L << 31), "lstm_chain: stage ", s, " input stream too large");
+    TORCH_CHECK(s == 0 || Din % 2 == 0, "lstm_chain: stage ", s, " input width must be even");
+    TORCH_CHECK(s > 0 || Din % 4 == 0, "lstm_chain: the input width must be a multiple of 4");
     {
       long long* pb = chain_prof_buf(x.get_device());
       S.prof = pb != nullptr ? pb + (size_t)s * CHAIN_PROF_STEPS * 8 : nullptr;
@@ -1683,8 +1929,9 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
 at::Tensor lstm_chain_status(const at::Tensor& like) {
   c10::DeviceGuard guard(like.device());
   int* p = chain_ctl(like.get_device());
-  at::Tensor o = at::empty({4}, like.options().dtype(at::kInt));
-  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int>(), p, 4 * sizeof(int), hipMemcpyDeviceToDevice, stream()) == hipSuccess,
+  // [0] epoch, [1] finished workgroups, [2] spin timeout, [3] rejected steps, .., [9] consumer re-polls
+  at::Tensor o = at::empty({12}, like.options().dtype(at::kInt));
+  TORCH_CHECK(hipMemcpyAsync(o.data_ptr<int>(), p, 12 * sizeof(int), hipMemcpyDeviceToDevice, stream()) == hipSuccess,
               "lstm_chain_status");
   return o;
 }

@@ -168,6 +168,10 @@ class FlatAdam(FlatOptimizer):
         # values (chain control word 7): the update then decides from the flags (adam_flagged, no
         # grid-wide scan of the gradient buffer)
         self.flagged_producers = False
+        # data parallel with the one-shot peer all-reduce (gnnqc.parallel.peer): a flag-driven step
+        # reduces the gradients INSIDE the update launch (peer_allreduce.hip adam_peer); the trainer
+        # then issues no separate collective
+        self.peer = None
 
     @property
     def grad_zeroed_by_step(self) -> bool:
@@ -181,6 +185,14 @@ class FlatAdam(FlatOptimizer):
             # guard + update (+ batch cursor) as ONE launch when the buffer fits a co-resident grid
             from ..utils.native import hip_ops
             from .lstm import chain_ctl
+            if self.flagged_producers and self.peer is not None:
+                pa = self.peer
+                if hip_ops().adam_peer(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
+                                       self.beta2, self.eps, float(grad_scale), self.wd, self.guard_state, self.cursor,
+                                       int(self.cursor_mod), pa.bases, pa.region, pa.rank, pa.cap):
+                    self.iterations += 1
+                    return
+                raise RuntimeError("adam_peer: gradient buffer too large for the fused peer update")
             if self.flagged_producers:
                 hip_ops().adam_flagged(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
                                        self.beta2, self.eps, float(grad_scale), self.wd, self.guard_state,

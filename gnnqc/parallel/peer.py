@@ -7,8 +7,9 @@ directly over the point-to-point xGMI links - one step instead of RCCL's 2 (N-1)
 753 KB buffer. The kernel is a plain launch (no host synchronisation), so it is captured in the
 multi-step training graph like the RCCL collective it replaces.
 
-Opt-in (``GNNQC_PEER_ALLREDUCE=1``) and validated against RCCL / gloo when it is set up
-(:meth:`PeerAllReduce.verify`); one process per GPU of one node, at most 8 ranks. The handles
+Selected by :func:`peer_mode` (default ``auto``: with two or more ranks it is set up, validated
+against RCCL / gloo (:meth:`PeerAllReduce.verify`) and timed against the process group's all-reduce,
+and used only if it verified and was faster); one process per GPU of one node, at most 8 ranks. The handles
 are exchanged with the default process group, so it works over gloo as well (tests: two ranks
 sharing one GPU). Between different GPUs over xGMI it has NOT been run (no multi-GPU box was
 available): treat it as unverified there until a multi-GPU run checks it against RCCL.
@@ -23,8 +24,20 @@ import torch
 from . import dist as D
 
 
+def peer_mode() -> str:
+    """``GNNQC_PEER_ALLREDUCE``: ``0`` off, ``1`` on whenever it verifies, ``auto`` (default) on when
+    it verifies AND beats the process group's all-reduce of the same buffer in a timing at setup
+    (more than one rank only: a one-rank group needs no collective)."""
+    v = os.environ.get("GNNQC_PEER_ALLREDUCE", "auto").strip().lower()
+    return {"1": "on", "on": "on", "0": "off", "off": "off"}.get(v, "auto")
+
+
 def peer_enabled() -> bool:
-    return os.environ.get("GNNQC_PEER_ALLREDUCE", "0") == "1"
+    return peer_mode() != "off"
+
+
+# the last setup's decision: {"mode", "verified", "rccl_us", "peer_us", "selected"} (bench.py reports it)
+LAST_SELECTION: dict = {}
 
 
 class PeerAllReduce:
@@ -88,25 +101,62 @@ _CACHE = {}
 
 
 def make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
-    """A verified peer all-reduce when ``GNNQC_PEER_ALLREDUCE=1`` (None otherwise or if it fails
-    verification, which falls back to the process group's collective). One registered region per
+    """A verified peer all-reduce (see :func:`peer_mode`; None when off, when it fails verification
+    or, in ``auto`` mode, when the process group's collective was faster - the caller then uses that). One registered region per
     (device, size, group size) for the whole process: every Trainer (one per CV fold) reuses it
     instead of exporting and opening a new set of IPC regions."""
-    if not peer_enabled() or torch.device(device).type != "cuda" or not D.is_initialized():
+    mode = peer_mode()
+    if mode == "off" or torch.device(device).type != "cuda" or not D.is_initialized():
         return None
-    key = (str(torch.device(device)), (int(numel) + 3) // 4 * 4, D.world_size(), D.rank())
+    if mode == "auto" and D.world_size() < 2:
+        return None
+    key = (str(torch.device(device)), (int(numel) + 3) // 4 * 4, D.world_size(), D.rank(), mode)
     if key in _CACHE:
         return _CACHE[key]
     pa = _make_peer_allreduce(numel, device)
-    if pa is not None:
-        _CACHE[key] = pa
+    LAST_SELECTION.clear()
+    LAST_SELECTION.update(mode=mode, verified=pa is not None, rccl_us=None, peer_us=None,
+                          selected="peer" if pa is not None else "process group")
+    if pa is not None and mode == "auto":
+        rccl_us, peer_us = _time_both(pa, numel, device)
+        LAST_SELECTION.update(rccl_us=rccl_us, peer_us=peer_us)
+        if not peer_us < rccl_us:
+            LAST_SELECTION["selected"] = "process group"
+            pa.close()
+            pa = None
+    _CACHE[key] = pa
     return pa
+
+
+@torch.no_grad()
+def _time_both(pa: "PeerAllReduce", numel: int, device, n: int = 30):
+    """Mean us of the process group's all-reduce and of the peer kernel on a scratch buffer of the
+    gradient's size (HIP events, max over ranks so every rank takes the same decision)."""
+    buf = torch.zeros(int(numel), device=device)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize(device)
+        return 1e3 * sum(a.elapsed_time(b) for a, b in ev) / n
+
+    r = timed(lambda: D.all_reduce_(buf, force=True))
+    q = timed(lambda: pa(buf))
+    t = torch.tensor([r, q], device=device if D.backend() == "nccl" else "cpu", dtype=torch.float64)
+    D.all_reduce_(t, op=torch.distributed.ReduceOp.MAX, force=True)
+    return float(t[0].item()), float(t[1].item())
 
 
 def close_all():
     """Close every cached peer region's peer mappings (process teardown)."""
     for pa in _CACHE.values():
-        pa.close()
+        if pa is not None:
+            pa.close()
     _CACHE.clear()
 
 
@@ -133,4 +183,4 @@ def _make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
     return pa
 
 
-__all__ = ["PeerAllReduce", "make_peer_allreduce", "peer_enabled", "close_all"]
+__all__ = ["PeerAllReduce", "make_peer_allreduce", "peer_enabled", "peer_mode", "close_all", "LAST_SELECTION"]

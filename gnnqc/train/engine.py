@@ -107,6 +107,10 @@ class Trainer:
             self.peer = make_peer_allreduce(self.opt.flat_g.numel(), self.device)
         self.dp_graph = (self.collective and self.use_graph and (D.backend() == "nccl" or self.peer is not None)
                          and os.environ.get("GNNQC_DP_GRAPH", "1") == "1")
+        # flag-driven steps reduce over the peers inside the Adam launch (one launch, one pass over the
+        # gradients; GNNQC_PEER_FUSED_ADAM=0 keeps the separate all-reduce kernel)
+        if self.peer is not None and hasattr(self.opt, "peer") and os.environ.get("GNNQC_PEER_FUSED_ADAM", "1") == "1":
+            self.opt.peer = self.peer
         self.opt_graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
         self.last_loss = torch.zeros((), device=self.device)
@@ -245,11 +249,17 @@ class Trainer:
         flat 753 KB buffer. Not bucketed and not overlapped with the backward on purpose: the
         cross-CU chain kernels assume no other kernel shares the device while they run, and a
         single small collective is latency-bound on xGMI, so splitting it only adds latency."""
+        if self.peer_fused():
+            return                # the update launch reduces (and carries the reject bits) itself
         if self.device.type == "cuda":
             from ..ops.lstm import chain_ctl
             from ..utils.native import hip_ops
             hip_ops().chain_poison(self.opt.flat_g, chain_ctl(self.device))
         self._all_reduce_flat()
+
+    def peer_fused(self) -> bool:
+        """Whether this step's gradient reduction runs inside the Adam launch (adam_peer)."""
+        return getattr(self.opt, "peer", None) is not None and bool(getattr(self.opt, "flagged_producers", False))
 
     def _all_reduce_flat(self):
         if self.peer is not None:

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-step phase clocks of the chain kernels' stages (GNNQC_CHAIN_PROF=1; tile 0, wave 0,
 s_memtime ticks): median over the first 64 steps of every phase of the step loop, per stage.
-Forward marks: 0 loop top, 1 MFMAs issued, 2 next input staged + ring reload issued, 3 gates /
-stores done, 4 after the step barrier. Backward: 0 top, 1 cell phase done, 2 next dh staged,
+Forward marks (compute wave 0): 0 loop top, 1 pre-activations out of the MFMAs, 2 gates / cell /
+outputs stored, 3 after the step barrier. Backward: 0 top, 1 cell phase done, 2 next dh staged,
 3 after the barrier, 4 dh_rec (U dz) ready, 5 dx MFMAs done. One JSON line per launch kind."""
 import json
 import os
@@ -27,6 +27,23 @@ def phases(pr, nmarks):
         d = (t[:, 1:nmarks] - t[:, :nmarks - 1]).median(0).values.tolist()
         per = (t[1:, 0] - t[:-1, 0]).median().item()
         out.append({"stage": s, "steps": len(steps), "step_ticks": round(per, 1), "phase_ticks": [round(x, 1) for x in d]})
+    return out
+
+
+def marks_rel(pr, nmarks):
+    """Median of (mark k - mark 0) per stage for k < nmarks (marks written by other waves included)."""
+    out = []
+    for s in range(pr.shape[0]):
+        v = pr[s].to(torch.float64)
+        ok = (v[:, 0] > 0)
+        if int(ok.sum()) < 4:
+            continue
+        row = {"stage": s}
+        for k in range(1, nmarks):
+            m = ok & (v[:, k] > 0)
+            if int(m.sum()) >= 4:
+                row[f"m{k}"] = round(float((v[m, k] - v[m, 0]).median()), 1)
+        out.append(row)
     return out
 
 
@@ -57,7 +74,10 @@ def main():
                                        *hc, e.double(), e)
     torch.cuda.synchronize()
     pf = ops.lstm_chain_prof(x).cpu()
-    print(json.dumps({"launch": "fwd (chain6 + time4 stage)", "stages": phases(pf, 5)}), flush=True)
+    print(json.dumps({"launch": "fwd (chain6 + time4 stage)", "stages": phases(pf, 4)}), flush=True)
+    # I/O waves (marks 4..6 of the step whose x they stage: start, tile staged, next load issued),
+    # relative to compute wave 0's step start
+    print(json.dumps({"launch": "fwd marks vs compute start", "stages": marks_rel(pf, 7)}), flush=True)
     h4, g4, c4, logits, loss = outs[-5:]
     pk = outs[-6]
     outs = outs[:-6]

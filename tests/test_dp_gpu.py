@@ -50,7 +50,7 @@ bufs = torch.cat([b.reshape(-1).double() for b in m.buffers() if b.is_floating_p
 out = {"sum": float(x[0]), "p": opt.flat_p.double().sum().item(), "p2": (opt.flat_p.double() ** 2).sum().item(),
        "b": bufs.sum().item(), "steps": t.global_step, "loss": logs["loss"], "skipped": logs["skipped_steps"],
        "dp_graph": bool(t.dp_graph), "multi": bool(t.multi_graph is not None), "ar_us": t.measure_allreduce(),
-       "peer": t.peer is not None}
+       "peer": t.peer is not None, "fused": bool(t.peer_fused())}
 with open(os.path.join(os.environ["OUT"], f"r{rank}.json"), "w") as f:
     json.dump(out, f)
 torch.distributed.destroy_process_group()
@@ -121,11 +121,33 @@ def test_peer_allreduce_two_ranks_one_gpu(tmp_path):
     assert a["ar_us"] is not None and a["ar_us"] > 0
 
 
+def test_peer_fused_adam_matches_separate_kernels_two_ranks(tmp_path):
+    """The peer reduction fused into the flag-driven Adam launch (adam_peer) trains like the peer
+    all-reduce kernel followed by adam_flagged, two ranks sharing the GPU."""
+    a, b = _run(tmp_path / "fused", 2, "gloo", NB="16", GNNQC_PEER_ALLREDUCE="1")
+    c, d = _run(tmp_path / "sep", 2, "gloo", NB="16", GNNQC_PEER_ALLREDUCE="1", GNNQC_PEER_FUSED_ADAM="0")
+    assert a["fused"] and b["fused"] and not c["fused"] and a["peer"] and c["peer"]
+    assert a["steps"] == c["steps"] == 16 and a["skipped"] == c["skipped"] == 0
+    for k in ("p", "p2", "loss"):
+        # ranks of one run agree bitwise; the two runs differ only by the float-atomic order of the
+        # GCN backward (a separate process each)
+        assert a[k] == b[k] and c[k] == d[k], (k, a[k], b[k], c[k], d[k])
+        assert abs(a[k] - c[k]) <= 1e-6 * abs(c[k]) + 1e-9, (k, a[k], c[k])
+
+
+def test_peer_auto_mode_selects_and_trains(tmp_path):
+    """Default (auto) peer mode with two ranks: set up, verified, timed against gloo, selected only
+    if faster; either way both ranks end identical."""
+    a, b = _run(tmp_path, 2, "gloo", NB="8")
+    assert a["peer"] == b["peer"]
+    assert a["p"] == b["p"] and a["p2"] == b["p2"] and a["skipped"] == 0
+
+
 def test_peer_allreduce_matches_rccl_single_rank(tmp_path):
     """The peer path on a one-rank nccl group with the chain kernels on trains like RCCL."""
     (a,) = _run(tmp_path / "peer", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="1",
                 GNNQC_PEER_ALLREDUCE="1")
     (b,) = _run(tmp_path / "rccl", 1, "nccl", chain=True, NB="16", GNNQC_DP_FORCE_COLLECTIVE="1")
-    assert a["peer"] and not b["peer"] and a["dp_graph"] and a["multi"]
+    assert a["peer"] and not b["peer"] and a["dp_graph"] and a["multi"] and a["fused"]
     for k in ("p", "p2", "loss"):
         assert abs(a[k] - b[k]) <= 1e-4 * abs(b[k]) + 1e-6, (k, a[k], b[k])
