@@ -68,6 +68,9 @@ static constexpr int CHAIN_SPIN = 1 << 20;
 #ifndef CHAIN_LD16
 #define CHAIN_LD16 0         // 1: one 16-byte buffer load per granule pair (measured: stale reads, ~4.5k re-polls per launch)
 #endif
+#ifndef CHAIN_DEFER_LD
+#define CHAIN_DEFER_LD 1     // I/O waves issue their next loads a step after staging (see the I/O loops)
+#endif
 #ifndef CHAIN_PRIO
 #define CHAIN_PRIO 2         // s_setprio of the compute waves of a stage with I/O waves
 #endif
@@ -482,7 +485,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   __syncthreads();
   if (IOW ? (streamer && iow == 0) : streamer) {
     stage_x(0, 0, 0);
-    load_x(0, min(D, T - 1));
+    if (!IOW || !CHAIN_DEFER_LD) load_x(0, min(D, T - 1));
   }
   float c = 0.f;
   __syncthreads();
@@ -579,13 +582,22 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
       publish_step(T - 1);
     } else {
       // I/O wave k stages the steps s = k (mod D): x_{t+1} in step t, then loads x_{t+1+D}
+      // the group's next loads are issued at the top of the step AFTER its staging step (right after
+      // that barrier, beside the compute waves' cell math) instead of before the barrier they would
+      // hold up; they still land D - 1 steps ahead of their use
       int kt = (iow + D - 1) % D;        // steps until this wave's turn: t = kt, kt + D, ...
+      int next_ld = iow == 0 ? D : -1;   // (group 0 staged x_0 in the prologue)
       for (int t = 0; t < T; ++t) {
+        if (CHAIN_DEFER_LD && next_ld >= 0) {
+          load_x(0, min(next_ld, T - 1));
+          next_ld = -1;
+        }
         if (kt == 0 && t + 1 < T) {
           if (iot == 0) chain_mark_wave(pr, t, 4);
           stage_x((t + 1) & 1, 0, t + 1);
           if (iot == 0) chain_mark_wave(pr, t, 5);
-          load_x(0, min(t + 1 + D, T - 1));
+          if (CHAIN_DEFER_LD) next_ld = t + 1 + D;
+          else load_x(0, min(t + 1 + D, T - 1));
           if (iot == 0) chain_mark_wave(pr, t, 6);
         }
         kt = kt == 0 ? D - 1 : kt - 1;
@@ -928,6 +940,14 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 
 #ifndef CHAINB_LEAD
 #define CHAINB_LEAD 1
+#endif
+#ifndef CHAINB_IO
+#define CHAINB_IO 0          // 1: H = 16 stages as compute / rotating I/O / publisher waves (chain_bwd_stage_io);
+                             // measured slower (bottom stages end 123 / 140 vs 113 / 117 us, bench 0.307 vs
+                             // 0.286 ms/step): the I/O waves' staging and load issue hold up the step barrier
+#endif
+#ifndef CHAINB_G
+#define CHAINB_G 2           // waves per backward I/O group: 2 = one for the cell records, one for dh
 #endif
 // ring depths (reverse steps of prefetch) per hidden size
 #ifndef CHAINB_D16
@@ -1290,6 +1310,322 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   if constexpr (!PUBW) store_dx((T - 1) & 1, 0, tagb);     // dx tile of t = 0
 }
 
+// The H = 16 reverse recurrence (the bottom layers' 181 steps: the backward's critical path) with the
+// forward's role split. Compute waves: per step, the cell's gate gradients from LDS inputs only (the
+// packed gates, c_t and c_{t-1} as one 16-byte record, dh from the stage above), dz to LDS, one
+// barrier, dh_rec = U dz and dx = W dz by MFMA from LDS; no global memory access at all. D rotating
+// I/O waves: wave k stages the records and the (tag-checked, un-pooled) dh tile of every step
+// s = k (mod D), loaded D steps ahead, with 16-byte loads of the tile's contiguous cell block. A
+// publisher wave stores each step's dz tile (16-byte stores) and publishes its dx, one step later.
+template <int H>
+struct ChainBIoLds {
+  static constexpr int ZS = 2 * 16 * (4 * H + 8) * 2;
+  static constexpr int DH = 2 * 16 * TMC<H>::HP * 4;
+  static constexpr int DX = 2 * 16 * 32 * 2 * 4;          // dx tiles (KX <= 2)
+  static constexpr int RC = 2 * TMC<H>::NT * 16;          // {gates, c_t, c_{t-1}} records
+  static constexpr int BYTES = ZS + DH + DX + RC;
+};
+__host__ __device__ constexpr int chainb_io_threads(int nt, int d) { return nt + 64 * d * CHAINB_G + 64; }
+template <int V>
+struct ChIc { static constexpr int value = V; };
+
+template <int H, int KX, int D, bool SRC, bool UP, bool XO>
+__device__ __forceinline__ void chain_bwd_stage_io(const ChainBStage S, int tile, int ntiles, int Mp, unsigned tagb,
+                                                   int* ctl, char* smem) {
+  using C = TMC<H>;
+  constexpr int NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
+  constexpr int NXB = KX * 2;
+  constexpr int TX = (NXB + NW - 1) / NW;
+  static_assert(C::CPL == 1 && 16 * H == NT && NT % 256 == 0, "one dh element per compute lane");
+  constexpr int CPLN = NT / 64;                     // cells per I/O lane (whole tile per I/O wave)
+  static_assert(CPLN % 4 == 0 || CPLN == 4, "I/O lanes move cells four at a time");
+  using L = ChainBIoLds<H>;
+  static_assert(L::BYTES <= CHAINB_LDS_STAGE, "chain bwd I/O LDS layout");
+  auto zs = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem);
+  auto dhs = reinterpret_cast<float (*)[16][C::HP]>(smem + L::ZS);
+  auto dxs = reinterpret_cast<float (*)[16][32 * KX]>(smem + L::ZS + L::DH);
+  auto rec = reinterpret_cast<uint4 (*)[NT]>(smem + L::ZS + L::DH + L::DX);
+
+  const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P, Ts = S.Ts;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, quad = lane >> 4;
+  const int row0 = tile * 16;
+  constexpr int G = CHAINB_G;
+  static_assert(G == 1 || G == 2, "backward I/O group: one wave, or a record wave and a dh wave");
+  const bool compute = w < NW;
+  const bool publisher = w == NW + D * G;
+  const int iow = (w - NW) / G;                     // I/O group: steps s = iow (mod D)
+  const int sub = (w - NW) % G;                     // (G = 2: 0 loads the cell records, 1 the dh tile)
+  constexpr int NTL = chainb_io_threads(NT, D);
+  for (int i = tid; i < 2 * 16 * C::HP; i += NTL) (&dhs[0][0][0])[i] = 0.f;
+  const size_t hstep = (size_t)Mp * H;
+  const size_t zstep = (size_t)Mp * G4;
+  const size_t xstep = (size_t)Mp * Din;
+  // source time of the dh of time tt (-1: past the last pooling window -> zero gradient)
+  auto src_t = [&](int tt) {
+    if constexpr (UP) return tt < Ts * P ? tt / P : -1;
+    else return tt;
+  };
+  long long* pr = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
+
+  // ---------------------------------------------------------------- I/O waves
+  // one slot: this tile's 4 cells x {gates (2 x 16 B), c_t, c_{t-1}} and 2 dh pairs (+ argmax bytes)
+  constexpr int NDP = NT / 2 / 64;                  // dh pairs per lane
+  uint4 sg[CPLN / 2];
+  float4 sc[CPLN / 4], scp[CPLN / 4];
+  u64x2_t sq[NDP];
+  unsigned short si[NDP];
+  // (SB: 0 = records only, 1 = dh only, 2 = both; a compile-time choice so no branch sits between a
+  // wave's loads and their use)
+  auto io_load = [&](auto sbc, int ss) {            // the inputs of reverse step ss
+    constexpr int SB = decltype(sbc)::value;
+    const int tt = max(T - 1 - ss, 0);
+    const size_t cell0 = ((size_t)tt * ntiles + tile) * NT;
+    const size_t cellp = ((size_t)max(tt - 1, 0) * ntiles + tile) * NT;
+    // (lane's cells: groups of four, 4 (lane + 64 q) + i; gates of a group = two 16-byte halves)
+    if constexpr (SB != 1) {
+#pragma unroll
+      for (int q = 0; q < CPLN / 2; ++q)
+        sg[q] = *reinterpret_cast<const uint4*>(S.g + (cell0 + 4 * (lane + 64 * (q / 2)) + 2 * (q % 2)) * 4);
+#pragma unroll
+      for (int q = 0; q < CPLN / 4; ++q) {
+        sc[q] = *reinterpret_cast<const float4*>(S.c + cell0 + 4 * (lane + 64 * q));
+        scp[q] = *reinterpret_cast<const float4*>(S.c + cellp + 4 * (lane + 64 * q));
+      }
+    }
+    const int st = max(src_t(tt), 0);
+#pragma unroll
+    for (int q = 0; q < (SB != 0 ? NDP : 0); ++q) {
+      const size_t e = (size_t)row0 * H + 2 * (lane + 64 * q) + (size_t)st * hstep;
+      if constexpr (SRC) sq[q] = u64x2_t{ld_granule(S.din + e), ld_granule(S.din + e + 1)};
+      else {
+        const float2 v = *reinterpret_cast<const float2*>(S.dh + e);
+        sq[q] = u64x2_t{(unsigned long long)__float_as_uint(v.x), (unsigned long long)__float_as_uint(v.y)};
+      }
+      if constexpr (UP) si[q] = *reinterpret_cast<const unsigned short*>(S.pidx + e);
+      else si[q] = 0;
+    }
+  };
+  auto io_stage = [&](auto sbc, int buf, int ss) {  // step ss's records and dh tile -> LDS buffer buf
+    constexpr int SB = decltype(sbc)::value;
+    const int tt = T - 1 - ss;
+    const int st = src_t(tt);
+    if constexpr (SRC && SB != 0) {
+      bool bad = false;
+#pragma unroll
+      for (int q = 0; q < NDP; ++q)
+        bad |= st >= 0 && ((unsigned)(sq[q].x >> 32) != (tagb | (unsigned)st) || (unsigned)(sq[q].y >> 32) != (tagb | (unsigned)st));
+      if (__builtin_amdgcn_ballot_w64(bad) != 0) {   // re-poll the whole tile at once (bounded)
+        const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int lim = lim0 > 0 ? lim0 : CHAIN_SPIN;
+        int nap = 1;
+        for (int it = 0;; ++it) {
+#pragma unroll
+          for (int q = 0; q < NDP; ++q) {
+            const size_t e = (size_t)row0 * H + 2 * (lane + 64 * q) + (size_t)max(st, 0) * hstep;
+            sq[q] = u64x2_t{ld_granule(S.din + e), ld_granule(S.din + e + 1)};
+          }
+          bad = false;
+#pragma unroll
+          for (int q = 0; q < NDP; ++q)
+            bad |= (unsigned)(sq[q].x >> 32) != (tagb | (unsigned)st) || (unsigned)(sq[q].y >> 32) != (tagb | (unsigned)st);
+          if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
+          if (it >= lim) {
+            __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(2);
+          nap = min(nap * 2, 16);
+        }
+      }
+    }
+    const unsigned ph = UP ? (unsigned)(tt % P) : 0u;
+#pragma unroll
+    for (int q = 0; q < (SB != 0 ? NDP : 0); ++q) {
+      const int e = 2 * (lane + 64 * q);
+      const float v0 = __uint_as_float((unsigned)sq[q].x), v1 = __uint_as_float((unsigned)sq[q].y);
+      const bool k0 = st >= 0 && (!UP || (si[q] & 0xffu) == ph), k1 = st >= 0 && (!UP || (si[q] >> 8) == ph);
+      *reinterpret_cast<float2*>(&dhs[buf][e / H][e % H]) = make_float2(k0 ? v0 : 0.f, k1 ? v1 : 0.f);
+    }
+    const float cm = tt > 0 ? 1.f : 0.f;
+#pragma unroll
+    for (int q = 0; q < (SB != 1 ? CPLN / 4 : 0); ++q) {
+      const int c0 = 4 * (lane + 64 * q);
+      const uint4 ga = sg[2 * q], gb = sg[2 * q + 1];
+      rec[buf][c0 + 0] = make_uint4(ga.x, ga.y, __float_as_uint(sc[q].x), __float_as_uint(scp[q].x * cm));
+      rec[buf][c0 + 1] = make_uint4(ga.z, ga.w, __float_as_uint(sc[q].y), __float_as_uint(scp[q].y * cm));
+      rec[buf][c0 + 2] = make_uint4(gb.x, gb.y, __float_as_uint(sc[q].z), __float_as_uint(scp[q].z * cm));
+      rec[buf][c0 + 3] = make_uint4(gb.z, gb.w, __float_as_uint(sc[q].w), __float_as_uint(scp[q].w * cm));
+    }
+  };
+
+  // ---------------------------------------------------------------- compute state
+  const int unit = 4 * w + quad;
+  const int au = 4 * w + (col >> 2);
+  bf16x8_t ufr[KB];
+  bf16x8_t wfr[TX][KB];
+  if (compute) {
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float val = S.U[(size_t)au * G4 + 32 * k + 8 * quad + j];
+        v[j] = (__bf16)(val * ((col & 3) == 0 ? 1.f : 0.f));
+      }
+      ufr[k] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < TX; ++q) {
+      const int xb = w + NW * q;
+      const int din = 16 * xb + col;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        bf16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = (__bf16)(S.W[(size_t)min(din, Dw - 1) * G4 + 32 * k + 8 * quad + j] *
+                          ((xb < NXB && din < Dw) ? 1.f : 0.f));
+        wfr[q][k] = v;
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- prologue
+  // run f with this I/O wave's share as a compile-time constant
+  auto io_dispatch = [&](auto f) {
+    if constexpr (G == 1) f(ChIc<2>{});
+    else if (sub == 0) f(ChIc<0>{});
+    else f(ChIc<1>{});
+  };
+  if (!compute && !publisher) {
+    if constexpr (SRC) {    // start once the stage above is D + LEAD steps ahead (see the forward)
+      const int tw = max(T - 1 - (D + CHAINB_LEAD), 0);
+      const int st = src_t(tw);
+      if (st >= 0) (void)chain_wait(S.din + (size_t)row0 * H + (size_t)st * hstep, tagb | (unsigned)st, ctl);
+    }
+    io_dispatch([&](auto sbc) { io_load(sbc, min(iow, T - 1)); });
+  }
+  __syncthreads();
+  if (!compute && !publisher && iow == 0) {
+    io_dispatch([&](auto sbc) {
+      io_stage(sbc, 0, 0);
+      if (!CHAIN_DEFER_LD) io_load(sbc, min(D, T - 1));
+    });
+  }
+  __syncthreads();
+  if (tid == 0 && S.trace_mid) S.trace_mid[blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
+
+  if (compute) {
+    if (CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(CHAIN_PRIO);
+    float dc = 0.f, dhr = 0.f;
+    for (int s = 0; s < T; ++s) {
+      const int t = T - 1 - s;
+      const int p = s & 1;
+      chain_mark(pr, s, 0);
+      {   // cell: gate gradients of (unit, sequence col) at time t
+        const uint4 r4 = rec[p][w * 64 + lane];
+        const float dh = dhs[p][col][unit] + dhr;
+        const float4 g4 = gates_unpack(make_uint2(r4.x, r4.y));
+        const float ct = __uint_as_float(r4.z), cp = __uint_as_float(r4.w);
+        const float tc = tanhf_fast(ct);
+        const float dct = dc + dh * g4.w * (1.f - tc * tc);
+        dc = dct * g4.y;
+        zs[p][col][0 * H + unit] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
+        zs[p][col][1 * H + unit] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
+        zs[p][col][2 * H + unit] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
+        zs[p][col][3 * H + unit] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
+      }
+      chain_mark(pr, s, 1);
+      lds_barrier();
+      chain_mark(pr, s, 2);
+      {   // dh_{t-1} = U dz_t (the serial chain), then dx^T = W dz^T
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+          if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a1, 0, 0, 0);
+          else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a0, 0, 0, 0);
+        }
+        dhr = a0[0] + a1[0];     // (U^T rows with (col & 3) == 0: element 0 is this lane's unit)
+      }
+      chain_mark(pr, s, 3);
+#pragma unroll
+      for (int q = 0; q < TX; ++q) {
+        const int xb = w + NW * q;
+        if (xb < NXB) {
+          f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < KB; ++k) {
+            const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q][k], bz, a, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dxs[p][col][16 * xb + 4 * quad + r] = a[r];
+        }
+      }
+      chain_mark(pr, s, 4);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  } else if (publisher) {
+    // after barrier s: step s's dz tile is complete (compute only reads it until barrier s + 1) and
+    // step s - 1's dx tile too (written after barrier s - 1)
+    auto store_dz = [&](int ss) {
+      const int tz = T - 1 - ss;
+      const int pb = ss & 1;
+      __bf16* zt = S.dz + ((size_t)tz * Mp + row0) * G4;
+#pragma unroll
+      for (int q = lane; q < 16 * G4 / 8; q += 64) {
+        const int e = 8 * q;
+        *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][e % G4]);
+      }
+    };
+    auto publish = [&](int ss) {            // step ss's dx tile
+      const int tz = T - 1 - ss;
+      const int pb = ss & 1;
+      const unsigned tag = tagb | (unsigned)tz;
+      const size_t xo = ((size_t)tz * Mp + row0) * Din;
+      for (int e = lane; e < 16 * Din; e += 64) {
+        const float v = dxs[pb][e / Din][e % Din];
+        if constexpr (XO) st_granule(S.sout + xo + e, v, tag);
+        else S.dx[xo + e] = v;
+      }
+    };
+    for (int s = 0; s < T; ++s) {
+      lds_barrier();
+      store_dz(s);
+      if (s >= 1) publish(s - 1);
+    }
+    __syncthreads();
+    publish(T - 1);
+    return;
+  } else {
+    io_dispatch([&](auto sbc) {
+      const bool mk = lane == 0 && sub == G - 1;      // (phase marks: the dh wave, which tag-checks)
+      int kt = (iow + D - 1) % D;           // steps until this group's turn
+      int next_ld = iow == 0 ? D : -1;      // (deferred loads: see the forward's I/O loop)
+      for (int s = 0; s < T; ++s) {
+        if (CHAIN_DEFER_LD && next_ld >= 0) {
+          io_load(sbc, min(next_ld, T - 1));
+          next_ld = -1;
+        }
+        if (kt == 0 && s + 1 < T) {
+          if (mk) chain_mark_wave(pr, s, 5);
+          io_stage(sbc, (s + 1) & 1, s + 1);
+          if (mk) chain_mark_wave(pr, s, 6);
+          if (CHAIN_DEFER_LD) next_ld = s + 1 + D;
+          else io_load(sbc, min(s + 1 + D, T - 1));
+          if (mk) chain_mark_wave(pr, s, 7);
+        }
+        kt = kt == 0 ? D - 1 : kt - 1;
+        lds_barrier();
+      }
+    });
+  }
+  __syncthreads();
+}
+
 // time4's backward on one 16-sequence tile with 1024 threads: the head backward (chain_head.h,
 // waves 8..15 repeating waves 0..7), then the reverse recurrence with two cells per lane:
 // dh_rec^T = U dz^T with wave w on unit tile w % 8 over K half w / 8, dx^T = W dz^T with din tile
@@ -1440,8 +1776,13 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   const bool src = s > 0 || A.t4.on;              // (stage 0 then reads time4's dx granules)
 #define GQ_CHAINB_BODY3(HH, KXX, DD, SRCV, UPV, XOV)                                    \
   {                                                                                     \
-    if (threadIdx.x >= TMC<HH>::NT + (TMC<HH>::NT + 64 <= 1024 ? 64 : 0)) return;       \
-    chain_bwd_stage<HH, KXX, DD, SRCV, UPV, XOV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
+    if constexpr (HH == 16 && CHAINB_IO) {                                              \
+      if (threadIdx.x >= chainb_io_threads(TMC<HH>::NT, DD)) return;                    \
+      chain_bwd_stage_io<HH, KXX, DD, SRCV, UPV, XOV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
+    } else {                                                                            \
+      if (threadIdx.x >= TMC<HH>::NT + (TMC<HH>::NT + 64 <= 1024 ? 64 : 0)) return;     \
+      chain_bwd_stage<HH, KXX, DD, SRCV, UPV, XOV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
+    }                                                                                   \
   }
 #define GQ_CHAINB_BODY2(HH, KXX, DD, SRCV, UPV)                                         \
   if (!SRCV || S.sout) GQ_CHAINB_BODY3(HH, KXX, DD, SRCV, UPV, true)                    \

@@ -79,6 +79,9 @@ void launch_grads_h(int DT, int grx, dim3 grid, hipStream_t st, const void* dz, 
   }
 }
 
+void lstm_grads_reduce_records(const at::Tensor& ws_t, int H, int Din, int splits, float* dW, float* dU, float* db,
+                               hipStream_t st);
+
 // Flat-row launcher shared by the sequence-major (lstm_grads) and time-major (lstm_tm_bwd)
 // paths: row r of dz / x / dx has h_{t-1} at row r - hshift when r % period >= hshift.
 // x rows have pitch ldx, dx rows pitch lddx; only the first Din (= rows of W) channels are used.
@@ -124,10 +127,26 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
   }
 #undef GQ_GR_H
   GQ_LAUNCH_CHECK();
+  lstm_grads_reduce_records(ws_t, H, Din, splits, dW, dU, db, st);
+}
+
+// Sum `splits` split records ([split][cb][DT + HT][4][64][4] floats, ws_t also holding the NG group
+// sums past them when splits > 512) into dW / dU / db: deferred to lstm_reduce_flush in deferred
+// mode, else one reduce launch (+ the group-sum launch).
+void lstm_grads_reduce_records(const at::Tensor& ws_t, int H, int Din, int splits, float* dW, float* dU, float* db,
+                               hipStream_t st) {
+  const int ncb = (4 * H) / GR_CB;
+  const int DT = (Din + 1 + 15) / 16;
+  const int HT = H / 16;
+  const int RC = (DT + HT) * 1024 * ncb;
+  const int NG = std::max(1, splits / 512);
+  TORCH_CHECK(ws_t.numel() >= (long)splits * RC + (NG > 1 ? (long)NG * RC : 0L), "lstm_grads: split records");
   if (defer_reduce_mode()) {                      // summed by lstm_reduce_flush with the other layers'
     deferred_reds().push_back(DeferredRed{ws_t, H, Din, splits, dW, dU, db});
     return;
   }
+  float* ws = ws_t.data_ptr<float>();
+  float* ws2 = ws + (size_t)splits * RC;
   // every weight-gradient reduction raises the non-finite flag (chain control word 7) that the
   // flag-driven Adam (adam_flagged) decides from
   int* nf = chain_ctl(c10::hip::current_device()) + 7;

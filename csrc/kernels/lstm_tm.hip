@@ -39,6 +39,8 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
                      float* dU, float* db, long rows, long period, long hshift, int H, int Din, int ldx,
                      long dx_cb_stride, int lddx, long x_elems, hipStream_t st);
 int lstm_grads_col_blocks(int H);
+void lstm_grads_reduce_records(const at::Tensor& ws_t, int H, int Din, int splits, float* dW, float* dU, float* db,
+                               hipStream_t st);
 int* chain_ctl(int dev);   // lstm_chain.hip: the device's chain control words
 void lstm_dx_rows(const void* dz, int zbf, const float* W, float* dx, long rows, int H, int Dw, int lddx,
                   hipStream_t st);
@@ -351,13 +353,27 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 //       lengthens every step of the serial chain and pushes H = 32 past the VGPR budget.
 //   DX: dx^T = W dz_t^T tile -> HBM (frozen-weight input gradients, e.g. integrated gradients).
 // dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
+typedef short s16x4_t __attribute__((ext_vector_type(4)));   // 4 bf16 (v_mfma_f32_16x16x16_bf16 operand)
+
+// WG (H <= 32 layers of many tiles, e.g. SoilNet's 418): the weight gradients ride in the
+// recurrence instead of a separate pass over the dz / x / h streams. Per reverse step and wave w
+// (gate rows 16w .. 16w + 15):
+//   dW^T | db += dz_t^T [x_t | 1]   and   dU^T += dz_t^T h_{t-1}
+// as v_mfma_f32_16x16x16_bf16 with K = the tile's 16 sequences: dz^T comes from a column-major
+// copy of the step's dz tile the cell phase writes next to the row-major one, x_t and h_{t-1} are
+// streamed through the same kind of register ring as the saved state and staged transposed (bf16)
+// beside it. The partial tiles stay in VGPRs for all T steps and leave once per workgroup as one
+// split record of the weight-gradient pass's layout (lstm_grads_body.h: [tile][cb][DT + HT][4]
+// [64][4]), summed over the tiles by the same fixed-order reduction. dz itself never reaches HBM.
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false>
 __device__ __forceinline__ void lstm_tm_bwd_body(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
-    int Mp, int T, int Din, int Dw, int tile, int ntiles) {
+    int Mp, int T, int Din, int Dw, int tile, int ntiles, const float* __restrict__ xw = nullptr,
+    const float* __restrict__ hw = nullptr, float* __restrict__ wsr = nullptr) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
+  static_assert(!WG || (CPL == 1 && NT == 16 * H && G4 == 16 * NW && GR == 4), "fused weight gradients: H <= 64");
   constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
   constexpr int TX = (NXB + NW - 1) / NW;         // dx tiles per wave
   static_assert(16 * G4 / 4 == NT, "one dz float4 granule per thread");
@@ -371,6 +387,26 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   const int row0 = tile * 16;
 
   for (int i = tid; i < 2 * 16 * C::HP; i += NT) (&dhs[0][0][0])[i] = 0.f;
+
+  // fused weight gradients (WG): transposed bf16 images [row][sequence] of dz_t, [x_t | 1] and h_{t-1}
+  constexpr int XR = WG ? 32 * KX + 16 : 1;        // x image rows: channels, the bias row, zero rows
+  constexpr int DTM = WG ? 2 * KX + 1 : 1;         // dW^T din blocks (incl. the bias row), upper bound
+  constexpr int HTW = WG ? H / 16 : 1;             // dU^T k blocks
+  __shared__ __attribute__((aligned(16))) __bf16 zT[WG ? 2 : 1][WG ? G4 : 1][20];
+  __shared__ __attribute__((aligned(16))) __bf16 xT[WG ? 2 : 1][XR][20];
+  __shared__ __attribute__((aligned(16))) __bf16 hT[WG ? 2 : 1][WG ? H : 1][20];
+  const int dtw = (Dw + 16) / 16;                  // din blocks of this layer (record layout DT)
+  f32x4_t accW[DTM], accU[HTW];
+  if constexpr (WG) {
+    for (int i = tid; i < 2 * XR * 20; i += NT) {
+      const int dn = (i / 20) % XR;
+      (&xT[0][0][0])[i] = (__bf16)(dn == Dw ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int d = 0; d < DTM; ++d) accW[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < HTW; ++k) accU[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   // A fragments of U (dh_rec) and W (dx^T): tile row `col` of cell group gi is unit
   // 4 gi + (col >> 2) when col % 4 == 0 and zero otherwise -> acc[0] is the lane's own cell
@@ -440,6 +476,19 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   const int gx_seq = gx / Din, gx_k = gx % Din;
   const size_t xstep = (size_t)Mp * Din;
   float* sbase = dx + (size_t)row0 * Din + gx;
+  // WG streams: x_t granule gx of the [16][Din] tile (the dx storer's mapping) and element tid of
+  // the [16][H] h_{t-1} tile, in rings over reverse steps like the saved state
+  Granule<GR> wx[WG ? D : 1];
+  float wh[WG ? D : 1];
+  const float* wxb = xw + (size_t)row0 * Din + gx;
+  const float* whb = hw + (size_t)row0 * H + tid;
+  const size_t whstep = (size_t)Mp * H;
+#define GQ_TMB_LOAD_W(J, SS)                                                        \
+  if constexpr (WG) {                                                               \
+    const int tt_ = max(T - 1 - (SS), 0);                                           \
+    wx[J].load(wxb + (size_t)tt_ * xstep);                                          \
+    wh[J] = whb[(size_t)max(tt_ - 1, 0) * whstep];                                  \
+  }
 
   // reverse step s <-> time t = T-1-s. Streams for step s are loaded D steps ahead.
 #define GQ_TMB_LOAD_D(J, SS)                                                                \
@@ -456,6 +505,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   for (int j = 0; j < D; ++j) {
     GQ_TMB_LOAD_STATE(j, j)
     GQ_TMB_LOAD_D(j, j)
+    GQ_TMB_LOAD_W(j, j)
   }
   __syncthreads();
   // stage step 0 (t = T-1) tiles
@@ -487,11 +537,31 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         const float tc = tanhf_fast(rc[cc][j]);
         const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
         dc[cc] = dct * g4.y;
-        zs[p][col][0 * H + u] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
-        zs[p][col][1 * H + u] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
-        zs[p][col][2 * H + u] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
-        zs[p][col][3 * H + u] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
+        const __bf16 z0 = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
+        const __bf16 z1 = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
+        const __bf16 z2 = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
+        const __bf16 z3 = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
+        zs[p][col][0 * H + u] = z0;
+        zs[p][col][1 * H + u] = z1;
+        zs[p][col][2 * H + u] = z2;
+        zs[p][col][3 * H + u] = z3;
+        if constexpr (WG) {
+          zT[p][0 * H + u][col] = z0;
+          zT[p][1 * H + u][col] = z1;
+          zT[p][2 * H + u][col] = z2;
+          zT[p][3 * H + u][col] = z3;
+        }
       }
+      if constexpr (WG) {       // stage [x_t | 1] and h_{t-1} of this step, refill the slots
+        const float hm = t >= 1 ? 1.f : 0.f;
+#pragma unroll
+        for (int q = 0; q < GR; ++q) {
+          const int dn = gx_k + q;
+          xT[p][dn][gx_seq] = (__bf16)(dn < Dw ? wx[j].v[q] : (dn == Dw ? 1.f : 0.f));
+        }
+        hT[p][tid % H][tid / H] = (__bf16)(wh[j] * hm);
+      }
+      GQ_TMB_LOAD_W(j, s + D)
       GQ_TMB_LOAD_STATE(j, s + D)
       *reinterpret_cast<float4*>(&dhs[p ^ 1][gd / H][gd % H]) = dh_tile(jn, t - 1);   // dh tile of step s+1
       GQ_TMB_LOAD_D(jn, s + 1 + D)
@@ -510,6 +580,21 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
           else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][k], bz, a0, 0, 0, 0);
         }
         dhr[cc] = a0[0] + a1[0];
+      }
+      // (a') weight gradients of this step (the unrolled chunk's pad steps past t = 0 add nothing)
+      if (WG && t >= 0) {
+        const s16x4_t az = *reinterpret_cast<const s16x4_t*>(&zT[p][16 * w + col][4 * quad]);
+#pragma unroll
+        for (int d = 0; d < DTM; ++d)
+          if (d < dtw) {                            // wave-uniform, no global memory access inside
+            const s16x4_t bx = *reinterpret_cast<const s16x4_t*>(&xT[p][16 * d + col][4 * quad]);
+            accW[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az, bx, accW[d], 0, 0, 0);
+          }
+#pragma unroll
+        for (int k = 0; k < HTW; ++k) {
+          const s16x4_t bh = *reinterpret_cast<const s16x4_t*>(&hT[p][16 * k + col][4 * quad]);
+          accU[k] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az, bh, accU[k], 0, 0, 0);
+        }
       }
       // (b) dz tile of this step -> HBM as bf16 (its exact values: the MFMAs above consumed
       // these bf16 values; steps past t = 0 pad the unrolled chunk: scratch row)
@@ -550,8 +635,19 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #pragma unroll
     for (int q = 0; q < GR; ++q) sbase[q] = dxs[pl][gx_seq][gx_k + q];
   }
+  if constexpr (WG) {   // this tile's split record: wave w = column block w / 4, record wave w % 4
+    const int cb = w >> 2, wr = w & 3;
+    float* rec = wsr + ((size_t)tile * (G4 / 64) + cb) * (size_t)(dtw + HTW) * 1024;
+#pragma unroll
+    for (int d = 0; d < DTM; ++d)
+      if (d < dtw) *reinterpret_cast<f32x4_t*>(rec + ((size_t)(d * 4 + wr) * 64 + lane) * 4) = accW[d];
+#pragma unroll
+    for (int k = 0; k < HTW; ++k)
+      *reinterpret_cast<f32x4_t*>(rec + ((size_t)((dtw + k) * 4 + wr) * 64 + lane) * 4) = accU[k];
+  }
 #undef GQ_TMB_LOAD_STATE
 #undef GQ_TMB_LOAD_D
+#undef GQ_TMB_LOAD_W
 }
 
 template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
@@ -560,6 +656,15 @@ __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw) {
   lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, blockIdx.x, gridDim.x);
+}
+
+template <int H, int KX, int D, bool DX, bool LAST>
+__global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_wg_kernel(
+    const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
+    const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, const float* __restrict__ x,
+    const float* __restrict__ h, float* __restrict__ ws, int Mp, int T, int Din, int Dw) {
+  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T, Din, Dw,
+                                                       blockIdx.x, gridDim.x, x, h, ws);
 }
 
 // =====================================================================================
@@ -613,6 +718,18 @@ __global__ __launch_bounds__(TMC<HR>::NT) void lstm_tm_bwd_dual_kernel(
 static bool tm_rec_dx() {       // read per call (host side of a launch; tests toggle it)
   const char* e = std::getenv("GNNQC_TM_RECDX");
   return !(e != nullptr && e[0] == '0');
+}
+
+// Weight gradients inside the backward recurrence (lstm_tm_bwd_wg_kernel) for layers of at least
+// GNNQC_TM_FUSED_WGRAD_MIN_TILES 16-sequence tiles (default 64: with few tiles the separate pass
+// spreads the rows over the whole GPU, the recurrence's workgroups cannot); GNNQC_TM_FUSED_WGRAD=0
+// turns it off. Read per call (tests switch them).
+static bool tm_fused_wgrad(int H, int Din, int gr, int ntiles) {
+  const char* e = std::getenv("GNNQC_TM_FUSED_WGRAD");
+  if (e != nullptr && e[0] == '0') return false;
+  const char* m = std::getenv("GNNQC_TM_FUSED_WGRAD_MIN_TILES");
+  const int min_tiles = m != nullptr ? std::atoi(m) : 64;
+  return (H == 16 || H == 32) && gr == 4 && Din <= 64 && ntiles >= min_tiles;
 }
 
 static int tm_granule(int Din, const void* x) {
@@ -1190,6 +1307,36 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   const int ntiles = Mp / 16;
   auto st = stream();
   const int ncb_w = lstm_grads_col_blocks(H);
+  if (wg && tm_fused_wgrad(H, Din, gr, ntiles)) {
+    // weight gradients inside the recurrence: one split record per tile, then the reduction
+    const int DT = (Dw + 1 + 15) / 16, RC = (DT + H / 16) * 1024 * ncb_w;
+    const int NG = std::max(1, ntiles / 512);
+    at::Tensor ws = at::empty({(long)ntiles * RC + (NG > 1 ? (long)NG * RC : 0L)}, x.options());
+    at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, x.options()) : at::empty({0}, x.options());
+    if (need_dx) TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 4 == 0 && h.is_contiguous(), "lstm_tm_bwd: h layout");
+#define GQ_TM_WG_CALL(DXV, LASTV)                                                                              \
+  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, 4, DXV, LASTV>), dim3(ntiles), dim3(TMC<HH>::NT), 0, st,    \
+                     dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), W.data_ptr<float>(),                \
+                     U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr, x.data_ptr<float>(),         \
+                     h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw)
+#define GQ_TM_WG_KX(...)                                                                                        \
+  if ((Din + 31) / 32 == 1) { constexpr int KXX = 1; __VA_ARGS__; }                                             \
+  else { constexpr int KXX = 2; __VA_ARGS__; }
+    switch (H) {
+      case 16: { constexpr int HH = 16;
+        GQ_TM_WG_KX(if (need_dx) { if (last) GQ_TM_WG_CALL(true, true); else GQ_TM_WG_CALL(true, false); }
+                    else { if (last) GQ_TM_WG_CALL(false, true); else GQ_TM_WG_CALL(false, false); }) break; }
+      default: { constexpr int HH = 32;
+        GQ_TM_WG_KX(if (need_dx) { if (last) GQ_TM_WG_CALL(true, true); else GQ_TM_WG_CALL(true, false); }
+                    else { if (last) GQ_TM_WG_CALL(false, true); else GQ_TM_WG_CALL(false, false); }) break; }
+    }
+#undef GQ_TM_WG_KX
+#undef GQ_TM_WG_CALL
+    GQ_LAUNCH_CHECK();
+    lstm_grads_reduce_records(ws, H, Dw, ntiles, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), st);
+    return need_dx ? dx.narrow(0, 0, T) : dx;
+  }
   if (wg && need_dx && ncb_w > 1 && tm_rec_dx()) {
     // several gate-column blocks: the weight-gradient pass could only produce dx as ncb partial
     // slabs plus a slab sum (ncb + 2 dx-sized passes); the recurrence computes dx^T = W dz^T

@@ -94,7 +94,11 @@ def main():
         ops.lstm_chain_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg, *chain_args)
     torch.cuda.synchronize()
     pb = ops.lstm_chain_prof(x).cpu()
-    print(json.dumps({"launch": "bwd (time4 stage + chain6)", "stages": phases(pb, 6)}), flush=True)
+    # H = 16 stages (chain_bwd_stage_io) mark 0 top, 1 cell done, 2 after the barrier, 3 dh_rec ready,
+    # 4 dx done; the split-K stages (H >= 32) 0..5 as in the docstring
+    print(json.dumps({"launch": "bwd (time4 stage + chain6)", "stages": phases(pb, 5)}), flush=True)
+    # H = 16 stages' I/O waves: marks 5..7 = staging start, tile staged, next loads issued
+    print(json.dumps({"launch": "bwd marks vs compute start", "stages": marks_rel(pb, 8)}), flush=True)
     st = ops.lstm_chain_status(x).cpu().tolist()
     print(json.dumps({"status": st}), flush=True)
 

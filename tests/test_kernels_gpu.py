@@ -350,9 +350,15 @@ def test_gcn_pool_weights_matches_eager(cuda_device, aggregate, pooling):
 @pytest.mark.parametrize("Din", [18, 16, 2, 32, 64])
 @pytest.mark.parametrize("ret_seq", [True, False])
 @pytest.mark.parametrize("wgrad", [True, False])
-def test_lstm_time_major_fused_bwd_matches_eager(cuda_device, H, Din, ret_seq, wgrad):
-    """lstm_tm_fwd / lstm_tm_bwd (recurrence + dx + fused dW/dU/db) vs fp64 eager."""
+@pytest.mark.parametrize("in_rec", [False, True])
+def test_lstm_time_major_fused_bwd_matches_eager(cuda_device, H, Din, ret_seq, wgrad, in_rec, monkeypatch):
+    """lstm_tm_fwd / lstm_tm_bwd (recurrence + dx + fused dW/dU/db) vs fp64 eager. in_rec: the
+    weight gradients inside the recurrence (lstm_tm_bwd_wg_kernel, H <= 32 with float4 x
+    granules), else the separate weight-gradient pass."""
     from gnnqc.ops.lstm import lstm_eager, lstm_layer_tm, tm_eligible
+    if in_rec and not (wgrad and H <= 32 and Din % 4 == 0):
+        pytest.skip("the in-recurrence weight gradients take H <= 32, Din % 4 == 0")
+    monkeypatch.setenv("GNNQC_TM_FUSED_WGRAD_MIN_TILES", "1" if in_rec else "100000")
     dev = cuda_device
     gen = torch.Generator().manual_seed(H * 100 + Din + 3 * ret_seq)
     M, T = 40, 13                     # 3 tiles (Mp = 48), T not a multiple of the ring depth
@@ -475,9 +481,14 @@ def test_timelayer_cnn_branch_hip_vs_eager(cuda_device, monkeypatch):
 
 @pytest.mark.parametrize("H", [16, 32])
 @pytest.mark.parametrize("wgrad", [True, False])
-def test_lstm_time_major_padded_channels(cuda_device, H, wgrad):
-    """x with zero channels past W's rows (19 -> 20, float4 loader granules) == unpadded eager."""
+@pytest.mark.parametrize("in_rec", [False, True])
+def test_lstm_time_major_padded_channels(cuda_device, H, wgrad, in_rec, monkeypatch):
+    """x with zero channels past W's rows (19 -> 20, float4 loader granules) == unpadded eager;
+    in_rec: weight gradients inside the recurrence (the bias row sits inside the last x granule)."""
     from gnnqc.ops.lstm import lstm_eager, lstm_layer_tm
+    if in_rec and not wgrad:
+        pytest.skip("in-recurrence weight gradients need wgrad")
+    monkeypatch.setenv("GNNQC_TM_FUSED_WGRAD_MIN_TILES", "1" if in_rec else "100000")
     dev = cuda_device
     gen = torch.Generator().manual_seed(H + 11)
     M, T, Din = 37, 14, 19
