@@ -353,16 +353,26 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 //       lengthens every step of the serial chain and pushes H = 32 past the VGPR budget.
 //   DX: dx^T = W dz_t^T tile -> HBM (frozen-weight input gradients, e.g. integrated gradients).
 // dhout: [T][Mp][H] (or [Mp][H] for the last step only). Skipped stores go to time row T.
-typedef short s16x4_t __attribute__((ext_vector_type(4)));   // 4 bf16 (v_mfma_f32_16x16x16_bf16 operand)
+#ifndef TMW_D16
+#define TMW_D16 4        // ring depth (reverse steps) of lstm_tm_bwd_wg_kernel's streams, H = 16
+#endif
+#ifndef TMW_D32
+#define TMW_D32 6        // H = 32 (T = 337 micro: 642 -> 555 us from 4 to 6)
+#endif
+#ifndef TMW_SKIP
+#define TMW_SKIP 0       // (timing experiments only, wrong results: 1 no weight MFMAs, 2 no x / h streams,
+#endif                   //  4 no transposed dz copy; T = 337 micro, H = 16: 368 -> 297 / 310 / 352 us)   // 4 bf16 (v_mfma_f32_16x16x16_bf16 operand)
 
 // WG (H <= 32 layers of many tiles, e.g. SoilNet's 418): the weight gradients ride in the
 // recurrence instead of a separate pass over the dz / x / h streams. Per reverse step and wave w
 // (gate rows 16w .. 16w + 15):
 //   dW^T | db += dz_t^T [x_t | 1]   and   dU^T += dz_t^T h_{t-1}
-// as v_mfma_f32_16x16x16_bf16 with K = the tile's 16 sequences: dz^T comes from a column-major
-// copy of the step's dz tile the cell phase writes next to the row-major one, x_t and h_{t-1} are
-// streamed through the same kind of register ring as the saved state and staged transposed (bf16)
-// beside it. The partial tiles stay in VGPRs for all T steps and leave once per workgroup as one
+// as v_mfma_f32_16x16x32_bf16 over a PAIR of steps (K = 2 x the tile's 16 sequences; issued every
+// other step, which halved their cost on the serial step against one 16x16x16 MFMA per step): dz^T
+// comes from a column-major copy of the step's dz tile the cell phase writes next to the row-major
+// one, x_t and h_{t-1} are streamed through the same kind of register ring as the saved state and
+// staged transposed (bf16) beside it; four image buffers (step & 3), since the pair's older step is
+// read while the faster waves already write the next one. The partial tiles stay in VGPRs for all T steps and leave once per workgroup as one
 // split record of the weight-gradient pass's layout (lstm_grads_body.h: [tile][cb][DT + HT][4]
 // [64][4]), summed over the tiles by the same fixed-order reduction. dz itself never reaches HBM.
 template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false>
@@ -392,14 +402,15 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   constexpr int XR = WG ? 32 * KX + 16 : 1;        // x image rows: channels, the bias row, zero rows
   constexpr int DTM = WG ? 2 * KX + 1 : 1;         // dW^T din blocks (incl. the bias row), upper bound
   constexpr int HTW = WG ? H / 16 : 1;             // dU^T k blocks
-  __shared__ __attribute__((aligned(16))) __bf16 zT[WG ? 2 : 1][WG ? G4 : 1][20];
-  __shared__ __attribute__((aligned(16))) __bf16 xT[WG ? 2 : 1][XR][20];
-  __shared__ __attribute__((aligned(16))) __bf16 hT[WG ? 2 : 1][WG ? H : 1][20];
+  constexpr int NB = WG ? 4 : 1, RP = 24;          // image buffers, row pitch (48 B: 16-byte aligned rows)
+  __shared__ __attribute__((aligned(16))) __bf16 zT[NB][WG ? G4 : 1][RP];
+  __shared__ __attribute__((aligned(16))) __bf16 xT[NB][XR][RP];
+  __shared__ __attribute__((aligned(16))) __bf16 hT[NB][WG ? H : 1][RP];
   const int dtw = (Dw + 16) / 16;                  // din blocks of this layer (record layout DT)
   f32x4_t accW[DTM], accU[HTW];
   if constexpr (WG) {
-    for (int i = tid; i < 2 * XR * 20; i += NT) {
-      const int dn = (i / 20) % XR;
+    for (int i = tid; i < NB * XR * RP; i += NT) {
+      const int dn = (i / RP) % XR;
       (&xT[0][0][0])[i] = (__bf16)(dn == Dw ? 1.f : 0.f);
     }
 #pragma unroll
@@ -476,15 +487,19 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   const int gx_seq = gx / Din, gx_k = gx % Din;
   const size_t xstep = (size_t)Mp * Din;
   float* sbase = dx + (size_t)row0 * Din + gx;
-  // WG streams: x_t granule gx of the [16][Din] tile (the dx storer's mapping) and element tid of
-  // the [16][H] h_{t-1} tile, in rings over reverse steps like the saved state
-  Granule<GR> wx[WG ? D : 1];
+  // WG streams: XG consecutive floats of the [16][Din] x_t tile (threads past the tile repeat it)
+  // and element tid of the [16][H] h_{t-1} tile, in rings over reverse steps like the saved state
+  constexpr int XG = WG ? (16 * 32 * KX / NT > 1 ? 16 * 32 * KX / NT : 1) : 1;
+  static_assert(XG <= 4, "x stream granule");
+  Granule<XG> wx[WG ? D : 1];
   float wh[WG ? D : 1];
-  const float* wxb = xw + (size_t)row0 * Din + gx;
+  const int wxe = (tid * XG) % (16 * Din);
+  const int wx_seq = wxe / Din, wx_k = wxe % Din;
+  const float* wxb = xw + (size_t)row0 * Din + wxe;
   const float* whb = hw + (size_t)row0 * H + tid;
   const size_t whstep = (size_t)Mp * H;
 #define GQ_TMB_LOAD_W(J, SS)                                                        \
-  if constexpr (WG) {                                                               \
+  if constexpr (WG && !(TMW_SKIP & 2)) {                                                               \
     const int tt_ = max(T - 1 - (SS), 0);                                           \
     wx[J].load(wxb + (size_t)tt_ * xstep);                                          \
     wh[J] = whb[(size_t)max(tt_ - 1, 0) * whstep];                                  \
@@ -545,21 +560,21 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         zs[p][col][1 * H + u] = z1;
         zs[p][col][2 * H + u] = z2;
         zs[p][col][3 * H + u] = z3;
-        if constexpr (WG) {
-          zT[p][0 * H + u][col] = z0;
-          zT[p][1 * H + u][col] = z1;
-          zT[p][2 * H + u][col] = z2;
-          zT[p][3 * H + u][col] = z3;
+        if constexpr (WG && !(TMW_SKIP & 4)) {
+          zT[s & 3][0 * H + u][col] = z0;
+          zT[s & 3][1 * H + u][col] = z1;
+          zT[s & 3][2 * H + u][col] = z2;
+          zT[s & 3][3 * H + u][col] = z3;
         }
       }
-      if constexpr (WG) {       // stage [x_t | 1] and h_{t-1} of this step, refill the slots
+      if constexpr (WG && !(TMW_SKIP & 2)) {   // stage [x_t | 1] and h_{t-1} of this step, refill the slots
         const float hm = t >= 1 ? 1.f : 0.f;
 #pragma unroll
-        for (int q = 0; q < GR; ++q) {
-          const int dn = gx_k + q;
-          xT[p][dn][gx_seq] = (__bf16)(dn < Dw ? wx[j].v[q] : (dn == Dw ? 1.f : 0.f));
+        for (int q = 0; q < XG; ++q) {
+          const int dn = wx_k + q;
+          xT[s & 3][dn][wx_seq] = (__bf16)(dn < Dw ? wx[j].v[q] : (dn == Dw ? 1.f : 0.f));
         }
-        hT[p][tid % H][tid / H] = (__bf16)(wh[j] * hm);
+        hT[s & 3][tid % H][tid / H] = (__bf16)(wh[j] * hm);
       }
       GQ_TMB_LOAD_W(j, s + D)
       GQ_TMB_LOAD_STATE(j, s + D)
@@ -581,19 +596,28 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         }
         dhr[cc] = a0[0] + a1[0];
       }
-      // (a') weight gradients of this step (the unrolled chunk's pad steps past t = 0 add nothing)
-      if (WG && t >= 0) {
-        const s16x4_t az = *reinterpret_cast<const s16x4_t*>(&zT[p][16 * w + col][4 * quad]);
+      // (a') weight gradients of the step pair (s - 1, s) at odd s, or of the last step alone
+      // (K lanes of the missing older step zeroed); the unrolled chunk's pad steps add nothing
+      if (WG && !(TMW_SKIP & 1) && t >= 0 && ((s & 1) || t == 0)) {
+        const int half = quad >> 1, so = 8 * (quad & 1);      // K = 8 quad + i -> (step of the pair, sequence)
+        const int bk = half ? (s & 3) : ((s - 1) & 3);
+        const bool live = half || (s & 1);
+        const bf16x8_t zero8 = {};
+        // (both operands of a dead half are zeroed: its buffers may hold anything, NaN patterns too)
+        bf16x8_t az = *reinterpret_cast<const bf16x8_t*>(&zT[bk][16 * w + col][so]);
+        az = live ? az : zero8;
 #pragma unroll
         for (int d = 0; d < DTM; ++d)
           if (d < dtw) {                            // wave-uniform, no global memory access inside
-            const s16x4_t bx = *reinterpret_cast<const s16x4_t*>(&xT[p][16 * d + col][4 * quad]);
-            accW[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az, bx, accW[d], 0, 0, 0);
+            bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xT[bk][16 * d + col][so]);
+            bx = live ? bx : zero8;
+            accW[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az, bx, accW[d], 0, 0, 0);
           }
 #pragma unroll
         for (int k = 0; k < HTW; ++k) {
-          const s16x4_t bh = *reinterpret_cast<const s16x4_t*>(&hT[p][16 * k + col][4 * quad]);
-          accU[k] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az, bh, accU[k], 0, 0, 0);
+          bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hT[bk][16 * k + col][so]);
+          bh = live ? bh : zero8;
+          accU[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az, bh, accU[k], 0, 0, 0);
         }
       }
       // (b) dz tile of this step -> HBM as bf16 (its exact values: the MFMAs above consumed
@@ -1316,7 +1340,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     if (need_dx) TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 4 == 0 && h.is_contiguous(), "lstm_tm_bwd: h layout");
 #define GQ_TM_WG_CALL(DXV, LASTV)                                                                              \
-  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, 4, DXV, LASTV>), dim3(ntiles), dim3(TMC<HH>::NT), 0, st,    \
+  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV>), dim3(ntiles), dim3(TMC<HH>::NT), 0, st,    \
                      dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), W.data_ptr<float>(),                \
                      U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr, x.data_ptr<float>(),         \
                      h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw)
