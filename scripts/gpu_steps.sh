@@ -44,17 +44,23 @@ for step in "$@"; do
         phase)  GNNQC_HIP_LIB=gnnqc/_lib/variants/prof.so run phase 300 $PY scripts/chain_phase_prof.py ;;
         stats)  prof stats 400 --kernel-trace --stats -d "$OUT/prof_stats" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line ;;
+        stats_ng) prof stats_ng 400 --kernel-trace --stats -d "$OUT/prof_stats_ng" -o run --output-format csv -- \
+                    $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line --no-graph ;;
         stats_ig) prof stats_ig 400 --kernel-trace --stats -d "$OUT/prof_stats_ig" -o run --output-format csv -- \
                     $PY "$ROOT/scripts/bench_ig.py" ;;
         stats_soil) prof stats_soil 400 --kernel-trace --stats -d "$OUT/prof_stats_soil" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --ds soilnet --steps 20 --warmup 3 --no-graph ;;
         pmc_cml) prof pmc_cml 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_cml" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line ;;
-        pmc_cml_mem) prof pmc_cml_mem 120 --kernel-trace --pmc FETCH_SIZE WRITE_SIZE -d "$OUT/prof_pmc_cml_mem" -o run \
+        pmc_cml_mem) prof pmc_cml_mem 120 --kernel-trace --pmc FETCH_SIZE -d "$OUT/prof_pmc_cml_mem" -o run \
+                    --output-format csv -- $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line ;;
+        pmc_cml_wr) prof pmc_cml_wr 120 --kernel-trace --pmc WRITE_SIZE -d "$OUT/prof_pmc_cml_wr" -o run \
                     --output-format csv -- $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line ;;
         pmc_soil) prof pmc_soil 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_soil" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --ds soilnet --steps 6 --warmup 2 --no-graph ;;
-        pmc_soil_mem) prof pmc_soil_mem 120 --kernel-trace --pmc FETCH_SIZE WRITE_SIZE -d "$OUT/prof_pmc_soil_mem" -o run \
+        pmc_soil_mem) prof pmc_soil_mem 120 --kernel-trace --pmc FETCH_SIZE -d "$OUT/prof_pmc_soil_mem" -o run \
+                    --output-format csv -- $PY "$ROOT/bench.py" --ds soilnet --steps 6 --warmup 2 --no-graph ;;
+        pmc_soil_wr) prof pmc_soil_wr 120 --kernel-trace --pmc WRITE_SIZE -d "$OUT/prof_pmc_soil_wr" -o run \
                     --output-format csv -- $PY "$ROOT/bench.py" --ds soilnet --steps 6 --warmup 2 --no-graph ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

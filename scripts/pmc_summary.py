@@ -64,11 +64,18 @@ def load_trace(d):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("dir")
+    ap.add_argument("dir", nargs="+", help="one or more runs (e.g. a FETCH_SIZE pass and a WRITE_SIZE pass)")
     ap.add_argument("--trace", default=None, help="kernel-trace run for durations")
     ap.add_argument("--top", type=int, default=20)
     args = ap.parse_args(argv)
-    per, dur = load_counters(args.dir)
+    per, dur = collections.defaultdict(lambda: collections.defaultdict(list)), collections.defaultdict(list)
+    for d in args.dir:
+        p1, d1 = load_counters(d)
+        for k, v in p1.items():
+            for c, vals in v.items():
+                per[k][c].extend(vals)
+        for k, v in d1.items():
+            dur[k].extend(v)
     if args.trace:
         tdur = load_trace(args.trace)
         for k, v in tdur.items():

@@ -16,19 +16,25 @@ def main():
     from gnnqc.utils.native import hip_ops
     ops = hip_ops()
     dev = torch.device("cuda:0")
-    T, Mp = int(os.environ.get("T", "337")), int(os.environ.get("MP", "6688"))
+    Mp = int(os.environ.get("MP", "6688"))
     reps = int(os.environ.get("REPS", "20"))
     torch.manual_seed(0)
-    for H, Din in ((16, 16), (32, 16), (32, 32)):
+    # CONFIGS: "H:Din:T,..." (default: the SoilNet layers' shapes; H = 64 has no in-recurrence path)
+    cfgs = [tuple(int(v) for v in c.split(":")) for c in
+            os.environ.get("CONFIGS", "16:16:337,32:16:112,32:32:112,64:32:37,64:64:37").split(",")]
+    for H, Din, T in cfgs:
         x = torch.randn(T, Mp, Din, device=dev) * 0.5
         W = torch.randn(Din, 4 * H, device=dev) * 0.2
         U = torch.randn(H, 4 * H, device=dev) * 0.2
         b = torch.zeros(4 * H, device=dev)
         h, g, c = ops.lstm_tm_fwd(x, W, U, b, True)
         dh = torch.randn(T, Mp, H, device=dev) * 0.1
-        for path in ("in_rec", "pass"):
+        for path in (("in_rec", "pass", "dx_only") if H <= 32 else ("pass", "dx_only")):
             os.environ["GNNQC_TM_FUSED_WGRAD"] = "1" if path == "in_rec" else "0"
-            dW, dU, db = torch.zeros_like(W), torch.zeros_like(U), torch.zeros_like(b)
+            if path == "dx_only":            # the recurrence alone (frozen weights: dx, no dz stream)
+                dW = dU = db = torch.zeros(0, device=dev)
+            else:
+                dW, dU, db = torch.zeros_like(W), torch.zeros_like(U), torch.zeros_like(b)
             for _ in range(3):
                 ops.lstm_tm_bwd(dh, g, c, x, h, W, U, dW, dU, db, True)
             torch.cuda.synchronize()
@@ -38,7 +44,7 @@ def main():
                 ops.lstm_tm_bwd(dh, g, c, x, h, W, U, dW, dU, db, True)
             e1.record()
             torch.cuda.synchronize()
-            print(json.dumps({"H": H, "Din": Din, "path": path, "us": round(e0.elapsed_time(e1) * 1e3 / reps, 1)}),
+            print(json.dumps({"H": H, "Din": Din, "T": T, "path": path, "us": round(e0.elapsed_time(e1) * 1e3 / reps, 1)}),
                   flush=True)
 
 
