@@ -439,8 +439,20 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
       ufr[cc][s] = v;
     }
   }
-  bf16x8_t wfr[DX ? TX : 1][DX ? KB : 1];
-  if constexpr (DX) {
+  // WL (H = 64: 16 waves, 128 VGPRs each): the dx A fragments are read from an LDS image of W^T
+  // instead of living in 32 VGPRs; in registers they pushed the body into 16-23 VGPRs of spills,
+  // whose scratch reloads sat on the serial step
+  constexpr bool WL = DX && H == 64;
+  constexpr bool WRG = DX && !WL;
+  __shared__ __attribute__((aligned(16))) __bf16 wls[WL ? 32 * KX : 1][WL ? G4 + 8 : 8];
+  if constexpr (WL) {
+    for (int i = tid; i < 32 * KX * G4; i += NT) {
+      const int dn = i / G4, g = i % G4;
+      wls[dn][g] = (__bf16)(dn < Dw ? W[(size_t)dn * G4 + g] : 0.f);
+    }
+  }
+  bf16x8_t wfr[WRG ? TX : 1][WRG ? KB : 1];
+  if constexpr (WRG) {
 #pragma unroll
     for (int q = 0; q < TX; ++q) {
       const int xb = w + NW * q;
@@ -644,7 +656,10 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
               const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
-              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[q][k], bz, a, 0, 0, 0);
+              bf16x8_t wa;
+              if constexpr (WL) wa = *reinterpret_cast<const bf16x8_t*>(&wls[16 * xb + col][32 * k + 8 * quad]);
+              else wa = wfr[q][k];
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bz, a, 0, 0, 0);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) dxs[p][col][16 * xb + 4 * quad + r] = a[r];
