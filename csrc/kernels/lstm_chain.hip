@@ -138,7 +138,12 @@ __device__ __forceinline__ void st_granule(unsigned long long* p, float v, unsig
 // memory system enough to slow the running stages' own streams severalfold.)
 template <bool INL>
 __device__ __forceinline__ unsigned long long chain_wait_body(const unsigned long long* p, unsigned want, int* ctl);
-__device__ __noinline__ unsigned long long chain_wait(const unsigned long long* p, unsigned want, int* ctl) {
+#ifdef CHAIN_WAIT_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+unsigned long long chain_wait(const unsigned long long* p, unsigned want, int* ctl) {
   return chain_wait_body<false>(p, want, ctl);
 }
 // inlined form for the forward I/O waves: a call in their step loop made the compiler drain vmcnt
@@ -837,11 +842,18 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
     if (threadIdx.x >= chain_live_threads(TMC<HH>::NT, DD, KXX, SRCV, PINV)) return;   \
     chain_stage<HH, TRAIN, KXX, DD, SRCV, PINV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
   }
+#ifdef CHAIN_KX1_ONLY      // (A/B probe: no 33-64-channel stage bodies in the kernel; such chains fail)
+#define GQ_CHAIN_SRC(HH, PINV, DD) if (KX == 1) GQ_CHAIN_BODY(HH, 1, DD, true, PINV)
+#define GQ_CHAIN_KX(HH)                                                                 \
+  if (src) { if (S.PIN == 3) { GQ_CHAIN_SRC(HH, 3, CHAIN_D3) } else { GQ_CHAIN_SRC(HH, 1, CHAIN_D) } } \
+  else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, CHAIN_D0, false, 1) }
+#else
 #define GQ_CHAIN_SRC(HH, PINV, DD)                                                      \
   if (KX == 1) GQ_CHAIN_BODY(HH, 1, DD, true, PINV) else GQ_CHAIN_BODY(HH, 2, DD, true, PINV)
 #define GQ_CHAIN_KX(HH)                                                                 \
   if (src) { if (S.PIN == 3) { GQ_CHAIN_SRC(HH, 3, CHAIN_D3) } else { GQ_CHAIN_SRC(HH, 1, CHAIN_D) } } \
   else { if (KX == 1) GQ_CHAIN_BODY(HH, 1, CHAIN_D0, false, 1) else GQ_CHAIN_BODY(HH, 2, CHAIN_D0, false, 1) }
+#endif
   if (H == 16) GQ_CHAIN_KX(16)
   else if (H == 32) GQ_CHAIN_KX(32)
   else GQ_CHAIN_KX(64)
