@@ -71,6 +71,15 @@ static constexpr int CHAIN_SPIN = 1 << 20;
 #ifndef CHAIN_DEFER_LD
 #define CHAIN_DEFER_LD 1     // I/O waves issue their next loads a step after staging (see the I/O loops)
 #endif
+#ifndef CHAIN_W_SLEEP
+#define CHAIN_W_SLEEP 0      // chain_wait back-off: s_sleep argument (x 64 clocks) per nap unit (8 / 8: 0.284 ms/step,
+#endif
+#ifndef CHAIN_W_NAPMAX
+#define CHAIN_W_NAPMAX 1     //   2 / 4: 0.278, 0 / 1: 0.275-0.277: lane 0's load latency paces the poll) and the largest nap
+#endif
+#ifndef CHAIN_RP_NAPMAX
+#define CHAIN_RP_NAPMAX 16   // bulk re-poll of a stale tile: largest nap (s_sleep 2 units) between rounds
+#endif
 #ifndef CHAIN_PRIO
 #define CHAIN_PRIO 2         // s_setprio of the compute waves of a stage with I/O waves
 #endif
@@ -169,8 +178,8 @@ __device__ __forceinline__ unsigned long long chain_wait_body(const unsigned lon
       v = ld_granule(p);
       if (__builtin_amdgcn_ballot_w64((unsigned)(v >> 32) != want) == 0) return v;
     }
-    for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(8);
-    nap = min(nap * 2, 8);
+    for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(CHAIN_W_SLEEP);
+    nap = min(nap * 2, CHAIN_W_NAPMAX);
   }
   __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return v;
@@ -382,7 +391,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
             break;
           }
           for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(2);
-          nap = min(nap * 2, 16);
+          nap = min(nap * 2, CHAIN_RP_NAPMAX);
         }
       }
       const size_t po = xbase + (size_t)tx * xstep;
@@ -1448,7 +1457,7 @@ __device__ __forceinline__ void chain_bwd_stage_io(const ChainBStage S, int tile
             break;
           }
           for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(2);
-          nap = min(nap * 2, 16);
+          nap = min(nap * 2, CHAIN_RP_NAPMAX);
         }
       }
     }
