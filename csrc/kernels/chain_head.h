@@ -270,9 +270,15 @@ struct ChainHeadBwdLds {
 // tile, global) feeds it: dh_{T-1} -> dh [16][F + 4] (LDS), the tile's weight-gradient record ->
 // hd.gpart[tile], then the tile's arrival is counted in hd.ticket (chain_head_bwd_reduce waits
 // for all of them).
+// Precompute mode (the chain FORWARD's time4 stage, right after the head forward; everything here
+// is linear in dL/dloss): hld >= 0 reads hT as the [16][hld] LDS tile of h_{T-1}, unit_gl takes
+// dL/dloss = 1 (the backward scales dh and the reduced records by the real one), count = false
+// leaves the arrival ticket alone (the records are complete at the launch boundary), and nlive
+// is the number of live waves that share the record tiles.
 template <int F>
 __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* __restrict__ hT, int tile, int ntiles,
-                                               float* dh, char* scratch) {
+                                               float* dh, char* scratch, int hld = -1, bool unit_gl = false,
+                                               bool count = true, int nlive = 0) {
   constexpr int HLP = F + 4, PT = 16 * CH_AP;
   using Rec = ChainHeadRec<F>;
   float* sh = reinterpret_cast<float*>(scratch);     // [16][HLP]
@@ -289,12 +295,14 @@ __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* 
   const int tid = ch_tid(), w = tid >> 6, j = tid & 63;
   const int l = tid & 63, lm = l & 15, lq = l >> 4;
   const int row0 = tile * 16;
+  const float* hsrc = hld < 0 ? hT + (size_t)row0 * F : hT;
+  const int hp = hld < 0 ? F : hld;
   for (int e = tid; e < 16 * F / 4; e += 64 * CH_NW) {
-    const float4 v = reinterpret_cast<const float4*>(hT + (size_t)row0 * F)[e];
     const int rr = 4 * e / F, k = 4 * e % F;
+    const float4 v = *reinterpret_cast<const float4*>(hsrc + (size_t)rr * hp + k);
     *reinterpret_cast<float4*>(sh + rr * HLP + k) = v;
   }
-  const float w3j = hd.W3[j], b3 = hd.b3[0], gl = hd.dloss[0];
+  const float w3j = hd.W3[j], b3 = hd.b3[0], gl = unit_gl ? 1.f : hd.dloss[0];
   float yy[2], mm[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -348,7 +356,7 @@ __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* 
   float* rec = hd.gpart + (size_t)tile * Rec::PITCH;
   float* rec2 = rec + F * CH_HU + CH_HU;
   // the record tiles are spread over ALL waves of the workgroup (8 or 16), each stored once
-  const int wa = threadIdx.x >> 6, nwa = blockDim.x >> 6;
+  const int wa = threadIdx.x >> 6, nwa = nlive > 0 ? nlive : (int)(blockDim.x >> 6);
   for (int t = wa; t < F / 16 * 4; t += nwa) {        // dW1 [F][64]: (F/16) x 4 tiles
     const int it = t >> 2, jt = t & 3;
     const ch_f4 acc = wgrad(sh, HLP, it, sdz1, jt);
@@ -378,6 +386,10 @@ __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* 
     for (int rr = 0; rr < 16; ++rr) s += misc[rr];
     ch_st(rec2 + CH_HU * CH_HU + 2 * CH_HU, s);                 // db3
   }
+  if (!count) {
+    __syncthreads();
+    return;
+  }
   // (sc1 stores, every wave's vmcnt(0), barrier, one lane's counter add: no fence)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -389,11 +401,15 @@ __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* 
 // sums its 1/ntiles slice of the records over the tiles in tile order (deterministic) and adds
 // it to the gradients; the last one to finish re-arms both counters. One workgroup reducing all
 // of it took ~60 us (25 rounds of 8 dependent-latency loads per thread).
+// pre: the records come from an earlier launch (chain_head_bwd's precompute mode): no arrival wait,
+// and every sum is scaled by `scale` (dL/dloss).
 template <int F>
-__device__ __forceinline__ void chain_head_bwd_reduce(const ChainHead hd, int tile, int ntiles) {
+__device__ __forceinline__ void chain_head_bwd_reduce(const ChainHead hd, int tile, int ntiles, bool pre = false,
+                                                      float scale = 1.f) {
   using Rec = ChainHeadRec<F>;
   __shared__ int bad;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && pre) bad = 0;
+  if (threadIdx.x == 0 && !pre) {
     int nap = 1, it = 0;
     bad = 0;
     while (__hip_atomic_load(hd.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles) {
@@ -426,7 +442,7 @@ __device__ __forceinline__ void chain_head_bwd_reduce(const ChainHead hd, int ti
       for (int q = 0; q < RB; ++q) {
       const int e = e0 + q * (int)blockDim.x;
       if (e >= e1) break;
-      const float s = acc[q];
+      const float s = acc[q] * scale;
       // (adam_flagged decides the step from such flags instead of scanning the gradient buffer)
       if (!isfinite(s)) __hip_atomic_store(hd.ctl + 7, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int o = e;

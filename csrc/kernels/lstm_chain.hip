@@ -117,6 +117,8 @@ struct ChainT4 {
   unsigned char* pin_idx;            //   and its argmax bytes
   int T, Din, Dw, on;
   ChainHead hd;
+  float* hb;                         // train: the head backward precomputed here ([ntiles][16][128]
+                                     // dh_{T-1} | records, dL/dloss = 1; nullptr: the backward runs it)
 };
 
 struct ChainArgs {
@@ -650,7 +652,9 @@ struct ChainT4Lds {
   static constexpr int HS = 2 * 16 * (128 + 8) * 2;       // bf16 h_{t-1} (double buffer)
   static constexpr int XS = 2 * 16 * (64 + 8) * 2;        // bf16 x_t (double buffer)
   static constexpr int HL = 16 * (128 + 4) * 4;           // fp32 h_{T-1} for the head
-  static constexpr int BYTES = HS + XS + HL + ChainHeadFwdLds<128>::BYTES;
+  static constexpr int DHT = 16 * (128 + 4) * 4;          // precomputed head backward: dh_{T-1}
+  static constexpr int HF = ChainHeadFwdLds<128>::BYTES, HB = DHT + ChainHeadBwdLds<128>::BYTES;
+  static constexpr int BYTES = HS + XS + HL + (HF > HB ? HF : HB);
 };
 
 template <bool TRAIN>
@@ -820,6 +824,22 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
           if (threadIdx.x >= 64 * CH_NW) return;    // the head runs on 8 waves (the rest exit)
           chain_head_fwd<128>(A.t4.hd, r, A.ntiles, reinterpret_cast<const float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS),
                               smem + ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL);
+          if constexpr (TRAIN) {
+            if (A.t4.hb != nullptr) {
+              // the head backward, here instead of at the start of the backward launch (it only needs
+              // this launch's outputs; dL/dloss = 1, scaled there): the backward's time4 stage then
+              // starts its reverse steps at once (the head backward was ~12 us of its critical path)
+              __syncthreads();                       // the head forward's scratch is free
+              constexpr int OFF = ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL;
+              float* dhs = reinterpret_cast<float*>(smem + OFF);
+              ChainHead hb = A.t4.hd;
+              hb.gpart = A.t4.hb + (size_t)A.ntiles * 16 * 128;
+              chain_head_bwd<128>(hb, reinterpret_cast<const float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS), r, A.ntiles,
+                                  dhs, smem + OFF + ChainT4Lds::DHT, 132, true, false, CH_NW);
+              for (int e = ch_tid(); e < 16 * 128; e += 64 * CH_NW)
+                A.t4.hb[((size_t)r * 16 + e / 128) * 128 + e % 128] = dhs[(e / 128) * 132 + e % 128];
+            }
+          }
           __syncthreads();
           if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
         }
@@ -905,6 +925,7 @@ struct ChainT4B {
   const float* g;                    // saved gates, fp32 (time4_head.hip t4_sidx layout)
   const float* c;                    // saved (c_t, c_{t-1})
   const bf16x8_t* pk;                // the forward's fragment image of (W, U) (lstm_chain_head_fwd)
+  const float* hb;                   // the forward's precomputed head backward (ChainT4::hb) or nullptr
   __bf16* dz;                        // [T+1][Mp][512] bf16 (the weight-gradient pass's input)
   unsigned long long* sout;          // dx granule stream [T][Mp][Din]
   int T, Din, Dw, on;
@@ -1653,7 +1674,7 @@ __device__ __forceinline__ void chain_bwd_stage_io(const ChainBStage S, int tile
 // w % 4 over K quarter w / 4 (partials summed through LDS), dz -> HBM, dx -> granules (tag =
 // pooled time of the chain's top layer). Then this tile's share of the head-gradient reduction.
 __device__ __forceinline__ void chain_t4_bwd_stage(const ChainT4B Q, int tile, int ntiles, int Mp, unsigned tagb,
-                                                   char* smem) {
+                                                   char* smem, long long* mk = nullptr) {
   constexpr int H = 128, G4 = 4 * H, NW = 16, CPL = 2, HP = H + 4, ZP = G4 + 8, XP = 68;
   using L = ChainT4BLds;
   static_assert(L::DHT % 16 == 0 && L::ZS % 16 == 0 && L::DN % 16 == 0, "t4 backward LDS layout");
@@ -1691,7 +1712,12 @@ __device__ __forceinline__ void chain_t4_bwd_stage(const ChainT4B Q, int tile, i
   };
   load_slot(0, T - 1);
   load_slot(1, T - 2);
-  chain_head_bwd<H>(Q.hd, Q.h + (size_t)(T - 1) * Mp * H, tile, ntiles, dhT, rs);
+  if (Q.hb != nullptr) {                           // precomputed by the forward (dL/dloss = 1): scale
+    const float gl = Q.hd.dloss[0];
+    for (int e = tid; e < 16 * H; e += 1024) dhT[(e / H) * HP + e % H] = gl * Q.hb[((size_t)tile * 16 + e / H) * H + e % H];
+  } else {
+    chain_head_bwd<H>(Q.hd, Q.h + (size_t)(T - 1) * Mp * H, tile, ntiles, dhT, rs);
+  }
   // weight fragments (after the head prologue: live through it they would crowd its registers),
   // from the forward's lane-contiguous fragment image (time4_head.hip's backward layout: wave
   // w' < 8 holds unit tile w' over the full K, and din tile w' % 4 over gate-column half w' / 4)
@@ -1706,6 +1732,7 @@ __device__ __forceinline__ void chain_t4_bwd_stage(const ChainT4B Q, int tile, i
     for (int s = 0; s < 4; ++s) wfr[s] = pw[(4 * (kq & 1) + s) * 64];
   }
   __syncthreads();                                 // the head scratch becomes the step tiles
+  if (mk != nullptr && tid == 0) mk[0] = (long long)__builtin_amdgcn_s_memrealtime();   // (trace: head done)
   // dx element of this thread (threads past the [16][Din] tile re-read the last one, no store)
   const int nx = 16 * Din;
   const bool ownx = tid < nx;
@@ -1766,7 +1793,14 @@ __device__ __forceinline__ void chain_t4_bwd_stage(const ChainT4B Q, int tile, i
     if (ownx) st_granule(Q.sout + xoff + (size_t)t * xstep, v, tagb | (unsigned)t);
   }
   }
-  chain_head_bwd_reduce<H>(Q.hd, tile, ntiles);
+  if (mk != nullptr && tid == 0) mk[64] = (long long)__builtin_amdgcn_s_memrealtime();  // (trace: steps done)
+  if (Q.hb != nullptr) {
+    ChainHead hd = Q.hd;
+    hd.gpart = const_cast<float*>(Q.hb) + (size_t)ntiles * 16 * H;
+    chain_head_bwd_reduce<H>(hd, tile, ntiles, true, Q.hd.dloss[0]);
+  } else {
+    chain_head_bwd_reduce<H>(Q.hd, tile, ntiles);
+  }
 }
 
 __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
@@ -1776,7 +1810,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   if (s == A.ns && A.t4.on && tile < A.ntiles) {  // time4 + head backward of this tile
     if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
     const unsigned tagb = chain_tag_base((unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    chain_t4_bwd_stage(A.t4, tile, A.ntiles, A.Mp, tagb, smem);
+    chain_t4_bwd_stage(A.t4, tile, A.ntiles, A.Mp, tagb, smem, blockIdx.x < 64 ? A.trace + 512 + blockIdx.x : nullptr);
     __syncthreads();
     if (threadIdx.x == 0) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
     chain_finish(A.ctl, nblk);
@@ -2068,6 +2102,7 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   }
   int nblk = ns * nt8;
   std::vector<at::Tensor> t4out;
+  at::Tensor hb_t;
   if (t4 != nullptr) {
     TORCH_CHECK(pkW != nullptr && pkU != nullptr, "lstm_chain_head_fwd: time4 weights");
     check_f32_cuda(*t4->b, "bt4");
@@ -2093,6 +2128,14 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     t4_head_fwd_args(Q.hd, t4->head, *t4->y, *t4->mask, t4->M, Mp, t4->alpha1, t4->alpha2, t4->w0, t4->w1, t4->sums,
                      t4->hist, logits, loss, part);
     t4out = {h4, g4, c4, logits, loss, part};
+    // the head backward precomputed by this launch (GNNQC_HEAD_BWD_IN_FWD=0: the backward runs it)
+    const char* hbe = std::getenv("GNNQC_HEAD_BWD_IN_FWD");
+    if (train && !(hbe != nullptr && hbe[0] == '0')) {
+      hb_t = at::empty({(long)ntiles * 16 * 128 + (long)ntiles * ChainHeadRec<128>::PITCH}, opt);
+      Q.hb = hb_t.data_ptr<float>();
+    } else {
+      hb_t = at::empty({0}, opt);
+    }
     nblk += nt8;
   }
   at::Tensor pk;
@@ -2120,6 +2163,7 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   for (auto& t : out)
     if (t.scalar_type() != at::kLong) res.push_back(t);
   if (pk.defined()) res.push_back(pk);
+  if (hb_t.defined()) res.push_back(hb_t);        // (headed launch: [.., pk, hb, h4, g4, c4, logits, loss])
   for (int i = 0; i < 5 && i < (int)t4out.size(); ++i) res.push_back(t4out[i]);
   return res;
 }
@@ -2157,7 +2201,8 @@ void t4_head_bwd_args(ChainHead& hd, at::TensorList head, const at::Tensor& y, c
 // lstm_chain_bwd (the top one must pool by 3). Returns [dz4 [T4 + 1, Mp, 512], dz_0 .. dz_{n-1}, dx].
 std::vector<at::Tensor> lstm_chain_head_bwd(const at::Tensor& dloss, const at::Tensor& x4, const at::Tensor& h4,
                                             const at::Tensor& g4, const at::Tensor& c4, const at::Tensor& Wt4,
-                                            const at::Tensor& Ut4, const at::Tensor& pk, at::TensorList head, const at::Tensor& y,
+                                            const at::Tensor& Ut4, const at::Tensor& pk, const at::Tensor& hb,
+                                            at::TensorList head, const at::Tensor& y,
                                             const at::Tensor& mask, int64_t M, double alpha1, double alpha2, double w0,
                                             double w1, at::TensorList hgrads, at::TensorList g, at::TensorList c,
                                             at::TensorList W, at::TensorList U, at::TensorList pidx,
@@ -2188,6 +2233,14 @@ std::vector<at::Tensor> lstm_chain_head_bwd(const at::Tensor& dloss, const at::T
   TORCH_CHECK(pk.is_cuda() && pk.is_contiguous() && pk.nbytes() == (size_t)T4PK_ALL * 16,
               "lstm_chain_head_bwd: pk must be the forward's full fragment image");
   Q.pk = reinterpret_cast<const bf16x8_t*>(pk.data_ptr());
+  if (hb.numel() > 0) {
+    check_f32_cuda(hb, "lstm_chain_head_bwd hb");
+    TORCH_CHECK(hb.numel() == (long)(Mp / 16) * 16 * 128 + (long)(Mp / 16) * ChainHeadRec<128>::PITCH,
+                "lstm_chain_head_bwd: hb must be the forward's precomputed head backward");
+    Q.hb = hb.data_ptr<float>();
+  } else {
+    Q.hb = nullptr;
+  }
   at::Tensor dz4 = at::empty({T4 + 1, Mp, 512}, opt.dtype(at::kBFloat16));
   Q.dz = bf16_ptr(dz4);
   Q.sout = reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>());

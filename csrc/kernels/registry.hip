@@ -51,7 +51,7 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_chain_bwd(Tensor dh, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");
   m.def("lstm_chain_head_bwd(Tensor dloss, Tensor x4, Tensor h4, Tensor g4, Tensor c4, Tensor Wt4, Tensor Ut4, "
-        "Tensor pk, Tensor[] head, Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, "
+        "Tensor pk, Tensor hb, Tensor[] head, Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, "
         "Tensor(a!)[] hgrads, Tensor[] g, Tensor[] c, Tensor[] W, Tensor[] U, Tensor[] pidx, int[] pool, "
         "int[] x_width, int[] T_in) -> Tensor[]");
   m.def("time4_head_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor pk, bool train, Tensor[] head, Tensor y, Tensor mask, "

@@ -457,12 +457,14 @@ class _HipLSTMChainHead(torch.autograd.Function):
                                            sums_, hist_)
             h4, g4, c4, logits, loss = outs[-5:]
             del outs[-5:]
+            hb = outs.pop()       # the head backward precomputed by the launch (dL/dloss = 1), or empty
             pk = outs.pop()
         else:
             # (the chain's spare workgroups build time4's weight-fragment image on the way)
             outs = ops.lstm_chain_fwd_pack(x, Ws[:ns], Us[:ns], bs[:ns], [int(p) for p in pools], need, Ws[ns],
                                            Us[ns])
             pk = outs.pop()
+            hb = e
             xt = outs[5 * (ns - 1) + 3] if pools[-1] else outs[5 * (ns - 1)]      # time4's input [T4, Mp, C]
             h4, g4, c4, logits, loss = ops.time4_head_fwd(xt, Ws[ns], Us[ns], bs[ns], pk, need, head, y, mask, int(M),
                                                           *[float(c) for c in consts], sums_, hist_)
@@ -470,7 +472,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
         ctx.params = params
         ctx.set_materialize_grads(False)     # (no zeros tensor for the non-differentiable logits)
         if need:
-            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs, h4, g4, c4, pk)
+            ctx.save_for_backward(x, y, mask, *Ws, *Us, *head, *outs, h4, g4, c4, pk, hb)
         ctx.mark_non_differentiable(logits)
         return loss.reshape(()), logits
 
@@ -485,7 +487,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
         Ws, Us = saved[3:4 + ns], saved[4 + ns:5 + 2 * ns]
         head = saved[5 + 2 * ns:11 + 2 * ns]
         outs = saved[11 + 2 * ns:11 + 7 * ns]
-        h4, g4, c4, pk = saved[11 + 7 * ns:]
+        h4, g4, c4, pk, hb = saved[11 + 7 * ns:]
         need = ctx.needs_input_grad
         npar = 3 * (ns + 1)
 
@@ -511,7 +513,7 @@ class _HipLSTMChainHead(torch.autograd.Function):
         if _t4_chain_on() and pools[-1] == 3 and xt.is_contiguous():
             # time4 + head backward as the first stage of the chain backward launch: the top
             # chain stage consumes time4's dx as it is produced
-            res = ops.lstm_chain_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], pk, list(head), y, mask, ctx.M, *ctx.consts,
+            res = ops.lstm_chain_head_bwd(g, xt, h4, g4, c4, Ws[ns], Us[ns], pk, hb, list(head), y, mask, ctx.M, *ctx.consts,
                                           [s for s, _ in hsinks], *chain_args)
             dz4 = res.pop(0)
         else:

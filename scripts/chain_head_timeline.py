@@ -61,12 +61,16 @@ def main():
         xs = st.x if hasattr(st, "x") else ids
         t = hip_ops().lstm_chain_trace(ids.float()).cpu()
         nt8, nsb = 8, 7
+        mid = t[512:768].double()
         tt = t[: 2 * nsb * nt8].view(nsb * nt8, 2).double()
         t0 = float(tt[:, 0][tt[:, 0] > 0].min())
         us = lambda v: round((float(v) - t0) / 100, 2)      # noqa: E731
         brows.append({"bwd_blocks_tile0": [{"block_row": k, "start_us": us(tt[k * nt8, 0]), "end_us": us(tt[k * nt8, 1])}
                                            for k in range(nsb)],
-                      "bwd_last_end_us": us(tt[:, 1].max())})
+                      "bwd_last_end_us": us(tt[:, 1].max()),
+                      # time4 + head backward workgroups (block rows 6): head backward done / reverse steps done
+                      "t4b_head_done_us": [us(mid[6 * nt8 + r]) for r in range(nt8)],
+                      "t4b_steps_done_us": [us(mid[64 + 6 * nt8 + r]) for r in range(nt8)]})
     for r in rows[-2:]:
         print(json.dumps(r), flush=True)
     for r in brows[-2:]:

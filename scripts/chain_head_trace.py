@@ -104,7 +104,7 @@ def main():
     print(json.dumps({"bwd": "chain6", "us": round(ub6, 2), "stages": stages(ops, x, 6, nt8, True)}), flush=True)
     # time4 + head backward as the first stage of the backward launch (lstm_chain_head_bwd);
     # stage 6 of the timeline is time4 (its blocks follow the six chain stages)
-    ubh = timeit(lambda: ops.lstm_chain_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg, *a6[1:]))
+    ubh = timeit(lambda: ops.lstm_chain_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, e, head, y, mask, M, *hc, hg, *a6[1:]))
     print(json.dumps({"bwd": "time4head+chain6", "us": round(ubh, 2), "stages": stages(ops, x, 7, nt8, True)}),
           flush=True)
     both = timeit(lambda: (ops.time4_head_fwd(xt, Ws[6], Us[6], bs[6], pk, True, head, y, mask, M, *hc, e.double(), e),

@@ -79,8 +79,9 @@ def main():
     # relative to compute wave 0's step start
     print(json.dumps({"launch": "fwd marks vs compute start", "stages": marks_rel(pf, 7)}), flush=True)
     h4, g4, c4, logits, loss = outs[-5:]
-    pk = outs[-6]
-    outs = outs[:-6]
+    hb = outs[-6]          # (the head backward the forward launch precomputed)
+    pk = outs[-7]
+    outs = outs[:-7]
     xt = outs[5 * 5 + 3]
     hg = [torch.zeros_like(p) for p in head]
     one = torch.ones(1, device=dev)
@@ -91,7 +92,7 @@ def main():
                   [Us[i] for i in order], [outs[5 * i + 4] if pools[i] else e8 for i in order],
                   [pools[i] for i in order], [xw[i] for i in order], [outs[5 * i].shape[0] for i in order])
     for _ in range(3):
-        ops.lstm_chain_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, head, y, mask, M, *hc, hg, *chain_args)
+        ops.lstm_chain_head_bwd(one, xt, h4, g4, c4, Ws[6], Us[6], pk, hb, head, y, mask, M, *hc, hg, *chain_args)
     torch.cuda.synchronize()
     pb = ops.lstm_chain_prof(x).cpu()
     # H = 16 stages (chain_bwd_stage_io) mark 0 top, 1 cell done, 2 after the barrier, 3 dh_rec ready,

@@ -187,3 +187,39 @@ def test_t4_chain_stage_matches_separate_launch(cuda_device, cml_windows, monkey
         le0, ze0 = model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0)
     torch.testing.assert_close(ze1, ze0, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(le1, le0, atol=1e-6, rtol=1e-5)
+
+
+def test_head_backward_precomputed_by_forward_launch(cuda_device, cml_windows, monkeypatch):
+    """The head backward run by the chain FORWARD launch (dL/dloss = 1, the backward scales dh_{T-1}
+    and the reduced head-gradient records by the real dL/dloss) == the head backward run at the start
+    of the backward launch: same code on the same values, so every gradient matches tightly; an
+    upstream gradient of 2.5 scales every gradient by 2.5 on the precomputed path."""
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    from gnnqc.utils.native import hip_ops
+    _, _, _, model, b = _setup(cuda_device, cml_windows)
+    inputs = b.model_inputs("cml")
+    monkeypatch.setenv("GNNQC_T4_CHAIN", "1")
+
+    def run(pre, scale=1.0):
+        monkeypatch.setenv("GNNQC_HEAD_BWD_IN_FWD", "1" if pre else "0")
+        for p in model.parameters():
+            p.grad = torch.zeros_like(p)
+        with direct_grad_accumulation(True):
+            loss, _ = model.fused_loss(inputs, b.y, b.y_mask, 1.0, 5.0)
+            loss.backward(torch.full((), scale, device=loss.device))
+        torch.cuda.synchronize()
+        return {n: p.grad.clone() for n, p in model.named_parameters()}
+
+    g0 = run(False)
+    g1 = run(True)
+    assert int(hip_ops().lstm_chain_status(b.y)[2].item()) == 0
+    for n in g0:
+        torch.testing.assert_close(g1[n], g0[n], atol=1e-7, rtol=1e-5, msg=n)
+    # dL/dloss = 2.5: the scaled dh_{T-1} / records vs the head backward with gl = 2.5 (fp32 products
+    # in a different order, then the same bf16 dz roundings: near-identical, compared by norm)
+    h0 = run(False, 2.5)
+    h1 = run(True, 2.5)
+    for n in h0:
+        err = (h1[n] - h0[n]).norm().item()
+        assert err <= 1e-4 * (h0[n].norm().item() + 1e-9), (n, err, h0[n].norm().item())
+        assert abs(h0[n].norm().item() - 2.5 * g0[n].norm().item()) <= 1e-2 * h0[n].norm().item() + 1e-9, n
