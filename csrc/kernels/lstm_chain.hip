@@ -217,14 +217,19 @@ __device__ __forceinline__ unsigned chain_tag_base(unsigned E) { return ((E % 0x
 // (stage 0) or from the previous stage's granule stream (SRC), the output also published as granules.
 // LDS of one stage (carved from the kernel's one buffer: the stage bodies must not each
 // reserve their own static arrays)
+#ifndef CHAIN_H64_CPL2
+#define CHAIN_H64_CPL2 1     // H = 64 forward stages: two cells per lane on 8 compute waves (see ChainCfg)
+#endif
 template <int H, int KX>
 struct ChainLds {
   static constexpr int HS = 2 * 16 * (TMC<H>::KPH + 8) * 2;
   static constexpr int XS = 2 * 16 * (32 * KX + 8) * 2;
   static constexpr int HF = 2 * 16 * TMC<H>::HP * 4;
-  // (stages with a publisher wave, H <= 32) the cells' packed gates and c of two steps
-  static constexpr int GS = H <= 32 ? 2 * TMC<H>::NT * 8 : 0;
-  static constexpr int CS = H <= 32 ? 2 * TMC<H>::NT * 4 : 0;
+  // (stages with a publisher wave: H <= 32, and H = 64 in its two-cells-per-lane layout) the cells'
+  // packed gates and c of two steps
+  static constexpr bool PUB = H <= 32 || CHAIN_H64_CPL2;
+  static constexpr int GS = PUB ? 2 * 16 * H * 8 : 0;
+  static constexpr int CS = PUB ? 2 * 16 * H * 4 : 0;
   static constexpr int BYTES = HS + XS + HF + GS + CS;
 };
 constexpr int chain_max2(int a, int b) { return a > b ? a : b; }
@@ -266,12 +271,24 @@ __host__ __device__ constexpr int chain_live_threads(int nt, int d, int kx, bool
                          pin) > 0 ? 64 : 0);
 }
 
+// Compute layout of a forward chain stage: one cell per lane (as TMC), except H = 64, which runs two
+// cells per lane on 8 compute waves so that the I/O waves and the publisher fit the 1024-thread
+// workgroup too (with 16 compute waves every thread streamed its own x granules and stored its own
+// outputs, and its loads waited behind its write-through stores). The saved gates / c keep the
+// one-cell-per-lane layout of the backward (cell (wave gi, lane), gi = compute wave + NW * cc).
+template <int H>
+struct ChainCfg {
+  static constexpr int CPL = (H == 64 && CHAIN_H64_CPL2) ? 2 : 1;
+  static constexpr int NW = H / 4 / CPL, NT = 64 * NW, G4 = 4 * H;
+  static constexpr int KSH = TMC<H>::KSH, KPH = TMC<H>::KPH, HP = TMC<H>::HP;
+  static constexpr int NWV = H / 4, NCELL = 64 * NWV;     // the saved-state layout's waves / cells per tile
+};
+
 template <int H, bool TRAIN, int KX, int D, bool SRC, int PIN>
 __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int ntiles, int Mp, unsigned tagb,
                                             int* ctl, char* smem) {
-  using C = TMC<H>;
-  constexpr int NW = C::NW, NT = C::NT, G4 = C::G4;
-  static_assert(C::CPL == 1, "chain stages run one cell per lane");
+  using C = ChainCfg<H>;
+  constexpr int NW = C::NW, NT = C::NT, G4 = C::G4, CPL = C::CPL, NWV = C::NWV, NCELL = C::NCELL;
   constexpr int KPX = 32 * KX;
   // elements per streamed granule: stage 0 reads float4 of x; a stream consumer reads two adjacent
   // 8-byte {value, tag} granules with one 16-byte load (each half is one whole granule)
@@ -289,8 +306,8 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   auto hs = reinterpret_cast<__bf16 (*)[16][C::KPH + 8]>(smem);
   auto xs = reinterpret_cast<__bf16 (*)[16][KPX + 8]>(smem + L::HS);
   auto hf = reinterpret_cast<float (*)[16][C::HP]>(smem + L::HS + L::XS);
-  auto gst = reinterpret_cast<uint2 (*)[NT]>(smem + L::HS + L::XS + L::HF);               // [2][NT] (IOW)
-  auto cst = reinterpret_cast<float (*)[NT]>(smem + L::HS + L::XS + L::HF + L::GS);      // [2][NT] (IOW)
+  auto gst = reinterpret_cast<uint2 (*)[NCELL]>(smem + L::HS + L::XS + L::HF);            // [2][cells] (IOW)
+  auto cst = reinterpret_cast<float (*)[NCELL]>(smem + L::HS + L::XS + L::HF + L::GS);   // [2][cells] (IOW)
 
   const int T = S.T, Din = S.Din, Dw = S.Dw, P = S.P;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -425,42 +442,57 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
 
   // ---- compute role: fragments of the pre-scaled gate weights, one cell (unit, sequence) per lane
   const int wc = compute ? w : 0;
-  const int au = 4 * wc + (col >> 2), ag = col & 3;
-  const int unit = 4 * wc + quad;
-  bf16x8_t ufr[C::KSH], wfr[KX];
-  f32x4_t bias4 = {0.f, 0.f, 0.f, 0.f};
-  if (compute) {
+  const int ag = col & 3;
+  int unit[CPL];
+  bf16x8_t ufr[CPL][C::KSH], wfr[CPL][KX];
+  f32x4_t bias4[CPL];
 #pragma unroll
-    for (int s = 0; s < C::KSH; ++s) {
-      bf16x8_t v;
+  for (int cc = 0; cc < CPL; ++cc) {
+    const int gi = wc + NW * cc;                 // (the cell group: a one-cell-per-lane wave)
+    const int au = 4 * gi + (col >> 2);
+    unit[cc] = 4 * gi + quad;
+    bias4[cc] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (compute) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 32 * s + 8 * quad + j;
-        v[j] = (__bf16)(S.U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+      for (int s = 0; s < C::KSH; ++s) {
+        bf16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * s + 8 * quad + j;
+          v[j] = (__bf16)(S.U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+        }
+        ufr[cc][s] = v;
       }
-      ufr[s] = v;
-    }
 #pragma unroll
-    for (int s = 0; s < KX; ++s) {
-      bf16x8_t v;
+      for (int s = 0; s < KX; ++s) {
+        bf16x8_t v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 32 * s + 8 * quad + j;
-        v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * s + 8 * quad + j;
+          v[j] = (__bf16)(S.W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
+        }
+        wfr[cc][s] = v;
       }
-      wfr[s] = v;
+      const int u = unit[cc];
+      bias4[cc] = f32x4_t{S.b[u], S.b[H + u], S.b[2 * H + u], S.b[3 * H + u]};
     }
-    bias4 = f32x4_t{S.b[unit], S.b[H + unit], S.b[2 * H + unit], S.b[3 * H + unit]};
   }
-  // this lane's output element (sequence row0 + col, unit) in the [T][Mp][H] streams
-  const size_t hoff = (size_t)(row0 + col) * H + unit;
-  float* hp = S.h + hoff;
-  unsigned long long* sp = S.sout != nullptr ? S.sout + hoff : nullptr;
+  // this lane's output elements (sequence row0 + col, unit) in the [T][Mp][H] streams
+  float* hp[CPL];
+  unsigned long long* sp[CPL];
+  __bf16* gp[CPL];
+  float* cp[CPL];
+  const size_t gstride = (size_t)ntiles * NWV * 64;
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) {
+    const size_t hoff = (size_t)(row0 + col) * H + unit[cc];
+    hp[cc] = S.h + hoff;
+    sp[cc] = S.sout != nullptr ? S.sout + hoff : nullptr;
+    gp[cc] = S.g + (((size_t)tile * NWV + wc + NW * cc) * 64 + lane) * 4;
+    cp[cc] = S.c + ((size_t)tile * NWV + wc + NW * cc) * 64 + lane;
+  }
   const bool publish = S.sout != nullptr;
   const bool own_pool = P > 0;
-  const size_t gstride = (size_t)ntiles * NW * 64;
-  __bf16* gp = S.g + (((size_t)tile * NW + wc) * 64 + lane) * 4;
-  float* cp = S.c + ((size_t)tile * NW + wc) * 64 + lane;
 
   // ---- a last stage that pools its own output: the pooling lanes (I/O wave 0, or the first 16 H / 4
   // threads) own float4 granules of the [16][H] tile
@@ -503,7 +535,9 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
     stage_x(0, 0, 0);
     if (!IOW || !CHAIN_DEFER_LD) load_x(0, min(D, T - 1));
   }
-  float c = 0.f;
+  float c[CPL];
+#pragma unroll
+  for (int cc = 0; cc < CPL; ++cc) c[cc] = 0.f;
   __syncthreads();
 
   long long* pr = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
@@ -512,47 +546,56 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
     constexpr bool DOI = decltype(IO)::value;
     const int p = t & 1;
     chain_mark(pr, t, 0);
-    f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc[CPL];
 #pragma unroll
-    for (int s = 0; s < KX; ++s) {
-      const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
-      accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[s], bx, accx, 0, 0, 0);
-    }
+    for (int cc = 0; cc < CPL; ++cc) {
+      f32x4_t accx = bias4[cc], acch = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < C::KSH; ++s) {
-      const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
-      acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[s], bh, acch, 0, 0, 0);
+      for (int s = 0; s < KX; ++s) {
+        const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xs[p][col][32 * s + 8 * quad]);
+        accx = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[cc][s], bx, accx, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < C::KSH; ++s) {
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hs[p][col][32 * s + 8 * quad]);
+        acch = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][s], bh, acch, 0, 0, 0);
+      }
+      acc[cc] = accx + acch;
     }
-    const f32x4_t a = accx + acch;
     chain_mark(pr, t, 1);
     if constexpr (DOI) {                 // (H = 64: every thread also streams x through its ring)
       stage_x(p ^ 1, rn, min(t + 1, T - 1));
       load_x(rn, min(t + 1 + D, T - 1));
     }
-    const float iv = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(0) * a[0]));
-    const float fv = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(1) * a[1]));
-    const float gv = 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(2) * a[2])) - 1.0f;
-    const float ov = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(3) * a[3]));
-    c = fv * c + iv * gv;
-    const float rc = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.8853900817779268f * c));
-    const float hv = (2.0f * ov) * rc - ov;            // o tanh(c)
-    hs[p ^ 1][col][unit] = (__bf16)hv;
-    // the granule that publishes h_t goes out at once, from registers (write-through: the consumer
-    // polls it); the bulk outputs (h, packed gates, c) are staged in LDS for the publisher wave, whose
-    // wide contiguous stores keep the CU's vector-memory path free for the consumer-side loads
-    if (publish) st_granule(sp + (size_t)t * hstep, hv, tagb | (unsigned)t);
-    if constexpr (IOW) {
-      hf[p][col][unit] = hv;
-      if constexpr (TRAIN) {
-        gst[p][wc * 64 + lane] = gates_pack(iv, fv, gv, ov);
-        cst[p][wc * 64 + lane] = c;
-      }
-    } else {
-      if (own_pool) hf[p][col][unit] = hv;
-      hp[(size_t)t * hstep] = hv;
-      if constexpr (TRAIN) {
-        *reinterpret_cast<uint2*>(gp + (size_t)t * gstride * 4) = gates_pack(iv, fv, gv, ov);
-        cp[(size_t)t * gstride] = c;
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) {
+      const f32x4_t a = acc[cc];
+      const int u = unit[cc], cell = (wc + NW * cc) * 64 + lane;
+      const float iv = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(0) * a[0]));
+      const float fv = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(1) * a[1]));
+      const float gv = 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(2) * a[2])) - 1.0f;
+      const float ov = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(chain_gate_scale(3) * a[3]));
+      c[cc] = fv * c[cc] + iv * gv;
+      const float rc = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.8853900817779268f * c[cc]));
+      const float hv = (2.0f * ov) * rc - ov;            // o tanh(c)
+      hs[p ^ 1][col][u] = (__bf16)hv;
+      // the granule that publishes h_t goes out at once, from registers (write-through: the consumer
+      // polls it); the bulk outputs (h, packed gates, c) are staged in LDS for the publisher wave, whose
+      // wide contiguous stores keep the CU's vector-memory path free for the consumer-side loads
+      if (publish) st_granule(sp[cc] + (size_t)t * hstep, hv, tagb | (unsigned)t);
+      if constexpr (IOW) {
+        hf[p][col][u] = hv;
+        if constexpr (TRAIN) {
+          gst[p][cell] = gates_pack(iv, fv, gv, ov);
+          cst[p][cell] = c[cc];
+        }
+      } else {
+        if (own_pool) hf[p][col][u] = hv;
+        hp[cc][(size_t)t * hstep] = hv;
+        if constexpr (TRAIN) {
+          *reinterpret_cast<uint2*>(gp[cc] + (size_t)t * gstride * 4) = gates_pack(iv, fv, gv, ov);
+          cp[cc][(size_t)t * gstride] = c[cc];
+        }
       }
     }
     chain_mark(pr, t, 2);
@@ -569,12 +612,12 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
       *reinterpret_cast<float4*>(S.h + tile_off + e) = *reinterpret_cast<const float4*>(&hf[pb][e / H][e % H]);
     }
     if constexpr (TRAIN) {
-      const size_t cell0 = ((size_t)tp * ntiles + tile) * NW * 64;     // this tile's cells of step tp
+      const size_t cell0 = ((size_t)tp * ntiles + tile) * NCELL;      // this tile's cells of step tp
 #pragma unroll
-      for (int q = lane; q < NT / 2; q += 64)
+      for (int q = lane; q < NCELL / 2; q += 64)
         *reinterpret_cast<uint4*>(S.g + (cell0 + 2 * q) * 4) = *reinterpret_cast<const uint4*>(&gst[pb][2 * q]);
 #pragma unroll
-      for (int q = lane; q < NT / 4; q += 64)
+      for (int q = lane; q < NCELL / 4; q += 64)
         *reinterpret_cast<float4*>(S.c + cell0 + 4 * q) = *reinterpret_cast<const float4*>(&cst[pb][4 * q]);
     }
     if (own_pool) pool_step(tp);
@@ -868,7 +911,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const bool src = s > 0;
 #define GQ_CHAIN_BODY(HH, KXX, DD, SRCV, PINV)                                          \
   {                                                                                     \
-    if (threadIdx.x >= chain_live_threads(TMC<HH>::NT, DD, KXX, SRCV, PINV)) return;   \
+    if (threadIdx.x >= chain_live_threads(ChainCfg<HH>::NT, DD, KXX, SRCV, PINV)) return; \
     chain_stage<HH, TRAIN, KXX, DD, SRCV, PINV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
   }
 #ifdef CHAIN_KX1_ONLY      // (A/B probe: no 33-64-channel stage bodies in the kernel; such chains fail)
