@@ -190,14 +190,21 @@ struct ChainHeadFwdLds {
 // Forward of the 16 rows of `tile` from hl [16][F + 4] (LDS).
 // (hd by value: a reference into a kernel's by-value argument struct makes the compiler copy the
 // whole struct to scratch)
+// staged: the weight images at ch_head_fwd_weights(scratch) were loaded earlier (ch_stage_weights,
+// e.g. while the chain's time4 stage still waited for its input)
 template <int F>
-__device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int ntiles, const float* hl, char* scratch) {
+__device__ __forceinline__ float* ch_head_fwd_weights(char* scratch) {
+  return reinterpret_cast<float*>(scratch) + 3 * 16 * CH_AP + 16 * 8;
+}
+template <int F>
+__device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int ntiles, const float* hl, char* scratch,
+                                               bool staged = false) {
   float* part = reinterpret_cast<float*>(scratch);    // [2][16][CH_AP]
   float* sa1 = part + 2 * 16 * CH_AP;                 // [16][CH_AP]
   float* rowv = sa1 + 16 * CH_AP;                     // [16][8]
   float* sW1 = rowv + 16 * 8;                         // [F][CH_WP]
   float* sW2 = sW1 + F * CH_WP;                       // [64][CH_WP]
-  ch_stage_weights<F>(hd, sW1, sW2);
+  if (!staged) ch_stage_weights<F>(hd, sW1, sW2);
   const int tid = threadIdx.x, w = tid >> 6, j = tid & 63;
   const float w3j = hd.W3[j], b3 = hd.b3[0];
   float yy[2], mm[2];
@@ -278,7 +285,8 @@ struct ChainHeadBwdLds {
 template <int F>
 __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* __restrict__ hT, int tile, int ntiles,
                                                float* dh, char* scratch, int hld = -1, bool unit_gl = false,
-                                               bool count = true, int nlive = 0) {
+                                               bool count = true, int nlive = 0, const float* pW1 = nullptr,
+                                               const float* pW2 = nullptr) {
   constexpr int HLP = F + 4, PT = 16 * CH_AP;
   using Rec = ChainHeadRec<F>;
   float* sh = reinterpret_cast<float*>(scratch);     // [16][HLP]
@@ -289,9 +297,10 @@ __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* 
   float* sad = sz2 + PT;                             // [16][CH_AP] leaky(z2) * d
   float* sdz1 = sad + PT;                            // [16][CH_AP] dz1
   float* misc = sdz1 + PT;                           // [32]: d per row, mask-sum reduction
-  float* sW1 = misc + 32;                            // [F][CH_WP]
-  float* sW2 = sW1 + F * CH_WP;                      // [64][CH_WP]
-  ch_stage_weights<F>(hd, sW1, sW2);
+  // (pW1 / pW2: images already staged by the caller, e.g. the forward's head)
+  float* sW1 = pW1 != nullptr ? const_cast<float*>(pW1) : misc + 32;   // [F][CH_WP]
+  float* sW2 = pW2 != nullptr ? const_cast<float*>(pW2) : sW1 + F * CH_WP;   // [64][CH_WP]
+  if (pW1 == nullptr) ch_stage_weights<F>(hd, sW1, sW2);
   const int tid = ch_tid(), w = tid >> 6, j = tid & 63;
   const int l = tid & 63, lm = l & 15, lq = l >> 4;
   const int row0 = tile * 16;

@@ -80,6 +80,9 @@ static constexpr int CHAIN_SPIN = 1 << 20;
 #ifndef CHAIN_RP_NAPMAX
 #define CHAIN_RP_NAPMAX 16   // bulk re-poll of a stale tile: largest nap (s_sleep 2 units) between rounds
 #endif
+#ifndef CHAIN_H64_CPL2
+#define CHAIN_H64_CPL2 1     // H = 64 forward stages: two cells per lane on 8 compute waves (see ChainCfg)
+#endif
 #ifndef CHAIN_PRIO
 #define CHAIN_PRIO 2         // s_setprio of the compute waves of a stage with I/O waves
 #endif
@@ -217,9 +220,6 @@ __device__ __forceinline__ unsigned chain_tag_base(unsigned E) { return ((E % 0x
 // (stage 0) or from the previous stage's granule stream (SRC), the output also published as granules.
 // LDS of one stage (carved from the kernel's one buffer: the stage bodies must not each
 // reserve their own static arrays)
-#ifndef CHAIN_H64_CPL2
-#define CHAIN_H64_CPL2 1     // H = 64 forward stages: two cells per lane on 8 compute waves (see ChainCfg)
-#endif
 template <int H, int KX>
 struct ChainLds {
   static constexpr int HS = 2 * 16 * (TMC<H>::KPH + 8) * 2;
@@ -260,14 +260,23 @@ __host__ __device__ constexpr int chain_io_waves(int nt, int d, int ngl = 1, int
   return nt + 64 * d + 64 <= 1024 && ngl * pin <= 12 ? d : 0;   // (+ the publisher wave)
 }
 // a pooling consumer (pin = 3 granules per element) splits each step's tile over two I/O waves
-__host__ __device__ constexpr int chain_io_group(int pin) { return pin > 1 ? 2 : 1; }
+// (and so does a 64-channel input of an H = 64 stage, 8 granule pairs per lane in one wave: its I/O
+// waves' registers spilled; with two waves per step the ring is 3 steps deep to fit the workgroup)
+__host__ __device__ constexpr int chain_io_group(int pin, int kx = 1, int h = 16) {
+  return pin > 1 || (h == 64 && kx == 2 && CHAIN_H64_CPL2) ? 2 : 1;
+}
+__host__ __device__ constexpr int chain_stage_d(int h, int kx, int d) {
+  return h == 64 && kx == 2 && CHAIN_H64_CPL2 && d > 3 ? 3 : d;
+}
 // threads of a stage workgroup that run the stage (compute + I/O waves + the publisher)
-__host__ __device__ constexpr int chain_live_threads(int nt, int d, int kx, bool src, int pin) {
-  return nt + 64 * chain_io_waves(nt, d * chain_io_group(pin),
-                                  (16 * 32 * kx / (src ? 2 : 4) + 64 * chain_io_group(pin) - 1) / (64 * chain_io_group(pin)),
+__host__ __device__ constexpr int chain_live_threads(int nt, int d, int kx, bool src, int pin, int h = 16) {
+  return nt + 64 * chain_io_waves(nt, d * chain_io_group(pin, kx, h),
+                                  (16 * 32 * kx / (src ? 2 : 4) + 64 * chain_io_group(pin, kx, h) - 1) /
+                                      (64 * chain_io_group(pin, kx, h)),
                                   pin) +
-         (chain_io_waves(nt, d * chain_io_group(pin),
-                         (16 * 32 * kx / (src ? 2 : 4) + 64 * chain_io_group(pin) - 1) / (64 * chain_io_group(pin)),
+         (chain_io_waves(nt, d * chain_io_group(pin, kx, h),
+                         (16 * 32 * kx / (src ? 2 : 4) + 64 * chain_io_group(pin, kx, h) - 1) /
+                             (64 * chain_io_group(pin, kx, h)),
                          pin) > 0 ? 64 : 0);
 }
 
@@ -293,7 +302,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
   // elements per streamed granule: stage 0 reads float4 of x; a stream consumer reads two adjacent
   // 8-byte {value, tag} granules with one 16-byte load (each half is one whole granule)
   constexpr int GR = SRC ? 2 : 4;
-  constexpr int G = chain_io_group(PIN);         // I/O waves sharing one step's tile
+  constexpr int G = chain_io_group(PIN, KX, H);  // I/O waves sharing one step's tile
   constexpr int NIOW = chain_io_waves(NT, D * G, (16 * KPX / GR + 64 * G - 1) / (64 * G), PIN);   // (0: none)
   constexpr bool IOW = NIOW > 0;
   constexpr int NIO = IOW ? 64 * G : NT;         // threads streaming one step's tile
@@ -696,8 +705,10 @@ struct ChainT4Lds {
   static constexpr int XS = 2 * 16 * (64 + 8) * 2;        // bf16 x_t (double buffer)
   static constexpr int HL = 16 * (128 + 4) * 4;           // fp32 h_{T-1} for the head
   static constexpr int DHT = 16 * (128 + 4) * 4;          // precomputed head backward: dh_{T-1}
-  static constexpr int HF = ChainHeadFwdLds<128>::BYTES, HB = DHT + ChainHeadBwdLds<128>::BYTES;
-  static constexpr int BYTES = HS + XS + HL + (HF > HB ? HF : HB);
+  // (the head backward's dh tile and scratch follow the head forward's, whose weight images it reuses)
+  static constexpr int HF = ChainHeadFwdLds<128>::BYTES;
+  static constexpr int HB = DHT + ChainHeadBwdLds<128>::BYTES - (128 + CH_HU) * CH_WP * 4;   // (no weight images)
+  static constexpr int BYTES = HS + XS + HL + HF + HB;
 };
 
 template <bool TRAIN>
@@ -767,9 +778,23 @@ __device__ __forceinline__ void chain_t4_stage(const ChainT4 Q, int tile, int nt
 #pragma unroll
     for (int r = 0; r < 3; ++r) bad |= (unsigned)(xq[r] >> 32) != (tagb | (unsigned)(3 * tx + r));
     if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+      // re-poll all three granules at once, inline (a call to chain_wait here made the compiler keep
+      // live registers in scratch around it: two scratch reloads in every step of this loop)
+      const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int lim = lim0 > 0 ? lim0 : CHAIN_SPIN;
+      for (int it = 0;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
-        xq[r] = chain_wait(Q.xin + xoff + (size_t)(3 * tx + r) * xstep, tagb | (unsigned)(3 * tx + r), ctl);
+        for (int r = 0; r < 3; ++r) xq[r] = ld_granule(Q.xin + xoff + (size_t)(3 * tx + r) * xstep);
+        bad = false;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) bad |= (unsigned)(xq[r] >> 32) != (tagb | (unsigned)(3 * tx + r));
+        if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
+        if (it >= lim) {
+          __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
     }
     float m = __uint_as_float((unsigned)xq[0]);
     unsigned arg = 0;
@@ -863,22 +888,31 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
         if (r < A.ntiles) {
           if (threadIdx.x == 0) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
           const unsigned tagb = chain_tag_base((unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          // the head's weight images go to LDS first: this workgroup then waits ~60 us for its first
+          // input anyway (the chain's stages are all far behind), and the head runs right after the
+          // last time4 step
+          constexpr int HOFF = ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL;
+          float* hW1 = ch_head_fwd_weights<128>(smem + HOFF);
+          ch_stage_weights<128>(A.t4.hd, hW1, hW1 + 128 * CH_WP);
           chain_t4_stage<TRAIN>(A.t4, r, A.ntiles, A.Mp, tagb, A.ctl, smem);
+          long long* mk = blockIdx.x < 64 ? A.trace + 512 + blockIdx.x : nullptr;   // (trace: phase ends)
+          if (mk != nullptr && threadIdx.x == 0) mk[0] = (long long)__builtin_amdgcn_s_memrealtime();
           if (threadIdx.x >= 64 * CH_NW) return;    // the head runs on 8 waves (the rest exit)
           chain_head_fwd<128>(A.t4.hd, r, A.ntiles, reinterpret_cast<const float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS),
-                              smem + ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL);
+                              smem + HOFF, true);
+          if (mk != nullptr && threadIdx.x == 0) mk[64] = (long long)__builtin_amdgcn_s_memrealtime();
           if constexpr (TRAIN) {
             if (A.t4.hb != nullptr) {
               // the head backward, here instead of at the start of the backward launch (it only needs
               // this launch's outputs; dL/dloss = 1, scaled there): the backward's time4 stage then
               // starts its reverse steps at once (the head backward was ~12 us of its critical path)
-              __syncthreads();                       // the head forward's scratch is free
-              constexpr int OFF = ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL;
+              __syncthreads();
+              constexpr int OFF = HOFF + ChainT4Lds::HF;   // (after the head forward's scratch and weights)
               float* dhs = reinterpret_cast<float*>(smem + OFF);
               ChainHead hb = A.t4.hd;
               hb.gpart = A.t4.hb + (size_t)A.ntiles * 16 * 128;
               chain_head_bwd<128>(hb, reinterpret_cast<const float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS), r, A.ntiles,
-                                  dhs, smem + OFF + ChainT4Lds::DHT, 132, true, false, CH_NW);
+                                  dhs, smem + OFF + ChainT4Lds::DHT, 132, true, false, CH_NW, hW1, hW1 + 128 * CH_WP);
               for (int e = ch_tid(); e < 16 * 128; e += 64 * CH_NW)
                 A.t4.hb[((size_t)r * 16 + e / 128) * 128 + e % 128] = dhs[(e / 128) * 132 + e % 128];
             }
@@ -911,8 +945,9 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   const bool src = s > 0;
 #define GQ_CHAIN_BODY(HH, KXX, DD, SRCV, PINV)                                          \
   {                                                                                     \
-    if (threadIdx.x >= chain_live_threads(ChainCfg<HH>::NT, DD, KXX, SRCV, PINV)) return; \
-    chain_stage<HH, TRAIN, KXX, DD, SRCV, PINV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
+    constexpr int DS = chain_stage_d(HH, KXX, DD);                                      \
+    if (threadIdx.x >= chain_live_threads(ChainCfg<HH>::NT, DS, KXX, SRCV, PINV, HH)) return; \
+    chain_stage<HH, TRAIN, KXX, DS, SRCV, PINV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
   }
 #ifdef CHAIN_KX1_ONLY      // (A/B probe: no 33-64-channel stage bodies in the kernel; such chains fail)
 #define GQ_CHAIN_SRC(HH, PINV, DD) if (KX == 1) GQ_CHAIN_BODY(HH, 1, DD, true, PINV)

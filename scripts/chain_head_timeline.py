@@ -44,8 +44,12 @@ def main():
         tt = t[: 2 * blocks].view(blocks, 2).double()
         t0 = float(tt[:, 0][tt[:, 0] > 0].min())
         us = lambda v: round((float(v) - t0) / 100, 2)      # noqa: E731
+        mid = t[512:768].double()
         rows.append({"stages": [{"stage": s, "start_us": us(tt[s * nt8, 0]), "end_us": us(tt[s * nt8, 1])}
                                 for s in range(ns)],
+                     # time4 workgroups: reverse... forward steps done / head forward done
+                     "t4_steps_done_us": [us(mid[ns * nt8 + r]) for r in range(nt8)],
+                     "t4_head_fwd_done_us": [us(mid[64 + ns * nt8 + r]) for r in range(nt8)],
                      "t4_head_end_us": [us(tt[ns * nt8 + r, 1]) for r in range(nt8)],
                      "t4_head_start_us": us(tt[ns * nt8, 0])})
         return orig(ctx, *a)
