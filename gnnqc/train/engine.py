@@ -127,6 +127,8 @@ class Trainer:
         self.graph_steps = max(1, int(os.environ.get("GNNQC_GRAPH_STEPS", "8")))
         self.multi_graph = None
         self._multi_key = None
+        self.multi_graph1 = None            # (one-step graph of the same form: leftover steps)
+        self._multi_key1 = None
         self._table = None
         self._cursor = torch.zeros(1, dtype=torch.long, device=self.device)
         self._graph_loss = None
@@ -285,9 +287,13 @@ class Trainer:
         self.opt.zero_grad()
         return 1e3 * sum(a.elapsed_time(b) for a, b in ev) / n
 
-    def _capture_multi(self, nrows: int):
+    def _capture_multi(self, nrows: int, steps: int = 0):
         """Capture ``graph_steps`` full training steps (gather -> forward -> backward -> guarded
-        Adam, which advances the device cursor) as ONE graph over the static table [nrows, B]."""
+        Adam, which advances the device cursor) as ONE graph over the static table [nrows, B].
+        ``steps=1``: the one-step graph of the same form (``multi_graph1``), which replays the
+        leftover steps of a run that is not a multiple of ``graph_steps`` from the same table and
+        cursor (the single-step graph's host id copy and launch gap cost ~10 us a step)."""
+        one = steps == 1
         from ..data.store import CursorIds
         snap = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
         ids = CursorIds(self._table, self._cursor)
@@ -300,15 +306,15 @@ class Trainer:
                     self._reduce_grads()          # (communicator + RCCL state warm before capture)
         torch.cuda.current_stream().wait_stream(s)
         self.opt.zero_grad()
-        self.multi_graph = torch.cuda.CUDAGraph()
+        graph = torch.cuda.CUDAGraph()
         it0 = self.opt.iterations
         self.opt.cursor, self.opt.cursor_mod = self._cursor, nrows
         # (thread-local capture mode: the process group's watchdog thread keeps polling its own
         # events while this thread captures)
         kw = {"capture_error_mode": "thread_local"} if self.dp_graph else {}
         try:
-            with torch.cuda.graph(self.multi_graph, **kw):
-                for _ in range(self.graph_steps):
+            with torch.cuda.graph(graph, **kw):
+                for _ in range(1 if one else self.graph_steps):
                     if self.dp_graph:
                         self._body(ids, with_opt=False)
                         self._reduce_grads()
@@ -318,8 +324,12 @@ class Trainer:
         finally:
             self.opt.cursor, self.opt.cursor_mod = None, 1
         self.opt.iterations = it0
-        self._multi_loss = self.last_loss
-        self._multi_key = (nrows, self._table.shape[1])
+        if one:
+            self.multi_graph1, self._multi_loss1 = graph, self.last_loss
+            self._multi_key1 = (nrows, self._table.shape[1])
+        else:
+            self.multi_graph, self._multi_loss = graph, self.last_loss
+            self._multi_key = (nrows, self._table.shape[1])
         with torch.no_grad():
             for k, v in self.model.state_dict().items():
                 v.copy_(snap[k])
@@ -336,10 +346,12 @@ class Trainer:
         if self._multi_ok():
             if self._table is None or tuple(self._table.shape) != tuple(rows.shape):
                 self._table = torch.empty_like(rows, dtype=torch.long)
-                self.multi_graph = None
+                self.multi_graph = self.multi_graph1 = None
             self._table.copy_(rows)
             if self.multi_graph is None or self._multi_key != (int(rows.shape[0]), rows.shape[1]):
                 self._capture_multi(int(rows.shape[0]))
+            if self.multi_graph1 is None or self._multi_key1 != (int(rows.shape[0]), rows.shape[1]):
+                self._capture_multi(int(rows.shape[0]), steps=1)
 
     def train_steps(self, rows: torch.Tensor, start: int, k: int):
         """``k`` training steps on batches ``rows[(start + i) % len(rows)]`` (rows: [n, B] device
@@ -347,6 +359,18 @@ class Trainer:
         the rest (and every step when fault injection or DP is on) go through :meth:`train_step`."""
         nb = int(rows.shape[0])
         S = self.graph_steps
+        one_ok = (self.multi_graph1 is not None and self._multi_ok() and self._table is not None
+                  and tuple(self._table.shape) == tuple(rows.shape) and self._multi_key1 == (nb, rows.shape[1]))
+        if k < S and one_ok:                 # (prepare_graphs captured the one-step form)
+            self.model.train()
+            self._table.copy_(rows, non_blocking=True)
+            self._cursor.fill_(start % nb)
+            for _ in range(k):
+                self.multi_graph1.replay()
+            self.opt.iterations += k
+            self.global_step += k
+            self.last_loss = self._multi_loss1
+            return self.last_loss
         if not self._multi_ok() or k < S:
             for i in range(k):
                 self.train_step(rows[(start + i) % nb])
@@ -354,7 +378,8 @@ class Trainer:
         self.model.train()
         if self._table is None or tuple(self._table.shape) != tuple(rows.shape):
             self._table = torch.empty_like(rows, dtype=torch.long)
-            self.multi_graph = None
+            self.multi_graph = self.multi_graph1 = None
+            one_ok = False
         if self.multi_graph is not None and self._multi_key != (nb, rows.shape[1]):
             self.multi_graph = None
         self._table.copy_(rows, non_blocking=True)
@@ -369,6 +394,13 @@ class Trainer:
         self.opt.iterations += n * S
         self.global_step += n * S
         self.last_loss = self._multi_loss
+        if k > n * S and one_ok:             # leftover steps: the one-step graph, same table and cursor
+            for _ in range(k - n * S):
+                self.multi_graph1.replay()
+            self.opt.iterations += k - n * S
+            self.global_step += k - n * S
+            self.last_loss = self._multi_loss1
+            return self.last_loss
         for i in range(n * S, k):
             self.train_step(rows[(start + i) % nb])
         return self.last_loss

@@ -47,7 +47,7 @@ def test_batch_gather_cursor_rows(cuda_device, cml_windows):
         assert torch.equal(getattr(got, name), getattr(ref, name)), name
 
 
-def _multi_vs_single_run(steps, st, pc, mc, rows, dev, monkeypatch):
+def _multi_vs_single_run(steps, st, pc, mc, rows, dev, monkeypatch, k=16, prepare=False):
     from gnnqc.models import GCNClassifier
     from gnnqc.ops.optim import make_optimizer
     from gnnqc.train.engine import Trainer
@@ -56,7 +56,10 @@ def _multi_vs_single_run(steps, st, pc, mc, rows, dev, monkeypatch):
     model = GCNClassifier(mc, pc).to(dev)
     opt = make_optimizer("adam", model.parameters(), 1e-3)
     tr = Trainer(model, st, opt, {0: 1.0, 1: 5.0}, use_graph=True, batch_size=32)
-    tr.train_steps(rows, 3, 16)
+    if prepare:
+        tr.prepare_graphs(rows)
+        assert (tr.multi_graph1 is not None) == (steps > 1)
+    tr.train_steps(rows, 3, k)
     torch.cuda.synchronize()
     assert (tr.multi_graph is not None) == (steps > 1)
     bufs = torch.cat([b.reshape(-1).double() for b in model.buffers() if b.is_floating_point()])
@@ -88,3 +91,24 @@ def test_multi_step_graph_matches_single_steps(cuda_device, cml_windows, monkeyp
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
     assert abs(a[4] - b[4]) <= 1e-4 * abs(b[4]) + 1e-6
     assert a[5:] == b[5:] == (16, 16)
+
+
+def test_leftover_steps_replay_the_one_step_graph(cuda_device, cml_windows, monkeypatch):
+    """11 steps with prepared graphs = one 8-step replay + three replays of the one-step graph of
+    the same form (same device table and cursor, no host id copies) == 11 single-step replays."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceLoader, DeviceStore
+    from gnnqc.ops import set_deterministic
+    pc, ws = cml_windows
+    mc = C.default("model_cml")
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    rows = DeviceLoader(st, list(range(st.n_windows)), 32, shuffle=True, seed=1).batch_ids()
+    prev = set_deterministic(True)
+    try:
+        a, b = [_multi_vs_single_run(steps, st, pc, mc, rows, cuda_device, monkeypatch, k=11, prepare=True)
+                for steps in (8, 1)]
+    finally:
+        set_deterministic(prev)
+    for x, y in zip(a[:4], b[:4]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+    assert a[5:] == b[5:] == (11, 11)
