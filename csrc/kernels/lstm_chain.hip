@@ -1141,11 +1141,24 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
           if (k >= Din) { k -= Din; ++row; }
         }
       };
+      // ... and the step's dz tile (16-byte stores from LDS; zs[s & 1] holds it from the barrier
+      // that follows step s's cell phase until the cell phase of step s + 2): the compute waves then
+      // issue only loads, so their waits are for their own loads alone
+      auto store_dz = [&](int ss) {
+        const int pb = ss & 1;
+        __bf16* zt = S.dz + ((size_t)(T - 1 - ss) * Mp + row0) * G4;
+#pragma unroll
+        for (int q = lane; q < 16 * G4 / 8; q += 64) {
+          const int e = 8 * q;
+          *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][e % G4]);
+        }
+      };
       __syncthreads();
       __syncthreads();
       if constexpr (SK) {            // two barriers per step; step s's dx tile is complete after the second
         for (int s = 0; s < nsteps; ++s) {
           lds_barrier();
+          if (s < T) store_dz(s);
           lds_barrier();
           if (s < T) publish(s & 1, T - 1 - s);
         }
@@ -1154,6 +1167,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         for (int s = 0; s < nsteps; ++s) {
           lds_barrier();
           const int t = T - 1 - s;
+          if (s < T) store_dz(s);
           if (s >= 1 && s <= T) publish((s - 1) & 1, t + 1);
         }
         __syncthreads();
@@ -1389,7 +1403,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
 #endif
       }
       chain_mark(pr, s, 4);
-      {   // dz tile -> HBM (weight-gradient pass)
+      if constexpr (!PUBW) {   // dz tile -> HBM (weight-gradient pass; else the publisher stores it)
         const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][gz_c]);
         const int tz = t >= 0 ? t : T;
         *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
