@@ -73,6 +73,22 @@ class MetricAccumulator:
         return {prefix + k: v for k, v in out.items()}
 
 
+def _graph_upload(graph) -> bool:
+    """hipGraphUpload of a captured graph's executable on the current stream: the first replay of a
+    graph otherwise pays the upload of its command buffers (done here, outside any timed region).
+    False when the runtime or the executable handle is not available (no effect then)."""
+    if graph is None or not torch.cuda.is_available():
+        return False
+    try:
+        import ctypes
+        exe = graph.raw_cuda_graph_exec()
+        lib = ctypes.CDLL("libamdhip64.so")
+        rc = lib.hipGraphUpload(ctypes.c_void_p(int(exe)), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        return rc == 0
+    except Exception:         # (older torch / no HIP runtime: the first replay uploads instead)
+        return False
+
+
 class Trainer:
     def __init__(self, model, store, optimizer, class_weights: Optional[Dict[int, float]], baseline: bool = False,
                  use_graph: bool = True, batch_size: int = 128):
@@ -352,6 +368,8 @@ class Trainer:
                 self._capture_multi(int(rows.shape[0]))
             if self.multi_graph1 is None or self._multi_key1 != (int(rows.shape[0]), rows.shape[1]):
                 self._capture_multi(int(rows.shape[0]), steps=1)
+        for g in (self.graph, self.multi_graph, self.multi_graph1):
+            _graph_upload(g)
 
     def train_steps(self, rows: torch.Tensor, start: int, k: int):
         """``k`` training steps on batches ``rows[(start + i) % len(rows)]`` (rows: [n, B] device
