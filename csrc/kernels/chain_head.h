@@ -197,8 +197,12 @@ __device__ __forceinline__ float* ch_head_fwd_weights(char* scratch) {
   return reinterpret_cast<float*>(scratch) + 3 * 16 * CH_AP + 16 * 8;
 }
 template <int F>
+__device__ __forceinline__ void chain_head_fwd_handoff(const ChainHead hd, int tile, int ntiles, char* scratch);
+// handoff = false: stop before the tile's loss partials are handed off (the caller runs
+// chain_head_fwd_handoff later, e.g. after more work whose latency hides the stores' acknowledgements)
+template <int F>
 __device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int ntiles, const float* hl, char* scratch,
-                                               bool staged = false) {
+                                               bool staged = false, bool handoff = true) {
   float* part = reinterpret_cast<float*>(scratch);    // [2][16][CH_AP]
   float* sa1 = part + 2 * 16 * CH_AP;                 // [16][CH_AP]
   float* rowv = sa1 + 16 * CH_AP;                     // [16][8]
@@ -242,6 +246,15 @@ __device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int
     }
   }
   __syncthreads();
+  if (handoff) chain_head_fwd_handoff<F>(hd, tile, ntiles, scratch);
+}
+
+// the tile's loss / metric partials (rowv, in the head forward's scratch) -> hd.part, and the loss
+// of the last tile to arrive
+template <int F>
+__device__ __forceinline__ void chain_head_fwd_handoff(const ChainHead hd, int tile, int ntiles, char* scratch) {
+  const float* rowv = reinterpret_cast<const float*>(scratch) + 3 * 16 * CH_AP;
+  const int tid = threadIdx.x;
   // hand-off without fences (MI355X_MICROARCH.md: an agent fence costs 1.7-3.5 us): sc1 stores,
   // the storing wave's vmcnt(0), a workgroup barrier, ONE lane's agent-scope counter add; the
   // workgroup whose add came last reads the partials with sc1 loads

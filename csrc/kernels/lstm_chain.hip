@@ -898,8 +898,9 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
           long long* mk = blockIdx.x < 64 ? A.trace + 512 + blockIdx.x : nullptr;   // (trace: phase ends)
           if (mk != nullptr && threadIdx.x == 0) mk[0] = (long long)__builtin_amdgcn_s_memrealtime();
           if (threadIdx.x >= 64 * CH_NW) return;    // the head runs on 8 waves (the rest exit)
+          const bool pre = TRAIN && A.t4.hb != nullptr;
           chain_head_fwd<128>(A.t4.hd, r, A.ntiles, reinterpret_cast<const float*>(smem + ChainT4Lds::HS + ChainT4Lds::XS),
-                              smem + HOFF, true);
+                              smem + HOFF, true, !pre);
           if (mk != nullptr && threadIdx.x == 0) mk[64] = (long long)__builtin_amdgcn_s_memrealtime();
           if constexpr (TRAIN) {
             if (A.t4.hb != nullptr) {
@@ -915,6 +916,8 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
                                   dhs, smem + OFF + ChainT4Lds::DHT, 132, true, false, CH_NW, hW1, hW1 + 128 * CH_WP);
               for (int e = ch_tid(); e < 16 * 128; e += 64 * CH_NW)
                 A.t4.hb[((size_t)r * 16 + e / 128) * 128 + e % 128] = dhs[(e / 128) * 132 + e % 128];
+              // the loss hand-off last: its stores' acknowledgement wait then overlaps nothing it delays
+              chain_head_fwd_handoff<128>(A.t4.hd, r, A.ntiles, smem + HOFF);
             }
           }
           __syncthreads();
