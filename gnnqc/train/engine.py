@@ -361,15 +361,25 @@ class Trainer:
             self._capture()
         if self._multi_ok():
             if self._table is None or tuple(self._table.shape) != tuple(rows.shape):
-                self._table = torch.empty_like(rows, dtype=torch.long)
+                self._table, self._table_src = torch.empty_like(rows, dtype=torch.long), None
                 self.multi_graph = self.multi_graph1 = None
-            self._table.copy_(rows)
+            self._load_table(rows)
             if self.multi_graph is None or self._multi_key != (int(rows.shape[0]), rows.shape[1]):
                 self._capture_multi(int(rows.shape[0]))
             if self.multi_graph1 is None or self._multi_key1 != (int(rows.shape[0]), rows.shape[1]):
                 self._capture_multi(int(rows.shape[0]), steps=1)
         for g in (self.graph, self.multi_graph, self.multi_graph1):
             _graph_upload(g)
+
+    def _load_table(self, rows: torch.Tensor):
+        """Copy the batch-id rows into the graphs' device table, unless the table already holds
+        exactly these rows (same tensor, unmodified since): a copy launch and its gap less per call."""
+        # (the source is kept referenced, so no other tensor can take its memory and pass as it)
+        src = getattr(self, "_table_src", None)
+        if src is not None and src[0] is rows and src[1] == rows._version:
+            return
+        self._table.copy_(rows, non_blocking=True)
+        self._table_src = (rows, rows._version)
 
     def train_steps(self, rows: torch.Tensor, start: int, k: int):
         """``k`` training steps on batches ``rows[(start + i) % len(rows)]`` (rows: [n, B] device
@@ -381,7 +391,7 @@ class Trainer:
                   and tuple(self._table.shape) == tuple(rows.shape) and self._multi_key1 == (nb, rows.shape[1]))
         if k < S and one_ok:                 # (prepare_graphs captured the one-step form)
             self.model.train()
-            self._table.copy_(rows, non_blocking=True)
+            self._load_table(rows)
             self._cursor.fill_(start % nb)
             for _ in range(k):
                 self.multi_graph1.replay()
@@ -395,12 +405,12 @@ class Trainer:
             return self.last_loss
         self.model.train()
         if self._table is None or tuple(self._table.shape) != tuple(rows.shape):
-            self._table = torch.empty_like(rows, dtype=torch.long)
+            self._table, self._table_src = torch.empty_like(rows, dtype=torch.long), None
             self.multi_graph = self.multi_graph1 = None
             one_ok = False
         if self.multi_graph is not None and self._multi_key != (nb, rows.shape[1]):
             self.multi_graph = None
-        self._table.copy_(rows, non_blocking=True)
+        self._load_table(rows)
         if self.multi_graph is None:
             if self.graph is None:
                 self._capture()              # the single-step graph shares the warm allocator state
