@@ -107,16 +107,18 @@ struct NodeSmem {
   float* vals;
   float* rs;
   float* mk;
+  float* xs;                                   // [2][N * Cin] staged node inputs of a step (Cin <= 4)
   __device__ NodeSmem(unsigned char* base, int N, int NWd, int F) {
     bits = reinterpret_cast<unsigned*>(base);
     vals = reinterpret_cast<float*>(bits + ((size_t)N * NWd + 3) / 4 * 4);   // 16-byte aligned rows
     rs = vals + (size_t)N * F;
     mk = rs + N;
+    xs = mk + N;
   }
 };
 
 static size_t node_smem_bytes(int N, int NWd, int F) {
-  return ((size_t)N * NWd + 3) / 4 * 16 + (size_t)N * F * 4 + (size_t)N * 8;
+  return ((size_t)N * NWd + 3) / 4 * 16 + (size_t)N * F * 4 + (size_t)N * 8 + (size_t)N * 32;
 }
 
 // ------------------------------------------------------------------ forward
@@ -140,9 +142,12 @@ __global__ __launch_bounds__(256) void gcn_node_fwd_kernel(
   for (int k = 0; k < Cin; ++k) wk[k] = W[k * F + f];
   const float bb = bias[f], sc = scale[f], sh = shift[f], al = alpha[f];
   const int t1 = min(t0 + tchunk, T);
+  // x_t (N * Cin floats) is staged in LDS one step ahead, during the previous step's gather: the
+  // activation loop below then reads LDS instead of issuing a dependent HBM load per item
+  for (int e = tid; e < N * Cin; e += 256) sm.xs[e] = x[((long)b * T + t0) * (long)N * Cin + e];
   for (int t = t0; t < t1; ++t) {
-    __syncthreads();                           // previous step's reads of vals are done
-    const float* xt = x + ((long)b * T + t) * (long)N * Cin;
+    __syncthreads();                           // previous step's reads of vals are done, xs[t] written
+    const float* xt = sm.xs + ((t - t0) & 1) * N * Cin;
     for (int e = tid; e < N * F; e += 256) {
       const int j = e / F;
       float z = bb;
@@ -152,6 +157,10 @@ __global__ __launch_bounds__(256) void gcn_node_fwd_kernel(
       sm.vals[e] = (y > 0.f ? y : al * y) * sm.mk[j];
     }
     __syncthreads();
+    if (t + 1 < t1) {                          // stage x_{t+1} (its buffer was last read in step t-1)
+      float* xn = sm.xs + ((t + 1 - t0) & 1) * N * Cin;
+      for (int e = tid; e < N * Cin; e += 256) xn[e] = x[((long)b * T + t + 1) * (long)N * Cin + e];
+    }
     float* ot = out + ((long)t * Mp + (long)b * N) * Cp;
     // V output channels per item (F, Cp multiples of V): aggregated groups walk the row mask once
     const int G = Cp / V;
@@ -222,12 +231,24 @@ __global__ __launch_bounds__(256) void gcn_node_bwd_kernel(
   for (int t = t0; t < t1; ++t) {
     __syncthreads();
     const float* dt = dout + ((long)t * Mp + (long)b * N) * Cp;
-    for (int e = tid; e < N * F; e += 256) {
-      const int i = e / F;
-      sm.vals[e] = dt[(long)i * Cp + f] * sm.rs[i];    // dagg_i / deg_i
+    if constexpr (V == 4) {                    // Cp % 4 == 0 (host): one 16-byte load per 4 channels
+#pragma unroll 4
+      for (int e = tid; e < N * G; e += 256) {
+        const int i = e / G, cc = (e - i * G) * 4;
+        float4 d = *reinterpret_cast<const float4*>(dt + (long)i * Cp + cc);
+        const float r = sm.rs[i];
+        d.x *= r; d.y *= r; d.z *= r; d.w *= r;          // dagg_i / deg_i
+        *reinterpret_cast<float4*>(sm.vals + i * F + cc) = d;
+      }
+    } else {
+      for (int e = tid; e < N * F; e += 256) {
+        const int i = e / F;
+        sm.vals[e] = dt[(long)i * Cp + f] * sm.rs[i];  // dagg_i / deg_i
+      }
     }
+    for (int e = tid; e < N * Cin; e += 256) sm.xs[e] = x[((long)b * T + t) * (long)N * Cin + e];
     __syncthreads();
-    const float* xt = x + ((long)b * T + t) * (long)N * Cin;
+    const float* xt = sm.xs;
     for (int e = tid; e < N * G; e += 256) {
       const int j = e / G;
       if (sm.mk[j] == 0.f) continue;               // masked node: activation forced to 0
@@ -443,7 +464,9 @@ at::Tensor gcn_node_bwd(const at::Tensor& x, const at::Tensor& bitsT, const at::
   c10::DeviceGuard guard(x.device());
   const int nacc = 3 + g.Cin;
   at::Tensor partial = at::empty({(long)g.grid.x * g.grid.y, nacc, g.F}, x.options());
-  GQ_NODE_CIN_DISPATCH(g.Cin, GQ_NODE_V_DISPATCH(g.F % 4 == 0,
+  const bool vec = g.F % 4 == 0 && dout.size(2) % 4 == 0 && dout.stride(1) == dout.size(2) &&
+                   (reinterpret_cast<uintptr_t>(dout.data_ptr()) % 16) == 0;
+  GQ_NODE_CIN_DISPATCH(g.Cin, GQ_NODE_V_DISPATCH(vec,
       allow_smem(gcn_node_bwd_kernel<CIN, VV>, g.smem);
       hipLaunchKernelGGL((gcn_node_bwd_kernel<CIN, VV>), g.grid, dim3(256), g.smem, stream(), x.data_ptr<float>(),
                          reinterpret_cast<const unsigned*>(bitsT.data_ptr<int>()), rs.data_ptr<float>(),
