@@ -374,7 +374,7 @@ struct NodeGeom {
   dim3 grid;
 };
 
-static NodeGeom node_geom(const at::Tensor& x, const at::Tensor& bits, const at::Tensor& W) {
+static NodeGeom node_geom(const at::Tensor& x, const at::Tensor& bits, const at::Tensor& W, int tdef = 2) {
   NodeGeom g;
   TORCH_CHECK(x.dim() == 4, "gcn_node: x must be [B,T,N,Cin]");
   g.B = x.size(0);
@@ -390,10 +390,13 @@ static NodeGeom node_geom(const at::Tensor& x, const at::Tensor& bits, const at:
   TORCH_CHECK(g.smem <= 150 * 1024, "gcn_node: graph too large for LDS (N=", g.N, ")");
   // enough workgroups to fill 256 CUs several times over
   const long steps = (long)g.B * g.T;
-  static const int tmax = [] {                 // steps per workgroup cap (A/B: GNNQC_NODE_TCHUNK)
+  // steps per workgroup cap (A/B: GNNQC_NODE_TCHUNK overrides both). SoilNet, scripts/node_tchunk_sweep.sh:
+  // forward 113 / 112 / 123 / 155 us and parameter backward 207 / 172 / 153 / 178 us at 1 / 2 / 4 / 8
+  static const int tenv = [] {
     const char* e = std::getenv("GNNQC_NODE_TCHUNK");
-    return e != nullptr ? std::max(1, std::atoi(e)) : 2;   // SoilNet: 2 best of 8 / 4 / 2 / 1 (bwd 238 -> 190 us)
+    return e != nullptr ? std::max(1, std::atoi(e)) : 0;
   }();
+  const int tmax = tenv > 0 ? tenv : tdef;
   g.tchunk = (int)std::max<long>(1, std::min<long>(tmax, steps / 1024));
   g.grid = dim3((g.T + g.tchunk - 1) / g.tchunk, g.B);
   return g;
@@ -458,7 +461,7 @@ at::Tensor gcn_node_bwd(const at::Tensor& x, const at::Tensor& bitsT, const at::
                         const at::Tensor& dout, const at::Tensor& W, const at::Tensor& b, const at::Tensor& scale,
                         const at::Tensor& shift, const at::Tensor& alpha) {
   for (auto* p : {&x, &rs, &mask, &dout, &W, &b, &scale, &shift, &alpha}) check_f32_cuda(*p, "gcn_node_bwd input");
-  NodeGeom g = node_geom(x, bitsT, W);
+  NodeGeom g = node_geom(x, bitsT, W, 4);
   TORCH_CHECK(dout.dim() == 3 && dout.size(0) == g.T && dout.size(1) >= (long)g.B * g.N && dout.size(2) >= g.F + g.Cin,
               "gcn_node_bwd: dout must be [T, Mp, Cp]");
   c10::DeviceGuard guard(x.device());
