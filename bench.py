@@ -17,6 +17,11 @@ shape of ``cml_raw_example.nc``) windowed with T = 181. Every timed step is a fu
 training step: on-device window gather, forward, weighted BCE, backward, gradient
 all-reduce (N > 1), Adam update.
 
+After the timed region the same line carries the quality half of BASELINE.json's headline metric
+("ROC-AUC (5-fold CV)"): the paper's 5-fold CV of the CML GCN and of the graph-less baseline LSTM
+(``cv``; folds dealt over the ranks under --gpus N), and the integrated-gradients throughput
+(``ig``). ``--no-cv-line`` / ``--no-ig-line`` skip them.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -24,6 +29,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -42,41 +48,89 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpu_count():
+    """GPUs this job may use, counted WITHOUT touching HIP (no ``torch.cuda`` call: on ROCm
+    ``torch.cuda.device_count`` falls back to ``hipGetDeviceCount`` when amdsmi is unavailable, which
+    would initialise the runtime in a parent that then forks its ranks). Reads the KFD topology
+    (``/sys/class/kfd/kfd/topology/nodes/*/properties``: GPU nodes have ``simd_count > 0``) and
+    honours ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES``. Returns
+    None when the topology is not readable (every rank then checks its own device count)."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = sorted(os.listdir(root), key=lambda s: int(s) if s.isdigit() else 1 << 30)
+    except OSError:
+        return None
+    n = 0
+    for nd in nodes:
+        try:
+            with open(os.path.join(root, nd, "properties")) as f:
+                props = dict(ln.split(None, 1) for ln in f.read().splitlines() if len(ln.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([s for s in v.split(",") if s.strip()]))
+    return n
+
+
 def launch_ranks(n: int, argv) -> int:
     """Run this script as ``n`` rank processes (one per GPU) and wait for all of them. The parent
-    only counts devices (``torch.cuda.device_count`` does not initialise HIP) and never calls into
-    the GPU; a child that fails takes the others down (exact Popen handles, no pattern kills) and
-    its exit code becomes this process's."""
-    ndev = torch.cuda.device_count()
+    never calls into HIP (GPUs are counted from sysfs, :func:`visible_gpu_count`); a child that
+    fails takes the others down (exact Popen handles, no pattern kills) and its exit code becomes
+    this process's. A SIGTERM / SIGINT of the parent (e.g. a driver timeout) stops every rank too."""
+    ndev = visible_gpu_count()
     if ndev and n > ndev:
         print(f"bench.py: --gpus {n} but only {ndev} GPUs are visible", file=sys.stderr)
         return 2
     port = _free_port()
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if not ndev:                  # CPU (gloo) rehearsal: do not oversubscribe the cores
-            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // n)))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+
+    def _raise(signum, _frame):
+        raise KeyboardInterrupt(f"signal {signum}")
+
+    prev = {s: signal.signal(s, _raise) for s in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
-                      file=sys.stderr)
-                for q in live:
-                    q.terminate()
-        time.sleep(0.05)
-    for p in procs:
-        p.wait()
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            if not ndev:                  # CPU (gloo) rehearsal: do not oversubscribe the cores
+                env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // n)))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    except KeyboardInterrupt as e:
+        print(f"bench.py: interrupted ({e}); stopping every rank", file=sys.stderr)
+        rc = rc or 130
+    finally:
+        for p in procs:                   # terminate, then kill, whatever is still running
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for s, h in prev.items():
+            signal.signal(s, h)
     return rc
 
 
@@ -117,6 +171,63 @@ def measure_ig(args, trainer, dev, world, rank, D):
             "sharding": "round-robin batches over ranks" if world > 1 else "one rank"}
 
 
+REF_CV_AUC = {"gcn": 0.941, "baseline": 0.885}   # CML 5-fold CV mean ROC-AUC (README.md:10)
+
+
+def measure_cv(args, dev, world, D):
+    """The quality half of BASELINE.json's headline metric: the paper's 5-fold cross-validation
+    protocol (contiguous folds of ``load_dataset_CV``, ``xai/libs/preprocessing_functions.py:804-836``;
+    CV training monitors ``loss``, ``xai/libs/fit_model.py:94-99``) for the CML GCN AND the graph-less
+    baseline LSTM, each fold a fresh random-init model trained for the config's epochs at the bench
+    dtype and scored by exact ROC-AUC on its held-out fold (``gnnqc.train.cv.run_cv``). Runs after the
+    timed region, on the CV data shape of ``scripts/cv_headline.sh`` (synthetic CML, 23 links x 28
+    days, 4 flagged links). Under ``--gpus N`` the folds are dealt over the ranks (fold f on rank
+    f % N, no collective inside a fold) and gathered."""
+    from gnnqc import config as C
+    from gnnqc.data.preprocessing import create_windows_dataset
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.data.synthetic import make_cml_raw
+    from gnnqc.train.cv import run_cv
+    gpu = dev.type == "cuda"
+    folds = args.cv_folds or (5 if gpu else 2)
+    sensors = args.cv_sensors or (23 if gpu else args.sensors)
+    days = args.cv_days or (28 if gpu else min(args.days, 3))
+    flagged = args.cv_flagged or (4 if gpu else 1)
+    pc = C.normalize_preproc(C.default("preprocessing_cml"))
+    mc = C.default("model_cml")
+    mc.runtime.compute_dtype = args.dtype
+    if args.cv_epochs or not gpu:
+        mc.epochs = int(args.cv_epochs or 1)
+    raw = make_cml_raw(n_sensors=sensors, n_flagged=flagged, n_minutes=int(days * 1440), seed=0)
+    pc["min_date"], pc["max_date"] = str(raw.time[0]), str(raw.time[-1])
+    ws = create_windows_dataset(pc, raw=raw)
+    store = DeviceStore(ws, "rolling_median", pc.graph, device=dev)
+    D.barrier()
+    t0 = time.perf_counter()
+    out = {"protocol": "%d-fold CV (contiguous folds, load_dataset_CV), fresh random-init model per fold, "
+                       "exact ROC-AUC on the held-out fold" % folds,
+           "data": "synthetic CML: %d links x %g days @1min, %d flagged links, T=%d, %d windows"
+                   % (sensors, days, flagged, ws.seq_len, ws.n_windows),
+           "folds": folds, "epochs": int(mc.epochs), "dtype": args.dtype,
+           "fold_per_rank": world > 1}
+    for name, baseline in (("gcn", False), ("baseline", True)):
+        s = run_cv(pc, mc, ws, folds=folds, baseline=baseline, store=store, seed=0, verbose=0,
+                   fold_per_rank=world > 1)
+        out[f"{name}_mean_auc"] = round(s["mean_auc"], 5)
+        out[f"{name}_std"] = round(s["std_auc"], 5)
+        out[f"{name}_fold_auc"] = [round(r["auc"], 5) for r in s["per_fold"]]
+        out[f"{name}_folds_run"] = s["folds_run"]
+        out[f"{name}_mean_mcc"] = round(s["mean_mcc"], 5)
+    if gpu:
+        torch.cuda.synchronize()
+    D.barrier()
+    out["seconds"] = round(D.max_over_ranks(time.perf_counter() - t0), 2)
+    out["gcn_minus_baseline_auc"] = round(out["gcn_mean_auc"] - out["baseline_mean_auc"], 5)
+    out["reference_mean_auc"] = dict(REF_CV_AUC)
+    out["vs_reference_gcn_auc"] = round(out["gcn_mean_auc"] / REF_CV_AUC["gcn"], 4)
+    return out
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
@@ -145,6 +256,14 @@ def main(argv=None):
                     help="windows per attribute() call (default 256 on a GPU, 4 on the CPU)")
     ap.add_argument("--ig-calls", type=int, default=None,
                     help="timed attribute() calls per rank (default 6 on a GPU, 1 on the CPU)")
+    ap.add_argument("--no-cv-line", dest="cv_line", action="store_false",
+                    help="skip the 5-fold CV ROC-AUC of the CML GCN and baseline (reported as 'cv' in the JSON line)")
+    ap.add_argument("--cv-folds", type=int, default=None, help="CV folds (default 5 on a GPU, 2 on the CPU)")
+    ap.add_argument("--cv-epochs", type=int, default=None, help="epochs per fold (default: the model config's, "
+                    "1 on the CPU)")
+    ap.add_argument("--cv-sensors", type=int, default=None, help="CV data: CML links (default 23)")
+    ap.add_argument("--cv-days", type=float, default=None, help="CV data: days (default 28)")
+    ap.add_argument("--cv-flagged", type=int, default=None, help="CV data: flagged links (default 4)")
     args = ap.parse_args(argv)
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -153,6 +272,10 @@ def main(argv=None):
         return 2
     if env_world is None and args.gpus > 1:
         return launch_ranks(args.gpus, argv)
+    if args.gpus > 1 and torch.cuda.is_available() and torch.cuda.device_count() < args.gpus:
+        # (a rank process may initialise HIP; the spawning parent never does)
+        print(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPUs are visible", file=sys.stderr)
+        return 2
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from gnnqc import config as C
@@ -249,6 +372,9 @@ def main(argv=None):
     ig = None
     if args.ig_line and not soil and not baseline:
         ig = measure_ig(args, trainer, dev, world, rank, D)
+    cv = None
+    if args.cv_line and not soil:
+        cv = measure_cv(args, dev, world, D)
     if rank == 0:
         out = {
             "metric": ("train windows/sec, SoilNet GCN (diagnostic; not the headline metric)" if soil else
@@ -289,6 +415,8 @@ def main(argv=None):
             out["knn5"] = knn
         if ig is not None:
             out["ig"] = ig
+        if cv is not None:
+            out["cv"] = cv
         if comm_us is not None:
             # the collective of the timed steps, run on its own (in-graph collectives cannot be timed one
             # by one), plus the setup-time comparison of both modes when the peer kernel was considered

@@ -230,8 +230,9 @@ void peer_allreduce(at::Tensor g, at::IntArrayRef bases, at::Tensor region, int6
 //   3. sums the W copies of the slice in rank order with cache-bypassing 16-byte loads (bit-identical
 //      on every rank) and applies Adam to the slice (gscale folds the 1 / world mean in), skipping
 //      non-finite elements (counted in state[5], identical on every rank);
-//   4. a relaxed arrival ticket (ctl[1]); the last arrival clears g[0] and the flags, advances the
-//      launch counter ctl[0], the step counter and the batch cursor.
+//   4. an arrival ticket (ctl[1]; release from a slice that timed out, acquire by the last arrival);
+//      the last arrival clears g[0] and the flags, advances the launch counter ctl[0], the step
+//      counter and the batch cursor.
 // Slices need no grid-wide barrier: a slice flag of launch k is only overwritten by launch k + 2 of
 // its writer, which cannot start before this rank has finished launch k (it needs this rank's flags
 // of launch k + 1); data[k & 1] likewise. Every wait is bounded: a timed-out slice rejects the step
@@ -367,13 +368,21 @@ __global__ __launch_bounds__(256) void adam_peer_kernel(PeerArgs A, float* __res
     }
   }
   if (skipped) atomicAdd(state + 5, skipped);
-  // ---- 4. arrival ticket; the last arrival finishes the step's bookkeeping
+  // ---- 4. arrival ticket; the last arrival finishes the step's bookkeeping. A workgroup whose wait
+  // timed out stored ctl[2] (lanes < W: the wave of tid 0) and arrives with a RELEASE ticket; the
+  // last arrival acquires after its ticket (the relaxed tickets in between continue the release
+  // sequence), so it sees every timeout before it decides. Slices that did not time out keep the
+  // relaxed ticket: a release there would drain the slice's update stores first (~6 us, adam.hip).
   __shared__ int last;
   __builtin_amdgcn_s_barrier();
-  if (tid == 0) last = __hip_atomic_fetch_add(A.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                       (int)gridDim.x - 1;
+  if (tid == 0) {
+    const int ticket = sok ? __hip_atomic_fetch_add(A.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : __hip_atomic_fetch_add(A.ctl + 1, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    last = ticket == (int)gridDim.x - 1;
+  }
   lds_barrier();
   if (!last || tid != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __hip_atomic_store(A.ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(A.ctl + 0, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   g[0] = 0.f;

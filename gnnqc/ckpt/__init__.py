@@ -6,9 +6,11 @@
   step counters); loaded with ``torch.load(weights_only=True)``;
 * ``gnnqc_meta.json``  - model/preprocessing config, class, epoch, RNG cursor;
 * ``variables/variables.{index,data-00000-of-00001}`` (+ ``_CHECKPOINTABLE_OBJECT_GRAPH``),
-  ``keras_metadata.pb`` and ``fingerprint.pb`` - the Keras SavedModel variable layout
-  (TensorBundle), object graph, per-layer JSON and content fingerprint, see
-  :mod:`gnnqc.ckpt.tensorbundle`, :mod:`gnnqc.ckpt.keras_layout`, :mod:`gnnqc.ckpt.keras_meta`.
+  ``saved_model.pb``, ``keras_metadata.pb`` and ``fingerprint.pb`` - the Keras SavedModel layout
+  (TensorBundle), object graph, best-effort SavedModel proto (meta graph tagged ``serve`` whose
+  SavedObjectGraph mirrors the object graph), per-layer JSON and content fingerprint, see
+  :mod:`gnnqc.ckpt.tensorbundle`, :mod:`gnnqc.ckpt.keras_layout`, :mod:`gnnqc.ckpt.saved_model`,
+  :mod:`gnnqc.ckpt.keras_meta`.
 
 ``load_model(path)`` rebuilds the model from the metadata and restores the state;
 ``load_keras_weights`` imports the reference's trained ``model_*`` directories.

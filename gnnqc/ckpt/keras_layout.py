@@ -69,6 +69,31 @@ def keras_tensors(model, optimizer=None) -> Dict[str, object]:
 OBJECT_GRAPH_KEY = "_CHECKPOINTABLE_OBJECT_GRAPH"
 
 
+def trackable_tree(keys, full_names: Optional[Dict[str, str]] = None) -> List[dict]:
+    """Node list of the object graph for a set of ``<path>/.ATTRIBUTES/VARIABLE_VALUE`` keys: node 0
+    is the root, every path prefix (``variables``, ``variables/3``, ``optimizer/_variables``, ...) is a
+    node whose ``children`` are ``(node_id, local_name)`` pairs, and a variable node carries
+    ``attrs = [(name, full_name, checkpoint_key)]`` and ``key``. Node ids follow sorted key order, so
+    the ``_CHECKPOINTABLE_OBJECT_GRAPH`` (:func:`object_graph`) and the ``SavedObjectGraph`` of
+    ``saved_model.pb`` (:mod:`gnnqc.ckpt.saved_model`) number their nodes identically."""
+    full_names = full_names or {}
+    nodes = [{"children": [], "attrs": [], "path": (), "key": None}]
+    index = {(): 0}
+    for key in sorted(keys):
+        if not key.endswith(SUFFIX):
+            continue
+        parts = tuple(key[: -len(SUFFIX)].split("/"))
+        for d in range(1, len(parts) + 1):
+            pre = parts[:d]
+            if pre not in index:
+                index[pre] = len(nodes)
+                nodes.append({"children": [], "attrs": [], "path": pre, "key": None})
+                nodes[index[parts[: d - 1]]]["children"].append((index[pre], parts[d - 1]))
+        nodes[index[parts]]["attrs"].append(("VARIABLE_VALUE", full_names.get(key, "/".join(parts)), key))
+        nodes[index[parts]]["key"] = key
+    return nodes
+
+
 def object_graph(keys, full_names: Optional[Dict[str, str]] = None) -> bytes:
     """``TrackableObjectGraph`` proto for a set of ``<path>/.ATTRIBUTES/VARIABLE_VALUE`` keys.
 
@@ -80,22 +105,8 @@ def object_graph(keys, full_names: Optional[Dict[str, str]] = None) -> bytes:
     checkpoint keys to objects. Function / signature nodes are not emitted (no graph is saved).
     Field numbers follow tensorflow/core/protobuf/trackable_object_graph.proto."""
     from .tensorbundle import _pb_bytes, _pb_varint
-    full_names = full_names or {}
-    nodes = [{"children": [], "attrs": []}]
-    index = {(): 0}
-    for key in sorted(keys):
-        if not key.endswith(SUFFIX):
-            continue
-        parts = tuple(key[: -len(SUFFIX)].split("/"))
-        for d in range(1, len(parts) + 1):
-            pre = parts[:d]
-            if pre not in index:
-                index[pre] = len(nodes)
-                nodes.append({"children": [], "attrs": []})
-                nodes[index[parts[: d - 1]]]["children"].append((index[pre], parts[d - 1]))
-        nodes[index[parts]]["attrs"].append(("VARIABLE_VALUE", full_names.get(key, "/".join(parts)), key))
     out = b""
-    for n in nodes:
+    for n in trackable_tree(keys, full_names):
         body = b"".join(_pb_bytes(1, _pb_varint(1, nid) + _pb_bytes(2, name.encode())) for nid, name in n["children"])
         body += b"".join(_pb_bytes(2, _pb_bytes(1, a.encode()) + _pb_bytes(2, f.encode()) + _pb_bytes(3, k.encode()))
                          for a, f, k in n["attrs"])
@@ -106,8 +117,8 @@ def object_graph(keys, full_names: Optional[Dict[str, str]] = None) -> bytes:
 def write_fingerprint(path: str):
     """``fingerprint.pb`` (``FingerprintDef``): 64-bit content hashes of what the directory holds
     (fields 1-5: saved-model checksum, graph hash, signature hash, object-graph hash, checkpoint
-    hash; 6: version). Our hashes are blake2b-64 of the files, not TF's farmhash; no saved
-    graph exists, so the graph / signature hashes are of empty inputs."""
+    hash; 6: version). Our hashes are blake2b-64 of the files, not TF's farmhash; saved_model.pb
+    holds no ops or signatures, so the graph / signature hashes are of empty inputs."""
     import hashlib
     from .tensorbundle import _pb_bytes, _pb_varint
 
@@ -127,18 +138,36 @@ def write_fingerprint(path: str):
     if os.path.exists(mp):
         with open(mp, "rb") as f:
             meta = f.read()
+    sm = b""
+    sp = os.path.join(path, "saved_model.pb")
+    if os.path.exists(sp):
+        with open(sp, "rb") as f:
+            sm = f.read()
     ck = h(idx, data)
-    fp = (_pb_varint(1, h(idx, data, meta)) + _pb_varint(2, h(b"")) + _pb_varint(3, h(b"")) + _pb_varint(4, h(idx))
-          + _pb_varint(5, ck) + _pb_bytes(6, b""))
+    # saved-model checksum over saved_model.pb (+ the bundle and metadata), object-graph hash over the
+    # SavedModel proto that carries the SavedObjectGraph (the bundle's index when none was written)
+    fp = (_pb_varint(1, h(sm, idx, data, meta)) + _pb_varint(2, h(b"")) + _pb_varint(3, h(b""))
+          + _pb_varint(4, h(sm) if sm else h(idx)) + _pb_varint(5, ck) + _pb_bytes(6, b""))
     with open(os.path.join(path, "fingerprint.pb"), "wb") as f:
         f.write(fp)
 
 
-def write_keras_variables(model, path: str, optimizer=None):
-    """Write ``<path>/variables/variables.{index,data-00000-of-00001}`` (with the object graph)."""
+def trainable_keys(model) -> List[str]:
+    """Checkpoint keys of the trainable ``variables/<i>`` (parameters; BN moving statistics are not)."""
+    return [_var_key(i) for i, (_, t) in enumerate(ordered_variables(model))
+            if isinstance(t, torch.nn.Parameter) and t.requires_grad]
+
+
+def write_keras_variables(model, path: str, optimizer=None, saved_model: bool = True):
+    """Write ``<path>/variables/variables.{index,data-00000-of-00001}`` (with the object graph) and,
+    unless ``saved_model=False``, the best-effort ``<path>/saved_model.pb`` whose SavedObjectGraph
+    mirrors that object graph node for node (:mod:`gnnqc.ckpt.saved_model`)."""
     t = keras_tensors(model, optimizer)
     t[OBJECT_GRAPH_KEY] = object_graph(list(t))
     write_bundle(os.path.join(path, "variables", "variables"), t)
+    if saved_model:
+        from .saved_model import write_saved_model
+        write_saved_model(path, t, trainable_keys(model))
 
 
 def _bundle_prefix(path: str) -> str:
@@ -240,5 +269,5 @@ def build_from_keras(path: str, ds_type: Optional[str] = None, baseline: Optiona
     return model.to(device), pc, mc
 
 
-__all__ = ["write_keras_variables", "load_keras_weights", "load_keras_optimizer", "read_keras_metadata",
+__all__ = ["write_keras_variables", "trainable_keys", "trackable_tree", "object_graph", "load_keras_weights", "load_keras_optimizer", "read_keras_metadata",
            "build_from_keras", "ordered_variables", "keras_tensors"]

@@ -334,7 +334,10 @@ def write_bundle(prefix: str, tensors: Dict[str, object]):
             raw, crc = _encode_strings([b])
             dtype, shape = DT_STRING, ()
         else:
-            arr = np.ascontiguousarray(np.asarray(val))
+            arr = np.asarray(val)
+            # (np.ascontiguousarray promotes a 0-d array to shape (1,): scalars such as
+            # optimizer/_iterations keep the reference's shape [] instead)
+            arr = np.ascontiguousarray(arr) if arr.ndim else arr.copy()
             if arr.dtype not in NP_TO_DT:
                 arr = arr.astype(np.float32)
             raw = arr.astype(arr.dtype.newbyteorder("<")).tobytes()

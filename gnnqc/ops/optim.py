@@ -192,7 +192,10 @@ class FlatAdam(FlatOptimizer):
                                        int(self.cursor_mod), pa.bases, pa.region, pa.rank, pa.cap):
                     self.iterations += 1
                     return
-                raise RuntimeError("adam_peer: gradient buffer too large for the fused peer update")
+                # more slices than the fused kernel's flag table: the two separate launches (the
+                # trainer issued no collective for this step, so reduce here, reject bits first)
+                hip_ops().chain_poison(self.flat_g, chain_ctl(self.flat_g.device))
+                pa(self.flat_g)
             if self.flagged_producers:
                 hip_ops().adam_flagged(self.flat_p, self.flat_g, self.m, self.v, self.lr_t, self.step_t, self.beta1,
                                        self.beta2, self.eps, float(grad_scale), self.wd, self.guard_state,

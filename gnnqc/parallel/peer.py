@@ -9,7 +9,11 @@ multi-step training graph like the RCCL collective it replaces.
 
 Selected by :func:`peer_mode` (default ``auto``: with two or more ranks it is set up, validated
 against RCCL / gloo (:meth:`PeerAllReduce.verify`) and timed against the process group's all-reduce,
-and used only if it verified and was faster); one process per GPU of one node, at most 8 ranks. The handles
+and used only if it verified and was faster); one process per GPU of one node, at most 8 ranks. A
+training step whose gradient producers all raise the non-finite flag reduces INSIDE the Adam launch
+(``adam_peer``): that fused kernel is checked separately at setup against the all-reduce kernel
+followed by ``adam_flagged`` on scratch buffers, timed against that pair, and used only when it agrees
+(and, in ``auto`` mode, is faster) on every rank (:func:`check_fused_adam`). The handles
 are exchanged with the default process group, so it works over gloo as well (tests: two ranks
 sharing one GPU). Between different GPUs over xGMI it has NOT been run (no multi-GPU box was
 available): treat it as unverified there until a multi-GPU run checks it against RCCL.
@@ -152,12 +156,111 @@ def _time_both(pa: "PeerAllReduce", numel: int, device, n: int = 30):
     return float(t[0].item()), float(t[1].item())
 
 
+PEER_SLICES = 1024        # peer_allreduce.hip: slice flags of the fused update (1024 floats each)
+
+
+def fused_adam_fits(numel: int) -> bool:
+    """Whether adam_peer can take a flat buffer of ``numel`` floats (one workgroup per 1024-float
+    slice, at most PEER_SLICES of them)."""
+    return max(1, (int(numel) // 4 + 255) // 256) <= PEER_SLICES
+
+
+_FUSED = {}
+
+
+@torch.no_grad()
+def check_fused_adam(pa: "PeerAllReduce", numel: int, device, beta1: float = 0.9, beta2: float = 0.999,
+                     eps: float = 1e-7, trials: int = 2, n_time: int = 20) -> bool:
+    """Setup check of the reduction fused into the Adam launch (``adam_peer``) before a trainer uses
+    it: on scratch p / m / v / g buffers (rank-dependent gradients), ``trials`` fused steps are
+    compared with the verified peer all-reduce followed by ``adam_flagged`` (same rank-order sum,
+    same update arithmetic: bitwise equal expected, tolerance 1e-6 relative), and the step counters
+    must agree. The verdict is all-reduced so every rank decides alike. In ``auto`` mode the fused
+    launch is also timed against the two separate launches and used only when faster (recorded in
+    LAST_SELECTION). Cached per peer region. False (the trainer keeps the two kernels) when the buffer
+    exceeds the fused kernel's slice table."""
+    key = (id(pa), int(numel))
+    if key in _FUSED:
+        return _FUSED[key]
+    from ..ops.lstm import chain_ctl
+    ops = pa.ops
+    dev = torch.device(device)
+    world = pa.world
+    ok = fused_adam_fits(numel)
+    fused_us = sep_us = None
+    if ok:
+        gen = torch.Generator(device="cpu").manual_seed(4321)
+        p0 = torch.randn(numel, generator=gen).to(dev)
+        m0 = (0.01 * torch.randn(numel, generator=gen)).to(dev)
+        v0 = (0.001 * torch.rand(numel, generator=gen)).to(dev)
+        gr = torch.Generator(device="cpu").manual_seed(77 + pa.rank)
+        lr = torch.tensor([1e-3], device=dev)
+        ext = chain_ctl(dev)
+        bufs = {}
+        for name in ("fused", "sep"):
+            bufs[name] = dict(p=p0.clone(), m=m0.clone(), v=v0.clone(), step=torch.zeros(1, device=dev),
+                              state=torch.tensor([0, 0, 1, 0, 0, 0, 0, 0], dtype=torch.int32, device=dev))
+
+        def fused(b, g):
+            return ops.adam_peer(b["p"], g, b["m"], b["v"], lr, b["step"], beta1, beta2, eps, 1.0 / world, 0.0,
+                                 b["state"], None, 1, pa.bases, pa.region, pa.rank, pa.cap)
+
+        def sep(b, g):
+            pa(g)
+            ops.adam_flagged(b["p"], g, b["m"], b["v"], lr, b["step"], beta1, beta2, eps, 1.0 / world, 0.0,
+                             b["state"], ext, None, 1)
+            return True
+
+        for _ in range(trials):
+            g = torch.randn(numel, generator=gr).to(dev)
+            g2 = g.clone()
+            ok &= bool(fused(bufs["fused"], g))
+            sep(bufs["sep"], g2)
+            torch.cuda.synchronize(dev)
+            ok &= not pa.timed_out() and bool((g == 0).all().item())
+        a, b = bufs["fused"], bufs["sep"]
+        for k in ("p", "m", "v"):
+            ok &= bool(torch.allclose(a[k], b[k], rtol=1e-6, atol=0.0))
+        ok &= float(a["step"].item()) == float(b["step"].item()) == float(trials)
+        if ok and peer_mode() == "auto":
+            g = torch.zeros(numel, device=dev)
+
+            def timed(fn, bb):
+                for _ in range(3):
+                    fn(bb, g)
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(n_time)]
+                for e0, e1 in ev:
+                    e0.record()
+                    fn(bb, g)
+                    e1.record()
+                torch.cuda.synchronize(dev)
+                return 1e3 * sum(e0.elapsed_time(e1) for e0, e1 in ev) / n_time
+            sep_us, fused_us = timed(sep, b), timed(fused, a)
+            t = torch.tensor([sep_us, fused_us], device=dev if D.backend() == "nccl" else "cpu", dtype=torch.float64)
+            D.all_reduce_(t, op=torch.distributed.ReduceOp.MAX, force=True)
+            sep_us, fused_us = float(t[0].item()), float(t[1].item())
+    flag = torch.tensor([0.0 if ok else 1.0], device=dev if D.backend() == "nccl" else "cpu")
+    D.all_reduce_(flag, force=True)
+    verified = float(flag.item()) == 0.0
+    use = verified and (fused_us is None or fused_us < sep_us)
+    LAST_SELECTION.update(fused_adam_verified=verified, fused_adam_us=fused_us, separate_adam_us=sep_us,
+                          fused_adam_selected=use)
+    if not verified and fused_adam_fits(numel):
+        import warnings
+        warnings.warn("adam_peer (peer reduction fused into Adam) failed its setup check: using the all-reduce "
+                      "kernel followed by adam_flagged")
+    _FUSED[key] = use
+    return use
+
+
 def close_all():
     """Close every cached peer region's peer mappings (process teardown)."""
     for pa in _CACHE.values():
         if pa is not None:
             pa.close()
     _CACHE.clear()
+    _FUSED.clear()
 
 
 def _make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
@@ -183,4 +286,5 @@ def _make_peer_allreduce(numel: int, device) -> Optional[PeerAllReduce]:
     return pa
 
 
-__all__ = ["PeerAllReduce", "make_peer_allreduce", "peer_enabled", "peer_mode", "close_all", "LAST_SELECTION"]
+__all__ = ["PeerAllReduce", "make_peer_allreduce", "peer_enabled", "peer_mode", "close_all", "LAST_SELECTION",
+           "check_fused_adam", "fused_adam_fits"]

@@ -125,8 +125,12 @@ class Trainer:
                          and os.environ.get("GNNQC_DP_GRAPH", "1") == "1")
         # flag-driven steps reduce over the peers inside the Adam launch (one launch, one pass over the
         # gradients; GNNQC_PEER_FUSED_ADAM=0 keeps the separate all-reduce kernel)
+        # (only after the fused kernel passed its own setup check against the two separate launches)
         if self.peer is not None and hasattr(self.opt, "peer") and os.environ.get("GNNQC_PEER_FUSED_ADAM", "1") == "1":
-            self.opt.peer = self.peer
+            from ..parallel.peer import check_fused_adam
+            if check_fused_adam(self.peer, self.opt.flat_g.numel(), self.device, self.opt.beta1, self.opt.beta2,
+                                self.opt.eps):
+                self.opt.peer = self.peer
         self.opt_graph = None
         self.static_wids = torch.full((self.batch_size,), -1, dtype=torch.long, device=self.device)
         self.last_loss = torch.zeros((), device=self.device)

@@ -19,7 +19,8 @@ def _bench(args, timeout=600, **env):
 
 
 def test_bench_spawns_ranks_and_reports_dp_line():
-    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--sensors", "8", "--days", "3"])
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--sensors", "8", "--days", "3",
+                "--cv-folds", "2", "--cv-epochs", "1"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout            # rank 0 only
@@ -29,6 +30,36 @@ def test_bench_spawns_ranks_and_reports_dp_line():
     assert out["value"] > 0 and out["ms_per_step"] > 0
     ig = out["ig"]
     assert ig["n_ranks"] == 2 and ig["value"] > 0 and ig["sharding"].startswith("round-robin")
+    cv = out["cv"]                              # the headline's ROC-AUC half: every fold run exactly once
+    assert cv["folds"] == 2 and cv["epochs"] == 1 and cv["fold_per_rank"] is True
+    for m in ("gcn", "baseline"):
+        assert cv[f"{m}_folds_run"] == [0, 1]
+        assert len(cv[f"{m}_fold_auc"]) == 2 and 0.0 <= cv[f"{m}_mean_auc"] <= 1.0
+    assert cv["seconds"] > 0 and cv["dtype"] == "bf16"
+
+
+def test_bench_parent_never_initialises_hip():
+    """The spawning parent must not call torch.cuda at all (on ROCm device_count() falls back to
+    hipGetDeviceCount without amdsmi, initialising HIP in a process that then forks its ranks): run
+    the parent with every such entry point poisoned; the children are fresh interpreters."""
+    boot = ("import sys, runpy, torch\n"
+            "def boom(*a, **k):\n"
+            "    raise RuntimeError('parent touched torch.cuda')\n"
+            "for name in ('device_count', '_lazy_init', 'is_available', 'init', 'set_device'):\n"
+            "    setattr(torch.cuda, name, boom)\n"
+            "torch._C._cuda_getDeviceCount = boom\n"
+            "sys.argv = [sys.argv[1]] + sys.argv[2:]\n"
+            "runpy.run_path(sys.argv[0], run_name='__main__')\n")
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", boot, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--sensors", "8", "--days", "3", "--no-ig-line", "--no-cv-line",
+                        "--no-knn-line"], cwd=ROOT, env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
 
 
 def test_bench_world_size_mismatch_fails():

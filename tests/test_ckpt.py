@@ -212,3 +212,42 @@ def test_object_graph_paths_match_reference():
     for k in ref_keys:
         assert _resolve(ref_nodes, k) == [k]
         assert _resolve(nodes, k) == [k]
+
+
+def test_saved_model_pb_mirrors_object_graph(tmp_path):
+    """saved_model.pb (best effort; no reference file exists to pin parity): one meta graph
+    tagged 'serve', V2 saver, and a SavedObjectGraph whose nodes are the bundle's object graph node for
+    node - same ids, same children - with variable records matching the stored tensors."""
+    from gnnqc.ckpt.saved_model import read_saved_model_summary
+    model, pc, mc = _model()
+    opt = FlatAdam(model.parameters(), lr=1e-3)
+    save_model(model, str(tmp_path), optimizer=opt, epoch=0, preproc_config=pc)
+    sm = read_saved_model_summary(str(tmp_path))
+    assert sm["schema_version"] == 1 and len(sm["meta_graphs"]) == 1
+    mg = sm["meta_graphs"][0]
+    assert mg["tags"] == ["serve"] and mg["saver_version"] == 2 and mg["tensorflow_version"].startswith("2.11")
+    b = read_bundle(str(tmp_path / "variables" / "variables"))
+    og = _graph_nodes(b["_CHECKPOINTABLE_OBJECT_GRAPH"])
+    ent = bundle_entries(str(tmp_path / "variables" / "variables"))
+    assert ent["optimizer/_iterations/.ATTRIBUTES/VARIABLE_VALUE"]["shape"] == []     # scalars: shape [] like
+    assert ent["optimizer/_learning_rate/.ATTRIBUTES/VARIABLE_VALUE"]["shape"] == []  # the reference's bundle
+    nodes = mg["nodes"]
+    assert len(nodes) == len(og)
+    n_train = 0
+    for i, (n, (ch, at)) in enumerate(zip(nodes, og)):
+        assert n["children"] == ch, i
+        if at:                                   # a variable node of the object graph
+            key = at[0][3]
+            assert n["kind"] == "variable" and n["name"] + "/.ATTRIBUTES/VARIABLE_VALUE" == key
+            assert n["dtype"] == ent[key]["dtype"] and n.get("shape", []) == list(ent[key]["shape"]), key
+            n_train += n["trainable"]
+        else:
+            assert n["kind"] == "user_object"
+    assert nodes[0]["identifier"] == "_tf_keras_model"
+    assert n_train == sum(1 for p in model.parameters() if p.requires_grad)
+    # every checkpoint key resolves along the SavedObjectGraph's own children too
+    for k in (k for k in b if k.endswith("/.ATTRIBUTES/VARIABLE_VALUE")):
+        node = 0
+        for part in k.split("/.ATTRIBUTES/")[0].split("/"):
+            node = dict((nm, j) for j, nm in nodes[node]["children"])[part]
+        assert nodes[node]["kind"] == "variable"
