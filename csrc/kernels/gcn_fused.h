@@ -5,6 +5,8 @@
 #pragma once
 #include "common.h"
 
+#include <vector>
+
 namespace gq {
 
 int* chain_ctl(int dev);   // lstm_chain.hip: word 7 = a gradient producer saw a non-finite value
@@ -85,6 +87,156 @@ struct GcnBwdJob {
   float* dalpha;
   int* nf;                                         // chain control word 7 (non-finite gradient)
 };
+
+// The closed form of gcn_glue.hip gcn_bwd_finalize_kernel (training) for feature f, applied to the
+// raw partial sums tot = (A = sum dy, Z = sum dy z, P = sum da y[y <= 0], Q_k = sum x_k dy) of any
+// subset of the rows (it is linear in them), added with float atomics; a non-finite contribution
+// raises the step's non-finite flag (chain control word 7)
+template <int Cin, int F>
+__device__ __forceinline__ void gcn_bwd_apply(const float (&tot)[3 + Cin], int f, const double* __restrict__ Sg,
+                                              const float* __restrict__ st, const float* __restrict__ W,
+                                              const float* __restrict__ bias, float* dW, float* dgamma, float* dbeta,
+                                              float* dalpha, int* nf) {
+  const float mu = st[f], inv = st[F + f], scf = st[2 * F + f];
+  const float A = tot[0], Z = tot[1], P = tot[2];
+  const float dg = inv * (Z - mu * A);
+  bool fin = isfinite(A) && isfinite(dg) && isfinite(P);
+  atomicAdd(dbeta + f, A);
+  atomicAdd(dgamma + f, dg);
+  atomicAdd(dalpha + f, P);
+  const double n = fmax(Sg[Cin + Cin * Cin], 1.0);
+  const double bf = bias[f];
+#pragma unroll
+  for (int k = 0; k < Cin; ++k) {
+    double s2w = 0.0;
+#pragma unroll
+    for (int l = 0; l < Cin; ++l) s2w += Sg[Cin + k * Cin + l] * (double)W[l * F + f];
+    const double s1 = Sg[k];
+    const double sxx = inv * (s2w + s1 * (bf - mu));
+    const float d = (float)(scf * (tot[3 + k] - s1 * A / n - sxx * dg / n));
+    fin = fin && isfinite(d);
+    atomicAdd(dW + k * F + f, d);
+  }
+  if (!fin) __hip_atomic_store(nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- the backward coefficients (gcn_fused_fwd_kernel COEF) as a side job: one workgroup of
+// blockDim.x threads (a multiple of 256) per sample row b of [0, Mp), all T steps, from the store and
+// the BatchNorm statistics st [4][F] (mu, inv, scale, shift) the forward kernel wrote. Run by spare
+// workgroups of the LSTM chain forward launch (its stages leave most CUs idle), or on its own.
+struct GcnCoefFwdJob {
+  GfData D;
+  int B, Mp, on;
+  const float* st;
+  const float* W;
+  const float* bias;
+  const float* alpha;
+  float* coef;                                     // [T][Mp][(3 + Cin) F]
+};
+
+constexpr int GCF_LDS_FLOATS = 16384;              // staged slab (64 KB): rows per pass = this / (N Cin)
+
+struct GcnCoefFwdLds {
+  static constexpr int BYTES = (GCF_LDS_FLOATS + 4 * GF_ROW_MAX) * 4;
+};
+
+// host: a coefficient job left by gcn_fused_fwd for the next chain forward launch (gcn_fused.hip)
+struct GcnPending {
+  GcnCoefFwdJob job;
+  std::vector<at::Tensor> keep;
+};
+bool gcn_coef_side_mode();
+GcnPending& gcn_pending(int dev);
+bool gcn_coef_take(int dev, GcnCoefFwdJob& job, std::vector<at::Tensor>& keep);
+
+template <int Cin, int F>
+__device__ __forceinline__ void gcn_coef_fwd_body(const GcnCoefFwdJob& J, int b, char* smem) {
+  constexpr int NA = 3 + Cin;
+  static_assert(F % 4 == 0, "feature quads");
+  const GfData& D = J.D;
+  const int tid = threadIdx.x, nthr = blockDim.x, N = D.N, T = D.T, NC = N * Cin;
+  float* sx = reinterpret_cast<float*>(smem);                       // [GCF_LDS_FLOATS]
+  float* svm = sx + GCF_LDS_FLOATS;                                  // [GF_ROW_MAX] x 4
+  float* spw = svm + GF_ROW_MAX;
+  float* ssh = spw + GF_ROW_MAX;
+  float* ssc = ssh + GF_ROW_MAX;
+  const long wraw = b < J.B ? gf_ids(D, J.B)[b] : -1;
+  if (wraw < 0) {                                   // padding sample / row: zero coefficients
+    for (long i = tid; i < (long)T * NA * F; i += nthr) {
+      const long t = i / (NA * F);
+      J.coef[(t * J.Mp + b) * (NA * F) + i % (NA * F)] = 0.f;
+    }
+    return;
+  }
+  const long w = wraw, g = D.wg[w], c0 = D.wc[w];
+  const long tn = D.time_norm ? c0 : 0;
+  if (tid < N) {
+    svm[tid] = D.wv[w * N + tid] ? 1.f : 0.f;
+    spw[tid] = D.pw[w * N + tid];
+  }
+  if (tid < NC) {
+    ssh[tid] = D.shift[(g * D.Tn + tn) * (long)NC + tid];
+    ssc[tid] = D.scale[(g * D.Tn + tn) * (long)NC + tid];
+  }
+  // thread -> (row lane rl, feature quad fq): F / 4 quads per row
+  constexpr int QPR = F / 4;
+  const int fq = tid % QPR, rl = tid / QPR, rlanes = nthr / QPR;
+  float rw[Cin][4], rb[4], scv[4], shv[4], al[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = 4 * fq + j;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) rw[k][j] = J.W[k * F + f];
+    rb[j] = J.bias[f];
+    scv[j] = J.st[2 * F + f];
+    shv[j] = J.st[3 * F + f];
+    al[j] = J.alpha[f];
+  }
+  const float* src = D.series + (g * D.Ttot + (c0 - D.tb)) * (long)NC;
+  const int RP = max(1, min(GCF_LDS_FLOATS / NC, rlanes));
+  __syncthreads();
+  for (int p0 = 0; p0 < T; p0 += RP) {
+    const int nr = min(RP, T - p0);
+    if (p0 > 0) __syncthreads();                  // previous pass's LDS reads are done
+    for (int i = tid; i < nr * NC; i += nthr) {
+      const int e = i % NC;
+      sx[i] = (src[(long)p0 * NC + i] - ssh[e]) * ssc[e] * svm[e / Cin];
+    }
+    __syncthreads();
+    for (int rr = rl; rr < nr; rr += rlanes) {
+      float cf[NA][4];
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cf[a][j] = 0.f;
+      const float* xr = sx + rr * NC;
+      for (int n = 0; n < N; ++n) {
+        const float wn = spw[n];
+        float xv[Cin];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float z = rb[j];
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) z += xv[k] * rw[k][j];
+          const float yv = z * scv[j] + shv[j];
+          const bool pos = yv > 0.f;
+          const float dp = pos ? wn : al[j] * wn;
+          cf[0][j] += dp;
+          cf[1][j] += dp * z;
+          cf[2][j] += pos ? 0.f : wn * yv;
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) cf[3 + k][j] += dp * xv[k];
+        }
+      }
+      float* co = J.coef + ((long)(p0 + rr) * J.Mp + b) * (NA * F) + 4 * fq;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        *reinterpret_cast<float4*>(co + a * F) = make_float4(cf[a][0], cf[a][1], cf[a][2], cf[a][3]);
+    }
+  }
+}
 
 template <int Cin, int F>
 struct GcnBwdLds {
@@ -231,28 +383,74 @@ __device__ __forceinline__ void gcn_fused_bwd_body(const GcnBwdJob J, int bx, in
   float tot[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) tot[a] = (red[0][a][f] + red[1][a][f]) + (red[2][a][f] + red[3][a][f]);
-  // the closed form of gcn_glue.hip gcn_bwd_finalize_kernel (training), applied to this partial
-  const float mu = st[f], inv = st[F + f], scf = st[2 * F + f];
-  const float A = tot[0], Z = tot[1], P = tot[2];
-  const float dg = inv * (Z - mu * A);
-  bool fin = isfinite(A) && isfinite(dg) && isfinite(P);
-  atomicAdd(dbeta + f, A);
-  atomicAdd(dgamma + f, dg);
-  atomicAdd(dalpha + f, P);
-  const double n = fmax(Sg[Cin + Cin * Cin], 1.0);
-  const double bf = bias[f];
+  gcn_bwd_apply<Cin, F>(tot, f, Sg, st, W, bias, dW, dgamma, dbeta, dalpha, nf);
+}
+
+// ---- backward from the forward's coefficients (gcn_fused_fwd_kernel COEF): the partial sums are
+// sum over rows of dh[row][c_off + f] * coef[row][a][f], a streaming dot product over [T * Mp] rows.
+// Workgroup bx of nblocks (256 threads: 16 rows x 16 features per pass, F = 16) sums its row range
+// and adds the closed form of its partial with float atomics.
+struct GcnCoefJob {
+  const float* dh;                                 // [>= T][Mp][Dh]
+  const float* coef;                               // [T][Mp][(3 + Cin) F]
+  long rows;                                       // T * Mp
+  int Dh, c_off, nblocks, key;                     // key = Cin * 64 + F
+  const double* Sg;
+  const float* st;
+  const float* W;
+  const float* bias;
+  float* dW;
+  float* dgamma;
+  float* dbeta;
+  float* dalpha;
+  int* nf;
+};
+
+template <int Cin, int F>
+__device__ __forceinline__ void gcn_coef_bwd_body(const GcnCoefJob& J, int bx) {
+  constexpr int NA = 3 + Cin, RPP = 256 / F;
+  static_assert(256 % F == 0 && F <= 64 && 64 % F == 0, "rows per pass");
+  __shared__ float red[4][NA][F];
+  const int tid = threadIdx.x, f = tid % F, rl = tid / F;
+  const long per = (J.rows + J.nblocks - 1) / J.nblocks;
+  const long r0 = (long)bx * per, r1 = min(J.rows, r0 + per);
+  float acc[NA];
 #pragma unroll
-  for (int k = 0; k < Cin; ++k) {
-    double s2w = 0.0;
+  for (int a = 0; a < NA; ++a) acc[a] = 0.f;
+  long r = r0 + rl;
+  for (; r + 3 * RPP < r1; r += 4 * RPP) {         // four rows in flight per thread
+    float g[4], c[4][NA];
 #pragma unroll
-    for (int l = 0; l < Cin; ++l) s2w += Sg[Cin + k * Cin + l] * (double)W[l * F + f];
-    const double s1 = Sg[k];
-    const double sxx = inv * (s2w + s1 * (bf - mu));
-    const float d = (float)(scf * (tot[3 + k] - s1 * A / n - sxx * dg / n));
-    fin = fin && isfinite(d);
-    atomicAdd(dW + k * F + f, d);
+    for (int u = 0; u < 4; ++u) {
+      const long ru = r + u * RPP;
+      g[u] = J.dh[ru * J.Dh + J.c_off + f];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) c[u][a] = J.coef[ru * (NA * F) + a * F + f];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) acc[a] += g[u] * c[u][a];
   }
-  if (!fin) __hip_atomic_store(nf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (; r < r1; r += RPP) {
+    const float g = J.dh[r * J.Dh + J.c_off + f];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) acc[a] += g * J.coef[r * (NA * F) + a * F + f];
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    float x = acc[a];
+#pragma unroll
+    for (int o = 32; o >= F; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane < F) red[wv][a][lane] = x;
+  }
+  __syncthreads();
+  if (tid >= F) return;
+  float tot[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) tot[a] = (red[0][a][f] + red[1][a][f]) + (red[2][a][f] + red[3][a][f]);
+  gcn_bwd_apply<Cin, F>(tot, f, J.Sg, J.st, J.W, J.bias, J.dW, J.dgamma, J.dbeta, J.dalpha, J.nf);
 }
 
 }  // namespace gq

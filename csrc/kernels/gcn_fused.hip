@@ -108,21 +108,32 @@ __global__ __launch_bounds__(256) void gcn_window_prep_kernel(GfData D, const fl
 }
 
 // ---- forward: grid (Mp, NY), 256 threads
-template <int Cin, int F>
+// COEF (training): also the backward coefficients of every (t, sample, feature f), written to
+// coef [T][Mp][NA][F] (NA = 3 + Cin), with dpos_n = w_n (y_nf > 0 ? 1 : alpha_f) over the nodes n:
+//   c0 = sum dpos_n, c1 = sum dpos_n z_nf, c2 = sum_{y_nf <= 0} w_n y_nf, c3+k = sum dpos_n x_nk
+// (z = x W + b before BatchNorm, y after it). The parameter gradient's partial sums of
+// gcn_fused_bwd_body are these times the pooled channel's upstream gradient dh[t][b][f], so the
+// backward becomes a streaming dot product (gcn_coef_bwd_body) with no window gather, slab staging
+// or per-node recompute behind the LSTM backward.
+template <int Cin, int F, bool COEF>
 __global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
     GfData D, int B, int Mp, int Cp, int rows, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ alpha,
     float* __restrict__ rmean, float* __restrict__ rvar, int training, float momentum, float eps,
     float* __restrict__ out, double* __restrict__ Sout, float* __restrict__ st, float* __restrict__ y,
-    float* __restrict__ ym, long* __restrict__ wid_out) {
+    float* __restrict__ ym, long* __restrict__ wid_out, float* __restrict__ coef) {
   constexpr int nstat = Cin + Cin * Cin + 1;
   constexpr int FQ = F / 4;
   constexpr int Ca = Cin;
+  constexpr int NA = 3 + Cin;
   const int b = blockIdx.x, tid = threadIdx.x, N = D.N, T = D.T;
   const int t0 = blockIdx.y * rows, t1 = min(T, t0 + rows);
   if (b >= B) {                                   // padding sequences of the time-major input: zeros
-    for (int t = t0; t < t1; ++t)
+    for (int t = t0; t < t1; ++t) {
       for (int c = tid; c < Cp; c += 256) out[((long)t * Mp + b) * Cp + c] = 0.f;
+      if constexpr (COEF)
+        for (int c = tid; c < NA * F; c += 256) coef[((long)t * Mp + b) * (NA * F) + c] = 0.f;
+    }
     return;
   }
   __shared__ double dred[4][nstat];
@@ -247,12 +258,18 @@ __global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
   const int ap = apl < 0 ? 0 : (int)apl;
   const int r = tid >> 2, q = tid & 3, f0 = q * FQ;
   float pwk[Cin][FQ], pb[FQ], pal[FQ];
+  float rwk[COEF ? Cin : 1][FQ], rb[FQ];           // COEF: the raw W, b (z before BatchNorm)
 #pragma unroll
   for (int j = 0; j < FQ; ++j) {
 #pragma unroll
     for (int k = 0; k < Cin; ++k) pwk[k][j] = prm[k][f0 + j];
     pb[j] = prm[Cin][f0 + j];
     pal[j] = prm[Cin + 1][f0 + j];
+    if constexpr (COEF) {
+#pragma unroll
+      for (int k = 0; k < Cin; ++k) rwk[k][j] = W[k * F + f0 + j];
+      rb[j] = bias[f0 + j];
+    }
   }
   for (int p0 = t0; p0 < t1; p0 += RP) {
     if (p0 != t0) {                               // (more rows than one pass: stage the next slab)
@@ -265,8 +282,13 @@ __global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
     for (int rr = r; rr < nr; rr += 64) {
       const int t = p0 + rr;
       float acc[FQ];
+      float cf[COEF ? NA : 1][FQ];
 #pragma unroll
-      for (int j = 0; j < FQ; ++j) acc[j] = 0.f;
+      for (int j = 0; j < FQ; ++j) {
+        acc[j] = 0.f;
+#pragma unroll
+        for (int a = 0; a < (COEF ? NA : 1); ++a) cf[a][j] = 0.f;
+      }
       const float* xr = sx + rr * NC;
       for (int n = 0; n < N; ++n) {
         const float wn = spw[n];
@@ -278,7 +300,19 @@ __global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
           float yv = pb[j];
 #pragma unroll
           for (int k = 0; k < Cin; ++k) yv += xv[k] * pwk[k][j];
-          acc[j] += wn * (yv > 0.f ? yv : pal[j] * yv);
+          const bool pos = yv > 0.f;
+          acc[j] += wn * (pos ? yv : pal[j] * yv);
+          if constexpr (COEF) {
+            float z = rb[j];
+#pragma unroll
+            for (int k = 0; k < Cin; ++k) z += xv[k] * rwk[k][j];
+            const float dp = pos ? wn : pal[j] * wn;
+            cf[0][j] += dp;
+            cf[1][j] += dp * z;
+            cf[2][j] += pos ? 0.f : wn * yv;
+#pragma unroll
+            for (int k = 0; k < Cin; ++k) cf[3 + k][j] += dp * xv[k];
+          }
         }
       }
       float* o = out + ((long)t * Mp + b) * Cp;
@@ -286,6 +320,18 @@ __global__ __launch_bounds__(256) void gcn_fused_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < FQ; ++j) o[Ca + f0 + j] = acc[j];
       for (int c = Ca + F + q; c < Cp; c += 4) o[c] = 0.f;
+      if constexpr (COEF) {
+        float* co = coef + ((long)t * Mp + b) * (NA * F) + f0;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          if constexpr (FQ == 4) {
+            *reinterpret_cast<float4*>(co + a * F) = make_float4(cf[a][0], cf[a][1], cf[a][2], cf[a][3]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < FQ; ++j) co[a * F + j] = cf[a][j];
+          }
+        }
+      }
     }
   }
 }
@@ -420,7 +466,7 @@ std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor
                                       bool time_norm, const at::Tensor& W, const at::Tensor& bias,
                                       const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& alpha,
                                       at::Tensor rmean, at::Tensor rvar, bool training, double momentum, double eps,
-                                      int64_t Mp, int64_t Cp) {
+                                      int64_t Mp, int64_t Cp, bool with_coef) {
   int B = 0;
   GfData D = gf_data(series, shift, scale, win_group, win_center, win_valid, win_label, group_anom_pos, mom, pw,
                      wids, table, cursor, tb, seq_len, time_norm, B);
@@ -441,13 +487,81 @@ std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor
   at::Tensor wid = at::empty({B}, win_group.options());
   int ny, rows;
   gf_grid(T, D.N * C, ny, rows);
-  GQ_GF_CIN(C, GQ_GF_F(F, hipLaunchKernelGGL((gcn_fused_fwd_kernel<CIN, FF>), dim3(Mp, ny), dim3(256), 0, stream(),
-      D, B, (int)Mp, (int)Cp, rows, W.data_ptr<float>(), bias.data_ptr<float>(), gamma.data_ptr<float>(),
-      beta.data_ptr<float>(), alpha.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
-      training ? 1 : 0, (float)momentum, (float)eps, out.data_ptr<float>(), training ? S.data_ptr<double>() : nullptr,
-      st.data_ptr<float>(), y.data_ptr<float>(), ym.data_ptr<float>(), wid.data_ptr<long>())));
+  // (the coefficient form: the CML configuration, 2 inputs / 16 features, training only). Side mode
+  // (default): the coefficients are left to spare workgroups of the next LSTM chain forward launch
+  // (gcn_coef_take), which runs while this kernel's output is consumed; else this kernel writes them.
+  const bool want = with_coef && training && C == 2 && F == 16;
+  at::Tensor coef = at::empty({want ? T : 0, want ? Mp : 0, (3 + C) * F}, fo);
+  const bool side = want && gcn_coef_side_mode();
+  const bool cf = want && !side;
+#define GQ_GF_FWD(CINV, FV, CFV)                                                                                      \
+  hipLaunchKernelGGL((gcn_fused_fwd_kernel<CINV, FV, CFV>), dim3(Mp, ny), dim3(256), 0, stream(), D, B, (int)Mp,      \
+      (int)Cp, rows, W.data_ptr<float>(), bias.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),    \
+      alpha.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), training ? 1 : 0, (float)momentum,     \
+      (float)eps, out.data_ptr<float>(), training ? S.data_ptr<double>() : nullptr, st.data_ptr<float>(),             \
+      y.data_ptr<float>(), ym.data_ptr<float>(), wid.data_ptr<long>(), cf ? coef.data_ptr<float>() : nullptr)
+  if (cf) GQ_GF_FWD(2, 16, true);
+  else GQ_GF_CIN(C, GQ_GF_F(F, GQ_GF_FWD(CIN, FF, false)));
+#undef GQ_GF_FWD
   GQ_LAUNCH_CHECK();
-  return {out, S, st, y, ym, wid};
+  if (side) {
+    GcnPending& pd = gcn_pending(series.get_device());
+    pd.job = GcnCoefFwdJob{};
+    pd.job.D = D;
+    pd.job.B = B;
+    pd.job.Mp = (int)Mp;
+    pd.job.on = 1;
+    pd.job.st = st.data_ptr<float>();
+    pd.job.W = W.data_ptr<float>();
+    pd.job.bias = bias.data_ptr<float>();
+    pd.job.alpha = alpha.data_ptr<float>();
+    pd.job.coef = coef.data_ptr<float>();
+    // (the tensors the job reads or writes stay referenced until it has been launched)
+    pd.keep = {coef, st, W, bias, alpha, series, shift, scale, win_group, win_center, win_valid, pw, wids, table};
+    if (cursor.has_value() && cursor->defined()) pd.keep.push_back(*cursor);
+  }
+  return {out, S, st, y, ym, wid, coef};
+}
+
+// ---- pending coefficient side job (per device)
+bool gcn_coef_side_mode() {
+  const char* e = std::getenv("GNNQC_GCN_COEF_SIDE");
+  return e == nullptr || std::atoi(e) != 0;
+}
+
+GcnPending& gcn_pending(int dev) {
+  static GcnPending slots[64];
+  TORCH_CHECK(dev >= 0 && dev < 64, "gcn_fused: device index");
+  return slots[dev];
+}
+
+// the pending job of the current device, handed to a launch that runs it (chain forward); clears it
+bool gcn_coef_take(int dev, GcnCoefFwdJob& job, std::vector<at::Tensor>& keep) {
+  GcnPending& pd = gcn_pending(dev);
+  if (!pd.job.on) return false;
+  job = pd.job;
+  keep.insert(keep.end(), pd.keep.begin(), pd.keep.end());
+  pd.job.on = 0;
+  pd.keep.clear();
+  return true;
+}
+
+__global__ __launch_bounds__(1024) void gcn_coef_fwd_kernel(GcnCoefFwdJob J) {
+  __shared__ __attribute__((aligned(16))) char smem[GcnCoefFwdLds::BYTES];
+  gcn_coef_fwd_body<2, 16>(J, blockIdx.x, smem);
+}
+
+// run the pending coefficient job on its own (nothing consumed it: no chain forward in between);
+// returns whether there was one
+bool gcn_coef_flush(const at::Tensor& like) {
+  TORCH_CHECK(like.is_cuda(), "gcn_coef_flush: a GPU tensor names the device");
+  c10::DeviceGuard guard(like.device());
+  GcnCoefFwdJob J{};
+  std::vector<at::Tensor> keep;
+  if (!gcn_coef_take(like.get_device(), J, keep)) return false;
+  hipLaunchKernelGGL(gcn_coef_fwd_kernel, dim3(J.Mp), dim3(1024), 0, stream(), J);
+  GQ_LAUNCH_CHECK();
+  return true;
 }
 
 // The training backward's job (gcn_fused_bwd_body): adds dW, dgamma, dbeta, dalpha (float atomics)
@@ -499,6 +613,56 @@ GcnBwdJob gcn_bwd_job(const at::Tensor& dh, int64_t c_off, const at::Tensor& ser
   return J;
 }
 
+// The coefficient-form backward's job: dh [>= T, Mp, Dh] channels [c_off, c_off + F) against coef
+// [T, Mp, (3 + Cin) F] of gcn_fused_fwd(with_coef); nblocks workgroups of 256 threads.
+GcnCoefJob gcn_coef_job(const at::Tensor& dh, int64_t c_off, const at::Tensor& coef, const at::Tensor& S,
+                        const at::Tensor& st, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& dW,
+                        const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dalpha) {
+  check_f32_cuda(dh, "dh");
+  check_f32_cuda(coef, "coef");
+  for (const at::Tensor* t : {&st, &W, &bias, &dW, &dgamma, &dbeta, &dalpha}) check_f32_cuda(*t, "gcn_coef_bwd operand");
+  const int C = (int)W.size(0), F = (int)W.size(1);
+  TORCH_CHECK(C == 2 && F == 16, "gcn_coef_bwd: the CML configuration (2 inputs, 16 features)");
+  TORCH_CHECK(coef.dim() == 3 && coef.size(2) == (3 + C) * F, "gcn_coef_bwd: coef [T, Mp, (3 + Cin) F]");
+  const long T = coef.size(0), Mp = coef.size(1);
+  TORCH_CHECK(dh.dim() == 3 && dh.size(0) >= T && dh.size(1) == Mp && dh.size(2) >= c_off + F,
+              "gcn_coef_bwd: dh [>= T, Mp, Dh] with the coefficients' T and Mp");
+  TORCH_CHECK(S.is_cuda() && S.scalar_type() == at::kDouble && S.numel() == C + C * C + 1, "gcn_coef_bwd: S");
+  TORCH_CHECK(dW.numel() == (long)C * F && dgamma.numel() == F && dbeta.numel() == F && dalpha.numel() == F &&
+                  st.numel() == 4 * F, "gcn_coef_bwd: gradient shapes");
+  GcnCoefJob J{};
+  J.dh = dh.data_ptr<float>();
+  J.coef = coef.data_ptr<float>();
+  J.rows = T * Mp;
+  J.Dh = (int)dh.size(2);
+  J.c_off = (int)c_off;
+  // ~180 rows per workgroup (the CML step: 128 workgroups over 23k rows): every workgroup's loads
+  // are one short burst, and 128 x 80 atomics onto 80 gradients stay cheap
+  J.nblocks = (int)std::max<long>(1, std::min<long>(256, (J.rows + 179) / 180));
+  J.key = C * 64 + F;
+  J.Sg = S.data_ptr<double>();
+  J.st = st.data_ptr<float>();
+  J.W = W.data_ptr<float>();
+  J.bias = bias.data_ptr<float>();
+  J.dW = dW.data_ptr<float>();
+  J.dgamma = dgamma.data_ptr<float>();
+  J.dbeta = dbeta.data_ptr<float>();
+  J.dalpha = dalpha.data_ptr<float>();
+  J.nf = chain_ctl(dh.get_device()) + 7;
+  return J;
+}
+
+__global__ __launch_bounds__(256) void gcn_coef_bwd_kernel(GcnCoefJob J) { gcn_coef_bwd_body<2, 16>(J, blockIdx.x); }
+
+void gcn_coef_bwd(const at::Tensor& dh, int64_t c_off, const at::Tensor& coef, const at::Tensor& S,
+                  const at::Tensor& st, const at::Tensor& W, const at::Tensor& bias, at::Tensor dW, at::Tensor dgamma,
+                  at::Tensor dbeta, at::Tensor dalpha) {
+  c10::DeviceGuard guard(dh.device());
+  const GcnCoefJob J = gcn_coef_job(dh, c_off, coef, S, st, W, bias, dW, dgamma, dbeta, dalpha);
+  if (J.rows > 0) hipLaunchKernelGGL(gcn_coef_bwd_kernel, dim3(J.nblocks), dim3(256), 0, stream(), J);
+  GQ_LAUNCH_CHECK();
+}
+
 void gcn_fused_bwd(const at::Tensor& dh, int64_t c_off, const at::Tensor& series, const at::Tensor& shift,
                    const at::Tensor& scale, const at::Tensor& win_group, const at::Tensor& win_center,
                    const at::Tensor& win_valid, const at::Tensor& group_anom_pos, const at::Tensor& pw,
@@ -524,4 +688,6 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("gcn_window_prep", &gq::gcn_window_prep);
   m.impl("gcn_fused_fwd", &gq::gcn_fused_fwd);
   m.impl("gcn_fused_bwd", &gq::gcn_fused_bwd);
+  m.impl("gcn_coef_bwd", &gq::gcn_coef_bwd);
+  m.impl("gcn_coef_flush", &gq::gcn_coef_flush);
 }

@@ -31,6 +31,7 @@
 // the backward, pooled output + argmax bytes), so the backward is unchanged.
 #include "chain_head.h"
 #include "common.h"
+#include "gcn_fused.h"
 #include "lstm_grads_body.h"
 #include "lstm_tm_common.h"
 
@@ -135,7 +136,11 @@ struct ChainArgs {
   const float* pkW;
   bf16x8_t* pk;
   int pkDw;
+  int npk;                           // packing workgroups
   ChainT4 t4;                        // t4.on: time4 + head as one more stage (blocks [ns nt8, (ns + 1) nt8))
+  // side job on the idle CUs: the GCN backward's coefficients (gcn_fused.h gcn_coef_fwd_body), one
+  // workgroup per sample row; it only reads the store and writes its own buffer, nothing waits on it
+  GcnCoefFwdJob cf;
 };
 
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
@@ -928,8 +933,12 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
       }
       r -= A.nt8;
     }
-    const int f = r * 1024 + (int)threadIdx.x;    // packing workgroups
-    if (A.pk != nullptr && f < T4PK_ALL) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
+    if (r < A.npk) {
+      const int f = r * 1024 + (int)threadIdx.x;  // packing workgroups
+      if (A.pk != nullptr && f < T4PK_ALL) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
+    } else if (A.cf.on && r - A.npk < A.cf.Mp) {  // GCN backward coefficients of sample row r - npk
+      gcn_coef_fwd_body<2, 16>(A.cf, r - A.npk, smem);
+    }
     chain_finish(A.ctl, nblk);
     return;
   }
@@ -1069,6 +1078,10 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
                              // measured slower (bottom stages end 123 / 140 vs 113 / 117 us, bench 0.307 vs
                              // 0.286 ms/step): the I/O waves' staging and load issue hold up the step barrier
 #endif
+#ifndef CHAINB_DXW
+#define CHAINB_DXW 1         // H = 16 stages: dx = W dz by a dedicated wave (not by compute waves 0 / 1 between
+                             // the step's MFMA and the next cell phase, which put it on the recurrence's path)
+#endif
 #ifndef CHAINB_G
 #define CHAINB_G 2           // waves per backward I/O group: 2 = one for the cell records, one for dh
 #endif
@@ -1082,6 +1095,12 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #ifndef CHAINB_D64
 #define CHAINB_D64 2
 #endif
+// threads of a backward stage workgroup: compute waves (+ the publisher wave when it fits, + the dx
+// wave of the split-free H = 16 stages)
+__host__ __device__ constexpr bool chainb_dxw(int h) { return CHAINB_DXW && h < 32 && TMC<16>::NT + 128 <= 1024; }
+__host__ __device__ constexpr int chainb_live_threads(int h, int nt) {
+  return nt + (nt + 64 <= 1024 ? 64 : 0) + (chainb_dxw(h) ? 64 : 0);
+}
 
 // lstm_tm_bwd_body (DZ + DX) with one dh element per lane from the stage above's stream
 // (or, stage 0, from global memory), un-pooled on load, and dx published element-wise.
@@ -1118,6 +1137,52 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   // step time). The publisher joins the same barriers and reads the dx tile from LDS.
   const int row0 = tile * 16;
   constexpr bool PUBW = NT + 64 <= 1024;
+  constexpr bool DXW = !SK && chainb_dxw(H);
+  static_assert(!DXW || PUBW, "the dx wave hands its tiles to the publisher");
+  if constexpr (DXW) {
+    // dx wave: after step s's barrier, dx^T = W dz^T of that step from zs[s & 1] into dxs[s & 1]
+    // (the publisher stores it after the next barrier, as before). It joins barrier s + 1 only once
+    // done, and zs[s & 1] is rewritten only in step s + 2's cell phase (after barrier s + 1), so the
+    // compute waves go from their dh_rec MFMA straight to the next cell phase.
+    if (tid >= NT + 64) {
+      const int col = lane & 15, quad = lane >> 4;
+      bf16x8_t wx[NXB][KB];
+#pragma unroll
+      for (int xb = 0; xb < NXB; ++xb) {
+        const int din = 16 * xb + col;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          bf16x8_t v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = (__bf16)(S.W[(size_t)min(din, Dw - 1) * G4 + 32 * k + 8 * quad + j] * (din < Dw ? 1.f : 0.f));
+          wx[xb][k] = v;
+        }
+      }
+      const int nsteps = (T + D - 1) / D * D;
+      __syncthreads();
+      __syncthreads();
+      for (int s = 0; s < nsteps; ++s) {
+        lds_barrier();
+        if (s < T) {
+          const int p = s & 1;
+          bf16x8_t bz[KB];
+#pragma unroll
+          for (int k = 0; k < KB; ++k) bz[k] = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+#pragma unroll
+          for (int xb = 0; xb < NXB; ++xb) {
+            f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < KB; ++k) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wx[xb][k], bz[k], a, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dxs[p][col][16 * xb + 4 * quad + r] = a[r];
+          }
+        }
+      }
+      __syncthreads();
+      return;
+    }
+  }
   if constexpr (PUBW) {
     if (tid >= NT) {
       const int nsteps = (T + D - 1) / D * D;
@@ -1219,8 +1284,8 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       ufr[s] = v;
     }
   }
-  bf16x8_t wfr[(L::WL || SK) ? 1 : TX][(L::WL || SK) ? 1 : KB];
-  if constexpr (SK) {
+  bf16x8_t wfr[(L::WL || SK || DXW) ? 1 : TX][(L::WL || SK || DXW) ? 1 : KB];
+  if constexpr (SK || DXW) {
   } else if constexpr (L::WL) {     // W^T blocks [NXB][16 din][4H] in LDS (unrolled: all loads in flight)
     static_assert((NXB * 16 * G4) % NT == 0, "W staging trip count");
 #pragma unroll
@@ -1421,7 +1486,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
 #pragma unroll
         for (int g = 0; g < KG; ++g) sdh += dpart[g][col][unit];
         dhr = sdh;
-      } else if (t >= 0) {   // dx^T = W dz^T of this step
+      } else if (!DXW && t >= 0) {   // dx^T = W dz^T of this step (DXW: the dx wave's)
 #pragma unroll
         for (int q = 0; q < TX; ++q) {
           const int xb = w + NW * q;
@@ -1930,7 +1995,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
       if (threadIdx.x >= chainb_io_threads(TMC<HH>::NT, DD)) return;                    \
       chain_bwd_stage_io<HH, KXX, DD, SRCV, UPV, XOV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
     } else {                                                                            \
-      if (threadIdx.x >= TMC<HH>::NT + (TMC<HH>::NT + 64 <= 1024 ? 64 : 0)) return;     \
+      if (threadIdx.x >= chainb_live_threads(HH, TMC<HH>::NT)) return;                   \
       chain_bwd_stage<HH, KXX, DD, SRCV, UPV, XOV>(S, tile, A.ntiles, A.Mp, tagb, A.ctl, smem); \
     }                                                                                   \
   }
@@ -2244,9 +2309,19 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     A.pkW = pkW->data_ptr<float>();
     A.pkDw = (int)pkW->size(0);
     A.pk = reinterpret_cast<bf16x8_t*>(pk.data_ptr<float>());
-    nblk += (T4PK_ALL + 1023) / 1024;
+    A.npk = (T4PK_ALL + 1023) / 1024;
+    nblk += A.npk;
     TORCH_CHECK(nblk <= chain_capacity(x.get_device()), "lstm_chain: ", nblk,
                 " workgroups cannot all be resident on this device");
+  }
+  // a pending GCN coefficient job (gcn_fused_fwd, side mode) rides on this launch when its
+  // workgroups fit the co-resident grid as well; else it stays pending (gcn_coef_flush runs it)
+  std::vector<at::Tensor> cf_keep;
+  if (gcn_pending(x.get_device()).job.on && train &&
+      nblk + gcn_pending(x.get_device()).job.Mp <= chain_capacity(x.get_device())) {
+    static_assert(GcnCoefFwdLds::BYTES <= CHAIN_LDS, "coefficient job LDS");
+    gcn_coef_take(x.get_device(), A.cf, cf_keep);
+    nblk += A.cf.Mp;
   }
   if (train)
     hipLaunchKernelGGL(lstm_chain_fwd_kernel<true>, dim3(nblk), dim3(1024), 0, stream(), A);

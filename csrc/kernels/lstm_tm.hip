@@ -1078,6 +1078,8 @@ struct MultiGrad {
   int n;
   int gcn_nb;                      // > 0: blocks [0, gcn_nb) run the fused GCN backward (gcn_fused.h)
   GcnBwdJob gcn;
+  int gcn_coef;                    // 1: those blocks run the coefficient form (gcn_coef_bwd_body) instead
+  GcnCoefJob gcnc;
 };
 struct MultiRed {
   RedJob j[MULTI_MAX];
@@ -1091,7 +1093,8 @@ __global__ __launch_bounds__(256) void lstm_grads_multi_kernel(MultiGrad M) {
   static_assert(GcnBwdLds<2, 16>::BYTES <= GradsLds<128, 5>::BYTES, "GCN job LDS");
   if ((int)blockIdx.x < M.gcn_nb) {                      // the GCN backward's workgroups
     const int gb = blockIdx.x;
-    if (M.gcn.key == 2 * 64 + 16)                          // (the CML configuration)
+    if (M.gcn_coef) gcn_coef_bwd_body<2, 16>(M.gcnc, gb);
+    else if (M.gcn.key == 2 * 64 + 16)                     // (the CML configuration)
       gcn_fused_bwd_body<2, 16>(M.gcn, gb % M.gcn.B, gb / M.gcn.B, smem);
     return;
   }
@@ -1137,6 +1140,10 @@ GcnBwdJob gcn_bwd_job(const at::Tensor& dh, int64_t c_off, const at::Tensor& ser
                       const at::Tensor& W, const at::Tensor& bias, const at::Tensor& alpha, const at::Tensor& dW,
                       const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dalpha, int& nblocks);
 
+GcnCoefJob gcn_coef_job(const at::Tensor& dh, int64_t c_off, const at::Tensor& coef, const at::Tensor& S,
+                        const at::Tensor& st, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& dW,
+                        const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dalpha);
+
 // grads of jobs (dz, x, h, W, period, hshift, ws) then reductions of rjobs (ws, W, dW, dU, db):
 // a reduce job may be one of this call's grads jobs (stream order runs the grads first).
 // gcn_t / gcn_i (optional): the arguments of gcn_fused_bwd - [dh, series, shift, scale, win_group,
@@ -1153,8 +1160,8 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
                   (int)gW.size() == ng && (int)period.size() == ng && (int)hshift.size() == ng &&
                   (int)gws.size() == ng && (int)rW.size() == nr && (int)rdW.size() == nr && (int)rdU.size() == nr &&
                   (int)rdb.size() == nr, "lstm_grads_multi: job lists");
-  TORCH_CHECK((gcn_t.size() == 0 && gcn_i.size() == 0) || (gcn_t.size() == 21 && gcn_i.size() == 4),
-              "lstm_grads_multi: gcn job lists");
+  TORCH_CHECK((gcn_t.size() == 0 && gcn_i.size() == 0) || (gcn_t.size() == 21 && gcn_i.size() == 4) ||
+                  (gcn_t.size() == 10 && gcn_i.size() == 1), "lstm_grads_multi: gcn job lists");
   TORCH_CHECK(gcn_t.size() == 0 || ng > 0, "lstm_grads_multi: a GCN job rides on a gradient launch");
   if (ng + nr == 0) return;
   c10::DeviceGuard guard(ng ? gz[0].device() : rws[0].device());
@@ -1162,7 +1169,12 @@ void lstm_grads_multi(at::TensorList gz, at::TensorList gx, at::TensorList gh, a
   if (ng) {
     MultiGrad M{};
     M.n = ng;
-    if (gcn_t.size() > 0) {
+    if (gcn_t.size() == 10) {        // coefficient form: [dh, coef, S, st, W, b, dW, dgamma, dbeta, dalpha] / [c_off]
+      M.gcnc = gcn_coef_job(gcn_t[0], gcn_i[0], gcn_t[1], gcn_t[2], gcn_t[3], gcn_t[4], gcn_t[5], gcn_t[6], gcn_t[7],
+                            gcn_t[8], gcn_t[9]);
+      M.gcn_coef = 1;
+      M.gcn_nb = M.gcnc.nblocks;
+    } else if (gcn_t.size() > 0) {
       const c10::optional<at::Tensor> cur = gcn_t[11].numel() > 0 ? c10::optional<at::Tensor>(gcn_t[11]) : c10::nullopt;
       M.gcn = gcn_bwd_job(gcn_t[0], gcn_i[0], gcn_t[1], gcn_t[2], gcn_t[3], gcn_t[4], gcn_t[5], gcn_t[6], gcn_t[7],
                           gcn_t[8], gcn_t[9], gcn_t[10], cur, gcn_i[1], gcn_i[2], gcn_i[3] != 0, gcn_t[12], gcn_t[13],

@@ -280,20 +280,23 @@ class _HipStoreGCN(torch.autograd.Function):
     """Window gather + GeneralConv + BatchNorm + PReLU + node pooling + concat in ONE launch,
     straight from the resident window store (``gcn_fused.hip``): ``(h [T, Mp, Cp], y, y_mask,
     wid)``. Backward: ONE launch adding the parameter gradients with float atomics (training mode
-    only; not bitwise reproducible, so the deterministic mode keeps :class:`_HipGCNPool`)."""
+    only; not bitwise reproducible, so the deterministic mode keeps :class:`_HipGCNPool`). In the
+    CML configuration the forward also emits the backward's coefficients and the backward is the
+    dot product of dh with them (``gcn_coef_bwd``), usually run inside the batched weight-gradient
+    launch."""
 
     @staticmethod
     def forward(ctx, data, ids, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
-                momentum: float, eps: float, Mp: int, Cp: int):
+                momentum: float, eps: float, Mp: int, Cp: int, coef: bool = False):
         from ..utils.native import hip_ops
         wids, table, cursor = ids
-        h, S, st, y, ym, wid = hip_ops().gcn_fused_fwd(
+        h, S, st, y, ym, wid, cf = hip_ops().gcn_fused_fwd(
             *data["fwd"], wids, table, cursor, *data["dims"], W.contiguous(), b.contiguous(), gamma.contiguous(),
             beta.contiguous(), alpha.contiguous(), running_mean, running_var, bool(training), float(momentum),
-            float(eps), int(Mp), int(Cp))
+            float(eps), int(Mp), int(Cp), coef)
         ctx.data, ctx.ids, ctx.training = data, ids, bool(training)
         ctx.params = (W, b, gamma, beta, alpha)
-        ctx.save_for_backward(W, b, alpha, S, st)
+        ctx.save_for_backward(W, b, alpha, S, st, cf)
         ctx.mark_non_differentiable(y, ym, wid)
         ctx.set_materialize_grads(False)
         return h, y, ym, wid
@@ -302,24 +305,37 @@ class _HipStoreGCN(torch.autograd.Function):
     def backward(ctx, dh, _dy, _dym, _dwid):
         from ..utils.native import hip_ops
         from .lstm import _grad_sink
-        W, b, alpha, S, st = ctx.saved_tensors
+        W, b, alpha, S, st, cf = ctx.saved_tensors
         need = ctx.needs_input_grad[2:7]
         if dh is None or not any(need):
             return (None,) * 14
         if not ctx.training:
             raise RuntimeError("gcn_fused backward: parameter gradients in eval mode take the generic path")
         sinks = [(_grad_sink(p) if n else (torch.zeros_like(p), False)) for p, n in zip(ctx.params, need)]
+        from .lstm import defer_to_grads_launch
+        direct = all(direct for (_, direct), n in zip(sinks, need) if n)
+        if cf.numel() > 0:
+            # coefficient form: dh x coef, deferred onto the batched LSTM weight-gradient launch when
+            # every gradient goes straight into .grad
+            ca = int(ctx.data["ca"])
+            # (the coefficients are normally written by spare workgroups of the chain forward launch;
+            # if no chain launch took the job, run it now)
+            hip_ops().gcn_coef_flush(cf)
+            jt = [dh.contiguous(), cf, S, st, W.contiguous(), b.contiguous(), sinks[0][0], sinks[2][0], sinks[3][0],
+                  sinks[4][0]]
+            if not (direct and defer_to_grads_launch((jt, [ca]))):
+                hip_ops().gcn_coef_bwd(jt[0], ca, *jt[1:])
+            grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need)]
+            return (None, None, *grads, None, None, None, None, None, None, None, None)
         wids, table, cursor = ctx.ids
         args = (dh.contiguous(), int(ctx.data["ca"]), *ctx.data["bwd"], wids, table, cursor, *ctx.data["dims"], S, st,
                 W.contiguous(), b.contiguous(), alpha.contiguous(), sinks[0][0], sinks[2][0], sinks[3][0], sinks[4][0])
-        from .lstm import defer_to_grads_launch
         # (deferred onto the batched LSTM weight-gradient launch when every gradient goes straight
         # into .grad and the configuration is the one that launch instantiates)
-        if not (all(direct for (_, direct), n in zip(sinks, need) if n) and tuple(W.shape) == (2, 16)
-                and defer_to_grads_launch(_gcn_job_lists(args))):
+        if not (direct and tuple(W.shape) == (2, 16) and defer_to_grads_launch(_gcn_job_lists(args))):
             hip_ops().gcn_fused_bwd(*args)
         grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need)]
-        return (None, None, *grads, None, None, None, None, None, None, None)
+        return (None, None, *grads, None, None, None, None, None, None, None, None)
 
 
 def _gcn_job_lists(args):
@@ -367,9 +383,16 @@ def gcn_pool_from_store(store, ids, layer, training: bool, pooling: str = "mean"
     Mp = (B + 15) // 16 * 16
     Cp = C + F_
     Cp += (-Cp) % 4
+    # training with gradients: the forward also writes the backward's per-(t, sample, feature)
+    # coefficients, so the backward is a streaming dot product against dh (gcn_coef_bwd). (Decided
+    # here: inside an autograd Function's forward grad mode is always off.)
+    import os
+    coef = (bool(training) and torch.is_grad_enabled() and tuple(layer.kernel.shape) == (2, 16)
+            and any(p.requires_grad for p in (layer.kernel, layer.bn_gamma, layer.bn_beta, layer.prelu_alpha))
+            and os.environ.get("GNNQC_GCN_COEF", "1") == "1")
     h, y, ym, wid = _HipStoreGCN.apply(data, idt, layer.kernel, layer.bias, layer.bn_gamma, layer.bn_beta,
                                        layer.prelu_alpha, layer.bn_moving_mean, layer.bn_moving_variance,
-                                       bool(training), float(layer.momentum), float(layer.eps), Mp, Cp)
+                                       bool(training), float(layer.momentum), float(layer.eps), Mp, Cp, coef)
     return h, B, y, ym, wid
 
 

@@ -69,7 +69,10 @@ def main():
         tt = t[: 2 * nsb * nt8].view(nsb * nt8, 2).double()
         t0 = float(tt[:, 0][tt[:, 0] > 0].min())
         us = lambda v: round((float(v) - t0) / 100, 2)      # noqa: E731
-        brows.append({"bwd_blocks_tile0": [{"block_row": k, "start_us": us(tt[k * nt8, 0]), "end_us": us(tt[k * nt8, 1])}
+        brows.append({"bwd_blocks_tile0": [{"block_row": k, "start_us": us(tt[k * nt8, 0]),
+                                            "loop_start_us": us(mid[k * nt8]) if k < nsb - 1 else None,
+                                            "end_us": us(tt[k * nt8, 1]),
+                                            "tile_end_us": [us(tt[k * nt8 + r, 1]) for r in range(nt8)]}
                                            for k in range(nsb)],
                       "bwd_last_end_us": us(tt[:, 1].max()),
                       # time4 + head backward workgroups (block rows 6): head backward done / reverse steps done

@@ -64,11 +64,15 @@ def test_fused_front_end_matches_generic(cuda_device, cml_windows, pooling, trai
     torch.testing.assert_close(g.bn_moving_variance, rv_generic, atol=1e-6, rtol=1e-5)
 
 
-def test_fused_front_end_gradients_match_generic(cuda_device, cml_windows):
+@pytest.mark.parametrize("coef", ["1", "0"])
+def test_fused_front_end_gradients_match_generic(cuda_device, cml_windows, monkeypatch, coef):
     """Parameter gradients of the fused backward (per-workgroup closed form + atomics) equal the
-    generic two-launch backward on the same upstream gradient."""
+    generic two-launch backward on the same upstream gradient - both in the coefficient form
+    (GNNQC_GCN_COEF=1: the forward writes per-(t, sample, feature) coefficients, the backward is
+    dh x coef) and in the recomputing form."""
     from gnnqc.ops.gcn import gcn_pool, gcn_pool_from_store
     from gnnqc.ops.lstm import direct_grad_accumulation
+    monkeypatch.setenv("GNNQC_GCN_COEF", coef)
     _, st, model = _setup(cuda_device, cml_windows)
     g = model.gcn_layer
     ids = _ids(st, 128, cuda_device, pad=3)
