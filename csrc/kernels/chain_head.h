@@ -79,7 +79,7 @@ __device__ __forceinline__ int ch_tid() { return threadIdx.x & (64 * CH_NW - 1);
 
 __device__ __forceinline__ float ch_mask_sum(const float* __restrict__ mask, int M, float* red) {
   float s = 0.f;
-  for (int i = ch_tid(); i < M; i += 64 * CH_NW) s += mask[i];
+  for (int i = ch_tid(); i < M; i += 64 * CH_NW) s += ch_ld(mask + i);   // (agent scope: the labels may come from this launch's producers)
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[ch_tid() >> 6] = s;
   __syncthreads();
@@ -215,8 +215,8 @@ __device__ __forceinline__ void chain_head_fwd(const ChainHead hd, int tile, int
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int rc = min(tile * 16 + w + 8 * q, hd.M - 1);
-    yy[q] = hd.y[rc];
-    mm[q] = hd.mask[rc];
+    yy[q] = ch_ld(hd.y + rc);
+    mm[q] = ch_ld(hd.mask + rc);
   }
   float z2[2];
   ch_head_z2<F>(hd, sW1, sW2, hl, part, nullptr, sa1, z2);
@@ -329,8 +329,8 @@ __device__ __forceinline__ void chain_head_bwd(const ChainHead hd, const float* 
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int rc = min(row0 + w + 8 * q, hd.M - 1);
-    yy[q] = hd.y[rc];
-    mm[q] = hd.mask[rc];
+    yy[q] = ch_ld(hd.y + rc);
+    mm[q] = ch_ld(hd.mask + rc);
   }
   const float n = ch_mask_sum(hd.mask, hd.M, misc + 16);    // (its barrier also publishes sh)
   float z2[2];

@@ -140,14 +140,308 @@ struct GcnCoefFwdLds {
   static constexpr int BYTES = (GCF_LDS_FLOATS + 4 * GF_ROW_MAX) * 4;
 };
 
-// host: a coefficient job left by gcn_fused_fwd for the next chain forward launch (gcn_fused.hip)
+// ---- the whole training-step forward as PRODUCER workgroups of the LSTM chain forward launch
+// (lstm_chain.hip): one workgroup (blockDim.x threads, a multiple of 256, F / 4 threads per row) per
+// sample row b of [0, Mp), all T steps. The arithmetic of gcn_fused_fwd_kernel (the batch's moment
+// records summed in one fixed order - the same in every workgroup -, the BatchNorm prep, the
+// node-pooled PReLU output, the flagged series) plus, when coef != nullptr, the backward
+// coefficients of gcn_coef_fwd_body. Each time-major input row goes to `out` (fp32, read by the
+// backward) and, when gout != nullptr, to the tagged granule stream gout ({value, tag | t} per
+// element), which the chain's first stage streams like a stage-to-stage hand-off: it starts on the
+// first steps while later rows are still being produced, instead of after a separate forward
+// launch and its tail. y / y_mask / wid leave through agent-scope stores and the workgroup then
+// counts itself in *done (the chain's head waits for every producer before it reads the labels).
+struct GcnProdJob {
+  GfData D;
+  int B, Mp, Cp, on;
+  const float* W;
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  const float* alpha;
+  float* rmean;
+  float* rvar;
+  float momentum, eps;
+  float* out;                                      // [T][Mp][Cp]
+  unsigned long long* gout;                        // [T][Mp][Cp] tagged granules (nullptr: none)
+  double* Sout;                                    // [nstat]
+  float* st;                                       // [4][F]: mu, inv, scale, shift
+  float* y;                                        // [B]
+  float* ym;                                       // [B]
+  long* wid;                                       // [B]
+  float* coef;                                     // [T][Mp][(3 + Cin) F] (nullptr: none)
+};
+
+struct GcnProdLds {
+  static constexpr int PRM = (GF_MAX_CIN + 2) * 32;   // floats: W', b', alpha per feature
+  static constexpr int BYTES = (GCF_LDS_FLOATS + 4 * GF_ROW_MAX + PRM) * 4 + 17 * 32 * 8;
+};
+
+__device__ __forceinline__ void gf_st_granule(unsigned long long* p, float v, unsigned tag) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int Cin, int F>
+__device__ __forceinline__ void gcn_prod_body(const GcnProdJob& J, int b, unsigned tagb, int* done, char* smem,
+                                              long long* mark = nullptr) {
+  constexpr int NA = 3 + Cin, nstat = Cin + Cin * Cin + 1, QPR = F / 4;
+  constexpr int SPT = 12;                                              // staged floats per thread and pass
+  static_assert(F % 4 == 0 && (Cin + 2) * F <= GcnProdLds::PRM && nstat <= 32, "producer layout");
+  const GfData& D = J.D;
+  const int tid = threadIdx.x, nthr = blockDim.x, N = D.N, T = D.T, NC = N * Cin;
+  const int lane = tid & 63, wv = tid >> 6, nwv = nthr >> 6;
+  float* sx = reinterpret_cast<float*>(smem);                         // [GCF_LDS_FLOATS]
+  float* svm = sx + GCF_LDS_FLOATS;                                    // [GF_ROW_MAX] x 4
+  float* spw = svm + GF_ROW_MAX;
+  float* ssh = spw + GF_ROW_MAX;
+  float* ssc = ssh + GF_ROW_MAX;
+  float* prm = ssc + GF_ROW_MAX;                                       // [Cin + 2][F]
+  double* dred = reinterpret_cast<double*>(prm + GcnProdLds::PRM);     // [16][32] + S [32]
+  double* S = dred + 16 * 32;
+  const long* ids = gf_ids(D, J.B);
+  const long wraw = b < J.B ? ids[b] : -1;
+  const bool live = wraw >= 0;
+  const long w = live ? wraw : 0;
+  const long g = D.wg[w], c0 = D.wc[w];
+  const long tn = D.time_norm ? c0 : 0;
+  const float* src = D.series + (g * D.Ttot + (c0 - D.tb)) * (long)NC;
+  // thread -> (row lane rl, feature quad fq); rows per pass: the LDS slab, the row lanes and the
+  // register staging (SPT floats per thread) all hold them
+  const int fq = tid % QPR, rl = tid / QPR, rlanes = nthr / QPR;
+  const int RP = max(1, min(min(GCF_LDS_FLOATS, SPT * nthr) / NC, rlanes));
+  // ---- phase A: every load before the first wait (the first pass's series slab, the node tables,
+  // the parameters, the batch's moment records): one memory round trip after id -> window
+  float v[SPT];
+  auto load_slab = [&](int p0, int n) {
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int i = tid + nthr * u;
+      v[u] = live && i < n ? src[(long)p0 * NC + i] : 0.f;
+    }
+  };
+  load_slab(0, min(RP, T) * NC);
+  float pv[Cin + 6];
+  if (tid < F) {
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) pv[k] = J.W[k * F + tid];
+    pv[Cin] = J.bias[tid];
+    pv[Cin + 1] = J.gamma[tid];
+    pv[Cin + 2] = J.beta[tid];
+    pv[Cin + 3] = J.alpha[tid];
+    pv[Cin + 4] = J.rmean[tid];
+    pv[Cin + 5] = J.rvar[tid];
+  }
+  float nv = 0.f, npw = 0.f, nsh = 0.f, nsc = 0.f;
+  if (tid < N) {
+    nv = live && D.wv[w * N + tid] ? 1.f : 0.f;
+    npw = live ? D.pw[w * N + tid] : 0.f;
+  }
+  if (tid < NC) {
+    nsh = D.shift[(g * D.Tn + tn) * (long)NC + tid];
+    nsc = D.scale[(g * D.Tn + tn) * (long)NC + tid];
+  }
+  double mv[nstat];
+#pragma unroll
+  for (int i = 0; i < nstat; ++i) mv[i] = 0.0;
+  for (int k = tid; k < J.B; k += nthr) {          // the batch's moments: B window records
+    const long wk = ids[k];
+    if (wk >= 0) {
+#pragma unroll
+      for (int i = 0; i < nstat; ++i) mv[i] += D.mom[wk * nstat + i];
+    }
+  }
+  // ---- phase B
+  if (tid < N) {
+    svm[tid] = nv;
+    spw[tid] = npw;
+  }
+  if (tid < NC) {
+    ssh[tid] = nsh;
+    ssc[tid] = nsc;
+  }
+#pragma unroll
+  for (int i = 0; i < nstat; ++i) {
+    double sv = mv[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    if (lane == 0) dred[wv * 32 + i] = sv;
+  }
+  __syncthreads();
+  if (mark != nullptr && tid == 0) mark[0] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (tid < nstat) {                               // fixed order: identical in every workgroup
+    double sv = 0.0;
+    for (int k = 0; k < nwv; ++k) sv += dred[k * 32 + tid];
+    S[tid] = sv;
+  }
+  auto park = [&](int n) {                         // normalise the staged values into sx
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int i = tid + nthr * u;
+      if (i < n) {
+        const int e = i % NC;
+        sx[i] = (v[u] - ssh[e]) * ssc[e] * svm[e / Cin];
+      }
+    }
+  };
+  park(min(RP, T) * NC);
+  __syncthreads();
+  if (tid < F) {                                   // BatchNorm (training statistics) folded into W', b'
+    const double cnt = fmax(S[Cin + Cin * Cin], 1.0);
+    double ex[Cin];
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) ex[k] = S[k] / cnt;
+    double m = pv[Cin], vv = 0.0;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) {
+      m += ex[k] * (double)pv[k];
+#pragma unroll
+      for (int l = 0; l < Cin; ++l) vv += (double)pv[k] * (S[Cin + k * Cin + l] / cnt - ex[k] * ex[l]) * (double)pv[l];
+    }
+    const float mu = (float)m, var = (float)fmax(vv, 0.0);
+    const float inv = rsqrtf(var + J.eps);
+    const float sc = pv[Cin + 1] * inv;
+    const float sh = pv[Cin + 2] - mu * sc;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) prm[k * F + tid] = pv[k] * sc;
+    prm[Cin * F + tid] = pv[Cin] * sc + sh;
+    prm[(Cin + 1) * F + tid] = pv[Cin + 3];
+    if (b == 0) {
+      J.st[tid] = mu;
+      J.st[F + tid] = inv;
+      J.st[2 * F + tid] = sc;
+      J.st[3 * F + tid] = sh;
+      J.rmean[tid] = pv[Cin + 4] * J.momentum + mu * (1.f - J.momentum);
+      J.rvar[tid] = pv[Cin + 5] * J.momentum + var * (1.f - J.momentum);
+    }
+  }
+  if (b == 0 && tid < nstat) J.Sout[tid] = S[tid];
+  __syncthreads();
+  if (mark != nullptr && tid == 0) mark[1] = (long long)__builtin_amdgcn_s_memrealtime();
+  float pwk[Cin][4], pb[4], pal[4], rwk[Cin][4], rb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = 4 * fq + j;
+#pragma unroll
+    for (int k = 0; k < Cin; ++k) {
+      pwk[k][j] = prm[k * F + f];
+      rwk[k][j] = J.W[k * F + f];
+    }
+    pb[j] = prm[Cin * F + f];
+    pal[j] = prm[(Cin + 1) * F + f];
+    rb[j] = J.bias[f];
+  }
+  const long apl = D.gap[g];
+  const int ap = apl < 0 ? 0 : (int)apl;
+  for (int p0 = 0; p0 < T; p0 += RP) {
+    const int nr = min(RP, T - p0);
+    if (p0 > 0) {                                  // (more rows than one pass: stage the next slab)
+      load_slab(p0, nr * NC);
+      __syncthreads();                             // previous pass's LDS reads are done
+      park(nr * NC);
+      __syncthreads();
+    }
+    // the pooled outputs first (the chain's first stage streams them), the coefficients after
+    for (int rr = rl; rr < nr; rr += rlanes) {
+      const int t = p0 + rr;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      const float* xr = sx + rr * NC;
+      for (int n = 0; n < N; ++n) {
+        const float wn = spw[n];
+        float xv[Cin];
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float yv = pb[j];
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) yv += xv[k] * pwk[k][j];
+          acc[j] += wn * (yv > 0.f ? yv : pal[j] * yv);
+        }
+      }
+      const long ro = ((long)t * J.Mp + b) * J.Cp;
+      if (J.gout != nullptr) {
+        const unsigned tag = tagb | (unsigned)t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gf_st_granule(J.gout + ro + Cin + 4 * fq + j, acc[j], tag);
+        if (fq == 0)
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) gf_st_granule(J.gout + ro + k, xr[ap * Cin + k], tag);
+        for (int c = Cin + F + fq; c < J.Cp; c += QPR) gf_st_granule(J.gout + ro + c, 0.f, tag);
+      }
+      float* o = J.out + ro;
+      *reinterpret_cast<float4*>(o + Cin + 4 * fq) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      if (fq == 0)
+#pragma unroll
+        for (int k = 0; k < Cin; ++k) o[k] = xr[ap * Cin + k];
+      for (int c = Cin + F + fq; c < J.Cp; c += QPR) o[c] = 0.f;
+    }
+    if (mark != nullptr && p0 == 0 && tid == 0) mark[2] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (J.coef != nullptr)
+      for (int rr = rl; rr < nr; rr += rlanes) {
+        const int t = p0 + rr;
+        float cf[NA][4];
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cf[a][j] = 0.f;
+        const float* xr = sx + rr * NC;
+        for (int n = 0; n < N; ++n) {
+          const float wn = spw[n];
+          float xv[Cin];
+#pragma unroll
+          for (int k = 0; k < Cin; ++k) xv[k] = xr[n * Cin + k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float yv = pb[j], z = rb[j];
+#pragma unroll
+            for (int k = 0; k < Cin; ++k) {
+              yv += xv[k] * pwk[k][j];
+              z += xv[k] * rwk[k][j];
+            }
+            const bool pos = yv > 0.f;
+            const float dp = pos ? wn : pal[j] * wn;
+            cf[0][j] += dp;
+            cf[1][j] += dp * z;
+            cf[2][j] += pos ? 0.f : wn * yv;
+#pragma unroll
+            for (int k = 0; k < Cin; ++k) cf[3 + k][j] += dp * xv[k];
+          }
+        }
+        float* co = J.coef + ((long)t * J.Mp + b) * (NA * F) + 4 * fq;
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+          *reinterpret_cast<float4*>(co + a * F) = make_float4(cf[a][0], cf[a][1], cf[a][2], cf[a][3]);
+      }
+  }
+  // ---- the labels (agent scope), then this workgroup's arrival (the chain's head waits for all)
+  if (tid == 0 && b < J.B) {
+    __hip_atomic_store(reinterpret_cast<unsigned*>(J.y + b), __float_as_uint(live ? D.wlab[w] : 0.f),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned*>(J.ym + b), __float_as_uint(live ? 1.f : 0.f), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(J.wid + b), (unsigned long long)wraw, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0 && done != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the label stores are acknowledged)
+    __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// host: jobs left by gcn_fused_fwd for the next chain forward launch (gcn_fused.hip): the
+// coefficient side job, or the whole forward as producer workgroups (prod)
 struct GcnPending {
   GcnCoefFwdJob job;
   std::vector<at::Tensor> keep;
+  GcnProdJob prod;
+  std::vector<at::Tensor> pkeep;
 };
 bool gcn_coef_side_mode();
 GcnPending& gcn_pending(int dev);
 bool gcn_coef_take(int dev, GcnCoefFwdJob& job, std::vector<at::Tensor>& keep);
+bool gcn_prod_take(int dev, GcnProdJob& job, std::vector<at::Tensor>& keep);
+bool gcn_prod_flush_dev(int dev);
 
 template <int Cin, int F>
 __device__ __forceinline__ void gcn_coef_fwd_body(const GcnCoefFwdJob& J, int b, char* smem) {

@@ -466,7 +466,7 @@ std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor
                                       bool time_norm, const at::Tensor& W, const at::Tensor& bias,
                                       const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& alpha,
                                       at::Tensor rmean, at::Tensor rvar, bool training, double momentum, double eps,
-                                      int64_t Mp, int64_t Cp, bool with_coef) {
+                                      int64_t Mp, int64_t Cp, bool with_coef, bool defer) {
   int B = 0;
   GfData D = gf_data(series, shift, scale, win_group, win_center, win_valid, win_label, group_anom_pos, mom, pw,
                      wids, table, cursor, tb, seq_len, time_norm, B);
@@ -492,6 +492,42 @@ std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor
   // (gcn_coef_take), which runs while this kernel's output is consumed; else this kernel writes them.
   const bool want = with_coef && training && C == 2 && F == 16;
   at::Tensor coef = at::empty({want ? T : 0, want ? Mp : 0, (3 + C) * F}, fo);
+  if (defer && training && C == 2 && F == 16 && T < 4096) {
+    // producer mode: no launch here; the next LSTM chain forward launch runs this forward as producer
+    // workgroups (gcn_prod_body) that stream its input to the chain's first stage (gcn_prod_flush
+    // runs it on its own if another consumer comes first)
+    at::Tensor gout = at::empty({T, Mp, Cp}, fo.dtype(at::kLong));
+    GcnPending& pd = gcn_pending(series.get_device());
+    TORCH_CHECK(!pd.prod.on, "gcn_fused_fwd: a deferred forward is still pending");
+    GcnProdJob& J = pd.prod;
+    J = GcnProdJob{};
+    J.D = D;
+    J.B = B;
+    J.Mp = (int)Mp;
+    J.Cp = (int)Cp;
+    J.on = 1;
+    J.W = W.data_ptr<float>();
+    J.bias = bias.data_ptr<float>();
+    J.gamma = gamma.data_ptr<float>();
+    J.beta = beta.data_ptr<float>();
+    J.alpha = alpha.data_ptr<float>();
+    J.rmean = rmean.data_ptr<float>();
+    J.rvar = rvar.data_ptr<float>();
+    J.momentum = (float)momentum;
+    J.eps = (float)eps;
+    J.out = out.data_ptr<float>();
+    J.gout = reinterpret_cast<unsigned long long*>(gout.data_ptr<int64_t>());
+    J.Sout = S.data_ptr<double>();
+    J.st = st.data_ptr<float>();
+    J.y = y.data_ptr<float>();
+    J.ym = ym.data_ptr<float>();
+    J.wid = wid.data_ptr<long>();
+    J.coef = want ? coef.data_ptr<float>() : nullptr;
+    pd.pkeep = {out, gout, S, st, y, ym, wid, coef, W, bias, gamma, beta, alpha, rmean, rvar, series, shift, scale,
+                win_group, win_center, win_valid, win_label, group_anom_pos, mom, pw, wids, table};
+    if (cursor.has_value() && cursor->defined()) pd.pkeep.push_back(*cursor);
+    return {out, S, st, y, ym, wid, coef};
+  }
   const bool side = want && gcn_coef_side_mode();
   const bool cf = want && !side;
 #define GQ_GF_FWD(CINV, FV, CFV)                                                                                      \
@@ -551,11 +587,48 @@ __global__ __launch_bounds__(1024) void gcn_coef_fwd_kernel(GcnCoefFwdJob J) {
   gcn_coef_fwd_body<2, 16>(J, blockIdx.x, smem);
 }
 
+// the pending producer job of the current device, handed to the chain forward launch; clears it
+bool gcn_prod_take(int dev, GcnProdJob& job, std::vector<at::Tensor>& keep) {
+  GcnPending& pd = gcn_pending(dev);
+  if (!pd.prod.on) return false;
+  job = pd.prod;
+  keep.insert(keep.end(), pd.pkeep.begin(), pd.pkeep.end());
+  pd.prod.on = 0;
+  pd.pkeep.clear();
+  return true;
+}
+
+template <int Cin, int F>
+__global__ __launch_bounds__(1024) void gcn_prod_kernel(GcnProdJob J) {
+  __shared__ __attribute__((aligned(16))) char smem[GcnProdLds::BYTES];
+  gcn_prod_body<Cin, F>(J, blockIdx.x, 0u, nullptr, smem);
+}
+
+// run a pending deferred forward on its own (no chain forward launch took it); returns whether
+// there was one. The granule stream is not written (nothing streams it).
+bool gcn_prod_flush_dev(int dev) {
+  GcnProdJob J{};
+  std::vector<at::Tensor> keep;
+  if (!gcn_prod_take(dev, J, keep)) return false;
+  J.gout = nullptr;
+  hipLaunchKernelGGL((gcn_prod_kernel<2, 16>), dim3(J.Mp), dim3(1024), 0, stream(), J);
+  GQ_LAUNCH_CHECK();
+  return true;
+}
+
+bool gcn_prod_flush(const at::Tensor& like) {
+  TORCH_CHECK(like.is_cuda(), "gcn_prod_flush: a GPU tensor names the device");
+  c10::DeviceGuard guard(like.device());
+  return gcn_prod_flush_dev(like.get_device());
+}
+
 // run the pending coefficient job on its own (nothing consumed it: no chain forward in between);
-// returns whether there was one
+// returns whether there was one (a pending deferred forward, which writes the coefficients too, runs
+// first)
 bool gcn_coef_flush(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "gcn_coef_flush: a GPU tensor names the device");
   c10::DeviceGuard guard(like.device());
+  if (gcn_prod_flush_dev(like.get_device())) return true;
   GcnCoefFwdJob J{};
   std::vector<at::Tensor> keep;
   if (!gcn_coef_take(like.get_device(), J, keep)) return false;
@@ -690,4 +763,5 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("gcn_fused_bwd", &gq::gcn_fused_bwd);
   m.impl("gcn_coef_bwd", &gq::gcn_coef_bwd);
   m.impl("gcn_coef_flush", &gq::gcn_coef_flush);
+  m.impl("gcn_prod_flush", &gq::gcn_prod_flush);
 }

@@ -141,7 +141,12 @@ struct ChainArgs {
   // side job on the idle CUs: the GCN backward's coefficients (gcn_fused.h gcn_coef_fwd_body), one
   // workgroup per sample row; it only reads the store and writes its own buffer, nothing waits on it
   GcnCoefFwdJob cf;
+  // gp.on: the GCN forward itself as producer workgroups (gcn_prod_body), one per sample row; the
+  // first stage streams their tagged granules (st[0].xin) and the head waits for all of them
+  // (ctl[10] counts them) before it reads the labels they write
+  GcnProdJob gp;
 };
+static_assert(sizeof(ChainArgs) <= 4096, "chain forward kernel arguments");
 
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -193,6 +198,20 @@ __device__ __forceinline__ unsigned long long chain_wait_body(const unsigned lon
   }
   __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return v;
+}
+
+// one thread: wait (bounded, back-off) until the counter *p reaches n; the hand-off data behind it
+// is read with agent-scope loads. A timeout flags the step (ctl[2]) as the granule waits do.
+__device__ __forceinline__ void chain_wait_count(const int* p, int n, int* ctl) {
+  const int lim0 = __hip_atomic_load(ctl + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int lim = lim0 > 0 ? lim0 : CHAIN_SPIN;
+  int nap = 1;
+  for (int it = 0; it < lim; ++it) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) return;
+    for (int k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(CHAIN_W_SLEEP);
+    nap = min(nap * 2, CHAIN_W_NAPMAX);
+  }
+  __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Per-step phase clocks of tile 0 (s_memtime: shader clock ticks) into pr[step][8] for the first
@@ -875,6 +894,7 @@ __device__ __forceinline__ void chain_finish(int* ctl, int nblk) {
     const int old = __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == nblk - 1) {            // last workgroup: next launch gets a new epoch
       __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + 10, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (GCN producers)
       __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -899,6 +919,10 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
           constexpr int HOFF = ChainT4Lds::HS + ChainT4Lds::XS + ChainT4Lds::HL;
           float* hW1 = ch_head_fwd_weights<128>(smem + HOFF);
           ch_stage_weights<128>(A.t4.hd, hW1, hW1 + 128 * CH_WP);
+          if (A.gp.on) {                          // the labels come from this launch's GCN producers
+            if (threadIdx.x == 0) chain_wait_count(A.ctl + 10, A.gp.Mp, A.ctl);
+            __syncthreads();
+          }
           chain_t4_stage<TRAIN>(A.t4, r, A.ntiles, A.Mp, tagb, A.ctl, smem);
           long long* mk = blockIdx.x < 64 ? A.trace + 512 + blockIdx.x : nullptr;   // (trace: phase ends)
           if (mk != nullptr && threadIdx.x == 0) mk[0] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -938,6 +962,14 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
       if (A.pk != nullptr && f < T4PK_ALL) t4_pack_one(f, A.pkU, A.pkW, A.pkDw, A.pk);
     } else if (A.cf.on && r - A.npk < A.cf.Mp) {  // GCN backward coefficients of sample row r - npk
       gcn_coef_fwd_body<2, 16>(A.cf, r - A.npk, smem);
+    } else if (A.gp.on && r - A.npk - (A.cf.on ? A.cf.Mp : 0) < A.gp.Mp) {   // GCN forward producer
+      // (trace: start / end at [2 blockIdx]; rows < 32: phase A loads in / BatchNorm prepped / the
+      // first pass's rows stored at [640 + 4 row + 0..2])
+      if (threadIdx.x == 0 && blockIdx.x < 256) A.trace[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
+      const unsigned E = (unsigned)__hip_atomic_load(A.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int row = r - A.npk - (A.cf.on ? A.cf.Mp : 0);
+      gcn_prod_body<2, 16>(A.gp, row, chain_tag_base(E), A.ctl + 10, smem, row < 32 ? A.trace + 640 + 4 * row : nullptr);
+      if (threadIdx.x == 0 && blockIdx.x < 256) A.trace[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
     }
     chain_finish(A.ctl, nblk);
     return;
@@ -954,7 +986,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_fwd_kernel(ChainArgs A) {
   // argument array made the compiler copy the whole array to scratch)
   const ChainStage S = A.st[s];
   const int H = S.H, KX = S.KX;
-  const bool src = s > 0;
+  const bool src = s > 0 || A.gp.on;              // (stage 0 then streams the GCN producers' granules)
 #define GQ_CHAIN_BODY(HH, KXX, DD, SRCV, PINV)                                          \
   {                                                                                     \
     constexpr int DS = chain_stage_d(HH, KXX, DD);                                      \
@@ -2313,6 +2345,29 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
     nblk += A.npk;
     TORCH_CHECK(nblk <= chain_capacity(x.get_device()), "lstm_chain: ", nblk,
                 " workgroups cannot all be resident on this device");
+  }
+  // a deferred GCN forward (gcn_fused_fwd defer) whose output is this launch's input runs as
+  // producer workgroups of this launch (the first stage streams their granules, the head waits for
+  // their labels); any other pending one runs on its own first
+  std::vector<at::Tensor> gp_keep;
+  {
+    const int dev = x.get_device();
+    const GcnProdJob& P = gcn_pending(dev).prod;
+    if (P.on) {
+      const int H0 = A.st[0].H, Din0 = A.st[0].Din;
+      const bool mine = train && t4 != nullptr && P.out == x.data_ptr<float>() && P.Mp == Mp &&
+                        P.Cp == Din0 && P.D.T == (int)x.size(0) && Din0 % 2 == 0 &&
+                        (H0 < 64 || 16 * Din0 / 2 <= 64 * TMC<64>::NW) &&
+                        (long)P.D.T * Mp * Din0 * 8 < (1L << 31) && nblk + P.Mp <= chain_capacity(dev);
+      if (mine) {
+        static_assert(GcnProdLds::BYTES <= CHAIN_LDS, "GCN producer LDS");
+        gcn_prod_take(dev, A.gp, gp_keep);
+        A.st[0].xin = A.gp.gout;
+        nblk += A.gp.Mp;
+      } else {
+        gcn_prod_flush_dev(dev);
+      }
+    }
   }
   // a pending GCN coefficient job (gcn_fused_fwd, side mode) rides on this launch when its
   // workgroups fit the co-resident grid as well; else it stays pending (gcn_coef_flush runs it)

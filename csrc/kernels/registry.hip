@@ -81,12 +81,13 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor win_valid, Tensor win_label, Tensor group_anom_pos, Tensor mom, Tensor pw, Tensor wids, "
         "Tensor table, Tensor? cursor, int tb, int seq_len, bool time_norm, Tensor W, Tensor b, Tensor gamma, "
         "Tensor beta, Tensor alpha, Tensor(a!) rmean, Tensor(b!) rvar, bool training, float momentum, float eps, "
-        "int Mp, int Cp, bool with_coef=False) -> Tensor[]");
+        "int Mp, int Cp, bool with_coef=False, bool defer=False) -> Tensor[]");
   m.def("gcn_fused_bwd(Tensor dh, int c_off, Tensor series, Tensor shift, Tensor scale, Tensor win_group, "
         "Tensor win_center, Tensor win_valid, Tensor group_anom_pos, Tensor pw, Tensor wids, Tensor table, "
         "Tensor? cursor, int tb, int seq_len, bool time_norm, Tensor S, Tensor st, Tensor W, Tensor b, "
         "Tensor alpha, Tensor(a!) dW, Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) dalpha) -> ()");
   m.def("gcn_coef_flush(Tensor like) -> bool");
+  m.def("gcn_prod_flush(Tensor like) -> bool");
   m.def("gcn_coef_bwd(Tensor dh, int c_off, Tensor coef, Tensor S, Tensor st, Tensor W, Tensor b, Tensor(a!) dW, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) dalpha) -> ()");
   // per-node GeneralConv writing the time-major LSTM input (gcn_node.hip)

@@ -260,9 +260,12 @@ class GCNClassifier(nn.Module):
         spec = self.head_spec()
         g = self.gcn_layer
         pooling = "selection" if self.pooling_type == "selection" else self.aggregation_type
-        h, M, y, ym, _ = gcn_pool_from_store(store, ids, g, self.training, pooling)
+        # (defer: the GCN forward runs inside the chain forward launch, as its input's producer)
+        h, M, y, ym, _ = gcn_pool_from_store(store, ids, g, self.training, pooling, defer=True)
         if not self.time_layer.head_chain_ok(h):
             from ..ops.head import fused_head_loss
+            from ..utils.native import hip_ops
+            hip_ops().gcn_prod_flush(h)
             return fused_head_loss(self.time_layer.forward_time_major(h, M), *spec, y, ym, w0, w1, sums, hist)
         return self.time_layer.forward_time_major_head(h, M, spec[:3], spec[3:], y, ym, w0, w1, sums, hist)
 

@@ -287,13 +287,13 @@ class _HipStoreGCN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, data, ids, W, b, gamma, beta, alpha, running_mean, running_var, training: bool,
-                momentum: float, eps: float, Mp: int, Cp: int, coef: bool = False):
+                momentum: float, eps: float, Mp: int, Cp: int, coef: bool = False, defer: bool = False):
         from ..utils.native import hip_ops
         wids, table, cursor = ids
         h, S, st, y, ym, wid, cf = hip_ops().gcn_fused_fwd(
             *data["fwd"], wids, table, cursor, *data["dims"], W.contiguous(), b.contiguous(), gamma.contiguous(),
             beta.contiguous(), alpha.contiguous(), running_mean, running_var, bool(training), float(momentum),
-            float(eps), int(Mp), int(Cp), coef)
+            float(eps), int(Mp), int(Cp), coef, defer)
         ctx.data, ctx.ids, ctx.training = data, ids, bool(training)
         ctx.params = (W, b, gamma, beta, alpha)
         ctx.save_for_backward(W, b, alpha, S, st, cf)
@@ -308,7 +308,7 @@ class _HipStoreGCN(torch.autograd.Function):
         W, b, alpha, S, st, cf = ctx.saved_tensors
         need = ctx.needs_input_grad[2:7]
         if dh is None or not any(need):
-            return (None,) * 14
+            return (None,) * 15
         if not ctx.training:
             raise RuntimeError("gcn_fused backward: parameter gradients in eval mode take the generic path")
         sinks = [(_grad_sink(p) if n else (torch.zeros_like(p), False)) for p, n in zip(ctx.params, need)]
@@ -326,7 +326,7 @@ class _HipStoreGCN(torch.autograd.Function):
             if not (direct and defer_to_grads_launch((jt, [ca]))):
                 hip_ops().gcn_coef_bwd(jt[0], ca, *jt[1:])
             grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need)]
-            return (None, None, *grads, None, None, None, None, None, None, None, None)
+            return (None, None, *grads, None, None, None, None, None, None, None, None, None)
         wids, table, cursor = ctx.ids
         args = (dh.contiguous(), int(ctx.data["ca"]), *ctx.data["bwd"], wids, table, cursor, *ctx.data["dims"], S, st,
                 W.contiguous(), b.contiguous(), alpha.contiguous(), sinks[0][0], sinks[2][0], sinks[3][0], sinks[4][0])
@@ -335,7 +335,7 @@ class _HipStoreGCN(torch.autograd.Function):
         if not (direct and tuple(W.shape) == (2, 16) and defer_to_grads_launch(_gcn_job_lists(args))):
             hip_ops().gcn_fused_bwd(*args)
         grads = [None if direct or not n else buf for (buf, direct), n in zip(sinks, need)]
-        return (None, None, *grads, None, None, None, None, None, None, None, None)
+        return (None, None, *grads, None, None, None, None, None, None, None, None, None)
 
 
 def _gcn_job_lists(args):
@@ -362,11 +362,16 @@ def store_gcn_ok(store, layer, training: bool, pooling: str) -> bool:
             and W.shape[1] in (8, 16, 32) and store.seq_len >= 1)
 
 
-def gcn_pool_from_store(store, ids, layer, training: bool, pooling: str = "mean"):
+def gcn_pool_from_store(store, ids, layer, training: bool, pooling: str = "mean", defer: bool = False):
     """The CML GCN front end of a training / evaluation step straight from ``store``:
     ``(h [T, Mp, Cp], B, y [B], y_mask [B], wid [B])`` with ``h`` the time-major LSTM input
     (``[flagged series | pooled GCN | 0 pad]``) of :meth:`gnnqc.models.timelayer.TimeLayer.forward_time_major`.
-    ``ids``: window ids [B] (-1 = padding) or a :class:`gnnqc.data.store.CursorIds`."""
+    ``ids``: window ids [B] (-1 = padding) or a :class:`gnnqc.data.store.CursorIds`.
+
+    ``defer`` (training with the coefficient-form backward only): no launch here; the next headed
+    LSTM chain forward launch whose input is ``h`` runs this forward as producer workgroups and its
+    first stage streams their output (``gcn_fused.h`` ``gcn_prod_body``). Every other consumer of the
+    outputs must call ``hip_ops().gcn_prod_flush(h)`` first (the backward does)."""
     from ..data.store import CursorIds
     agg_mean = layer.aggregate == "mean"
     pool = {"mean": 0, "sum": 1, "selection": 2}[pooling]
@@ -390,9 +395,13 @@ def gcn_pool_from_store(store, ids, layer, training: bool, pooling: str = "mean"
     coef = (bool(training) and torch.is_grad_enabled() and tuple(layer.kernel.shape) == (2, 16)
             and any(p.requires_grad for p in (layer.kernel, layer.bn_gamma, layer.bn_beta, layer.prelu_alpha))
             and os.environ.get("GNNQC_GCN_COEF", "1") == "1")
+    # (off by default: measured slower - the producers' id -> window -> series load chain and
+    # per-row compute take ~13 us inside the chain launch vs 11.4 us for the forward's own launch;
+    # profiles/r5_gcn_producer_ab.txt)
+    defer = bool(defer and coef and os.environ.get("GNNQC_GCN_PROD", "0") == "1")
     h, y, ym, wid = _HipStoreGCN.apply(data, idt, layer.kernel, layer.bias, layer.bn_gamma, layer.bn_beta,
                                        layer.prelu_alpha, layer.bn_moving_mean, layer.bn_moving_variance,
-                                       bool(training), float(layer.momentum), float(layer.eps), Mp, Cp, coef)
+                                       bool(training), float(layer.momentum), float(layer.eps), Mp, Cp, coef, defer)
     return h, B, y, ym, wid
 
 

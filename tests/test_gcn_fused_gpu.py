@@ -221,3 +221,64 @@ def test_adam_flagged_matches_guarded_and_honours_flags(cuda_device):
     torch.cuda.synchronize()
     assert b.flat_p[5] == before[5] and int(b.guard_state[5].item()) == 1
     assert torch.count_nonzero(b.flat_p != before) == b.flat_p.numel() - 1
+
+def test_deferred_forward_flushed_matches_own_launch(cuda_device, cml_windows, monkeypatch):
+    """gcn_fused_fwd(defer): the producer body (gcn_fused.h gcn_prod_body), here run on its own by
+    gcn_prod_flush, writes the same time-major input, labels, ids and running statistics as the
+    forward kernel (the batch moments are summed in another fixed order: equal to rounding)."""
+    from gnnqc.ops.gcn import gcn_pool_from_store
+    from gnnqc.utils.native import hip_ops
+    monkeypatch.setenv("GNNQC_GCN_PROD", "1")
+    _, st, model = _setup(cuda_device, cml_windows)
+    g = model.gcn_layer
+    ids = _ids(st, 100, cuda_device, pad=5)
+    rm0, rv0 = g.bn_moving_mean.clone(), g.bn_moving_variance.clone()
+    out = {}
+    for defer in (False, True):
+        with torch.no_grad():
+            g.bn_moving_mean.copy_(rm0)
+            g.bn_moving_variance.copy_(rv0)
+        h, M, y, ym, wid = gcn_pool_from_store(st, ids, g, True, "mean", defer=defer)
+        assert bool(hip_ops().gcn_prod_flush(h)) == defer
+        assert not hip_ops().gcn_prod_flush(h)
+        torch.cuda.synchronize()
+        out[defer] = (h.detach().clone(), y.clone(), ym.clone(), wid.clone(), g.bn_moving_mean.clone(),
+                      g.bn_moving_variance.clone())
+    a, r = out[True], out[False]
+    torch.testing.assert_close(a[0], r[0], atol=2e-5, rtol=2e-5)
+    torch.testing.assert_close(a[1], r[1])
+    torch.testing.assert_close(a[2], r[2])
+    assert torch.equal(a[3], r[3])
+    torch.testing.assert_close(a[4], r[4], atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(a[5], r[5], atol=1e-6, rtol=1e-5)
+
+
+def test_gcn_producers_in_chain_forward_match_own_launch(cuda_device, cml_windows, monkeypatch):
+    """The CML loss with the GCN forward run as producer workgroups of the chain forward launch (its
+    first stage streams their granules, the head waits for their labels; GNNQC_GCN_PROD=1,
+    opt-in) == the GCN forward's own launch: loss, logits and every parameter gradient."""
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    from gnnqc.utils.native import hip_ops
+    _, st, model = _setup(cuda_device, cml_windows)
+    ids = _ids(st, 128, cuda_device, pad=2)
+    assert model.store_fused_ok(st)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GNNQC_GCN_PROD", flag)
+        m = copy.deepcopy(model)
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        with direct_grad_accumulation(True):
+            loss, logits = m.fused_store_loss(st, ids, 1.0, 5.0, None, None)
+            assert not hip_ops().gcn_prod_flush(logits)      # (the chain launch took the job)
+            loss.backward()
+        torch.cuda.synchronize()
+        out[flag] = (float(loss), logits.clone(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                     m.gcn_layer.bn_moving_mean.clone())
+    a, r = out["1"], out["0"]
+    assert abs(a[0] - r[0]) <= 1e-5 * abs(r[0]) + 1e-6, (a[0], r[0])
+    torch.testing.assert_close(a[1], r[1], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(a[3], r[3], atol=1e-6, rtol=1e-5)
+    for n in r[2]:
+        x, y = a[2][n], r[2][n]
+        assert (x - y).norm().item() <= 1e-2 * (y.norm().item() + 1e-6), (n, (x - y).norm().item())
