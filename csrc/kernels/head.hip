@@ -79,7 +79,9 @@ __device__ float block_mask_sum(const float* __restrict__ mask, int R, float* re
   return s;
 }
 
-template <int F>
+// PROB (frozen-weight attribution, e.g. integrated gradients): logits[r] receives sigmoid(z_r), no
+// loss, metrics or histogram (y, mask, aux, sums, hist unused)
+template <int F, bool PROB = false>
 __global__ __launch_bounds__(256) void head_fwd_kernel(
     const float* __restrict__ feat, int ldf, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ W3,
@@ -105,9 +107,9 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
   stage_lds<F * HU, HU, HU>(&sW1[0][0], W1);
   stage_lds<HU * HU, HU, HU>(&sW2[0][0], W2);
   const float bj1 = b1[j], bj2 = b2[j], w3 = W3[j], b3v = b3[0];
-  const float nm = block_mask_sum(mask, R, red);
+  const float nm = PROB ? 0.f : block_mask_sum(mask, R, red);
   const float inv = 1.f / fmaxf(nm, 1.f);
-  if (blockIdx.x == 0 && tid == 0) aux[1] = nm;
+  if (!PROB && blockIdx.x == 0 && tid == 0) aux[1] = nm;
   float m_loss = 0.f, m_n = 0.f, m_tp = 0.f, m_tn = 0.f, m_fp = 0.f, m_fn = 0.f;
   const int ntiles = (R + HT - 1) / HT;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -163,7 +165,10 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
       const float v = wave_sum(sa2[g * RPG + i][j] * w3);
       if (j == i) zr = v;
     }
-    {
+    if constexpr (PROB) {
+      const int row = row0 + g * RPG + (j % RPG);
+      if (j < RPG && row < R) logits[row] = sigmoidf_fast(zr + b3v);
+    } else {
       const int row = row0 + g * RPG + (j % RPG);
       const int rc = min(row, R - 1);
       const float yy_ = y[rc], m_ = mask[rc];        // loads outside any per-lane branch
@@ -191,6 +196,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     }
     __syncthreads();
   }
+  if constexpr (PROB) return;
   if (lds_hist)
     for (int e = tid; e < 2 * bins; e += 256)
       if (shist[e] != 0.f) atomicAdd(&hist[e], shist[e]);
@@ -215,7 +221,9 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
 }
 
 // Backward. gout: device scalar dL/dloss; aux[1]: mask sum from the forward.
-template <int F>
+// PROB: the input gradient of sum_r sigmoid(z_r) (logits holds the forward's sigmoid(z)):
+// dz3_r = s_r (1 - s_r); no weight gradients (gout, aux, y, mask and the gradient sinks unused)
+template <int F, bool PROB = false>
 __global__ __launch_bounds__(256) void head_bwd_kernel(
     const float* __restrict__ feat, int ldf, const float* __restrict__ W1, const float* __restrict__ W2,
     const float* __restrict__ W3, const float* __restrict__ z1, const float* __restrict__ z2,
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   __shared__ float sdz3[HT];
   __shared__ float red[4][HU + 1];
   const int tid = threadIdx.x, j = tid & 63, g = tid >> 6;
-  const float scale = gout[0] / fmaxf(aux[1], 1.f);
+  const float scale = PROB ? 1.f : gout[0] / fmaxf(aux[1], 1.f);
   stage_lds<F * HU, HU, HU + 1>(&sW1[0][0], W1);
   stage_lds<HU * HU, HU, HU + 1>(&sW2[0][0], W2);
   const float w3j = W3[j];
@@ -268,9 +276,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     {
       const int row = row0 + (tid & (HT - 1));
       const int rc = min(row, R - 1);
-      const float yy = y[rc];
-      const float wc = yy > 0.5f ? w1 : w0;
-      const float d = (row < R ? 1.f : 0.f) * scale * mask[rc] * wc * (sigmoidf_fast(logits[rc]) - yy);
+      float d;
+      if constexpr (PROB) {
+        const float sp = logits[rc];
+        d = (row < R ? 1.f : 0.f) * sp * (1.f - sp);
+      } else {
+        const float yy = y[rc];
+        const float wc = yy > 0.5f ? w1 : w0;
+        d = (row < R ? 1.f : 0.f) * scale * mask[rc] * wc * (sigmoidf_fast(logits[rc]) - yy);
+      }
       if (tid < HT) {             // LDS / register only inside the branch
         sdz3[tid] = d;
         ab3 += d;
@@ -287,12 +301,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     }
     __syncthreads();
     // dW2[i][j] = sum_r a1[r][i] dz2[r][j] ; db2 ; da1 -> dz1
-    #pragma unroll 4
-    for (int r = 0; r < HT; ++r) {
-      const float d = sz2[r][j];
+    if constexpr (!PROB) {
+      #pragma unroll 4
+      for (int r = 0; r < HT; ++r) {
+        const float d = sz2[r][j];
 #pragma unroll
-      for (int q = 0; q < UPG; ++q) aW2[q] += sa1[r][g * UPG + q] * d;
-      if (g == 0) ab2 += d;
+        for (int q = 0; q < UPG; ++q) aW2[q] += sa1[r][g * UPG + q] * d;
+        if (g == 0) ab2 += d;
+      }
     }
     float da[RPG];
 #pragma unroll
@@ -312,12 +328,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     }
     __syncthreads();
     // dW1[k][j] = sum_r feat[r][k] dz1[r][j] ; db1
-    #pragma unroll 4
-    for (int r = 0; r < HT; ++r) {
-      const float d = sz1[r][j];
+    if constexpr (!PROB) {
+      #pragma unroll 4
+      for (int r = 0; r < HT; ++r) {
+        const float d = sz1[r][j];
 #pragma unroll
-      for (int q = 0; q < KPT; ++q) aW1[q] += sf[r][g * KPT + q] * d;
-      if (g == 0) ab1 += d;
+        for (int q = 0; q < KPT; ++q) aW1[q] += sf[r][g * KPT + q] * d;
+        if (g == 0) ab1 += d;
+      }
     }
     // dfeat[r][k] = sum_j dz1[r][j] W1[k][j]
     if (dfeat != nullptr) {
@@ -339,6 +357,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     }
     __syncthreads();
   }
+  if constexpr (PROB) return;
   // flush: coalesced atomics (lanes = consecutive j); a non-finite partial raises the flag the
   // flag-driven Adam decides from (chain control word 7)
   bool fin = isfinite(aW3) && isfinite(ab1) && isfinite(ab2) && isfinite(ab3);
@@ -456,9 +475,63 @@ at::Tensor head_bwd(const at::Tensor& feat, const at::Tensor& W1, const at::Tens
   return dfeat;
 }
 
+// Frozen-weight head for attribution: [z1 (R,64), z2 (R,64), prob (R) = sigmoid(logit)]
+std::vector<at::Tensor> head_prob_fwd(const at::Tensor& feat, const at::Tensor& W1, const at::Tensor& b1,
+                                      const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& W3,
+                                      const at::Tensor& b3, double alpha1, double alpha2) {
+  TORCH_CHECK(feat.is_cuda() && feat.scalar_type() == at::kFloat && feat.dim() == 2 && feat.stride(1) == 1 &&
+                  feat.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(feat.data_ptr()) % 16 == 0,
+              "gnnqc head_prob_fwd: feat must be a float32 GPU matrix with 16-byte aligned rows");
+  const int R = (int)feat.size(0), F = (int)feat.size(1);
+  const at::Tensor* ops[] = {&W1, &b1, &W2, &b2, &W3, &b3};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "head operand");
+  TORCH_CHECK(R >= 1 && W1.size(0) == F && W1.size(1) == HU && W2.size(0) == HU && W2.size(1) == HU &&
+                  W3.numel() == HU && b1.numel() == HU && b2.numel() == HU && b3.numel() == 1,
+              "gnnqc head_prob_fwd: expected Dense(F,64)-Dense(64,64)-Dense(64,1)");
+  c10::DeviceGuard guard(feat.device());
+  auto opt = feat.options();
+  at::Tensor z1 = at::empty({R, HU}, opt), z2 = at::empty({R, HU}, opt), pr = at::empty({R}, opt);
+  const int grid = head_grid(R, true);
+  GQ_HEAD_F_DISPATCH(F, hipLaunchKernelGGL((head_fwd_kernel<FF, true>), dim3(grid), dim3(256), 0, stream(),
+                                           feat.data_ptr<float>(), (int)feat.stride(0), W1.data_ptr<float>(),
+                                           b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
+                                           W3.data_ptr<float>(), b3.data_ptr<float>(), nullptr, nullptr, R,
+                                           (float)alpha1, (float)alpha2, 0.f, 0.f, z1.data_ptr<float>(),
+                                           z2.data_ptr<float>(), pr.data_ptr<float>(), nullptr, nullptr, nullptr, 2));
+  GQ_LAUNCH_CHECK();
+  return {z1, z2, pr};
+}
+
+// d sum_r sigmoid(z_r) / d feat of head_prob_fwd's rows (no weight gradients)
+at::Tensor head_prob_bwd(const at::Tensor& feat, const at::Tensor& W1, const at::Tensor& W2, const at::Tensor& W3,
+                         const at::Tensor& z1, const at::Tensor& z2, const at::Tensor& prob, double alpha1,
+                         double alpha2) {
+  const int R = (int)feat.size(0), F = (int)feat.size(1);
+  TORCH_CHECK(feat.is_cuda() && feat.scalar_type() == at::kFloat && feat.stride(1) == 1 && feat.stride(0) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(feat.data_ptr()) % 16 == 0, "gnnqc head_prob_bwd: feat layout");
+  const at::Tensor* ops[] = {&W1, &W2, &W3, &z1, &z2, &prob};
+  for (const at::Tensor* t : ops) check_f32_cuda(*t, "head_prob_bwd operand");
+  TORCH_CHECK(z1.size(0) == R && z2.size(0) == R && prob.numel() == R && W1.size(0) == F && W1.size(1) == HU &&
+                  W2.numel() == HU * HU && W3.numel() == HU, "gnnqc head_prob_bwd: shapes");
+  c10::DeviceGuard guard(feat.device());
+  at::Tensor dfeat = at::empty({R, F}, feat.options());
+  const int grid = head_grid(R);
+  GQ_HEAD_F_DISPATCH(F, hipLaunchKernelGGL((head_bwd_kernel<FF, true>), dim3(grid), dim3(256), 0, stream(),
+                                           feat.data_ptr<float>(), (int)feat.stride(0), W1.data_ptr<float>(),
+                                           W2.data_ptr<float>(), W3.data_ptr<float>(), z1.data_ptr<float>(),
+                                           z2.data_ptr<float>(), prob.data_ptr<float>(), nullptr, nullptr, R,
+                                           (float)alpha1, (float)alpha2, 0.f, 0.f, nullptr, nullptr,
+                                           dfeat.data_ptr<float>(), F, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                           nullptr, nullptr));
+  GQ_LAUNCH_CHECK();
+  return dfeat;
+}
+
 }  // namespace gq
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("head_fwd", &gq::head_fwd);
   m.impl("head_bwd", &gq::head_bwd);
+  m.impl("head_prob_fwd", &gq::head_prob_fwd);
+  m.impl("head_prob_bwd", &gq::head_prob_bwd);
 }

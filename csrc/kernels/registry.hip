@@ -137,6 +137,10 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("head_bwd(Tensor feat, Tensor W1, Tensor W2, Tensor W3, Tensor z1, Tensor z2, Tensor logits, Tensor y, "
         "Tensor mask, float alpha1, float alpha2, float w0, float w1, Tensor gout, Tensor aux, Tensor(a!) dW1, "
         "Tensor(b!) db1, Tensor(c!) dW2, Tensor(d!) db2, Tensor(e!) dW3, Tensor(f!) db3, bool need_dfeat) -> Tensor");
+  m.def("head_prob_fwd(Tensor feat, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, float alpha1, "
+        "float alpha2) -> Tensor[]");
+  m.def("head_prob_bwd(Tensor feat, Tensor W1, Tensor W2, Tensor W3, Tensor z1, Tensor z2, Tensor prob, "
+        "float alpha1, float alpha2) -> Tensor");
   // MaxPooling1D with byte argmax (pool.hip)
   m.def("maxpool1d_fwd(Tensor x, int p) -> Tensor[]");
   m.def("maxpool1d_bwd(Tensor dy, Tensor idx, int T, int p) -> Tensor");

@@ -303,9 +303,27 @@ class IntegratedGradients:
             h0 = ops.ig_gcn_pool_fwd(x, w, anom, g.kernel.contiguous(), g.bias.contiguous(), st[2].contiguous(),
                                      st[3].contiguous(), g.prelu_alpha.contiguous(), a, int(Cp))
         h0.requires_grad_(True)
-        out = torch.sigmoid(m.head(m.time_layer.forward_time_major(h0, kk * B)))
-        y = self._select(out, B, kk, target)
-        (gh,) = torch.autograd.grad(y.sum(), h0)
+        feat = m.time_layer.forward_time_major(h0, kk * B)
+        spec = m.head_spec()
+        if (spec is not None and feat.dim() == 2 and feat.shape[1] in (32, 64, 128) and feat.dtype == torch.float32
+                and spec[0].kernel.shape[1] == 64 and tuple(spec[1].kernel.shape) == (64, 64)
+                and tuple(spec[2].kernel.shape) == (64, 1) and os.environ.get("GNNQC_IG_HEAD_HIP", "1") == "1"):
+            # the frozen head on HIP (head.hip, PROB mode): sigmoid outputs, then d sum(sigmoid) / d feat
+            # in one more launch; autograd only carries that gradient back through the LSTM stack
+            d1, d2, d3, a1, a2 = spec
+            ff = feat.detach()
+            if not (ff.stride(1) == 1 and ff.stride(0) % 4 == 0 and ff.data_ptr() % 16 == 0):
+                ff = ff.contiguous()
+            W1, W2, W3 = d1.kernel.contiguous(), d2.kernel.contiguous(), d3.kernel.contiguous()
+            z1, z2, prob = ops.head_prob_fwd(ff, W1, d1.bias.contiguous(), W2, d2.bias.contiguous(), W3,
+                                             d3.bias.contiguous(), float(a1), float(a2))
+            dfeat = ops.head_prob_bwd(ff, W1, W2, W3, z1, z2, prob, float(a1), float(a2))
+            (gh,) = torch.autograd.grad(feat, h0, dfeat)
+            y = prob
+        else:
+            out = torch.sigmoid(m.head(feat))
+            y = self._select(out, B, kk, target)
+            (gh,) = torch.autograd.grad(y.sum(), h0)
         path_pred_rows.copy_(y.detach().view(kk, B).to(path_pred_rows.dtype))
         ops.ig_gcn_pool_bwd(x, w, mask, gh.contiguous(), g.kernel.contiguous(), g.bias.contiguous(),
                             st[2].contiguous(), st[3].contiguous(), g.prelu_alpha.contiguous(), a, wt.float(),

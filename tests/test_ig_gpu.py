@@ -124,3 +124,45 @@ def test_ig_graph_replay_matches_eager(cuda_device, cml_windows):
     for k in ("grad_x", "grad_anom", "pred", "path_pred"):
         err = (got[k] - ref[k]).abs().max().item()
         assert err <= 1e-5 * ref[k].abs().max().item() + 1e-7, (k, err)
+
+
+def test_head_prob_kernels_match_torch(cuda_device):
+    """head_prob_fwd / head_prob_bwd (head.hip PROB mode): sigmoid of the Dense-LeakyReLU head and
+    the input gradient of sum(sigmoid) against autograd on a plain fp32 PyTorch head."""
+    from gnnqc.ops.head import head_eager
+    from gnnqc.utils.native import hip_ops
+    torch.manual_seed(0)
+    for R, F in ((37, 128), (300, 64)):
+        feat = torch.randn(R, F, device=cuda_device)
+        W1, b1 = torch.randn(F, 64, device=cuda_device) * 0.2, torch.randn(64, device=cuda_device) * 0.1
+        W2, b2 = torch.randn(64, 64, device=cuda_device) * 0.2, torch.randn(64, device=cuda_device) * 0.1
+        W3, b3 = torch.randn(64, 1, device=cuda_device) * 0.3, torch.randn(1, device=cuda_device) * 0.1
+        z1, z2, prob = hip_ops().head_prob_fwd(feat, W1, b1, W2, b2, W3, b3, 0.3, 0.2)
+        dfeat = hip_ops().head_prob_bwd(feat, W1, W2, W3, z1, z2, prob, 0.3, 0.2)
+        f = feat.clone().requires_grad_(True)
+        ref = torch.sigmoid(head_eager(f, W1, b1, W2, b2, W3, b3, 0.3, 0.2))
+        (g,) = torch.autograd.grad(ref.sum(), f)
+        torch.testing.assert_close(prob, ref.detach(), atol=2e-6, rtol=1e-5)
+        torch.testing.assert_close(dfeat, g, atol=1e-6, rtol=1e-4)
+
+
+def test_ig_hip_head_matches_torch_head(cuda_device, cml_windows, monkeypatch):
+    """The path-folded IG with the frozen head on HIP (GNNQC_IG_HEAD_HIP=1, default) == with the
+    PyTorch head (rocBLAS GEMMs + aten LeakyReLU / sigmoid)."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.xai.ig import IntegratedGradients
+    pc, ws = cml_windows
+    torch.manual_seed(7)
+    model = GCNClassifier(C.default("model_cml"), pc).to(cuda_device)
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    b = st.gather(torch.tensor([3, 8, 21, 33], device=cuda_device))
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GNNQC_IG_HEAD_HIP", flag)
+        res[flag] = IntegratedGradients(model, "cml", m_steps=24, use_graph=False).attribute(b)
+    torch.cuda.synchronize()
+    for k in ("grad_x", "grad_anom", "pred", "path_pred"):
+        err = (res["1"][k] - res["0"][k]).abs().max().item()
+        assert err <= 1e-5 * res["0"][k].abs().max().item() + 1e-7, (k, err)

@@ -16,7 +16,7 @@ def test_hip_library_registers_its_ops():
             "import sys; ops = torch.ops.gnnqc; "
             "names = ['lstm_chain_head_fwd', 'lstm_chain_head_bwd', 'lstm_grads_multi', 'gcn_fused_bwd', "
             "'adam_flagged', 'time4_head_bwd', 'lstm_defer_reduce', 'lstm_reduce_flush', 'gcn_fused_fwd', "
-            "'gcn_prod_flush', 'gcn_coef_flush', 'gcn_coef_bwd']; "
+            "'gcn_prod_flush', 'gcn_coef_flush', 'gcn_coef_bwd', 'head_prob_fwd', 'head_prob_bwd']; "
             "[getattr(ops, n) for n in names]; print('ok')" % LIB)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stderr[-2000:])
