@@ -1350,9 +1350,14 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   unsigned long long rq[D];
   unsigned ri[D];
   auto sidx = [&](int tt) { return ((((size_t)tt * ntiles + tile) * NW + w)) * 64 + lane; };
+  // tt / P as a multiply-high with the magic floor(2^32 / P) + 1 (exact for tt * P < 2^32; here
+  // tt < 4096, P <= 255): the per-step integer divisions by the run-time pool size cost the
+  // un-pooling stages ~160 shader clocks per step on the dh staging (phase table, round 5)
+  const unsigned pmag = UP ? 0xFFFFFFFFu / (unsigned)max(P, 1) + 1u : 0u;
+  auto divp = [&](int tt) { return (int)__umulhi((unsigned)tt, pmag); };
   // source time of the dh of time tt (-1: past the last pooling window -> zero gradient)
   auto src_t = [&](int tt) {
-    if constexpr (UP) return tt < Ts * P ? tt / P : -1;
+    if constexpr (UP) return tt < Ts * P ? divp(tt) : -1;
     else return tt;
   };
   const size_t eoff = (size_t)row0 * H + tid;        // this lane's dh element in a [Mp][H] row block
@@ -1377,7 +1382,8 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         rq[J] = chain_wait(S.din + eoff + (size_t)max(st, 0) * hstep, tagb | (unsigned)max(st, 0), ctl);
     }
     const float v = __uint_as_float((unsigned)rq[J]);
-    const bool keep = st >= 0 && (!UP || ri[J] == (unsigned)(tt % P));
+    bool keep = st >= 0;
+    if constexpr (UP) keep = keep && ri[J] == (unsigned)(tt - st * P);
     return keep ? v : 0.f;
   };
   // dz storer (one float4 granule of the [16][4H] tile per thread)
@@ -2068,6 +2074,16 @@ static long long* chain_trace_buf(int dev) {
 
 // tile 0's per-step phase clocks [CHAIN_MAX stages][CHAIN_PROF_STEPS][8] of the last launch with
 // GNNQC_CHAIN_PROF=1 (forward and backward use the same buffer)
+static long long* chain_prof_buf(int dev);
+// zero the phase-clock buffer before a profiled launch: a stage with fewer than CHAIN_PROF_STEPS
+// steps (or fewer marks) than the previous launch's would otherwise leave that launch's rows behind
+// (the round-4 table's backward rows 0-1 and m6 columns were such leftovers)
+static void chain_prof_clear(int dev) {
+  long long* pb = chain_prof_buf(dev);
+  if (pb != nullptr)
+    TORCH_CHECK(hipMemsetAsync(pb, 0, CHAIN_MAX * CHAIN_PROF_STEPS * 8 * sizeof(long long), stream()) == hipSuccess,
+                "chain prof clear");
+}
 static long long* chain_prof_buf(int dev) {
 #ifdef GQ_CHAIN_PROF
   static const bool on = [] {
@@ -2228,6 +2244,7 @@ static std::vector<at::Tensor> chain_fwd_impl(const at::Tensor& x, at::TensorLis
   A.Mp = Mp;
   A.ctl = chain_ctl(x.get_device());
   A.trace = chain_trace_buf(x.get_device());
+  chain_prof_clear(x.get_device());
   std::vector<at::Tensor> out;
   at::Tensor prev_stream;
   int T = (int)x.size(0), Din = (int)x.size(2);
@@ -2503,6 +2520,7 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
   A.Mp = Mp;
   A.ctl = chain_ctl(dh.get_device());
   A.trace = chain_trace_buf(dh.get_device());
+  chain_prof_clear(dh.get_device());
   std::vector<at::Tensor> dzs;
   at::Tensor dx, prev;
   for (int s = 0; s < ns; ++s) {
