@@ -669,6 +669,7 @@ __device__ __forceinline__ void chain_stage(const ChainStage& S, int tile, int n
     } else if (publisher) {
       for (int t = 0; t < T; ++t) {
         if (t >= 1) publish_step(t - 1);
+        chain_mark_wave(pr, t, 7);         // (the publisher reaches the step barrier)
         lds_barrier();
       }
       publish_step(T - 1);
@@ -1209,6 +1210,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
 #pragma unroll
             for (int r = 0; r < 4; ++r) dxs[p][col][16 * xb + 4 * quad + r] = a[r];
           }
+          chain_mark_wave((S.prof != nullptr && tile == 0) ? S.prof : nullptr, s, 6);   // (dx tile in LDS)
         }
       }
       __syncthreads();
@@ -1264,11 +1266,13 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         }
         __syncthreads();
       } else {
+        long long* prw = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
         for (int s = 0; s < nsteps; ++s) {
           lds_barrier();
           const int t = T - 1 - s;
           if (s < T) store_dz(s);
           if (s >= 1 && s <= T) publish((s - 1) & 1, t + 1);
+          if (s < T) chain_mark_wave(prw, s, 7);   // (the publisher's work of the step is issued)
         }
         __syncthreads();
         publish((T - 1) & 1, 0);

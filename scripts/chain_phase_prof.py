@@ -77,7 +77,8 @@ def main():
     print(json.dumps({"launch": "fwd (chain6 + time4 stage)", "stages": phases(pf, 4)}), flush=True)
     # I/O waves (marks 4..6 of the step whose x they stage: start, tile staged, next load issued),
     # relative to compute wave 0's step start
-    print(json.dumps({"launch": "fwd marks vs compute start", "stages": marks_rel(pf, 7)}), flush=True)
+    # (+ m7: the publisher wave reaches the step barrier)
+    print(json.dumps({"launch": "fwd marks vs compute start", "stages": marks_rel(pf, 8)}), flush=True)
     h4, g4, c4, logits, loss = outs[-5:]
     hb = outs[-6]          # (the head backward the forward launch precomputed)
     pk = outs[-7]
@@ -99,6 +100,7 @@ def main():
     # 4 dx done; the split-K stages (H >= 32) 0..5 as in the docstring
     print(json.dumps({"launch": "bwd (time4 stage + chain6)", "stages": phases(pb, 5)}), flush=True)
     # H = 16 stages' I/O waves: marks 5..7 = staging start, tile staged, next loads issued
+    # (non-I/O H = 16 stages: m6 the dx wave's tile is in LDS, m7 the publisher's stores are issued)
     print(json.dumps({"launch": "bwd marks vs compute start", "stages": marks_rel(pb, 8)}), flush=True)
     st = ops.lstm_chain_status(x).cpu().tolist()
     print(json.dumps({"status": st}), flush=True)
