@@ -130,9 +130,10 @@ def test_peer_fused_adam_matches_separate_kernels_two_ranks(tmp_path):
     assert a["steps"] == c["steps"] == 16 and a["skipped"] == c["skipped"] == 0
     for k in ("p", "p2", "loss"):
         # ranks of one run agree bitwise; the two runs differ only by the float-atomic order of the
-        # GCN backward (a separate process each)
+        # GCN backward (a separate process each), which 16 Adam steps amplify to ~2e-6 of the norm
+        # (measured); a wrong or missing slice update is orders of magnitude larger
         assert a[k] == b[k] and c[k] == d[k], (k, a[k], b[k], c[k], d[k])
-        assert abs(a[k] - c[k]) <= 1e-6 * abs(c[k]) + 1e-9, (k, a[k], c[k])
+        assert abs(a[k] - c[k]) <= 1e-4 * abs(c[k]) + 1e-9, (k, a[k], c[k])
 
 
 def test_peer_auto_mode_selects_and_trains(tmp_path):
