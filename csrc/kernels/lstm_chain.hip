@@ -1036,6 +1036,13 @@ struct ChainBStage {
   float* dx;                         // last stage: fp32 dx [T][Mp][Din]
   long long* trace_mid;              // profiling: time the step loop starts
   long long* prof;                   // profiling (GNNQC_CHAIN_PROF=1): tile 0's per-step phase clocks
+  // producer-side un-pooling (uidx != nullptr): the MaxPooling1D(uP) between this stage's input and the
+  // stage below is undone HERE - its argmax bytes [T][Mp][Din] are staged in LDS once and every dx
+  // element is published as uP full-resolution granules (value at the argmax step, 0 elsewhere) into a
+  // [uT][Mp][Din] stream, so the stage below (punp = 1) streams plain dh with no argmax load or select
+  // on its recurrence
+  const unsigned char* uidx;
+  int uP, uT, punp;
   int H, T, Din, Dw, KX, P, Ts;
 };
 
@@ -1062,6 +1069,7 @@ struct ChainBArgs {
   long long* trace;
   ChainT4B t4;                       // t4.on: blocks [ns nt8, (ns + 1) nt8) run time4's backward
 };
+static_assert(sizeof(ChainBArgs) <= 4096, "chain backward kernel arguments");
 
 template <int H, int KX>
 struct ChainBLds {
@@ -1223,6 +1231,23 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       const int nx = 16 * Din;
       const size_t xstep = (size_t)Mp * Din;
       const int dq = 64 / Din, dr = 64 % Din;
+      // producer-side un-pooling: this tile's argmax bytes of all T steps in LDS (loaded before the
+      // publisher's first store, so no load of it waits behind its write-through stores), and the
+      // full-resolution steps past the last pooling window published as zeros up front (the stage
+      // below needs them first)
+      constexpr int UPOFF = ((SK ? LK::BYTES : L::BYTES) + 15) / 16 * 16;
+      unsigned char* ub = reinterpret_cast<unsigned char*>(smem + UPOFF);
+      const bool unp = XO && S.uidx != nullptr;
+      if (unp) {
+        const int nw4 = T * 16 * Din / 4;
+        for (int i = lane; i < nw4; i += 64) {
+          const int e = 4 * i, ts = e / (16 * Din), r = e % (16 * Din);
+          *reinterpret_cast<unsigned*>(ub + e) =
+              *reinterpret_cast<const unsigned*>(S.uidx + ((size_t)ts * Mp + row0) * Din + r);
+        }
+        for (int tt = T * S.uP; tt < S.uT; ++tt)
+          for (int e = lane; e < nx; e += 64) st_granule(S.sout + (size_t)row0 * Din + e + (size_t)tt * xstep, 0.f, tagb | (unsigned)tt);
+      }
       auto publish = [&](int buf, int ts) {
         const unsigned tag = tagb | (unsigned)ts;
         int row = lane / Din, k = lane % Din;
@@ -1235,9 +1260,18 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
           } else {
             v = dxs[buf][row][k];
           }
-          const size_t o = (size_t)row0 * Din + e + (size_t)ts * xstep;
-          if constexpr (XO) st_granule(S.sout + o, v, tag);
-          else S.dx[o] = v;
+          if (unp) {
+            const unsigned b = ub[(ts * 16 + row) * Din + k];
+            for (int qq = 0; qq < S.uP; ++qq) {
+              const int tt = ts * S.uP + qq;
+              st_granule(S.sout + (size_t)row0 * Din + e + (size_t)tt * xstep, b == (unsigned)qq ? v : 0.f,
+                         tagb | (unsigned)tt);
+            }
+          } else {
+            const size_t o = (size_t)row0 * Din + e + (size_t)ts * xstep;
+            if constexpr (XO) st_granule(S.sout + o, v, tag);
+            else S.dx[o] = v;
+          }
           row += dq;
           k += dr;
           if (k >= Din) { k -= Din; ++row; }
@@ -2046,7 +2080,7 @@ __global__ __launch_bounds__(1024) void lstm_chain_bwd_kernel(ChainBArgs A) {
   else GQ_CHAINB_BODY3(HH, KXX, DD, SRCV, UPV, false)
 #define GQ_CHAINB_BODY(HH, KXX, DD)                                                     \
   {                                                                                     \
-    if (src) { if (S.P > 0) { GQ_CHAINB_BODY2(HH, KXX, DD, true, true) }                \
+    if (src) { if (S.P > 0 && !S.punp) { GQ_CHAINB_BODY2(HH, KXX, DD, true, true) }    \
                else { GQ_CHAINB_BODY2(HH, KXX, DD, true, false) } }                     \
     else { if (S.P > 0) { GQ_CHAINB_BODY3(HH, KXX, DD, false, true, true) }             \
            else { GQ_CHAINB_BODY3(HH, KXX, DD, false, false, true) } }                  \
@@ -2559,8 +2593,36 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
     S.dz = bf16_ptr(dz);
     dzs.push_back(dz);
     const bool last = s + 1 == ns && ns > 1;     // (a single stage publishes: profiling)
+    // producer-side un-pooling of the stage below's input pool (ChainBStage::uidx)
+    S.uidx = nullptr;
+    S.uP = 0;
+    S.uT = 0;
+    S.punp = s > 0 ? A.st[s - 1].uidx != nullptr : 0;
+    int sT = T;                                  // rows of this stage's dx stream
+    if (!last && s + 1 < ns && pool[s + 1] > 0) {
+      static const bool on = [] {
+        const char* e = std::getenv("GNNQC_CHAINB_PUNPOOL");
+        return e == nullptr || std::atoi(e) != 0;
+      }();
+      const int Hs = H, KXs = (Din + 31) / 32;
+      const int stage_bytes = Hs >= 32 ? (KXs == 1 ? (Hs == 32 ? ChainBLdsSK<32, 1>::BYTES : ChainBLdsSK<64, 1>::BYTES)
+                                                   : (Hs == 32 ? ChainBLdsSK<32, 2>::BYTES : ChainBLdsSK<64, 2>::BYTES))
+                                       : (KXs == 1 ? ChainBLds<16, 1>::BYTES : ChainBLds<16, 2>::BYTES);
+      const long ub = (long)T * 16 * Din;
+      const int uT = (int)T_in[s + 1];
+      // (the publisher wave un-pools: H = 64 stages fill the workgroup with compute waves and store dx themselves)
+      if (on && 16 * H + 64 <= 1024 && (stage_bytes + 15) / 16 * 16 + ub <= CHAINB_LDS && (long)uT * Mp * Din * 8 < (1L << 31) &&
+          T * (int)pool[s + 1] <= uT) {
+        TORCH_CHECK(pidx[s + 1].numel() == (long)T * Mp * Din && pidx[s + 1].scalar_type() == at::kByte,
+                    "lstm_chain_bwd: argmax bytes of stage ", s + 1);
+        S.uidx = pidx[s + 1].data_ptr<uint8_t>();
+        S.uP = (int)pool[s + 1];
+        S.uT = uT;
+        sT = uT;
+      }
+    }
     if (!last) {
-      at::Tensor so = at::empty({T + 1, Mp, Din}, opt.dtype(at::kLong));
+      at::Tensor so = at::empty({sT + 1, Mp, Din}, opt.dtype(at::kLong));
       S.sout = reinterpret_cast<unsigned long long*>(so.data_ptr<int64_t>());
       S.dx = nullptr;
       keep.push_back(so);
