@@ -1123,6 +1123,15 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #define CHAINB_DXW 1         // H = 16 stages: dx = W dz by a dedicated wave (not by compute waves 0 / 1 between
                              // the step's MFMA and the next cell phase, which put it on the recurrence's path)
 #endif
+#ifndef CHAINB_PUBBATCH
+#define CHAINB_PUBBATCH 4    // backward publisher: LDS reads of this many dx elements per lane, then their stores
+#endif
+#ifndef CHAINB_NPUB
+#define CHAINB_NPUB 2        // publisher waves per H <= 32 stage (each publishes every NPUB-th 64-element slice)
+#endif
+#ifndef CHAINB_DZW
+#define CHAINB_DZW 1         // 1: a dz wave stores each step's dz tile (else the publisher wave does)
+#endif
 #ifndef CHAINB_G
 #define CHAINB_G 2           // waves per backward I/O group: 2 = one for the cell records, one for dh
 #endif
@@ -1138,9 +1147,19 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #endif
 // threads of a backward stage workgroup: compute waves (+ the publisher wave when it fits, + the dx
 // wave of the split-free H = 16 stages)
-__host__ __device__ constexpr bool chainb_dxw(int h) { return CHAINB_DXW && h < 32 && TMC<16>::NT + 128 <= 1024; }
+__host__ __device__ constexpr bool chainb_dxw(int h) {
+  return CHAINB_DXW && h < 32 && TMC<16>::NT + 64 * CHAINB_NPUB + 64 <= 1024;
+}
+// (+ the dz wave: the step's dz tile leaves from its own wave, beside the publisher's dx granules)
+// publisher waves of a stage (0: H = 64, whose compute waves fill the workgroup)
+__host__ __device__ constexpr int chainb_npub(int h, int nt) {
+  return nt + 64 > 1024 ? 0 : (nt + 64 * CHAINB_NPUB + (chainb_dxw(h) ? 64 : 0) + 64 <= 1024 ? CHAINB_NPUB : 1);
+}
+__host__ __device__ constexpr bool chainb_dzw(int h, int nt) {
+  return CHAINB_DZW && chainb_npub(h, nt) > 0 && nt + 64 * chainb_npub(h, nt) + 64 + (chainb_dxw(h) ? 64 : 0) <= 1024;
+}
 __host__ __device__ constexpr int chainb_live_threads(int h, int nt) {
-  return nt + (nt + 64 <= 1024 ? 64 : 0) + (chainb_dxw(h) ? 64 : 0);
+  return nt + 64 * chainb_npub(h, nt) + (chainb_dxw(h) ? 64 : 0) + (chainb_dzw(h, nt) ? 64 : 0);
 }
 
 // lstm_tm_bwd_body (DZ + DX) with one dh element per lane from the stage above's stream
@@ -1178,14 +1197,41 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   // step time). The publisher joins the same barriers and reads the dx tile from LDS.
   const int row0 = tile * 16;
   constexpr bool PUBW = NT + 64 <= 1024;
+  constexpr int NPUB = chainb_npub(H, NT);
   constexpr bool DXW = !SK && chainb_dxw(H);
+  constexpr bool DZW = PUBW && chainb_dzw(H, NT);
+  static_assert(PUBW == (NPUB > 0), "publisher waves");
   static_assert(!DXW || PUBW, "the dx wave hands its tiles to the publisher");
+  if constexpr (DZW) {
+    // dz wave: after step s's barrier (the second one of the step, SK: its first), the dz tile of step s
+    // from zs[s & 1] (held until step s + 2's cell phase) -> HBM with 16-byte stores
+    if (tid >= NT + 64 * NPUB + (DXW ? 64 : 0)) {
+      const int nsteps = (T + D - 1) / D * D;
+      __syncthreads();
+      __syncthreads();
+      for (int s = 0; s < nsteps; ++s) {
+        lds_barrier();
+        if (s < T) {
+          const int pb = s & 1;
+          __bf16* zt = S.dz + ((size_t)(T - 1 - s) * Mp + row0) * G4;
+#pragma unroll
+          for (int q = lane; q < 16 * G4 / 8; q += 64) {
+            const int e = 8 * q;
+            *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][e % G4]);
+          }
+        }
+        if constexpr (SK) lds_barrier();
+      }
+      __syncthreads();
+      return;
+    }
+  }
   if constexpr (DXW) {
     // dx wave: after step s's barrier, dx^T = W dz^T of that step from zs[s & 1] into dxs[s & 1]
     // (the publisher stores it after the next barrier, as before). It joins barrier s + 1 only once
     // done, and zs[s & 1] is rewritten only in step s + 2's cell phase (after barrier s + 1), so the
     // compute waves go from their dh_rec MFMA straight to the next cell phase.
-    if (tid >= NT + 64) {
+    if (tid >= NT + 64 * NPUB) {
       const int col = lane & 15, quad = lane >> 4;
       bf16x8_t wx[NXB][KB];
 #pragma unroll
@@ -1230,7 +1276,10 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       const int nsteps = (T + D - 1) / D * D;
       const int nx = 16 * Din;
       const size_t xstep = (size_t)Mp * Din;
-      const int dq = 64 / Din, dr = 64 % Din;
+      // publisher wave pj of NPUB publishes the 64-element slices pj, pj + NPUB, ... of each dx tile
+      const int pj = (tid - NT) >> 6;
+      constexpr int ESTR = 64 * (NPUB > 0 ? NPUB : 1);
+      const int dq = ESTR / Din, dr = ESTR % Din;
       // producer-side un-pooling: this tile's argmax bytes of all T steps in LDS (loaded before the
       // publisher's first store, so no load of it waits behind its write-through stores), and the
       // full-resolution steps past the last pooling window published as zeros up front (the stage
@@ -1240,41 +1289,61 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       const bool unp = XO && S.uidx != nullptr;
       if (unp) {
         const int nw4 = T * 16 * Din / 4;
-        for (int i = lane; i < nw4; i += 64) {
+        for (int i = tid - NT; i < nw4; i += ESTR) {
           const int e = 4 * i, ts = e / (16 * Din), r = e % (16 * Din);
           *reinterpret_cast<unsigned*>(ub + e) =
               *reinterpret_cast<const unsigned*>(S.uidx + ((size_t)ts * Mp + row0) * Din + r);
         }
         for (int tt = T * S.uP; tt < S.uT; ++tt)
-          for (int e = lane; e < nx; e += 64) st_granule(S.sout + (size_t)row0 * Din + e + (size_t)tt * xstep, 0.f, tagb | (unsigned)tt);
+          for (int e = tid - NT; e < nx; e += ESTR)
+            st_granule(S.sout + (size_t)row0 * Din + e + (size_t)tt * xstep, 0.f, tagb | (unsigned)tt);
       }
+      // LDS reads of CHAINB_PUBBATCH elements per lane first, then their stores: a read -> wait -> store
+      // loop per element paid one LDS round trip per element on the publisher's step (16 Din / 64 =
+      // Din / 4 elements per lane, the same count on every lane since Din % 4 == 0). (All Din / 4 at
+      // once, up to 16, pushed the kernel from 32 to 176 bytes of scratch: chain bwd 133 -> 258 us.)
+      constexpr int PUBN = CHAINB_PUBBATCH > 0 ? CHAINB_PUBBATCH : 1;   // elements per lane per batch
       auto publish = [&](int buf, int ts) {
         const unsigned tag = tagb | (unsigned)ts;
-        int row = lane / Din, k = lane % Din;
-        for (int e = lane; e < nx; e += 64) {        // (the publisher's own divergence only)
-          float v;
-          if constexpr (SK) {
-            v = 0.f;
+        for (int e0 = 64 * pj; e0 < nx; e0 += ESTR * PUBN) {
+        const int niter = min((nx - e0 + ESTR - 1) / ESTR, PUBN);
+        float vv[PUBN];
+        unsigned bb[PUBN];
+        int row = (lane + e0) / Din, k = (lane + e0) % Din;
 #pragma unroll
-            for (int g = 0; g < KXG; ++g) v += xpart[buf][g][row][k];
-          } else {
-            v = dxs[buf][row][k];
-          }
-          if (unp) {
-            const unsigned b = ub[(ts * 16 + row) * Din + k];
-            for (int qq = 0; qq < S.uP; ++qq) {
-              const int tt = ts * S.uP + qq;
-              st_granule(S.sout + (size_t)row0 * Din + e + (size_t)tt * xstep, b == (unsigned)qq ? v : 0.f,
-                         tagb | (unsigned)tt);
+        for (int i = 0; i < PUBN; ++i) {
+          if (i < niter) {                          // wave-uniform
+            if constexpr (SK) {
+              float v = 0.f;
+#pragma unroll
+              for (int g = 0; g < KXG; ++g) v += xpart[buf][g][row][k];
+              vv[i] = v;
+            } else {
+              vv[i] = dxs[buf][row][k];
             }
-          } else {
-            const size_t o = (size_t)row0 * Din + e + (size_t)ts * xstep;
-            if constexpr (XO) st_granule(S.sout + o, v, tag);
-            else S.dx[o] = v;
+            bb[i] = unp ? (unsigned)ub[(ts * 16 + row) * Din + k] : 0u;
           }
           row += dq;
           k += dr;
           if (k >= Din) { k -= Din; ++row; }
+        }
+#pragma unroll
+        for (int i = 0; i < PUBN; ++i) {
+          if (i < niter) {
+            const int e = e0 + lane + ESTR * i;
+            if (unp) {
+              for (int qq = 0; qq < S.uP; ++qq) {
+                const int tt = ts * S.uP + qq;
+                st_granule(S.sout + (size_t)row0 * Din + e + (size_t)tt * xstep, bb[i] == (unsigned)qq ? vv[i] : 0.f,
+                           tagb | (unsigned)tt);
+              }
+            } else {
+              const size_t o = (size_t)row0 * Din + e + (size_t)ts * xstep;
+              if constexpr (XO) st_granule(S.sout + o, vv[i], tag);
+              else S.dx[o] = vv[i];
+            }
+          }
+        }
         }
       };
       // ... and the step's dz tile (16-byte stores from LDS; zs[s & 1] holds it from the barrier
@@ -1294,17 +1363,17 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       if constexpr (SK) {            // two barriers per step; step s's dx tile is complete after the second
         for (int s = 0; s < nsteps; ++s) {
           lds_barrier();
-          if (s < T) store_dz(s);
+          if (!DZW && s < T) store_dz(s);
           lds_barrier();
           if (s < T) publish(s & 1, T - 1 - s);
         }
         __syncthreads();
       } else {
-        long long* prw = (S.prof != nullptr && tile == 0) ? S.prof : nullptr;
+        long long* prw = (S.prof != nullptr && tile == 0 && pj == 0) ? S.prof : nullptr;
         for (int s = 0; s < nsteps; ++s) {
           lds_barrier();
           const int t = T - 1 - s;
-          if (s < T) store_dz(s);
+          if (!DZW && s < T) store_dz(s);
           if (s >= 1 && s <= T) publish((s - 1) & 1, t + 1);
           if (s < T) chain_mark_wave(prw, s, 7);   // (the publisher's work of the step is issued)
         }
