@@ -1127,7 +1127,8 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #define CHAINB_PUBBATCH 4    // backward publisher: LDS reads of this many dx elements per lane, then their stores
 #endif
 #ifndef CHAINB_NPUB
-#define CHAINB_NPUB 2        // publisher waves per H <= 32 stage (each publishes every NPUB-th 64-element slice)
+#define CHAINB_NPUB 4        // publisher waves per H <= 32 stage (each publishes every NPUB-th 64-element slice;
+                             // same-box chain bwd 156.8 / 136.9 / 133.0 / 130.0 us for 1 / 2 / 3 / 4)
 #endif
 #ifndef CHAINB_DZW
 #define CHAINB_DZW 1         // 1: a dz wave stores each step's dz tile (else the publisher wave does)
@@ -1153,7 +1154,9 @@ __host__ __device__ constexpr bool chainb_dxw(int h) {
 // (+ the dz wave: the step's dz tile leaves from its own wave, beside the publisher's dx granules)
 // publisher waves of a stage (0: H = 64, whose compute waves fill the workgroup)
 __host__ __device__ constexpr int chainb_npub(int h, int nt) {
-  return nt + 64 > 1024 ? 0 : (nt + 64 * CHAINB_NPUB + (chainb_dxw(h) ? 64 : 0) + 64 <= 1024 ? CHAINB_NPUB : 1);
+  return nt + 64 > 1024 ? 0
+       : chainb_max(1, CHAINB_NPUB < (1024 - nt - (chainb_dxw(h) ? 64 : 0) - 64) / 64
+                           ? CHAINB_NPUB : (1024 - nt - (chainb_dxw(h) ? 64 : 0) - 64) / 64);
 }
 __host__ __device__ constexpr bool chainb_dzw(int h, int nt) {
   return CHAINB_DZW && chainb_npub(h, nt) > 0 && nt + 64 * chainb_npub(h, nt) + 64 + (chainb_dxw(h) ? 64 : 0) <= 1024;
