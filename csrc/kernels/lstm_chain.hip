@@ -1130,6 +1130,9 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #define CHAINB_NPUB 4        // publisher waves per H <= 32 stage (each publishes every NPUB-th 64-element slice;
                              // same-box chain bwd 156.8 / 136.9 / 133.0 / 130.0 us for 1 / 2 / 3 / 4)
 #endif
+#ifndef CHAINB_PUBPRIO
+#define CHAINB_PUBPRIO 2     // s_setprio of the backward publisher and dz waves (same-box A/B: chain bwd 127.3 -> 124.2 us, bench 0.2626 -> 0.2596 ms)
+#endif
 #ifndef CHAINB_DZW
 #define CHAINB_DZW 1         // 1: a dz wave stores each step's dz tile (else the publisher wave does)
 #endif
@@ -1209,6 +1212,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
     // dz wave: after step s's barrier (the second one of the step, SK: its first), the dz tile of step s
     // from zs[s & 1] (held until step s + 2's cell phase) -> HBM with 16-byte stores
     if (tid >= NT + 64 * NPUB + (DXW ? 64 : 0)) {
+      if (CHAINB_PUBPRIO > 0) __builtin_amdgcn_s_setprio(CHAINB_PUBPRIO);
       const int nsteps = (T + D - 1) / D * D;
       __syncthreads();
       __syncthreads();
@@ -1276,6 +1280,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   }
   if constexpr (PUBW) {
     if (tid >= NT) {
+      if (CHAINB_PUBPRIO > 0) __builtin_amdgcn_s_setprio(CHAINB_PUBPRIO);
       const int nsteps = (T + D - 1) / D * D;
       const int nx = 16 * Din;
       const size_t xstep = (size_t)Mp * Din;
