@@ -1133,6 +1133,9 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #ifndef CHAINB_PUBPRIO
 #define CHAINB_PUBPRIO 2     // s_setprio of the backward publisher and dz waves (same-box A/B: chain bwd 127.3 -> 124.2 us, bench 0.2626 -> 0.2596 ms)
 #endif
+#ifndef CHAINB_DXPRIO
+#define CHAINB_DXPRIO 2      // s_setprio of the backward dx wave (same-box A/B: chain bwd 124.0 -> 122.2 us, bench 0.2589 -> 0.2562 ms)
+#endif
 #ifndef CHAINB_DZW
 #define CHAINB_DZW 1         // 1: a dz wave stores each step's dz tile (else the publisher wave does)
 #endif
@@ -1239,6 +1242,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
     // done, and zs[s & 1] is rewritten only in step s + 2's cell phase (after barrier s + 1), so the
     // compute waves go from their dh_rec MFMA straight to the next cell phase.
     if (tid >= NT + 64 * NPUB) {
+      if (CHAINB_DXPRIO > 0) __builtin_amdgcn_s_setprio(CHAINB_DXPRIO);
       const int col = lane & 15, quad = lane >> 4;
       bf16x8_t wx[NXB][KB];
 #pragma unroll
