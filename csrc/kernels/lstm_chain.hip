@@ -1136,6 +1136,10 @@ static constexpr int CHAINB_LDS = ChainT4BLds::BYTES > CHAINB_LDS_STAGE ? ChainT
 #ifndef CHAINB_DXPRIO
 #define CHAINB_DXPRIO 2      // s_setprio of the backward dx wave (same-box A/B: chain bwd 124.0 -> 122.2 us, bench 0.2589 -> 0.2562 ms)
 #endif
+#ifndef CHAINB_PUNPOOL
+#define CHAINB_PUNPOOL 0     // 1: producer-side un-pooling (ChainBStage::uidx). Off: against the round-5 baseline
+                             // build on one box it measured chain bwd 121.4 (on) / 123.9 (compiled in, off) vs 115.9 us
+#endif
 #ifndef CHAINB_DZW
 #define CHAINB_DZW 1         // 1: a dz wave stores each step's dz tile (else the publisher wave does)
 #endif
@@ -1298,7 +1302,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       // below needs them first)
       constexpr int UPOFF = ((SK ? LK::BYTES : L::BYTES) + 15) / 16 * 16;
       unsigned char* ub = reinterpret_cast<unsigned char*>(smem + UPOFF);
-      const bool unp = XO && S.uidx != nullptr;
+      const bool unp = CHAINB_PUNPOOL && XO && S.uidx != nullptr;
       if (unp) {
         const int nw4 = T * 16 * Din / 4;
         for (int i = tid - NT; i < nw4; i += ESTR) {
@@ -2683,7 +2687,7 @@ static std::vector<at::Tensor> chain_bwd_setup(ChainBArgs& A, std::vector<at::Te
     if (!last && s + 1 < ns && pool[s + 1] > 0) {
       static const bool on = [] {
         const char* e = std::getenv("GNNQC_CHAINB_PUNPOOL");
-        return e == nullptr || std::atoi(e) != 0;
+        return CHAINB_PUNPOOL && (e == nullptr || std::atoi(e) != 0);
       }();
       const int Hs = H, KXs = (Din + 31) / 32;
       const int stage_bytes = Hs >= 32 ? (KXs == 1 ? (Hs == 32 ? ChainBLdsSK<32, 1>::BYTES : ChainBLdsSK<64, 1>::BYTES)
