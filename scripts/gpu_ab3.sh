@@ -1,6 +1,6 @@
 cd "${GRAFT_REPO_ROOT}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-B=$PWD/gnnqc/_lib/variants/base.so
+B=${B:-$PWD/gnnqc/_lib/variants/base.so}
 VARIANTS="${V3:-cur:- base:GNNQC_HIP_LIB=$B}" bash scripts/gpu_prof_variants.sh > gpurun_out/ab3.txt 2>&1 || exit 3
 for r in 1 2; do
   for v in ${V3N:-cur base}; do
