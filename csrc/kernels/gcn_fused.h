@@ -440,6 +440,7 @@ struct GcnPending {
 bool gcn_coef_side_mode();
 GcnPending& gcn_pending(int dev);
 bool gcn_coef_take(int dev, GcnCoefFwdJob& job, std::vector<at::Tensor>& keep);
+bool gcn_coef_flush_dev(int dev);
 bool gcn_prod_take(int dev, GcnProdJob& job, std::vector<at::Tensor>& keep);
 bool gcn_prod_flush_dev(int dev);
 

@@ -541,6 +541,9 @@ std::vector<at::Tensor> gcn_fused_fwd(const at::Tensor& series, const at::Tensor
 #undef GQ_GF_FWD
   GQ_LAUNCH_CHECK();
   if (side) {
+    // a job left pending by an earlier forward (no chain forward took it: e.g. a second micro-batch
+    // forward before the first backward) runs now, or its coefficient tensor would never be written
+    gcn_coef_flush_dev(series.get_device());
     GcnPending& pd = gcn_pending(series.get_device());
     pd.job = GcnCoefFwdJob{};
     pd.job.D = D;
@@ -622,6 +625,16 @@ bool gcn_prod_flush(const at::Tensor& like) {
   return gcn_prod_flush_dev(like.get_device());
 }
 
+// run the pending coefficient side job of device ``dev`` on its own; returns whether there was one
+bool gcn_coef_flush_dev(int dev) {
+  GcnCoefFwdJob J{};
+  std::vector<at::Tensor> keep;
+  if (!gcn_coef_take(dev, J, keep)) return false;
+  hipLaunchKernelGGL(gcn_coef_fwd_kernel, dim3(J.Mp), dim3(1024), 0, stream(), J);
+  GQ_LAUNCH_CHECK();
+  return true;
+}
+
 // run the pending coefficient job on its own (nothing consumed it: no chain forward in between);
 // returns whether there was one (a pending deferred forward, which writes the coefficients too, runs
 // first)
@@ -629,12 +642,7 @@ bool gcn_coef_flush(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "gcn_coef_flush: a GPU tensor names the device");
   c10::DeviceGuard guard(like.device());
   if (gcn_prod_flush_dev(like.get_device())) return true;
-  GcnCoefFwdJob J{};
-  std::vector<at::Tensor> keep;
-  if (!gcn_coef_take(like.get_device(), J, keep)) return false;
-  hipLaunchKernelGGL(gcn_coef_fwd_kernel, dim3(J.Mp), dim3(1024), 0, stream(), J);
-  GQ_LAUNCH_CHECK();
-  return true;
+  return gcn_coef_flush_dev(like.get_device());
 }
 
 // The training backward's job (gcn_fused_bwd_body): adds dW, dgamma, dbeta, dalpha (float atomics)

@@ -1476,8 +1476,10 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   // tt / P as a multiply-high with the magic floor(2^32 / P) + 1 (exact for tt * P < 2^32; here
   // tt < 4096, P <= 255): the per-step integer divisions by the run-time pool size cost the
   // un-pooling stages ~160 shader clocks per step on the dh staging (phase table, round 5)
-  const unsigned pmag = UP ? 0xFFFFFFFFu / (unsigned)max(P, 1) + 1u : 0u;
-  auto divp = [&](int tt) { return (int)__umulhi((unsigned)tt, pmag); };
+  // un-pooling stages; the magic of P == 1 would be 2^32, which wraps to 0, so that pool size
+  // (a chain that ends in MaxPooling1D(1)) takes the identity instead
+  const unsigned pmag = (UP && P > 1) ? 0xFFFFFFFFu / (unsigned)P + 1u : 0u;
+  auto divp = [&](int tt) { return P > 1 ? (int)__umulhi((unsigned)tt, pmag) : tt; };
   // source time of the dh of time tt (-1: past the last pooling window -> zero gradient)
   auto src_t = [&](int tt) {
     if constexpr (UP) return tt < Ts * P ? divp(tt) : -1;

@@ -237,6 +237,9 @@ void peer_allreduce(at::Tensor g, at::IntArrayRef bases, at::Tensor region, int6
 // its writer, which cannot start before this rank has finished launch k (it needs this rank's flags
 // of launch k + 1); data[k & 1] likewise. Every wait is bounded: a timed-out slice rejects the step
 // on this rank (no parameter of the slice changes), sets ctl[2] (the host raises at the epoch end).
+// The slices of the timed-out launch that did not time out have updated already (undoing them would
+// need a grid-wide barrier in every launch); from the next launch on, the sticky ctl[2] rejects the
+// step on every rank (see ``sticky``), so the ranks stop at the same state until the job stops.
 template <int W>
 __global__ __launch_bounds__(256) void adam_peer_kernel(PeerArgs A, float* __restrict__ p, float* __restrict__ m,
                                                         float* __restrict__ v, const float* __restrict__ lr_p,
@@ -253,7 +256,12 @@ __global__ __launch_bounds__(256) void adam_peer_kernel(PeerArgs A, float* __res
   const int timeout = __hip_atomic_load(ext + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nonfin = __hip_atomic_load(ext + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float g0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int bad = (timeout != 0 || nonfin != 0 || !isfinite(g0)) ? 1 : 0;
+  // ctl[2] is sticky (only the host clears it): after a peer spin timeout in an earlier launch this
+  // rank rejects, and through its flag bit makes EVERY rank reject, every later step, so no rank
+  // trains on while another holds the partial update of the timed-out launch (the host raises on
+  // every rank at the epoch end; the job resumes from its last checkpoint)
+  const int sticky = __hip_atomic_load(A.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int bad = (timeout != 0 || nonfin != 0 || sticky != 0 || !isfinite(g0)) ? 1 : 0;
   const long n4 = A.n / 4;
   const long i = (long)b * 256 + tid;
   // ---- 1. publish

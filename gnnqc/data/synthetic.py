@@ -63,11 +63,54 @@ def _rain_field(n_sensors, n_time, mx, my, rng, rain_fraction=0.06, minutes_per_
     return rate
 
 
-def _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp):
-    """Anomaly events of flagged link ``s`` added to its TL rows, with the experts' flags."""
+def _rainlike_attenuation(rng, T, kcoef1, kcoef2, length):
+    """(t0, prof1, prof2): the attenuation a rain cell passing over ONE link would cause (a cell drawn
+    like :func:`_rain_field`'s - duration, peak, small-scale variability - with its track through the
+    link, seen by no other link), through the same power law and wet-antenna term as real rain."""
+    dur = int(rng.uniform(30, 300))
+    t0 = int(rng.integers(0, max(1, T - dur)))
+    speed = rng.uniform(15, 60) / 60.0
+    radius = rng.uniform(3, 14)
+    miss = rng.uniform(0, 0.7) * radius                 # closest approach of the track to the link
+    peak = rng.gamma(2.0, 8.0)
+    tt = np.arange(dur)
+    along = speed * (tt - dur * rng.uniform(0.3, 0.7))
+    env = _smooth_bump(dur, 1.0, rng)
+    env = env * np.clip(1 + 0.3 * np.convolve(rng.standard_normal(dur), np.ones(9) / 9, "same"), 0.2, 2)
+    rate = peak * env * np.exp(-(along ** 2 + miss ** 2) / (2 * radius ** 2))
+    wet = 1.2 * (1 - np.exp(-rate / 1.5))
+    return t0, kcoef1 * rate ** 1.05 * length + wet, kcoef2 * rate ** 1.05 * length + wet
+
+
+def _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp,
+                          rainlike_frac=0.0, link=None):
+    """Anomaly events of flagged link ``s`` added to its TL rows, with the experts' flags.
+
+    ``rainlike_frac`` > 0: that fraction of the events is rain-shaped (:func:`_rainlike_attenuation`,
+    flagged as ``Dew``: a wet antenna without rain). On the link's own series such an event is drawn
+    from the same distribution as real rain attenuation; only the neighbours tell them apart (real
+    rain cells are seen by every link they pass). ``link`` = (kcoef1, kcoef2,
+    length) of link ``s``."""
     n_events = rng.poisson(anomaly_rate * days * 1.6)
+    base_p = np.array([0.3, 0.25, 0.3, 0.15])
     for _ in range(n_events):
-        kind = rng.choice(4, p=[0.3, 0.25, 0.3, 0.15])
+        if rainlike_frac > 0:
+            kind = rng.choice(5, p=list(base_p * (1.0 - rainlike_frac)) + [rainlike_frac])
+        else:
+            kind = rng.choice(4, p=base_p)
+        if kind == 4:    # rain-like: a wet-antenna event with rain's rise and decay
+            t0, p1, p2 = _rainlike_attenuation(rng, T, *link)
+            dur = len(p1)
+            tl1[s, t0:t0 + dur] += p1
+            tl2[s, t0:t0 + dur] += p2
+            on = np.nonzero(p1 > 0.1 * max(float(p1.max()), 1e-6))[0]
+            a0, a1 = t0 + int(on[0]), t0 + int(on[-1]) + 1
+            for e in range(n_exp):
+                if rng.random() < 0.92:
+                    j0 = int(np.clip(a0 + rng.integers(-6, 7), 0, T - 1))
+                    j1 = int(np.clip(a1 + rng.integers(-6, 7), j0 + 1, T))
+                    flags[flag_names[1]][e, s, j0:j1] = True
+            continue
         if kind == 0:    # jump: level shift for a while
             dur = int(rng.uniform(20, 240))
             t0 = int(rng.integers(0, T - dur))
@@ -105,12 +148,16 @@ def _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_
 def make_cml_raw(n_sensors: int = 23, n_flagged: int = 1, n_minutes: int = 40320,
                  start: str = "2019-07-02T00:00", seed: int = 0, center=(51.5, 7.45),
                  extent_km: float = 12.0, anomaly_rate: float = 1.0, rain_fraction: float = 0.06,
-                 gap_rate: float = 2e-4, difficulty: float = 1.0) -> SensorData:
+                 gap_rate: float = 2e-4, difficulty: float = 1.0, rainlike_frac: float = 0.0) -> SensorData:
     """CML raw dataset (schema of ``cml_raw_example.nc``).
 
     ``anomaly_rate`` scales the number of anomaly events per flagged link
     (1.0 ~ 10-15% anomalous minutes); ``difficulty`` scales how rain-like the
     anomalies look (amplitudes/shape overlap with rain attenuation).
+    ``rainlike_frac``: fraction of the anomaly events that are rain-shaped wet-antenna events seen by
+    the flagged link only (:func:`_rainlike_attenuation`): on the link's own series they cannot be
+    told from rain, so only the neighbourhood separates them (0 = none; the RNG stream is then the
+    one of earlier versions).
     """
     rng = np.random.default_rng(seed)
     S, T = n_sensors, n_minutes
@@ -156,7 +203,8 @@ def make_cml_raw(n_sensors: int = 23, n_flagged: int = 1, n_minutes: int = 40320
     flags = {k: np.zeros((n_exp, S, T), dtype=bool) for k in flag_names}
     days = T / 1440.0
     for s in np.nonzero(flagged)[0]:
-        _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp)
+        _inject_cml_anomalies(rng, tl1, tl2, flags, flag_names, s, T, days, anomaly_rate, difficulty, n_exp,
+                              rainlike_frac, (float(kcoef1[s, 0]), float(kcoef2[s, 0]), float(length[s])))
     # --- quantisation, gaps, out-of-range spikes
     tl1 = np.round(tl1 * 10) / 10
     tl2 = np.round(tl2 * 10) / 10

@@ -78,6 +78,12 @@ class PeerAllReduce:
         ctl = self.region[2 * self.cap + 8 * 16: 2 * self.cap + 8 * 16 + 16].view(torch.int32)
         return bool(ctl[2].item())
 
+    def inject_timeout(self):
+        """Fault injection (tests): mark this rank's region as if a peer spin had timed out. The fused
+        update (``adam_peer``) then rejects every later step on every rank, and the epoch end raises."""
+        ctl = self.region[2 * self.cap + 8 * 16: 2 * self.cap + 8 * 16 + 16].view(torch.int32)
+        ctl[2].fill_(1)
+
     @torch.no_grad()
     def verify(self, trials: int = 3) -> bool:
         """Compare with the process group's all-reduce on rank-dependent data (every rank takes
@@ -222,27 +228,30 @@ def check_fused_adam(pa: "PeerAllReduce", numel: int, device, beta1: float = 0.9
         for k in ("p", "m", "v"):
             ok &= bool(torch.allclose(a[k], b[k], rtol=1e-6, atol=0.0))
         ok &= float(a["step"].item()) == float(b["step"].item()) == float(trials)
-        if ok and peer_mode() == "auto":
-            g = torch.zeros(numel, device=dev)
-
-            def timed(fn, bb):
-                for _ in range(3):
-                    fn(bb, g)
-                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                      for _ in range(n_time)]
-                for e0, e1 in ev:
-                    e0.record()
-                    fn(bb, g)
-                    e1.record()
-                torch.cuda.synchronize(dev)
-                return 1e3 * sum(e0.elapsed_time(e1) for e0, e1 in ev) / n_time
-            sep_us, fused_us = timed(sep, b), timed(fused, a)
-            t = torch.tensor([sep_us, fused_us], device=dev if D.backend() == "nccl" else "cpu", dtype=torch.float64)
-            D.all_reduce_(t, op=torch.distributed.ReduceOp.MAX, force=True)
-            sep_us, fused_us = float(t[0].item()), float(t[1].item())
+    # agree on the verdict BEFORE the timing block: ``ok`` is rank-local (timeouts, the g == 0 check,
+    # allclose), and the timing block issues peer launches and a collective, so every rank must take
+    # the same branch or the collective sequences mismatch
     flag = torch.tensor([0.0 if ok else 1.0], device=dev if D.backend() == "nccl" else "cpu")
     D.all_reduce_(flag, force=True)
     verified = float(flag.item()) == 0.0
+    if verified and peer_mode() == "auto":
+        g = torch.zeros(numel, device=dev)
+
+        def timed(fn, bb):
+            for _ in range(3):
+                fn(bb, g)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(n_time)]
+            for e0, e1 in ev:
+                e0.record()
+                fn(bb, g)
+                e1.record()
+            torch.cuda.synchronize(dev)
+            return 1e3 * sum(e0.elapsed_time(e1) for e0, e1 in ev) / n_time
+        sep_us, fused_us = timed(sep, b), timed(fused, a)
+        t = torch.tensor([sep_us, fused_us], device=dev if D.backend() == "nccl" else "cpu", dtype=torch.float64)
+        D.all_reduce_(t, op=torch.distributed.ReduceOp.MAX, force=True)
+        sep_us, fused_us = float(t[0].item()), float(t[1].item())
     use = verified and (fused_us is None or fused_us < sep_us)
     LAST_SELECTION.update(fused_adam_verified=verified, fused_adam_us=fused_us, separate_adam_us=sep_us,
                           fused_adam_selected=use)

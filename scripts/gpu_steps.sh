@@ -39,23 +39,34 @@ for step in "$@"; do
         bench)  run bench 300 $PY bench.py --steps 50 --warmup 10 ;;
         bench1) run bench1 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 ;;
         soil)   run soil 300 $PY bench.py --ds soilnet --steps 20 --warmup 5 --no-knn-line ;;
+        cnn)    run cnn 300 $PY bench.py --time-layer cnn --steps 40 --warmup 5 ;;
+        stats_cnn) prof stats_cnn 400 --kernel-trace --stats -d "$OUT/prof_stats_cnn" -o run --output-format csv -- \
+                    $PY "$ROOT/bench.py" --time-layer cnn --steps 40 --warmup 5 ;;
+        pmc_cnn) prof pmc_cnn 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_cnn" -o run --output-format csv -- \
+                    $PY "$ROOT/bench.py" --time-layer cnn --steps 16 --warmup 2 ;;
+        pmc_cnn_mem) prof pmc_cnn_mem 120 --kernel-trace --pmc FETCH_SIZE -d "$OUT/prof_pmc_cnn_mem" -o run \
+                    --output-format csv -- $PY "$ROOT/bench.py" --time-layer cnn --steps 16 --warmup 2 ;;
+        pmc_cnn_wr) prof pmc_cnn_wr 120 --kernel-trace --pmc WRITE_SIZE -d "$OUT/prof_pmc_cnn_wr" -o run \
+                    --output-format csv -- $PY "$ROOT/bench.py" --time-layer cnn --steps 16 --warmup 2 ;;
+        cvcml)  run cvcml 400 $PY bench.py --steps 8 --warmup 2 --no-knn-line --no-ig-line --no-soil-line ${CV_ARGS:-} ;;
+        cvsoil) run cvsoil 600 $PY bench.py --steps 8 --warmup 2 --no-knn-line --no-ig-line ${CV_ARGS:-} ;;
         ig)     run ig 300 $PY scripts/bench_ig.py ;;
         ar)     run ar 300 $PY scripts/ar_us.py ;;
         phase)  GNNQC_HIP_LIB=gnnqc/_lib/variants/prof.so run phase 300 $PY scripts/chain_phase_prof.py ;;
         stats)  prof stats 400 --kernel-trace --stats -d "$OUT/prof_stats" -o run --output-format csv -- \
-                    $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line --no-cv-line ;;
+                    $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line --no-cv-line --no-soil-line ;;
         stats_ng) prof stats_ng 400 --kernel-trace --stats -d "$OUT/prof_stats_ng" -o run --output-format csv -- \
-                    $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line --no-cv-line --no-graph ;;
+                    $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line --no-cv-line --no-soil-line --no-graph ;;
         stats_ig) prof stats_ig 400 --kernel-trace --stats -d "$OUT/prof_stats_ig" -o run --output-format csv -- \
                     $PY "$ROOT/scripts/bench_ig.py" ;;
         stats_soil) prof stats_soil 400 --kernel-trace --stats -d "$OUT/prof_stats_soil" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --ds soilnet --steps 20 --warmup 3 --no-graph ;;
         pmc_cml) prof pmc_cml 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_cml" -o run --output-format csv -- \
-                    $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line --no-cv-line --no-ig-line ;;
+                    $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line --no-cv-line --no-ig-line --no-soil-line ;;
         pmc_cml_mem) prof pmc_cml_mem 120 --kernel-trace --pmc FETCH_SIZE -d "$OUT/prof_pmc_cml_mem" -o run \
-                    --output-format csv -- $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line --no-cv-line --no-ig-line ;;
+                    --output-format csv -- $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line --no-cv-line --no-ig-line --no-soil-line ;;
         pmc_cml_wr) prof pmc_cml_wr 120 --kernel-trace --pmc WRITE_SIZE -d "$OUT/prof_pmc_cml_wr" -o run \
-                    --output-format csv -- $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line --no-cv-line --no-ig-line ;;
+                    --output-format csv -- $PY "$ROOT/bench.py" --steps 16 --warmup 2 --no-knn-line --no-cv-line --no-ig-line --no-soil-line ;;
         pmc_soil) prof pmc_soil 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_soil" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --ds soilnet --steps 6 --warmup 2 --no-graph ;;
         pmc_soil_mem) prof pmc_soil_mem 120 --kernel-trace --pmc FETCH_SIZE -d "$OUT/prof_pmc_soil_mem" -o run \

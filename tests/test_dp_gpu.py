@@ -46,11 +46,28 @@ loader = DeviceLoader(st, list(range(min(st.n_windows, 32 * nb * world))), 32, s
                       world_size=world, drop_last=True)
 logs = t.train_epoch(loader, 0)
 torch.cuda.synchronize()
+inj = os.environ.get("INJECT_PEER_TIMEOUT_RANK")
+extra = {}
+if inj is not None:          # fault injection: a peer spin timeout recorded on one rank
+    p_before = opt.flat_p.double().sum().item()
+    if rank == int(inj):
+        t.peer.inject_timeout()
+    torch.cuda.synchronize()
+    try:
+        t.train_epoch(loader, 1)
+        extra["raised"] = False
+    except RuntimeError as e:
+        extra["raised"] = "spin timeout" in str(e)
+    torch.cuda.synchronize()
+    extra.update(p_before=p_before, p_after=opt.flat_p.double().sum().item(),
+                 rejected=int(opt.guard_state[3].item()) if getattr(opt, "guard_state", None) is not None else -1)
 bufs = torch.cat([b.reshape(-1).double() for b in m.buffers() if b.is_floating_point()])
 out = {"sum": float(x[0]), "p": opt.flat_p.double().sum().item(), "p2": (opt.flat_p.double() ** 2).sum().item(),
        "b": bufs.sum().item(), "steps": t.global_step, "loss": logs["loss"], "skipped": logs["skipped_steps"],
        "dp_graph": bool(t.dp_graph), "multi": bool(t.multi_graph is not None), "ar_us": t.measure_allreduce(),
-       "peer": t.peer is not None, "fused": bool(t.peer_fused())}
+       "peer": t.peer is not None, "fused": bool(t.peer_fused()),
+       "ps2": torch.nn.functional.pad(opt.flat_p.double(), (0, (-opt.flat_p.numel()) % 1024)).view(-1, 1024)
+              .pow(2).sum(1).tolist(), **extra}
 with open(os.path.join(os.environ["OUT"], f"r{rank}.json"), "w") as f:
     json.dump(out, f)
 torch.distributed.destroy_process_group()
@@ -130,10 +147,15 @@ def test_peer_fused_adam_matches_separate_kernels_two_ranks(tmp_path):
     assert a["steps"] == c["steps"] == 16 and a["skipped"] == c["skipped"] == 0
     for k in ("p", "p2", "loss"):
         # ranks of one run agree bitwise; the two runs differ only by the float-atomic order of the
-        # GCN backward (a separate process each), which 16 Adam steps amplify to ~2e-6 of the norm
-        # (measured); a wrong or missing slice update is orders of magnitude larger
+        # GCN backward (a separate process each; deterministic mode has no flag-driven update to
+        # fuse), which 16 Adam steps amplify to ~2e-6 of the norm (measured)
         assert a[k] == b[k] and c[k] == d[k], (k, a[k], b[k], c[k], d[k])
         assert abs(a[k] - c[k]) <= 1e-4 * abs(c[k]) + 1e-9, (k, a[k], c[k])
+    # per 1024-float slice (one adam_peer workgroup each): sum of squares of the parameters. A slice
+    # whose update was skipped or stale moves its sum by ~2 dp / p (percents after 16 steps), far
+    # outside the atomic-order noise
+    for i, (u, v) in enumerate(zip(a["ps2"], c["ps2"])):
+        assert abs(u - v) <= 1e-4 * abs(v) + 1e-9, (i, u, v)
 
 
 def test_peer_auto_mode_selects_and_trains(tmp_path):
@@ -152,3 +174,13 @@ def test_peer_allreduce_matches_rccl_single_rank(tmp_path):
     assert a["peer"] and not b["peer"] and a["dp_graph"] and a["multi"] and a["fused"]
     for k in ("p", "p2", "loss"):
         assert abs(a[k] - b[k]) <= 1e-4 * abs(b[k]) + 1e-6, (k, a[k], b[k])
+
+
+def test_peer_fused_timeout_rejects_every_later_step_on_every_rank(tmp_path):
+    """adam_peer fault handling: after a peer spin timeout recorded on ONE rank (injected), every
+    later step is rejected on EVERY rank (the timed-out rank's flag bit carries the rejection), so
+    the ranks' parameters stay identical and unchanged, and the epoch end raises on every rank."""
+    a, b = _run(tmp_path, 2, "gloo", NB="16", GNNQC_PEER_ALLREDUCE="1", INJECT_PEER_TIMEOUT_RANK="1")
+    assert a["fused"] and b["fused"]
+    assert a["raised"] and b["raised"], "the epoch end must raise on every rank"
+    assert a["p_after"] == b["p_after"] == a["p_before"] == b["p_before"], (a, b)

@@ -104,6 +104,43 @@ def test_fused_front_end_gradients_match_generic(cuda_device, cml_windows, monke
         torch.testing.assert_close(a, r, atol=1e-4 * (r.abs().max().item() + 1e-3), rtol=1e-4, msg=n)
 
 
+def test_two_forwards_before_backward_coef_side_job(cuda_device, cml_windows, monkeypatch):
+    """Gradient accumulation over micro-batches: two store-fused forwards, then the backward of
+    both. In the coefficient side mode the first forward's coefficient job is still pending when the
+    second forward installs its own (no chain forward in between took it); it must be flushed, not
+    dropped (dropped, the first backward would read an unwritten coefficient tensor). Parameter
+    gradients equal the recomputing backward (GNNQC_GCN_COEF=0)."""
+    from gnnqc.ops.gcn import gcn_pool_from_store
+    from gnnqc.ops.lstm import direct_grad_accumulation
+    _, st, model = _setup(cuda_device, cml_windows)
+    g = model.gcn_layer
+    params = [g.kernel, g.bias, g.bn_gamma, g.bn_beta, g.prelu_alpha]
+    ids = [_ids(st, 128, cuda_device, pad=3), _ids(st, 128, cuda_device)[32:].contiguous()]
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    dhs = None
+    out = {}
+    rm0, rv0 = g.bn_moving_mean.clone(), g.bn_moving_variance.clone()
+    for coef in ("0", "1"):
+        monkeypatch.setenv("GNNQC_GCN_COEF", coef)
+        with torch.no_grad():
+            g.bn_moving_mean.copy_(rm0)
+            g.bn_moving_variance.copy_(rv0)
+        for p in params:
+            p.grad = torch.zeros_like(p)
+        with direct_grad_accumulation(True):
+            hs = [gcn_pool_from_store(st, i, g, True, "mean")[0] for i in ids]
+            if dhs is None:
+                dhs = [torch.randn(h.shape, generator=gen).to(cuda_device) for h in hs]
+                dhs[0][:, 128:] = 0
+                dhs[1][:, 96:] = 0
+            for h, dh in zip(hs, dhs):
+                h.backward(dh)
+        torch.cuda.synchronize()
+        out[coef] = [p.grad.clone() for p in params]
+    for n, a, r in zip(["W", "b", "gamma", "beta", "alpha"], out["1"], out["0"]):
+        torch.testing.assert_close(a, r, atol=1e-4 * (r.abs().max().item() + 1e-3), rtol=1e-4, msg=n)
+
+
 def test_training_step_store_path_matches_gather_path(cuda_device, cml_windows, monkeypatch):
     """Two full training steps (forward, backward, guarded Adam) through the Trainer with the
     store-fused front end and with the generic gather path: same loss and parameters."""

@@ -704,6 +704,40 @@ def test_chain_forward_matches_per_layer(cuda_device, monkeypatch, M, bwd):
         assert (a - b_).norm().item() <= 5e-3 * (b_.norm().item() + 1e-6)
 
 
+@pytest.mark.parametrize("P", [1, 2])
+def test_chain_odd_pool_size_matches_per_layer(cuda_device, monkeypatch, P):
+    """A chain that ends in MaxPooling1D(P != 3) (``_chain_plan`` accepts 1..255): forward and
+    chain backward == the per-layer kernels. P = 1 guards the un-pooling stage's multiply-high
+    division (its magic 2^32 wraps to 0, which once sent every dh to source step 0)."""
+    from gnnqc.models.timelayer import TimeLayer
+    from gnnqc.utils.native import hip_ops
+    torch.manual_seed(0)
+    tl = TimeLayer(18, 16, 2, "lstm", pool_size=P).to(cuda_device)
+    x = torch.randn(64, 181, 18, device=cuda_device)
+    monkeypatch.setenv("GNNQC_NO_PAIR", "1")
+    monkeypatch.setenv("GNNQC_CHAIN_BWD", "1")
+    h = torch.zeros(181, 64, 20, device=cuda_device)
+    plan = tl._chain_plan(tl._sequence(), h)
+    assert plan is not None and plan[1] == [0, P], plan
+
+    def run(chain):
+        monkeypatch.setenv("GNNQC_CHAIN", "1" if chain else "0")
+        xi = x.clone().requires_grad_(True)
+        for p in tl.parameters():
+            p.grad = None
+        out = tl(xi)
+        out.pow(2).sum().backward()
+        return out.detach(), [xi.grad.clone()] + [p.grad.clone() for p in tl.parameters()]
+
+    o0, g0 = run(False)
+    o1, g1 = run(True)
+    torch.cuda.synchronize()
+    assert int(hip_ops().lstm_chain_status(x).cpu()[2]) == 0, "a consumer spin timed out"
+    torch.testing.assert_close(o1, o0, atol=1e-5, rtol=1e-5)
+    for a, b_ in zip(g1, g0):
+        assert (a - b_).norm().item() <= 5e-3 * (b_.norm().item() + 1e-6)
+
+
 def _soil_small_windows():
     from gnnqc import config as C
     from gnnqc.data.preprocessing import create_windows_dataset
