@@ -237,8 +237,11 @@ def measure_cv(args, dev, world, D, ds: str = "cml"):
            "data": desc, "folds": folds, "epochs": int(mc.epochs), "dtype": args.dtype,
            "fold_per_rank": world > 1}
     for name, baseline in (("gcn", False), ("baseline", True)):
+        def progress(r, name=name):       # (stderr: stdout carries the one JSON line)
+            print("bench.py: cv %s %s fold %d auc %.4f (%.1f s)" % (ds, name, r["fold"], r["auc"], r["seconds"]),
+                  file=sys.stderr, flush=True)
         s = run_cv(pc, mc, ws, folds=folds, baseline=baseline, store=store, seed=0, verbose=0,
-                   fold_per_rank=world > 1)
+                   fold_per_rank=world > 1, progress=progress)
         out[f"{name}_mean_auc"] = round(s["mean_auc"], 5)
         out[f"{name}_std"] = round(s["std_auc"], 5)
         out[f"{name}_fold_auc"] = [round(r["auc"], 5) for r in s["per_fold"]]
@@ -384,9 +387,9 @@ def main(argv=None):
     ap.add_argument("--cv-sensors", type=int, default=None, help="CML CV data: links (default 23)")
     ap.add_argument("--cv-days", type=float, default=None, help="CML CV data: days (default 28)")
     ap.add_argument("--cv-flagged", type=int, default=None, help="CML CV data: flagged links (default 4)")
-    ap.add_argument("--cv-rainlike", type=float, default=0.5,
+    ap.add_argument("--cv-rainlike", type=float, default=0.85,
                     help="CML CV data: fraction of the anomaly events that are rain-shaped (flagged link only)")
-    ap.add_argument("--cv-rain-fraction", type=float, default=0.12, help="CML CV data: rain_fraction")
+    ap.add_argument("--cv-rain-fraction", type=float, default=0.15, help="CML CV data: rain_fraction")
     ap.add_argument("--no-soil-line", dest="soil_line", action="store_false",
                     help="skip the SoilNet sub-record of the CML line (training throughput B=32 T=337 and its 5-fold "
                          "CV, reported as 'soilnet')")

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import json
 import time
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 import torch
@@ -29,9 +29,11 @@ from .fit import train_model
 def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, baseline: bool = False,
            device="cpu", seed: int = 0, store: Optional[DeviceStore] = None, gap_days: Optional[int] = None,
            verbose: int = 1, log_path: Optional[str] = None, max_folds: Optional[int] = None,
-           fold_ids: Optional[List[int]] = None, fold_per_rank: bool = False) -> Dict:
+           fold_ids: Optional[List[int]] = None, fold_per_rank: bool = False,
+           progress: Optional[Callable[[Dict], None]] = None) -> Dict:
     """``fold_ids`` runs only those folds (e.g. to spread a CV over several jobs; merge
-    the per-fold JSONL lines with :func:`summarize_folds`).
+    the per-fold JSONL lines with :func:`summarize_folds`). ``progress`` is called with each
+    finished fold's result on the rank that ran it (e.g. a progress line on stderr).
 
     ``fold_per_rank`` (one process per GPU): instead of data-parallel training of every fold,
     rank r trains folds r, r + world, ... on its own GPU with no collective in its steps (the
@@ -52,7 +54,7 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
         mine = todo[D.global_rank()::D.global_world_size()]
         with D.local():
             part = run_cv(pc, mc, windows, k, baseline, device, seed, store, gap_days, verbose, None, None,
-                          mine if mine else [], False)["per_fold"] if mine else []
+                          mine if mine else [], False, progress)["per_fold"] if mine else []
         merged = sorted((r for chunk in D.all_gather_object(part) for r in chunk), key=lambda r: r["fold"])
         if log_path and D.is_main():
             with open(log_path, "a") as f:
@@ -73,15 +75,21 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
                                   store=store, verbose=max(0, verbose - 1))
         r = flatten_predictions(predict(model, store, test_loader, baseline))
         y, p = r["y"] > 0.5, r["p"]
-        auc = M.roc_auc_score(y, p)
-        thr = M.select_threshold(p, y, verbose=False)
-        yp = p > thr
-        res = {"fold": fold, "auc": auc, "mcc": M.matthews_corrcoef(y, yp), "precision": M.precision_score(y, yp),
-               "recall": M.recall_score(y, yp), "accuracy": M.accuracy_score(y, yp), "threshold": thr,
+        if y.size:
+            auc = M.roc_auc_score(y, p)
+            thr = M.select_threshold(p, y, verbose=False)
+            yp = p > thr
+            scores = {"auc": auc, "mcc": M.matthews_corrcoef(y, yp), "precision": M.precision_score(y, yp),
+                      "recall": M.recall_score(y, yp), "accuracy": M.accuracy_score(y, yp), "threshold": thr}
+        else:       # no labelled window in the held-out fold (tiny data): no score, the mean skips it
+            scores = {k2: float("nan") for k2 in ("auc", "mcc", "precision", "recall", "accuracy", "threshold")}
+        res = {"fold": fold, **scores,
                "n_train": int(len(tr)), "n_test": int(len(te)), "test_pos_rate": float(y.mean()) if y.size else 0.0,
                "final_train_loss": float(hist.history["loss"][-1]), "seconds": time.time() - t0,
                "loss_curve": [round(float(v), 5) for v in hist.history["loss"]]}
         results.append(res)
+        if progress is not None:
+            progress(res)
         if verbose and D.is_main():
             print(json.dumps({k2: (round(v, 4) if isinstance(v, float) else v) for k2, v in res.items()
                               if k2 != "loss_curve"}), flush=True)
@@ -94,11 +102,14 @@ def run_cv(preproc_config, model_config, windows, folds: Optional[int] = None, b
 def summarize_folds(results: List[Dict], model: str, ds_type: str, folds: int) -> Dict:
     """Headline summary (mean / std ROC-AUC, mean MCC) of per-fold result dicts."""
     aucs = np.array([r["auc"] for r in results], dtype=np.float64)
+    aucs = aucs[np.isfinite(aucs)]                 # (a fold without labelled windows has no score)
+    mccs = np.array([r["mcc"] for r in results], dtype=np.float64)
+    mccs = mccs[np.isfinite(mccs)]
     return {
         "model": model, "ds_type": ds_type, "folds": folds, "folds_run": sorted(int(r["fold"]) for r in results),
-        "mean_auc": float(np.nanmean(aucs)) if aucs.size else float("nan"),
-        "std_auc": float(np.nanstd(aucs)) if aucs.size else float("nan"),
-        "mean_mcc": float(np.mean([r["mcc"] for r in results])) if results else float("nan"),
+        "mean_auc": float(aucs.mean()) if aucs.size else float("nan"),
+        "std_auc": float(aucs.std()) if aucs.size else float("nan"),
+        "mean_mcc": float(mccs.mean()) if mccs.size else float("nan"),
         "per_fold": results,
     }
 

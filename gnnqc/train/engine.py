@@ -581,6 +581,10 @@ def predict(model, store, loader, baseline: bool = False, gather_all: bool = Tru
     if store.device.type == "cuda":
         from ..ops.lstm import check_chain
         check_chain(store.device)
+    if not ps:                          # no batch on this rank (e.g. a tiny held-out fold)
+        N = () if store.per_sensor else (store.n_nodes,)
+        ps = ys = ms = [torch.zeros((0, *N), device=store.device)]
+        ws = [torch.zeros(0, dtype=torch.long, device=store.device)]
     p = torch.cat(ps)
     y = torch.cat(ys)
     m = torch.cat(ms)

@@ -37,7 +37,7 @@ for step in "$@"; do
         tests)  run tests 600 $PY -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         smoke)  run smoke 300 $PY -c "import __graft_entry__ as g; g.smoke()" ;;
         bench)  run bench 300 $PY bench.py --steps 50 --warmup 10 ;;
-        bench1) run bench1 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 ;;
+        bench1) run bench1 600 $PY bench.py --gpus 1 --steps 20 --warmup 5 ;;
         soil)   run soil 300 $PY bench.py --ds soilnet --steps 20 --warmup 5 --no-knn-line ;;
         cnn)    run cnn 300 $PY bench.py --time-layer cnn --steps 40 --warmup 5 ;;
         stats_cnn) prof stats_cnn 400 --kernel-trace --stats -d "$OUT/prof_stats_cnn" -o run --output-format csv -- \

@@ -153,7 +153,7 @@ def _gcn_worker(rank, world, port, out_dir, ids, n_epoch_batches, ds="cml"):
     D.destroy()
 
 
-@pytest.mark.parametrize("world,ds", [(2, "cml"), (4, "cml"), (2, "soilnet")])
+@pytest.mark.parametrize("world,ds", [(2, "cml"), (4, "cml"), (2, "soilnet"), (4, "soilnet")])
 def test_gcn_dp_gradients_and_bn_statistics(tmp_path, world, ds):
     """GCNClassifier under data parallelism (gloo, the RCCL path by construction): the all-reduced
     gradient equals the mean of single-process per-shard gradients (BatchNorm batch statistics are
