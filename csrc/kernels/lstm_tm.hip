@@ -58,7 +58,11 @@ struct TmOcc {
   static constexpr int W = (NT >= 1024 && KX == 1) ? 8 : 1;
 };
 
-template <int H, bool TRAIN, int KX, int GR, int D>
+// SG = false (train mode, recompute-gates backward, lstm_tm_bwd_body RG): only c is saved; the
+// backward recomputes the gates from x_t and h_{t-1} (same bf16 operands, same MFMA order: bitwise the
+// forward's pre-activations), which halves the forward's state stream (h + c + packed gates = 16 B per
+// cell-step -> 8 B) and drops the backward's 8-byte gate read
+template <int H, bool TRAIN, int KX, int GR, int D, bool SG = true>
 __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_tm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hout, __bf16* __restrict__ gbuf,
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
         hf[p][col][u] = hv;
         if constexpr (TRAIN) {                       // steps past T-1 write the scratch row T
           const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
-          *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
+          if constexpr (SG) *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
           cbuf[o] = c[cc];
         }
       }
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
 // recurrence of T + 1 steps instead of two of T. Outputs and saved state are exactly those
 // of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
 // (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
-template <int H, bool TRAIN, int KX, int GR, int D>
+template <int H, bool TRAIN, int KX, int GR, int D, bool SG = true>
 __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
         hf[L][p][col][unit] = hv;
         if constexpr (TRAIN) {                       // invalid steps write the scratch row T
           const size_t o = (((size_t)(tc >= 0 ? min(tc, T) : T) * ntiles + tile) * NW + w) * 64 + lane;
-          *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
+          if constexpr (SG) *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
           cbuf[o] = c;
         }
       }
@@ -375,15 +379,24 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 // read while the faster waves already write the next one. The partial tiles stay in VGPRs for all T steps and leave once per workgroup as one
 // split record of the weight-gradient pass's layout (lstm_grads_body.h: [tile][cb][DT + HT][4]
 // [64][4]), summed over the tiles by the same fixed-order reduction. dz itself never reaches HBM.
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false>
+// RG (recompute gates): the forward saved no gates (lstm_tm_fwd SG = false). Each step's i, f, g, o
+// are recomputed here from x_t and h_{t-1} - the forward's own bf16 operands, fragments, bias and MFMA
+// order, so the pre-activations are bitwise the forward's - one step ahead, in the MFMA phase of the
+// step before (off the serial chain: they depend on saved data only). x_t / h_{t-1} come through the
+// same register rings as the WG streams and are staged row-major ([sequence][channel], the forward's B
+// operand layout) into a double buffer.
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false, bool RG = false>
 __device__ __forceinline__ void lstm_tm_bwd_body(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw, int tile, int ntiles, const float* __restrict__ xw = nullptr,
-    const float* __restrict__ hw = nullptr, float* __restrict__ wsr = nullptr) {
+    const float* __restrict__ hw = nullptr, float* __restrict__ wsr = nullptr,
+    const float* __restrict__ bias = nullptr) {
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
   static_assert(!WG || (CPL == 1 && NT == 16 * H && G4 == 16 * NW && GR == 4), "fused weight gradients: H <= 64");
+  static_assert(!RG || (CPL == 1 && NT == 16 * H && GR == 4), "recomputed gates: H <= 64, 16-byte x granules");
+  constexpr bool XS = WG || RG;                   // x_t / h_{t-1} streams
   constexpr int NXB = KX * 2;                     // din blocks of dx^T (16 rows each)
   constexpr int TX = (NXB + NW - 1) / NW;         // dx tiles per wave
   static_assert(16 * G4 / 4 == NT, "one dz float4 granule per thread");
@@ -469,7 +482,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   }
 
   // ---- streams. internal state (per lane, ring over reverse steps): gates, c_t
-  uint2 rg[CPL][D];                               // packed bf16 gates
+  uint2 rg[CPL][RG ? 1 : D];                      // packed bf16 gates (not saved under RG)
   float rc[CPL][D];
   auto idx = [&](int tt, int cc) { return ((((size_t)tt * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane; };
 #define GQ_TMB_LOAD_STATE(J, SS)                                                    \
@@ -477,7 +490,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
     const int tt_ = max(T - 1 - (SS), 0);                                           \
     _Pragma("unroll") for (int cc = 0; cc < CPL; ++cc) {                            \
       const size_t o_ = idx(tt_, cc);                                               \
-      rg[cc][J] = *reinterpret_cast<const uint2*>(gbuf + o_ * 4);                   \
+      if constexpr (!RG) rg[cc][J] = *reinterpret_cast<const uint2*>(gbuf + o_ * 4); \
       rc[cc][J] = cbuf[o_];                                                         \
     }                                                                               \
   }
@@ -501,21 +514,81 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   float* sbase = dx + (size_t)row0 * Din + gx;
   // WG streams: XG consecutive floats of the [16][Din] x_t tile (threads past the tile repeat it)
   // and element tid of the [16][H] h_{t-1} tile, in rings over reverse steps like the saved state
-  constexpr int XG = WG ? (16 * 32 * KX / NT > 1 ? 16 * 32 * KX / NT : 1) : 1;
+  constexpr int XG = XS ? (16 * 32 * KX / NT > 1 ? 16 * 32 * KX / NT : 1) : 1;
   static_assert(XG <= 4, "x stream granule");
-  Granule<XG> wx[WG ? D : 1];
-  float wh[WG ? D : 1];
+  Granule<XG> wx[XS ? D : 1];
+  float wh[XS ? D : 1];
   const int wxe = (tid * XG) % (16 * Din);
   const int wx_seq = wxe / Din, wx_k = wxe % Din;
   const float* wxb = xw + (size_t)row0 * Din + wxe;
   const float* whb = hw + (size_t)row0 * H + tid;
   const size_t whstep = (size_t)Mp * H;
 #define GQ_TMB_LOAD_W(J, SS)                                                        \
-  if constexpr (WG && !(TMW_SKIP & 2)) {                                                               \
+  if constexpr (XS && !(TMW_SKIP & 2)) {                                                               \
     const int tt_ = max(T - 1 - (SS), 0);                                           \
     wx[J].load(wxb + (size_t)tt_ * xstep);                                          \
     wh[J] = whb[(size_t)max(tt_ - 1, 0) * whstep];                                  \
   }
+
+  // RG: the forward's A fragments (rows permuted: tile row `col` = gate (col & 3) of unit 4 w + (col >> 2)),
+  // bias, and the row-major bf16 x_t / h_{t-1} double buffers
+  constexpr int KSH = C::KSH;
+  __shared__ __attribute__((aligned(16))) __bf16 xrs[RG ? 2 : 1][16][RG ? 32 * KX + 8 : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 hrs[RG ? 2 : 1][16][RG ? C::KPH + 8 : 8];
+  bf16x8_t fu[RG ? KSH : 1], fw[RG ? KX : 1];
+  f32x4_t fb4 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RG) {
+    for (int i = tid; i < 2 * 16 * (32 * KX + 8); i += NT) (&xrs[0][0][0])[i] = (__bf16)0.0f;
+    for (int i = tid; i < 2 * 16 * (C::KPH + 8); i += NT) (&hrs[0][0][0])[i] = (__bf16)0.0f;
+    const int au = 4 * w + (col >> 2), ag = col & 3;
+#pragma unroll
+    for (int s = 0; s < KSH; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(U[min(k, H - 1) * G4 + ag * H + au] * (k < H ? 1.0f : 0.0f));
+      }
+      fu[s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      bf16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * quad + j;
+        v[j] = (__bf16)(W[min(k, Dw - 1) * G4 + ag * H + au] * (k < Dw ? 1.0f : 0.0f));
+      }
+      fw[s] = v;
+    }
+    const int u = 4 * w + quad;
+    fb4 = f32x4_t{bias[u], bias[H + u], bias[2 * H + u], bias[3 * H + u]};
+  }
+  // x_tt and h_{tt-1} of ring slot J into buffer b (h_{-1} = 0)
+  auto rg_stage = [&](int b, int J, int tt) {
+    if constexpr (RG) {
+#pragma unroll
+      for (int q = 0; q < XG; ++q) xrs[b][wx_seq][wx_k + q] = (__bf16)wx[J].v[q];
+      hrs[b][tid / H][tid % H] = (__bf16)(wh[J] * (tt >= 1 ? 1.f : 0.f));
+    }
+  };
+  // pre-activations from buffer b: exactly the forward's two MFMA chains (x part from the bias)
+  auto rg_pre = [&](int b) -> f32x4_t {
+    f32x4_t ax = fb4, ah = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (RG) {
+#pragma unroll
+      for (int s = 0; s < KX; ++s) {
+        const bf16x8_t bx = *reinterpret_cast<const bf16x8_t*>(&xrs[b][col][32 * s + 8 * quad]);
+        ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s], bx, ax, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < KSH; ++s) {
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(&hrs[b][col][32 * s + 8 * quad]);
+        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[s], bh, ah, 0, 0, 0);
+      }
+    }
+    return ax + ah;
+  };
 
   // reverse step s <-> time t = T-1-s. Streams for step s are loaded D steps ahead.
 #define GQ_TMB_LOAD_D(J, SS)                                                                \
@@ -538,10 +611,12 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   // stage step 0 (t = T-1) tiles
   *reinterpret_cast<float4*>(&dhs[0][gd / H][gd % H]) = dh_tile(0, T - 1);
   GQ_TMB_LOAD_D(0, D)
+  rg_stage(0, 0, T - 1);
   float dc[CPL], dhr[CPL], dhn[CPL];
 #pragma unroll
   for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
   __syncthreads();
+  f32x4_t pre = rg_pre(0);                        // (RG) pre-activations of step 0
   // dh_out of the step to come, read from LDS one step early (right after the barrier that
   // published it) so the cell phase does not wait on an LDS round trip
 #pragma unroll
@@ -560,7 +635,11 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         const int u = unit[cc];
         const float cp = rc[cc][jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
         const float dh = dhn[cc] + dhr[cc];
-        const float4 g4 = gates_unpack(rg[cc][j]);
+        float4 g4;
+        if constexpr (RG)
+          g4 = make_float4(sigmoidf_fast(pre[0]), sigmoidf_fast(pre[1]), tanhf_fast(pre[2]), sigmoidf_fast(pre[3]));
+        else
+          g4 = gates_unpack(rg[cc][j]);
         const float tc = tanhf_fast(rc[cc][j]);
         const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
         dc[cc] = dct * g4.y;
@@ -588,6 +667,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         }
         hT[s & 3][tid % H][tid / H] = (__bf16)(wh[j] * hm);
       }
+      rg_stage((s + 1) & 1, jn, t - 1);            // (RG) x_{t-1}, h_{t-2}: the next step's gates
       GQ_TMB_LOAD_W(j, s + D)
       GQ_TMB_LOAD_STATE(j, s + D)
       *reinterpret_cast<float4*>(&dhs[p ^ 1][gd / H][gd % H]) = dh_tile(jn, t - 1);   // dh tile of step s+1
@@ -608,6 +688,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         }
         dhr[cc] = a0[0] + a1[0];
       }
+      if constexpr (RG) pre = rg_pre((s + 1) & 1);   // next step's gates, behind the serial chain
       // (a') weight gradients of the step pair (s - 1, s) at odd s, or of the last step alone
       // (K lanes of the missing older step zeroed); the unrolled chunk's pad steps add nothing
       if (WG && !(TMW_SKIP & 1) && t >= 0 && ((s & 1) || t == 0)) {
@@ -689,21 +770,24 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #undef GQ_TMB_LOAD_W
 }
 
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST>
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool RG = false>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
-    int Mp, int T, int Din, int Dw) {
-  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, blockIdx.x, gridDim.x);
+    int Mp, int T, int Din, int Dw, const float* __restrict__ x = nullptr, const float* __restrict__ h = nullptr,
+    const float* __restrict__ bias = nullptr) {
+  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, false, RG>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, blockIdx.x,
+                                                          gridDim.x, x, h, nullptr, bias);
 }
 
-template <int H, int KX, int D, bool DX, bool LAST>
+template <int H, int KX, int D, bool DX, bool LAST, bool RG = false>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_wg_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, const float* __restrict__ x,
-    const float* __restrict__ h, float* __restrict__ ws, int Mp, int T, int Din, int Dw) {
-  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T, Din, Dw,
-                                                       blockIdx.x, gridDim.x, x, h, ws);
+    const float* __restrict__ h, float* __restrict__ ws, int Mp, int T, int Din, int Dw,
+    const float* __restrict__ bias = nullptr) {
+  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true, RG>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T, Din, Dw,
+                                                           blockIdx.x, gridDim.x, x, h, ws, bias);
 }
 
 // =====================================================================================
@@ -788,6 +872,10 @@ static bool tm_supported(int H, int Din, int gr) {
   return 16 * Din / gr <= 16 * H;
 }
 
+// recompute-gates backward (lstm_tm_bwd_body RG): one cell per lane with the x / h streams of the
+// fused weight-gradient kernel (H <= 32, Din <= 64, 16-byte x granules)
+static bool tm_rg_ok(int H, int gr) { return (H == 16 || H == 32) && gr == 4; }
+
 // (MaxPooling1D fused into the recurrences - running max + argmax in the forward, un-pooling on
 // load in the backward - was measured slower on both shapes: CML 0.766 vs 0.713 ms, SoilNet 3.920 vs
 // 3.894 ms; profiles/r3_bench_soilnet_poolfusion.json. Pooling runs as pool.hip kernels.)
@@ -795,8 +883,12 @@ template <int H, bool TRAIN, int KX, int GR>
 static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* U, const float* b, float* h, __bf16* g,
                        float* c, int Mp, int T, int Din, int Dw, hipStream_t st) {
   constexpr int D = 6;
-  hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W, U, b, h,
-                     g, c, Mp, T, Din, Dw);
+  if (TRAIN && g == nullptr)      // recompute-gates backward: c only
+    hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D, false>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W,
+                       U, b, h, g, c, Mp, T, Din, Dw);
+  else
+    hipLaunchKernelGGL((lstm_tm_fwd_kernel<H, TRAIN, KX, GR, D>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, x, W, U, b,
+                       h, g, c, Mp, T, Din, Dw);
 }
 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
@@ -837,8 +929,10 @@ static void tm_bwd_cfg(int ntiles, const float* dh, const __bf16* g, const float
 
 // x: [T, Mp, Din] time-major; W: [Dw, 4H] with Dw <= Din (x channels >= Dw must be zero, e.g. the
 // alignment padding of a 19-channel input to 20). Returns [h (T,Mp,H), gates (state), c (state)].
+// store_gates = false (train): the gates state is empty and the backward recomputes the gates
+// (lstm_tm_bwd with an empty g; H <= 32, 16-byte x granules: tm_rg_ok).
 std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U,
-                                    const at::Tensor& b, bool train) {
+                                    const at::Tensor& b, bool train, bool store_gates) {
   check_f32_cuda(x, "x");
   check_f32_cuda(W, "W");
   check_f32_cuda(U, "U");
@@ -851,15 +945,17 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
               "lstm_tm_fwd: weight shapes");
   const int gr = tm_granule(Din, x.data_ptr());
   TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
+  TORCH_CHECK(store_gates || !train || tm_rg_ok(H, gr), "lstm_tm_fwd: recomputed gates need H <= 32, Din % 4 == 0");
   c10::DeviceGuard guard(x.device());
   auto opt = x.options();
   // one extra (scratch) time row: stores of steps that have nothing to store land there
   at::Tensor h = at::empty({T + 1, Mp, H}, opt);
-  at::Tensor g = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  at::Tensor g = (train && store_gates) ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16))
+                                        : at::empty({0}, opt.dtype(at::kBFloat16));
   at::Tensor c = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
   const int ntiles = Mp / 16;
   auto st = stream();
-  __bf16* gp = train ? bf16_ptr(g) : nullptr;
+  __bf16* gp = (train && store_gates) ? bf16_ptr(g) : nullptr;
   float* cp = train ? c.data_ptr<float>() : nullptr;
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (train) tm_fwd_cfg<HH, true, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
@@ -874,7 +970,7 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
 // Returns [hA, gA, cA, hB, gB, cB] with the layouts of lstm_tm_fwd.
 std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, const at::Tensor& UA,
                                      const at::Tensor& bA, const at::Tensor& WB, const at::Tensor& UB,
-                                     const at::Tensor& bB, bool train) {
+                                     const at::Tensor& bB, bool train, bool store_gates) {
   for (const at::Tensor* t : {&x, &WA, &UA, &bA, &WB, &UB, &bB}) check_f32_cuda(*t, "lstm_tm2_fwd operand");
   TORCH_CHECK(x.dim() == 3, "lstm_tm2_fwd: x must be [T, Mp, Din]");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)UA.size(0);
@@ -886,27 +982,30 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
               "lstm_tm2_fwd: layer B must be H -> H with the same H");
   const int gr = tm_granule(Din, x.data_ptr());
   TORCH_CHECK(H <= 32 && tm_supported(H, Din, gr), "lstm_tm2_fwd: unsupported (H, Din) = (", H, ", ", Din, ")");
+  TORCH_CHECK(store_gates || !train || tm_rg_ok(H, gr), "lstm_tm2_fwd: recomputed gates need Din % 4 == 0");
+  const bool sg = train && store_gates;
   c10::DeviceGuard guard(x.device());
   auto opt = x.options();
   auto mk = [&](bool state, int last) {
     return state ? (train ? at::empty({T + 1, Mp, H, last}, opt) : at::empty({0}, opt)) : at::empty({T + 1, Mp, H}, opt);
   };
   at::Tensor hA = mk(false, 0), hB = mk(false, 0);
-  at::Tensor gA = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
-  at::Tensor gB = train ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  at::Tensor gA = sg ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt.dtype(at::kBFloat16));
+  at::Tensor gB = sg ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt.dtype(at::kBFloat16));
   at::Tensor cA = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
   at::Tensor cB = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
   const int ntiles = Mp / 16;
   auto st = stream();
-  __bf16* PG[2] = {train ? bf16_ptr(gA) : nullptr, train ? bf16_ptr(gB) : nullptr};
+  __bf16* PG[2] = {sg ? bf16_ptr(gA) : nullptr, sg ? bf16_ptr(gB) : nullptr};
   float* P[4] = {nullptr, train ? cA.data_ptr<float>() : nullptr, nullptr, train ? cB.data_ptr<float>() : nullptr};
-#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR)                                                                         \
-  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,        \
+#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, SGV)                                                                    \
+  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, SGV>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,   \
                      x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
                      WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), PG[0], \
                      P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw)
   GQ_TM2_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
-      if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR); else GQ_TM2_LAUNCH(HH, false, KXX, GRR))));
+      if (sg) GQ_TM2_LAUNCH(HH, true, KXX, GRR, true); else if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, false);
+      else GQ_TM2_LAUNCH(HH, false, KXX, GRR, true))));
 #undef GQ_TM2_LAUNCH
   GQ_LAUNCH_CHECK();
   return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB};
@@ -1330,20 +1429,22 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
 }
 
 // dh: [T, Mp, H] (or [Mp, H] when only the last step has a gradient). Returns dx [T, Mp, Din]
-// (empty if !need_dx) and accumulates dW, dU, db when they are non-empty.
+// (empty if !need_dx) and accumulates dW, dU, db when they are non-empty. An empty g (the forward ran
+// with store_gates = false) selects the recompute-gates backward, which needs the bias b.
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
-                       const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, at::Tensor dW, at::Tensor dU,
-                       at::Tensor db, bool need_dx) {
-  const at::Tensor* ops[] = {&dh, &c, &x, &h, &W, &U};
+                       const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
+                       at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx) {
+  const at::Tensor* ops[] = {&dh, &c, &x, &h, &W, &U, &b};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
-  check_gates_cuda(g);
+  const bool rg = g.numel() == 0;
+  if (!rg) check_gates_cuda(g);
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
   const int Dw = (int)W.size(0);
-  TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H, "lstm_tm_bwd: W shape");
+  TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H && b.numel() == 4 * H, "lstm_tm_bwd: W / b shape");
   const bool last = dh.dim() == 2;
   TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H)
                    : (dh.size(0) == T && dh.size(1) == Mp && dh.size(2) == H), "lstm_tm_bwd: dh shape");
-  TORCH_CHECK(g.numel() == (long)(T + 1) * Mp * H * 4 && c.numel() == (long)(T + 1) * Mp * H &&
+  TORCH_CHECK((rg || g.numel() == (long)(T + 1) * Mp * H * 4) && c.numel() == (long)(T + 1) * Mp * H &&
                   h.numel() == (long)T * Mp * H, "lstm_tm_bwd: saved state shapes");
   const bool wg = dW.numel() > 0;
   if (wg) {
@@ -1354,11 +1455,14 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   }
   const int gr = tm_granule(Din, x.data_ptr());
   TORCH_CHECK(tm_supported(H, Din, gr), "lstm_tm_bwd: unsupported shape");
+  TORCH_CHECK(!rg || (tm_rg_ok(H, gr) && Din <= 64 && h.is_contiguous() && x.is_contiguous()),
+              "lstm_tm_bwd: recomputed gates need H <= 32, Din <= 64, contiguous 16-byte aligned x / h");
   c10::DeviceGuard guard(x.device());
   const int ntiles = Mp / 16;
   auto st = stream();
   const int ncb_w = lstm_grads_col_blocks(H);
-  if (wg && tm_fused_wgrad(H, Din, gr, ntiles)) {
+  __bf16* gptr = rg ? nullptr : bf16_ptr(g);
+  if (wg && (rg || tm_fused_wgrad(H, Din, gr, ntiles))) {
     // weight gradients inside the recurrence: one split record per tile, then the reduction
     const int DT = (Dw + 1 + 15) / 16, RC = (DT + H / 16) * 1024 * ncb_w;
     const int NG = std::max(1, ntiles / 512);
@@ -1366,11 +1470,13 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, x.options()) : at::empty({0}, x.options());
     if (need_dx) TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 4 == 0 && h.is_contiguous(), "lstm_tm_bwd: h layout");
-#define GQ_TM_WG_CALL(DXV, LASTV)                                                                              \
-  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV>), dim3(ntiles), dim3(TMC<HH>::NT), 0, st,    \
-                     dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), W.data_ptr<float>(),                \
+#define GQ_TM_WG_CALL2(DXV, LASTV, RGV)                                                                        \
+  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV, RGV>), dim3(ntiles), \
+                     dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), gptr, c.data_ptr<float>(), W.data_ptr<float>(), \
                      U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr, x.data_ptr<float>(),         \
-                     h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw)
+                     h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw, b.data_ptr<float>())
+#define GQ_TM_WG_CALL(DXV, LASTV) \
+  do { if (rg) GQ_TM_WG_CALL2(DXV, LASTV, true); else GQ_TM_WG_CALL2(DXV, LASTV, false); } while (0)
 #define GQ_TM_WG_KX(...)                                                                                        \
   if ((Din + 31) / 32 == 1) { constexpr int KXX = 1; __VA_ARGS__; }                                             \
   else { constexpr int KXX = 2; __VA_ARGS__; }
@@ -1384,10 +1490,12 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     }
 #undef GQ_TM_WG_KX
 #undef GQ_TM_WG_CALL
+#undef GQ_TM_WG_CALL2
     GQ_LAUNCH_CHECK();
     lstm_grads_reduce_records(ws, H, Dw, ntiles, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), st);
     return need_dx ? dx.narrow(0, 0, T) : dx;
   }
+  TORCH_CHECK(!rg || !wg, "lstm_tm_bwd: recomputed gates with weight gradients take the fused kernel");
   if (wg && need_dx && ncb_w > 1 && tm_rec_dx()) {
     // several gate-column blocks: the weight-gradient pass could only produce dx as ncb partial
     // slabs plus a slab sum (ncb + 2 dx-sized passes); the recurrence computes dx^T = W dz^T
@@ -1430,8 +1538,20 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   }
   at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
   TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
+  if (rg) {      // frozen weights (integrated gradients), gates recomputed: H <= 32, GR = 4
+#define GQ_TM_RG_CALL(LASTV)                                                                                   \
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<HH, KXX, 4, 4, false, true, LASTV, true>), dim3(ntiles), dim3(TMC<HH>::NT), \
+                     0, st, dh.data_ptr<float>(), nullptr, c.data_ptr<float>(), W.data_ptr<float>(),              \
+                     U.data_ptr<float>(), dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, x.data_ptr<float>(),     \
+                     h.data_ptr<float>(), b.data_ptr<float>())
+    GQ_TM2_H_DISPATCH(H, if ((Din + 31) / 32 == 1) { constexpr int KXX = 1; if (last) GQ_TM_RG_CALL(true); else GQ_TM_RG_CALL(false); }
+                         else { constexpr int KXX = 2; if (last) GQ_TM_RG_CALL(true); else GQ_TM_RG_CALL(false); });
+#undef GQ_TM_RG_CALL
+    GQ_LAUNCH_CHECK();
+    return dx.narrow(0, 0, T);
+  }
 #define GQ_TM_BWD_CALL(LASTV)                                                                               \
-  tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),          \
+  tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), gptr,                 \
                                                c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
                                                dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st)
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,

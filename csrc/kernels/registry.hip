@@ -28,9 +28,9 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("lstm_grads(Tensor dz, Tensor x, Tensor hseq, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
         "bool need_dx) -> Tensor");
   // time-major LSTM with fused backward (lstm_tm.hip)
-  m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train) -> Tensor[]");
+  m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train, bool store_gates=True) -> Tensor[]");
   m.def("lstm_tm2_fwd(Tensor x, Tensor WA, Tensor UA, Tensor bA, Tensor WB, Tensor UB, Tensor bB, "
-        "bool train) -> Tensor[]");
+        "bool train, bool store_gates=True) -> Tensor[]");
   m.def("lstm_tm_grads(Tensor dz, Tensor x, Tensor h, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
         "bool need_dx) -> Tensor");
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");
@@ -63,7 +63,7 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor gh, Tensor gW, int g_period, int g_hshift, Tensor gws, Tensor rws, Tensor rW, Tensor(a!) rdW, "
         "Tensor(b!) rdU, Tensor(c!) rdb) -> Tensor");
   m.def("lstm_grads_job_ws(Tensor dz, Tensor x, Tensor W, int H) -> Tensor");
-  m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor(a!) dW, "
+  m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor b, Tensor(a!) dW, "
         "Tensor(b!) dU, Tensor(c!) db, bool need_dx) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)
   m.def("gcn_stats(Tensor x, Tensor mask) -> Tensor");

@@ -319,7 +319,7 @@ class _HipLSTM(torch.autograd.Function):
                 None, None)
 
 
-def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx):
+def _tm_layer_backward(dout, x, W, U, b, h, g, c, params, need_w, need_dx):
     """Backward of one time-major layer (the pipe when it takes the layer, else one fused kernel).
     Returns dx (or None) and the three weight gradients to hand to autograd (None where they
     were accumulated directly into ``.grad``)."""
@@ -333,12 +333,12 @@ def _tm_layer_backward(dout, x, W, U, h, g, c, params, need_w, need_dx):
         e = x.new_zeros(0)
         sinks = [(e, True)] * 3
     Wc, Uc = W.contiguous(), U.contiguous()
-    if wgrad and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+    if wgrad and g.numel() > 0 and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
         dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, Wc, Uc, sinks, need_dx)
     else:
         with _deferred_reduce(wgrad and all(d for _, d in sinks)):
-            dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, sinks[0][0], sinks[1][0],
-                                       sinks[2][0], need_dx)
+            dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, Wc, Uc, b.contiguous(), sinks[0][0],
+                                       sinks[1][0], sinks[2][0], need_dx)
     grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need_w)]
     return (dx if need_dx else None), grads
 
@@ -418,8 +418,8 @@ class _HipLSTMChain(torch.autograd.Function):
             else:
                 xi = outs[5 * (i - 1) + 3] if pools[i - 1] else outs[5 * (i - 1)]
             need_dx = i > 0 or bool(need[0])
-            dx, gr = _tm_layer_backward(dh, xi, Ws[i], Us[i], h, g, c, ctx.params[3 * i:3 * i + 3],
-                                        need[2 + 3 * i:5 + 3 * i], need_dx)
+            dx, gr = _tm_layer_backward(dh, xi, Ws[i], Us[i], ctx.params[3 * i + 2], h, g, c,
+                                        ctx.params[3 * i:3 * i + 3], need[2 + 3 * i:5 + 3 * i], need_dx)
             grads[3 * i:3 * i + 3] = gr
             dh = dx
         return (dx if need[0] else None, None, *grads)
@@ -664,17 +664,18 @@ class _HipLSTMTM(torch.autograd.Function):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:4])
-        h, g, c = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need)
+        sg = not recompute_gates(x, U.shape[0], any(ctx.needs_input_grad[1:4]))
+        h, g, c = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need, sg)
         ctx.params = (W, U, b)
         ctx.return_sequences = return_sequences
         if need:
-            ctx.save_for_backward(x, W, U, h, g, c)
+            ctx.save_for_backward(x, W, U, b, h, g, c)
         return h if return_sequences else h[-1]
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
-        x, W, U, h, g, c = ctx.saved_tensors
+        x, W, U, b, h, g, c = ctx.saved_tensors
         need = ctx.needs_input_grad
         wgrad = any(need[1:4])
         need_dx = bool(need[0])
@@ -685,12 +686,12 @@ class _HipLSTMTM(torch.autograd.Function):
         else:
             e = x.new_zeros(0)
             sinks = [(e, True)] * 3
-        if wgrad and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+        if wgrad and g.numel() > 0 and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
             dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
         else:
             with _deferred_reduce(wgrad and all(d for _, d in sinks)):
                 dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
-                                           sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
+                                           b.contiguous(), sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
         grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
         return (dx if need_dx else None, *grads, None)
 
@@ -707,19 +708,20 @@ class _HipLSTMTMPair(torch.autograd.Function):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:7])
+        sg = not recompute_gates(x, UA.shape[0], any(ctx.needs_input_grad[1:7]))
         hA, gA, cA, hB, gB, cB = hip_ops().lstm_tm2_fwd(
             x, WA.contiguous(), UA.contiguous(), bA.contiguous(), WB.contiguous(), UB.contiguous(), bB.contiguous(),
-            need)
+            need, sg)
         ctx.params = (WA, UA, bA, WB, UB, bB)
         if need:
-            ctx.save_for_backward(x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB)
+            ctx.save_for_backward(x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB)
         return hB
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        x, WA, UA, hA, gA, cA, WB, UB, hB, gB, cB = ctx.saved_tensors
+        x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB = ctx.saved_tensors
         need = ctx.needs_input_grad
         e = x.new_zeros(0)
         dout = dout.contiguous()
@@ -733,17 +735,18 @@ class _HipLSTMTMPair(torch.autograd.Function):
         sA = sinks(ctx.params[:3], need[1:4])
         need_dx = bool(need[0])
         dx = None
-        if (any(need[4:7]) and any(need[1:4]) and _pipe_on(sB, x.shape[1]) and _pipe_on(sA, x.shape[1])
+        if (any(need[4:7]) and any(need[1:4]) and gA.numel() > 0 and _pipe_on(sB, x.shape[1])
+                and _pipe_on(sA, x.shape[1])
                 and _pipe_x_ok(x, WA.shape[0]) and _pipe_x_ok(hA, WB.shape[0])):
             dhA = _pipe_tm_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
             dx = _pipe_tm_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
             with _deferred_reduce(all(d for _, d in sB) and all(d for _, d in sA)):
-                dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(),
+                dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), bB.contiguous(),
                                       sB[0][0], sB[1][0], sB[2][0], True)
                 if need_dx or any(need[1:4]):
-                    dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA[0][0], sA[1][0],
-                                         sA[2][0], need_dx)
+                    dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), bA.contiguous(),
+                                         sA[0][0], sA[1][0], sA[2][0], need_dx)
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
         return (dx if need_dx else None, *gA_, *gB_)
@@ -752,6 +755,21 @@ class _HipLSTMTMPair(torch.autograd.Function):
 def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:
     """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``)."""
     return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias)
+
+
+def recompute_gates(x: torch.Tensor, H: int, weight_grads: bool) -> bool:
+    """Whether a time-major layer's forward saves no gates and its backward recomputes them from
+    x_t and h_{t-1} (``lstm_tm.hip`` RG: bitwise the forward's pre-activations; halves the forward's
+    state stream). H in {16, 32}, 16-byte x granules, and the backward must take the fused kernel:
+    frozen weights (integrated gradients), or too many sequences for the pipelined backward
+    (``PIPE_MAX_SEQ``). ``GNNQC_TM_RG=0`` keeps the saved gates."""
+    import os
+    if os.environ.get("GNNQC_TM_RG", "1") != "1" or H not in (16, 32):
+        return False
+    Din = x.shape[-1]
+    if Din % 4 or Din > 64 or x.data_ptr() % 16 or not x.is_contiguous():
+        return False
+    return (not weight_grads) or x.shape[1] > PIPE_MAX_SEQ or not _Pipe.enabled
 
 
 def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf16: bool = True) -> bool:

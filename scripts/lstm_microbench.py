@@ -65,10 +65,10 @@ def main():
                 dht = torch.randn_like(ht)
                 r["tm_fwd_train_us"] = timeit(lambda: ops.lstm_tm_fwd(xt, W, U, b, True), args.reps)
                 r["tm_fwd_infer_us"] = timeit(lambda: ops.lstm_tm_fwd(xt, W, U, b, False), args.reps)
-                r["tm_bwd_fused_us"] = timeit(lambda: ops.lstm_tm_bwd(dht, gt2, ct, xt, ht, W, U, dW, dU, db, True),
+                r["tm_bwd_fused_us"] = timeit(lambda: ops.lstm_tm_bwd(dht, gt2, ct, xt, ht, W, U, b, dW, dU, db, True),
                                               args.reps)
                 e = torch.zeros(0, device=dev)
-                r["tm_bwd_nowgrad_us"] = timeit(lambda: ops.lstm_tm_bwd(dht, gt2, ct, xt, ht, W, U, e, e, e, True),
+                r["tm_bwd_nowgrad_us"] = timeit(lambda: ops.lstm_tm_bwd(dht, gt2, ct, xt, ht, W, U, b, e, e, e, True),
                                                 args.reps)
                 for k in ("tm_fwd_train_us", "tm_fwd_infer_us", "tm_bwd_fused_us", "tm_bwd_nowgrad_us"):
                     r[k.replace("_us", "_ns_per_step")] = round(r[k] * 1000.0 / T, 1)

@@ -36,12 +36,12 @@ def main():
             else:
                 dW, dU, db = torch.zeros_like(W), torch.zeros_like(U), torch.zeros_like(b)
             for _ in range(3):
-                ops.lstm_tm_bwd(dh, g, c, x, h, W, U, dW, dU, db, True)
+                ops.lstm_tm_bwd(dh, g, c, x, h, W, U, b, dW, dU, db, True)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                ops.lstm_tm_bwd(dh, g, c, x, h, W, U, dW, dU, db, True)
+                ops.lstm_tm_bwd(dh, g, c, x, h, W, U, b, dW, dU, db, True)
             e1.record()
             torch.cuda.synchronize()
             print(json.dumps({"H": H, "Din": Din, "T": T, "path": path, "us": round(e0.elapsed_time(e1) * 1e3 / reps, 1)}),

@@ -386,6 +386,58 @@ def test_lstm_time_major_fused_bwd_matches_eager(cuda_device, H, Din, ret_seq, w
     assert float(xt.grad[:, M:].abs().max()) == 0.0          # padded rows get no gradient
 
 
+@pytest.mark.parametrize("H", [16, 32])
+@pytest.mark.parametrize("Din", [20, 32, 64])
+@pytest.mark.parametrize("wgrad", [True, False])
+@pytest.mark.parametrize("pair", [False, True])
+def test_lstm_tm_recomputed_gates_match_saved_gates(cuda_device, monkeypatch, H, Din, wgrad, pair):
+    """Recompute-gates backward (lstm_tm.hip RG: the forward saves only c, the backward recomputes
+    i, f, g, o from x_t and h_{t-1}) vs the saved-gates form: identical forward output, gradients
+    within bf16-gate rounding of each other, and the RG gradients against an fp64 eager oracle."""
+    from gnnqc.ops import lstm as L
+    from gnnqc.utils.native import hip_ops
+    monkeypatch.setattr(L._Pipe, "enabled", False)      # (training layers of any size take RG)
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(7 * H + Din + 100 * wgrad + 1000 * pair)
+    M, T, Mp = 72, 37, 80
+    x = torch.zeros(T, Mp, Din)
+    x[:, :M] = torch.randn(T, M, Din, generator=gen)
+    x = x.to(dev)
+    WA, UA, bA = _lstm_params(Din, H, gen, dev)
+    WB, UB, bB = _lstm_params(H, H, gen, dev)
+    dout = torch.randn(T, Mp, H, generator=gen).to(dev)
+    dout[:, M:] = 0
+    _, g_rg, c_rg = hip_ops().lstm_tm_fwd(x, WA, UA, bA, True, False)
+    assert g_rg.numel() == 0 and c_rg.numel() == (T + 1) * Mp * H
+
+    def run(rg):
+        monkeypatch.setenv("GNNQC_TM_RG", "1" if rg else "0")
+        xi = x.clone().requires_grad_(True)
+        ps = [t.clone().requires_grad_(wgrad) for t in ((WA, UA, bA, WB, UB, bB) if pair else (WA, UA, bA))]
+        out = L._HipLSTMTMPair.apply(xi, *ps) if pair else L.lstm_layer_tm(xi, *ps, True)
+        out.backward(dout)
+        return out.detach(), [xi.grad] + ([p.grad for p in ps] if wgrad else [])
+
+    o0, g0 = run(False)
+    o1, g1 = run(True)
+    assert torch.equal(o0, o1)                       # the forward arithmetic is unchanged
+    for a, b_ in zip(g1, g0):
+        assert (a - b_).norm().item() <= 2e-2 * (b_.norm().item() + 1e-6)
+    # fp64 oracle of the RG gradients
+    ref_in = [x[:, :M].transpose(0, 1).double().clone().requires_grad_(True)]
+    ref_ps = [t.double().clone().requires_grad_(True) for t in ((WA, UA, bA, WB, UB, bB) if pair else (WA, UA, bA))]
+    h = L.lstm_eager(ref_in[0], *ref_ps[:3], return_sequences=True)
+    if pair:
+        h = L.lstm_eager(h, *ref_ps[3:], return_sequences=True)
+    h.backward(dout[:, :M].transpose(0, 1).double())
+    got = [g1[0][:, :M].transpose(0, 1)] + (g1[1:] if wgrad else [])
+    refs = [ref_in[0].grad] + ([p.grad for p in ref_ps] if wgrad else [])
+    for a, r in zip(got, refs):
+        err = (a.double() - r).abs().max().item() / (r.abs().max().item() + 1e-6)
+        assert err < 5e-2, err
+    assert float(g1[0][:, M:].abs().max()) == 0.0
+
+
 def test_timelayer_time_major_matches_sequence_major(cuda_device, monkeypatch):
     """The CML TimeLayer (LSTM 16,16 | pool | 32,32 | pool | 64,64 | pool | 128): time-major
     fused path vs the sequence-major kernels - forward and every parameter gradient."""
