@@ -58,6 +58,56 @@ __global__ __launch_bounds__(256) void maxpool1d_bwd_kernel(const float* __restr
   }
 }
 
+// Row-granular forms for wide rows (the time-major TimeLayer views a [T, Mp, C] tensor as one
+// [1, T, Mp C] row set: C4 in the 10^4..10^5 range): a 3-D grid (float4 column block, output step,
+// sequence) instead of a flat grid-stride loop, so no thread divides a 64-bit index (the flat form's
+// e % C4, e / C4 per element cost more than its memory traffic)
+__global__ __launch_bounds__(256) void maxpool1d_fwd_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                                 uint8_t* __restrict__ idx, int T, int To, long C4,
+                                                                 int p) {
+  const long c4 = blockIdx.x * 256L + threadIdx.x;
+  if (c4 >= C4) return;
+  const long m = blockIdx.z;
+  const int to = blockIdx.y;
+  const float4* src = reinterpret_cast<const float4*>(x) + (m * T + (long)to * p) * C4 + c4;
+  float4 best = src[0];
+  uchar4 bi = make_uchar4(0, 0, 0, 0);
+  for (int k = 1; k < p; ++k) {
+    const float4 v = src[(long)k * C4];
+    if (v.x > best.x) { best.x = v.x; bi.x = k; }
+    if (v.y > best.y) { best.y = v.y; bi.y = k; }
+    if (v.z > best.z) { best.z = v.z; bi.z = k; }
+    if (v.w > best.w) { best.w = v.w; bi.w = k; }
+  }
+  const long o = (m * To + to) * C4 + c4;
+  reinterpret_cast<float4*>(y)[o] = best;
+  reinterpret_cast<uchar4*>(idx)[o] = bi;
+}
+
+__global__ __launch_bounds__(256) void maxpool1d_bwd_rows_kernel(const float* __restrict__ dy,
+                                                                 const uint8_t* __restrict__ idx,
+                                                                 float* __restrict__ dx, int T, int To, long C4,
+                                                                 int p) {
+  const long c4 = blockIdx.x * 256L + threadIdx.x;
+  if (c4 >= C4) return;
+  const long m = blockIdx.z;
+  const int t = blockIdx.y;
+  const int to = t / p, k = t - to * p;            // (block-uniform)
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (to < To) {
+    const long s = (m * To + to) * C4 + c4;
+    const float4 g = reinterpret_cast<const float4*>(dy)[s];
+    const uchar4 b = reinterpret_cast<const uchar4*>(idx)[s];
+    o.x = b.x == k ? g.x : 0.f;
+    o.y = b.y == k ? g.y : 0.f;
+    o.z = b.z == k ? g.z : 0.f;
+    o.w = b.w == k ? g.w : 0.f;
+  }
+  reinterpret_cast<float4*>(dx)[(m * T + t) * C4 + c4] = o;
+}
+
+static bool pool_rows_form(long M, long C4) { return C4 >= 256 && M <= 65535; }
+
 static int ew_grid(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 4096)); }
 
 std::vector<at::Tensor> maxpool1d_fwd(const at::Tensor& x, int64_t p) {
@@ -70,7 +120,12 @@ std::vector<at::Tensor> maxpool1d_fwd(const at::Tensor& x, int64_t p) {
   at::Tensor y = at::empty({M, To, C}, x.options());
   at::Tensor idx = at::empty({M, To, C}, x.options().dtype(at::kByte));
   const long n = M * To * (C / 4);
-  if (n > 0) {
+  if (n > 0 && pool_rows_form(M, C / 4)) {
+    hipLaunchKernelGGL(maxpool1d_fwd_rows_kernel, dim3((unsigned)((C / 4 + 255) / 256), To, (unsigned)M), dim3(256), 0,
+                       stream(), x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(), T, To,
+                       (long)(C / 4), (int)p);
+    GQ_LAUNCH_CHECK();
+  } else if (n > 0) {
     hipLaunchKernelGGL(maxpool1d_fwd_kernel, dim3(ew_grid(n)), dim3(256), 0, stream(), x.data_ptr<float>(),
                        y.data_ptr<float>(), idx.data_ptr<uint8_t>(), M, T, To, C / 4, (int)p);
     GQ_LAUNCH_CHECK();
@@ -88,7 +143,12 @@ at::Tensor maxpool1d_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t T,
   c10::DeviceGuard guard(dy.device());
   at::Tensor dx = at::empty({M, T, C}, dy.options());
   const long n = M * T * (C / 4);
-  if (n > 0) {
+  if (n > 0 && pool_rows_form(M, C / 4)) {
+    hipLaunchKernelGGL(maxpool1d_bwd_rows_kernel, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)T, (unsigned)M),
+                       dim3(256), 0, stream(), dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(),
+                       (int)T, To, (long)(C / 4), (int)p);
+    GQ_LAUNCH_CHECK();
+  } else if (n > 0) {
     hipLaunchKernelGGL(maxpool1d_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, stream(), dy.data_ptr<float>(),
                        idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), M, (int)T, To, C / 4, (int)p);
     GQ_LAUNCH_CHECK();

@@ -311,7 +311,8 @@ def test_fused_head_direct_grad_accumulation(cuda_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,T,C,p", [(50, 181, 16, 3), (7, 60, 32, 3), (3, 22, 128, 2), (5, 10, 64, 4)])
+@pytest.mark.parametrize("M,T,C,p", [(50, 181, 16, 3), (7, 60, 32, 3), (3, 22, 128, 2), (5, 10, 64, 4),
+                                     (1, 181, 4096, 3), (2, 37, 1100, 3), (1, 11, 2048, 1)])
 def test_maxpool1d_matches_eager(cuda_device, M, T, C, p):
     from gnnqc.ops.pool import max_pool1d
     gen = torch.Generator().manual_seed(M * T + C)
