@@ -385,13 +385,20 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 // step before (off the serial chain: they depend on saved data only). x_t / h_{t-1} come through the
 // same register rings as the WG streams and are staged row-major ([sequence][channel], the forward's B
 // operand layout) into a double buffer.
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false, bool RG = false>
+// UP (un-pool on load): the layer's output went through MaxPooling1D(P) (valid, stride P) and dhout is
+// the POOLED gradient [T / P][Mp][H] with the pool's byte argmax pidx of the same shape; the dh stream
+// reads pooled granule floor(t / P) and its 4 argmax bytes and keeps the components whose argmax is
+// t mod P (zero past the last window), as maxpool1d_bwd would have written them at full resolution -
+// that kernel and its full-resolution dh round trip through HBM are gone.
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false, bool RG = false,
+          bool UP = false>
 __device__ __forceinline__ void lstm_tm_bwd_body(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw, int tile, int ntiles, const float* __restrict__ xw = nullptr,
     const float* __restrict__ hw = nullptr, float* __restrict__ wsr = nullptr,
-    const float* __restrict__ bias = nullptr) {
+    const float* __restrict__ bias = nullptr, const unsigned char* __restrict__ pidx = nullptr, int P = 1) {
+  static_assert(!(UP && LAST), "un-pooling needs a per-step gradient");
   using C = TMC<H>;
   constexpr int CPL = C::CPL, NW = C::NW, NT = C::NT, G4 = C::G4, KB = C::KB;
   static_assert(!WG || (CPL == 1 && NT == 16 * H && G4 == 16 * NW && GR == 4), "fused weight gradients: H <= 64");
@@ -500,6 +507,10 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   const int gd = (tid % n_gd) * 4;
   const float* dbase = dhout + (size_t)row0 * H + gd;
   const size_t dstep = LAST ? 0 : (size_t)Mp * H;
+  const unsigned* ibase = UP ? reinterpret_cast<const unsigned*>(pidx + (size_t)row0 * H + gd) : nullptr;
+  const int Ts = UP ? T / P : 0;
+  // t / P as a multiply-high (exact for t * P < 2^32); P == 1 is the identity (its magic would wrap)
+  const unsigned pmag = (UP && P > 1) ? 0xFFFFFFFFu / (unsigned)P + 1u : 0u;
   float4 rd[D];
   auto dh_tile = [&](int j, int t) -> float4 { (void)t; return rd[j]; };
   // dz storer: one float4 granule of the [16][4H] tile per thread
@@ -592,7 +603,19 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 
   // reverse step s <-> time t = T-1-s. Streams for step s are loaded D steps ahead.
 #define GQ_TMB_LOAD_D(J, SS)                                                                \
-  {                                                                                         \
+  if constexpr (UP) {                                                                       \
+    const int tt_ = max(T - 1 - (SS), 0);                                                   \
+    const int st_ = P > 1 ? (int)__umulhi((unsigned)tt_, pmag) : tt_;                      \
+    const int sc_ = min(st_, Ts - 1);                                                       \
+    float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)sc_ * dstep);              \
+    const unsigned id_ = ibase[(size_t)sc_ * dstep / 4];                                    \
+    const unsigned ph_ = st_ < Ts ? (unsigned)(tt_ - st_ * P) : 0xffu + 1u;                 \
+    v_.x = (id_ & 0xffu) == ph_ ? v_.x : 0.f;                                               \
+    v_.y = ((id_ >> 8) & 0xffu) == ph_ ? v_.y : 0.f;                                        \
+    v_.z = ((id_ >> 16) & 0xffu) == ph_ ? v_.z : 0.f;                                       \
+    v_.w = (id_ >> 24) == ph_ ? v_.w : 0.f;                                                 \
+    rd[J] = v_;                                                                             \
+  } else {                                                                                  \
     const int tt_ = max(T - 1 - (SS), 0);                                                   \
     float4 v_ = *reinterpret_cast<const float4*>(dbase + (size_t)tt_ * dstep);              \
     if (LAST) {                                                                             \
@@ -616,7 +639,14 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #pragma unroll
   for (int cc = 0; cc < CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
   __syncthreads();
-  f32x4_t pre = rg_pre(0);                        // (RG) pre-activations of step 0
+  // (RG) gates of the step to come: pre-activations from the MFMA phase of the step before, activated
+  // at the end of that phase (after its dx / weight-gradient MFMAs have covered the MFMA latency)
+  auto rg_act = [&](const f32x4_t& a) {
+    return make_float4(sigmoidf_fast(a[0]), sigmoidf_fast(a[1]), tanhf_fast(a[2]), sigmoidf_fast(a[3]));
+  };
+  f32x4_t pre = rg_pre(0);
+  float4 gn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (RG) gn = rg_act(pre);
   // dh_out of the step to come, read from LDS one step early (right after the barrier that
   // published it) so the cell phase does not wait on an LDS round trip
 #pragma unroll
@@ -637,7 +667,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         const float dh = dhn[cc] + dhr[cc];
         float4 g4;
         if constexpr (RG)
-          g4 = make_float4(sigmoidf_fast(pre[0]), sigmoidf_fast(pre[1]), tanhf_fast(pre[2]), sigmoidf_fast(pre[3]));
+          g4 = gn;
         else
           g4 = gates_unpack(rg[cc][j]);
         const float tc = tanhf_fast(rc[cc][j]);
@@ -747,6 +777,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
           }
         }
       }
+      if constexpr (RG) gn = rg_act(pre);           // the next step's gates
     }
   }
   __syncthreads();
@@ -770,24 +801,24 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #undef GQ_TMB_LOAD_W
 }
 
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool RG = false>
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool RG = false, bool UP = false>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw, const float* __restrict__ x = nullptr, const float* __restrict__ h = nullptr,
-    const float* __restrict__ bias = nullptr) {
-  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, false, RG>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw, blockIdx.x,
-                                                          gridDim.x, x, h, nullptr, bias);
+    const float* __restrict__ bias = nullptr, const unsigned char* __restrict__ pidx = nullptr, int P = 1) {
+  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, false, RG, UP>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw,
+                                                              blockIdx.x, gridDim.x, x, h, nullptr, bias, pidx, P);
 }
 
-template <int H, int KX, int D, bool DX, bool LAST, bool RG = false>
+template <int H, int KX, int D, bool DX, bool LAST, bool RG = false, bool UP = false>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_wg_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, const float* __restrict__ x,
     const float* __restrict__ h, float* __restrict__ ws, int Mp, int T, int Din, int Dw,
-    const float* __restrict__ bias = nullptr) {
-  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true, RG>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T, Din, Dw,
-                                                           blockIdx.x, gridDim.x, x, h, ws, bias);
+    const float* __restrict__ bias = nullptr, const unsigned char* __restrict__ pidx = nullptr, int P = 1) {
+  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true, RG, UP>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T, Din, Dw,
+                                                               blockIdx.x, gridDim.x, x, h, ws, bias, pidx, P);
 }
 
 // =====================================================================================
@@ -893,8 +924,18 @@ static void tm_fwd_cfg(int ntiles, const float* x, const float* W, const float* 
 
 template <int H, int KX, int GR, bool DZF, bool DXF, bool LAST>
 static void tm_bwd_cfg(int ntiles, const float* dh, const __bf16* g, const float* c, const float* W, const float* U,
-                       float* dx, __bf16* dz, int Mp, int T, int Din, int Dw, hipStream_t st) {
+                       float* dx, __bf16* dz, int Mp, int T, int Din, int Dw, hipStream_t st,
+                       const unsigned char* pidx = nullptr, int P = 0) {
   constexpr int D = H >= 64 ? 2 : 4;        // H = 64: 16 waves x 128 VGPRs, shorter state rings
+  if constexpr (!LAST && GR == 4) {
+    if (pidx != nullptr) {                  // un-pool on load (the pooled dh of a fused layer + pool)
+      hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST, false, true>), dim3(ntiles),
+                         dim3(TMC<H>::NT), 0, st, dh, g, c, W, U, dx, dz, Mp, T, Din, Dw, nullptr, nullptr, nullptr,
+                         pidx, P);
+      return;
+    }
+  }
+  TORCH_CHECK(pidx == nullptr, "lstm_tm_bwd: un-pooling takes a per-step gradient and 16-byte granules");
   hipLaunchKernelGGL((lstm_tm_bwd_kernel<H, KX, GR, D, DZF, DXF, LAST>), dim3(ntiles), dim3(TMC<H>::NT), 0, st, dh, g,
                      c, W, U, dx, dz, Mp, T, Din, Dw);
 }
@@ -1431,9 +1472,12 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
 // dh: [T, Mp, H] (or [Mp, H] when only the last step has a gradient). Returns dx [T, Mp, Din]
 // (empty if !need_dx) and accumulates dW, dU, db when they are non-empty. An empty g (the forward ran
 // with store_gates = false) selects the recompute-gates backward, which needs the bias b.
+// pidx / pool (optional): the layer's output went through MaxPooling1D(pool) and dh is the POOLED
+// gradient [T / pool, Mp, H] with the pool's byte argmax pidx (un-pooled on load, lstm_tm_bwd_body UP).
 at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tensor& c, const at::Tensor& x,
                        const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
-                       at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx) {
+                       at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx,
+                       const c10::optional<at::Tensor>& pidx_opt, int64_t pool) {
   const at::Tensor* ops[] = {&dh, &c, &x, &h, &W, &U, &b};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
   const bool rg = g.numel() == 0;
@@ -1442,8 +1486,18 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   const int Dw = (int)W.size(0);
   TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H && b.numel() == 4 * H, "lstm_tm_bwd: W / b shape");
   const bool last = dh.dim() == 2;
+  const bool up = pidx_opt.has_value() && pidx_opt->defined() && pidx_opt->numel() > 0;
+  const unsigned char* pidx = nullptr;
+  const int P = up ? (int)pool : 1;
+  if (up) {
+    TORCH_CHECK(!last && P >= 1 && P <= 255 && T / P >= 1, "lstm_tm_bwd: pool size 1..255 <= T, per-step gradient");
+    TORCH_CHECK(pidx_opt->is_cuda() && pidx_opt->scalar_type() == at::kByte && pidx_opt->is_contiguous() &&
+                    pidx_opt->sizes() == dh.sizes(), "lstm_tm_bwd: pidx must be a contiguous uint8 tensor shaped like dh");
+    pidx = pidx_opt->data_ptr<uint8_t>();
+  }
   TORCH_CHECK(last ? (dh.size(0) == Mp && dh.size(1) == H)
-                   : (dh.size(0) == T && dh.size(1) == Mp && dh.size(2) == H), "lstm_tm_bwd: dh shape");
+                   : (dh.size(0) == (up ? T / P : T) && dh.size(1) == Mp && dh.size(2) == H), "lstm_tm_bwd: dh shape");
+  TORCH_CHECK(dh.is_contiguous(), "lstm_tm_bwd: dh must be contiguous");
   TORCH_CHECK((rg || g.numel() == (long)(T + 1) * Mp * H * 4) && c.numel() == (long)(T + 1) * Mp * H &&
                   h.numel() == (long)T * Mp * H, "lstm_tm_bwd: saved state shapes");
   const bool wg = dW.numel() > 0;
@@ -1470,11 +1524,15 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, x.options()) : at::empty({0}, x.options());
     if (need_dx) TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 4 == 0 && h.is_contiguous(), "lstm_tm_bwd: h layout");
+#define GQ_TM_WG_CALL3(DXV, LASTV, RGV, UPV)                                                                   \
+  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV, RGV, UPV>),          \
+                     dim3(ntiles), dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), gptr, c.data_ptr<float>(),    \
+                     W.data_ptr<float>(), U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr,         \
+                     x.data_ptr<float>(), h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw,            \
+                     b.data_ptr<float>(), pidx, P)
 #define GQ_TM_WG_CALL2(DXV, LASTV, RGV)                                                                        \
-  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV, RGV>), dim3(ntiles), \
-                     dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), gptr, c.data_ptr<float>(), W.data_ptr<float>(), \
-                     U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr, x.data_ptr<float>(),         \
-                     h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw, b.data_ptr<float>())
+  do { if constexpr (!LASTV) { if (up) { GQ_TM_WG_CALL3(DXV, LASTV, RGV, true); break; } }                      \
+       GQ_TM_WG_CALL3(DXV, LASTV, RGV, false); } while (0)
 #define GQ_TM_WG_CALL(DXV, LASTV) \
   do { if (rg) GQ_TM_WG_CALL2(DXV, LASTV, true); else GQ_TM_WG_CALL2(DXV, LASTV, false); } while (0)
 #define GQ_TM_WG_KX(...)                                                                                        \
@@ -1491,6 +1549,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #undef GQ_TM_WG_KX
 #undef GQ_TM_WG_CALL
 #undef GQ_TM_WG_CALL2
+#undef GQ_TM_WG_CALL3
     GQ_LAUNCH_CHECK();
     lstm_grads_reduce_records(ws, H, Dw, ntiles, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), st);
     return need_dx ? dx.narrow(0, 0, T) : dx;
@@ -1506,7 +1565,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #define GQ_TM_BWD_CALL2(LASTV)                                                                              \
   tm_bwd_cfg<HH, KXX, GRR, true, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), \
                                               W.data_ptr<float>(), U.data_ptr<float>(), dx.data_ptr<float>(),  \
-                                              bf16_ptr(dz), Mp, T, Din, Dw, st)
+                                              bf16_ptr(dz), Mp, T, Din, Dw, st, pidx, P)
     GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
         if (last) GQ_TM_BWD_CALL2(true); else GQ_TM_BWD_CALL2(false))));
 #undef GQ_TM_BWD_CALL2
@@ -1517,7 +1576,9 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
                     rows * Din, Din, rows * Din, st);
     return dx.narrow(0, 0, T);
   }
+  TORCH_CHECK(!(up && wg && !need_dx), "lstm_tm_bwd: un-pooling without dx takes the fused kernels");
   if (wg) {
+    TORCH_CHECK(!up, "lstm_tm_bwd: un-pooling is not wired into the dz + weight-gradient pass path");
     // recurrence -> dz (bf16), then dW/dU/db (+ dx) in one pass over T*Mp rows
     at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));
     GQ_TM_H_DISPATCH(H,
@@ -1539,21 +1600,24 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
   TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
   if (rg) {      // frozen weights (integrated gradients), gates recomputed: H <= 32, GR = 4
-#define GQ_TM_RG_CALL(LASTV)                                                                                   \
-  hipLaunchKernelGGL((lstm_tm_bwd_kernel<HH, KXX, 4, 4, false, true, LASTV, true>), dim3(ntiles), dim3(TMC<HH>::NT), \
-                     0, st, dh.data_ptr<float>(), nullptr, c.data_ptr<float>(), W.data_ptr<float>(),              \
-                     U.data_ptr<float>(), dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, x.data_ptr<float>(),     \
-                     h.data_ptr<float>(), b.data_ptr<float>())
+#define GQ_TM_RG_CALL2(LASTV, UPV)                                                                             \
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<HH, KXX, 4, 4, false, true, LASTV, true, UPV>), dim3(ntiles),            \
+                     dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), nullptr, c.data_ptr<float>(),                 \
+                     W.data_ptr<float>(), U.data_ptr<float>(), dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw,     \
+                     x.data_ptr<float>(), h.data_ptr<float>(), b.data_ptr<float>(), pidx, P)
+#define GQ_TM_RG_CALL(LASTV) \
+  do { if constexpr (!LASTV) { if (up) { GQ_TM_RG_CALL2(LASTV, true); break; } } GQ_TM_RG_CALL2(LASTV, false); } while (0)
     GQ_TM2_H_DISPATCH(H, if ((Din + 31) / 32 == 1) { constexpr int KXX = 1; if (last) GQ_TM_RG_CALL(true); else GQ_TM_RG_CALL(false); }
                          else { constexpr int KXX = 2; if (last) GQ_TM_RG_CALL(true); else GQ_TM_RG_CALL(false); });
 #undef GQ_TM_RG_CALL
+#undef GQ_TM_RG_CALL2
     GQ_LAUNCH_CHECK();
     return dx.narrow(0, 0, T);
   }
 #define GQ_TM_BWD_CALL(LASTV)                                                                               \
   tm_bwd_cfg<HH, KXX, GRR, false, true, LASTV>(ntiles, dh.data_ptr<float>(), gptr,                 \
                                                c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), \
-                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st)
+                                               dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw, st, pidx, P)
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (last) GQ_TM_BWD_CALL(true); else GQ_TM_BWD_CALL(false))));
 #undef GQ_TM_BWD_CALL

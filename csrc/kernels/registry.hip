@@ -64,7 +64,7 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor(b!) rdU, Tensor(c!) rdb) -> Tensor");
   m.def("lstm_grads_job_ws(Tensor dz, Tensor x, Tensor W, int H) -> Tensor");
   m.def("lstm_tm_bwd(Tensor dh, Tensor g, Tensor c, Tensor x, Tensor h, Tensor W, Tensor U, Tensor b, Tensor(a!) dW, "
-        "Tensor(b!) dU, Tensor(c!) db, bool need_dx) -> Tensor");
+        "Tensor(b!) dU, Tensor(c!) db, bool need_dx, Tensor? pidx=None, int pool=0) -> Tensor");
   // fused GeneralConv + BatchNorm + PReLU + node pooling (gcn.hip)
   m.def("gcn_stats(Tensor x, Tensor mask) -> Tensor");
   m.def("gcn_pool_fwd(Tensor x, Tensor w, Tensor anom, Tensor W, Tensor b, Tensor scale, Tensor shift, "

@@ -100,7 +100,7 @@ class TimeLayer(nn.Module):
         rows past M; C may carry zero channels past the first layer's input width).
         Returns ``[M, out_features]``. Producers that can write this layout directly (the
         SoilNet GCN kernel) skip the transpose/pad copy of :meth:`_forward_tm`."""
-        from ..ops.lstm import _chain_on, lstm_chain_tm, lstm_layer_tm, lstm_pair_tm, tm_eligible
+        from ..ops.lstm import _chain_on, lstm_chain_tm, lstm_layer_tm, lstm_pair_tm, pool_fusion, tm_eligible
         from ..ops.pool import max_pool1d_tm
         tm = True
         seq = self._sequence()
@@ -116,15 +116,29 @@ class TimeLayer(nn.Module):
                 h = max_pool1d_tm(h, mod.pool_size) if tm else mod(h)
                 continue
             nxt = seq[i] if i < len(seq) else None
+
+            def fused_pool(j, units):
+                # a MaxPooling1D right after the layer(s): pooled inside their autograd node, and the
+                # backward recurrence un-pools the pooled gradient on load (no maxpool1d_bwd pass)
+                p = seq[j] if j < len(seq) else None
+                if (isinstance(p, MaxPooling1D) and pool_fusion() and units % 4 == 0 and h.shape[-1] % 4 == 0
+                        and 1 <= p.pool_size <= 255 and h.shape[0] // p.pool_size >= 1):
+                    return p.pool_size
+                return 0
+
             if (tm and isinstance(nxt, LSTM) and mod.return_sequences and nxt.return_sequences
                     and mod.units <= 32 and nxt.units == mod.units and nxt.kernel.shape[0] == mod.units and _pair_fusion()
                     and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16)
                     and nxt.activation == mod.activation and nxt.compute_bf16 == mod.compute_bf16):
                 i += 1
-                h = lstm_pair_tm(h, mod, nxt)      # two layers, one pipelined forward kernel
+                P = fused_pool(i, mod.units)
+                h = lstm_pair_tm(h, mod, nxt, P)   # two layers, one pipelined forward kernel
+                i += 1 if P else 0
                 continue
             if tm and tm_eligible(h, mod.units, h.shape[-1], mod.activation, mod.compute_bf16):
-                h = lstm_layer_tm(h, mod.kernel, mod.recurrent_kernel, mod.bias, mod.return_sequences)
+                P = fused_pool(i, mod.units) if mod.return_sequences else 0
+                h = lstm_layer_tm(h, mod.kernel, mod.recurrent_kernel, mod.bias, mod.return_sequences, P)
+                i += 1 if P else 0
                 if not mod.return_sequences:
                     return h[:M]
                 continue

@@ -660,7 +660,7 @@ class _HipLSTMTM(torch.autograd.Function):
     accumulated straight into the gradient buffers (direct mode) or returned."""
 
     @staticmethod
-    def forward(ctx, x, W, U, b, return_sequences: bool):
+    def forward(ctx, x, W, U, b, return_sequences: bool, pool: int = 0):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:4])
@@ -668,14 +668,16 @@ class _HipLSTMTM(torch.autograd.Function):
         h, g, c = hip_ops().lstm_tm_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need, sg)
         ctx.params = (W, U, b)
         ctx.return_sequences = return_sequences
+        out, idx = _pool_out(h, pool) if (pool and return_sequences) else (h, x.new_zeros(0, dtype=torch.uint8))
+        ctx.pool = int(pool) if return_sequences else 0
         if need:
-            ctx.save_for_backward(x, W, U, b, h, g, c)
-        return h if return_sequences else h[-1]
+            ctx.save_for_backward(x, W, U, b, h, g, c, idx)
+        return out if return_sequences else h[-1]
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
-        x, W, U, b, h, g, c = ctx.saved_tensors
+        x, W, U, b, h, g, c, idx = ctx.saved_tensors
         need = ctx.needs_input_grad
         wgrad = any(need[1:4])
         need_dx = bool(need[0])
@@ -687,13 +689,15 @@ class _HipLSTMTM(torch.autograd.Function):
             e = x.new_zeros(0)
             sinks = [(e, True)] * 3
         if wgrad and g.numel() > 0 and _pipe_on(sinks, x.shape[1]) and _pipe_x_ok(x, W.shape[0]):
+            dout = _unpool(dout, idx, ctx.pool, h.shape[0])
             dx = _pipe_tm_backward(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(), sinks, need_dx)
         else:
             with _deferred_reduce(wgrad and all(d for _, d in sinks)):
                 dx = hip_ops().lstm_tm_bwd(dout.contiguous(), g, c, x, h, W.contiguous(), U.contiguous(),
-                                           b.contiguous(), sinks[0][0], sinks[1][0], sinks[2][0], need_dx)
+                                           b.contiguous(), sinks[0][0], sinks[1][0], sinks[2][0], need_dx,
+                                           idx if ctx.pool else None, ctx.pool)
         grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
-        return (dx if need_dx else None, *grads, None)
+        return (dx if need_dx else None, *grads, None, None)
 
 
 class _HipLSTMTMPair(torch.autograd.Function):
@@ -704,7 +708,7 @@ class _HipLSTMTMPair(torch.autograd.Function):
     SIMD's MFMA pipe - and removed.)"""
 
     @staticmethod
-    def forward(ctx, x, WA, UA, bA, WB, UB, bB):
+    def forward(ctx, x, WA, UA, bA, WB, UB, bB, pool: int = 0):
         from ..utils.native import hip_ops
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:7])
@@ -713,15 +717,17 @@ class _HipLSTMTMPair(torch.autograd.Function):
             x, WA.contiguous(), UA.contiguous(), bA.contiguous(), WB.contiguous(), UB.contiguous(), bB.contiguous(),
             need, sg)
         ctx.params = (WA, UA, bA, WB, UB, bB)
+        out, idx = _pool_out(hB, pool) if pool else (hB, x.new_zeros(0, dtype=torch.uint8))
+        ctx.pool = int(pool)
         if need:
-            ctx.save_for_backward(x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB)
-        return hB
+            ctx.save_for_backward(x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB, idx)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
         from ..utils.native import hip_ops
         ops = hip_ops()
-        x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB = ctx.saved_tensors
+        x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB, idx = ctx.saved_tensors
         need = ctx.needs_input_grad
         e = x.new_zeros(0)
         dout = dout.contiguous()
@@ -738,23 +744,53 @@ class _HipLSTMTMPair(torch.autograd.Function):
         if (any(need[4:7]) and any(need[1:4]) and gA.numel() > 0 and _pipe_on(sB, x.shape[1])
                 and _pipe_on(sA, x.shape[1])
                 and _pipe_x_ok(x, WA.shape[0]) and _pipe_x_ok(hA, WB.shape[0])):
+            dout = _unpool(dout, idx, ctx.pool, hB.shape[0])
             dhA = _pipe_tm_backward(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), sB, True)
             dx = _pipe_tm_backward(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), sA, need_dx)
         else:
             with _deferred_reduce(all(d for _, d in sB) and all(d for _, d in sA)):
                 dhA = ops.lstm_tm_bwd(dout, gB, cB, hA, hB, WB.contiguous(), UB.contiguous(), bB.contiguous(),
-                                      sB[0][0], sB[1][0], sB[2][0], True)
+                                      sB[0][0], sB[1][0], sB[2][0], True, idx if ctx.pool else None, ctx.pool)
                 if need_dx or any(need[1:4]):
                     dx = ops.lstm_tm_bwd(dhA, gA, cA, x, hA, WA.contiguous(), UA.contiguous(), bA.contiguous(),
                                          sA[0][0], sA[1][0], sA[2][0], need_dx)
         gA_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sA, need[1:4])]
         gB_ = [None if (direct or not n) else buf for (buf, direct), n in zip(sB, need[4:7])]
-        return (dx if need_dx else None, *gA_, *gB_)
+        return (dx if need_dx else None, *gA_, *gB_, None)
 
 
-def lstm_pair_tm(x_tm, A, B) -> torch.Tensor:
-    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``)."""
-    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias)
+def _pool_out(h: torch.Tensor, pool: int):
+    """MaxPooling1D(pool) of a time-major [T, Mp, H] output inside a layer's autograd node: (pooled
+    [T // pool, Mp, H], byte argmax). The node's backward then takes the pooled gradient and the
+    recurrence un-pools it on load (``lstm_tm_bwd`` pidx)."""
+    from ..utils.native import hip_ops
+    T, Mp, H = h.shape
+    y, idx = hip_ops().maxpool1d_fwd(h.contiguous().view(1, T, Mp * H), int(pool))
+    return y.view(T // pool, Mp, H), idx.view(T // pool, Mp, H)
+
+
+def _unpool(dout: torch.Tensor, idx: torch.Tensor, pool: int, T: int) -> torch.Tensor:
+    """Full-resolution gradient of a fused pool (paths whose recurrence does not un-pool on load)."""
+    if not pool:
+        return dout
+    from ..utils.native import hip_ops
+    Ts, Mp, H = dout.shape
+    return hip_ops().maxpool1d_bwd(dout.contiguous().view(1, Ts, Mp * H), idx.view(1, Ts, Mp * H), T,
+                                   int(pool)).view(T, Mp, H)
+
+
+def pool_fusion() -> bool:
+    """Whether a MaxPooling1D after a time-major layer (pair) runs inside that layer's autograd node
+    with the un-pooling done by the recurrence's dh loads (``GNNQC_TM_POOL_FUSE=0``: separate pool)."""
+    import os
+    return os.environ.get("GNNQC_TM_POOL_FUSE", "1") == "1"
+
+
+def lstm_pair_tm(x_tm, A, B, pool: int = 0) -> torch.Tensor:
+    """Fused forward of two stacked LSTM modules (``gnnqc.models.layers.LSTM``), optionally followed
+    by MaxPooling1D(``pool``) in the same autograd node."""
+    return _HipLSTMTMPair.apply(x_tm, A.kernel, A.recurrent_kernel, A.bias, B.kernel, B.recurrent_kernel, B.bias,
+                                int(pool))
 
 
 def recompute_gates(x: torch.Tensor, H: int, weight_grads: bool) -> bool:
@@ -780,9 +816,10 @@ def tm_eligible(x: torch.Tensor, H: int, Din: int, activation: str = "tanh", bf1
 
 
 def lstm_layer_tm(x_tm: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
-                  return_sequences: bool = True) -> torch.Tensor:
-    """Time-major layer ``[T, Mp, Din] -> [T, Mp, H]`` (or the last step)."""
-    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences))
+                  return_sequences: bool = True, pool: int = 0) -> torch.Tensor:
+    """Time-major layer ``[T, Mp, Din] -> [T, Mp, H]`` (or the last step), optionally followed by
+    MaxPooling1D(``pool``) in the same autograd node."""
+    return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences), int(pool))
 
 
 def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,

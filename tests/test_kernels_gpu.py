@@ -439,6 +439,36 @@ def test_lstm_tm_recomputed_gates_match_saved_gates(cuda_device, monkeypatch, H,
     assert float(g1[0][:, M:].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("M,frozen", [(300, False), (700, False), (300, True)])
+def test_timelayer_fused_pool_unpool_on_load_matches_separate_pool(cuda_device, monkeypatch, M, frozen):
+    """MaxPooling1D fused into the preceding time-major layer (pair)'s autograd node, the backward
+    recurrence un-pooling the pooled gradient on load (lstm_tm_bwd pidx / pool), vs separate
+    maxpool1d kernels: same output, same input / weight gradients (identical arithmetic). ``frozen``:
+    input gradients only (the integrated-gradients path)."""
+    from gnnqc.models.timelayer import TimeLayer
+    torch.manual_seed(0)
+    tl = TimeLayer(20, 16, 2, "lstm", pool_size=3).to(cuda_device)
+    for p in tl.parameters():
+        p.requires_grad_(not frozen)
+    x = torch.randn(M, 181, 20, device=cuda_device)
+    monkeypatch.setenv("GNNQC_CHAIN", "0")
+
+    def run(fuse):
+        monkeypatch.setenv("GNNQC_TM_POOL_FUSE", "1" if fuse else "0")
+        xi = x.clone().requires_grad_(True)
+        for p in tl.parameters():
+            p.grad = None
+        out = tl(xi)
+        out.pow(2).sum().backward()
+        return out.detach(), [xi.grad.clone()] + [p.grad.clone() for p in tl.parameters() if p.requires_grad]
+
+    o0, g0 = run(False)
+    o1, g1 = run(True)
+    torch.testing.assert_close(o1, o0, atol=0, rtol=0)
+    for a, b_ in zip(g1, g0):
+        torch.testing.assert_close(a, b_, atol=1e-6 * (b_.abs().max().item() + 1e-6), rtol=1e-5)
+
+
 def test_timelayer_time_major_matches_sequence_major(cuda_device, monkeypatch):
     """The CML TimeLayer (LSTM 16,16 | pool | 32,32 | pool | 64,64 | pool | 128): time-major
     fused path vs the sequence-major kernels - forward and every parameter gradient."""
