@@ -1469,6 +1469,8 @@ at::Tensor lstm_tm_grads(const at::Tensor& dz, const at::Tensor& x, const at::Te
   return ncb == 1 ? dx[0] : dx.sum(0);
 }
 
+at::Tensor maxpool1d_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t T, int64_t p);   // pool.hip
+
 // dh: [T, Mp, H] (or [Mp, H] when only the last step has a gradient). Returns dx [T, Mp, Din]
 // (empty if !need_dx) and accumulates dW, dU, db when they are non-empty. An empty g (the forward ran
 // with store_gates = false) selects the recompute-gates backward, which needs the bias b.
@@ -1576,15 +1578,17 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
                     rows * Din, Din, rows * Din, st);
     return dx.narrow(0, 0, T);
   }
-  TORCH_CHECK(!(up && wg && !need_dx), "lstm_tm_bwd: un-pooling without dx takes the fused kernels");
   if (wg) {
-    TORCH_CHECK(!up, "lstm_tm_bwd: un-pooling is not wired into the dz + weight-gradient pass path");
-    // recurrence -> dz (bf16), then dW/dU/db (+ dx) in one pass over T*Mp rows
+    // recurrence -> dz (bf16), then dW/dU/db (+ dx) in one pass over T*Mp rows. (A pooled gradient
+    // is un-pooled to full resolution first: this path's recurrence is instantiated without UP.)
+    const at::Tensor dhf = up ? maxpool1d_bwd(dh.view({1, T / P, (long)Mp * H}), pidx_opt->view({1, T / P, (long)Mp * H}),
+                                              T, P).view({T, Mp, H})
+                              : dh;
     at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));
     GQ_TM_H_DISPATCH(H,
-        if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
+        if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dhf.data_ptr<float>(), bf16_ptr(g),
               c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st);
-        else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dh.data_ptr<float>(), bf16_ptr(g),
+        else tm_bwd_cfg<HH, 1, 1, true, false, false>(ntiles, dhf.data_ptr<float>(), bf16_ptr(g),
               c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st));
     GQ_LAUNCH_CHECK();
     const long rows = (long)T * Mp;
