@@ -207,12 +207,17 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
 // recurrence of T + 1 steps instead of two of T. Outputs and saved state are exactly those
 // of two lstm_tm_fwd_kernel launches (same bf16 operands, same accumulation order).
 // (The reference stacks time1/time2 and time_layers[2i]/[2i+1], libs/create_model.py:61-79.)
-template <int H, bool TRAIN, int KX, int GR, int D, bool SG = true>
+// PL: MaxPooling1D(P) of layer B's output in the same launch - the storer lanes of layer B keep a
+// running max + byte argmax of their h granule (PoolAcc) and write the pooled tile and its argmax
+// when a window closes (the maxpool1d_fwd pass over hB is gone; hB itself is still stored for the
+// backward)
+template <int H, bool TRAIN, int KX, int GR, int D, bool SG = true, bool PL = false>
 __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) void lstm_tm2_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ WA, const float* __restrict__ UA,
     const float* __restrict__ bA, const float* __restrict__ WB, const float* __restrict__ UB,
     const float* __restrict__ bB, float* __restrict__ hA, __bf16* __restrict__ gA, float* __restrict__ cA,
-    float* __restrict__ hB, __bf16* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw) {
+    float* __restrict__ hB, __bf16* __restrict__ gB, float* __restrict__ cB, int Mp, int T, int Din, int Dw,
+    int P = 0, float* __restrict__ pout = nullptr, unsigned* __restrict__ iout = nullptr) {
   using C = TMC<H>;
   static_assert(C::CPL == 1, "pair kernel: one cell per lane (H <= 64)");
   constexpr int NW = C::NW, NTL = C::NT, G4 = C::G4;
@@ -279,6 +284,9 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
   const size_t hstep = (size_t)Mp * H;
   __bf16* gbuf = layerB ? gB : gA;
   float* cbuf = layerB ? cB : cA;
+  PoolAcc pacc{};
+  const bool pooler = PL && layerB && wave_uniform(tl < n_gh);
+  const int To = PL ? T / P : 0;
 #pragma unroll
   for (int j = 0; j < D; ++j) xr[j].load(xbase + (size_t)min(j, T - 1) * xstep);
   __syncthreads();
@@ -301,6 +309,9 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
         const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][gh / H][gh % H]);
         *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+        if constexpr (PL) {
+          if (pooler && ts < T) pacc.step(v, ts, P, To, pout, iout, (size_t)row0 * H + gh, hstep);
+        }
       }
       f32x4_t accx = bias4, acch = {0.f, 0.f, 0.f, 0.f};   // independent MFMA chains
       if (layerB) {
@@ -1009,9 +1020,11 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
 
 // Pair forward (lstm_tm2_fwd_kernel): x [T, Mp, Din]; A: W [Dw <= Din, 4H], B: W [H, 4H].
 // Returns [hA, gA, cA, hB, gB, cB] with the layouts of lstm_tm_fwd.
+// pool > 0: MaxPooling1D(pool) of hB in the same launch; two more outputs [pooled (T/pool, Mp, H), argmax
+// bytes (same shape)]
 std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, const at::Tensor& UA,
                                      const at::Tensor& bA, const at::Tensor& WB, const at::Tensor& UB,
-                                     const at::Tensor& bB, bool train, bool store_gates) {
+                                     const at::Tensor& bB, bool train, bool store_gates, int64_t pool) {
   for (const at::Tensor* t : {&x, &WA, &UA, &bA, &WB, &UB, &bB}) check_f32_cuda(*t, "lstm_tm2_fwd operand");
   TORCH_CHECK(x.dim() == 3, "lstm_tm2_fwd: x must be [T, Mp, Din]");
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)UA.size(0);
@@ -1039,17 +1052,23 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   auto st = stream();
   __bf16* PG[2] = {sg ? bf16_ptr(gA) : nullptr, sg ? bf16_ptr(gB) : nullptr};
   float* P[4] = {nullptr, train ? cA.data_ptr<float>() : nullptr, nullptr, train ? cB.data_ptr<float>() : nullptr};
-#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, SGV)                                                                    \
-  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, SGV>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0, st,   \
-                     x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),        \
+  at::Tensor pooled, pidx;
+  const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
+#define GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, PLV)                                                              \
+  hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, SGV, PLV>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,  \
+                     st, x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),    \
                      WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), PG[0], \
-                     P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw)
+                     P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw, pl.P, pl.out, pl.idx)
+#define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, SGV)                                                                    \
+  do { if (pl.P > 0) GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, true); else GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, false); } \
+  while (0)
   GQ_TM2_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (sg) GQ_TM2_LAUNCH(HH, true, KXX, GRR, true); else if (train) GQ_TM2_LAUNCH(HH, true, KXX, GRR, false);
       else GQ_TM2_LAUNCH(HH, false, KXX, GRR, true))));
 #undef GQ_TM2_LAUNCH
+#undef GQ_TM2_LAUNCH2
   GQ_LAUNCH_CHECK();
-  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB};
+  return {hA.narrow(0, 0, T), gA, cA, hB.narrow(0, 0, T), gB, cB, pooled, pidx};
 }
 
 // ---- pipelined backward (see lstm_tm_bwd_dual_kernel)

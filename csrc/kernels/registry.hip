@@ -30,7 +30,7 @@ TORCH_LIBRARY(gnnqc, m) {
   // time-major LSTM with fused backward (lstm_tm.hip)
   m.def("lstm_tm_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train, bool store_gates=True) -> Tensor[]");
   m.def("lstm_tm2_fwd(Tensor x, Tensor WA, Tensor UA, Tensor bA, Tensor WB, Tensor UB, Tensor bB, "
-        "bool train, bool store_gates=True) -> Tensor[]");
+        "bool train, bool store_gates=True, int pool=0) -> Tensor[]");
   m.def("lstm_tm_grads(Tensor dz, Tensor x, Tensor h, Tensor W, Tensor(a!) dW, Tensor(b!) dU, Tensor(c!) db, "
         "bool need_dx) -> Tensor");
   m.def("lstm_dx(Tensor dz, Tensor W, Tensor like) -> Tensor");

@@ -713,11 +713,16 @@ class _HipLSTMTMPair(torch.autograd.Function):
         x = x.contiguous()
         need = any(ctx.needs_input_grad[:7])
         sg = not recompute_gates(x, UA.shape[0], any(ctx.needs_input_grad[1:7]))
-        hA, gA, cA, hB, gB, cB = hip_ops().lstm_tm2_fwd(
+        import os
+        kp = int(pool) if (pool and os.environ.get("GNNQC_TM_POOL_IN_FWD", "1") == "1") else 0
+        hA, gA, cA, hB, gB, cB, pooled, pidx = hip_ops().lstm_tm2_fwd(
             x, WA.contiguous(), UA.contiguous(), bA.contiguous(), WB.contiguous(), UB.contiguous(), bB.contiguous(),
-            need, sg)
+            need, sg, kp)
         ctx.params = (WA, UA, bA, WB, UB, bB)
-        out, idx = _pool_out(hB, pool) if pool else (hB, x.new_zeros(0, dtype=torch.uint8))
+        if kp:                            # pooled by layer B's storer lanes in the same launch
+            out, idx = pooled, pidx
+        else:
+            out, idx = _pool_out(hB, pool) if pool else (hB, x.new_zeros(0, dtype=torch.uint8))
         ctx.pool = int(pool)
         if need:
             ctx.save_for_backward(x, WA, UA, bA, hA, gA, cA, WB, UB, bB, hB, gB, cB, idx)

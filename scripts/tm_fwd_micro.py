@@ -26,7 +26,7 @@ def main():
             WA, UA = torch.randn(Din, 4 * H, device=dev) * 0.2, torch.randn(H, 4 * H, device=dev) * 0.2
             WB, UB = torch.randn(H, 4 * H, device=dev) * 0.2, torch.randn(H, 4 * H, device=dev) * 0.2
             b = torch.zeros(4 * H, device=dev)
-            for name, fn in (("pair", lambda: ops.lstm_tm2_fwd(x, WA, UA, b, WB, UB, b, True)),
+            for name, fn in (("pair", lambda: ops.lstm_tm2_fwd(x, WA, UA, b, WB, UB, b, True)[:6]),
                              ("single", lambda: ops.lstm_tm_fwd(x, WA, UA, b, True))):
                 for _ in range(2):
                     fn()

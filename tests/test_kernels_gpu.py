@@ -469,6 +469,25 @@ def test_timelayer_fused_pool_unpool_on_load_matches_separate_pool(cuda_device, 
         torch.testing.assert_close(a, b_, atol=1e-6 * (b_.abs().max().item() + 1e-6), rtol=1e-5)
 
 
+@pytest.mark.parametrize("H,P,T", [(16, 3, 181), (32, 3, 60), (16, 2, 37), (32, 1, 12)])
+def test_lstm_tm2_fwd_in_kernel_pool_matches_maxpool(cuda_device, H, P, T):
+    """MaxPooling1D(P) of layer B's output by the pair kernel's storer lanes (lstm_tm2_fwd pool=P)
+    == maxpool1d_fwd over the stored hB: pooled values and argmax bytes, bitwise; hA / hB unchanged."""
+    from gnnqc.utils.native import hip_ops
+    ops = hip_ops()
+    gen = torch.Generator().manual_seed(H * 10 + P + T)
+    Mp, Din = 48, 20
+    x = torch.randn(T, Mp, Din, generator=gen).to(cuda_device)
+    WA, UA, bA = _lstm_params(Din, H, gen, cuda_device)
+    WB, UB, bB = _lstm_params(H, H, gen, cuda_device)
+    r0 = ops.lstm_tm2_fwd(x, WA, UA, bA, WB, UB, bB, True, False, 0)
+    r1 = ops.lstm_tm2_fwd(x, WA, UA, bA, WB, UB, bB, True, False, P)
+    assert torch.equal(r0[0], r1[0]) and torch.equal(r0[3], r1[3])
+    ref, ridx = ops.maxpool1d_fwd(r0[3].contiguous().view(1, T, Mp * H), P)
+    assert torch.equal(r1[6].view(1, T // P, Mp * H), ref)
+    assert torch.equal(r1[7].view(1, T // P, Mp * H), ridx)
+
+
 def test_timelayer_time_major_matches_sequence_major(cuda_device, monkeypatch):
     """The CML TimeLayer (LSTM 16,16 | pool | 32,32 | pool | 64,64 | pool | 128): time-major
     fused path vs the sequence-major kernels - forward and every parameter gradient."""
