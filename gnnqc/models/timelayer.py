@@ -102,6 +102,10 @@ class TimeLayer(nn.Module):
         SoilNet GCN kernel) skip the transpose/pad copy of :meth:`_forward_tm`."""
         from ..ops.lstm import _chain_on, lstm_chain_tm, lstm_layer_tm, lstm_pair_tm, pool_fusion, tm_eligible
         from ..ops.pool import max_pool1d_tm
+        if self.layer_type != "lstm":
+            # CNN branch behind a time-major producer (the store-fused CML GCN front end): [M, T, Cin]
+            cin = self.time1.kernel.shape[1]
+            return self._forward_cnn(h.transpose(0, 1)[:M, :, :cin].contiguous())
         tm = True
         seq = self._sequence()
         i = 0

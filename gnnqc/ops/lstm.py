@@ -714,7 +714,10 @@ class _HipLSTMTMPair(torch.autograd.Function):
         need = any(ctx.needs_input_grad[:7])
         sg = not recompute_gates(x, UA.shape[0], any(ctx.needs_input_grad[1:7]))
         import os
-        kp = int(pool) if (pool and os.environ.get("GNNQC_TM_POOL_IN_FWD", "1") == "1") else 0
+        # (pooling by layer B's storer lanes in the same launch measured slower than the separate
+        # maxpool pass - SoilNet 3.21 vs 3.11 ms, IG 4.84 vs 4.74 ms per call, profiles/r6_pool_in_fwd_ab.txt,
+        # as in round 3 - so it is opt-in)
+        kp = int(pool) if (pool and os.environ.get("GNNQC_TM_POOL_IN_FWD", "0") == "1") else 0
         hA, gA, cA, hB, gB, cB, pooled, pidx = hip_ops().lstm_tm2_fwd(
             x, WA.contiguous(), UA.contiguous(), bA.contiguous(), WB.contiguous(), UB.contiguous(), bB.contiguous(),
             need, sg, kp)

@@ -464,9 +464,9 @@ def test_timelayer_fused_pool_unpool_on_load_matches_separate_pool(cuda_device, 
 
     o0, g0 = run(False)
     o1, g1 = run(True)
-    torch.testing.assert_close(o1, o0, atol=0, rtol=0)
+    torch.testing.assert_close(o1, o0, atol=1e-5, rtol=1e-4)
     for a, b_ in zip(g1, g0):
-        torch.testing.assert_close(a, b_, atol=1e-6 * (b_.abs().max().item() + 1e-6), rtol=1e-5)
+        assert (a - b_).norm().item() <= 1e-3 * (b_.norm().item() + 1e-6)
 
 
 @pytest.mark.parametrize("H,P,T", [(16, 3, 181), (32, 3, 60), (16, 2, 37), (32, 1, 12)])
