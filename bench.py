@@ -146,10 +146,14 @@ def measure_ig(args, trainer, dev, world, rank, D):
     them. Aggregate explained windows/s over the max-over-ranks time."""
     from gnnqc.xai.ig import IntegratedGradients
     gpu = dev.type == "cuda"
-    B = args.ig_windows or (256 if gpu else 4)
+    max_rows = 32768
+    # windows per call: one full path chunk (max_rows // (m_steps + 1) = 324 windows x 101 points = 2,046
+    # sixteen-sequence tiles, whole rounds of the recurrence grids; 256 windows leave a 16 % tail round,
+    # profiles/r6_ig_windows_per_call.txt)
+    B = args.ig_windows or (max_rows // 101 if gpu else 4)
     nb = args.ig_calls or (6 if gpu else 1)
     store, model = trainer.store, trainer.model
-    expl = IntegratedGradients(model, "cml", m_steps=100, max_rows=32768)
+    expl = IntegratedGradients(model, "cml", m_steps=100, max_rows=max_rows)
     span = max(1, store.n_windows - B)
 
     def ig_batch(j):                  # this rank's j-th batch = global batch rank + world * j
@@ -375,7 +379,7 @@ def main(argv=None):
                     help="skip the integrated-gradients throughput (BASELINE.json config v; reported as 'ig' in "
                          "the JSON line; under DP every rank explains its own shard of the batches)")
     ap.add_argument("--ig-windows", type=int, default=None,
-                    help="windows per attribute() call (default 256 on a GPU, 4 on the CPU)")
+                    help="windows per attribute() call (default 324 = one 32768-row path chunk on a GPU, 4 on the CPU)")
     ap.add_argument("--ig-calls", type=int, default=None,
                     help="timed attribute() calls per rank (default 6 on a GPU, 1 on the CPU)")
     ap.add_argument("--no-cv-line", dest="cv_line", action="store_false",
