@@ -34,63 +34,104 @@ struct ConvArgs {
   float a_scale;       // multiplier of A (1/T for the GAP backward)
   int bcast;           // A rows indexed by sequence only (GAP backward)
   float inv_T;
+  int wflip;           // W is the FORWARD layer's [k][Cout][Cin] (p.Cin / p.Cout swapped): read it as
+                       // flip(0).transpose(1, 2), the dx pass's weights, without materialising them
 };
 
-template <int NT>      // NT = ceil(Cout / 16) output tiles
+// NT = output tiles of 16 columns per workgroup (grid.y splits Cout into groups of NT tiles when the
+// row tiles alone would leave the chip idle). GATE: the A loads form dy * leaky'(y) (dx pass); the
+// forward skips the second load.
+// Index math is table-driven: per tile the 64 rows' (sequence start, t) and per K chunk the columns'
+// (tap, channel) go to LDS once, so the gather loop has no integer division; each wave gathers its 16
+// rows with the lanes on consecutive K columns (consecutive channels of one tap: contiguous loads).
+template <int NT, bool GATE>
 __global__ __launch_bounds__(256) void conv1d_fwd_kernel(ConvArgs p) {
   extern __shared__ __attribute__((aligned(16))) __bf16 smem[];
   const int Kp = p.Kp, KCH = p.KCH, LD = KCH + CV_PAD;
-  __bf16* Wt = smem;                          // [NT*16][LD]   W^T chunk
-  __bf16* As = smem + NT * 16 * LD;           // [CV_RT][LD]   im2col chunk
+  constexpr int NTC = NT * 16;                    // output columns of this workgroup
+  __bf16* Wt = smem;                              // [NTC][LD]   W^T chunk
+  __bf16* As = smem + NTC * LD;                   // [CV_RT][LD] im2col chunk
+  int* rinfo = reinterpret_cast<int*>(As + CV_RT * LD);      // [CV_RT]: sequence start row | -1 past rows
+  int* tinfo = rinfo + CV_RT;                                 // [CV_RT]: t
+  int* minfo = tinfo + CV_RT;                                 // [CV_RT]: sequence
+  int* kinfo = minfo + CV_RT;                                 // [KCH]: (tap << 16) | channel, -1 past K
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, quad = lane >> 4;
   const int KC = p.k * p.Cin;
-  const int nch = (Kp + KCH - 1) / KCH;       // kernel-uniform
+  const int nch = (Kp + KCH - 1) / KCH;           // kernel-uniform
+  const int n0 = blockIdx.y * NTC;                // first output column of this workgroup
 
   float bias[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    const int n = 16 * nt + col;
+    const int n = n0 + 16 * nt + col;
     bias[nt] = p.bias != nullptr ? p.bias[min(n, p.Cout - 1)] : 0.f;
   }
 
   const long ntiles = (p.rows + CV_RT - 1) / CV_RT;
-  bool w_staged = false;
+  bool staged = false;
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const long r0 = tile * CV_RT;
     f32x4_t acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();                              // previous tile's reads of the tables are done
+    if (tid < CV_RT) {
+      const long r = r0 + tid;
+      const long rc = min(r, p.rows - 1);
+      const long m = rc / p.T;
+      rinfo[tid] = r < p.rows ? (int)(m * p.T) : -1;
+      tinfo[tid] = (int)(rc - m * p.T);
+      minfo[tid] = (int)m;
+    }
     for (int ch = 0; ch < nch; ++ch) {
       const int k0 = ch * KCH;
-      __syncthreads();   // previous chunk / tile reads of As (and Wt) are done
-      if (!w_staged) {   // W^T chunk: Wt[n][kk - k0] = W[tap][i][n]  (zero padded); once if resident
-        for (int e = tid; e < NT * 16 * KCH; e += 256) {
-          const int n = e / KCH, kk = k0 + e % KCH;
-          const float m_ = (n < p.Cout && kk < KC) ? 1.f : 0.f;
-          const float v = p.W[(size_t)min(kk, KC - 1) * p.Cout + min(n, p.Cout - 1)];
-          Wt[n * LD + (kk - k0)] = (__bf16)(v * m_);
+      __syncthreads();                            // previous chunk's reads of As / Wt / kinfo are done
+      if (!staged) {
+        for (int kk = tid; kk < KCH; kk += 256) {
+          const int kg = k0 + kk;
+          const int tap = kg / p.Cin;
+          kinfo[kk] = kg < KC ? ((tap << 16) | (kg - tap * p.Cin)) : -1;
         }
-        w_staged = nch == 1;
+        // W^T chunk: Wt[n][kk] = W[k0 + kk][n0 + n] (zero padded); consecutive threads read
+        // consecutive output columns (coalesced); once per workgroup when K fits one chunk
+        for (int e = tid; e < NTC * KCH; e += 256) {
+          const int n = e % NTC, kk = e / NTC;      // (NTC: a power of two)
+          const int kg = k0 + kk, ng = n0 + n;
+          const float m_ = (ng < p.Cout && kg < KC) ? 1.f : 0.f;
+          const int kc = min(kg, KC - 1), nc = min(ng, p.Cout - 1);
+          size_t wi = (size_t)kc * p.Cout + nc;
+          if (p.wflip) {                            // W_fwd[k - 1 - tap][nc][i] ([k][Cout_fwd = p.Cin][Cin_fwd = p.Cout])
+            const int tap = kc / p.Cin, i = kc - tap * p.Cin;
+            wi = ((size_t)(p.k - 1 - tap) * p.Cout + nc) * p.Cin + i;
+          }
+          Wt[n * LD + kk] = (__bf16)(p.W[wi] * m_);
+        }
+        staged = nch == 1;
       }
-      // ---- im2col A chunk [64][KCH]
-      for (int e = tid; e < CV_RT * KCH; e += 256) {
-        const int rr = e / KCH, kk = k0 + e % KCH;
-        const long r = r0 + rr;
-        const long rc = min(r, p.rows - 1);
-        const long m = rc / p.T;
-        const int t = (int)(rc - m * p.T);
-        const int tap = kk / p.Cin, i = kk - tap * p.Cin;
-        const int ts = t + tap - p.left;
-        const bool ok = r < p.rows && kk < KC && ts >= 0 && ts < p.T;
-        const int tsc = min(max(ts, 0), p.T - 1);
-        const int ic = min(i, p.Cin - 1);
-        const long src = p.bcast ? m : m * p.T + tsc;
-        // unconditional loads (the forward passes gate = x with slope 1): no branch around VMEM
-        const float v = p.a[(size_t)src * p.lda + ic];
-        const float gy = p.gate[(size_t)(m * p.T + tsc) * p.Cin + ic];
-        As[rr * LD + (kk - k0)] = (__bf16)(ok ? v * (gy > 0.f ? 1.f : p.gate_alpha) * p.a_scale : 0.f);
+      __syncthreads();
+      // ---- im2col A chunk: wave w gathers rows 16w .. 16w+15, lanes on K columns
+      for (int kb = 0; kb < KCH; kb += 64) {
+        const int kk = kb + lane;
+        const int ki = kk < KCH ? kinfo[kk] : -1;
+        const int tap = ki >> 16, ic = ki & 0xffff;
+#pragma unroll 4
+        for (int r = 0; r < 16; ++r) {
+          const int rr = 16 * w + r;
+          const int rb = rinfo[rr], t = tinfo[rr];  // (LDS broadcast)
+          const int ts = t + tap - p.left;
+          const bool ok = ki >= 0 && rb >= 0 && ts >= 0 && ts < p.T;
+          const int tsc = min(max(ts, 0), p.T - 1);
+          const long src = p.bcast ? (long)minfo[rr] : (long)(rb >= 0 ? rb : 0) + tsc;
+          const int icc = ki >= 0 ? ic : 0;
+          float v = p.a[(size_t)src * p.lda + icc];
+          if constexpr (GATE) {
+            const float gy = p.gate[((size_t)(rb >= 0 ? rb : 0) + tsc) * p.Cin + icc];
+            v *= (gy > 0.f ? 1.f : p.gate_alpha) * p.a_scale;
+          }
+          if (kk < KCH) As[rr * LD + kk] = (__bf16)(ok ? v : 0.f);
+        }
       }
       __syncthreads();
       const int kw = min(KCH, Kp - k0);
@@ -103,12 +144,12 @@ __global__ __launch_bounds__(256) void conv1d_fwd_kernel(ConvArgs p) {
         }
       }
     }
-    // ---- epilogue: lane holds rows 16w + 4quad + q of column 16nt + col
+    // ---- epilogue: lane holds rows 16w + 4quad + q of column n0 + 16nt + col
     const long rb = r0 + 16 * w + 4 * quad;
     const long m_first = min(rb, p.rows - 1) / p.T, m_last = min(rb + 3, p.rows - 1) / p.T;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int n = 16 * nt + col;
+      const int n = n0 + 16 * nt + col;
       float gs = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -137,8 +178,13 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
                                                             const float* __restrict__ x, float* __restrict__ dW,
                                                             float* __restrict__ db, long rows, int T, int Cin,
                                                             int Cout, int k, int left, float alpha, int gap) {
+  constexpr int KT = DT * 16;
   __shared__ __attribute__((aligned(16))) __bf16 dzT[64][CW_LD];
-  __shared__ __attribute__((aligned(16))) __bf16 xT[DT * 16][CW_LD];
+  __shared__ __attribute__((aligned(16))) __bf16 xT[KT][CW_LD];
+  // index tables (no integer division in the staging loops): per im2col column (tap << 16 | channel;
+  // -2 = the ones row of db, -1 = padding), per tile row (sequence start row, t, sequence)
+  __shared__ int kinfo[KT];
+  __shared__ int rbase[CW_RT], tinf[CW_RT], minf[CW_RT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, quad = lane >> 4;
@@ -146,34 +192,46 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
   const int KC = k * Cin;
   const long ntiles = (rows + CW_RT - 1) / CW_RT;
   const float inv_T = 1.f / (float)T;
+  for (int kk = tid; kk < KT; kk += 256) {
+    const int tap = kk / Cin;
+    kinfo[kk] = kk < KC ? ((tap << 16) | (kk - tap * Cin)) : (kk == KC ? -2 : -1);
+  }
   f32x4_t acc[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   for (long tile = blockIdx.y; tile < ntiles; tile += gridDim.y) {
     const long r0 = tile * CW_RT;
-    for (int e = tid; e < CW_RT * 64; e += 256) {
-      const int rr = e / 64, oo = e % 64;
-      const long r = r0 + rr;
-      const long rc = min(r, rows - 1);
-      const int o = min(o0 + oo, Cout - 1);
-      const float gy = y[(size_t)rc * Cout + o];
-      const float d = dy[(size_t)(gap ? rc / T : rc) * Cout + o] * (gap ? inv_T : 1.f);
-      const bool ok = r < rows && o0 + oo < Cout;
-      dzT[oo][rr] = (__bf16)(ok ? d * (gy > 0.f ? 1.f : alpha) : 0.f);
-    }
-    for (int e = tid; e < CW_RT * DT * 16; e += 256) {
-      const int rr = e / (DT * 16), kk = e % (DT * 16);
-      const long r = r0 + rr;
+    __syncthreads();                              // previous tile's reads of the images / tables
+    if (tid < CW_RT) {
+      const long r = r0 + tid;
       const long rc = min(r, rows - 1);
       const long m = rc / T;
-      const int t = (int)(rc - m * T);
-      const int tap = kk / Cin, i = kk - tap * Cin;
+      rbase[tid] = r < rows ? (int)(m * T) : -1;
+      tinf[tid] = (int)(rc - m * T);
+      minf[tid] = (int)m;
+    }
+    __syncthreads();
+    for (int e = tid; e < CW_RT * 64; e += 256) {
+      const int rr = e >> 6, oo = e & 63;
+      const int rb = rbase[rr];
+      const long rc = rb >= 0 ? (long)rb + tinf[rr] : 0;
+      const int o = min(o0 + oo, Cout - 1);
+      const float gy = y[(size_t)rc * Cout + o];
+      const float d = dy[(size_t)(gap ? minf[rr] : rc) * Cout + o] * (gap ? inv_T : 1.f);
+      const bool ok = rb >= 0 && o0 + oo < Cout;
+      dzT[oo][rr] = (__bf16)(ok ? d * (gy > 0.f ? 1.f : alpha) : 0.f);
+    }
+    for (int e = tid; e < CW_RT * KT; e += 256) {
+      const int kk = e % KT, rr = e / KT;         // (KT: compile-time)
+      const int ki = kinfo[kk];
+      const int rb = rbase[rr], t = tinf[rr];
+      const int tap = ki >> 16, i = ki & 0xffff;
       const int ts = t + tap - left;
       const int tsc = min(max(ts, 0), T - 1);
-      const float v = x[(size_t)(m * T + tsc) * Cin + min(i, Cin - 1)];
-      const bool ok = r < rows && kk < KC && ts >= 0 && ts < T;
-      xT[kk][rr] = (__bf16)(ok ? v : ((kk == KC && r < rows) ? 1.f : 0.f));
+      const float v = x[((size_t)(rb >= 0 ? rb : 0) + tsc) * Cin + (ki >= 0 ? i : 0)];
+      const bool ok = rb >= 0 && ki >= 0 && ts >= 0 && ts < T;
+      xT[kk][rr] = (__bf16)(ok ? v : ((ki == -2 && rb >= 0) ? 1.f : 0.f));
     }
     __syncthreads();
     const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&dzT[16 * w + col][8 * quad]);
@@ -182,7 +240,6 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
       const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&xT[16 * d + col][8 * quad]);
       acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[d], 0, 0, 0);
     }
-    __syncthreads();
   }
   // flush: lane holds o = o0 + 16w + 4quad + q, kk = 16d + col
 #pragma unroll
@@ -207,7 +264,9 @@ static int conv_ntp(int Cout) {
   return NT <= 1 ? 1 : NT <= 2 ? 2 : NT <= 4 ? 4 : 8;
 }
 
-static size_t conv_lds(int NTp, int KCH) { return (size_t)(NTp * 16 + CV_RT) * (KCH + CV_PAD) * sizeof(__bf16); }
+static size_t conv_lds(int NTp, int KCH) {
+  return (size_t)(NTp * 16 + CV_RT) * (KCH + CV_PAD) * sizeof(__bf16) + (3 * CV_RT + KCH) * sizeof(int);
+}
 
 // K chunk: all of K (W^T resident) when it fits 80 KB (two workgroups per CU), else the
 // largest multiple of 32 that does
@@ -222,25 +281,32 @@ bool conv1d_supported(int k, int Cin, int Cout) {
   return k >= 1 && Cin >= 1 && Cout >= 1 && Cout <= 128 && Cin <= 128 && (k * Cin + 1 + 15) / 16 <= 24;
 }
 
-static void launch_conv_fwd(ConvArgs& a) {
-  const int NTp = conv_ntp(a.Cout);
-  a.KCH = conv_kch(NTp, a.Kp);
-  const size_t lds = conv_lds(NTp, a.KCH);
+static void launch_conv_fwd(ConvArgs& a, bool gate) {
+  const int NT = conv_ntp(a.Cout);
   const long ntiles = (a.rows + CV_RT - 1) / CV_RT;
+  // few row tiles (the deep, short layers): split the output columns over grid.y so the launch has
+  // enough workgroups (each gathers the same A tile, small next to the idle chip it fills)
+  int NTW = NT;
+  while (NTW > 1 && ntiles * (NT / NTW) < 256) NTW /= 2;
+  a.KCH = conv_kch(NTW, a.Kp);
+  const size_t lds = conv_lds(NTW, a.KCH);
   const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024) / lds)));
-  const int grid = (int)std::max<long>(1, std::min<long>(ntiles, 256L * per_cu));
+  const int gx = (int)std::max<long>(1, std::min<long>(ntiles, 256L * per_cu / (NT / NTW)));
+  dim3 grid(gx, NT / NTW);
   auto st = stream();
-#define GQ_CV_NT(N)                                                                                  \
-  case N:                                                                                            \
+#define GQ_CV_NT(N, G)                                                                               \
+  {                                                                                                  \
     if (lds > 64 * 1024)                                                                             \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1d_fwd_kernel<N>),                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1d_fwd_kernel<N, G>),             \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
-    hipLaunchKernelGGL(conv1d_fwd_kernel<N>, dim3(grid), dim3(256), lds, st, a);                     \
-    break;
-  switch (NTp) {
-    GQ_CV_NT(1) GQ_CV_NT(2) GQ_CV_NT(4) GQ_CV_NT(8)
+    hipLaunchKernelGGL((conv1d_fwd_kernel<N, G>), grid, dim3(256), lds, st, a);                      \
+  }
+#define GQ_CV_G(N) case N: if (gate) GQ_CV_NT(N, true) else GQ_CV_NT(N, false) break;
+  switch (NTW) {
+    GQ_CV_G(1) GQ_CV_G(2) GQ_CV_G(4) GQ_CV_G(8)
     default: TORCH_CHECK(false, "conv1d: Cout too large");
   }
+#undef GQ_CV_G
 #undef GQ_CV_NT
   GQ_LAUNCH_CHECK();
 }
@@ -270,7 +336,7 @@ std::vector<at::Tensor> conv1d_fwd(const at::Tensor& x, const at::Tensor& W, con
   a.rows = (long)M * T;
   a.T = T; a.Cin = Cin; a.Cout = Cout; a.k = k; a.left = (k - 1) / 2; a.lda = Cin; a.Kp = conv_kp(k, Cin);
   a.alpha = (float)alpha; a.gate_alpha = 1.f; a.a_scale = 1.f; a.bcast = 0; a.inv_T = 1.f / (float)T;
-  launch_conv_fwd(a);
+  launch_conv_fwd(a, false);
   return {y, g};
 }
 
@@ -317,12 +383,14 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
     GQ_LAUNCH_CHECK();
   }
   if (need_dx) {
-    // dx = conv_same(dz, Wf) with Wf[tap'][o][i] = W[k-1-tap'][i][o] and left' = k-1-left
-    at::Tensor Wf = W.flip(0).transpose(1, 2).contiguous();
+    // dx = conv_same(dz, Wf) with Wf[tap'][o][i] = W[k-1-tap'][i][o] and left' = k-1-left (read in place:
+    // wflip)
+    const at::Tensor Wc = W.contiguous();
     ConvArgs a{};
     a.a = dy.data_ptr<float>();
     a.gate = y.data_ptr<float>();
-    a.W = Wf.data_ptr<float>();
+    a.W = Wc.data_ptr<float>();
+    a.wflip = 1;
     a.bias = nullptr;
     a.y = dx.data_ptr<float>();
     a.g = nullptr;
@@ -331,7 +399,7 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
     a.Kp = conv_kp(k, Cout);
     a.alpha = 1.f; a.gate_alpha = (float)alpha; a.a_scale = gap ? 1.f / (float)T : 1.f; a.bcast = gap ? 1 : 0;
     a.inv_T = 1.f / (float)T;
-    launch_conv_fwd(a);
+    launch_conv_fwd(a, true);
   }
   return dx;
 }

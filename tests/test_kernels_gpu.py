@@ -524,7 +524,7 @@ def test_timelayer_time_major_matches_sequence_major(cuda_device, monkeypatch):
 
 @pytest.mark.parametrize("k,cin,cout,T,gap", [(5, 18, 16, 181, False), (3, 16, 32, 60, False), (5, 32, 64, 20, False),
                                               (5, 64, 128, 6, True), (1, 7, 16, 13, False), (4, 16, 16, 9, True),
-                                              (7, 3, 24, 50, False)])
+                                              (7, 3, 24, 50, False), (3, 120, 128, 40, False), (3, 120, 100, 300, True)])
 def test_conv1d_act_matches_eager(cuda_device, k, cin, cout, T, gap):
     """Fused Conv1D(same)+LeakyReLU(+GAP) HIP kernels vs fp64 eager: output, dx, dW, db."""
     from gnnqc.ops.conv import conv1d_act, conv1d_act_eager, hip_conv_supported
