@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256) void conv1d_fwd_kernel(ConvArgs p) {
         const int kk = kb + lane;
         const int ki = kk < KCH ? kinfo[kk] : -1;
         const int tap = ki >> 16, ic = ki & 0xffff;
-#pragma unroll 4
+        // (fully unrolled: the 16 rows' loads are in flight together; the gather is latency-bound)
+#pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rr = 16 * w + r;
           const int rb = rinfo[rr], t = tinfo[rr];  // (LDS broadcast)
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
       minf[tid] = (int)m;
     }
     __syncthreads();
+#pragma unroll
     for (int e = tid; e < CW_RT * 64; e += 256) {
       const int rr = e >> 6, oo = e & 63;
       const int rb = rbase[rr];
@@ -222,6 +224,7 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
       const bool ok = rb >= 0 && o0 + oo < Cout;
       dzT[oo][rr] = (__bf16)(ok ? d * (gy > 0.f ? 1.f : alpha) : 0.f);
     }
+#pragma unroll 6
     for (int e = tid; e < CW_RT * KT; e += 256) {
       const int kk = e % KT, rr = e / KT;         // (KT: compile-time)
       const int ki = kinfo[kk];
@@ -364,7 +367,10 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
     const int DT = (k * Cin + 1 + 15) / 16;
     const long ntiles = (rows + CW_RT - 1) / CW_RT;
     const int ncb = (Cout + 63) / 64;
-    const int splits = deterministic_mode() ? 1 : (int)std::max<long>(1, std::min<long>(ntiles, 256 / ncb));
+    // splits: every split flushes its whole dW^T tile with atomics, and all splits hit the same
+    // addresses, so the L2 atomic unit serialises them (256 splits: 40-55 us per call, the flush not the
+    // math); 64 keeps the tiles per split small and the contention a quarter
+    const int splits = deterministic_mode() ? 1 : (int)std::max<long>(1, std::min<long>(ntiles, 64 / ncb));
     dim3 grid(ncb, splits);
     auto st = stream();
     switch (DT) {
