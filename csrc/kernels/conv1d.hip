@@ -174,10 +174,14 @@ __global__ __launch_bounds__(256) void conv1d_fwd_kernel(ConvArgs p) {
 constexpr int CW_RT = 32;
 constexpr int CW_LD = CW_RT + 8;
 
+// Each split (grid.y) leaves its partial dW^T | db tile in ws[split][CoutP][KT] with plain stores;
+// conv1d_wgrad_reduce_kernel sums the splits in a fixed order (deterministic). (Flushed with atomics,
+// all splits hit the same addresses and the L2 atomic unit serialised them: 40-55 us per call at 256
+// splits, profiles/r6_cnn_kernel_stats_*.)
 template <int DT>      // DT = ceil((k*Cin + 1) / 16) im2col column tiles (incl. the ones row)
 __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ y,
-                                                            const float* __restrict__ x, float* __restrict__ dW,
-                                                            float* __restrict__ db, long rows, int T, int Cin,
+                                                            const float* __restrict__ x, float* __restrict__ ws,
+                                                            int CoutP, long rows, int T, int Cin,
                                                             int Cout, int k, int left, float alpha, int gap) {
   constexpr int KT = DT * 16;
   __shared__ __attribute__((aligned(16))) __bf16 dzT[64][CW_LD];
@@ -244,19 +248,29 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
       acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[d], 0, 0, 0);
     }
   }
-  // flush: lane holds o = o0 + 16w + 4quad + q, kk = 16d + col
+  // partial record: lane holds o = o0 + 16w + 4quad + q, kk = 16d + col
+  float* rec = ws + (size_t)blockIdx.y * CoutP * KT;
 #pragma unroll
   for (int d = 0; d < DT; ++d) {
     const int kk = 16 * d + col;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int o = o0 + 16 * w + 4 * quad + q;
-      if (o < Cout) {
-        if (kk < KC) atomicAdd(&dW[(size_t)kk * Cout + o], acc[d][q]);
-        else if (kk == KC) atomicAdd(&db[o], acc[d][q]);
-      }
-    }
+    for (int q = 0; q < 4; ++q) rec[(size_t)(o0 + 16 * w + 4 * quad + q) * KT + kk] = acc[d][q];
   }
+}
+
+// dW[kk][o] += sum over splits of ws[split][o][kk] (kk < KC), db[o] += ... (kk == KC); fixed order
+__global__ __launch_bounds__(256) void conv1d_wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int CoutP,
+                                                                   int KT, int KC, int Cout, float* __restrict__ dW,
+                                                                   float* __restrict__ db) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= CoutP * KT) return;
+  const int o = e / KT, kk = e - o * KT;
+  if (o >= Cout || kk > KC) return;
+  const size_t stride = (size_t)CoutP * KT;
+  float s = 0.f;
+  for (int sp = 0; sp < splits; ++sp) s += ws[sp * stride + e];
+  if (kk < KC) dW[(size_t)kk * Cout + o] += s;
+  else db[o] += s;
 }
 
 // ----------------------------------------------------------------------------- host
@@ -367,17 +381,17 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
     const int DT = (k * Cin + 1 + 15) / 16;
     const long ntiles = (rows + CW_RT - 1) / CW_RT;
     const int ncb = (Cout + 63) / 64;
-    // splits: every split flushes its whole dW^T tile with atomics, and all splits hit the same
-    // addresses, so the L2 atomic unit serialises them (256 splits: 40-55 us per call, the flush not the
-    // math); 64 keeps the tiles per split small and the contention a quarter
-    const int splits = deterministic_mode() ? 1 : (int)std::max<long>(1, std::min<long>(ntiles, 64 / ncb));
+    // splits write partial records, reduced in a fixed order by a second launch (deterministic)
+    const int splits = (int)std::max<long>(1, std::min<long>(ntiles, 256 / ncb));
+    const int CoutP = ncb * 64, KT = DT * 16;
+    at::Tensor ws = at::empty({(long)splits * CoutP * KT}, x.options());
     dim3 grid(ncb, splits);
     auto st = stream();
     switch (DT) {
 #define GQ_CW_DT(D)                                                                                               \
   case D:                                                                                                         \
     hipLaunchKernelGGL(conv1d_wgrad_kernel<D>, grid, dim3(256), 0, st, dy.data_ptr<float>(), y.data_ptr<float>(), \
-                       x.data_ptr<float>(), dW.data_ptr<float>(), db.data_ptr<float>(), rows, T, Cin, Cout, k,    \
+                       x.data_ptr<float>(), ws.data_ptr<float>(), CoutP, rows, T, Cin, Cout, k,                   \
                        (k - 1) / 2, (float)alpha, (int)gap);                                                      \
     break;
       GQ_CW_DT(1) GQ_CW_DT(2) GQ_CW_DT(3) GQ_CW_DT(4) GQ_CW_DT(5) GQ_CW_DT(6) GQ_CW_DT(7) GQ_CW_DT(8)
@@ -386,6 +400,10 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
 #undef GQ_CW_DT
       default: TORCH_CHECK(false, "conv1d_bwd: k*Cin too large");
     }
+    GQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(conv1d_wgrad_reduce_kernel, dim3((CoutP * KT + 255) / 256), dim3(256), 0, st,
+                       ws.data_ptr<float>(), splits, CoutP, KT, k * Cin, Cout, dW.data_ptr<float>(),
+                       db.data_ptr<float>());
     GQ_LAUNCH_CHECK();
   }
   if (need_dx) {
