@@ -258,17 +258,33 @@ __global__ __launch_bounds__(256) void conv1d_wgrad_kernel(const float* __restri
   }
 }
 
-// dW[kk][o] += sum over splits of ws[split][o][kk] (kk < KC), db[o] += ... (kk == KC); fixed order
+// dW[kk][o] += sum over splits of ws[split][o][kk] (kk < KC), db[o] += ... (kk == KC). A workgroup
+// takes 16 consecutive elements; its 16 thread groups sum every 16th split (loads in flight together),
+// then the 16 group sums are added in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void conv1d_wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int CoutP,
                                                                    int KT, int KC, int Cout, float* __restrict__ dW,
                                                                    float* __restrict__ db) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= CoutP * KT) return;
-  const int o = e / KT, kk = e - o * KT;
-  if (o >= Cout || kk > KC) return;
-  const size_t stride = (size_t)CoutP * KT;
+  __shared__ float part[16][17];
+  const int el = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const long E = (long)CoutP * KT;
+  const long e = (long)blockIdx.x * 16 + el;
+  const long ec = e < E ? e : E - 1;
+  float s0 = 0.f, s1 = 0.f;
+  int sp = g;
+#pragma unroll 4
+  for (; sp + 16 < splits; sp += 32) {
+    s0 += ws[(size_t)sp * E + ec];
+    s1 += ws[(size_t)(sp + 16) * E + ec];
+  }
+  if (sp < splits) s0 += ws[(size_t)sp * E + ec];
+  part[g][el] = s0 + s1;
+  __syncthreads();
+  if (g != 0 || e >= E) return;
   float s = 0.f;
-  for (int sp = 0; sp < splits; ++sp) s += ws[sp * stride + e];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s += part[q][el];
+  const int o = (int)(e / KT), kk = (int)(e - (long)o * KT);
+  if (o >= Cout || kk > KC) return;
   if (kk < KC) dW[(size_t)kk * Cout + o] += s;
   else db[o] += s;
 }
@@ -401,7 +417,7 @@ at::Tensor conv1d_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tenso
       default: TORCH_CHECK(false, "conv1d_bwd: k*Cin too large");
     }
     GQ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(conv1d_wgrad_reduce_kernel, dim3((CoutP * KT + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(conv1d_wgrad_reduce_kernel, dim3((CoutP * KT + 15) / 16), dim3(256), 0, st,
                        ws.data_ptr<float>(), splits, CoutP, KT, k * Cin, Cout, dW.data_ptr<float>(),
                        db.data_ptr<float>());
     GQ_LAUNCH_CHECK();
