@@ -303,9 +303,9 @@ static size_t conv_lds(int NTp, int KCH) {
 
 // K chunk: all of K (W^T resident) when it fits 80 KB (two workgroups per CU), else the
 // largest multiple of 32 that does
-static int conv_kch(int NTp, int Kp) {
+static int conv_kch(int NTp, int Kp, size_t limit = 80 * 1024) {
   int kch = Kp;
-  while (kch > 32 && conv_lds(NTp, kch) > 80 * 1024) kch -= 32;
+  while (kch > 32 && conv_lds(NTp, kch) > limit) kch -= 32;
   return kch;
 }
 
@@ -321,7 +321,8 @@ static void launch_conv_fwd(ConvArgs& a, bool gate) {
   // enough workgroups (each gathers the same A tile, small next to the idle chip it fills)
   int NTW = NT;
   while (NTW > 1 && ntiles * (NT / NTW) < 256) NTW /= 2;
-  a.KCH = conv_kch(NTW, a.Kp);
+  // (a grid of at most one workgroup per CU may take the whole LDS: K in one chunk, one gather pass)
+  a.KCH = conv_kch(NTW, a.Kp, ntiles * (NT / NTW) <= 256 ? 160 * 1024 : 80 * 1024);
   const size_t lds = conv_lds(NTW, a.KCH);
   const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024) / lds)));
   const int gx = (int)std::max<long>(1, std::min<long>(ntiles, 256L * per_cu / (NT / NTW)));
