@@ -374,6 +374,12 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 #ifndef TMW_D32
 #define TMW_D32 6        // H = 32 (T = 337 micro: 642 -> 555 us from 4 to 6)
 #endif
+#ifndef TMB_PACKED_Z
+#define TMB_PACKED_Z 1   // backward: dz / x images stored as packed dwords (0: 16-bit stores, the round-5 form)
+#endif
+__device__ __forceinline__ unsigned __bf16_bits(__bf16 v) {
+  return (unsigned)__builtin_bit_cast(unsigned short, v);
+}
 #ifndef TMW_SKIP
 #define TMW_SKIP 0       // (timing experiments only, wrong results: 1 no weight MFMAs, 2 no x / h streams,
 #endif                   //  4 no transposed dz copy; T = 337 micro, H = 16: 368 -> 297 / 310 / 352 us)   // 4 bf16 (v_mfma_f32_16x16x16_bf16 operand)
@@ -589,8 +595,15 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   // x_tt and h_{tt-1} of ring slot J into buffer b (h_{-1} = 0)
   auto rg_stage = [&](int b, int J, int tt) {
     if constexpr (RG) {
+      if constexpr (XG % 2 == 0 && TMB_PACKED_Z) {   // channel pairs as dwords (wx_k is even)
 #pragma unroll
-      for (int q = 0; q < XG; ++q) xrs[b][wx_seq][wx_k + q] = (__bf16)wx[J].v[q];
+        for (int q = 0; q < XG; q += 2)
+          *reinterpret_cast<unsigned*>(&xrs[b][wx_seq][wx_k + q]) =
+              __bf16_bits((__bf16)wx[J].v[q]) | (__bf16_bits((__bf16)wx[J].v[q + 1]) << 16);
+      } else {
+#pragma unroll
+        for (int q = 0; q < XG; ++q) xrs[b][wx_seq][wx_k + q] = (__bf16)wx[J].v[q];
+      }
       hrs[b][tid / H][tid % H] = (__bf16)(wh[J] * (tt >= 1 ? 1.f : 0.f));
     }
   };
@@ -688,15 +701,43 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         const __bf16 z1 = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
         const __bf16 z2 = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
         const __bf16 z3 = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
-        zs[p][col][0 * H + u] = z0;
-        zs[p][col][1 * H + u] = z1;
-        zs[p][col][2 * H + u] = z2;
-        zs[p][col][3 * H + u] = z3;
-        if constexpr (WG && !(TMW_SKIP & 4)) {
-          zT[s & 3][0 * H + u][col] = z0;
-          zT[s & 3][1 * H + u][col] = z1;
-          zT[s & 3][2 * H + u][col] = z2;
-          zT[s & 3][3 * H + u][col] = z3;
+        if constexpr (CPL == 1 && TMB_PACKED_Z) {
+          // dword stores instead of 16-bit ones (two lanes writing the two halves of one dword was a
+          // 2-way bank conflict on every dz store: ~1/3 of the LDS cycles of the H = 16 backward were
+          // conflicts). zs: units u, u + 1 (quads q, q ^ 1 = lanes l, l ^ 16) share a dword; the even quad
+          // stores gates 0, 1, the odd one gates 2, 3, after one exchange of packed gate pairs. zT:
+          // sequences col, col ^ 1 (lanes l, l ^ 1) share a dword; the same split by col parity.
+          const unsigned b0 = __bf16_bits(z0), b1 = __bf16_bits(z1), b2 = __bf16_bits(z2), b3 = __bf16_bits(z3);
+          const unsigned lo = b0 | (b1 << 16), hi = b2 | (b3 << 16);
+          const bool qo = quad & 1;
+          const unsigned rq = (unsigned)__shfl_xor((int)(qo ? lo : hi), 16, 64);   // partner unit's pair
+          const int gq = qo ? 2 : 0, ub = u & ~1;
+          const unsigned mq0 = qo ? b2 : b0, mq1 = qo ? b3 : b1;                    // my gates gq, gq + 1
+          const unsigned w0 = qo ? ((rq & 0xffffu) | (mq0 << 16)) : (mq0 | (rq << 16));
+          const unsigned w1 = qo ? ((rq >> 16) | (mq1 << 16)) : (mq1 | (rq & 0xffff0000u));
+          *reinterpret_cast<unsigned*>(&zs[p][col][gq * H + ub]) = w0;
+          *reinterpret_cast<unsigned*>(&zs[p][col][(gq + 1) * H + ub]) = w1;
+          if constexpr (WG && !(TMW_SKIP & 4)) {
+            const bool co = col & 1;
+            const unsigned rc2 = (unsigned)__shfl_xor((int)(co ? lo : hi), 1, 64);  // partner sequence's pair
+            const int gc = co ? 2 : 0, cb = col & ~1;
+            const unsigned mc0 = co ? b2 : b0, mc1 = co ? b3 : b1;
+            const unsigned v0 = co ? ((rc2 & 0xffffu) | (mc0 << 16)) : (mc0 | (rc2 << 16));
+            const unsigned v1 = co ? ((rc2 >> 16) | (mc1 << 16)) : (mc1 | (rc2 & 0xffff0000u));
+            *reinterpret_cast<unsigned*>(&zT[s & 3][gc * H + u][cb]) = v0;
+            *reinterpret_cast<unsigned*>(&zT[s & 3][(gc + 1) * H + u][cb]) = v1;
+          }
+        } else {
+          zs[p][col][0 * H + u] = z0;
+          zs[p][col][1 * H + u] = z1;
+          zs[p][col][2 * H + u] = z2;
+          zs[p][col][3 * H + u] = z3;
+          if constexpr (WG && !(TMW_SKIP & 4)) {
+            zT[s & 3][0 * H + u][col] = z0;
+            zT[s & 3][1 * H + u][col] = z1;
+            zT[s & 3][2 * H + u][col] = z2;
+            zT[s & 3][3 * H + u][col] = z3;
+          }
         }
       }
       if constexpr (WG && !(TMW_SKIP & 2)) {   // stage [x_t | 1] and h_{t-1} of this step, refill the slots
