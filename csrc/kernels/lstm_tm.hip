@@ -375,7 +375,10 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 #define TMW_D32 6        // H = 32 (T = 337 micro: 642 -> 555 us from 4 to 6)
 #endif
 #ifndef TMB_PACKED_Z
-#define TMB_PACKED_Z 1   // backward: dz / x images stored as packed dwords (0: 16-bit stores, the round-5 form)
+// backward: dz / x images stored as packed dwords after a lane-pair exchange (1) instead of 16-bit stores
+// (0). The 16-bit stores conflict 2-way, but the exchanges cost more: 1 measured slower (SoilNet 3.29 vs
+// 3.14 ms, IG 5.86 vs 5.67 ms per call, profiles/r6_packed_z_ab.txt)
+#define TMB_PACKED_Z 0
 #endif
 __device__ __forceinline__ unsigned __bf16_bits(__bf16 v) {
   return (unsigned)__builtin_bit_cast(unsigned short, v);
