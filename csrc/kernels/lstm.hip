@@ -56,11 +56,19 @@ __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d
 
 // ---------------------------------------------------------------- forward
 // VEC: x rows are 16-byte aligned and Din % 8 == 0 -> two float4 per chunk
+// Saved gates: bf16 in BF16 mode (8 instead of 16 bytes per cell-step; the gates lie in (0, 1) / (-1, 1)
+// and combine with bf16 MFMA operands in the backward), fp32 in the fp32 reference mode.
+#ifndef LSTM_BF16_GATES
+#define LSTM_BF16_GATES 1     // 0: fp32 saved gates in bf16 mode too (the round-5 form, for A/B builds)
+#endif
+template <bool BF16>
+using gate_t = typename std::conditional<BF16 && LSTM_BF16_GATES, __bf16, float>::type;
+
 template <int H, bool BF16, bool TRAIN, int KX, int D, bool VEC>
 __global__ __launch_bounds__(64 * (H / 16)) void lstm_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ U,
     const float* __restrict__ bias, float* __restrict__ hseq, float* __restrict__ cseq,
-    float* __restrict__ gates, int M, int T, int Din, int ldx) {
+    gate_t<BF16>* __restrict__ gates, int M, int T, int Din, int ldx) {
   using C = LstmCfg<H, BF16>;
   constexpr int G4 = C::G4;
   constexpr int KS = C::KS;
@@ -211,11 +219,19 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_fwd_kernel(
         st4(hseq + o * H + u0, hv[0], hv[1], hv[2], hv[3]);
         if constexpr (TRAIN) {
           st4(cseq + o * H + u0, c[0], c[1], c[2], c[3]);
-          float* gp = gates + o * G4 + u0;
-          st4(gp + 0 * H, iv[0], iv[1], iv[2], iv[3]);
-          st4(gp + 1 * H, fv[0], fv[1], fv[2], fv[3]);
-          st4(gp + 2 * H, gv[0], gv[1], gv[2], gv[3]);
-          st4(gp + 3 * H, ov[0], ov[1], ov[2], ov[3]);
+          gate_t<BF16>* gp = gates + o * G4 + u0;
+          if constexpr (BF16 && LSTM_BF16_GATES) {
+            typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4_t*>(gp + 0 * H) = bf16x4_t{(__bf16)iv[0], (__bf16)iv[1], (__bf16)iv[2], (__bf16)iv[3]};
+            *reinterpret_cast<bf16x4_t*>(gp + 1 * H) = bf16x4_t{(__bf16)fv[0], (__bf16)fv[1], (__bf16)fv[2], (__bf16)fv[3]};
+            *reinterpret_cast<bf16x4_t*>(gp + 2 * H) = bf16x4_t{(__bf16)gv[0], (__bf16)gv[1], (__bf16)gv[2], (__bf16)gv[3]};
+            *reinterpret_cast<bf16x4_t*>(gp + 3 * H) = bf16x4_t{(__bf16)ov[0], (__bf16)ov[1], (__bf16)ov[2], (__bf16)ov[3]};
+          } else {
+            st4(gp + 0 * H, iv[0], iv[1], iv[2], iv[3]);
+            st4(gp + 1 * H, fv[0], fv[1], fv[2], fv[3]);
+            st4(gp + 2 * H, gv[0], gv[1], gv[2], gv[3]);
+            st4(gp + 3 * H, ov[0], ov[1], ov[2], ov[3]);
+          }
         }
       }
       lds_barrier();
@@ -228,7 +244,7 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_fwd_kernel(
 // ---------------------------------------------------------------- backward
 template <int H, bool BF16, int D>
 __global__ __launch_bounds__(64 * (H / 16)) void lstm_bwd_kernel(
-    const float* __restrict__ dh_out, const float* __restrict__ gates, const float* __restrict__ cseq,
+    const float* __restrict__ dh_out, const gate_t<BF16>* __restrict__ gates, const float* __restrict__ cseq,
     const float* __restrict__ U, void* __restrict__ dz_out, int M, int T) {
   // BF16: dz is stored as bf16 (the weight-gradient / dx passes round it to bf16 for their MFMAs
   // anyway: same results, half the bytes); fp32 reference mode keeps fp32 dz
@@ -267,11 +283,20 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_bwd_kernel(
 
   // ring slot j: reverse step s = s0 + j (t = T-1-s): i,f,g,o, c_t, dh_t
   float4 rg[D][4], rc[D], rd[D];
+  auto ld_gate4 = [](const gate_t<BF16>* p) -> float4 {
+    if constexpr (BF16 && LSTM_BF16_GATES) {
+      const uint2 u = *reinterpret_cast<const uint2*>(p);
+      return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                         __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      return ld4(p);
+    }
+  };
 #define GQ_BWD_LOAD(J, SS)                                                 \
   {                                                                        \
     const int tt = max(T - 1 - (SS), 0);                                   \
     const size_t o = (size_t)lseq * T + tt;                                \
-    _Pragma("unroll") for (int g = 0; g < 4; ++g) rg[J][g] = ld4(gates + o * G4 + g * H + u0); \
+    _Pragma("unroll") for (int g = 0; g < 4; ++g) rg[J][g] = ld_gate4(gates + o * G4 + g * H + u0); \
     rc[J] = ld4(cseq + o * H + u0);                                        \
     rd[J] = ld4(dh_out + o * H + u0);                                      \
   }
@@ -365,17 +390,17 @@ __global__ __launch_bounds__(64 * (H / 16)) void lstm_bwd_kernel(
 // D x (VMEM ops per step) stays below the 63-entry vmcnt counter.
 template <int H, bool BF16, bool TRAIN, int KX, bool VEC>
 void launch_fwd_cfg(dim3 grid, dim3 block, hipStream_t st, const float* x, const float* W, const float* U,
-                    const float* b, float* h, float* c, float* g, int M, int T, int Din, int ldx) {
+                    const float* b, float* h, float* c, void* g, int M, int T, int Din, int ldx) {
   constexpr int loads = VEC ? 2 * KX : 8 * KX;
   constexpr int ops = loads + (TRAIN ? 6 : 1);
   constexpr int Dv = 56 / ops < 2 ? 2 : (56 / ops > 8 ? 8 : 56 / ops);
   constexpr int D = (H >= 128 || !BF16) ? 2 : Dv;
-  hipLaunchKernelGGL((lstm_fwd_kernel<H, BF16, TRAIN, KX, D, VEC>), grid, block, 0, st, x, W, U, b, h, c, g, M, T,
-                     Din, ldx);
+  hipLaunchKernelGGL((lstm_fwd_kernel<H, BF16, TRAIN, KX, D, VEC>), grid, block, 0, st, x, W, U, b, h, c,
+                     reinterpret_cast<gate_t<BF16>*>(g), M, T, Din, ldx);
 }
 
 template <int H, bool BF16, bool TRAIN>
-void launch_fwd_h(const float* x, const float* W, const float* U, const float* b, float* h, float* c, float* g,
+void launch_fwd_h(const float* x, const float* W, const float* U, const float* b, float* h, float* c, void* g,
                   int M, int T, int Din, int ldx, hipStream_t st) {
   dim3 grid((M + 15) / 16), block(64 * (H / 16));
   const int kx = (Din + 31) / 32;
@@ -391,7 +416,7 @@ void launch_fwd_h(const float* x, const float* W, const float* U, const float* b
 }
 
 template <bool BF16, bool TRAIN>
-void launch_fwd(int H, const float* x, const float* W, const float* U, const float* b, float* h, float* c, float* g,
+void launch_fwd(int H, const float* x, const float* W, const float* U, const float* b, float* h, float* c, void* g,
                 int M, int T, int Din, int ldx, hipStream_t st) {
   switch (H) {
     case 16: launch_fwd_h<16, BF16, TRAIN>(x, W, U, b, h, c, g, M, T, Din, ldx, st); break;
@@ -406,8 +431,9 @@ template <int H, bool BF16>
 constexpr int bwd_ring() { return (H >= 128 || !BF16) ? 3 : 5; }   // 10 VMEM ops per step
 
 template <bool BF16>
-void launch_bwd(int H, const float* dh, const float* g, const float* c, const float* U, void* dz, int M, int T,
+void launch_bwd(int H, const float* dh, const void* gv, const float* c, const float* U, void* dz, int M, int T,
                 hipStream_t st) {
+  const gate_t<BF16>* g = reinterpret_cast<const gate_t<BF16>*>(gv);
   dim3 grid((M + 15) / 16);
   switch (H) {
 #define GQ_CASE(HH)                                                                                       \
@@ -440,14 +466,15 @@ std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const
   const int Mp = (M + 15) / 16 * 16;   // stores go to whole 16-row tiles
   at::Tensor h = at::empty({Mp, T, H}, opt);
   at::Tensor c = train ? at::empty({Mp, T, H}, opt) : at::empty({0}, opt);
-  at::Tensor g = train ? at::empty({Mp, T, 4 * H}, opt) : at::empty({0}, opt);
+  at::Tensor g = train ? at::empty({Mp, T, 4 * H}, (bf16 && LSTM_BF16_GATES) ? opt.dtype(at::kBFloat16) : opt)
+                        : at::empty({0}, opt);
   auto cut = [&](at::Tensor t) { return (train && Mp != M) ? t.narrow(0, 0, M) : t; };
   if (M == 0 || T == 0) return {h.narrow(0, 0, M), cut(c), cut(g)};
   auto st = stream();
   const float *xp = x.data_ptr<float>(), *Wp = W.data_ptr<float>(), *Up = U.data_ptr<float>(), *bp = b.data_ptr<float>();
   float* hp = h.data_ptr<float>();
   float* cp = train ? c.data_ptr<float>() : nullptr;
-  float* gp = train ? g.data_ptr<float>() : nullptr;
+  void* gp = train ? g.data_ptr() : nullptr;
   if (bf16) {
     if (train) launch_fwd<true, true>(H, xp, Wp, Up, bp, hp, cp, gp, M, T, Din, ldx, st);
     else launch_fwd<true, false>(H, xp, Wp, Up, bp, hp, cp, gp, M, T, Din, ldx, st);
@@ -462,7 +489,9 @@ std::vector<at::Tensor> lstm_fwd(const at::Tensor& x, const at::Tensor& W, const
 at::Tensor lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Tensor& cseq, const at::Tensor& U,
                     bool bf16) {
   check_f32_cuda(dh, "dh");
-  check_f32_cuda(gates, "gates");
+  TORCH_CHECK(gates.is_cuda() && gates.is_contiguous() &&
+                  gates.scalar_type() == ((bf16 && LSTM_BF16_GATES) ? at::kBFloat16 : at::kFloat),
+              "lstm_bwd: gates must be the forward's (bf16 in bf16 mode, fp32 otherwise)");
   check_f32_cuda(cseq, "cseq");
   check_f32_cuda(U, "U");
   const int M = dh.size(0), T = dh.size(1), H = U.size(0);
@@ -473,8 +502,8 @@ at::Tensor lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Ten
   at::Tensor dz = at::empty({Mp, T, 4 * H}, dh.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
   if (M == 0 || T == 0) return dz.narrow(0, 0, M);
   auto st = stream();
-  if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr(), M, T, st);
-  else launch_bwd<false>(H, dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr(), M, T, st);
+  if (bf16) launch_bwd<true>(H, dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr(), M, T, st);
+  else launch_bwd<false>(H, dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr<float>(), U.data_ptr<float>(), dz.data_ptr(), M, T, st);
   GQ_LAUNCH_CHECK();
   return Mp == M ? dz : dz.narrow(0, 0, M);
 }
