@@ -27,7 +27,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=4, help="timed batches per rank")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256, help="windows explained per attribute() call")
+    ap.add_argument("--batch", type=int, default=324, help="windows explained per attribute() call "
+                    "(324 = one full 32768-row path chunk)")
     ap.add_argument("--m-steps", type=int, default=100)
     ap.add_argument("--max-rows", type=int, default=32768, help="path rows (windows x path points) per pass")
     args = ap.parse_args(argv)
