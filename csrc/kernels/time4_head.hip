@@ -38,20 +38,23 @@ constexpr int T4HP = T4H + 4;
 struct T4Args {
   const float* x;                        // [T][Mp][Din] (time-major, 16-B aligned rows)
   const float *W, *U, *b;                // [Dw][4H], [H][4H], [4H]
-  float* h;                              // [T][Mp][H]
+  float* h;                              // [T][Mp][H] (hlast: [Mp][H], the last step only)
   float* g;                              // train: [T][tiles][NW][CPL][64][4]
-  float* c;                              // train: [T][tiles][NW][CPL][64][2]: c_t, c_{t-1}
+  float* c;                              // train: [T][tiles][NW][CPL][64][2]: c_t, c_{t-1} (CG: [..][64] c_t)
+  uint2* gb;                             // CG train: [T][tiles][NW][CPL][64] packed bf16 gates
+  const float* dhT;                      // CG backward: [Mp][H] gradient of the last state
   __bf16* dz;                            // backward: [T + 1][Mp][4H] bf16
   float* dx;                             // backward: [T][Mp][Din]
   int T, Mp, Din, Dw, ntiles;
   ChainHead hd;
   int head;
+  int hlast;                             // forward: store h of the last step only ([Mp][H])
   long long* trace;                      // [blocks][16] s_memrealtime marks of the last launch (profiling)
   const bf16x8_t* pk;                    // forward: A-fragment image (lstm_tm_common.h), or nullptr
 };
 
 __device__ __forceinline__ void t4_mark(long long* tr, int i) {
-  if (threadIdx.x == 0) tr[blockIdx.x * 16 + i] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (tr != nullptr && threadIdx.x == 0) tr[blockIdx.x * 16 + i] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 __device__ __forceinline__ size_t t4_sidx(int t, int ntiles, int tile, int w, int cc, int lane) {
@@ -95,7 +98,12 @@ __device__ __forceinline__ void t4_stage_rows(__bf16* dst, const float* __restri
   }
 }
 
-template <bool TRAIN, int KX>
+// CG (the standalone layer, time4_fwd / time4_bwd): compact saved state - packed bf16 gates and
+// c_t only (12 instead of 24 bytes per cell and step) - and workgroups that loop over tiles, so
+// the weight fragments are staged once per workgroup rather than once per 16 sequences (an
+// integrated-gradients pass runs 32k sequences: 2048 tiles on 256 workgroups). With the head
+// (grid = tiles) the loop runs once.
+template <bool TRAIN, int KX, bool CG = false>
 __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
   using L = T4FwdLds<KX>;
   constexpr int XP = L::XP;
@@ -105,7 +113,6 @@ __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
   float* hl = reinterpret_cast<float*>(smem + L::XS + L::HS);
   char* scratch = smem + L::XS + L::HS + L::HL;
 
-  const int tile = blockIdx.x, row0 = tile * 16;
   const int T = A.T, Mp = A.Mp, Din = A.Din, Dw = A.Dw, ntiles = A.ntiles;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -167,6 +174,8 @@ __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
     }
     __syncthreads();
   }
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int row0 = tile * 16;
   // the tile's whole input sequence -> LDS (bf16, channels >= Din zero)
   for (int e = tid; e < T * 16 * XP; e += T4NT) (&xs[0][0][0])[e] = (__bf16)0.f;
   for (int e = tid; e < 2 * 16 * (T4H + 8); e += T4NT) (&hs[0][0][0])[e] = (__bf16)0.f;
@@ -222,12 +231,20 @@ __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
       const float hv = ov * tanhf_fast(c[cc]);
       const int u = unit[cc];
       hs[p ^ 1][col][u] = (__bf16)hv;
-      A.h[((size_t)t * Mp + row0 + col) * T4H + u] = hv;
+      if (!A.hlast)
+        A.h[((size_t)t * Mp + row0 + col) * T4H + u] = hv;
+      else if (t == T - 1)
+        A.h[(size_t)(row0 + col) * T4H + u] = hv;
       if (t == T - 1) hl[col * T4HP + u] = hv;
       if constexpr (TRAIN) {
         const size_t o = t4_sidx(t, ntiles, tile, w, cc, lane);
-        *reinterpret_cast<float4*>(A.g + o * 4) = make_float4(iv, fv, gv, ov);
-        *reinterpret_cast<float2*>(A.c + o * 2) = make_float2(c[cc], cold);
+        if constexpr (CG) {
+          A.gb[o] = gates_pack(iv, fv, gv, ov);
+          A.c[o] = c[cc];
+        } else {
+          *reinterpret_cast<float4*>(A.g + o * 4) = make_float4(iv, fv, gv, ov);
+          *reinterpret_cast<float2*>(A.c + o * 2) = make_float2(c[cc], cold);
+        }
       }
     }
     lds_barrier();
@@ -236,6 +253,8 @@ __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
   __syncthreads();
   if (A.head) chain_head_fwd<T4H>(A.hd, tile, ntiles, hl, scratch);
   __syncthreads();
+  if constexpr (!CG) break;              // (grid = tiles)
+  }
   t4_mark(A.trace, 15);
 }
 
@@ -250,7 +269,7 @@ struct T4BwdLds {
   static constexpr int BYTES = DH + (STEP > ChainHeadBwdLds<T4H>::BYTES ? STEP : ChainHeadBwdLds<T4H>::BYTES);
 };
 
-template <int KX>
+template <int KX, bool CG = false>
 __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
   using L = T4BwdLds<KX>;
   constexpr int DXP = 32 * KX + 4;
@@ -261,7 +280,7 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
   auto dhn = reinterpret_cast<float (*)[T4HP]>(rs + L::ZS);
   auto dxp = reinterpret_cast<float (*)[16][DXP]>(rs + L::ZS + L::DN);
 
-  const int tile = blockIdx.x, row0 = tile * 16;
+  int tile = blockIdx.x;
   const int T = A.T, Mp = A.Mp, Din = A.Din, Dw = A.Dw, ntiles = A.ntiles;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -274,22 +293,39 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
   // forward state ring (2 reverse steps: gates, c_t, c_{t-1}); a slot is refilled right after the
   // cell phase that consumed it, before that step's stores (vmcnt retires in order, so a wait for
   // a slot then covers only stores issued two steps earlier)
-  float4 rg[2][T4CPL];
+  // (CG: packed bf16 gates, unpacked when consumed, and c_t / c_{t-1} from two step slots)
+  using GR = std::conditional_t<CG, uint2, float4>;
+  GR rg[2][T4CPL];
   float2 rcs[2][T4CPL];
   auto load_slot = [&](int j, int t) {
     const int tc = max(t, 0);
 #pragma unroll
     for (int cc = 0; cc < T4CPL; ++cc) {
       const size_t o = t4_sidx(tc, ntiles, tile, w, cc, lane);
-      rg[j][cc] = *reinterpret_cast<const float4*>(A.g + o * 4);
-      rcs[j][cc] = *reinterpret_cast<const float2*>(A.c + o * 2);
+      if constexpr (CG) {
+        rg[j][cc] = A.gb[o];
+        rcs[j][cc] = make_float2(A.c[o], A.c[t4_sidx(max(t - 1, 0), ntiles, tile, w, cc, lane)]);
+      } else {
+        rg[j][cc] = *reinterpret_cast<const float4*>(A.g + o * 4);
+        rcs[j][cc] = *reinterpret_cast<const float2*>(A.c + o * 2);
+      }
+    }
+  };
+  auto load_dhT = [&]() {   // CG: the last state's gradient [Mp][H] -> LDS
+    const float4* src = reinterpret_cast<const float4*>(A.dhT + (size_t)tile * 16 * T4H);
+    for (int e = tid; e < 16 * T4H / 4; e += T4NT) {
+      const int r = e / (T4H / 4), k = 4 * (e % (T4H / 4));
+      *reinterpret_cast<float4*>(dhT + r * T4HP + k) = src[e];
     }
   };
   load_slot(0, T - 1);
   load_slot(1, T - 2);
 
   t4_mark(A.trace, 0);
-  chain_head_bwd<T4H>(A.hd, A.h + (size_t)(T - 1) * Mp * T4H, tile, ntiles, dhT, rs);
+  if constexpr (CG)
+    load_dhT();
+  else
+    chain_head_bwd<T4H>(A.hd, A.h + (size_t)(T - 1) * Mp * T4H, tile, ntiles, dhT, rs);
   // recurrent / input weights as A fragments, after the head prologue (live through it they
   // pushed the kernel past 256 VGPRs into scratch): from the chain forward's backward image
   // (lane-contiguous 16-B loads), else gathered (16 rows per load instruction: ~10 us)
@@ -322,11 +358,13 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
   __syncthreads();                      // the head scratch becomes the step tiles
   t4_mark(A.trace, 1);
 
+  const size_t zstep = (size_t)Mp * T4G;
+  const int nx = 16 * Din;
+  for (;;) {                            // tiles (one pass unless CG)
+  const int row0 = tile * 16;
   float dc[T4CPL], dhr[T4CPL];
 #pragma unroll
   for (int cc = 0; cc < T4CPL; ++cc) dc[cc] = dhr[cc] = 0.f;
-  const size_t zstep = (size_t)Mp * T4G;
-  const int nx = 16 * Din;
   for (int s0 = 0; s0 < T; s0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -337,8 +375,13 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
       for (int cc = 0; cc < T4CPL; ++cc) {
         const int u = unit[cc];
         const float dh = dhr[cc] + (s == 0 ? dhT[col * T4HP + u] : 0.f);
-        const float4 g = rg[j][cc];
-        const float cprev = rcs[j][cc].y;      // (0 at t = 0: the forward's initial state)
+        float4 g;
+        if constexpr (CG)
+          g = gates_unpack(rg[j][cc]);
+        else
+          g = rg[j][cc];
+        // (0 at t = 0: the forward's initial state; CG reads a clamped slot there)
+        const float cprev = (CG && t == 0) ? 0.f : rcs[j][cc].y;
         const float tc = tanhf_fast(rcs[j][cc].x);
         const float dct = dc[cc] + dh * g.w * (1.f - tc * tc);
         dc[cc] = dct * g.y;
@@ -349,11 +392,13 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
       }
       load_slot(j, t - 2);
       lds_barrier();
+      if (!CG || A.dz != nullptr) {   // (uniform; CG: none without weight gradients)
 #pragma unroll
-      for (int q = 0; q < 16 * T4G / 4 / T4NT; ++q) {   // dz_t -> HBM, the bf16 values the MFMAs use
-        const int e = tid + T4NT * q, sq = e / (T4G / 4), c4 = (e % (T4G / 4)) * 4;
-        const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[sq][c4]);
-        *reinterpret_cast<bf16x4_t*>(A.dz + (size_t)t * zstep + (size_t)(row0 + sq) * T4G + c4) = zv;
+        for (int q = 0; q < 16 * T4G / 4 / T4NT; ++q) {   // dz_t -> HBM, the bf16 values the MFMAs use
+          const int e = tid + T4NT * q, sq = e / (T4G / 4), c4 = (e % (T4G / 4)) * 4;
+          const bf16x4_t zv = *reinterpret_cast<const bf16x4_t*>(&zs[sq][c4]);
+          *reinterpret_cast<bf16x4_t*>(A.dz + (size_t)t * zstep + (size_t)(row0 + sq) * T4G + c4) = zv;
+        }
       }
       {   // dh_rec^T for unit tile w (full K) and dx^T for din tile dt over gate-column half kh,
           // as 4 + 2 interleaved accumulator chains
@@ -395,7 +440,15 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
       t4_mark(A.trace, 2 + min(s, 9));
     }
   }
-  chain_head_bwd_reduce<T4H>(A.hd, tile, ntiles);
+  if constexpr (!CG) break;
+  tile += gridDim.x;
+  if (tile >= ntiles) break;
+  load_slot(0, T - 1);                   // the next tile: state ring and last-state gradient
+  load_slot(1, T - 2);
+  load_dhT();
+  __syncthreads();
+  }
+  if constexpr (!CG) chain_head_bwd_reduce<T4H>(A.hd, tile, ntiles);
   __syncthreads();
   t4_mark(A.trace, 15);
 }
@@ -615,10 +668,107 @@ std::vector<at::Tensor> time4_head_bwd(const at::Tensor& dloss, const at::Tensor
   return {dz, dx};
 }
 
+// ------------------------------------------------------------- the layer alone (no head)
+// time4 as a standalone time-major layer returning its last state, for passes with many
+// sequences (integrated gradients: 32k path sequences per launch, where the seq-major
+// lstm_fwd<128> / lstm_bwd / lstm_dx path plus its layout copies took ~0.7 ms). CG kernels:
+// compact saved state, workgroups looping over tiles.
+static int t4_grid(int ntiles, int64_t max_blocks) {
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "time4: device");
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "time4: CUs");
+  int g = std::min(ntiles, std::max(cus, 1));       // one 512-thread workgroup per CU (LDS / VGPRs)
+  if (max_blocks > 0) g = std::min<int64_t>(g, max_blocks);
+  return std::max(g, 1);
+}
+
+// x [T, Mp, Din] time-major. Returns [h, g, c]: h = [T, Mp, 128] (all_h) or the last state
+// [Mp, 128]; with train the compact saved state g (packed bf16 gates) and c for time4_bwd.
+std::vector<at::Tensor> time4_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
+                                  bool train, bool all_h, int64_t max_blocks) {
+  int T, Mp, Din, Dw;
+  t4_check(x, W, U, T, Mp, Din, Dw);
+  check_f32_cuda(b, "b");
+  TORCH_CHECK(b.numel() == T4G, "time4_fwd: bias size");
+  c10::DeviceGuard guard(x.device());
+  auto opt = x.options();
+  const int ntiles = Mp / 16;
+  const long cells = (long)T * Mp * T4H;
+  at::Tensor h = all_h ? at::empty({T, Mp, T4H}, opt) : at::empty({Mp, T4H}, opt);
+  at::Tensor g = train ? at::empty({cells * 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  at::Tensor c = train ? at::empty({cells}, opt) : at::empty({0}, opt);
+  T4Args A{};
+  A.x = x.data_ptr<float>();
+  A.W = W.data_ptr<float>();
+  A.U = U.data_ptr<float>();
+  A.b = b.data_ptr<float>();
+  A.h = h.data_ptr<float>();
+  A.gb = train ? reinterpret_cast<uint2*>(g.data_ptr()) : nullptr;
+  A.c = train ? c.data_ptr<float>() : nullptr;
+  A.T = T;
+  A.Mp = Mp;
+  A.Din = Din;
+  A.Dw = Dw;
+  A.ntiles = ntiles;
+  A.hlast = all_h ? 0 : 1;
+  const dim3 grid(t4_grid(ntiles, max_blocks));
+  const int KX = (Din + 31) / 32;
+#define GQ_T4F(TR, K) hipLaunchKernelGGL((t4_head_fwd_kernel<TR, K, true>), grid, dim3(T4NT), 0, stream(), A)
+  if (train) { if (KX == 1) GQ_T4F(true, 1); else GQ_T4F(true, 2); }
+  else { if (KX == 1) GQ_T4F(false, 1); else GQ_T4F(false, 2); }
+#undef GQ_T4F
+  GQ_LAUNCH_CHECK();
+  return {h, g, c};
+}
+
+// dh [Mp, 128]: gradient of the last state; x / g / c from time4_fwd(train). Returns [dz, dx]:
+// dz [T + 1, Mp, 512] bf16 for lstm_tm_grads when need_dz (else empty), dx [T, Mp, Din].
+std::vector<at::Tensor> time4_bwd(const at::Tensor& dh, const at::Tensor& x, const at::Tensor& g, const at::Tensor& c,
+                                  const at::Tensor& W, const at::Tensor& U, bool need_dz, int64_t max_blocks) {
+  int T, Mp, Din, Dw;
+  t4_check(x, W, U, T, Mp, Din, Dw);
+  check_f32_cuda(dh, "dh");
+  check_f32_cuda(c, "c");
+  const long cells = (long)T * Mp * T4H;
+  TORCH_CHECK(dh.numel() == (long)Mp * T4H, "time4_bwd: dh must be [Mp, 128]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dh.data_ptr()) % 16 == 0, "time4_bwd: dh must be 16-byte aligned");
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kBFloat16 && g.numel() == cells * 4 &&
+                  c.numel() == cells, "time4_bwd: saved state from time4_fwd(train=True)");
+  c10::DeviceGuard guard(x.device());
+  auto opt = x.options();
+  const int ntiles = Mp / 16;
+  at::Tensor dz = need_dz ? at::empty({T + 1, Mp, T4G}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  at::Tensor dx = at::empty({T, Mp, Din}, opt);
+  T4Args A{};
+  A.x = x.data_ptr<float>();
+  A.W = W.data_ptr<float>();
+  A.U = U.data_ptr<float>();
+  A.gb = reinterpret_cast<uint2*>(const_cast<void*>(g.data_ptr()));
+  A.c = const_cast<float*>(c.data_ptr<float>());
+  A.dhT = dh.data_ptr<float>();
+  A.dz = need_dz ? bf16_ptr(dz) : nullptr;
+  A.dx = dx.data_ptr<float>();
+  A.T = T;
+  A.Mp = Mp;
+  A.Din = Din;
+  A.Dw = Dw;
+  A.ntiles = ntiles;
+  const dim3 grid(t4_grid(ntiles, max_blocks));
+  if ((Din + 31) / 32 == 1)
+    hipLaunchKernelGGL((t4_head_bwd_kernel<1, true>), grid, dim3(T4NT), 0, stream(), A);
+  else
+    hipLaunchKernelGGL((t4_head_bwd_kernel<2, true>), grid, dim3(T4NT), 0, stream(), A);
+  GQ_LAUNCH_CHECK();
+  return {dz, dx};
+}
+
 }  // namespace gq
 
 TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("time4_head_fwd", &gq::time4_head_fwd);
   m.impl("time4_head_bwd", &gq::time4_head_bwd);
   m.impl("time4_trace", &gq::time4_trace);
+  m.impl("time4_fwd", &gq::time4_fwd);
+  m.impl("time4_bwd", &gq::time4_bwd);
 }

@@ -100,7 +100,8 @@ class TimeLayer(nn.Module):
         rows past M; C may carry zero channels past the first layer's input width).
         Returns ``[M, out_features]``. Producers that can write this layout directly (the
         SoilNet GCN kernel) skip the transpose/pad copy of :meth:`_forward_tm`."""
-        from ..ops.lstm import _chain_on, lstm_chain_tm, lstm_layer_tm, lstm_pair_tm, pool_fusion, tm_eligible
+        from ..ops.lstm import (_chain_on, last128_eligible, lstm_chain_tm, lstm_last128_tm, lstm_layer_tm,
+                                lstm_pair_tm, pool_fusion, tm_eligible)
         from ..ops.pool import max_pool1d_tm
         if self.layer_type != "lstm":
             # CNN branch behind a time-major producer (the store-fused CML GCN front end): [M, T, Cin]
@@ -146,6 +147,8 @@ class TimeLayer(nn.Module):
                 if not mod.return_sequences:
                     return h[:M]
                 continue
+            if tm and last128_eligible(h, mod):      # time4 (H = 128, last state) on the time-major input
+                return lstm_last128_tm(h, mod)[:M]
             if tm:                                   # leave time-major: [T, Mp, C] -> [M, T, C]
                 h = h.transpose(0, 1)
                 if h.shape[0] != M:                  # (a no-op slice would still cost a zero-fill + copy in backward)

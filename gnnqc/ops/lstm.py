@@ -830,6 +830,62 @@ def lstm_layer_tm(x_tm: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch
     return _HipLSTMTM.apply(x_tm, W, U, b, bool(return_sequences), int(pool))
 
 
+class _HipLSTMLast128(torch.autograd.Function):
+    """An H = 128 layer returning its last state on a time-major input [T, Mp, Din] (T <= 16):
+    ``time4_head.hip`` in its standalone mode (``time4_fwd`` / ``time4_bwd``: no head, compact
+    saved state, workgroups looping over 16-sequence tiles). Replaces, for the time layer's last
+    LSTM (time4, ``libs/create_model.py:61-79``), the sequence-major lstm_fwd<128> / lstm_bwd /
+    lstm_dx kernels and the [T, Mp, C] <-> [M, T, C] copies around them. Weight gradients: the
+    backward's dz through ``lstm_tm_grads`` (the training chain-head path's weight pass)."""
+
+    @staticmethod
+    def forward(ctx, x, W, U, b):
+        from ..utils.native import hip_ops
+        x = x.contiguous()
+        need = any(ctx.needs_input_grad[:4])
+        wgrad = any(ctx.needs_input_grad[1:4])
+        h, g, c = hip_ops().time4_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), need, wgrad)
+        ctx.params = (W, U, b)
+        if need:
+            ctx.save_for_backward(x, W, U, g, c, h if wgrad else x.new_zeros(0))
+        return h[-1] if wgrad else h
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..utils.native import hip_ops
+        ops = hip_ops()
+        x, W, U, g, c, h = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        wgrad = any(need[1:4])
+        Wc = W.contiguous()
+        dz, dx = ops.time4_bwd(dout.contiguous(), x, g, c, Wc, U.contiguous(), wgrad)
+        grads = [None, None, None]
+        if wgrad:
+            sinks = [_grad_sink(p) for p in ctx.params]
+            with _deferred_reduce(all(d for _, d in sinks)):
+                ops.lstm_tm_grads(dz, x, h, Wc, sinks[0][0], sinks[1][0], sinks[2][0], False)
+            grads = [None if (direct or not n) else buf for (buf, direct), n in zip(sinks, need[1:4])]
+        return (dx if need[0] else None, *grads)
+
+
+def last128_eligible(x: torch.Tensor, mod) -> bool:
+    """Whether :class:`_HipLSTMLast128` takes LSTM module ``mod`` on time-major ``x`` [T, Mp, Din]
+    (``GNNQC_T4_TM=0``: the sequence-major kernels)."""
+    import os
+    from . import use_hip
+    if os.environ.get("GNNQC_T4_TM", "1") != "1" or not use_hip(x) or x.dim() != 3:
+        return False
+    T, Mp, Din = x.shape
+    return (mod.units == 128 and not mod.return_sequences and mod.activation == "tanh" and mod.compute_bf16
+            and 1 <= T <= 16 and Mp % 16 == 0 and Din % 4 == 0 and 4 <= Din <= 64
+            and mod.kernel.shape[0] <= Din and x.dtype == torch.float32)
+
+
+def lstm_last128_tm(x_tm: torch.Tensor, mod) -> torch.Tensor:
+    """Last state [Mp, 128] of LSTM module ``mod`` on time-major ``x_tm`` (see ``last128_eligible``)."""
+    return _HipLSTMLast128.apply(x_tm, mod.kernel, mod.recurrent_kernel, mod.bias)
+
+
 def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor,
                return_sequences: bool = True, activation: str = "tanh", bf16: bool = True) -> torch.Tensor:
     """Dispatch: HIP persistent kernel on GPU (tanh, H multiple of 16), eager otherwise."""
@@ -842,4 +898,5 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
 
 __all__ = ["unflagged_grad_writes", "lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
            "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError", "lstm_chain_head_tm",
+           "lstm_last128_tm", "last128_eligible",
            "direct_grad_accumulation"]

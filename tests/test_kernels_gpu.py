@@ -1008,3 +1008,97 @@ def test_split_optimizer_graph_matches_fused(cuda_device, cml_windows, monkeypat
         set_deterministic(prev)
     assert abs(l1 - l0) < 1e-5 * abs(l0) + 1e-6, (l1, l0)
     assert (p1 - p0).norm().item() < 1e-6 * p0.norm().item()
+
+
+@pytest.mark.parametrize("Din,Dw,T,wgrad", [(64, 64, 6, True), (64, 64, 6, False), (32, 28, 1, True),
+                                            (64, 60, 16, False), (16, 16, 3, True)])
+def test_time4_standalone_last_state_matches_fp64_oracle(cuda_device, Din, Dw, T, wgrad):
+    """time4 (H = 128, last state) as a standalone time-major layer (time4_fwd / time4_bwd: compact
+    saved state, workgroups looping over tiles) vs an fp64 eager LSTM: last state, input gradient
+    (zero past the W rows and on padded rows) and weight gradients (dz -> lstm_tm_grads)."""
+    from gnnqc.ops import lstm as L
+    dev = cuda_device
+    gen = torch.Generator().manual_seed(Din * 100 + Dw + T + 7 * wgrad)
+    M, Mp = 72, 80
+    x = torch.zeros(T, Mp, Din)
+    x[:, :M] = torch.randn(T, M, Din, generator=gen)
+    x = x.to(dev)
+    W, U, b = _lstm_params(Dw, 128, gen, dev)
+    U = U * 0.5
+    dout = torch.randn(Mp, 128, generator=gen).to(dev)
+    dout[M:] = 0
+    xi = x.clone().requires_grad_(True)
+    ps = [t.clone().requires_grad_(wgrad) for t in (W, U, b)]
+    out = L._HipLSTMLast128.apply(xi, *ps)
+    assert out.shape == (Mp, 128)
+    out.backward(dout)
+    rx = x[:, :M, :Dw].transpose(0, 1).double().clone().requires_grad_(True)
+    rps = [t.double().clone().requires_grad_(True) for t in (W, U, b)]
+    ref = L.lstm_eager(rx, *rps, return_sequences=False)
+    ref.backward(dout[:M].double())
+    err = (out[:M].double() - ref).abs().max().item()
+    assert err < 3e-2, err                         # (bf16 MFMA operands, as the other bf16 LSTM tests)
+    got = [xi.grad[:, :M, :Dw].transpose(0, 1)] + ([p.grad for p in ps] if wgrad else [])
+    refs = [rx.grad] + ([p.grad for p in rps] if wgrad else [])
+    for name, a, r in zip("xWUb", got, refs):
+        rel = (a.double() - r).abs().max().item() / (r.abs().max().item() + 1e-6)
+        assert rel < 5e-2, (name, rel)
+    assert float(xi.grad[:, M:].abs().max()) == 0.0
+    if Dw < Din:
+        assert float(xi.grad[..., Dw:].abs().max()) == 0.0
+
+
+def test_time4_standalone_tile_loop_matches_one_tile_per_workgroup(cuda_device):
+    """time4_fwd / time4_bwd with 3 workgroups looping over 21 tiles == one workgroup per tile, bitwise."""
+    from gnnqc.utils.native import hip_ops
+    ops = hip_ops()
+    gen = torch.Generator().manual_seed(5)
+    T, Mp, Din = 6, 21 * 16, 64
+    x = torch.randn(T, Mp, Din, generator=gen).to(cuda_device)
+    W, U, b = _lstm_params(Din, 128, gen, cuda_device)
+    dh = torch.randn(Mp, 128, generator=gen).to(cuda_device)
+    for all_h in (False, True):
+        r0 = ops.time4_fwd(x, W, U, b, True, all_h, 0)
+        r1 = ops.time4_fwd(x, W, U, b, True, all_h, 3)
+        for a, c in zip(r0, r1):
+            assert torch.equal(a, c)
+        e0 = ops.time4_fwd(x, W, U, b, False, all_h, 3)[0]
+        # inference (nothing saved): the same states up to the compiler's contraction choices
+        torch.testing.assert_close(e0, r0[0], atol=1e-4, rtol=1e-4)
+    b0 = ops.time4_bwd(dh, x, r0[1], r0[2], W, U, True, 0)
+    b1 = ops.time4_bwd(dh, x, r0[1], r0[2], W, U, True, 3)
+    assert torch.equal(b0[1], b1[1]) and torch.equal(b0[0][:T], b1[0][:T])
+    n0 = ops.time4_bwd(dh, x, r0[1], r0[2], W, U, False, 3)
+    assert n0[0].numel() == 0 and torch.equal(n0[1], b0[1])
+
+
+@pytest.mark.parametrize("frozen", [False, True])
+def test_timelayer_time_major_last128_matches_sequence_major(cuda_device, monkeypatch, frozen):
+    """TimeLayer.forward_time_major with time4 on the standalone time-major kernels (GNNQC_T4_TM=1)
+    vs the sequence-major lstm_fwd<128> path: outputs and gradients within bf16 rounding."""
+    from gnnqc.models.timelayer import TimeLayer
+    torch.manual_seed(1)
+    tl = TimeLayer(20, 16, 2, "lstm", pool_size=3).to(cuda_device)
+    for p in tl.parameters():
+        p.requires_grad_(not frozen)
+    M, T = 300, 180
+    Mp = (M + 15) // 16 * 16
+    x = torch.zeros(T, Mp, 20, device=cuda_device)
+    x[:, :M] = torch.randn(T, M, 20, device=cuda_device)
+    monkeypatch.setenv("GNNQC_CHAIN", "0")
+
+    def run(on):
+        monkeypatch.setenv("GNNQC_T4_TM", "1" if on else "0")
+        xi = x.clone().requires_grad_(True)
+        for p in tl.parameters():
+            p.grad = None
+        out = tl.forward_time_major(xi, M)
+        out.pow(2).sum().backward()
+        return out.detach(), [xi.grad.clone()] + [p.grad.clone() for p in tl.parameters() if p.requires_grad]
+
+    o0, g0 = run(False)
+    o1, g1 = run(True)
+    assert o1.shape == o0.shape == (M, 128)
+    assert (o1 - o0).abs().max().item() < 2e-2
+    for a, b_ in zip(g1, g0):
+        assert (a - b_).norm().item() <= 3e-2 * (b_.norm().item() + 1e-6)
