@@ -32,6 +32,17 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Virtual block index for hardware block L of an N-block launch such that the `group` virtual
+// blocks g * group ... g * group + group - 1 run on ONE XCD (blocks are dealt round-robin over the
+// 8 XCDs: L and L + 8 share one). For launches whose groups re-read the same tiles (e.g. the
+// column blocks of one row split): each XCD's L2 then serves the re-reads instead of all 8 XCDs
+// fetching the tile from HBM. Identity unless N is a multiple of 8 * group.
+__device__ __forceinline__ int xcd_group_remap(int L, int N, int group) {
+  if (group <= 1 || N % (8 * group) != 0) return L;
+  const int x = L & 7, k = L >> 3;      // the k-th block dealt to x's XCD
+  return ((k / group) * 8 + x) * group + k % group;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

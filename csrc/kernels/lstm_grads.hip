@@ -35,8 +35,14 @@ __global__ __launch_bounds__(256) void lstm_grads_kernel(
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ ws, long rows, long period,
     long hshift, int Din, int ldx, long dx_cb_stride, int lddx, int xg, long x_elems) {
   __shared__ __attribute__((aligned(16))) char smem[GradsLds<H, DT>::BYTES];
+  // the column blocks of a row split share its x / h_{t-1} tiles: keep them on one XCD
+#ifndef GQ_GRADS_NO_XCD
+  const int v = xcd_group_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y, gridDim.x);
+#else
+  const int v = blockIdx.x + gridDim.x * blockIdx.y;      // (A/B: dispatch order)
+#endif
   lstm_grads_body<H, DT, GRX, false, ZT>(dz, x, hseq, W, dx, ws, rows, period, hshift, Din, ldx, dx_cb_stride, lddx,
-                                         xg, x_elems, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, smem);
+                                         xg, x_elems, v % gridDim.x, v / gridDim.x, gridDim.x, gridDim.y, smem);
 }
 
 __global__ __launch_bounds__(256) void lstm_grads_reduce_kernel(const float* __restrict__ ws, int splits, int RC,

@@ -60,8 +60,10 @@ TORCH_LIBRARY(gnnqc, m) {
         "Tensor y, Tensor mask, int M, float alpha1, float alpha2, float w0, float w1, Tensor(a!)[] hgrads) -> Tensor[]");
   m.def("time4_trace(Tensor like) -> Tensor");
   m.def("time4_fwd(Tensor x, Tensor W, Tensor U, Tensor b, bool train, bool all_h, int max_blocks=0) -> Tensor[]");
-  m.def("time4_bwd(Tensor dh, Tensor x, Tensor g, Tensor c, Tensor W, Tensor U, bool need_dz, int max_blocks=0) "
-        "-> Tensor[]");
+  m.def("time4_bwd(Tensor dh, Tensor x, Tensor g, Tensor c, Tensor W, Tensor U, bool need_dz, int max_blocks=0, "
+        "Tensor? row_scale=None) -> Tensor[]");
+  m.def("time4_prob_fwd(Tensor x, Tensor W, Tensor U, Tensor b, Tensor[] head, float alpha1, float alpha2, int M, "
+        "bool train, int max_blocks=0) -> Tensor[]");
   m.def("lstm_tm_bwd_pipe(Tensor dh, Tensor g, Tensor c, Tensor W, Tensor U, int T, Tensor gz, Tensor gx, "
         "Tensor gh, Tensor gW, int g_period, int g_hshift, Tensor gws, Tensor rws, Tensor rW, Tensor(a!) rdW, "
         "Tensor(b!) rdU, Tensor(c!) rdb) -> Tensor");

@@ -43,6 +43,9 @@ struct T4Args {
   float* c;                              // train: [T][tiles][NW][CPL][64][2]: c_t, c_{t-1} (CG: [..][64] c_t)
   uint2* gb;                             // CG train: [T][tiles][NW][CPL][64] packed bf16 gates
   const float* dhT;                      // CG backward: [Mp][H] gradient of the last state
+  const float* dhs;                      // CG backward (optional): [Mp] row scales of dhT
+  float* prob;                           // CG forward with the head: [Mp] sigmoid outputs
+  float* dhg;                            //   and [Mp][H] d prob / d h_{T-1}
   __bf16* dz;                            // backward: [T + 1][Mp][4H] bf16
   float* dx;                             // backward: [T][Mp][Din]
   int T, Mp, Din, Dw, ntiles;
@@ -62,13 +65,75 @@ __device__ __forceinline__ size_t t4_sidx(int t, int ntiles, int tile, int w, in
 }
 
 // ------------------------------------------------------------------------------------ forward
-template <int KX>
+// LDS of the integrated-gradients head epilogue (t4_prob_head): part [2][16][AP], z1, a1 / dz1,
+// dz2 [16][AP], dh [16][F + 4], the W1 / W2 images
+template <int F>
+struct T4ProbLds {
+  static constexpr int BYTES = (5 * 16 * CH_AP + 16 * (F + 4) + (F + CH_HU) * CH_WP) * 4;
+};
+
+// Integrated-gradients epilogue of the standalone forward (CG with a head): the head's sigmoid
+// output p of the tile's 16 rows (from h_{T-1} in hl [16][F + 4]) -> prob, and dp / dh_{T-1} ->
+// dhg [Mp][F]: the seed of time4_bwd's recurrence for d sum(p) / dx (rows >= M: p = 0, dh = 0).
+// Replaces head_prob_fwd / head_prob_bwd (two launches, ~90 us on a 32k-row IG pass). staged:
+// the W1 / W2 images in the scratch are still those of an earlier tile of this workgroup.
+template <int F>
+__device__ __forceinline__ void t4_prob_head(const ChainHead hd, int tile, const float* hl, char* scratch, bool staged,
+                                             float* __restrict__ prob, float* __restrict__ dhg) {
+  constexpr int HLP = F + 4, PT = 16 * CH_AP;
+  float* part = reinterpret_cast<float*>(scratch);   // [2][16][AP]
+  float* sz1 = part + 2 * PT;                        // z1
+  float* sa1 = sz1 + PT;                             // leaky(z1), then dz1
+  float* sdz2 = sa1 + PT;                            // dz2
+  float* dh = sdz2 + PT;                             // [16][HLP]
+  float* sW1 = dh + 16 * HLP;                        // [F][WP]
+  float* sW2 = sW1 + F * CH_WP;                      // [64][WP]
+  if (!staged) ch_stage_weights<F>(hd, sW1, sW2);
+  const int tid = ch_tid(), w = tid >> 6, j = tid & 63;
+  const float w3j = hd.W3[j], b3 = hd.b3[0];
+  float z2[2];
+  ch_head_z2<F>(hd, sW1, sW2, hl, part, sz1, sa1, z2);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = w + 8 * q, row = tile * 16 + r;
+    const float z = wave_sum(ch_leaky(z2[q], hd.alpha2) * w3j) + b3;
+    const float p = row < hd.M ? sigmoidf_fast(z) : 0.f;
+    sdz2[r * CH_AP + j] = p * (1.f - p) * w3j * ch_dleaky(z2[q], hd.alpha2);
+    if (j == 0) prob[row] = p;
+  }
+  __syncthreads();
+  {   // da1 = dz2 W2^T
+    const int ot = w & 3, kh = w >> 2;
+    ch_put(part + kh * PT, CH_AP, ot, ch_mm_wt<8>(sW2, CH_WP, ot, kh * 32, sdz2, CH_AP));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = w + 8 * q;
+    const float da = part[r * CH_AP + j] + part[PT + r * CH_AP + j];
+    sa1[r * CH_AP + j] = da * ch_dleaky(sz1[r * CH_AP + j], hd.alpha1);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < F / 16 / CH_NW; ++q) {          // dh = dz1 W1^T
+    const int ot = w + CH_NW * q;
+    ch_put(dh, HLP, ot, ch_mm_wt<16>(sW1, CH_WP, ot, 0, sa1, CH_AP));
+  }
+  __syncthreads();
+  for (int e = tid; e < 16 * F / 4; e += 64 * CH_NW) {
+    const int r = 4 * e / F, k = 4 * e % F;
+    *reinterpret_cast<float4*>(dhg + (size_t)(tile * 16 + r) * F + k) = *reinterpret_cast<const float4*>(dh + r * HLP + k);
+  }
+}
+
+template <int KX, bool CG = false>
 struct T4FwdLds {
   static constexpr int XP = 32 * KX + 8;
   static constexpr int XS = T4MAXT * 16 * XP * 2;        // bf16 input tiles of every step
   static constexpr int HS = 2 * 16 * (T4H + 8) * 2;      // bf16 h_{t-1} (double buffer)
   static constexpr int HL = 16 * T4HP * 4;               // fp32 h_{T-1} for the head
-  static constexpr int WORK = XS + HS + HL + ChainHeadFwdLds<T4H>::BYTES;
+  static constexpr int HEAD = CG ? T4ProbLds<T4H>::BYTES : ChainHeadFwdLds<T4H>::BYTES;
+  static constexpr int WORK = XS + HS + HL + HEAD;
   static constexpr int STAGE = T4H * (T4G + 8) * 2;       // bf16 U (then W) staged for the fragments
   static constexpr int BYTES = WORK > STAGE ? WORK : STAGE;
 };
@@ -105,7 +170,7 @@ __device__ __forceinline__ void t4_stage_rows(__bf16* dst, const float* __restri
 // (grid = tiles) the loop runs once.
 template <bool TRAIN, int KX, bool CG = false>
 __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
-  using L = T4FwdLds<KX>;
+  using L = T4FwdLds<KX, CG>;
   constexpr int XP = L::XP;
   __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
   auto xs = reinterpret_cast<__bf16 (*)[16][XP]>(smem);
@@ -251,7 +316,11 @@ __global__ __launch_bounds__(T4NT) void t4_head_fwd_kernel(T4Args A) {
     t4_mark(A.trace, 2 + min(t, 9));
   }
   __syncthreads();
-  if (A.head) chain_head_fwd<T4H>(A.hd, tile, ntiles, hl, scratch);
+  if constexpr (CG) {
+    if (A.head) t4_prob_head<T4H>(A.hd, tile, hl, scratch, tile != (int)blockIdx.x, A.prob, A.dhg);
+  } else {
+    if (A.head) chain_head_fwd<T4H>(A.hd, tile, ntiles, hl, scratch);
+  }
   __syncthreads();
   if constexpr (!CG) break;              // (grid = tiles)
   }
@@ -311,11 +380,16 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
       }
     }
   };
-  auto load_dhT = [&]() {   // CG: the last state's gradient [Mp][H] -> LDS
+  auto load_dhT = [&]() {   // CG: the last state's gradient [Mp][H] (x the row scales) -> LDS
     const float4* src = reinterpret_cast<const float4*>(A.dhT + (size_t)tile * 16 * T4H);
     for (int e = tid; e < 16 * T4H / 4; e += T4NT) {
       const int r = e / (T4H / 4), k = 4 * (e % (T4H / 4));
-      *reinterpret_cast<float4*>(dhT + r * T4HP + k) = src[e];
+      float4 v = src[e];
+      if (A.dhs != nullptr) {
+        const float sc = A.dhs[tile * 16 + r];
+        v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+      }
+      *reinterpret_cast<float4*>(dhT + r * T4HP + k) = v;
     }
   };
   load_slot(0, T - 1);
@@ -722,10 +796,71 @@ std::vector<at::Tensor> time4_fwd(const at::Tensor& x, const at::Tensor& W, cons
   return {h, g, c};
 }
 
+// time4 + the frozen Dense head for integrated gradients: x [T, Mp, Din]; head = [W1, b1, W2, b2, W3,
+// b3] (Dense(128,64)-LeakyReLU(alpha1)-Dense(64,64)-LeakyReLU(alpha2)-Dense(64,1)-sigmoid). Returns
+// [prob [Mp], dh [Mp, 128] = d prob / d h_{T-1} (rows >= M zero), g, c]: time4_bwd(dh, ...,
+// row_scale = d loss / d prob) then gives the input gradient without a head backward launch.
+std::vector<at::Tensor> time4_prob_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
+                                       at::TensorList head, double alpha1, double alpha2, int64_t M, bool train,
+                                       int64_t max_blocks) {
+  int T, Mp, Din, Dw;
+  t4_check(x, W, U, T, Mp, Din, Dw);
+  check_f32_cuda(b, "b");
+  TORCH_CHECK(b.numel() == T4G, "time4_prob_fwd: bias size");
+  TORCH_CHECK(head.size() == 6, "time4_prob_fwd: expected W1, b1, W2, b2, W3, b3");
+  for (const at::Tensor& t : head) check_f32_cuda(t, "time4_prob_fwd head weight");
+  TORCH_CHECK(head[0].numel() == (long)T4H * CH_HU && head[1].numel() == CH_HU && head[2].numel() == CH_HU * CH_HU &&
+                  head[3].numel() == CH_HU && head[4].numel() == CH_HU && head[5].numel() == 1,
+              "time4_prob_fwd: expected Dense(128,64)-Dense(64,64)-Dense(64,1)");
+  TORCH_CHECK(M >= 1 && M <= Mp, "time4_prob_fwd: rows");
+  c10::DeviceGuard guard(x.device());
+  auto opt = x.options();
+  const int ntiles = Mp / 16;
+  const long cells = (long)T * Mp * T4H;
+  at::Tensor h = at::empty({Mp, T4H}, opt), prob = at::empty({Mp}, opt), dh = at::empty({Mp, T4H}, opt);
+  at::Tensor g = train ? at::empty({cells * 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  at::Tensor c = train ? at::empty({cells}, opt) : at::empty({0}, opt);
+  T4Args A{};
+  A.x = x.data_ptr<float>();
+  A.W = W.data_ptr<float>();
+  A.U = U.data_ptr<float>();
+  A.b = b.data_ptr<float>();
+  A.h = h.data_ptr<float>();
+  A.gb = train ? reinterpret_cast<uint2*>(g.data_ptr()) : nullptr;
+  A.c = train ? c.data_ptr<float>() : nullptr;
+  A.T = T;
+  A.Mp = Mp;
+  A.Din = Din;
+  A.Dw = Dw;
+  A.ntiles = ntiles;
+  A.hlast = 1;
+  A.head = 1;
+  A.prob = prob.data_ptr<float>();
+  A.dhg = dh.data_ptr<float>();
+  A.hd.W1 = head[0].data_ptr<float>();
+  A.hd.b1 = head[1].data_ptr<float>();
+  A.hd.W2 = head[2].data_ptr<float>();
+  A.hd.b2 = head[3].data_ptr<float>();
+  A.hd.W3 = head[4].data_ptr<float>();
+  A.hd.b3 = head[5].data_ptr<float>();
+  A.hd.M = (int)M;
+  A.hd.alpha1 = (float)alpha1;
+  A.hd.alpha2 = (float)alpha2;
+  const dim3 grid(t4_grid(ntiles, max_blocks));
+  const int KX = (Din + 31) / 32;
+#define GQ_T4F(TR, K) hipLaunchKernelGGL((t4_head_fwd_kernel<TR, K, true>), grid, dim3(T4NT), 0, stream(), A)
+  if (train) { if (KX == 1) GQ_T4F(true, 1); else GQ_T4F(true, 2); }
+  else { if (KX == 1) GQ_T4F(false, 1); else GQ_T4F(false, 2); }
+#undef GQ_T4F
+  GQ_LAUNCH_CHECK();
+  return {prob, dh, g, c};
+}
+
 // dh [Mp, 128]: gradient of the last state; x / g / c from time4_fwd(train). Returns [dz, dx]:
 // dz [T + 1, Mp, 512] bf16 for lstm_tm_grads when need_dz (else empty), dx [T, Mp, Din].
 std::vector<at::Tensor> time4_bwd(const at::Tensor& dh, const at::Tensor& x, const at::Tensor& g, const at::Tensor& c,
-                                  const at::Tensor& W, const at::Tensor& U, bool need_dz, int64_t max_blocks) {
+                                  const at::Tensor& W, const at::Tensor& U, bool need_dz, int64_t max_blocks,
+                                  const c10::optional<at::Tensor>& row_scale) {
   int T, Mp, Din, Dw;
   t4_check(x, W, U, T, Mp, Din, Dw);
   check_f32_cuda(dh, "dh");
@@ -747,6 +882,11 @@ std::vector<at::Tensor> time4_bwd(const at::Tensor& dh, const at::Tensor& x, con
   A.gb = reinterpret_cast<uint2*>(const_cast<void*>(g.data_ptr()));
   A.c = const_cast<float*>(c.data_ptr<float>());
   A.dhT = dh.data_ptr<float>();
+  if (row_scale.has_value() && row_scale->defined()) {
+    check_f32_cuda(*row_scale, "row_scale");
+    TORCH_CHECK(row_scale->numel() == Mp, "time4_bwd: row_scale must have Mp entries");
+    A.dhs = row_scale->data_ptr<float>();
+  }
   A.dz = need_dz ? bf16_ptr(dz) : nullptr;
   A.dx = dx.data_ptr<float>();
   A.T = T;
@@ -771,4 +911,5 @@ TORCH_LIBRARY_IMPL(gnnqc, CUDA, m) {
   m.impl("time4_trace", &gq::time4_trace);
   m.impl("time4_fwd", &gq::time4_fwd);
   m.impl("time4_bwd", &gq::time4_bwd);
+  m.impl("time4_prob_fwd", &gq::time4_prob_fwd);
 }

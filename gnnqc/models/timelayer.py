@@ -95,7 +95,7 @@ class TimeLayer(nn.Module):
             h = F.pad(h, (0, cpad, 0, Mp - M))
         return self.forward_time_major(h.contiguous(), M)
 
-    def forward_time_major(self, h: torch.Tensor, M: int) -> torch.Tensor:
+    def forward_time_major(self, h: torch.Tensor, M: int, last=None) -> torch.Tensor:
         """LSTM branch on a time-major input ``[T, Mp, C]`` (Mp = M rounded up to 16, zero
         rows past M; C may carry zero channels past the first layer's input width).
         Returns ``[M, out_features]``. Producers that can write this layout directly (the
@@ -148,7 +148,8 @@ class TimeLayer(nn.Module):
                     return h[:M]
                 continue
             if tm and last128_eligible(h, mod):      # time4 (H = 128, last state) on the time-major input
-                return lstm_last128_tm(h, mod)[:M]
+                # (``last(h, mod)``: the caller takes this layer over, e.g. fused with a frozen head)
+                return last(h, mod) if last is not None else lstm_last128_tm(h, mod)[:M]
             if tm:                                   # leave time-major: [T, Mp, C] -> [M, T, C]
                 h = h.transpose(0, 1)
                 if h.shape[0] != M:                  # (a no-op slice would still cost a zero-fill + copy in backward)

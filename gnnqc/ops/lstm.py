@@ -868,6 +868,42 @@ class _HipLSTMLast128(torch.autograd.Function):
         return (dx if need[0] else None, *grads)
 
 
+class _HipLSTMLast128Prob(torch.autograd.Function):
+    """time4 (as :class:`_HipLSTMLast128`) + the FROZEN Dense head for integrated gradients:
+    ``time4_prob_fwd`` returns the head's sigmoid outputs and, from the same launch,
+    d prob / d h_{T-1}; the backward scales those rows by d loss / d prob and runs the time4
+    recurrence (``time4_bwd`` row_scale): input gradient only (weights and head frozen)."""
+
+    @staticmethod
+    def forward(ctx, x, W, U, b, head, alphas, M):
+        from ..utils.native import hip_ops
+        x = x.contiguous()
+        need = bool(ctx.needs_input_grad[0])
+        prob, dh, g, c = hip_ops().time4_prob_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(),
+                                                  [t.contiguous() for t in head], float(alphas[0]),
+                                                  float(alphas[1]), int(M), need)
+        if need:
+            ctx.save_for_backward(x, W, U, g, c, dh)
+        ctx.M = int(M)
+        return prob[:M]
+
+    @staticmethod
+    def backward(ctx, dprob):
+        from ..utils.native import hip_ops
+        x, W, U, g, c, dh = ctx.saved_tensors
+        scale = torch.nn.functional.pad(dprob.float(), (0, x.shape[1] - ctx.M)).contiguous()
+        _, dx = hip_ops().time4_bwd(dh, x, g, c, W.contiguous(), U.contiguous(), False, 0, scale)
+        return dx, None, None, None, None, None, None
+
+
+def lstm_last128_prob_tm(x_tm: torch.Tensor, mod, head, alphas, M: int) -> torch.Tensor:
+    """Sigmoid outputs [M] of LSTM module ``mod`` (H = 128, last state; see ``last128_eligible``) and
+    the frozen head ``head`` = [W1, b1, W2, b2, W3, b3] with LeakyReLU slopes ``alphas``."""
+    if any(t.requires_grad for t in [mod.kernel, mod.recurrent_kernel, mod.bias, *head]):
+        raise ValueError("lstm_last128_prob_tm: weights must be frozen (integrated gradients)")
+    return _HipLSTMLast128Prob.apply(x_tm, mod.kernel, mod.recurrent_kernel, mod.bias, tuple(head), tuple(alphas), int(M))
+
+
 def last128_eligible(x: torch.Tensor, mod) -> bool:
     """Whether :class:`_HipLSTMLast128` takes LSTM module ``mod`` on time-major ``x`` [T, Mp, Din]
     (``GNNQC_T4_TM=0``: the sequence-major kernels)."""
@@ -898,5 +934,5 @@ def lstm_layer(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tenso
 
 __all__ = ["unflagged_grad_writes", "lstm_layer", "lstm_eager", "lstm_layer_tm", "lstm_pair_tm", "lstm_chain_tm", "chain_fits", "tm_eligible",
            "chain_capacity", "chain_ctl", "check_chain", "ChainTimeoutError", "lstm_chain_head_tm",
-           "lstm_last128_tm", "last128_eligible",
+           "lstm_last128_tm", "lstm_last128_prob_tm", "last128_eligible",
            "direct_grad_accumulation"]

@@ -303,9 +303,26 @@ class IntegratedGradients:
             h0 = ops.ig_gcn_pool_fwd(x, w, anom, g.kernel.contiguous(), g.bias.contiguous(), st[2].contiguous(),
                                      st[3].contiguous(), g.prelu_alpha.contiguous(), a, int(Cp))
         h0.requires_grad_(True)
-        feat = m.time_layer.forward_time_major(h0, kk * B)
         spec = m.head_spec()
-        if (spec is not None and feat.dim() == 2 and feat.shape[1] in (32, 64, 128) and feat.dtype == torch.float32
+        taken = []
+        last = None
+        if (spec is not None and os.environ.get("GNNQC_IG_T4_HEAD", "1") == "1"
+                and tuple(spec[0].kernel.shape) == (128, 64) and tuple(spec[1].kernel.shape) == (64, 64)
+                and tuple(spec[2].kernel.shape) == (64, 1) and all(d.bias is not None for d in spec[:3])):
+            # time4 + the frozen head in one launch (time4_prob_fwd: sigmoid outputs and d p / d h_{T-1}),
+            # the recurrence backward seeded with it (no head launches)
+            from ..ops.lstm import lstm_last128_prob_tm
+            head_w = [spec[0].kernel, spec[0].bias, spec[1].kernel, spec[1].bias, spec[2].kernel, spec[2].bias]
+
+            def last(hin, mod):
+                taken.append(True)
+                return lstm_last128_prob_tm(hin, mod, head_w, (spec[3], spec[4]), kk * B)
+
+        feat = m.time_layer.forward_time_major(h0, kk * B, last=last)
+        if taken:
+            y = feat
+            (gh,) = torch.autograd.grad(y.sum(), h0)
+        elif (spec is not None and feat.dim() == 2 and feat.shape[1] in (32, 64, 128) and feat.dtype == torch.float32
                 and spec[0].kernel.shape[1] == 64 and tuple(spec[1].kernel.shape) == (64, 64)
                 and tuple(spec[2].kernel.shape) == (64, 1) and os.environ.get("GNNQC_IG_HEAD_HIP", "1") == "1"):
             # the frozen head on HIP (head.hip, PROB mode): sigmoid outputs, then d sum(sigmoid) / d feat

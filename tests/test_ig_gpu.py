@@ -166,3 +166,38 @@ def test_ig_hip_head_matches_torch_head(cuda_device, cml_windows, monkeypatch):
     for k in ("grad_x", "grad_anom", "pred", "path_pred"):
         err = (res["1"][k] - res["0"][k]).abs().max().item()
         assert err <= 1e-5 * res["0"][k].abs().max().item() + 1e-7, (k, err)
+
+
+def test_ig_time4_fused_head_matches_separate_head(cuda_device, cml_windows, monkeypatch):
+    """The path-folded IG with time4 + the frozen head in one launch (GNNQC_IG_T4_HEAD=1, default:
+    time4_prob_fwd -> sigmoid outputs and d p / d h_{T-1}; time4_bwd seeded with them) == time4 alone
+    followed by the head_prob kernels (GNNQC_IG_T4_HEAD=0); and the fused launch really ran."""
+    from gnnqc import config as C
+    from gnnqc.data.store import DeviceStore
+    from gnnqc.models import GCNClassifier
+    from gnnqc.ops import lstm as L
+    from gnnqc.xai.ig import IntegratedGradients
+    pc, ws = cml_windows
+    torch.manual_seed(11)
+    model = GCNClassifier(C.default("model_cml"), pc).to(cuda_device)
+    with torch.no_grad():
+        model.dense_out.bias.fill_(0.3)
+    st = DeviceStore(ws, "rolling_median", pc.graph, device=cuda_device)
+    b = st.gather(torch.tensor([3, 8, 21, 33, 34], device=cuda_device))
+    calls = []
+    orig = L._HipLSTMLast128Prob.forward
+
+    def spy(ctx, *a):
+        calls.append(1)
+        return orig(ctx, *a)
+
+    monkeypatch.setattr(L._HipLSTMLast128Prob, "forward", staticmethod(spy))
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GNNQC_IG_T4_HEAD", flag)
+        res[flag] = IntegratedGradients(model, "cml", m_steps=24, use_graph=False).attribute(b)
+    torch.cuda.synchronize()
+    assert calls, "the fused time4 + head path did not run"
+    for k in ("grad_x", "grad_anom", "pred", "path_pred"):
+        err = (res["1"][k] - res["0"][k]).abs().max().item()
+        assert err <= 1e-4 * res["0"][k].abs().max().item() + 1e-7, (k, err)
