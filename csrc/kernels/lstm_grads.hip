@@ -100,11 +100,14 @@ void lstm_grads_rows(const void* dz, int zbf, const float* x, const float* hseq,
   const int ncb = (4 * H) / GR_CB;
   const long ntiles = (rows + GR_ROWS - 1) / GR_ROWS;
   // ~2 tiles per workgroup for small row counts (latency: everything in flight at once),
-  // up to ~8 workgroups per CU for large ones. The split count depends only on the shape
-  // and the reduce kernel sums in a fixed order: bitwise reproducible in every mode.
+  // ~2 workgroups per CU for large ones: each split writes a (DT + HT) x 4H record that the
+  // reduction reads back, so more splits cost record traffic (SoilNet, 8.5k sequences x 12-37
+  // steps: budget 2048 / 1024 / 512 / 256 -> 2.986 / 2.950 / 2.919 / 3.060 ms per step,
+  // profiles/r6_grads_budget_ab.txt). The split count depends only on the shape and the reduce
+  // kernel sums in a fixed order: bitwise reproducible in every mode.
   static const int wg_budget = [] {            // workgroups per pass (A/B: GNNQC_GRADS_WG)
     const char* e = std::getenv("GNNQC_GRADS_WG");
-    return e != nullptr ? std::max(256, std::atoi(e)) : 2048;
+    return e != nullptr ? std::max(256, std::atoi(e)) : 512;
   }();
   const int splits = (int)std::max<long>(1, std::min<long>((ntiles + 1) / 2, std::max(64, wg_budget / ncb)));
   const int DT = (Din + 1 + 15) / 16;
