@@ -59,6 +59,12 @@ for step in "$@"; do
                     $PY "$ROOT/bench.py" --steps 40 --warmup 5 --no-knn-line --no-ig-line --no-cv-line --no-soil-line --no-graph ;;
         stats_ig) prof stats_ig 400 --kernel-trace --stats -d "$OUT/prof_stats_ig" -o run --output-format csv -- \
                     $PY "$ROOT/scripts/bench_ig.py" ;;
+        pmc_ig) prof pmc_ig 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_ig" -o run --output-format csv -- \
+                    $PY "$ROOT/scripts/bench_ig.py" --batches 2 ;;
+        pmc_ig_mem) prof pmc_ig_mem 120 --kernel-trace --pmc FETCH_SIZE -d "$OUT/prof_pmc_ig_mem" -o run \
+                    --output-format csv -- $PY "$ROOT/scripts/bench_ig.py" --batches 2 ;;
+        pmc_ig_wr) prof pmc_ig_wr 120 --kernel-trace --pmc WRITE_SIZE -d "$OUT/prof_pmc_ig_wr" -o run \
+                    --output-format csv -- $PY "$ROOT/scripts/bench_ig.py" --batches 2 ;;
         stats_soil) prof stats_soil 400 --kernel-trace --stats -d "$OUT/prof_stats_soil" -o run --output-format csv -- \
                     $PY "$ROOT/bench.py" --ds soilnet --steps 20 --warmup 3 --no-graph ;;
         pmc_cml) prof pmc_cml 120 --kernel-trace --pmc $PMC_SQ -d "$OUT/prof_pmc_cml" -o run --output-format csv -- \
