@@ -1,4 +1,4 @@
-import sys; sys.path.insert(0,'/tmp/lds')
+import sys; sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.abspath(__file__)))
 from sim import cycles, ideal
 def analyze(H, KX, Din, zpitch_extra=8, dxs_pitch=None, dxs_T=False, dhs_pad=4, xr_pad=8, hr_pad=8):
     G4 = 4*H; NT = 16*H; NW = NT//64; KB = G4//32; KPH = ((H+31)//32)*32; KSH = KPH//32

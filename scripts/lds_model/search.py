@@ -1,4 +1,4 @@
-import sys; sys.path.insert(0,'/tmp/lds')
+import sys; sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.abspath(__file__)))
 from bwd import analyze
 cases = ((16,1,24),(16,1,16),(16,1,20),(32,1,16),(32,1,32),(32,1,24))
 def total(**kw):

@@ -1,4 +1,4 @@
-import sys; sys.path.insert(0,'/tmp/lds')
+import sys; sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.abspath(__file__)))
 from sim import cycles, ideal
 def analyze(H, KX, Din, RP=24):
     G4 = 4*H; NT = 16*H; NW = NT//64
