@@ -1071,12 +1071,21 @@ struct ChainBArgs {
 };
 static_assert(sizeof(ChainBArgs) <= 4096, "chain backward kernel arguments");
 
+// LDS pitches of the backward stages (bf16 dz rows G4 + ZPAD, fp32 dx rows 32 KX + XPAD), chosen with
+// scripts/lds_model as in lstm_tm.hip's backward: with a 32-float dx pitch the dx wave's dx^T stores
+// (16 sequences x 4 quads per wave) fell on 2 banks of ds_write_b32's 32 (16-way); 33 leaves 2-way
+#ifndef CHAINB_ZPAD
+#define CHAINB_ZPAD 16
+#endif
+#ifndef CHAINB_XPAD
+#define CHAINB_XPAD 1
+#endif
 template <int H, int KX>
 struct ChainBLds {
   static constexpr bool WL = H >= 32;             // W^T fragments of dx from LDS (VGPR budget)
-  static constexpr int ZS = 2 * 16 * (4 * H + 8) * 2;
+  static constexpr int ZS = 2 * 16 * (4 * H + CHAINB_ZPAD) * 2;
   static constexpr int DH = 2 * 16 * TMC<H>::HP * 4;
-  static constexpr int DX = 2 * 16 * 32 * KX * 4;
+  static constexpr int DX = 2 * 16 * (32 * KX + CHAINB_XPAD) * 4;
   static constexpr int WB = WL ? 2 * KX * 16 * (4 * H + 8) * 2 : 0;
   static constexpr int BYTES = ZS + DH + DX + WB;
 };
@@ -1088,7 +1097,7 @@ struct ChainBLds {
 template <int H, int KX>
 struct ChainBLdsSK {
   static constexpr int NW = TMC<H>::NW, UT = H / 16, KG = NW / UT, NXB = 2 * KX, KXG = NW / NXB;
-  static constexpr int ZS = 2 * 16 * (4 * H + 8) * 2;
+  static constexpr int ZS = 2 * 16 * (4 * H + CHAINB_ZPAD) * 2;
   static constexpr int DH = 2 * 16 * TMC<H>::HP * 4;
   static constexpr int DP = KG * 16 * TMC<H>::HP * 4;
   static constexpr int XPP = 32 * KX + 4;              // xpart row pitch
@@ -1192,9 +1201,9 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   static_assert(!SK || (NW % UT == 0 && KB % KG == 0 && NW % NXB == 0 && KB % KXG == 0), "split-K tiling");
   static_assert(L::BYTES <= CHAINB_LDS_STAGE && LK::BYTES <= CHAINB_LDS_STAGE && L::ZS % 16 == 0 && L::DH % 16 == 0,
                 "chain bwd LDS layout");
-  auto zs = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem);
+  auto zs = reinterpret_cast<__bf16 (*)[16][G4 + CHAINB_ZPAD]>(smem);
   auto dhs = reinterpret_cast<float (*)[16][C::HP]>(smem + L::ZS);
-  auto dxs = reinterpret_cast<float (*)[16][32 * KX]>(smem + L::ZS + L::DH);
+  auto dxs = reinterpret_cast<float (*)[16][32 * KX + CHAINB_XPAD]>(smem + L::ZS + L::DH);
   auto wl = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem + L::ZS + L::DH + L::DX);
   auto dpart = reinterpret_cast<float (*)[16][C::HP]>(smem + LK::ZS + LK::DH);                      // [KG]
   auto xpart = reinterpret_cast<float (*)[KXG][16][LK::XPP]>(smem + LK::ZS + LK::DH + LK::DP);      // [2][KXG]

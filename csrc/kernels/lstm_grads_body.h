@@ -10,6 +10,15 @@ namespace gq {
 constexpr int GR_ROWS = 32;         // rows (sequence, step) per tile = MFMA K
 constexpr int GR_CB = 64;           // gate-units per column block (4 waves x 16)
 constexpr int GR_LDR = GR_ROWS + 8; // padded LDS row length (bf16) of transposed images
+// Staging map of the per-tile register images: GR_SEQ_FAST = 1 gives consecutive lanes consecutive
+// row pairs of ONE channel / gate-unit quad, so the packed (rows 2p, 2p + 1) stores into the
+// transposed images hit consecutive dwords (with consecutive lanes on consecutive channels the 32
+// lanes of a ds_write_b32 group land on 2-4 banks: 8- to 16-way, scripts/lds_model/grads.py), but
+// the global loads then read 16 rows x 16-32 B per wave instead of whole rows. Measured slightly
+// slower (SoilNet 2.737 vs 2.724 ms, profiles/r6_grads_stage_map_ab.txt): off.
+#ifndef GR_SEQ_FAST
+#define GR_SEQ_FAST 0
+#endif
 
 // a weight-gradient pass (lstm_grads_body) and its split reduction as kernel-argument records
 struct GradJob {
@@ -138,7 +147,10 @@ __device__ __forceinline__ void lstm_grads_body(
   float rx[GRX == 4 ? 1 : XGM][GRX];
   float4 rxp[GRX == 4 ? XGP : 1][2];
   float4 rh[HG][2];                 // h_{t-1}: rows 2p and 2p + 1 of unit quad c (item = p * H/4 + c)
-  const int zr = tid >> 4, zc = (tid & 15) * 4;
+  const int zr = GR_SEQ_FAST ? (tid & 15) : (tid >> 4), zc = (GR_SEQ_FAST ? (tid >> 4) : (tid & 15)) * 4;
+  // (x / h_{t-1} items: row pair and channel quad of item `it`)
+  auto it_pair = [&](int it, int nq) { return GR_SEQ_FAST ? (it & 15) : it / nq; };
+  auto it_quad = [&](int it, int nq) { return GR_SEQ_FAST ? (it >> 4) : it % nq; };
   const long xspan = (long)GR_ROWS * ldx;
   // x_elems: floats readable from x (a strided view may end before rows * ldx)
   const long xlast = (x_elems - GRX) / GRX * GRX, hlast = rows * (long)H - 4;
@@ -164,7 +176,7 @@ __device__ __forceinline__ void lstm_grads_body(
       for (int i = 0; i < XGP; ++i) {
         if (i < xg) {                             // kernel argument: a scalar (uniform) branch
           const int it = min(tid + 256 * i, nit - 1);
-          const long o = (r0 + 2 * (it / nq)) * ldx + 4 * (it % nq);
+          const long o = (r0 + 2 * it_pair(it, nq)) * ldx + 4 * it_quad(it, nq);
           rxp[i][0] = *reinterpret_cast<const float4*>(x + min(o, xlast));
           rxp[i][1] = *reinterpret_cast<const float4*>(x + min(o + ldx, xlast));
         }
@@ -181,7 +193,7 @@ __device__ __forceinline__ void lstm_grads_body(
 #pragma unroll
     for (int i = 0; i < HG; ++i) {
       const int it = min(tid + 256 * i, GR_ROWS / 2 * H / 4 - 1);     // (idle lanes re-read the last item)
-      const long o = (r0 - hshift + 2 * (it / (H / 4))) * H + 4 * (it % (H / 4));
+      const long o = (r0 - hshift + 2 * it_pair(it, H / 4)) * H + 4 * it_quad(it, H / 4);
       rh[i][0] = *reinterpret_cast<const float4*>(hseq + min(max(o, 0L), hlast));
       rh[i][1] = *reinterpret_cast<const float4*>(hseq + min(max(o + H, 0L), hlast));
     }
@@ -201,8 +213,10 @@ __device__ __forceinline__ void lstm_grads_body(
       const bf16x4_t b = bf16x4_t{(__bf16)(rz[1].x * m1), (__bf16)(rz[1].y * m1), (__bf16)(rz[1].z * m1),
                                   (__bf16)(rz[1].w * m1)};
       if constexpr (!CH) {
-        *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = a;
-        *reinterpret_cast<bf16x4_t*>(&dzR[rr + 1][zc]) = b;
+        if (dx != nullptr) {   // (uniform) the row-major copy feeds only the dx products
+          *reinterpret_cast<bf16x4_t*>(&dzR[rr][zc]) = a;
+          *reinterpret_cast<bf16x4_t*>(&dzR[rr + 1][zc]) = b;
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16x2_t*>(&dzT[zc + j][rr]) = bf16x2_t{a[j], b[j]};
@@ -214,7 +228,7 @@ __device__ __forceinline__ void lstm_grads_body(
       for (int i = 0; i < XGP; ++i) {
         const int it = tid + 256 * i;
         if (i < xg && it < nit) {                 // one packed bf16x2 (rows 2p, 2p + 1) per channel
-          const int rr = 2 * (it / nq), d0 = 4 * (it % nq);
+          const int rr = 2 * it_pair(it, nq), d0 = 4 * it_quad(it, nq);
           const float ma = (r0 + rr < rows) ? 1.f : 0.f, mb = (r0 + rr + 1 < rows) ? 1.f : 0.f;
           const float a[4] = {rxp[i][0].x, rxp[i][0].y, rxp[i][0].z, rxp[i][0].w};
           const float b[4] = {rxp[i][1].x, rxp[i][1].y, rxp[i][1].z, rxp[i][1].w};
@@ -241,7 +255,7 @@ __device__ __forceinline__ void lstm_grads_body(
       // one packed bf16x2 (rows 2p, 2p + 1) per unit: conflict-free across a wave's lanes
       const int it = tid + 256 * i;
       if (it < GR_ROWS / 2 * H / 4) {
-        const int rr = 2 * (it / (H / 4)), k0 = 4 * (it % (H / 4));
+        const int rr = 2 * it_pair(it, H / 4), k0 = 4 * it_quad(it, H / 4);
         const long ra = r0 + rr, rb = ra + 1;
         const float ma = (ra < rows && ra % period >= hshift) ? 1.f : 0.f;
         const float mb = (rb < rows && rb % period >= hshift) ? 1.f : 0.f;

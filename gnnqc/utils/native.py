@@ -20,6 +20,9 @@ HOST_LIB = os.path.join(LIB_DIR, "libgnnqc_host.so")
 # GNNQC_HIP_LIB: an alternative build of the HIP library (A/B measurements of compile-time variants,
 # scripts/build_chain_variants.py); unset in every normal run
 HIP_LIB = os.environ.get("GNNQC_HIP_LIB") or os.path.join(LIB_DIR, "libgnnqc_hip.so")
+if not os.path.isabs(HIP_LIB) and not os.path.exists(HIP_LIB):
+    # (a relative variant path is taken from the repository root, whatever the working directory)
+    HIP_LIB = os.path.join(os.path.dirname(os.path.dirname(LIB_DIR)), HIP_LIB)
 
 _lock = threading.Lock()
 _host = None

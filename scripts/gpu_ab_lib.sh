@@ -12,7 +12,7 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   && for r in 1 2; do
     for v in new old; do
       if [ $v = old ]; then export GNNQC_HIP_LIB=$V; else unset GNNQC_HIP_LIB; fi
-      timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-ig-line --no-cv-line \
+      timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-ig-line --no-cv-line --no-soil-line \
         > gpurun_out/bench_ab_${v}_$r.log 2>&1 || exit 3
       echo "$v run $r: $(grep -m1 -o '"ms_per_step": [0-9.]*' gpurun_out/bench_ab_${v}_$r.log)"
     done

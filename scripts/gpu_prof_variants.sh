@@ -10,7 +10,7 @@ for spec in $VARIANTS; do
   (
     for a in ${kv//,/ }; do [ "$a" != "-" ] && export "$a"; done
     cd /tmp && TMPDIR=/tmp timeout -k 10 200 rocprofv3 --kernel-trace -d "$ROOT/gpurun_out/prof_$name" -o run \
-      --output-format csv -- python3 "$ROOT/bench.py" --steps ${STEPS:-40} --warmup 5 --no-knn-line --no-ig-line \
+      --output-format csv -- python3 "$ROOT/bench.py" --steps ${STEPS:-40} --warmup 5 --no-knn-line --no-ig-line --no-soil-line \
       --no-cv-line > "$ROOT/gpurun_out/prof_$name.log" 2>&1
   ) || { tail -5 gpurun_out/prof_$name.log; exit 3; }
   python3 scripts/graph_steady_state.py gpurun_out/prof_$name > gpurun_out/ss_$name.txt && cat gpurun_out/ss_$name.txt
