@@ -259,7 +259,7 @@ __global__ __launch_bounds__(IGG_BWB * IGG_NMAX) void ig_gcn_pool_bwd_kernel(
     const float* __restrict__ g, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ prelu_a,
     const float* __restrict__ alphas, const float* __restrict__ wts, float* __restrict__ acc_x,
-    float* __restrict__ acc_a, int B, int T, int N, int Ca, int kk, int s_off, int Mp, int Cp) {
+    float* __restrict__ acc_a, int B, int T, int N, int Ca, int kk, int s_off, int Mp, int Cp, int first) {
   constexpr int PC = F + 4;                         // prefix channels: F GCN + 4 anomaly slots
   extern __shared__ __attribute__((aligned(16))) float sP[];   // [IGG_BWB][kk + 1][PC]
   __shared__ float sA[IGG_KMAX];
@@ -290,7 +290,11 @@ __global__ __launch_bounds__(IGG_BWB * IGG_NMAX) void ig_gcn_pool_bwd_kernel(
   __syncthreads();
   if (b >= B) return;
   const float* P = sP + bl * rowp;
-  if (n < Ca) acc_a[((long)b * T + t) * Ca + n] += P[kk * PC + F + n];
+  // (first: this launch writes the accumulators instead of adding - no zero-fill pass before it)
+  if (n < Ca) {
+    float* oa = acc_a + ((long)b * T + t) * Ca + n;
+    *oa = (first ? 0.f : *oa) + P[kk * PC + F + n];
+  }
   if (n >= N) return;
   float xv[Cin];
 #pragma unroll
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(IGG_BWB * IGG_NMAX) void ig_gcn_pool_bwd_kernel(
   }
   float* o = acc_x + (((long)b * T + t) * N + n) * Cin;
 #pragma unroll
-  for (int k = 0; k < Cin; ++k) o[k] += mw * d[k];
+  for (int k = 0; k < Cin; ++k) o[k] = (first ? 0.f : o[k]) + mw * d[k];
 }
 
 #define GQ_IGG_DISPATCH(CIN_RT, F_RT, ...)                                                         \
@@ -386,11 +390,12 @@ at::Tensor ig_gcn_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::T
   return out;
 }
 
-// g = dL/d out [T, Mp, Cp] of ig_gcn_pool_fwd; accumulates into acc_x [B,T,N,Cin] and acc_a [B,T,Ca].
+// g = dL/d out [T, Mp, Cp] of ig_gcn_pool_fwd; accumulates into acc_x [B,T,N,Cin] and acc_a [B,T,Ca]
+// (overwrite: the first launch writes them - uninitialised accumulators need no zero fill).
 void ig_gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& mask, const at::Tensor& g,
                      const at::Tensor& W, const at::Tensor& b, const at::Tensor& scale, const at::Tensor& shift,
                      const at::Tensor& alpha, const at::Tensor& alphas, const at::Tensor& wts, at::Tensor acc_x,
-                     at::Tensor acc_a) {
+                     at::Tensor acc_a, bool overwrite) {
   for (auto* p : {&x, &w, &mask, &g, &W, &b, &scale, &shift, &alpha, &alphas, &wts})
     check_f32_cuda(*p, "ig_gcn_pool_bwd input");
   check_f32_cuda(acc_x, "ig_gcn_pool_bwd acc_x");
@@ -420,7 +425,8 @@ void ig_gcn_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor&
                            mask.data_ptr<float>(), g.data_ptr<float>(), W.data_ptr<float>(), b.data_ptr<float>(),
                            scale.data_ptr<float>(), shift.data_ptr<float>(), alpha.data_ptr<float>(),
                            alphas.data_ptr<float>() + s0, wts.data_ptr<float>() + s0, acc_x.data_ptr<float>(),
-                           Ca ? acc_a.data_ptr<float>() : nullptr, B, T, N, Ca, ks, s0, (int)g.size(1), Cp));
+                           Ca ? acc_a.data_ptr<float>() : nullptr, B, T, N, Ca, ks, s0, (int)g.size(1), Cp,
+                           (overwrite && s0 == 0) ? 1 : 0));
     GQ_LAUNCH_CHECK();
   }
 }

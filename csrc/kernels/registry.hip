@@ -129,7 +129,7 @@ TORCH_LIBRARY(gnnqc, m) {
   m.def("ig_gcn_pool_fwd(Tensor x, Tensor w, Tensor anom, Tensor W, Tensor b, Tensor scale, Tensor shift, "
         "Tensor alpha, Tensor alphas, int Cp) -> Tensor");
   m.def("ig_gcn_pool_bwd(Tensor x, Tensor w, Tensor mask, Tensor g, Tensor W, Tensor b, Tensor scale, Tensor shift, "
-        "Tensor alpha, Tensor alphas, Tensor wts, Tensor(a!) acc_x, Tensor(b!) acc_a) -> ()");
+        "Tensor alpha, Tensor alphas, Tensor wts, Tensor(a!) acc_x, Tensor(b!) acc_a, bool overwrite=False) -> ()");
   m.def("ig_accum(Tensor(a!) acc, Tensor g, Tensor w) -> ()");
   m.def("ig_finalize(Tensor acc, Tensor v, int mode) -> Tensor");
   m.def("chain_poison(Tensor(a!) g, Tensor ext) -> ()");

@@ -43,7 +43,8 @@ struct T4Args {
   float* c;                              // train: [T][tiles][NW][CPL][64][2]: c_t, c_{t-1} (CG: [..][64] c_t)
   uint2* gb;                             // CG train: [T][tiles][NW][CPL][64] packed bf16 gates
   const float* dhT;                      // CG backward: [Mp][H] gradient of the last state
-  const float* dhs;                      // CG backward (optional): [Mp] row scales of dhT
+  const float* dhs;                      // CG backward (optional): row scales of dhT (rows >= dhs_n: 0)
+  int dhs_n;
   float* prob;                           // CG forward with the head: [Mp] sigmoid outputs
   float* dhg;                            //   and [Mp][H] d prob / d h_{T-1}
   __bf16* dz;                            // backward: [T + 1][Mp][4H] bf16
@@ -386,7 +387,8 @@ __global__ __launch_bounds__(T4NT) void t4_head_bwd_kernel(T4Args A) {
       const int r = e / (T4H / 4), k = 4 * (e % (T4H / 4));
       float4 v = src[e];
       if (A.dhs != nullptr) {
-        const float sc = A.dhs[tile * 16 + r];
+        const int row = tile * 16 + r;
+        const float sc = row < A.dhs_n ? A.dhs[min(row, A.dhs_n - 1)] : 0.f;
         v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
       }
       *reinterpret_cast<float4*>(dhT + r * T4HP + k) = v;
@@ -884,8 +886,10 @@ std::vector<at::Tensor> time4_bwd(const at::Tensor& dh, const at::Tensor& x, con
   A.dhT = dh.data_ptr<float>();
   if (row_scale.has_value() && row_scale->defined()) {
     check_f32_cuda(*row_scale, "row_scale");
-    TORCH_CHECK(row_scale->numel() == Mp, "time4_bwd: row_scale must have Mp entries");
+    TORCH_CHECK(row_scale->numel() >= 1 && row_scale->numel() <= Mp && row_scale->is_contiguous(),
+                "time4_bwd: row_scale must have 1..Mp entries (rows past them get 0)");
     A.dhs = row_scale->data_ptr<float>();
+    A.dhs_n = (int)row_scale->numel();
   }
   A.dz = need_dz ? bf16_ptr(dz) : nullptr;
   A.dx = dx.data_ptr<float>();

@@ -199,14 +199,17 @@ class IntegratedGradients:
             self._wts = trapezoid_weights(self.m_steps, dev).to(dt)
             self._path_key = key
         alphas, wts = self._alphas, self._wts
-        acc = [torch.zeros_like(v, dtype=dt) for v in vals]
+        # (GNNQC_IG_LEAN=0: zero-filled accumulators and a sum() seed, the pre-round-6-close form, for A/B)
+        lean = fused and os.environ.get("GNNQC_IG_LEAN", "1") == "1"
+        acc = [(torch.empty_like if lean else torch.zeros_like)(v, dtype=dt) for v in vals]
         path_pred = torch.empty(self.m_steps + 1, B, device=dev, dtype=dt)
         k = max(1, min(self.m_steps + 1, self.max_rows // max(B, 1)))
         vf = [v.to(dt).contiguous() for v in vals]
         with _frozen(model), torch.enable_grad():
             for s in (range(0, self.m_steps + 1, k) if fused else ()):
+                # (the first chunk's gradient launch writes the accumulators: no zero fill)
                 self._cml_path_folded_chunk(batch, alphas[s:s + k].contiguous(), wts[s:s + k].contiguous(),
-                                            acc, path_pred[s:s + k], target)
+                                            acc, path_pred[s:s + k], target, first=(s == 0 and lean))
             for s in (range(0, self.m_steps + 1, k) if not fused else ()):
                 a = alphas[s:s + k]
                 kk = a.numel()
@@ -278,7 +281,7 @@ class IntegratedGradients:
         return bool(shape_ok and anom.shape[-1] <= min(F, 4) and not (g.dropout and m.training))
 
     def _cml_path_folded_chunk(self, batch, a: torch.Tensor, wt: torch.Tensor, acc, path_pred_rows,
-                               target: Optional[torch.Tensor]):
+                               target: Optional[torch.Tensor], first: bool = False):
         """One chunk of path points: GCN forward of all of them (one launch), the TimeLayer + head
         on the path batch, one backward to the LSTM input, then one launch that turns that gradient
         into the trapezoid-weighted input gradients of x and anom (accumulated into ``acc``)."""
@@ -321,7 +324,14 @@ class IntegratedGradients:
         feat = m.time_layer.forward_time_major(h0, kk * B, last=last)
         if taken:
             y = feat
-            (gh,) = torch.autograd.grad(y.sum(), h0)
+            # d sum(y) / d h0 with a cached ones seed (no reduction + fill launches per call)
+            if os.environ.get("GNNQC_IG_LEAN", "1") == "1":
+                ones = getattr(self, "_ones", None)
+                if ones is None or ones.shape != y.shape or ones.device != y.device:
+                    ones = self._ones = torch.ones_like(y)
+                (gh,) = torch.autograd.grad(y, h0, ones)
+            else:
+                (gh,) = torch.autograd.grad(y.sum(), h0)
         elif (spec is not None and feat.dim() == 2 and feat.shape[1] in (32, 64, 128) and feat.dtype == torch.float32
                 and spec[0].kernel.shape[1] == 64 and tuple(spec[1].kernel.shape) == (64, 64)
                 and tuple(spec[2].kernel.shape) == (64, 1) and os.environ.get("GNNQC_IG_HEAD_HIP", "1") == "1"):
@@ -344,7 +354,7 @@ class IntegratedGradients:
         path_pred_rows.copy_(y.detach().view(kk, B).to(path_pred_rows.dtype))
         ops.ig_gcn_pool_bwd(x, w, mask, gh.contiguous(), g.kernel.contiguous(), g.bias.contiguous(),
                             st[2].contiguous(), st[3].contiguous(), g.prelu_alpha.contiguous(), a, wt.float(),
-                            acc[0], acc[1])
+                            acc[0], acc[1], bool(first))
 
 
 def completeness_gap(ig_res: Dict[str, torch.Tensor]) -> torch.Tensor:
