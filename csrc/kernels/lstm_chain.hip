@@ -1080,6 +1080,9 @@ static_assert(sizeof(ChainBArgs) <= 4096, "chain backward kernel arguments");
 #ifndef CHAINB_XPAD
 #define CHAINB_XPAD 1
 #endif
+#ifndef CHAINB_ZSWZ
+#define CHAINB_ZSWZ 0    // swizzled dz tile: same-box CML 0.2477 vs 0.2459 ms unswizzled (profiles/r6_zs_swizzle_ab.txt)
+#endif
 template <int H, int KX>
 struct ChainBLds {
   static constexpr bool WL = H >= 32;             // W^T fragments of dx from LDS (VGPR budget)
@@ -1202,6 +1205,8 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
   static_assert(L::BYTES <= CHAINB_LDS_STAGE && LK::BYTES <= CHAINB_LDS_STAGE && L::ZS % 16 == 0 && L::DH % 16 == 0,
                 "chain bwd LDS layout");
   auto zs = reinterpret_cast<__bf16 (*)[16][G4 + CHAINB_ZPAD]>(smem);
+  // dz element e of sequence c at zs[.][c][chz(c, e)]: 16-byte chunk XOR bit 2 of the sequence (as lstm_tm.hip)
+  auto chz = [](int c, int e) { return CHAINB_ZSWZ ? e ^ (((c >> 2) & 1) << 3) : e; };
   auto dhs = reinterpret_cast<float (*)[16][C::HP]>(smem + L::ZS);
   auto dxs = reinterpret_cast<float (*)[16][32 * KX + CHAINB_XPAD]>(smem + L::ZS + L::DH);
   auto wl = reinterpret_cast<__bf16 (*)[16][G4 + 8]>(smem + L::ZS + L::DH + L::DX);
@@ -1240,7 +1245,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
 #pragma unroll
           for (int q = lane; q < 16 * G4 / 8; q += 64) {
             const int e = 8 * q;
-            *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][e % G4]);
+            *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][chz(e / G4, e % G4)]);
           }
         }
         if constexpr (SK) lds_barrier();
@@ -1279,7 +1284,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
           const int p = s & 1;
           bf16x8_t bz[KB];
 #pragma unroll
-          for (int k = 0; k < KB; ++k) bz[k] = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+          for (int k = 0; k < KB; ++k) bz[k] = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][chz(col, 32 * k + 8 * quad)]);
 #pragma unroll
           for (int xb = 0; xb < NXB; ++xb) {
             f32x4_t a = {0.f, 0.f, 0.f, 0.f};
@@ -1380,7 +1385,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
 #pragma unroll
         for (int q = lane; q < 16 * G4 / 8; q += 64) {
           const int e = 8 * q;
-          *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][e % G4]);
+          *reinterpret_cast<uint4*>(zt + e) = *reinterpret_cast<const uint4*>(&zs[pb][e / G4][chz(e / G4, e % G4)]);
         }
       };
       __syncthreads();
@@ -1586,10 +1591,10 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         const float tc = tanhf_fast(rc[j]);
         const float dct = dc + dh * g4.w * (1.f - tc * tc);
         dc = dct * g4.y;
-        zs[p][col][0 * H + unit] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
-        zs[p][col][1 * H + unit] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
-        zs[p][col][2 * H + unit] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
-        zs[p][col][3 * H + unit] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
+        zs[p][col][chz(col, 0 * H + unit)] = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
+        zs[p][col][chz(col, 1 * H + unit)] = (__bf16)(dct * cp * g4.y * (1.f - g4.y));
+        zs[p][col][chz(col, 2 * H + unit)] = (__bf16)(dct * g4.x * (1.f - g4.z * g4.z));
+        zs[p][col][chz(col, 3 * H + unit)] = (__bf16)(dh * tc * g4.w * (1.f - g4.w));
       }
       {   // state of step s + D and the dh of step s + 1 (time t - 1)
         const int tt = max(T - 1 - (s + D), 0);
@@ -1615,13 +1620,13 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < KPG; ++q) {
-          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * (kg * KPG + q) + 8 * quad]);
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][chz(col, 32 * (kg * KPG + q) + 8 * quad)]);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[q], bz, a, 0, 0, 0);
         }
         f32x4_t b = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < KPX; ++q) {
-          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * (kx * KPX + q) + 8 * quad]);
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][chz(col, 32 * (kx * KPX + q) + 8 * quad)]);
           b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufk[q], bz, b, 0, 0, 0);
         }
 #pragma unroll
@@ -1633,7 +1638,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
         f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
-          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][chz(col, 32 * k + 8 * quad)]);
           if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a1, 0, 0, 0);
           else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[k], bz, a0, 0, 0, 0);
         }
@@ -1644,7 +1649,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
       }
       chain_mark(pr, s, 4);
       if constexpr (!PUBW) {   // dz tile -> HBM (weight-gradient pass; else the publisher stores it)
-        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][gz_c]);
+        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][chz(gz_seq, gz_c)]);
         const int tz = t >= 0 ? t : T;
         *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
       }
@@ -1666,7 +1671,7 @@ __device__ __forceinline__ void chain_bwd_stage(const ChainBStage S, int tile, i
             f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
-              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][chz(col, 32 * k + 8 * quad)]);
               bf16x8_t wa;
               if constexpr (L::WL) wa = *reinterpret_cast<const bf16x8_t*>(&wl[xb][col][32 * k + 8 * quad]);
               else wa = wfr[q][k];

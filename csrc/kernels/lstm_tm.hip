@@ -383,6 +383,9 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 __device__ __forceinline__ unsigned __bf16_bits(__bf16 v) {
   return (unsigned)__builtin_bit_cast(unsigned short, v);
 }
+#ifndef TMB_ZSWZ
+#define TMB_ZSWZ 1       // swizzled dz tile in the backward (A/B: 0)
+#endif
 #ifndef TMW_SKIP
 #define TMW_SKIP 0       // (timing experiments only, wrong results: 1 no weight MFMAs, 2 no x / h streams,
 #endif                   //  4 no transposed dz copy; T = 337 micro, H = 16: 368 -> 297 / 310 / 352 us)   // 4 bf16 (v_mfma_f32_16x16x16_bf16 operand)
@@ -433,6 +436,9 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   // quads - landed on 2 banks with a 32-float pitch: 16-way), x / h staging rows + 16 bf16
   constexpr int ZSP = G4 + 16, DXP = DX ? 32 * KX + 1 : 1;
   __shared__ __attribute__((aligned(16))) __bf16 zs[2][16][ZSP];        // dz row-major (B of U dz^T, W dz^T)
+  // dz element e of sequence c sits at zs[.][c][zsw(c, e)]: 16-byte chunk index XOR bit 2 of the sequence
+  // (scripts/lds_model/zs_swizzle.py: with the G4 + 16 pitch the cell phase's 16-bit stores were 4-way)
+  auto zsw = [](int c, int e) { return TMB_ZSWZ ? e ^ (((c >> 2) & 1) << 3) : e; };
   __shared__ __attribute__((aligned(16))) float dhs[2][16][C::HP];      // dh_out tile
   __shared__ __attribute__((aligned(16))) float dxs[2][16][DXP];        // dx tile
 
@@ -723,8 +729,8 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
           const unsigned mq0 = qo ? b2 : b0, mq1 = qo ? b3 : b1;                    // my gates gq, gq + 1
           const unsigned w0 = qo ? ((rq & 0xffffu) | (mq0 << 16)) : (mq0 | (rq << 16));
           const unsigned w1 = qo ? ((rq >> 16) | (mq1 << 16)) : (mq1 | (rq & 0xffff0000u));
-          *reinterpret_cast<unsigned*>(&zs[p][col][gq * H + ub]) = w0;
-          *reinterpret_cast<unsigned*>(&zs[p][col][(gq + 1) * H + ub]) = w1;
+          *reinterpret_cast<unsigned*>(&zs[p][col][zsw(col, gq * H + ub)]) = w0;
+          *reinterpret_cast<unsigned*>(&zs[p][col][zsw(col, (gq + 1) * H + ub)]) = w1;
           if constexpr (WG && !(TMW_SKIP & 4)) {
             const bool co = col & 1;
             const unsigned rc2 = (unsigned)__shfl_xor((int)(co ? lo : hi), 1, 64);  // partner sequence's pair
@@ -736,10 +742,10 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
             *reinterpret_cast<unsigned*>(&zT[s & 3][(gc + 1) * H + u][cb]) = v1;
           }
         } else {
-          zs[p][col][0 * H + u] = z0;
-          zs[p][col][1 * H + u] = z1;
-          zs[p][col][2 * H + u] = z2;
-          zs[p][col][3 * H + u] = z3;
+          zs[p][col][zsw(col, 0 * H + u)] = z0;
+          zs[p][col][zsw(col, 1 * H + u)] = z1;
+          zs[p][col][zsw(col, 2 * H + u)] = z2;
+          zs[p][col][zsw(col, 3 * H + u)] = z3;
           if constexpr (WG && !(TMW_SKIP & 4)) {
             zT[s & 3][0 * H + u][col] = z0;
             zT[s & 3][1 * H + u][col] = z1;
@@ -772,7 +778,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
         f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
-          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+          const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][zsw(col, 32 * k + 8 * quad)]);
           if (k & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][k], bz, a1, 0, 0, 0);
           else a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ufr[cc][k], bz, a0, 0, 0, 0);
         }
@@ -806,7 +812,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
       // (b) dz tile of this step -> HBM as bf16 (its exact values: the MFMAs above consumed
       // these bf16 values; steps past t = 0 pad the unrolled chunk: scratch row)
       if constexpr (DZ) {
-        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][gz_c]);
+        const uint2 zv = *reinterpret_cast<const uint2*>(&zs[p][gz_seq][zsw(gz_seq, gz_c)]);
         const int tz = t >= 0 ? t : T;
         *reinterpret_cast<uint2*>(zbase + (size_t)tz * zstep) = zv;
       }
@@ -826,7 +832,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
             f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
-              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][32 * k + 8 * quad]);
+              const bf16x8_t bz = *reinterpret_cast<const bf16x8_t*>(&zs[p][col][zsw(col, 32 * k + 8 * quad)]);
               bf16x8_t wa;
               if constexpr (WL) wa = *reinterpret_cast<const bf16x8_t*>(&wls[16 * xb + col][32 * k + 8 * quad]);
               else wa = wfr[q][k];
