@@ -191,7 +191,8 @@ __global__ __launch_bounds__(TMC<H>::NT, (TmOcc<TMC<H>::NT, KX>::W)) void lstm_t
         if constexpr (TRAIN) {                       // steps past T-1 write the scratch row T
           const size_t o = ((((size_t)min(t, T) * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane;
           if constexpr (SG) *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
-          cbuf[o] = c[cc];
+          if constexpr (!SG && TM_RG_BF16C) reinterpret_cast<__bf16*>(cbuf)[o] = (__bf16)c[cc];
+          else cbuf[o] = c[cc];
         }
       }
       lds_barrier();
@@ -352,7 +353,8 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
         if constexpr (TRAIN) {                       // invalid steps write the scratch row T
           const size_t o = (((size_t)(tc >= 0 ? min(tc, T) : T) * ntiles + tile) * NW + w) * 64 + lane;
           if constexpr (SG) *reinterpret_cast<uint2*>(gbuf + o * 4) = gates_pack(iv, fv, gv, ov);
-          cbuf[o] = c;
+          if constexpr (!SG && TM_RG_BF16C) reinterpret_cast<__bf16*>(cbuf)[o] = (__bf16)c;
+          else cbuf[o] = c;
         }
       }
       lds_barrier();
@@ -383,6 +385,9 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 __device__ __forceinline__ unsigned __bf16_bits(__bf16 v) {
   return (unsigned)__builtin_bit_cast(unsigned short, v);
 }
+#ifndef TM_RG_BF16C
+#define TM_RG_BF16C 1    // recompute-gates layers save c_t in bf16 (the forward keeps fp32 in registers; A/B: 0)
+#endif
 #ifndef TMB_ZSWZ
 #define TMB_ZSWZ 1       // swizzled dz tile in the backward (A/B: 0)
 #endif
@@ -521,7 +526,9 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 
   // ---- streams. internal state (per lane, ring over reverse steps): gates, c_t
   uint2 rg[CPL][RG ? 1 : D];                      // packed bf16 gates (not saved under RG)
-  float rc[CPL][D];
+  // c_t ring: under RG the forward saved c in bf16 (TM_RG_BF16C), kept raw here and widened where used
+  using CT = std::conditional_t<RG && TM_RG_BF16C, __bf16, float>;
+  CT rc[CPL][D];
   auto idx = [&](int tt, int cc) { return ((((size_t)tt * ntiles + tile) * NW + w) * CPL + cc) * 64 + lane; };
 #define GQ_TMB_LOAD_STATE(J, SS)                                                    \
   {                                                                                 \
@@ -529,7 +536,7 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
     _Pragma("unroll") for (int cc = 0; cc < CPL; ++cc) {                            \
       const size_t o_ = idx(tt_, cc);                                               \
       if constexpr (!RG) rg[cc][J] = *reinterpret_cast<const uint2*>(gbuf + o_ * 4); \
-      rc[cc][J] = cbuf[o_];                                                         \
+      rc[cc][J] = reinterpret_cast<const CT*>(cbuf)[o_];                            \
     }                                                                               \
   }
   // Streams: every wave loads and stages granule (tid mod n) of each contiguous tile (no
@@ -701,14 +708,14 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #pragma unroll
       for (int cc = 0; cc < CPL; ++cc) {
         const int u = unit[cc];
-        const float cp = rc[cc][jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
+        const float cp = (float)rc[cc][jn] * (t > 0 ? 1.f : 0.f);      // c_{t-1}
         const float dh = dhn[cc] + dhr[cc];
         float4 g4;
         if constexpr (RG)
           g4 = gn;
         else
           g4 = gates_unpack(rg[cc][j]);
-        const float tc = tanhf_fast(rc[cc][j]);
+        const float tc = tanhf_fast((float)rc[cc][j]);
         const float dct = dc[cc] + dh * g4.w * (1.f - tc * tc);
         dc[cc] = dct * g4.y;
         const __bf16 z0 = (__bf16)(dct * g4.z * g4.x * (1.f - g4.x));
@@ -1059,11 +1066,12 @@ std::vector<at::Tensor> lstm_tm_fwd(const at::Tensor& x, const at::Tensor& W, co
   at::Tensor h = at::empty({T + 1, Mp, H}, opt);
   at::Tensor g = (train && store_gates) ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16))
                                         : at::empty({0}, opt.dtype(at::kBFloat16));
-  at::Tensor c = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
+  const bool cbf = train && !store_gates && TM_RG_BF16C;     // (recompute-gates c in bf16)
+  at::Tensor c = train ? at::empty({T + 1, Mp, H}, cbf ? opt.dtype(at::kBFloat16) : opt) : at::empty({0}, opt);
   const int ntiles = Mp / 16;
   auto st = stream();
   __bf16* gp = (train && store_gates) ? bf16_ptr(g) : nullptr;
-  float* cp = train ? c.data_ptr<float>() : nullptr;
+  float* cp = train ? reinterpret_cast<float*>(c.data_ptr()) : nullptr;
   GQ_TM_H_DISPATCH(H, GQ_TM_KX_DISPATCH((Din + 31) / 32, GQ_TM_GR_DISPATCH(gr,
       if (train) tm_fwd_cfg<HH, true, KXX, GRR>(ntiles, x.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
                                                 b.data_ptr<float>(), h.data_ptr<float>(), gp, cp, Mp, T, Din, Dw, st);
@@ -1101,12 +1109,15 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   at::Tensor hA = mk(false, 0), hB = mk(false, 0);
   at::Tensor gA = sg ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt.dtype(at::kBFloat16));
   at::Tensor gB = sg ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt.dtype(at::kBFloat16));
-  at::Tensor cA = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
-  at::Tensor cB = train ? at::empty({T + 1, Mp, H}, opt) : at::empty({0}, opt);
+  const bool cbf = train && !sg && TM_RG_BF16C;              // (recompute-gates c in bf16)
+  const auto copt = cbf ? opt.dtype(at::kBFloat16) : opt;
+  at::Tensor cA = train ? at::empty({T + 1, Mp, H}, copt) : at::empty({0}, opt);
+  at::Tensor cB = train ? at::empty({T + 1, Mp, H}, copt) : at::empty({0}, opt);
   const int ntiles = Mp / 16;
   auto st = stream();
   __bf16* PG[2] = {sg ? bf16_ptr(gA) : nullptr, sg ? bf16_ptr(gB) : nullptr};
-  float* P[4] = {nullptr, train ? cA.data_ptr<float>() : nullptr, nullptr, train ? cB.data_ptr<float>() : nullptr};
+  float* P[4] = {nullptr, train ? reinterpret_cast<float*>(cA.data_ptr()) : nullptr, nullptr,
+                 train ? reinterpret_cast<float*>(cB.data_ptr()) : nullptr};
   at::Tensor pooled, pidx;
   const TmPool pl = tm_pool_outputs((int)pool, T, Mp, H, opt, pooled, pidx);
 #define GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, PLV)                                                              \
@@ -1554,10 +1565,15 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
                        const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
                        at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx,
                        const c10::optional<at::Tensor>& pidx_opt, int64_t pool) {
-  const at::Tensor* ops[] = {&dh, &c, &x, &h, &W, &U, &b};
+  const at::Tensor* ops[] = {&dh, &x, &h, &W, &U, &b};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
   const bool rg = g.numel() == 0;
   if (!rg) check_gates_cuda(g);
+  // (recompute gates: c_t saved in bf16 by the forward, TM_RG_BF16C)
+  TORCH_CHECK(c.is_cuda() && c.is_contiguous() &&
+                  c.scalar_type() == ((rg && TM_RG_BF16C) ? at::kBFloat16 : at::kFloat),
+              "lstm_tm_bwd: c must be the forward's saved state (", (rg && TM_RG_BF16C) ? "bf16" : "fp32", ")");
+  const float* cptr = reinterpret_cast<const float*>(c.data_ptr());
   const int T = (int)x.size(0), Mp = (int)x.size(1), Din = (int)x.size(2), H = (int)U.size(0);
   const int Dw = (int)W.size(0);
   TORCH_CHECK(Dw >= 1 && Dw <= Din && W.size(1) == 4 * H && b.numel() == 4 * H, "lstm_tm_bwd: W / b shape");
@@ -1602,7 +1618,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 4 == 0 && h.is_contiguous(), "lstm_tm_bwd: h layout");
 #define GQ_TM_WG_CALL3(DXV, LASTV, RGV, UPV)                                                                   \
   hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV, RGV, UPV>),          \
-                     dim3(ntiles), dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), gptr, c.data_ptr<float>(),    \
+                     dim3(ntiles), dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), gptr, cptr,                   \
                      W.data_ptr<float>(), U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr,         \
                      x.data_ptr<float>(), h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw,            \
                      b.data_ptr<float>(), pidx, P)
@@ -1680,7 +1696,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
   if (rg) {      // frozen weights (integrated gradients), gates recomputed: H <= 32, GR = 4
 #define GQ_TM_RG_CALL2(LASTV, UPV)                                                                             \
   hipLaunchKernelGGL((lstm_tm_bwd_kernel<HH, KXX, 4, 4, false, true, LASTV, true, UPV>), dim3(ntiles),            \
-                     dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), nullptr, c.data_ptr<float>(),                 \
+                     dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), nullptr, cptr,                                \
                      W.data_ptr<float>(), U.data_ptr<float>(), dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw,     \
                      x.data_ptr<float>(), h.data_ptr<float>(), b.data_ptr<float>(), pidx, P)
 #define GQ_TM_RG_CALL(LASTV) \

@@ -10,7 +10,8 @@ forward   z_t = bf16(x_t) bf16(W) + bf16(h_{t-1}) bf16(U) + b; gates / c / h in 
           the gates saved for the backward are bf16 for H <= 64 (the time-major kernels pack
           them, ``lstm_tm_common.h gates_pack``) and full precision for H = 128 (the training
           chain's time4; the standalone time4 layer and lstm_fwd<128> save bf16 gates as well -
-          a difference well inside the tests' tolerances);
+          a difference well inside the tests' tolerances); the recompute-gates layers (lstm_tm.hip RG)
+          save c_t in bf16 (TM_RG_BF16C), likewise not modelled here;
 backward  dz_t (the four gate pre-activation gradients, from the saved gates) is rounded to
           bf16 - the value the kernels store and feed to every MFMA; dh_{t-1} = dz_t bf16(U)^T,
           dx = dz bf16(W)^T, dW = bf16(x)^T dz, dU = bf16(h_{t-1})^T dz, db = sum dz.
