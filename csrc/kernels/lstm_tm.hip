@@ -32,6 +32,10 @@
 #include "gcn_fused.h"
 #include "lstm_tm_common.h"
 
+#ifndef TM_RG_BF16C
+#define TM_RG_BF16C 1    // recompute-gates layers save c_t in bf16 (the forward keeps fp32 in registers; A/B: 0)
+#endif
+
 namespace gq {
 
 // lstm_grads.hip: weight gradients (+ dx) over flat rows, h_{t-1} hshift rows back
@@ -385,9 +389,6 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
 __device__ __forceinline__ unsigned __bf16_bits(__bf16 v) {
   return (unsigned)__builtin_bit_cast(unsigned short, v);
 }
-#ifndef TM_RG_BF16C
-#define TM_RG_BF16C 1    // recompute-gates layers save c_t in bf16 (the forward keeps fp32 in registers; A/B: 0)
-#endif
 #ifndef TMB_ZSWZ
 #define TMB_ZSWZ 1       // swizzled dz tile in the backward (A/B: 0)
 #endif
