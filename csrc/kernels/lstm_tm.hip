@@ -32,6 +32,9 @@
 #include "gcn_fused.h"
 #include "lstm_tm_common.h"
 
+#ifndef TM_RG_BF16H
+#define TM_RG_BF16H 1    // recompute-gates pairs save layer A's h in bf16 (its only readers stage it as bf16; A/B: 0)
+#endif
 #ifndef TM_RG_BF16C
 #define TM_RG_BF16C 1    // recompute-gates layers save c_t in bf16 (the forward keeps fp32 in registers; A/B: 0)
 #endif
@@ -286,6 +289,10 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
   constexpr int n_gh = 16 * H / 4;
   const int gh = (tl % n_gh) * 4;
   float* hbase = (layerB ? hB : hA) + (size_t)row0 * H + gh;
+  // recompute-gates pairs (training without saved gates) store layer A's h in bf16: its readers are this
+  // pair's backward (B's x stream, A's h_{t-1} stream), which stage it as bf16 MFMA operands anyway
+  constexpr bool HBA = TRAIN && !SG && TM_RG_BF16H;
+  __bf16* hbaseA = reinterpret_cast<__bf16*>(hA) + (size_t)row0 * H + gh;
   const size_t hstep = (size_t)Mp * H;
   __bf16* gbuf = layerB ? gB : gA;
   float* cbuf = layerB ? cB : cA;
@@ -313,7 +320,11 @@ __global__ __launch_bounds__(2 * TMC<H>::NT, (TmOcc<2 * TMC<H>::NT, KX>::W)) voi
       {
         const int ts = (tc >= 1 && tc <= T) ? tc - 1 : T;
         const float4 v = *reinterpret_cast<const float4*>(&hf[L][p ^ 1][gh / H][gh % H]);
-        *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
+        if (HBA && !layerB)                        // (uniform) layer A's h in bf16, TM_RG_BF16H
+          *reinterpret_cast<bf16x4_t*>(hbaseA + (size_t)ts * hstep) =
+              bf16x4_t{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        else
+          *reinterpret_cast<float4*>(hbase + (size_t)ts * hstep) = v;
         if constexpr (PL) {
           if (pooler && ts < T) pacc.step(v, ts, P, To, pout, iout, (size_t)row0 * H + gh, hstep);
         }
@@ -420,7 +431,7 @@ __device__ __forceinline__ unsigned __bf16_bits(__bf16 v) {
 // t mod P (zero past the last window), as maxpool1d_bwd would have written them at full resolution -
 // that kernel and its full-resolution dh round trip through HBM are gone.
 template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool WG = false, bool RG = false,
-          bool UP = false>
+          bool UP = false, bool XB = false, bool HB = false>
 __device__ __forceinline__ void lstm_tm_bwd_body(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
@@ -566,12 +577,13 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
   // and element tid of the [16][H] h_{t-1} tile, in rings over reverse steps like the saved state
   constexpr int XG = XS ? (16 * 32 * KX / NT > 1 ? 16 * 32 * KX / NT : 1) : 1;
   static_assert(XG <= 4, "x stream granule");
-  Granule<XG> wx[XS ? D : 1];
-  float wh[XS ? D : 1];
+  // XB / HB: x / h_{t-1} are bf16 (a recompute-gates pair's layer-A output, TM_RG_BF16H)
+  std::conditional_t<XB, GranuleH<XG>, Granule<XG>> wx[XS ? D : 1];
+  std::conditional_t<HB, __bf16, float> wh[XS ? D : 1];
   const int wxe = (tid * XG) % (16 * Din);
   const int wx_seq = wxe / Din, wx_k = wxe % Din;
-  const float* wxb = xw + (size_t)row0 * Din + wxe;
-  const float* whb = hw + (size_t)row0 * H + tid;
+  const auto wxb = reinterpret_cast<std::conditional_t<XB, const __bf16*, const float*>>(xw) + (size_t)row0 * Din + wxe;
+  const auto whb = reinterpret_cast<std::conditional_t<HB, const __bf16*, const float*>>(hw) + (size_t)row0 * H + tid;
   const size_t whstep = (size_t)Mp * H;
 #define GQ_TMB_LOAD_W(J, SS)                                                        \
   if constexpr (XS && !(TMW_SKIP & 2)) {                                                               \
@@ -621,12 +633,12 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #pragma unroll
         for (int q = 0; q < XG; q += 2)
           *reinterpret_cast<unsigned*>(&xrs[b][wx_seq][wx_k + q]) =
-              __bf16_bits((__bf16)wx[J].v[q]) | (__bf16_bits((__bf16)wx[J].v[q + 1]) << 16);
+              __bf16_bits(wx[J].bf(q)) | (__bf16_bits(wx[J].bf(q + 1)) << 16);
       } else {
 #pragma unroll
-        for (int q = 0; q < XG; ++q) xrs[b][wx_seq][wx_k + q] = (__bf16)wx[J].v[q];
+        for (int q = 0; q < XG; ++q) xrs[b][wx_seq][wx_k + q] = wx[J].bf(q);
       }
-      hrs[b][tid / H][tid % H] = (__bf16)(wh[J] * (tt >= 1 ? 1.f : 0.f));
+      hrs[b][tid / H][tid % H] = (__bf16)((float)wh[J] * (tt >= 1 ? 1.f : 0.f));
     }
   };
   // pre-activations from buffer b: exactly the forward's two MFMA chains (x part from the bias)
@@ -767,9 +779,9 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #pragma unroll
         for (int q = 0; q < XG; ++q) {
           const int dn = wx_k + q;
-          xT[s & 3][dn][wx_seq] = (__bf16)(dn < Dw ? wx[j].v[q] : (dn == Dw ? 1.f : 0.f));
+          xT[s & 3][dn][wx_seq] = dn < Dw ? wx[j].bf(q) : (__bf16)(dn == Dw ? 1.f : 0.f);
         }
-        hT[s & 3][tid % H][tid / H] = (__bf16)(wh[j] * hm);
+        hT[s & 3][tid % H][tid / H] = (__bf16)((float)wh[j] * hm);
       }
       rg_stage((s + 1) & 1, jn, t - 1);            // (RG) x_{t-1}, h_{t-2}: the next step's gates
       GQ_TMB_LOAD_W(j, s + D)
@@ -875,24 +887,27 @@ __device__ __forceinline__ void lstm_tm_bwd_body(
 #undef GQ_TMB_LOAD_W
 }
 
-template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool RG = false, bool UP = false>
+template <int H, int KX, int GR, int D, bool DZ, bool DX, bool LAST, bool RG = false, bool UP = false,
+          bool XB = false, bool HB = false>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, __bf16* __restrict__ dz,
     int Mp, int T, int Din, int Dw, const float* __restrict__ x = nullptr, const float* __restrict__ h = nullptr,
     const float* __restrict__ bias = nullptr, const unsigned char* __restrict__ pidx = nullptr, int P = 1) {
-  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, false, RG, UP>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din, Dw,
-                                                              blockIdx.x, gridDim.x, x, h, nullptr, bias, pidx, P);
+  lstm_tm_bwd_body<H, KX, GR, D, DZ, DX, LAST, false, RG, UP, XB, HB>(dhout, gbuf, cbuf, W, U, dx, dz, Mp, T, Din,
+                                                                      Dw, blockIdx.x, gridDim.x, x, h, nullptr, bias,
+                                                                      pidx, P);
 }
 
-template <int H, int KX, int D, bool DX, bool LAST, bool RG = false, bool UP = false>
+template <int H, int KX, int D, bool DX, bool LAST, bool RG = false, bool UP = false, bool XB = false, bool HB = false>
 __global__ __launch_bounds__(TMC<H>::NT) void lstm_tm_bwd_wg_kernel(
     const float* __restrict__ dhout, const __bf16* __restrict__ gbuf, const float* __restrict__ cbuf,
     const float* __restrict__ W, const float* __restrict__ U, float* __restrict__ dx, const float* __restrict__ x,
     const float* __restrict__ h, float* __restrict__ ws, int Mp, int T, int Din, int Dw,
     const float* __restrict__ bias = nullptr, const unsigned char* __restrict__ pidx = nullptr, int P = 1) {
-  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true, RG, UP>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T, Din, Dw,
-                                                               blockIdx.x, gridDim.x, x, h, ws, bias, pidx, P);
+  lstm_tm_bwd_body<H, KX, 4, D, false, DX, LAST, true, RG, UP, XB, HB>(dhout, gbuf, cbuf, W, U, dx, nullptr, Mp, T,
+                                                                       Din, Dw, blockIdx.x, gridDim.x, x, h, ws, bias,
+                                                                       pidx, P);
 }
 
 // =====================================================================================
@@ -1107,7 +1122,8 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
   auto mk = [&](bool state, int last) {
     return state ? (train ? at::empty({T + 1, Mp, H, last}, opt) : at::empty({0}, opt)) : at::empty({T + 1, Mp, H}, opt);
   };
-  at::Tensor hA = mk(false, 0), hB = mk(false, 0);
+  at::Tensor hA = (train && !sg && TM_RG_BF16H) ? at::empty({T + 1, Mp, H}, opt.dtype(at::kBFloat16)) : mk(false, 0);
+  at::Tensor hB = mk(false, 0);
   at::Tensor gA = sg ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt.dtype(at::kBFloat16));
   at::Tensor gB = sg ? at::empty({T + 1, Mp, H, 4}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt.dtype(at::kBFloat16));
   const bool cbf = train && !sg && TM_RG_BF16C;              // (recompute-gates c in bf16)
@@ -1124,7 +1140,7 @@ std::vector<at::Tensor> lstm_tm2_fwd(const at::Tensor& x, const at::Tensor& WA, 
 #define GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, PLV)                                                              \
   hipLaunchKernelGGL((lstm_tm2_fwd_kernel<HH, TR, KXX, GRR, 6, SGV, PLV>), dim3(ntiles), dim3(2 * TMC<HH>::NT), 0,  \
                      st, x.data_ptr<float>(), WA.data_ptr<float>(), UA.data_ptr<float>(), bA.data_ptr<float>(),    \
-                     WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), hA.data_ptr<float>(), PG[0], \
+                     WB.data_ptr<float>(), UB.data_ptr<float>(), bB.data_ptr<float>(), reinterpret_cast<float*>(hA.data_ptr()), PG[0], \
                      P[1], hB.data_ptr<float>(), PG[1], P[3], Mp, T, Din, Dw, pl.P, pl.out, pl.idx)
 #define GQ_TM2_LAUNCH(HH, TR, KXX, GRR, SGV)                                                                    \
   do { if (pl.P > 0) GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, true); else GQ_TM2_LAUNCH2(HH, TR, KXX, GRR, SGV, false); } \
@@ -1566,9 +1582,18 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
                        const at::Tensor& h, const at::Tensor& W, const at::Tensor& U, const at::Tensor& b,
                        at::Tensor dW, at::Tensor dU, at::Tensor db, bool need_dx,
                        const c10::optional<at::Tensor>& pidx_opt, int64_t pool) {
-  const at::Tensor* ops[] = {&dh, &x, &h, &W, &U, &b};
+  const at::Tensor* ops[] = {&dh, &W, &U, &b};
   for (const at::Tensor* t : ops) check_f32_cuda(*t, "lstm_tm_bwd operand");
   const bool rg = g.numel() == 0;
+  // x / h in bf16: a recompute-gates pair's layer-A output (TM_RG_BF16H) as layer B's x or layer A's h
+  const bool xb = x.scalar_type() == at::kBFloat16, hb = h.scalar_type() == at::kBFloat16;
+  if (!xb) check_f32_cuda(x, "lstm_tm_bwd x");
+  if (!hb) check_f32_cuda(h, "lstm_tm_bwd h");
+  TORCH_CHECK(((!xb && !hb) || rg) && !(xb && hb) && x.is_cuda() && h.is_cuda(),
+              "lstm_tm_bwd: bf16 x or h only from a recompute-gates pair forward");
+  const float* xptr = reinterpret_cast<const float*>(x.data_ptr());
+  const auto fopt = x.options().dtype(at::kFloat);   // (fp32 outputs / workspaces whatever x's dtype)
+  const float* hptr = reinterpret_cast<const float*>(h.data_ptr());
   if (!rg) check_gates_cuda(g);
   // (recompute gates: c_t saved in bf16 by the forward, TM_RG_BF16C)
   TORCH_CHECK(c.is_cuda() && c.is_contiguous() &&
@@ -1613,16 +1638,19 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     // weight gradients inside the recurrence: one split record per tile, then the reduction
     const int DT = (Dw + 1 + 15) / 16, RC = (DT + H / 16) * 1024 * ncb_w;
     const int NG = std::max(1, ntiles / 512);
-    at::Tensor ws = at::empty({(long)ntiles * RC + (NG > 1 ? (long)NG * RC : 0L)}, x.options());
-    at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, x.options()) : at::empty({0}, x.options());
+    at::Tensor ws = at::empty({(long)ntiles * RC + (NG > 1 ? (long)NG * RC : 0L)}, fopt);
+    at::Tensor dx = need_dx ? at::empty({T + 1, Mp, Din}, fopt) : at::empty({0}, fopt);
     if (need_dx) TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 4 == 0 && h.is_contiguous(), "lstm_tm_bwd: h layout");
-#define GQ_TM_WG_CALL3(DXV, LASTV, RGV, UPV)                                                                   \
-  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV, RGV, UPV>),          \
+#define GQ_TM_WG_CALL4(DXV, LASTV, RGV, UPV, XBV, HBV)                                                         \
+  hipLaunchKernelGGL((lstm_tm_bwd_wg_kernel<HH, KXX, HH == 16 ? TMW_D16 : TMW_D32, DXV, LASTV, RGV, UPV, XBV, HBV>), \
                      dim3(ntiles), dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), gptr, cptr,                   \
                      W.data_ptr<float>(), U.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr,         \
-                     x.data_ptr<float>(), h.data_ptr<float>(), ws.data_ptr<float>(), Mp, T, Din, Dw,            \
-                     b.data_ptr<float>(), pidx, P)
+                     xptr, hptr, ws.data_ptr<float>(), Mp, T, Din, Dw, b.data_ptr<float>(), pidx, P)
+#define GQ_TM_WG_CALL3(DXV, LASTV, RGV, UPV)                                                                   \
+  do { if constexpr (RGV) { if (xb) { GQ_TM_WG_CALL4(DXV, LASTV, RGV, UPV, true, false); break; }                \
+                            if (hb) { GQ_TM_WG_CALL4(DXV, LASTV, RGV, UPV, false, true); break; } }              \
+       GQ_TM_WG_CALL4(DXV, LASTV, RGV, UPV, false, false); } while (0)
 #define GQ_TM_WG_CALL2(DXV, LASTV, RGV)                                                                        \
   do { if constexpr (!LASTV) { if (up) { GQ_TM_WG_CALL3(DXV, LASTV, RGV, true); break; } }                      \
        GQ_TM_WG_CALL3(DXV, LASTV, RGV, false); } while (0)
@@ -1643,6 +1671,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
 #undef GQ_TM_WG_CALL
 #undef GQ_TM_WG_CALL2
 #undef GQ_TM_WG_CALL3
+#undef GQ_TM_WG_CALL4
     GQ_LAUNCH_CHECK();
     lstm_grads_reduce_records(ws, H, Dw, ntiles, dW.data_ptr<float>(), dU.data_ptr<float>(), db.data_ptr<float>(), st);
     return need_dx ? dx.narrow(0, 0, T) : dx;
@@ -1652,8 +1681,8 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     // several gate-column blocks: the weight-gradient pass could only produce dx as ncb partial
     // slabs plus a slab sum (ncb + 2 dx-sized passes); the recurrence computes dx^T = W dz^T
     // itself instead (its MFMA phase has the whole 4H dz tile in LDS) and writes dx once.
-    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));
-    at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, fopt.dtype(at::kBFloat16));
+    at::Tensor dx = at::empty({T + 1, Mp, Din}, fopt);
     TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
 #define GQ_TM_BWD_CALL2(LASTV)                                                                              \
   tm_bwd_cfg<HH, KXX, GRR, true, true, LASTV>(ntiles, dh.data_ptr<float>(), bf16_ptr(g), c.data_ptr<float>(), \
@@ -1675,7 +1704,7 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     const at::Tensor dhf = up ? maxpool1d_bwd(dh.view({1, T / P, (long)Mp * H}), pidx_opt->view({1, T / P, (long)Mp * H}),
                                               T, P).view({T, Mp, H})
                               : dh;
-    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, x.options().dtype(at::kBFloat16));
+    at::Tensor dz = at::empty({T + 1, Mp, 4 * H}, fopt.dtype(at::kBFloat16));
     GQ_TM_H_DISPATCH(H,
         if (last) tm_bwd_cfg<HH, 1, 1, true, false, true>(ntiles, dhf.data_ptr<float>(), bf16_ptr(g),
               c.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(), nullptr, bf16_ptr(dz), Mp, T, Din, Dw, st);
@@ -1685,27 +1714,32 @@ at::Tensor lstm_tm_bwd(const at::Tensor& dh, const at::Tensor& g, const at::Tens
     const long rows = (long)T * Mp;
     const int ncb = lstm_grads_col_blocks(H);
     // dx keeps the x layout (Din channels); padding channels (>= Dw) get zero gradient
-    at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, x.options()) : at::empty({0}, x.options());
+    at::Tensor dx = need_dx ? at::empty({ncb, T, Mp, Din}, fopt) : at::empty({0}, fopt);
     lstm_grads_rows(dz.data_ptr(), 1, x.data_ptr<float>(), h.data_ptr<float>(), W.data_ptr<float>(),
                     need_dx ? dx.data_ptr<float>() : nullptr, dW.data_ptr<float>(), dU.data_ptr<float>(),
                     db.data_ptr<float>(), rows, rows, Mp, H, Dw, Din, rows * Din, Din, rows * Din, st);
     if (!need_dx) return dx;
     return ncb == 1 ? dx[0] : dx.sum(0);
   }
-  at::Tensor dx = at::empty({T + 1, Mp, Din}, x.options());
+  at::Tensor dx = at::empty({T + 1, Mp, Din}, fopt);
   TORCH_CHECK(tm_granule(Din, dx.data_ptr()) >= gr, "lstm_tm_bwd: dx alignment");
   if (rg) {      // frozen weights (integrated gradients), gates recomputed: H <= 32, GR = 4
-#define GQ_TM_RG_CALL2(LASTV, UPV)                                                                             \
-  hipLaunchKernelGGL((lstm_tm_bwd_kernel<HH, KXX, 4, 4, false, true, LASTV, true, UPV>), dim3(ntiles),            \
+#define GQ_TM_RG_CALL3(LASTV, UPV, XBV, HBV)                                                                   \
+  hipLaunchKernelGGL((lstm_tm_bwd_kernel<HH, KXX, 4, 4, false, true, LASTV, true, UPV, XBV, HBV>), dim3(ntiles),  \
                      dim3(TMC<HH>::NT), 0, st, dh.data_ptr<float>(), nullptr, cptr,                                \
                      W.data_ptr<float>(), U.data_ptr<float>(), dx.data_ptr<float>(), nullptr, Mp, T, Din, Dw,     \
-                     x.data_ptr<float>(), h.data_ptr<float>(), b.data_ptr<float>(), pidx, P)
+                     xptr, hptr, b.data_ptr<float>(), pidx, P)
+#define GQ_TM_RG_CALL2(LASTV, UPV)                                                                             \
+  do { if (xb) { GQ_TM_RG_CALL3(LASTV, UPV, true, false); break; }                                             \
+       if (hb) { GQ_TM_RG_CALL3(LASTV, UPV, false, true); break; }                                             \
+       GQ_TM_RG_CALL3(LASTV, UPV, false, false); } while (0)
 #define GQ_TM_RG_CALL(LASTV) \
   do { if constexpr (!LASTV) { if (up) { GQ_TM_RG_CALL2(LASTV, true); break; } } GQ_TM_RG_CALL2(LASTV, false); } while (0)
     GQ_TM2_H_DISPATCH(H, if ((Din + 31) / 32 == 1) { constexpr int KXX = 1; if (last) GQ_TM_RG_CALL(true); else GQ_TM_RG_CALL(false); }
                          else { constexpr int KXX = 2; if (last) GQ_TM_RG_CALL(true); else GQ_TM_RG_CALL(false); });
 #undef GQ_TM_RG_CALL
 #undef GQ_TM_RG_CALL2
+#undef GQ_TM_RG_CALL3
     GQ_LAUNCH_CHECK();
     return dx.narrow(0, 0, T);
   }

@@ -2,6 +2,8 @@
 #pragma once
 #include "common.h"
 
+#include <type_traits>
+
 namespace gq {
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -54,6 +56,22 @@ struct Granule {
     }
   }
   __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
+  __device__ __forceinline__ __bf16 bf(int q) const { return (__bf16)v[q]; }
+};
+
+// The same GR-element granule from bf16 data, kept as the raw bits: a ring slot's load is waited for
+// where the value is used (staged into LDS as bf16), not at the load
+template <int GR>
+struct GranuleH {
+  using R = std::conditional_t<GR == 4, uint2, std::conditional_t<GR == 2, unsigned, unsigned short>>;
+  R r;
+  __device__ __forceinline__ void load(const __bf16* p) { r = *reinterpret_cast<const R*>(p); }
+  __device__ __forceinline__ __bf16 bf(int q) const {
+    unsigned w;
+    if constexpr (GR == 4) w = q < 2 ? r.x : r.y;
+    else w = (unsigned)r;
+    return __builtin_bit_cast(__bf16, (unsigned short)((q & 1) ? (w >> 16) : (w & 0xffffu)));
+  }
 };
 
 // ---- fused MaxPooling1D(P) (valid, stride P) of a stored h sequence (the chain forward's last
