@@ -202,14 +202,18 @@ class IntegratedGradients:
         # (GNNQC_IG_LEAN=0: zero-filled accumulators and a sum() seed, the pre-round-6-close form, for A/B)
         lean = fused and os.environ.get("GNNQC_IG_LEAN", "1") == "1"
         acc = [(torch.empty_like if lean else torch.zeros_like)(v, dtype=dt) for v in vals]
-        path_pred = torch.empty(self.m_steps + 1, B, device=dev, dtype=dt)
         k = max(1, min(self.m_steps + 1, self.max_rows // max(B, 1)))
+        # (one fused chunk covering the whole path: its output rows are the path predictions, no copy)
+        whole = lean and k >= self.m_steps + 1 and dt == torch.float32
+        path_pred = None if whole else torch.empty(self.m_steps + 1, B, device=dev, dtype=dt)
         vf = [v.to(dt).contiguous() for v in vals]
         with _frozen(model), torch.enable_grad():
             for s in (range(0, self.m_steps + 1, k) if fused else ()):
                 # (the first chunk's gradient launch writes the accumulators: no zero fill)
                 self._cml_path_folded_chunk(batch, alphas[s:s + k].contiguous(), wts[s:s + k].contiguous(),
-                                            acc, path_pred[s:s + k], target, first=(s == 0 and lean))
+                                            acc, None if whole else path_pred[s:s + k], target, first=(s == 0 and lean))
+                if whole:
+                    path_pred = self._last_y.reshape(self.m_steps + 1, B)
             for s in (range(0, self.m_steps + 1, k) if not fused else ()):
                 a = alphas[s:s + k]
                 kk = a.numel()
@@ -351,7 +355,10 @@ class IntegratedGradients:
             out = torch.sigmoid(m.head(feat))
             y = self._select(out, B, kk, target)
             (gh,) = torch.autograd.grad(y.sum(), h0)
-        path_pred_rows.copy_(y.detach().view(kk, B).to(path_pred_rows.dtype))
+        if path_pred_rows is None:
+            self._last_y = y.detach()
+        else:
+            path_pred_rows.copy_(y.detach().view(kk, B).to(path_pred_rows.dtype))
         ops.ig_gcn_pool_bwd(x, w, mask, gh.contiguous(), g.kernel.contiguous(), g.bias.contiguous(),
                             st[2].contiguous(), st[3].contiguous(), g.prelu_alpha.contiguous(), a, wt.float(),
                             acc[0], acc[1], bool(first))
